@@ -1,0 +1,214 @@
+"""Throughput of the keypoint-set pose path on MI355X (BASELINE.json metric).
+
+One step = one batch of synthetic SPEED-shaped 416x416 crops, resident in HBM, through
+backbone -> transformer -> keypoint heads + fused PostProcess -> batched PnP -> SPEED score
+(+ one RCCL all-gather of the per-image pose records when N > 1).  Default workload is
+BASELINE config 2: ResNet50-s8 + 6/6 transformer, 11 queries, bf16, bs=64 per GPU, EPnP only.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+Prints ONE JSON line (rank 0).  The dominant kernel's launches are bracketed with HIP events
+on the launch stream during the timed region (spe_model_profile_*) for the roofline object.
+"""
+import argparse
+import glob
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(REPO, "satellite-pose-estimation_amd"))
+
+PEAK = {"bf16": {"mfma": 2500.0}, "fp32": {"mfma": 157.3}, "hbm": 8000.0}   # TFLOP/s, GB/s (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--batch", type=int, default=64, help="images per GPU per step")
+    p.add_argument("--size", type=int, default=416)
+    p.add_argument("--queries", type=int, default=11)
+    p.add_argument("--layers", type=int, default=6)
+    p.add_argument("--solver", default="epnp", choices=["epnp", "epnp_lm", "ransac_p3p_lm", "epnp_ransac_sigma"])
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--cpu-seconds", type=float, default=15.0)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    return p.parse_args()
+
+
+def cpu_baseline(cfg, seconds):
+    """Oracle port (torch-fp32 CPU model + C solver) timed on this host's cores on a bounded
+    sample of the same workload: single 416x416 images, repeated until `seconds` elapse."""
+    import torch
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import model_ref
+    import pnp_ref
+    from spe.config import Camera, world_points
+    from spe.synthetic import random_weights, synthetic_batch
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    w = random_weights(cfg, 0)
+    b = synthetic_batch(cfg, 1, 99)
+    W, K = world_points(), Camera.K
+    n, t0 = 0, time.perf_counter()
+    with torch.no_grad():
+        while True:
+            o = model_ref.forward(b["images"], w, cfg)
+            pp = model_ref.postprocess(o["pred_logits"], o["pred_points"], b["clip_bbox"])
+            pnp_ref.pnp_batch(pp[0]["points"][None], pp[0]["logits"][None], K, W, mode=pnp_ref.MODE_EPNP)
+            n += 1
+            if time.perf_counter() - t0 >= seconds:
+                break
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{n} single-image passes (416x416, Q=11, 6/6, fp32 torch-CPU model + C EPnP oracle) in {dt:.1f}s"}
+
+
+def traffic_for(kind):
+    """HBM bytes per launch of `kind` from a committed PMC summary (profiles/pmc_*.json), or None."""
+    best = None
+    for f in sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*.json"))):
+        try:
+            d = json.load(open(f))
+        except Exception:
+            continue
+        if d.get("kind") == kind and "hbm_bytes_per_launch" in d:
+            best = d["hbm_bytes_per_launch"]
+    return best
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    from spe import dist as sd
+    from spe.config import SpeConfig
+    from spe.models import DETR
+    from spe.pipeline import PosePipeline
+    from spe.solver import build_solver
+    from spe.synthetic import random_weights, synthetic_batch
+    from spe import _lib
+
+    rank, world, local = sd.init_distributed_mode()
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    cfg = SpeConfig(input_size=args.size, num_queries=args.queries, enc_layers=args.layers, dec_layers=args.layers)
+    B = args.batch
+    model = DETR(cfg, dtype=args.dtype)
+    model.load_state_dict(random_weights(cfg, 0))
+    solver = build_solver(argparse.Namespace(solver=args.solver, repro=20))
+    pipe = PosePipeline(model, solver, B, device=dev)
+    data = synthetic_batch(cfg, B, seed=1000 + rank)
+    pipe.load(torch.from_numpy(data["images"]).to(dev), torch.from_numpy(data["clip_bbox"]).float().to(dev),
+              torch.from_numpy(data["quat"]).to(dev), torch.from_numpy(data["tvec"]).to(dev))
+    torch.cuda.synchronize()
+
+    def step():
+        out = pipe.run()
+        if world > 1:
+            rec = sd.pack_records(out["poses"]["quat"], out["poses"]["tvec"], out["s_t"], out["s_q"],
+                                  out["poses"]["status"])
+            sd.all_gather_records(rec)
+        return out
+
+    for _ in range(max(args.warmup, 1)):
+        step()
+    torch.cuda.synchronize()
+
+    # dominant kernel class: one fully profiled step after warm-up
+    L = _lib.lib()
+    L.spe_model_profile_begin(model._h, b"")
+    step()
+    n = L.spe_model_profile_end(model._h)
+    import ctypes
+    tot = {}
+    kb = ctypes.create_string_buffer(64)
+    ms, fl, by = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+    for i in range(n):
+        L.spe_model_profile_get(model._h, i, kb, 64, ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(by))
+        k = kb.value.decode()
+        t = tot.setdefault(k, [0.0, 0])
+        t[0] += ms.value
+        t[1] += 1
+    dominant = max(tot, key=lambda k: tot[k][0])
+
+    # ---- timed region: K steps, dominant kernel bracketed with HIP events on its stream
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    L.spe_model_profile_begin(model._h, dominant.encode())
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    n = L.spe_model_profile_end(model._h)
+    k_ms, k_fl, k_by, k_n = 0.0, 0.0, 0.0, 0
+    for i in range(n):
+        L.spe_model_profile_get(model._h, i, kb, 64, ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(by))
+        if kb.value.decode() == dominant:
+            k_ms += ms.value; k_fl += fl.value; k_by += by.value; k_n += 1
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+
+    score = float((out["s_t"] + out["s_q"]).mean().item())
+    status = out["poses"]["status"].cpu()
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+    total_images = B * world * args.steps
+    avg_ms = k_ms / max(k_n, 1)
+    mfma_bound = dominant.startswith(("conv", "gemm", "attn"))
+    if mfma_bound:
+        achieved = (k_fl / max(k_n, 1)) / (avg_ms * 1e-3) / 1e12
+        peak = PEAK[args.dtype]["mfma"]
+        unit = "TFLOP/s"
+    else:
+        achieved = (k_by / max(k_n, 1)) / (avg_ms * 1e-3) / 1e9
+        peak = PEAK["hbm"]
+        unit = "GB/s"
+    result = {
+        "metric": "images/sec end-to-end (backbone->kpts->PnP) at 416x416; SPEED pose score",
+        "value": total_images / elapsed,
+        "unit": "images/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": args.dtype,
+        "data": "synthetic (seeded SPEED-shaped crops, random-init weights; no checkpoint in the reference)",
+        "config": {"workload": f"BASELINE config 2: ResNet50-s8 + {args.layers}/{args.layers} DETR, "
+                               f"{args.queries} queries, {args.size}x{args.size}, solver={args.solver}",
+                   "global_batch": B * world, "per_gpu_batch": B, "input_size": args.size,
+                   "num_queries": args.queries, "parallelism": f"dp{world} (image sharding)"},
+        "roofline": {"kernel": dominant, "bound": "mfma" if mfma_bound else "hbm", "achieved": achieved,
+                     "peak": peak, "unit": unit, "frac": achieved / peak,
+                     "traffic": traffic_for(dominant), "launches": k_n, "avg_launch_ms": avg_ms,
+                     "algorithmic_flops_per_launch": k_fl / max(k_n, 1),
+                     "algorithmic_bytes_per_launch": k_by / max(k_n, 1)},
+        "kernel_time_ms_per_step": {k: v[0] for k, v in sorted(tot.items(), key=lambda kv: -kv[1][0])},
+        "speed_score_mean_random_weights": score,
+        "solver_status_counts": {str(s): int((status == s).sum()) for s in range(5)},
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+    print(json.dumps(result))
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,132 @@
+/* spe.h — C ABI of the MI355X-native keypoint-set pose path (libspe.so).
+ *
+ * The reference (wwhitecyan/satellite-pose-estimation, REV/ = "Revisiting Monocular Satellite
+ * Pose Estimation With Transformer") has no FFI layer: its seams are Python call signatures.
+ * Each entry point below replaces one of them; the Python host package (spe/) binds them with
+ * ctypes and keeps the reference's call surface.
+ *
+ * Conventions: plain pointers and sizes only; device pointers are caller-owned HIP device memory;
+ * `stream` is a hipStream_t (NULL = default stream); no entry point allocates or synchronises
+ * on the hot path (spe_forward / spe_pnp_batch / spe_speed_score are graph-capturable);
+ * return 0 on success, a negative SPE_E_* code on argument errors, or a positive hipError_t.
+ */
+#ifndef SPE_H_
+#define SPE_H_
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SPE_ABI_VERSION 1
+
+enum {
+  SPE_E_ARG = -1,        /* bad argument / size */
+  SPE_E_STATE = -2,      /* model not finalized / already finalized */
+  SPE_E_MISSING = -3,    /* a required parameter key was never set */
+  SPE_E_KEY = -4,        /* unknown parameter key or wrong element count */
+  SPE_E_WORKSPACE = -5,  /* workspace too small */
+  SPE_E_LAUNCH = -6      /* kernel launch rejected its shapes */
+};
+
+enum { SPE_DTYPE_BF16_ = 0, SPE_DTYPE_F32_ = 1 };
+
+/* Solver modes.
+ *  SPE_PNP_EPNP              cv2.solvePnPGeneric(EPNP) on all selected points
+ *                            (UNC/utils/speed_eval_ceres.py:153-169) — BASELINE config 2
+ *  SPE_PNP_RANSAC_P3P_LM     cv2.solvePnPRansac(P3P) + solvePnPGeneric(ITERATIVE) on inliers
+ *                            (REV/utils/speed_eval.py:209-230) — BASELINE config 3
+ *  SPE_PNP_EPNP_RANSAC_SIGMA cv2.solvePnPRansac(EPNP) + sigma-weighted Huber LM
+ *                            (UNC/utils/speed_eval.py:332-420) — BASELINE config 4
+ *  SPE_PNP_EPNP_LM           EPnP + solvePnPGeneric(ITERATIVE) on all points */
+enum { SPE_PNP_EPNP = 0, SPE_PNP_RANSAC_P3P_LM = 1, SPE_PNP_EPNP_RANSAC_SIGMA = 2, SPE_PNP_EPNP_LM = 3 };
+
+/* Per-image solver status (reference exception mapping, REV/datasets/speed.py:355-363).
+ *  OK              pose solved
+ *  NO_FG           no foreground label -> IndexError in the reference -> zero pose
+ *  CV_ERROR        fewer than 4 correspondences -> cv2.error (CV_Assert npoints >= 4) -> zero pose
+ *  RANSAC_FALLBACK no consensus: the reference keeps the rvec/tvec of the last RANSAC hypothesis
+ *                  (OpenCV's callback shares them) and skips refinement; same here
+ *  UNPINNED        behaviour OpenCV leaves uninitialised (e.g. P3P failure on exactly 4 points);
+ *                  defined here as a zero pose */
+enum { SPE_PNP_OK = 0, SPE_PNP_NO_FG = 1, SPE_PNP_CV_ERROR = 2, SPE_PNP_RANSAC_FALLBACK = 3, SPE_PNP_UNPINNED = 4 };
+
+typedef struct spe_model spe_model;
+
+/* Mirrors the argparse fields build_model(args) reads (REV/main.py:90-187). */
+typedef struct {
+  int input_size;       /* --input_size (416) */
+  int num_queries;      /* --num_queries (11) */
+  int enc_layers;       /* --enc_layers (6) */
+  int dec_layers;       /* --dec_layers (6) */
+  int hidden_dim;       /* --hidden_dim (256; only 256 supported) */
+  int nheads;           /* --nheads (8; head_dim must be 32) */
+  int dim_feedforward;  /* --dim_feedforward (2048) */
+  int sigma_head;       /* 1: UNC-style sigma head (sigma_embed.layers.*) */
+  int dtype;            /* SPE_DTYPE_BF16_ (bf16 storage, fp32 accumulate) or SPE_DTYPE_F32_ */
+} spe_model_config;
+
+typedef struct {
+  float* logits;          /* [B,Q,12] pred_logits (required) */
+  float* points;          /* [B,Q,2]  pred_points, sigmoid, crop-normalised (required) */
+  const float* clip_bbox; /* [B,4] x1,y1,x2,y2 (nullable) -> fused PostProcess */
+  float* probs;           /* [B,Q,12] softmax(pred_logits) (nullable, needs clip_bbox) */
+  float* points_px;       /* [B,Q,2]  image-pixel points (nullable, needs clip_bbox) */
+  float* log_sigmas;      /* [B,Q,2]  sigma head raw output (nullable) */
+  float* sigmas;          /* [B,Q,2]  exp(log_sigmas) (nullable) */
+  float* hs;              /* [B,Q,256] last decoder layer after decoder_norm (nullable) */
+} spe_forward_outputs;
+
+int spe_abi_version(void);
+const char* spe_last_error(void);
+
+/* Model lifecycle.  Replaces build_model(args) (REV/models/__init__.py:5-6) + load_state_dict
+ * (REV/main.py:264-274): parameters are handed over by their reference state_dict key
+ * (412 keys, e.g. "backbone.0.body.layer1.0.conv1.weight"), fp32, host memory. */
+int spe_model_create(const spe_model_config* cfg, spe_model** out);
+void spe_model_destroy(spe_model* m);
+int spe_model_set_param(spe_model* m, const char* key, const float* host_data, int64_t numel);
+int spe_model_num_params(const spe_model* m);                 /* number of required keys */
+const char* spe_model_param_name(const spe_model* m, int i);  /* i-th required key */
+int spe_model_finalize(spe_model* m);  /* fold FrozenBN, pack NHWC/[N][K] weights, upload (current device) */
+int64_t spe_model_workspace_bytes(const spe_model* m, int batch);
+
+/* DETR.forward + PostProcess (REV/models/detr_speed.py:59-92,266-293).
+ * images: device [B,3,S,S] fp32, ImageNet-normalised (REV/datasets/speed.py:25-41). */
+int spe_forward(spe_model* m, void* stream, const float* images, int batch, void* workspace, int64_t workspace_bytes,
+                const spe_forward_outputs* out);
+
+/* PostProcess alone (REV/models/detr_speed.py:266-293). */
+int spe_postprocess(void* stream, const float* logits, const float* points, const float* clip_bbox, int batch,
+                    int num_queries, float* probs, float* points_px);
+
+/* Batched solver (SimplePoseSolver.__call__ per image, REV/utils/speed_eval.py:164-242;
+ * SimplePoseSolverSigma, UNC/utils/speed_eval.py:332-420).  All pointers are device memory.
+ * K: 3x3 row-major fp64; world: [C-1][3] fp64 landmarks (REV/all_result.json).
+ * quat: [B,4] (float32 values, Blender order w,x,y,z); tvec/rvec: [B,3] fp64;
+ * corr_label: [B,16] label of each correspondence in first-seen order (-1 padded);
+ * inlier_mask: [B] bit i = correspondence i is a RANSAC inlier.  Nullable: sigmas, rvec,
+ * status, n_corr, corr_label, inlier_mask. */
+int spe_pnp_batch(void* stream, const float* points_px, const float* probs, const float* sigmas, int batch,
+                  int num_queries, int num_classes, const double* K, const double* world, int mode, float repro,
+                  int ransac_iters, double confidence, float* quat, double* tvec, double* rvec, int32_t* status,
+                  int32_t* n_corr, int32_t* corr_label, uint32_t* inlier_mask);
+
+/* speed_score per image (REV/utils/speed_eval.py:245-262), device pointers. */
+int spe_speed_score(void* stream, const float* quat, const double* tvec, const double* q_gt, const double* t_gt,
+                    int batch, double* s_t, double* s_q);
+
+/* Per-launch profiling of spe_forward with HIP events on the launch stream (no reference
+ * counterpart; used by bench.py for the roofline).  begin: every later launch whose kind starts
+ * with `kind_prefix` ("" = all; kinds: conv.*, gemm.*, attn.enc, attn.dec_*, ln.*, eltwise.*,
+ * heads) is bracketed by events.  end: stops recording, waits for the events, returns the
+ * record count.  get: record i -> kind, elapsed ms, algorithmic flops and bytes. */
+int spe_model_profile_begin(spe_model* m, const char* kind_prefix);
+int spe_model_profile_end(spe_model* m);
+int spe_model_profile_get(const spe_model* m, int i, char* kind, int kind_len, double* ms, double* flops,
+                          double* bytes);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,99 @@
+"""ORACLE (test infrastructure only — never imported by the product path).
+
+ctypes front-end of oracle/pnp_ref.c (the CPU restatement of the reference solver chain,
+REV/utils/speed_eval.py:143-262, UNC/utils/speed_eval.py:269-420) plus numpy restatements of
+the SPEED score (REV/utils/speed_eval.py:245-262) and of the per-image correspondence
+selection (REV/utils/speed_eval.py:152-206), used as checkers by tests/, smoke() and the
+bench's cpu_baseline leg.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from collections import OrderedDict
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "build", "liboracle_pnp.so")
+MAXN = 16
+
+MODE_EPNP, MODE_RANSAC_P3P_LM, MODE_EPNP_RANSAC_SIGMA, MODE_EPNP_LM = 0, 1, 2, 3
+ST_OK, ST_NO_FG, ST_CV_ERROR, ST_RANSAC_FALLBACK, ST_UNPINNED = 0, 1, 2, 3, 4
+
+_lib = None
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        _lib = ctypes.CDLL(LIB)
+        P = ctypes.c_void_p
+        _lib.oracle_pnp_batch.argtypes = [P, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, ctypes.c_int,
+                                          ctypes.c_float, ctypes.c_int, ctypes.c_double, P, P, P, P, P, P]
+        _lib.oracle_speed_score.argtypes = [P, P, P, P, P, P]
+    return _lib
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+def pnp_batch(points, probs, K, world, mode=MODE_RANSAC_P3P_LM, repro=20.0, sigmas=None, iters=100, conf=0.99):
+    """points [B,Q,2] px, probs [B,Q,C] -> dict(quat [B,4], tvec [B,3], status [B], n_corr [B],
+    corr_label [B,16], inlier_mask [B])."""
+    points = np.ascontiguousarray(points, np.float32)
+    probs = np.ascontiguousarray(probs, np.float32)
+    B, Q, C = probs.shape
+    sig = None if sigmas is None else np.ascontiguousarray(sigmas, np.float32)
+    K = np.ascontiguousarray(K, np.float64)
+    world = np.ascontiguousarray(world, np.float64)
+    out = dict(quat=np.zeros((B, 4)), tvec=np.zeros((B, 3)), status=np.zeros(B, np.int32),
+               n_corr=np.zeros(B, np.int32), corr_label=np.full((B, MAXN), -1, np.int32),
+               inlier_mask=np.zeros(B, np.uint32))
+    lib().oracle_pnp_batch(_p(points), _p(probs), _p(sig), B, Q, C, _p(K), _p(world), mode, repro, iters, conf,
+                           _p(out["quat"]), _p(out["tvec"]), _p(out["status"]), _p(out["n_corr"]),
+                           _p(out["corr_label"]), _p(out["inlier_mask"]))
+    return out
+
+
+def speed_score(q_pr, t_pr, q_gt, t_gt):
+    """numpy restatement of REV/utils/speed_eval.py:245-262."""
+    q_pr = np.asarray(q_pr, np.float64).flatten()
+    t_pr = np.asarray(t_pr, np.float64).flatten()
+    q_gt = np.asarray(q_gt, np.float64).flatten()
+    t_gt = np.asarray(t_gt, np.float64).flatten()
+    if q_pr[0] < 0:
+        q_pr = -q_pr
+    if q_gt[0] < 0:
+        q_gt = -q_gt
+    s_t = np.linalg.norm(t_pr - t_gt) / np.linalg.norm(t_gt)
+    s_q = 2 * np.arccos(min(np.abs(np.dot(q_pr, q_gt)), 1))
+    return s_t, s_q
+
+
+def select_correspondences(points, probs):
+    """REV/utils/speed_eval.py:152-206: label = argmax, drop no-object, best-score query per
+    label, first-seen label order.  Returns (labels[list], points float32 [n,2])."""
+    labels = probs.argmax(1)
+    scores = probs.max(1)
+    P = OrderedDict()
+    for q in range(len(labels)):
+        lab = int(labels[q])
+        if lab == probs.shape[1] - 1:
+            continue
+        P.setdefault(lab, []).append((points[q, 0], points[q, 1], scores[q]))
+    labs, pts = [], []
+    for lab, lst in P.items():
+        arr = np.asarray(lst)
+        best = arr[:, -1].argmax()
+        labs.append(lab)
+        pts.append(arr[best, :2])
+    return labs, np.asarray(pts, np.float32).reshape(-1, 2)

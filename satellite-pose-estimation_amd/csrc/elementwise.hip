@@ -1,0 +1,168 @@
+// HBM-bound helpers of the backbone / transformer, vectorised 16 B per lane.
+//   pack_input   NCHW fp32 crop batch (REV/datasets/speed.py:25-41 output contract)
+//                -> NHWC with channels padded to 8 (stem implicit-GEMM operand)
+//   maxpool3s2   torchvision ResNet stem max-pool (3x3, stride 2, pad 1)
+//   upsample2x   nn.UpsamplingBilinear2d(scale_factor=2) == align_corners=True
+//                (REV/models/backbone.py:127,141)
+//   layernorm    nn.LayerNorm(256, eps=1e-5), one wave per row, two-pass variance
+//                (REV/models/transformer.py:147-148,165,167,194-196,117-124)
+#include "spe_common.h"
+#include "spe_kernels.h"
+
+namespace {
+
+template <typename T>
+__global__ void pack_input_kernel(const float* __restrict__ img, T* __restrict__ out, int B, int S) {
+  const size_t npx = (size_t)B * S * S;
+  for (size_t p = blockIdx.x * (size_t)blockDim.x + threadIdx.x; p < npx; p += (size_t)gridDim.x * blockDim.x) {
+    const size_t b = p / ((size_t)S * S), hw = p - b * S * S;
+    const float* src = img + b * 3 * S * S + hw;
+    float v[8] = {src[0], src[(size_t)S * S], src[2 * (size_t)S * S], 0.f, 0.f, 0.f, 0.f, 0.f};
+    if constexpr (sizeof(T) == 2) {
+      st16(out + p * 8, pack16<T>(v));
+    } else {
+      st16(out + p * 8, pack16<T>(v));
+      st16(out + p * 8 + 4, pack16<T>(v + 4));
+    }
+  }
+}
+
+template <typename T>
+__global__ void maxpool_kernel(const T* __restrict__ in, T* __restrict__ out, int B, int H, int W, int C, int Ho, int Wo) {
+  constexpr int CE = Chunk<T>::CE;
+  const int cch = C / CE;
+  const size_t n = (size_t)B * Ho * Wo * cch;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % cch);
+    size_t r = i / cch;
+    const int ow = (int)(r % Wo); r /= Wo;
+    const int oh = (int)(r % Ho);
+    const int b = (int)(r / Ho);
+    float mx[CE];
+#pragma unroll
+    for (int e = 0; e < CE; ++e) mx[e] = -INFINITY;
+    for (int kh = 0; kh < 3; ++kh) {
+      const int ih = oh * 2 - 1 + kh;
+      if (ih < 0 || ih >= H) continue;
+      for (int kw = 0; kw < 3; ++kw) {
+        const int iw = ow * 2 - 1 + kw;
+        if (iw < 0 || iw >= W) continue;
+        float f[CE];
+        unpack16<T>(ld16(in + (((size_t)b * H + ih) * W + iw) * C + c * CE), f);
+#pragma unroll
+        for (int e = 0; e < CE; ++e) mx[e] = fmaxf(mx[e], f[e]);
+      }
+    }
+    st16(out + (((size_t)b * Ho + oh) * Wo + ow) * C + c * CE, pack16<T>(mx));
+  }
+}
+
+template <typename T>
+__global__ void upsample_kernel(const T* __restrict__ in, T* __restrict__ out, int B, int H, int W, int C) {
+  constexpr int CE = Chunk<T>::CE;
+  const int Ho = 2 * H, Wo = 2 * W, cch = C / CE;
+  const float sy = Ho > 1 ? (float)(H - 1) / (float)(Ho - 1) : 0.f;
+  const float sx = Wo > 1 ? (float)(W - 1) / (float)(Wo - 1) : 0.f;
+  const size_t n = (size_t)B * Ho * Wo * cch;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % cch);
+    size_t r = i / cch;
+    const int ox = (int)(r % Wo); r /= Wo;
+    const int oy = (int)(r % Ho);
+    const int b = (int)(r / Ho);
+    // PyTorch upsample_bilinear2d, align_corners=True: src = dst * (in-1)/(out-1)
+    const float fy = oy * sy, fx = ox * sx;
+    const int y0 = (int)fy, x0 = (int)fx;
+    const int y1 = y0 + (y0 < H - 1), x1 = x0 + (x0 < W - 1);
+    const float ly = fy - y0, lx = fx - x0;
+    const float hy = 1.f - ly, hx = 1.f - lx;
+    const T* base = in + (size_t)b * H * W * C + c * CE;
+    float a[CE], bb[CE], cc[CE], d[CE], v[CE];
+    unpack16<T>(ld16(base + ((size_t)y0 * W + x0) * C), a);
+    unpack16<T>(ld16(base + ((size_t)y0 * W + x1) * C), bb);
+    unpack16<T>(ld16(base + ((size_t)y1 * W + x0) * C), cc);
+    unpack16<T>(ld16(base + ((size_t)y1 * W + x1) * C), d);
+#pragma unroll
+    for (int e = 0; e < CE; ++e) v[e] = hy * (hx * a[e] + lx * bb[e]) + ly * (hx * cc[e] + lx * d[e]);
+    st16(out + (((size_t)b * Ho + oy) * Wo + ox) * C + c * CE, pack16<T>(v));
+  }
+}
+
+// D = 256: each lane owns 4 consecutive features.
+template <typename T>
+__global__ void layernorm_kernel(const T* __restrict__ x, const float* __restrict__ gamma, const float* __restrict__ beta,
+                                 T* __restrict__ out, float* __restrict__ out_f32, int M, int D) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const T* xr = x + (size_t)row * D;
+  float v[4];
+  if constexpr (sizeof(T) == 2) {
+    u32x2 u = ld8(xr + 4 * lane);
+    v[0] = __uint_as_float(u.x << 16); v[1] = __uint_as_float(u.x & 0xffff0000u);
+    v[2] = __uint_as_float(u.y << 16); v[3] = __uint_as_float(u.y & 0xffff0000u);
+  } else {
+    unpack16<float>(ld16(xr + 4 * lane), v);
+  }
+  const float mean = wave_sum(v[0] + v[1] + v[2] + v[3]) * (1.f / D);
+  float d0 = v[0] - mean, d1 = v[1] - mean, d2 = v[2] - mean, d3 = v[3] - mean;
+  const float var = wave_sum(d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3) * (1.f / D);
+  const float rs = rsqrtf(var + 1e-5f);
+  const f32x4 g = *reinterpret_cast<const f32x4*>(gamma + 4 * lane);
+  const f32x4 be = *reinterpret_cast<const f32x4*>(beta + 4 * lane);
+  float y[4] = {d0 * rs * g[0] + be[0], d1 * rs * g[1] + be[1], d2 * rs * g[2] + be[2], d3 * rs * g[3] + be[3]};
+  if (out) {
+    T* o = out + (size_t)row * D + 4 * lane;
+    if constexpr (sizeof(T) == 2) st8(o, u32x2{pack_bf16x2(y[0], y[1]), pack_bf16x2(y[2], y[3])});
+    else st16(o, pack16<float>(y));
+  }
+  if (out_f32) st16(out_f32 + (size_t)row * D + 4 * lane, pack16<float>(y));
+}
+
+inline int grid_for(size_t n, int block) {
+  size_t g = (n + block - 1) / block;
+  return (int)(g > 65536 ? 65536 : (g < 1 ? 1 : g));
+}
+
+}  // namespace
+
+int spe_launch_pack_input(const float* img, void* out, int B, int S, int dtype, hipStream_t s) {
+  const size_t n = (size_t)B * S * S;
+  if (dtype == SPE_DTYPE_BF16) hipLaunchKernelGGL(pack_input_kernel<bf16>, grid_for(n, 256), 256, 0, s, img, (bf16*)out, B, S);
+  else hipLaunchKernelGGL(pack_input_kernel<float>, grid_for(n, 256), 256, 0, s, img, (float*)out, B, S);
+  return (int)hipGetLastError();
+}
+
+int spe_launch_maxpool3s2(const void* in, void* out, int B, int H, int W, int C, int Ho, int Wo, int dtype, hipStream_t s) {
+  const int ce = dtype == SPE_DTYPE_BF16 ? 8 : 4;
+  if (C % ce) return -5;
+  const size_t n = (size_t)B * Ho * Wo * (C / ce);
+  if (dtype == SPE_DTYPE_BF16)
+    hipLaunchKernelGGL(maxpool_kernel<bf16>, grid_for(n, 256), 256, 0, s, (const bf16*)in, (bf16*)out, B, H, W, C, Ho, Wo);
+  else
+    hipLaunchKernelGGL(maxpool_kernel<float>, grid_for(n, 256), 256, 0, s, (const float*)in, (float*)out, B, H, W, C, Ho, Wo);
+  return (int)hipGetLastError();
+}
+
+int spe_launch_upsample2x(const void* in, void* out, int B, int H, int W, int C, int dtype, hipStream_t s) {
+  const int ce = dtype == SPE_DTYPE_BF16 ? 8 : 4;
+  if (C % ce) return -5;
+  const size_t n = (size_t)B * 4 * H * W * (C / ce);
+  if (dtype == SPE_DTYPE_BF16)
+    hipLaunchKernelGGL(upsample_kernel<bf16>, grid_for(n, 256), 256, 0, s, (const bf16*)in, (bf16*)out, B, H, W, C);
+  else
+    hipLaunchKernelGGL(upsample_kernel<float>, grid_for(n, 256), 256, 0, s, (const float*)in, (float*)out, B, H, W, C);
+  return (int)hipGetLastError();
+}
+
+int spe_launch_layernorm(const void* x, const float* gamma, const float* beta, void* out, float* out_f32, int M, int D,
+                         int dtype, hipStream_t s) {
+  if (D != 256) return -6;
+  const int rows_per_block = 4;
+  dim3 grid((M + rows_per_block - 1) / rows_per_block), block(64 * rows_per_block);
+  if (dtype == SPE_DTYPE_BF16)
+    hipLaunchKernelGGL(layernorm_kernel<bf16>, grid, block, 0, s, (const bf16*)x, gamma, beta, (bf16*)out, out_f32, M, D);
+  else
+    hipLaunchKernelGGL(layernorm_kernel<float>, grid, block, 0, s, (const float*)x, gamma, beta, (float*)out, out_f32, M, D);
+  return (int)hipGetLastError();
+}

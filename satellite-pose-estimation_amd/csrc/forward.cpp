@@ -1,0 +1,384 @@
+// Native runtime of the keypoint-set predictor, part 2: the launch sequence of one forward
+// pass (REV/models/detr_speed.py:59-92 -> backbone.py:133-149 -> transformer.py:51-63 ->
+// heads + PostProcess) on one HIP stream, and the solver / score entry points.  No allocation
+// or synchronisation happens inside spe_forward / spe_pnp_batch / spe_speed_score, so a caller
+// may capture them into a hipGraph.  Every launch goes through run_gemm / run_attn / run_other,
+// which bracket it with HIP events when the per-launch profiler is on (bench roofline).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+
+#include "model_state.h"
+#include "spe_pnp.h"
+
+#define fail spe_fail
+
+namespace {
+
+hipEvent_t next_event(spe_model* m) {
+  Profiler& p = m->prof;
+  if (p.next_event == p.pool.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    p.pool.push_back(e);
+  }
+  return p.pool[p.next_event++];
+}
+
+bool prof_match(const spe_model* m, const char* kind) {
+  return m->prof.on && std::strncmp(kind, m->prof.filter.c_str(), m->prof.filter.size()) == 0;
+}
+
+int run_other(spe_model* m, const char* kind, double flops, double bytes, hipStream_t s, const std::function<int()>& fn) {
+  if (!prof_match(m, kind)) return fn();
+  ProfRecord r{kind, kind, flops, bytes, next_event(m), next_event(m)};
+  if (!r.beg || !r.end) return (int)hipErrorOutOfMemory;
+  (void)hipEventRecord(r.beg, s);
+  int rc = fn();
+  (void)hipEventRecord(r.end, s);
+  m->prof.recs.push_back(r);
+  return rc;
+}
+
+int run_gemm(spe_model* m, const char* kind, const GemmArgs& g, int mode, hipStream_t s) {
+  const double E = m->esz;
+  const double a_elems = mode == GEMM_CONV ? (double)(g.M / (g.Ho * g.Wo)) * g.H * g.W * g.Cin : (double)g.M * g.K;
+  const double bytes = (a_elems + (double)g.N * g.K + (double)g.M * g.N * (g.R ? 2 : 1)) * E +
+                       (mode == GEMM_LINEAR_ADD ? (double)g.prow * g.K * E : 0.0);
+  return run_other(m, kind, 2.0 * g.M * g.N * g.K, bytes, s,
+                   [&] { return spe_launch_gemm(g, m->cfg.dtype, mode, s); });
+}
+
+int run_attn(spe_model* m, const char* kind, const AttnArgs& a, hipStream_t s) {
+  const double flops = 4.0 * a.B * a.H * (double)a.Tq * a.Tk * 32;
+  const double bytes = (double)a.B * a.H * 32 * (2.0 * a.Tq + 2.0 * a.Tk) * m->esz;
+  return run_other(m, kind, flops, bytes, s, [&] { return spe_launch_attention(a, m->cfg.dtype, s); });
+}
+
+GemmArgs linear_args(const Conv& c, const void* A, int lda, int M, void* C, int ldc) {
+  GemmArgs g{};
+  g.A = A; g.lda = lda;
+  g.B = c.w; g.ldb = c.Kpad;
+  g.M = M; g.N = c.N; g.K = c.K;
+  g.bias = c.bias;
+  g.C = C; g.ldc = ldc;
+  return g;
+}
+
+GemmArgs conv_args(const Conv& c, const void* X, int B, int H, int W, void* Y, int ldc) {
+  GemmArgs g{};
+  g.A = X;
+  g.H = H; g.W = W; g.Cin = c.Cin; g.KH = c.KH; g.KW = c.KW; g.stride = c.stride; g.pad = c.pad;
+  g.Ho = (H + 2 * c.pad - c.KH) / c.stride + 1;
+  g.Wo = (W + 2 * c.pad - c.KW) / c.stride + 1;
+  g.B = c.w; g.ldb = c.Kpad;
+  g.M = B * g.Ho * g.Wo; g.N = c.N; g.K = c.K;
+  g.bias = c.bias;
+  g.C = Y; g.ldc = ldc;
+  return g;
+}
+
+#define CK(x)                                                                   \
+  do {                                                                          \
+    int _r = (x);                                                               \
+    if (_r != 0) {                                                              \
+      char _b[256];                                                             \
+      snprintf(_b, sizeof _b, "%s failed (%d) at %s:%d", #x, _r, __FILE__, __LINE__); \
+      return fail(_r < 0 ? SPE_E_LAUNCH : _r, _b);                              \
+    }                                                                           \
+  } while (0)
+
+
+
+}  // namespace
+
+extern "C" {
+
+int spe_forward(spe_model* m, void* stream, const float* images, int B, void* workspace, int64_t ws_bytes,
+                const spe_forward_outputs* out) {
+  if (!m || !images || !workspace || !out || !out->logits || !out->points || B <= 0)
+    return fail(SPE_E_ARG, "null argument");
+  if (!m->finalized) return fail(SPE_E_STATE, "model not finalized");
+  const Ws w = spe_plan(m, B);
+  if ((int64_t)w.total > ws_bytes) return fail(SPE_E_WORKSPACE, "workspace too small");
+  hipStream_t s = (hipStream_t)stream;
+  const auto& c = m->cfg;
+  const int dt = c.dtype, S = c.input_size, d = c.hidden_dim, ff = c.dim_feedforward, Q = c.num_queries;
+  const int L = c.dec_layers;
+  char* ws = (char*)workspace;
+  auto P = [&](size_t off) { return (void*)(ws + off); };
+
+  // ---------------- backbone (REV/models/backbone.py:133-149)
+  CK(run_other(m, "eltwise.pack", 0.0, (double)B * S * S * (12 + 8 * m->esz), s, [&] { return spe_launch_pack_input(images, P(w.x0), B, S, dt, s); }));
+  {
+    GemmArgs g = conv_args(m->stem, P(w.x0), B, S, S, P(w.stem), 64);
+    g.relu = 1;
+    CK(run_gemm(m, "conv.stem", g, GEMM_CONV, s));
+  }
+  int H = S / 2;
+  const int Hp = (H + 2 - 3) / 2 + 1;
+  CK(run_other(m, "eltwise.maxpool", 0.0, (double)B * 64 * (H * H + Hp * Hp) * m->esz, s, [&] { return spe_launch_maxpool3s2(P(w.stem), P(w.pool), B, H, H, 64, Hp, Hp, dt, s); }));
+  H = Hp;
+  size_t cur = w.pool;                                  // aliases bufA
+  int cin = 64;
+  for (size_t bi = 0; bi < m->blocks.size(); ++bi) {
+    const Block& blk = m->blocks[bi];
+    // layer1: blocks 0-2, layer2: 3-6 (its output xs8 is kept for the neck), layer3: 7-12
+    const size_t outbuf = (bi == 6) ? w.xs8 : (cur == w.bufA ? w.bufB : w.bufA);
+    const int Ho = (H + 2 - 3) / blk.stride + 1;
+    {  // conv1 1x1 + bn1 + relu
+      GemmArgs g = linear_args(blk.c1, P(cur), cin, B * H * H, P(w.t1), blk.c1.N);
+      g.relu = 1;
+      CK(run_gemm(m, "conv.1x1", g, GEMM_LINEAR, s));
+    }
+    {  // conv2 3x3 (stride on the 3x3, ResNet v1.5) + bn2 + relu
+      GemmArgs g = conv_args(blk.c2, P(w.t1), B, H, H, P(w.t2), blk.c2.N);
+      g.relu = 1;
+      CK(run_gemm(m, "conv.3x3", g, GEMM_CONV, s));
+    }
+    size_t res = cur;
+    if (blk.has_ds) {
+      if (blk.stride == 1) {
+        GemmArgs g = linear_args(blk.ds, P(cur), cin, B * H * H, P(w.ds), blk.ds.N);
+        CK(run_gemm(m, "conv.1x1", g, GEMM_LINEAR, s));
+      } else {
+        GemmArgs g = conv_args(blk.ds, P(cur), B, H, H, P(w.ds), blk.ds.N);
+        CK(run_gemm(m, "conv.1x1s2", g, GEMM_CONV, s));
+      }
+      res = w.ds;
+    }
+    {  // conv3 1x1 + bn3 + residual + relu
+      GemmArgs g = linear_args(blk.c3, P(w.t2), blk.c2.N, B * Ho * Ho, P(outbuf), blk.c3.N);
+      g.R = P(res); g.ldr = blk.c3.N; g.relu = 1;
+      CK(run_gemm(m, "conv.1x1", g, GEMM_LINEAR, s));
+    }
+    cin = blk.c3.N;
+    H = Ho;
+    cur = outbuf;
+  }
+  const size_t xs16 = cur;                              // [B, S/16, S/16, 1024]
+  const int F = S / 8, T = F * F;
+  {  // s8_latern 1x1 512->256 into channels [0,256) of the concat buffer
+    GemmArgs g = linear_args(m->s8, P(w.xs8), 512, B * T, P(w.cat), 512);
+    g.bias = nullptr;
+    CK(run_gemm(m, "conv.neck", g, GEMM_LINEAR, s));
+  }
+  CK(run_other(m, "eltwise.upsample", 0.0, (double)B * 1024 * 5 * (S / 16) * (S / 16) * m->esz, s, [&] { return spe_launch_upsample2x(P(xs16), P(w.up), B, S / 16, S / 16, 1024, dt, s); }));
+  {  // s16_latern 3x3 1024->256 into channels [256,512)
+    GemmArgs g = conv_args(m->s16, P(w.up), B, F, F, (char*)P(w.cat) + 256 * m->esz, 512);
+    g.bias = nullptr;
+    CK(run_gemm(m, "conv.neck", g, GEMM_CONV, s));
+  }
+  {  // output_conv 3x3 512->512 + bias
+    GemmArgs g = conv_args(m->outc, P(w.cat), B, F, F, P(w.neck), 512);
+    CK(run_gemm(m, "conv.neck", g, GEMM_CONV, s));
+  }
+  {  // input_proj 1x1 512->256 + bias -> src [B*T, 256] (token order h*W+w)
+    GemmArgs g = linear_args(m->inproj, P(w.neck), 512, B * T, P(w.src), d);
+    CK(run_gemm(m, "gemm.input_proj", g, GEMM_LINEAR, s));
+  }
+
+  // ---------------- encoder (REV/models/transformer.py:154-167)
+  const float scale = 1.0f / std::sqrt(32.0f);
+  const int Mt = B * T;
+  for (const Enc& e : m->enc) {
+    {
+      GemmArgs g = linear_args(e.qk, P(w.src), d, Mt, P(w.qkv), 3 * d);
+      g.P = m->pos; g.ldp = d; g.prow = T;
+      CK(run_gemm(m, "gemm.enc.qk", g, GEMM_LINEAR_ADD, s));
+    }
+    {
+      GemmArgs g = linear_args(e.v, P(w.src), d, Mt, P(w.vt), 8);
+      g.vt_T = T; g.vt_B = B;
+      CK(run_gemm(m, "gemm.enc.v", g, GEMM_LINEAR, s));
+    }
+    {
+      AttnArgs a{};
+      a.q = P(w.qkv); a.ldq = 3 * d;
+      a.k = (char*)P(w.qkv) + d * m->esz; a.ldk = 3 * d;
+      a.vt = P(w.vt);
+      a.o = P(w.ao); a.ldo = d;
+      a.B = B; a.H = c.nheads; a.Tq = T; a.Tk = T; a.scale = scale;
+      CK(run_attn(m, "attn.enc", a, s));
+    }
+    {
+      GemmArgs g = linear_args(e.o, P(w.ao), d, Mt, P(w.tmp), d);
+      g.R = P(w.src); g.ldr = d;
+      CK(run_gemm(m, "gemm.enc.o", g, GEMM_LINEAR, s));
+    }
+    CK(run_other(m, "ln.enc", 0.0, (double)Mt * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.tmp), e.n1g, e.n1b, P(w.src), nullptr, Mt, d, dt, s); }));
+    {
+      GemmArgs g = linear_args(e.l1, P(w.src), d, Mt, P(w.ffn), ff);
+      g.relu = 1;
+      CK(run_gemm(m, "gemm.enc.ffn1", g, GEMM_LINEAR, s));
+    }
+    {
+      GemmArgs g = linear_args(e.l2, P(w.ffn), ff, Mt, P(w.tmp), d);
+      g.R = P(w.src); g.ldr = d;
+      CK(run_gemm(m, "gemm.enc.ffn2", g, GEMM_LINEAR, s));
+    }
+    CK(run_other(m, "ln.enc", 0.0, (double)Mt * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.tmp), e.n2g, e.n2b, P(w.src), nullptr, Mt, d, dt, s); }));
+  }
+  // memory = src.  Cross-attention K (memory + pos) and V^T (memory) for all decoder layers.
+  {
+    GemmArgs g = linear_args(m->crossK, P(w.src), d, Mt, P(w.ck), L * d);
+    g.P = m->pos; g.ldp = d; g.prow = T;
+    CK(run_gemm(m, "gemm.cross_kv", g, GEMM_LINEAR_ADD, s));
+  }
+  {
+    GemmArgs g = linear_args(m->crossV, P(w.src), d, Mt, P(w.cvt), 8);
+    g.vt_T = T; g.vt_B = B;
+    CK(run_gemm(m, "gemm.cross_kv", g, GEMM_LINEAR, s));
+  }
+
+  // ---------------- decoder (REV/models/transformer.py:100-129,218-239)
+  const int Mq = B * Q;
+  CK((int)hipMemsetAsync(P(w.tgt), 0, (size_t)Mq * d * m->esz, s));
+  for (int l = 0; l < L; ++l) {
+    const Dec& e = m->dec[l];
+    {
+      GemmArgs g = linear_args(e.sqk, P(w.tgt), d, Mq, P(w.dqkv), 3 * d);
+      g.P = m->qpos; g.ldp = d; g.prow = Q;
+      CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR_ADD, s));
+    }
+    {
+      GemmArgs g = linear_args(e.sv, P(w.tgt), d, Mq, P(w.dvt), 8);
+      g.vt_T = Q; g.vt_B = B;
+      CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR, s));
+    }
+    {
+      AttnArgs a{};
+      a.q = P(w.dqkv); a.ldq = 3 * d;
+      a.k = (char*)P(w.dqkv) + d * m->esz; a.ldk = 3 * d;
+      a.vt = P(w.dvt);
+      a.o = P(w.dao); a.ldo = d;
+      a.B = B; a.H = c.nheads; a.Tq = Q; a.Tk = Q; a.scale = scale;
+      CK(run_attn(m, "attn.dec_self", a, s));
+    }
+    {
+      GemmArgs g = linear_args(e.so, P(w.dao), d, Mq, P(w.dtmp), d);
+      g.R = P(w.tgt); g.ldr = d;
+      CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR, s));
+    }
+    CK(run_other(m, "ln.dec", 0.0, (double)Mq * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.dtmp), e.n1g, e.n1b, P(w.tgt), nullptr, Mq, d, dt, s); }));
+    {
+      GemmArgs g = linear_args(e.cq, P(w.tgt), d, Mq, P(w.dqc), d);
+      g.P = m->qpos; g.ldp = d; g.prow = Q;
+      CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR_ADD, s));
+    }
+    {
+      AttnArgs a{};
+      a.q = P(w.dqc); a.ldq = d;
+      a.k = (char*)P(w.ck) + (size_t)l * d * m->esz; a.ldk = L * d;
+      a.vt = (char*)P(w.cvt) + (size_t)l * B * d * T * m->esz;
+      a.o = P(w.dao); a.ldo = d;
+      a.B = B; a.H = c.nheads; a.Tq = Q; a.Tk = T; a.scale = scale;
+      CK(run_attn(m, "attn.dec_cross", a, s));
+    }
+    {
+      GemmArgs g = linear_args(e.co, P(w.dao), d, Mq, P(w.dtmp), d);
+      g.R = P(w.tgt); g.ldr = d;
+      CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR, s));
+    }
+    CK(run_other(m, "ln.dec", 0.0, (double)Mq * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.dtmp), e.n2g, e.n2b, P(w.tgt), nullptr, Mq, d, dt, s); }));
+    {
+      GemmArgs g = linear_args(e.l1, P(w.tgt), d, Mq, P(w.dffn), ff);
+      g.relu = 1;
+      CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR, s));
+    }
+    {
+      GemmArgs g = linear_args(e.l2, P(w.dffn), ff, Mq, P(w.dtmp), d);
+      g.R = P(w.tgt); g.ldr = d;
+      CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR, s));
+    }
+    CK(run_other(m, "ln.dec", 0.0, (double)Mq * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.dtmp), e.n3g, e.n3b, P(w.tgt), nullptr, Mq, d, dt, s); }));
+  }
+  float* hs = out->hs ? out->hs : (float*)P(w.hs);
+  CK(run_other(m, "ln.dec", 0.0, (double)Mq * d * (m->esz + 4), s, [&] { return spe_launch_layernorm(P(w.tgt), m->dng, m->dnb, nullptr, hs, Mq, d, dt, s); }));
+
+  // ---------------- heads + PostProcess (REV/models/detr_speed.py:83-92,266-293)
+  HeadArgs h = m->head;
+  h.hs = hs; h.B = B; h.Q = Q;
+  h.clip_bbox = out->clip_bbox;
+  h.logits = out->logits; h.points = out->points;
+  h.probs = out->clip_bbox ? out->probs : nullptr;
+  h.points_px = out->clip_bbox ? out->points_px : nullptr;
+  h.log_sigmas = out->log_sigmas; h.sigmas = out->sigmas;
+  if (!c.sigma_head) { h.log_sigmas = nullptr; h.sigmas = nullptr; }
+  CK(run_other(m, "heads", 0.0, (double)Mq * d * 4, s, [&] { return spe_launch_heads(h, s); }));
+  return 0;
+}
+
+int spe_postprocess(void* stream, const float* logits, const float* points, const float* clip_bbox, int B, int Q,
+                    float* probs, float* points_px) {
+  if (!logits || !points || !clip_bbox || !probs || !points_px || B < 0 || Q <= 0) return fail(SPE_E_ARG, "bad argument");
+  CK(spe_launch_postprocess(logits, points, clip_bbox, B, Q, probs, points_px, (hipStream_t)stream));
+  return 0;
+}
+
+int spe_pnp_batch(void* stream, const float* points_px, const float* probs, const float* sigmas, int B, int Q, int C,
+                  const double* K, const double* world, int mode, float repro, int ransac_iters, double confidence,
+                  float* quat, double* tvec, double* rvec, int32_t* status, int32_t* n_corr, int32_t* corr_label,
+                  uint32_t* inlier_mask) {
+  if (!points_px || !probs || !K || !world || !quat || !tvec || B < 0 || Q <= 0 || Q > 64 || C < 2 || C > 17)
+    return fail(SPE_E_ARG, "bad argument");
+  if (mode < SPE_PNP_EPNP || mode > SPE_PNP_EPNP_LM) return fail(SPE_E_ARG, "bad solver mode");
+  if (ransac_iters < 1 || ransac_iters > 256 || !(confidence > 0 && confidence < 1))
+    return fail(SPE_E_ARG, "ransac_iters must be in [1,256], confidence in (0,1)");
+  PnpArgs a{};
+  a.points = points_px; a.probs = probs; a.sigmas = sigmas;
+  a.B = B; a.Q = Q; a.C = C; a.K = K; a.world = world; a.mode = mode; a.repro = repro;
+  a.ransac_iters = ransac_iters; a.confidence = confidence;
+  a.quat = quat; a.tvec = tvec; a.rvec = rvec; a.status = status; a.n_corr = n_corr;
+  a.corr_label = corr_label; a.inlier_mask = inlier_mask;
+  CK(spe_launch_pnp(a, (hipStream_t)stream));
+  return 0;
+}
+
+int spe_speed_score(void* stream, const float* quat, const double* tvec, const double* q_gt, const double* t_gt, int B,
+                    double* s_t, double* s_q) {
+  if (!quat || !tvec || !q_gt || !t_gt || !s_t || !s_q || B < 0) return fail(SPE_E_ARG, "bad argument");
+  CK(spe_launch_score(quat, tvec, q_gt, t_gt, B, s_t, s_q, (hipStream_t)stream));
+  return 0;
+}
+
+int spe_model_profile_begin(spe_model* m, const char* kind_prefix) {
+  if (!m) return fail(SPE_E_ARG, "null model");
+  m->prof.on = true;
+  m->prof.filter = kind_prefix ? kind_prefix : "";
+  m->prof.recs.clear();
+  m->prof.next_event = 0;
+  return 0;
+}
+
+int spe_model_profile_end(spe_model* m) {
+  if (!m) return fail(SPE_E_ARG, "null model");
+  m->prof.on = false;
+  for (auto& r : m->prof.recs) {
+    hipError_t e = hipEventSynchronize(r.end);
+    if (e != hipSuccess) return fail((int)e, "profile event sync failed");
+  }
+  return (int)m->prof.recs.size();
+}
+
+int spe_model_profile_get(const spe_model* m, int i, char* kind, int kind_len, double* ms, double* flops,
+                          double* bytes) {
+  if (!m || i < 0 || i >= (int)m->prof.recs.size()) return fail(SPE_E_ARG, "bad profile record index");
+  const ProfRecord& r = m->prof.recs[i];
+  if (kind && kind_len > 0) {
+    std::strncpy(kind, r.kind.c_str(), kind_len - 1);
+    kind[kind_len - 1] = 0;
+  }
+  float t = 0.f;
+  hipError_t e = hipEventElapsedTime(&t, r.beg, r.end);
+  if (e != hipSuccess) return fail((int)e, "hipEventElapsedTime failed");
+  if (ms) *ms = t;
+  if (flops) *flops = r.flops;
+  if (bytes) *bytes = r.bytes;
+  return 0;
+}
+
+}  // extern "C"

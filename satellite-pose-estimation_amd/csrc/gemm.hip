@@ -1,0 +1,318 @@
+// MFMA GEMM / implicit-GEMM convolution for gfx950 with fused epilogues.
+//
+// One kernel serves every contraction on the path except attention:
+//   * ResNet-50 convs (REV/models/backbone.py:114-131 via torchvision), FrozenBN folded into
+//     the weights + bias (REV/models/backbone.py:44-54), ReLU / residual add fused;
+//   * neck 1x1 / 3x3 convs (REV/models/backbone.py:127-131), concat fused by writing into a
+//     channel slice of one NHWC buffer (ldc + column offset);
+//   * input_proj (REV/models/detr_speed.py:54-55) and every nn.Linear / MHA projection of the
+//     transformer (REV/models/transformer.py:137-145,181-191), with the `src + pos` /
+//     `tgt + query_pos` add fused into the A-operand load (REV/models/transformer.py:158,225)
+//     and the value projection optionally stored head-transposed ([g][b][hd][token]) for the
+//     attention kernel's V^T tiles.
+//
+// C[M,N] = A[M,K] . W[N,K]^T (+bias, +residual, ReLU).  Activations are NHWC / token-major
+// rows, weights row-major [N][Kpad] (Kpad % 64 == 0, zero padded).
+// Tile 128x128, 256 threads = 4 waves (2x2), wave tile 64x64 = 4x4 16x16 MFMA fragments.
+// One K-step moves 128 bytes of every row: 64 bf16 (2 x mfma_f32_16x16x32_bf16) or 32 fp32
+// (8 x mfma_f32_16x16x4f32, exact f32).  Global -> register -> LDS staging, double-buffered,
+// XOR-swizzled 16-byte slots (conflict-free ds_read_b128 fragment reads), one barrier per step.
+#include "spe_common.h"
+#include "spe_kernels.h"
+
+namespace {
+
+constexpr int BM = 128, BN = 128, NT = 256;
+constexpr int STAGE_BYTES = (BM + BN) * 128;          // 32 KiB per stage
+constexpr int EPI_LD = BN + 4;                         // fp32 row stride of the epilogue tile
+constexpr int SMEM_BYTES = (2 * STAGE_BYTES > BM * EPI_LD * 4) ? 2 * STAGE_BYTES : BM * EPI_LD * 4;
+
+SPE_DEV int swz(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+
+template <typename T, int MODE>
+struct ALoader {
+  static constexpr int CE = Chunk<T>::CE;
+  // per-thread: 4 rows, one chunk column
+  const char* base[4];
+  int ih0[4], iw0[4];
+  bool rv[4];
+
+  SPE_DEV void init(const GemmArgs& g, int m0, int tid) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int m = m0 + (tid >> 3) + 32 * i;
+      rv[i] = m < g.M;
+      int mm = rv[i] ? m : 0;
+      if (MODE == GEMM_CONV) {
+        int hw = g.Ho * g.Wo;
+        int b = mm / hw, r = mm - b * hw;
+        int oh = r / g.Wo, ow = r - oh * g.Wo;
+        ih0[i] = oh * g.stride - g.pad;
+        iw0[i] = ow * g.stride - g.pad;
+        base[i] = (const char*)g.A + (size_t)b * g.H * g.W * g.Cin * sizeof(T);
+      } else {
+        base[i] = (const char*)g.A + (size_t)mm * g.lda * sizeof(T);
+        ih0[i] = (MODE == GEMM_LINEAR_ADD) ? (mm % g.prow) : 0;
+        iw0[i] = 0;
+      }
+    }
+  }
+
+  SPE_DEV void load(const GemmArgs& g, int kstep, int tid, u32x4* r) const {
+    constexpr int BKE = 128 / sizeof(T);
+    const int k = kstep * BKE + (tid & 7) * CE;
+    const bool kv = k < g.K;
+    if (MODE == GEMM_CONV) {
+      int kpos = k / g.Cin, ci = k - kpos * g.Cin;
+      int kh = kpos / g.KW, kw = kpos - kh * g.KW;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        int ih = ih0[i] + kh, iw = iw0[i] + kw;
+        bool v = kv && rv[i] && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+        r[i] = v ? ld16(base[i] + ((size_t)(ih * g.W + iw) * g.Cin + ci) * sizeof(T)) : u32x4{0, 0, 0, 0};
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        bool v = kv && rv[i];
+        u32x4 x = v ? ld16(base[i] + (size_t)k * sizeof(T)) : u32x4{0, 0, 0, 0};
+        if (MODE == GEMM_LINEAR_ADD) {
+          if (v) {
+            u32x4 p = ld16((const char*)g.P + ((size_t)ih0[i] * g.ldp + k) * sizeof(T));
+            float fx[CE], fp[CE];
+            unpack16<T>(x, fx);
+            unpack16<T>(p, fp);
+#pragma unroll
+            for (int e = 0; e < CE; ++e) fx[e] += fp[e];
+            x = pack16<T>(fx);
+          }
+        }
+        r[i] = x;
+      }
+    }
+  }
+};
+
+template <typename T>
+SPE_DEV void load_b(const GemmArgs& g, int n0, int kstep, int tid, u32x4* r) {
+  constexpr int BKE = 128 / sizeof(T);
+  const int k = kstep * BKE + (tid & 7) * Chunk<T>::CE;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int n = n0 + (tid >> 3) + 32 * i;
+    r[i] = (n < g.N) ? ld16((const char*)g.B + ((size_t)n * g.ldb + k) * sizeof(T)) : u32x4{0, 0, 0, 0};
+  }
+}
+
+SPE_DEV void store_stage(char* st, int tid, const u32x4* ra, const u32x4* rb) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int row = (tid >> 3) + 32 * i, c = tid & 7;
+    st16(st + swz(row, c), ra[i]);
+    st16(st + BM * 128 + swz(row, c), rb[i]);
+  }
+}
+
+template <typename T>
+SPE_DEV void mma_step(const char* st, int wr, int wc, int lane, f32x4 (&acc)[4][4]) {
+  const int g = lane >> 4, rr = lane & 15;
+  u32x4 a0[4], a1[4], b0[4], b1[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    int row = wr * 64 + i * 16 + rr;
+    a0[i] = ld16(st + swz(row, g));
+    a1[i] = ld16(st + swz(row, g + 4));
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    int row = wc * 64 + j * 16 + rr;
+    b0[j] = ld16(st + BM * 128 + swz(row, g));
+    b1[j] = ld16(st + BM * 128 + swz(row, g + 4));
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      if constexpr (sizeof(T) == 2) {
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a0[i]),
+                                                             __builtin_bit_cast(bf16x8, b0[j]), acc[i][j], 0, 0, 0);
+        acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a1[i]),
+                                                             __builtin_bit_cast(bf16x8, b1[j]), acc[i][j], 0, 0, 0);
+      } else {
+        f32x4 fa0 = __builtin_bit_cast(f32x4, a0[i]), fb0 = __builtin_bit_cast(f32x4, b0[j]);
+        f32x4 fa1 = __builtin_bit_cast(f32x4, a1[i]), fb1 = __builtin_bit_cast(f32x4, b1[j]);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa0[s], fb0[s], acc[i][j], 0, 0, 0);
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x4f32(fa1[s], fb1[s], acc[i][j], 0, 0, 0);
+      }
+    }
+}
+
+template <typename T, int MODE>
+__global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int tilesN = (g.N + BN - 1) / BN;
+  const int nwg = gridDim.x;
+  const int t = xcd_remap(blockIdx.x, nwg);
+  const int m0 = (t / tilesN) * BM, n0 = (t % tilesN) * BN;
+  constexpr int BKE = 128 / sizeof(T);
+  const int nk = (g.K + BKE - 1) / BKE;
+
+  ALoader<T, MODE> al;
+  al.init(g, m0, tid);
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  u32x4 ra[4], rb[4];
+  al.load(g, 0, tid, ra);
+  load_b<T>(g, n0, 0, tid, rb);
+  store_stage(smem, tid, ra, rb);
+  __syncthreads();
+  for (int ks = 0; ks < nk; ++ks) {
+    const bool more = ks + 1 < nk;
+    if (more) {
+      al.load(g, ks + 1, tid, ra);
+      load_b<T>(g, n0, ks + 1, tid, rb);
+    }
+    mma_step<T>(smem + (ks & 1) * STAGE_BYTES, wr, wc, lane, acc);
+    if (more) store_stage(smem + ((ks + 1) & 1) * STAGE_BYTES, tid, ra, rb);
+    __syncthreads();
+  }
+
+  // ---- epilogue: accumulators -> LDS fp32 tile -> fused bias/residual/ReLU -> wide stores
+  float* ct = reinterpret_cast<float*>(smem);
+  {
+    const int q = lane >> 4, c = lane & 15;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          ct[(wr * 64 + i * 16 + q * 4 + r) * EPI_LD + wc * 64 + j * 16 + c] = acc[i][j][r];
+  }
+  __syncthreads();
+
+  if (g.vt_T > 0) {
+    // head-transposed store: column n = grp*256 + hd -> C[((grp*vt_B + b)*256 + hd)*T + tok]
+    const int col = tid & 127, n = n0 + col;
+    if (n >= g.N) return;
+    const float bv = g.bias ? g.bias[n] : 0.f;
+    const int grp = n >> 8, hd = n & 255;
+    for (int rg = (tid >> 7) * 8; rg < BM; rg += 16) {
+      const int m = m0 + rg;
+      if (m >= g.M) break;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = ct[(rg + e) * EPI_LD + col] + bv;
+      const int b = m / g.vt_T, tok = m - b * g.vt_T;
+      const size_t rowbase = ((size_t)(grp * g.vt_B + b) * 256 + hd) * g.vt_T;
+      if ((g.vt_T & 7) == 0 && m + 8 <= g.M) {
+        char* cp = (char*)g.C + (rowbase + tok) * sizeof(T);
+        if constexpr (sizeof(T) == 2) {
+          st16(cp, pack16<T>(v));
+        } else {
+          st16(cp, pack16<T>(v));
+          st16(cp + 16, pack16<T>(v + 4));
+        }
+      } else {
+        for (int e = 0; e < 8 && m + e < g.M; ++e) {
+          const int me = m + e, be = me / g.vt_T, te = me - be * g.vt_T;
+          ((T*)g.C)[((size_t)(grp * g.vt_B + be) * 256 + hd) * g.vt_T + te] = from_f32<T>(v[e]);
+        }
+      }
+    }
+    return;
+  }
+
+  const int cg = (tid & 15) * 8;
+  const int n = n0 + cg;
+  if (n >= g.N) return;
+  float bv[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) bv[e] = (g.bias && n + e < g.N) ? g.bias[n + e] : 0.f;
+  const bool full = n + 8 <= g.N;
+  for (int rr = tid >> 4; rr < BM; rr += 16) {
+    const int m = m0 + rr;
+    if (m >= g.M) break;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = ct[rr * EPI_LD + cg + e] + bv[e];
+    if (g.R) {
+      const T* rp = (const T*)g.R + (size_t)m * g.ldr + n;
+      if (full) {
+        if constexpr (sizeof(T) == 2) {
+          float f[8];
+          unpack16<T>(ld16(rp), f);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += f[e];
+        } else {
+          float f[8];
+          unpack16<T>(ld16(rp), f);
+          unpack16<T>(ld16(rp + 4), f + 4);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] += f[e];
+        }
+      } else {
+        for (int e = 0; e < 8 && n + e < g.N; ++e) v[e] += to_f32(rp[e]);
+      }
+    }
+    if (g.relu) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+    if (g.out_f32) {
+      float* cp = (float*)g.C + (size_t)m * g.ldc + n;
+      if (full) {
+        st16(cp, pack16<float>(v));
+        st16(cp + 4, pack16<float>(v + 4));
+      } else {
+        for (int e = 0; e < 8 && n + e < g.N; ++e) cp[e] = v[e];
+      }
+    } else {
+      T* cp = (T*)g.C + (size_t)m * g.ldc + n;
+      if (full) {
+        if constexpr (sizeof(T) == 2) {
+          st16(cp, pack16<T>(v));
+        } else {
+          st16(cp, pack16<T>(v));
+          st16(cp + 4, pack16<T>(v + 4));
+        }
+      } else {
+        for (int e = 0; e < 8 && n + e < g.N; ++e) cp[e] = from_f32<T>(v[e]);
+      }
+    }
+  }
+}
+
+template <typename T>
+int launch_t(const GemmArgs& g, int mode, hipStream_t s) {
+  const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
+  if (tiles <= 0) return 0;
+  dim3 grid(tiles), block(NT);
+  switch (mode) {
+    case GEMM_LINEAR: hipLaunchKernelGGL((gemm_kernel<T, GEMM_LINEAR>), grid, block, 0, s, g); break;
+    case GEMM_LINEAR_ADD: hipLaunchKernelGGL((gemm_kernel<T, GEMM_LINEAR_ADD>), grid, block, 0, s, g); break;
+    case GEMM_CONV: hipLaunchKernelGGL((gemm_kernel<T, GEMM_CONV>), grid, block, 0, s, g); break;
+    default: return -1;
+  }
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+int spe_launch_gemm(const GemmArgs& g, int dtype, int mode, hipStream_t s) {
+  constexpr int CEb = 8, CEf = 4;
+  const int ce = dtype == SPE_DTYPE_BF16 ? CEb : CEf;
+  if (g.K % ce) return -2;                                   // K must be whole 16-byte chunks
+  if (mode == GEMM_CONV && (g.Cin % ce)) return -3;
+  if (g.ldb % 64) return -4;                                 // weights padded to 64 elements
+  if ((g.lda % ce) || (g.ldc % (g.out_f32 ? 4 : ce)) || (g.R && (g.ldr % ce))) return -5;
+  return dtype == SPE_DTYPE_BF16 ? launch_t<bf16>(g, mode, s) : launch_t<float>(g, mode, s);
+}

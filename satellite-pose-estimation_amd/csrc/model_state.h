@@ -1,0 +1,78 @@
+// Internal state of a spe_model (shared by registry.cpp and forward.cpp).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "../../include/spe.h"
+#include "spe_kernels.h"
+
+struct Conv {              // conv / linear packed as [N][Kpad] in T, bias fp32
+  void* w = nullptr;
+  float* bias = nullptr;
+  int N = 0, K = 0, Kpad = 0, Cin = 0, KH = 1, KW = 1, stride = 1, pad = 0;
+};
+
+struct Block {
+  Conv c1, c2, c3, ds;
+  bool has_ds = false;
+  int stride = 1;
+};
+
+struct Enc {
+  Conv qk, v, o, l1, l2;
+  float *n1g, *n1b, *n2g, *n2b;
+};
+
+struct Dec {
+  Conv sqk, sv, so, cq, co, l1, l2;
+  float *n1g, *n1b, *n2g, *n2b, *n3g, *n3b;
+};
+
+struct Ws {                // workspace layout (byte offsets)
+  size_t x0, stem, pool, bufA, bufB, t1, t2, ds, xs8, up, cat, neck;
+  size_t src, qkv, vt, ao, tmp, ffn, ck, cvt;
+  size_t tgt, dtmp, dqkv, dvt, dao, dqc, dffn, hs;
+  size_t total;
+};
+
+// Per-launch HIP-event profiler (spe_model_profile_*): brackets every launch whose kind
+// starts with `filter` with events on the launch stream and accumulates algorithmic work.
+struct ProfRecord {
+  std::string kind, name;
+  double flops, bytes;
+  hipEvent_t beg, end;
+};
+struct Profiler {
+  bool on = false;
+  std::string filter;
+  std::vector<ProfRecord> recs;
+  std::vector<hipEvent_t> pool;
+  size_t next_event = 0;
+};
+
+struct spe_model {
+  spe_model_config cfg{};
+  int esz = 2;
+  std::vector<std::pair<std::string, std::vector<int64_t>>> spec;
+  std::map<std::string, std::vector<float>> host;
+  bool finalized = false;
+  char* dmem = nullptr;
+  size_t dbytes = 0, dused = 0;
+  int upload_err = 0;
+  Conv stem, s8, s16, outc, inproj, crossK, crossV;
+  std::vector<Block> blocks;
+  std::vector<Enc> enc;
+  std::vector<Dec> dec;
+  void* pos = nullptr;     // [tokens][256] T
+  void* qpos = nullptr;    // [Q][256] T
+  float *dng = nullptr, *dnb = nullptr;
+  HeadArgs head{};
+  Profiler prof;
+};
+
+int spe_fail(int code, const std::string& msg);
+Ws spe_plan(const spe_model* m, int B);

@@ -1,0 +1,435 @@
+// Native runtime of the keypoint-set predictor, part 1: parameter registry in the
+// reference's state_dict key space (REV/models/detr_speed.py:296-336 -> 412 keys), FrozenBN
+// folding (REV/models/backbone.py:44-54), weight packing ([N][KH][KW][Cin] rows, bf16/fp32),
+// workspace planning.  The launch sequence lives in forward.cpp.
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+
+#include "model_state.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+uint16_t f2bf(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return (uint16_t)((u >> 16) | 0x40);  // quiet NaN
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+}  // namespace
+
+int spe_fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define fail spe_fail
+
+namespace {
+
+std::vector<std::pair<std::string, std::vector<int64_t>>> build_spec(const spe_model_config& c) {
+  std::vector<std::pair<std::string, std::vector<int64_t>>> s;
+  const int64_t d = c.hidden_dim, ff = c.dim_feedforward;
+  auto add = [&](const std::string& k, std::vector<int64_t> sh) { s.emplace_back(k, std::move(sh)); };
+  auto bn = [&](const std::string& p, int64_t ch) {
+    for (const char* n : {"weight", "bias", "running_mean", "running_var"}) add(p + "." + n, {ch});
+  };
+  for (int i = 0; i < c.enc_layers; ++i) {
+    std::string p = "transformer.encoder.layers." + std::to_string(i);
+    add(p + ".self_attn.in_proj_weight", {3 * d, d}); add(p + ".self_attn.in_proj_bias", {3 * d});
+    add(p + ".self_attn.out_proj.weight", {d, d}); add(p + ".self_attn.out_proj.bias", {d});
+    add(p + ".linear1.weight", {ff, d}); add(p + ".linear1.bias", {ff});
+    add(p + ".linear2.weight", {d, ff}); add(p + ".linear2.bias", {d});
+    for (const char* n : {"norm1", "norm2"}) { add(p + "." + n + ".weight", {d}); add(p + "." + n + ".bias", {d}); }
+  }
+  for (int i = 0; i < c.dec_layers; ++i) {
+    std::string p = "transformer.decoder.layers." + std::to_string(i);
+    for (const char* a : {"self_attn", "multihead_attn"}) {
+      add(p + "." + a + ".in_proj_weight", {3 * d, d}); add(p + "." + a + ".in_proj_bias", {3 * d});
+      add(p + "." + a + ".out_proj.weight", {d, d}); add(p + "." + a + ".out_proj.bias", {d});
+    }
+    add(p + ".linear1.weight", {ff, d}); add(p + ".linear1.bias", {ff});
+    add(p + ".linear2.weight", {d, ff}); add(p + ".linear2.bias", {d});
+    for (const char* n : {"norm1", "norm2", "norm3"}) { add(p + "." + n + ".weight", {d}); add(p + "." + n + ".bias", {d}); }
+  }
+  add("transformer.decoder.norm.weight", {d}); add("transformer.decoder.norm.bias", {d});
+  add("cls_embed.weight", {12, d}); add("cls_embed.bias", {12});
+  add("point_embed.layers.0.weight", {d, d}); add("point_embed.layers.0.bias", {d});
+  add("point_embed.layers.1.weight", {d, d}); add("point_embed.layers.1.bias", {d});
+  add("point_embed.layers.2.weight", {2, d}); add("point_embed.layers.2.bias", {2});
+  add("query_embed.weight", {c.num_queries, d});
+  add("input_proj.weight", {d, 512, 1, 1}); add("input_proj.bias", {d});
+  const std::string b = "backbone.0.body";
+  add(b + ".conv1.weight", {64, 3, 7, 7});
+  bn(b + ".bn1", 64);
+  int64_t cin = 64;
+  const int widths[3] = {64, 128, 256}, nblk[3] = {3, 4, 6};
+  for (int li = 0; li < 3; ++li)
+    for (int k = 0; k < nblk[li]; ++k) {
+      const int64_t w = widths[li];
+      std::string p = b + ".layer" + std::to_string(li + 1) + "." + std::to_string(k);
+      add(p + ".conv1.weight", {w, cin, 1, 1}); bn(p + ".bn1", w);
+      add(p + ".conv2.weight", {w, w, 3, 3}); bn(p + ".bn2", w);
+      add(p + ".conv3.weight", {4 * w, w, 1, 1}); bn(p + ".bn3", 4 * w);
+      if (k == 0) { add(p + ".downsample.0.weight", {4 * w, cin, 1, 1}); bn(p + ".downsample.1", 4 * w); }
+      cin = 4 * w;
+    }
+  add("backbone.0.s8_latern.weight", {256, 512, 1, 1});
+  add("backbone.0.s16_latern.weight", {256, 1024, 3, 3});
+  add("backbone.0.output_conv.weight", {512, 512, 3, 3});
+  add("backbone.0.output_conv.bias", {512});
+  if (c.sigma_head) {
+    add("sigma_embed.layers.0.weight", {d, d}); add("sigma_embed.layers.0.bias", {d});
+    add("sigma_embed.layers.1.weight", {d, d}); add("sigma_embed.layers.1.bias", {d});
+    add("sigma_embed.layers.2.weight", {1, d}); add("sigma_embed.layers.2.bias", {1});
+  }
+  return s;
+}
+
+void* dalloc(spe_model* m, size_t bytes) {
+  size_t off = (m->dused + 255) & ~size_t(255);
+  m->dused = off + bytes;
+  return m->dmem ? (void*)(m->dmem + off) : nullptr;
+}
+
+// pack host fp32 [N][K] rows (already in K order) into device T [N][Kpad]
+void* upload_rows(spe_model* m, const std::vector<float>& rows, int N, int K, int Kpad) {
+  void* dst = dalloc(m, (size_t)N * Kpad * m->esz);
+  if (!m->dmem) return nullptr;
+  if (m->esz == 2) {
+    std::vector<uint16_t> h((size_t)N * Kpad, 0);
+    for (int n = 0; n < N; ++n)
+      for (int k = 0; k < K; ++k) h[(size_t)n * Kpad + k] = f2bf(rows[(size_t)n * K + k]);
+    m->upload_err |= (int)hipMemcpy(dst, h.data(), h.size() * 2, hipMemcpyHostToDevice);
+  } else {
+    std::vector<float> h((size_t)N * Kpad, 0.f);
+    for (int n = 0; n < N; ++n) std::memcpy(&h[(size_t)n * Kpad], &rows[(size_t)n * K], (size_t)K * 4);
+    m->upload_err |= (int)hipMemcpy(dst, h.data(), h.size() * 4, hipMemcpyHostToDevice);
+  }
+  return dst;
+}
+
+float* upload_f32(spe_model* m, const float* p, size_t n) {
+  float* dst = (float*)dalloc(m, n * 4);
+  if (m->dmem) m->upload_err |= (int)hipMemcpy(dst, p, n * 4, hipMemcpyHostToDevice);
+  return dst;
+}
+
+void* upload_T(spe_model* m, const std::vector<float>& v) {
+  void* dst = dalloc(m, v.size() * m->esz);
+  if (!m->dmem) return nullptr;
+  if (m->esz == 2) {
+    std::vector<uint16_t> h(v.size());
+    for (size_t i = 0; i < v.size(); ++i) h[i] = f2bf(v[i]);
+    m->upload_err |= (int)hipMemcpy(dst, h.data(), h.size() * 2, hipMemcpyHostToDevice);
+  } else {
+    m->upload_err |= (int)hipMemcpy(dst, v.data(), v.size() * 4, hipMemcpyHostToDevice);
+  }
+  return dst;
+}
+
+int pad64(int k) { return (k + 63) / 64 * 64; }
+
+// conv weight [Cout][Cin][KH][KW] (+FrozenBN) -> [Cout][KH][KW][Cin_pad] rows, folded bias
+Conv make_conv(spe_model* m, const std::string& wkey, const std::string& bnkey, const std::string& biaskey, int cin_pad,
+               int stride, int pad) {
+  const auto& spec_w = m->host[wkey];
+  int64_t cout = 0, cin = 0, kh = 0, kw = 0;
+  for (auto& s : m->spec)
+    if (s.first == wkey) { cout = s.second[0]; cin = s.second[1]; kh = s.second[2]; kw = s.second[3]; }
+  std::vector<double> scale(cout, 1.0), shift(cout, 0.0);
+  if (!bnkey.empty()) {
+    const auto& g = m->host[bnkey + ".weight"];
+    const auto& b = m->host[bnkey + ".bias"];
+    const auto& rm = m->host[bnkey + ".running_mean"];
+    const auto& rv = m->host[bnkey + ".running_var"];
+    for (int64_t c = 0; c < cout; ++c) {
+      scale[c] = (double)g[c] / std::sqrt((double)rv[c] + 1e-5);
+      shift[c] = (double)b[c] - (double)rm[c] * scale[c];
+    }
+  }
+  if (!biaskey.empty()) {
+    const auto& bb = m->host[biaskey];
+    for (int64_t c = 0; c < cout; ++c) shift[c] += bb[c];
+  }
+  const int cp = cin_pad > 0 ? cin_pad : (int)cin;
+  const int K = (int)(kh * kw * cp);
+  std::vector<float> rows((size_t)cout * K, 0.f);
+  for (int64_t co = 0; co < cout; ++co)
+    for (int64_t ci = 0; ci < cin; ++ci)
+      for (int64_t y = 0; y < kh; ++y)
+        for (int64_t x = 0; x < kw; ++x)
+          rows[(size_t)co * K + (y * kw + x) * cp + ci] =
+              (float)(spec_w[((co * cin + ci) * kh + y) * kw + x] * scale[co]);
+  std::vector<float> bias(shift.begin(), shift.end());
+  Conv c;
+  c.N = (int)cout; c.K = K; c.Kpad = pad64(K); c.Cin = cp; c.KH = (int)kh; c.KW = (int)kw; c.stride = stride; c.pad = pad;
+  c.w = upload_rows(m, rows, c.N, c.K, c.Kpad);
+  c.bias = upload_f32(m, bias.data(), bias.size());
+  return c;
+}
+
+// linear rows [r0, r0+n) of a [*, K] weight + bias slice
+Conv make_linear(spe_model* m, const std::string& wkey, const std::string& bkey, int r0, int n, int K) {
+  const auto& w = m->host[wkey];
+  std::vector<float> rows(w.begin() + (size_t)r0 * K, w.begin() + (size_t)(r0 + n) * K);
+  Conv c;
+  c.N = n; c.K = K; c.Kpad = pad64(K); c.Cin = K;
+  c.w = upload_rows(m, rows, n, K, c.Kpad);
+  const auto& b = m->host[bkey];
+  c.bias = upload_f32(m, b.data() + r0, n);
+  return c;
+}
+
+float* upload_key(spe_model* m, const std::string& k) {
+  const auto& v = m->host[k];
+  return upload_f32(m, v.data(), v.size());
+}
+
+float* upload_transposed(spe_model* m, const std::string& k, int out, int in) {
+  const auto& v = m->host[k];
+  std::vector<float> t((size_t)in * out);
+  for (int o = 0; o < out; ++o)
+    for (int i = 0; i < in; ++i) t[(size_t)i * out + o] = v[(size_t)o * in + i];
+  return upload_f32(m, t.data(), t.size());
+}
+
+// sine position table for an all-valid mask (REV/models/position_encoding.py:30-53),
+// [h*w][256] in token order h*W + w
+std::vector<float> sine_pos(int h, int w, int d) {
+  const int npf = d / 2;
+  const float eps = 1e-6f, scale = 6.283185307179586f;
+  std::vector<float> out((size_t)h * w * d);
+  std::vector<float> dim_t(npf);
+  for (int i = 0; i < npf; ++i) dim_t[i] = std::pow(10000.0f, (float)(2 * (i / 2)) / (float)npf);
+  for (int y = 0; y < h; ++y)
+    for (int x = 0; x < w; ++x) {
+      const float ye = (float)(y + 1) / ((float)h + eps) * scale;
+      const float xe = (float)(x + 1) / ((float)w + eps) * scale;
+      float* o = &out[((size_t)y * w + x) * d];
+      for (int i = 0; i < npf; ++i) {
+        const float py = ye / dim_t[i], px = xe / dim_t[i];
+        o[i] = (i & 1) ? std::cos(py) : std::sin(py);
+        o[npf + i] = (i & 1) ? std::cos(px) : std::sin(px);
+      }
+    }
+  return out;
+}
+
+int build_device(spe_model* m) {
+  const auto& c = m->cfg;
+  const int d = c.hidden_dim, ff = c.dim_feedforward, Q = c.num_queries;
+  const std::string b = "backbone.0.body";
+  m->stem = make_conv(m, b + ".conv1.weight", b + ".bn1", "", 8, 2, 3);
+  m->blocks.clear();
+  const int nblk[3] = {3, 4, 6};
+  for (int li = 0; li < 3; ++li)
+    for (int k = 0; k < nblk[li]; ++k) {
+      std::string p = b + ".layer" + std::to_string(li + 1) + "." + std::to_string(k);
+      Block blk;
+      blk.stride = (k == 0 && li > 0) ? 2 : 1;
+      blk.c1 = make_conv(m, p + ".conv1.weight", p + ".bn1", "", 0, 1, 0);
+      blk.c2 = make_conv(m, p + ".conv2.weight", p + ".bn2", "", 0, blk.stride, 1);
+      blk.c3 = make_conv(m, p + ".conv3.weight", p + ".bn3", "", 0, 1, 0);
+      if (k == 0) {
+        blk.has_ds = true;
+        blk.ds = make_conv(m, p + ".downsample.0.weight", p + ".downsample.1", "", 0, blk.stride, 0);
+      }
+      m->blocks.push_back(blk);
+    }
+  m->s8 = make_conv(m, "backbone.0.s8_latern.weight", "", "", 0, 1, 0);
+  m->s16 = make_conv(m, "backbone.0.s16_latern.weight", "", "", 0, 1, 1);
+  m->outc = make_conv(m, "backbone.0.output_conv.weight", "", "backbone.0.output_conv.bias", 0, 1, 1);
+  m->inproj = make_conv(m, "input_proj.weight", "", "input_proj.bias", 0, 1, 0);
+
+  m->enc.clear();
+  for (int i = 0; i < c.enc_layers; ++i) {
+    std::string p = "transformer.encoder.layers." + std::to_string(i);
+    Enc e;
+    e.qk = make_linear(m, p + ".self_attn.in_proj_weight", p + ".self_attn.in_proj_bias", 0, 2 * d, d);
+    e.v = make_linear(m, p + ".self_attn.in_proj_weight", p + ".self_attn.in_proj_bias", 2 * d, d, d);
+    e.o = make_linear(m, p + ".self_attn.out_proj.weight", p + ".self_attn.out_proj.bias", 0, d, d);
+    e.l1 = make_linear(m, p + ".linear1.weight", p + ".linear1.bias", 0, ff, d);
+    e.l2 = make_linear(m, p + ".linear2.weight", p + ".linear2.bias", 0, d, ff);
+    e.n1g = upload_key(m, p + ".norm1.weight"); e.n1b = upload_key(m, p + ".norm1.bias");
+    e.n2g = upload_key(m, p + ".norm2.weight"); e.n2b = upload_key(m, p + ".norm2.bias");
+    m->enc.push_back(e);
+  }
+  m->dec.clear();
+  std::vector<float> kall, vall, kb, vb;
+  for (int i = 0; i < c.dec_layers; ++i) {
+    std::string p = "transformer.decoder.layers." + std::to_string(i);
+    Dec e;
+    e.sqk = make_linear(m, p + ".self_attn.in_proj_weight", p + ".self_attn.in_proj_bias", 0, 2 * d, d);
+    e.sv = make_linear(m, p + ".self_attn.in_proj_weight", p + ".self_attn.in_proj_bias", 2 * d, d, d);
+    e.so = make_linear(m, p + ".self_attn.out_proj.weight", p + ".self_attn.out_proj.bias", 0, d, d);
+    e.cq = make_linear(m, p + ".multihead_attn.in_proj_weight", p + ".multihead_attn.in_proj_bias", 0, d, d);
+    e.co = make_linear(m, p + ".multihead_attn.out_proj.weight", p + ".multihead_attn.out_proj.bias", 0, d, d);
+    e.l1 = make_linear(m, p + ".linear1.weight", p + ".linear1.bias", 0, ff, d);
+    e.l2 = make_linear(m, p + ".linear2.weight", p + ".linear2.bias", 0, d, ff);
+    e.n1g = upload_key(m, p + ".norm1.weight"); e.n1b = upload_key(m, p + ".norm1.bias");
+    e.n2g = upload_key(m, p + ".norm2.weight"); e.n2b = upload_key(m, p + ".norm2.bias");
+    e.n3g = upload_key(m, p + ".norm3.weight"); e.n3b = upload_key(m, p + ".norm3.bias");
+    m->dec.push_back(e);
+    const auto& w = m->host[p + ".multihead_attn.in_proj_weight"];
+    const auto& bb = m->host[p + ".multihead_attn.in_proj_bias"];
+    kall.insert(kall.end(), w.begin() + (size_t)d * d, w.begin() + (size_t)2 * d * d);
+    vall.insert(vall.end(), w.begin() + (size_t)2 * d * d, w.begin() + (size_t)3 * d * d);
+    kb.insert(kb.end(), bb.begin() + d, bb.begin() + 2 * d);
+    vb.insert(vb.end(), bb.begin() + 2 * d, bb.begin() + 3 * d);
+  }
+  // all decoder layers' cross-attention K/V projections of the (fixed) memory, batched
+  m->crossK.N = m->crossV.N = c.dec_layers * d;
+  m->crossK.K = m->crossV.K = d;
+  m->crossK.Kpad = m->crossV.Kpad = pad64(d);
+  m->crossK.w = upload_rows(m, kall, m->crossK.N, d, m->crossK.Kpad);
+  m->crossK.bias = upload_f32(m, kb.data(), kb.size());
+  m->crossV.w = upload_rows(m, vall, m->crossV.N, d, m->crossV.Kpad);
+  m->crossV.bias = upload_f32(m, vb.data(), vb.size());
+
+  const int fs = c.input_size / 8;
+  m->pos = upload_T(m, sine_pos(fs, fs, d));
+  m->qpos = upload_T(m, m->host["query_embed.weight"]);
+  m->dng = upload_key(m, "transformer.decoder.norm.weight");
+  m->dnb = upload_key(m, "transformer.decoder.norm.bias");
+
+  HeadArgs& h = m->head;
+  h.D = d;
+  h.cls_wt = upload_transposed(m, "cls_embed.weight", 12, d); h.cls_b = upload_key(m, "cls_embed.bias");
+  h.pt_w0t = upload_transposed(m, "point_embed.layers.0.weight", d, d); h.pt_b0 = upload_key(m, "point_embed.layers.0.bias");
+  h.pt_w1t = upload_transposed(m, "point_embed.layers.1.weight", d, d); h.pt_b1 = upload_key(m, "point_embed.layers.1.bias");
+  h.pt_w2t = upload_transposed(m, "point_embed.layers.2.weight", 2, d); h.pt_b2 = upload_key(m, "point_embed.layers.2.bias");
+  if (c.sigma_head) {
+    h.sg_w0t = upload_transposed(m, "sigma_embed.layers.0.weight", d, d); h.sg_b0 = upload_key(m, "sigma_embed.layers.0.bias");
+    h.sg_w1t = upload_transposed(m, "sigma_embed.layers.1.weight", d, d); h.sg_b1 = upload_key(m, "sigma_embed.layers.1.bias");
+    h.sg_w2t = upload_transposed(m, "sigma_embed.layers.2.weight", 1, d); h.sg_b2 = upload_key(m, "sigma_embed.layers.2.bias");
+  } else {
+    h.sg_w0t = h.sg_b0 = h.sg_w1t = h.sg_b1 = h.sg_w2t = h.sg_b2 = nullptr;
+  }
+  (void)Q;
+  return 0;
+}
+
+}  // namespace
+
+Ws spe_plan(const spe_model* m, int B) {
+  const auto& c = m->cfg;
+  const size_t E = m->esz;
+  const size_t S = c.input_size, H2 = S / 2, H4 = S / 4, H8 = S / 8, H16 = S / 16;
+  const size_t T = H8 * H8, Q = c.num_queries, d = c.hidden_dim, ff = c.dim_feedforward, L = c.dec_layers;
+  Ws w{};
+  size_t off = 0;
+  auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) & ~size_t(255); return o; };
+  const size_t big = (size_t)B * std::max(H4 * H4 * 256, H2 * H2 * 64) * E;
+  w.bufA = take(big);
+  w.bufB = take(big);
+  w.stem = w.bufB;                                   // consumed by the max-pool before layer1 writes bufB
+  w.pool = w.bufA;
+  w.t1 = take((size_t)B * std::max(std::max(H4 * H4 * 128, S * S * 8), H8 * H8 * 256) * E);
+  w.x0 = w.t1;                                       // consumed by the stem before t1 is used
+  w.t2 = take((size_t)B * std::max(H4 * H4 * 64, std::max(H8 * H8 * 128, H16 * H16 * 256)) * E);
+  w.ds = take((size_t)B * H4 * H4 * 256 * E);
+  w.xs8 = take((size_t)B * H8 * H8 * 512 * E);
+  w.up = take((size_t)B * H8 * H8 * 1024 * E);
+  w.cat = take((size_t)B * H8 * H8 * 512 * E);
+  w.neck = take((size_t)B * H8 * H8 * 512 * E);
+  w.src = take((size_t)B * T * d * E);
+  w.qkv = take((size_t)B * T * 3 * d * E);
+  w.vt = take((size_t)B * T * d * E);
+  w.ao = take((size_t)B * T * d * E);
+  w.tmp = take((size_t)B * T * d * E);
+  w.ffn = take((size_t)B * T * ff * E);
+  w.ck = take((size_t)B * T * L * d * E);
+  w.cvt = take((size_t)B * T * L * d * E);
+  w.tgt = take((size_t)B * Q * d * E);
+  w.dtmp = take((size_t)B * Q * d * E);
+  w.dqkv = take((size_t)B * Q * 3 * d * E);
+  w.dvt = take((size_t)B * Q * d * E);
+  w.dao = take((size_t)B * Q * d * E);
+  w.dqc = take((size_t)B * Q * d * E);
+  w.dffn = take((size_t)B * Q * ff * E);
+  w.hs = take((size_t)B * Q * d * 4);
+  w.total = off;
+  return w;
+}
+
+extern "C" {
+
+int spe_abi_version(void) { return SPE_ABI_VERSION; }
+const char* spe_last_error(void) { return g_err.c_str(); }
+
+int spe_model_create(const spe_model_config* cfg, spe_model** out) {
+  if (!cfg || !out) return fail(SPE_E_ARG, "null argument");
+  if (cfg->hidden_dim != 256 || cfg->nheads * 32 != cfg->hidden_dim)
+    return fail(SPE_E_ARG, "only hidden_dim=256 with head_dim=32 is supported");
+  if (cfg->input_size % 16 || cfg->input_size < 32) return fail(SPE_E_ARG, "input_size must be a multiple of 16");
+  if (cfg->num_queries < 1 || cfg->num_queries > 64) return fail(SPE_E_ARG, "num_queries must be in [1, 64]");
+  if (cfg->dim_feedforward % 64) return fail(SPE_E_ARG, "dim_feedforward must be a multiple of 64");
+  if (cfg->dtype != SPE_DTYPE_BF16_ && cfg->dtype != SPE_DTYPE_F32_) return fail(SPE_E_ARG, "bad dtype");
+  spe_model* m = new spe_model();
+  m->cfg = *cfg;
+  m->esz = cfg->dtype == SPE_DTYPE_BF16_ ? 2 : 4;
+  m->spec = build_spec(*cfg);
+  *out = m;
+  return 0;
+}
+
+void spe_model_destroy(spe_model* m) {
+  if (!m) return;
+  if (m->dmem) (void)hipFree(m->dmem);
+  for (auto e : m->prof.pool) (void)hipEventDestroy(e);
+  delete m;
+}
+
+int spe_model_num_params(const spe_model* m) { return m ? (int)m->spec.size() : 0; }
+const char* spe_model_param_name(const spe_model* m, int i) {
+  return (m && i >= 0 && i < (int)m->spec.size()) ? m->spec[i].first.c_str() : nullptr;
+}
+
+int spe_model_set_param(spe_model* m, const char* key, const float* data, int64_t numel) {
+  if (!m || !key || !data) return fail(SPE_E_ARG, "null argument");
+  if (m->finalized) return fail(SPE_E_STATE, "model already finalized");
+  for (auto& s : m->spec)
+    if (s.first == key) {
+      int64_t n = 1;
+      for (auto v : s.second) n *= v;
+      if (n != numel) return fail(SPE_E_KEY, std::string("wrong element count for ") + key);
+      m->host[key].assign(data, data + numel);
+      return 0;
+    }
+  return fail(SPE_E_KEY, std::string("unknown parameter key ") + key);
+}
+
+int spe_model_finalize(spe_model* m) {
+  if (!m) return fail(SPE_E_ARG, "null model");
+  if (m->finalized) return fail(SPE_E_STATE, "model already finalized");
+  for (auto& s : m->spec)
+    if (!m->host.count(s.first)) return fail(SPE_E_MISSING, "missing parameter " + s.first);
+  // pass 1 sizes the device block, pass 2 packs and uploads
+  m->dmem = nullptr;
+  m->dused = 0;
+  build_device(m);
+  m->dbytes = m->dused;
+  hipError_t e = hipMalloc((void**)&m->dmem, m->dbytes);
+  if (e != hipSuccess) return fail((int)e, "hipMalloc of weights failed");
+  m->dused = 0;
+  m->upload_err = 0;
+  build_device(m);
+  e = hipDeviceSynchronize();
+  if (e != hipSuccess || m->upload_err) return fail(e != hipSuccess ? (int)e : m->upload_err, "weight upload failed");
+  m->host.clear();
+  m->finalized = true;
+  return 0;
+}
+
+int64_t spe_model_workspace_bytes(const spe_model* m, int batch) {
+  if (!m || batch <= 0) return -1;
+  return (int64_t)spe_plan(m, batch).total;
+}
+
+}  // extern "C"

@@ -1,0 +1,78 @@
+// Shared device helpers for the gfx950 (CDNA4) keypoint-set pose path.
+// Storage type T is either __bf16 (throughput path, fp32 accumulate) or float (parity path,
+// exact-f32 MFMA).  Every kernel is written once for both, so the fp32 parity tests exercise
+// the same tiling and indexing as the bf16 bench path.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef __bf16 bf16;
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+
+#define SPE_DEV __device__ __forceinline__
+
+SPE_DEV float to_f32(float x) { return x; }
+SPE_DEV float to_f32(bf16 x) { return (float)x; }
+template <typename T> SPE_DEV T from_f32(float x);
+template <> SPE_DEV float from_f32<float>(float x) { return x; }
+template <> SPE_DEV bf16 from_f32<bf16>(float x) { return (bf16)x; }
+
+// 16-byte chunk holds CE elements of T.
+template <typename T> struct Chunk { static constexpr int CE = 16 / sizeof(T); };
+
+// load / store 16 bytes
+SPE_DEV u32x4 ld16(const void* p) { return *reinterpret_cast<const u32x4*>(p); }
+SPE_DEV void st16(void* p, u32x4 v) { *reinterpret_cast<u32x4*>(p) = v; }
+SPE_DEV u32x2 ld8(const void* p) { return *reinterpret_cast<const u32x2*>(p); }
+SPE_DEV void st8(void* p, u32x2 v) { *reinterpret_cast<u32x2*>(p) = v; }
+
+// unpack a 16-byte chunk to floats / pack floats to a chunk
+template <typename T> SPE_DEV void unpack16(u32x4 v, float* f);
+template <> SPE_DEV void unpack16<float>(u32x4 v, float* f) {
+  f[0] = __uint_as_float(v.x); f[1] = __uint_as_float(v.y);
+  f[2] = __uint_as_float(v.z); f[3] = __uint_as_float(v.w);
+}
+template <> SPE_DEV void unpack16<bf16>(u32x4 v, float* f) {
+  uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    f[2 * i] = __uint_as_float(w[i] << 16);
+    f[2 * i + 1] = __uint_as_float(w[i] & 0xffff0000u);
+  }
+}
+template <typename T> SPE_DEV u32x4 pack16(const float* f);
+template <> SPE_DEV u32x4 pack16<float>(const float* f) {
+  return u32x4{__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]), __float_as_uint(f[3])};
+}
+SPE_DEV uint32_t pack_bf16x2(float lo, float hi) {
+  bf16 a = (bf16)lo, b = (bf16)hi;
+  return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+}
+template <> SPE_DEV u32x4 pack16<bf16>(const float* f) {
+  return u32x4{pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]), pack_bf16x2(f[6], f[7])};
+}
+
+SPE_DEV float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+SPE_DEV float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// Bijective XCD-aware remap of a 1-D grid: blocks that land on one XCD (b % 8 equal under
+// round-robin dispatch) get a contiguous range of tile ids, so neighbouring tiles that share
+// operand panels hit the same L2.  Speed only, never correctness.
+SPE_DEV int xcd_remap(int bid, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7;
+  const int xcd = bid & 7, idx = bid >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
+}

@@ -1,0 +1,62 @@
+// Internal launcher interface between the C++ runtime (model.cpp, pnp host code) and the HIP
+// kernels.  Not part of the public C ABI (include/spe.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+enum { SPE_DTYPE_BF16 = 0, SPE_DTYPE_F32 = 1 };
+enum { GEMM_LINEAR = 0, GEMM_LINEAR_ADD = 1, GEMM_CONV = 2 };
+
+struct GemmArgs {
+  const void* A; int lda;          // LINEAR*: A[m*lda + k]; CONV: NHWC input [B][H][W][Cin]
+  const void* P; int ldp; int prow;// LINEAR_ADD: A += P[(m % prow)*ldp + k]
+  int H, W, Cin, KH, KW, stride, pad, Ho, Wo;   // CONV geometry
+  const void* B; int ldb;          // weights [N][ldb], ldb % 64 == 0
+  int M, N, K;
+  const float* bias;               // [N] or null
+  const void* R; int ldr;          // residual [m*ldr + n] or null
+  int relu;
+  void* C; int ldc;                // output [m*ldc + n]
+  int out_f32;                     // store fp32 instead of T
+  int vt_T, vt_B;                  // >0: head-transposed store (see gemm.hip)
+};
+int spe_launch_gemm(const GemmArgs& g, int dtype, int mode, hipStream_t s);
+
+struct AttnArgs {
+  const void* q; int ldq;          // query row b*Tq+i, head h at columns [h*32, h*32+32)
+  const void* k; int ldk;          // key row b*Tk+j
+  const void* vt;                  // V^T [B][H][32][Tk]
+  void* o; int ldo;                // output row b*Tq+i
+  int B, H, Tq, Tk;
+  float scale;                     // softmax scale (1/sqrt(head_dim))
+};
+int spe_launch_attention(const AttnArgs& a, int dtype, hipStream_t s);
+
+int spe_launch_pack_input(const float* img, void* out, int B, int S, int dtype, hipStream_t s);
+int spe_launch_maxpool3s2(const void* in, void* out, int B, int H, int W, int C, int Ho, int Wo,
+                          int dtype, hipStream_t s);
+int spe_launch_upsample2x(const void* in, void* out, int B, int H, int W, int C, int dtype, hipStream_t s);
+int spe_launch_layernorm(const void* x, const float* gamma, const float* beta, void* out, float* out_f32,
+                         int M, int D, int dtype, hipStream_t s);
+
+struct HeadArgs {
+  const float* hs;                 // [B*Q][256] fp32 (decoder_norm output of the last layer)
+  int B, Q, D;
+  const float* cls_wt; const float* cls_b;        // [D][12], [12]
+  const float* pt_w0t; const float* pt_b0;        // [D][D]
+  const float* pt_w1t; const float* pt_b1;
+  const float* pt_w2t; const float* pt_b2;        // [D][2]
+  const float* sg_w0t; const float* sg_b0;        // sigma head (nullable)
+  const float* sg_w1t; const float* sg_b1;
+  const float* sg_w2t; const float* sg_b2;        // [D][1]
+  const float* clip_bbox;          // [B][4] (nullable -> no pixel rescale)
+  float* logits;                   // [B][Q][12]
+  float* points;                   // [B][Q][2] crop-normalised (sigmoid)
+  float* probs;                    // [B][Q][12] softmax (nullable)
+  float* points_px;                // [B][Q][2] image px (nullable)
+  float* log_sigmas;               // [B][Q][2] (nullable)
+  float* sigmas;                   // [B][Q][2] exp (nullable)
+};
+int spe_launch_heads(const HeadArgs& a, hipStream_t s);
+int spe_launch_postprocess(const float* logits, const float* points, const float* clip_bbox, int B, int Q,
+                           float* probs, float* points_px, hipStream_t s);

@@ -1,0 +1,99 @@
+"""ctypes binding of libspe.so (C ABI in include/spe.h).
+
+torch is imported first on purpose: its bundled libamdhip64.so.7 is then the HIP runtime the
+library binds to (same SONAME), so device pointers and streams are shared with torch.
+There is no fallback: if the library is missing the import fails loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libspe.so")
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+I64 = ctypes.c_int64
+F = ctypes.c_float
+D = ctypes.c_double
+
+SPE_DTYPE_BF16, SPE_DTYPE_F32 = 0, 1
+SPE_PNP_EPNP, SPE_PNP_RANSAC_P3P_LM, SPE_PNP_EPNP_RANSAC_SIGMA, SPE_PNP_EPNP_LM = 0, 1, 2, 3
+SPE_PNP_OK, SPE_PNP_NO_FG, SPE_PNP_CV_ERROR, SPE_PNP_RANSAC_FALLBACK, SPE_PNP_UNPINNED = 0, 1, 2, 3, 4
+
+# every symbol include/spe.h declares (checked by tests/test_capi.py)
+EXPORTS = ["spe_abi_version", "spe_last_error", "spe_model_create", "spe_model_destroy", "spe_model_set_param",
+           "spe_model_num_params", "spe_model_param_name", "spe_model_finalize", "spe_model_workspace_bytes",
+           "spe_forward", "spe_postprocess", "spe_pnp_batch", "spe_speed_score", "spe_model_profile_begin",
+           "spe_model_profile_end", "spe_model_profile_get"]
+
+
+class ModelConfig(ctypes.Structure):
+    _fields_ = [("input_size", I), ("num_queries", I), ("enc_layers", I), ("dec_layers", I), ("hidden_dim", I),
+                ("nheads", I), ("dim_feedforward", I), ("sigma_head", I), ("dtype", I)]
+
+
+class ForwardOutputs(ctypes.Structure):
+    _fields_ = [("logits", P), ("points", P), ("clip_bbox", P), ("probs", P), ("points_px", P),
+                ("log_sigmas", P), ("sigmas", P), ("hs", P)]
+
+
+class SpeError(RuntimeError):
+    pass
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"libspe.so not built ({LIB_PATH}); run __graft_entry__.build()")
+    L = ctypes.CDLL(LIB_PATH)
+    L.spe_abi_version.restype = I
+    L.spe_last_error.restype = ctypes.c_char_p
+    L.spe_model_create.argtypes = [ctypes.POINTER(ModelConfig), ctypes.POINTER(P)]
+    L.spe_model_destroy.argtypes = [P]
+    L.spe_model_destroy.restype = None
+    L.spe_model_set_param.argtypes = [P, ctypes.c_char_p, P, I64]
+    L.spe_model_num_params.argtypes = [P]
+    L.spe_model_param_name.argtypes = [P, I]
+    L.spe_model_param_name.restype = ctypes.c_char_p
+    L.spe_model_finalize.argtypes = [P]
+    L.spe_model_workspace_bytes.argtypes = [P, I]
+    L.spe_model_workspace_bytes.restype = I64
+    L.spe_forward.argtypes = [P, P, P, I, P, I64, ctypes.POINTER(ForwardOutputs)]
+    L.spe_postprocess.argtypes = [P, P, P, P, I, I, P, P]
+    L.spe_pnp_batch.argtypes = [P, P, P, P, I, I, I, P, P, I, F, I, D, P, P, P, P, P, P, P]
+    L.spe_speed_score.argtypes = [P, P, P, P, P, I, P, P]
+    L.spe_model_profile_begin.argtypes = [P, ctypes.c_char_p]
+    L.spe_model_profile_end.argtypes = [P]
+    L.spe_model_profile_get.argtypes = [P, I, ctypes.c_char_p, I, ctypes.POINTER(D), ctypes.POINTER(D),
+                                        ctypes.POINTER(D)]
+    if L.spe_abi_version() != 1:
+        raise ImportError("libspe.so ABI version mismatch")
+    _lib = L
+    return L
+
+
+def check(rc: int, what: str):
+    if rc != 0:
+        msg = lib().spe_last_error().decode(errors="replace")
+        raise SpeError(f"{what} failed with code {rc}: {msg}")
+
+
+def ptr(t):
+    """Device (or host) pointer of a torch tensor, None for None."""
+    if t is None:
+        return None
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def stream_ptr(stream=None):
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return ctypes.c_void_p(s.cuda_stream)

@@ -1,0 +1,35 @@
+"""evaluate() with the reference's signature (REV/engine.py:78-135).
+
+Per batch: one device pass (model + fused PostProcess), one batched solver launch and one
+D2H copy of the pose records, instead of the reference's per-image Python solver loop.
+The criterion (Hungarian matcher + losses, REV/engine.py:99-112) only feeds logging and is
+skipped when None (it is out of the inference scope).
+"""
+from __future__ import annotations
+
+import torch
+
+from . import dist as spe_dist
+from .speed_eval import SpeedEval, device_speed_score
+
+
+@torch.no_grad()
+def evaluate(model, criterion, postprocessors, data_loader, gt_file, solver, device, output_dir=None):
+    evaluator = SpeedEval(gt_file, solver)
+    for samples, targets in data_loader:
+        samples = samples.to(device)
+        filenames = [t["filename"] for t in targets]
+        clip = torch.stack([torch.as_tensor(t["clip_bbox"], dtype=torch.float32) for t in targets]).to(device)
+        outputs = model(samples, clip_bbox=clip)
+        if criterion is not None:
+            criterion(outputs, [{k: v.to(device) for k, v in t.items() if torch.is_tensor(v)} for t in targets])
+        poses = solver.solve_batch(outputs["points_px"], outputs["probs"], outputs.get("sigmas"))
+        gt = [evaluator.ground_truth[f] for f in filenames]
+        q_gt = torch.tensor([g["quat"] for g in gt], dtype=torch.float64, device=device)
+        t_gt = torch.tensor([g["tvec"] for g in gt], dtype=torch.float64, device=device)
+        s_t, s_q = device_speed_score(poses["quat"], poses["tvec"], q_gt, t_gt)
+        evaluator.update_batch(filenames, outputs["points_px"], outputs["probs"], poses, s_t, s_q)
+    evaluator.log = spe_dist.all_gather_log(evaluator.log)
+    evaluator.summarize()
+    stats = {"speed_eval_pose": evaluator.stats}
+    return stats, evaluator

@@ -1,0 +1,167 @@
+"""Host-side mirror of the reference model interface (REV/models/__init__.py:5-6,
+REV/models/detr_speed.py:32-100,264-336) over the HIP path in libspe.so.
+
+    model, criterion, postprocessors = build_model(args)
+    model.load_state_dict(state_dict)      # the reference's 412 keys (checkpoint['model'])
+    out = model(samples)                   # NestedTensor | list[Tensor] | Tensor [B,3,S,S]
+    results = postprocessors['points'](out, clip_bbox_list)
+
+Every forward runs the hand-written HIP kernels through the C ABI; there is no torch/CPU
+compute fallback.  torch is only used for device memory and the current stream.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+from torch import nn
+
+from . import _lib
+from .config import SpeConfig
+from .misc import NestedTensor, nested_tensor_from_tensor_list
+
+
+class DETR(nn.Module):
+    """Keypoint-set predictor (REV/models/detr_speed.py:32-100), HIP implementation.
+
+    dtype "bf16": bf16 storage / MFMA with fp32 accumulation, softmax, LayerNorm and heads
+    (throughput path).  dtype "fp32": exact-f32 MFMA everywhere (parity path)."""
+
+    def __init__(self, cfg: SpeConfig, dtype: str = "bf16", aux_loss: bool = False):
+        super().__init__()
+        self.cfg = cfg
+        self.num_queries = cfg.num_queries
+        self.aux_loss = aux_loss
+        self.dtype = dtype
+        self._pending = {}
+        self._handle = None
+        self._ws = None
+        self._ws_batch = 0
+        L = _lib.lib()
+        c = _lib.ModelConfig(cfg.input_size, cfg.num_queries, cfg.enc_layers, cfg.dec_layers, cfg.hidden_dim,
+                             cfg.nheads, cfg.dim_feedforward, int(cfg.sigma_head),
+                             _lib.SPE_DTYPE_BF16 if dtype == "bf16" else _lib.SPE_DTYPE_F32)
+        h = ctypes.c_void_p()
+        _lib.check(L.spe_model_create(ctypes.byref(c), ctypes.byref(h)), "spe_model_create")
+        self._h = h
+        self._keys = [L.spe_model_param_name(h, i).decode() for i in range(L.spe_model_num_params(h))]
+
+    # ---------------------------------------------------------------- parameters
+    def param_keys(self):
+        return list(self._keys)
+
+    def load_state_dict(self, state_dict, strict: bool = True):
+        """Accepts the reference's state_dict (torch tensors or numpy arrays).  Keys outside the
+        inference path (none for REV) are reported as unexpected, like nn.Module."""
+        L = _lib.lib()
+        unexpected = []
+        for k, v in state_dict.items():
+            if k.endswith("num_batches_tracked"):       # FrozenBatchNorm2d drops it (backbone.py:36-42)
+                continue
+            if k not in self._keys:
+                unexpected.append(k)
+                continue
+            a = np.ascontiguousarray(v.detach().cpu().numpy() if torch.is_tensor(v) else v, dtype=np.float32)
+            _lib.check(L.spe_model_set_param(self._h, k.encode(), a.ctypes.data_as(ctypes.c_void_p), a.size),
+                       f"set_param({k})")
+            self._pending[k] = True
+        missing = [k for k in self._keys if k not in self._pending]
+        if strict and (missing or unexpected):
+            raise RuntimeError(f"load_state_dict: missing={missing[:5]}... unexpected={unexpected[:5]}...")
+        self._finalize()
+        return missing, unexpected
+
+    def _finalize(self):
+        if self._handle is None and len(self._pending) == len(self._keys):
+            _lib.check(_lib.lib().spe_model_finalize(self._h), "spe_model_finalize")
+            self._handle = self._h
+
+    def workspace(self, B, device):
+        if self._ws is None or self._ws_batch < B:
+            nbytes = _lib.lib().spe_model_workspace_bytes(self._h, B)
+            self._ws = torch.empty(int(nbytes), dtype=torch.uint8, device=device)
+            self._ws_batch = B
+        return self._ws
+
+    # ---------------------------------------------------------------- forward
+    def forward(self, samples, clip_bbox=None, stream=None):
+        """REV/models/detr_speed.py:59-92.  Returns pred_logits [B,Q,12], pred_points [B,Q,2]
+        (+ pred_sigmas as log-sigma when the sigma head is configured).  Passing `clip_bbox`
+        ([B,4] device fp32) also runs the fused PostProcess and adds `probs` / `points_px`."""
+        if self._handle is None:
+            raise RuntimeError("DETR: load_state_dict() with every parameter before forward()")
+        if isinstance(samples, (list, tuple)):            # REV/models/detr_speed.py:74-75
+            samples = nested_tensor_from_tensor_list(list(samples))
+        images = samples.tensors if isinstance(samples, NestedTensor) else samples
+        if not images.is_cuda:
+            raise RuntimeError("DETR (HIP) expects device tensors; call samples.to('cuda')")
+        images = images.contiguous().float()
+        B, C, H, W = images.shape
+        S = self.cfg.input_size
+        if C != 3 or H != S or W != S:
+            raise ValueError(f"expected [B,3,{S},{S}] input, got {tuple(images.shape)}")
+        dev = images.device
+        Q = self.cfg.num_queries
+        out = {"pred_logits": torch.empty(B, Q, 12, device=dev), "pred_points": torch.empty(B, Q, 2, device=dev)}
+        if self.cfg.sigma_head:
+            out["pred_sigmas"] = torch.empty(B, Q, 2, device=dev)
+            out["sigmas"] = torch.empty(B, Q, 2, device=dev)
+        if clip_bbox is not None:
+            clip_bbox = clip_bbox.to(device=dev, dtype=torch.float32).contiguous()
+            out["probs"] = torch.empty(B, Q, 12, device=dev)
+            out["points_px"] = torch.empty(B, Q, 2, device=dev)
+        o = _lib.ForwardOutputs(_lib.ptr(out["pred_logits"]), _lib.ptr(out["pred_points"]), _lib.ptr(clip_bbox),
+                                _lib.ptr(out.get("probs")), _lib.ptr(out.get("points_px")),
+                                _lib.ptr(out.get("pred_sigmas")), _lib.ptr(out.get("sigmas")), None)
+        ws = self.workspace(B, dev)
+        _lib.check(_lib.lib().spe_forward(self._h, _lib.stream_ptr(stream), _lib.ptr(images), B, _lib.ptr(ws),
+                                          ws.numel(), ctypes.byref(o)), "spe_forward")
+        return out
+
+    def __del__(self):
+        try:
+            if getattr(self, "_h", None):
+                _lib.lib().spe_model_destroy(self._h)
+                self._h = None
+        except Exception:
+            pass
+
+
+class PostProcess(nn.Module):
+    """REV/models/detr_speed.py:264-293 (and the sigma variant,
+    UNC/src/zoo/rtdetr/rtdetr_postprocessor.py:44-78): softmax over the 12 classes and
+    crop -> image pixel rescale, on device; returns the reference's list of numpy dicts."""
+
+    @torch.no_grad()
+    def forward(self, outputs, clip_bbox, stream=None):
+        logits, points = outputs["pred_logits"], outputs["pred_points"]
+        B, Q, _ = logits.shape
+        assert len(clip_bbox) == B
+        dev = logits.device
+        bb = torch.stack([torch.as_tensor(b, dtype=torch.float32) for b in clip_bbox]).to(dev)
+        if "probs" in outputs and "points_px" in outputs:
+            probs, pts = outputs["probs"], outputs["points_px"]
+        else:
+            probs = torch.empty_like(logits)
+            pts = torch.empty_like(points)
+            _lib.check(_lib.lib().spe_postprocess(_lib.stream_ptr(stream), _lib.ptr(logits.contiguous()),
+                                                   _lib.ptr(points.contiguous()), _lib.ptr(bb), B, Q,
+                                                   _lib.ptr(probs), _lib.ptr(pts)), "spe_postprocess")
+        probs, pts = probs.cpu().numpy(), pts.cpu().numpy()
+        res = [{"logits": probs[i], "points": pts[i]} for i in range(B)]
+        if "sigmas" in outputs:
+            sg = outputs["sigmas"].cpu().numpy()
+            for i in range(B):
+                res[i]["sigmas"] = sg[i]
+        return res
+
+
+def build_model(args, dtype: str = None):
+    """REV/models/__init__.py:5-6 / detr_speed.py:296-336.  Returns (model, criterion,
+    postprocessors).  The training criterion (Hungarian matcher + losses) is outside the
+    inference hot path and is returned as None (out of scope)."""
+    cfg = SpeConfig.from_args(args)
+    dtype = dtype or getattr(args, "dtype", "bf16")
+    model = DETR(cfg, dtype=dtype, aux_loss=bool(getattr(args, "aux_loss", False)))
+    return model, None, {"points": PostProcess()}

@@ -1,0 +1,62 @@
+"""Whole-batch device pipeline of the evaluate() hot loop (REV/engine.py:91-123 without the
+logging-only criterion): images -> backbone/transformer/heads + fused PostProcess -> batched
+PnP -> SPEED scores, all on one HIP stream with no host round trip.  Optionally captured
+into a HIP graph (torch.cuda.CUDAGraph drives hipStreamBeginCapture on ROCm): spe_forward,
+spe_pnp_batch and spe_speed_score never allocate or synchronise.
+"""
+from __future__ import annotations
+
+import torch
+
+from .models import DETR
+from .solver import PoseSolver
+from .speed_eval import device_speed_score
+
+
+class PosePipeline:
+    def __init__(self, model: DETR, solver: PoseSolver, batch: int, device="cuda", use_graph: bool = False):
+        self.model, self.solver, self.B = model, solver, batch
+        self.device = torch.device(device)
+        S, Q = model.cfg.input_size, model.cfg.num_queries
+        dev = self.device
+        self.images = torch.zeros(batch, 3, S, S, device=dev)
+        self.clip_bbox = torch.zeros(batch, 4, device=dev)
+        self.q_gt = torch.zeros(batch, 4, dtype=torch.float64, device=dev)
+        self.t_gt = torch.zeros(batch, 3, dtype=torch.float64, device=dev)
+        self.q_gt[:, 0] = 1
+        self.t_gt[:, 2] = 10
+        model.workspace(batch, dev)
+        self.use_graph = use_graph
+        self.graph = None
+        self.out = None
+        _ = Q
+
+    def _body(self):
+        fo = self.model(self.images, clip_bbox=self.clip_bbox)
+        sig = fo.get("sigmas")
+        poses = self.solver.solve_batch(fo["points_px"], fo["probs"], sig)
+        s_t, s_q = device_speed_score(poses["quat"], poses["tvec"], self.q_gt, self.t_gt)
+        return {"forward": fo, "poses": poses, "s_t": s_t, "s_q": s_q}
+
+    def load(self, images, clip_bbox, q_gt=None, t_gt=None):
+        self.images.copy_(images, non_blocking=True)
+        self.clip_bbox.copy_(clip_bbox, non_blocking=True)
+        if q_gt is not None:
+            self.q_gt.copy_(q_gt, non_blocking=True)
+            self.t_gt.copy_(t_gt, non_blocking=True)
+
+    def run(self):
+        if not self.use_graph:
+            self.out = self._body()
+            return self.out
+        if self.graph is None:
+            s = torch.cuda.Stream()
+            s.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(s):
+                self._body()                       # warm-up: allocations happen outside capture
+            torch.cuda.current_stream().wait_stream(s)
+            self.graph = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.graph):
+                self.out = self._body()
+        self.graph.replay()
+        return self.out

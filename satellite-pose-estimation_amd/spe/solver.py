@@ -1,0 +1,123 @@
+"""Pose solvers with the reference's interface (REV/utils/speed_eval.py:21-242,
+UNC/utils/speed_eval.py:322-420, UNC/utils/speed_eval_ceres.py:43-169), executed by the
+batched HIP solver kernel (csrc/pnp.hip) through spe_pnp_batch.
+
+    solver = build_solver(args)                 # args.repro (20), args.solver
+    quat, tvec = solver(points, logits)         # one image, numpy, like the reference
+    poses = solver.solve_batch(points_px, probs) # whole batch on device (hot path)
+
+Failures raise exactly what the reference raises so SpeedEval.update maps them to a zero
+pose: IndexError when no foreground label survives, SolverError (the cv2.error stand-in)
+when OpenCV would assert (fewer than 4 correspondences) or leave its output undefined.
+"""
+from __future__ import annotations
+
+import numpy as np
+import torch
+
+from . import _lib
+from .config import Camera, world_points
+
+MODES = {"epnp": _lib.SPE_PNP_EPNP, "ransac_p3p_lm": _lib.SPE_PNP_RANSAC_P3P_LM,
+         "epnp_ransac_sigma": _lib.SPE_PNP_EPNP_RANSAC_SIGMA, "epnp_lm": _lib.SPE_PNP_EPNP_LM}
+
+
+class SolverError(RuntimeError):
+    """Raised where the reference's cv2 call raises cv2.error."""
+
+
+class PoseSolver:
+    """Holds the 11 world landmarks (REV/utils/speed_eval.py:28-39) and camera K."""
+
+    def __init__(self, mode=_lib.SPE_PNP_RANSAC_P3P_LM, repro=20.0, ransac_iters=100, confidence=0.99):
+        self.W_Pt = world_points()
+        self.K = Camera.K.copy()
+        self.mode = mode
+        self.reprojectionError = float(repro)
+        self.ransac_iters = int(ransac_iters)
+        self.confidence = float(confidence)
+        self._dev = {}
+
+    def _consts(self, device):
+        key = str(device)
+        if key not in self._dev:
+            self._dev[key] = (torch.as_tensor(self.K, dtype=torch.float64, device=device).contiguous(),
+                              torch.as_tensor(self.W_Pt, dtype=torch.float64, device=device).contiguous())
+        return self._dev[key]
+
+    def solve_batch(self, points_px, probs, sigmas=None, stream=None, out=None):
+        """points_px [B,Q,2], probs [B,Q,C] (+ sigmas [B,Q,2]) device fp32 -> dict of device
+        tensors quat [B,4] f32, tvec [B,3] f64, rvec, status, n_corr, corr_label [B,16],
+        inlier_mask [B]."""
+        B, Q, C = probs.shape
+        dev = probs.device
+        Kd, Wd = self._consts(dev)
+        if out is None:
+            out = dict(quat=torch.empty(B, 4, device=dev), tvec=torch.empty(B, 3, dtype=torch.float64, device=dev),
+                       rvec=torch.empty(B, 3, dtype=torch.float64, device=dev),
+                       status=torch.empty(B, dtype=torch.int32, device=dev),
+                       n_corr=torch.empty(B, dtype=torch.int32, device=dev),
+                       corr_label=torch.empty(B, 16, dtype=torch.int32, device=dev),
+                       inlier_mask=torch.empty(B, dtype=torch.int32, device=dev))
+        _lib.check(_lib.lib().spe_pnp_batch(
+            _lib.stream_ptr(stream), _lib.ptr(points_px.contiguous()), _lib.ptr(probs.contiguous()),
+            _lib.ptr(sigmas.contiguous() if sigmas is not None else None), B, Q, C, _lib.ptr(Kd), _lib.ptr(Wd),
+            self.mode, self.reprojectionError, self.ransac_iters, self.confidence, _lib.ptr(out["quat"]),
+            _lib.ptr(out["tvec"]), _lib.ptr(out["rvec"]), _lib.ptr(out["status"]), _lib.ptr(out["n_corr"]),
+            _lib.ptr(out["corr_label"]), _lib.ptr(out["inlier_mask"])), "spe_pnp_batch")
+        return out
+
+    def find_index(self, logits):
+        return logits.argmax(1), logits.max(1)
+
+    def __call__(self, points, logits, sigmas=None, device=None):
+        """One image, numpy in / numpy out (REV/utils/speed_eval.py:164-242)."""
+        points = np.asarray(points, dtype=np.float32)
+        logits = np.asarray(logits, dtype=np.float32)
+        assert points.shape[0] == logits.shape[0], "[Solver]: num_queries!"
+        dev = device or torch.device("cuda")
+        p = torch.from_numpy(points[None].copy()).to(dev)
+        l = torch.from_numpy(logits[None].copy()).to(dev)
+        s = torch.from_numpy(np.asarray(sigmas, np.float32)[None].copy()).to(dev) if sigmas is not None else None
+        o = self.solve_batch(p, l, s)
+        st = int(o["status"][0].item())
+        if st == _lib.SPE_PNP_NO_FG:
+            raise IndexError("no foreground keypoint")
+        if st in (_lib.SPE_PNP_CV_ERROR, _lib.SPE_PNP_UNPINNED):
+            raise SolverError(f"solver status {st}")
+        return o["quat"][0].double().cpu().numpy(), o["tvec"][0].cpu().numpy()
+
+
+class SimplePoseSolver(PoseSolver):
+    """cv2.solvePnPRansac(P3P, reprojectionError=args.repro) + solvePnPGeneric(ITERATIVE)
+    (REV/utils/speed_eval.py:143-242)."""
+
+    def __init__(self, args=None):
+        super().__init__(_lib.SPE_PNP_RANSAC_P3P_LM, getattr(args, "repro", 20) if args is not None else 20)
+
+
+class SimplePoseSolverSigma(PoseSolver):
+    """EPnP-RANSAC (reprojection 25) + sigma-weighted Huber LM (UNC/utils/speed_eval.py:322-420)."""
+
+    def __init__(self, args=None):
+        super().__init__(_lib.SPE_PNP_EPNP_RANSAC_SIGMA, 25.0)
+
+
+class EPnPSolver(PoseSolver):
+    """solvePnPGeneric(EPNP) on all selected points (UNC/utils/speed_eval_ceres.py:153-169);
+    BASELINE config 2 ("EPnP only, no RANSAC")."""
+
+    def __init__(self, args=None, refine=False):
+        super().__init__(_lib.SPE_PNP_EPNP_LM if refine else _lib.SPE_PNP_EPNP, 20.0)
+
+
+def build_solver(args=None):
+    """REV/utils/speed_eval.py:21-22 (SimplePoseSolver); `args.solver` selects the variant."""
+    name = getattr(args, "solver", "ransac_p3p_lm") if args is not None else "ransac_p3p_lm"
+    if name == "ransac_p3p_lm":
+        return SimplePoseSolver(args)
+    if name == "epnp_ransac_sigma":
+        return SimplePoseSolverSigma(args)
+    if name in ("epnp", "epnp_lm"):
+        return EPnPSolver(args, refine=name == "epnp_lm")
+    raise ValueError(f"unknown solver {name}")

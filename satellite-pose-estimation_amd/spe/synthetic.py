@@ -1,0 +1,157 @@
+"""Seeded synthetic inputs for the keypoint-set pose path.
+
+* `param_shapes(cfg)`  - the reference's state_dict key space (412 keys for the REV
+  DETR, REV/models/detr_speed.py:32-56, backbone.py:105-131, transformer.py:18-49),
+  plus the optional UNC-style sigma head.
+* `random_weights(cfg, seed)` - deterministic random-init weights in that key space
+  (there is no trained checkpoint in the reference tree), with non-trivial FrozenBN
+  statistics so the BN folding path is exercised.
+* `synthetic_batch(cfg, B, seed)` - SPEED-shaped crops: GT pose, projected landmarks,
+  val-rule clip box (REV/datasets/speed.py:246-260), rendered crop, ImageNet
+  normalisation (REV/datasets/speed.py:25-41).
+Everything is numpy PCG64 so that the same seed yields the same bytes on every box.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .config import SpeConfig, Camera, world_points, project
+
+IMAGENET_MEAN = np.array([0.485, 0.456, 0.406], np.float32)
+IMAGENET_STD = np.array([0.229, 0.224, 0.225], np.float32)
+
+_RESNET50_STAGES = [(64, 3, 1), (128, 4, 2), (256, 6, 2)]   # layer1..3 (layer4 never runs)
+
+
+def _bn_keys(prefix, c):
+    return [(f"{prefix}.{n}", (c,)) for n in ("weight", "bias", "running_mean", "running_var")]
+
+
+def param_shapes(cfg: SpeConfig):
+    """Ordered list of (key, shape) in the reference's state_dict naming."""
+    d, ff, Q = cfg.hidden_dim, cfg.dim_feedforward, cfg.num_queries
+    out = []
+    for i in range(cfg.enc_layers):
+        p = f"transformer.encoder.layers.{i}"
+        out += [(f"{p}.self_attn.in_proj_weight", (3 * d, d)), (f"{p}.self_attn.in_proj_bias", (3 * d,)),
+                (f"{p}.self_attn.out_proj.weight", (d, d)), (f"{p}.self_attn.out_proj.bias", (d,)),
+                (f"{p}.linear1.weight", (ff, d)), (f"{p}.linear1.bias", (ff,)),
+                (f"{p}.linear2.weight", (d, ff)), (f"{p}.linear2.bias", (d,)),
+                (f"{p}.norm1.weight", (d,)), (f"{p}.norm1.bias", (d,)),
+                (f"{p}.norm2.weight", (d,)), (f"{p}.norm2.bias", (d,))]
+    for i in range(cfg.dec_layers):
+        p = f"transformer.decoder.layers.{i}"
+        for a in ("self_attn", "multihead_attn"):
+            out += [(f"{p}.{a}.in_proj_weight", (3 * d, d)), (f"{p}.{a}.in_proj_bias", (3 * d,)),
+                    (f"{p}.{a}.out_proj.weight", (d, d)), (f"{p}.{a}.out_proj.bias", (d,))]
+        out += [(f"{p}.linear1.weight", (ff, d)), (f"{p}.linear1.bias", (ff,)),
+                (f"{p}.linear2.weight", (d, ff)), (f"{p}.linear2.bias", (d,))]
+        for n in ("norm1", "norm2", "norm3"):
+            out += [(f"{p}.{n}.weight", (d,)), (f"{p}.{n}.bias", (d,))]
+    out += [("transformer.decoder.norm.weight", (d,)), ("transformer.decoder.norm.bias", (d,)),
+            ("cls_embed.weight", (cfg.num_classes + 1, d)), ("cls_embed.bias", (cfg.num_classes + 1,))]
+    for j, (o, i) in enumerate([(d, d), (d, d), (2, d)]):
+        out += [(f"point_embed.layers.{j}.weight", (o, i)), (f"point_embed.layers.{j}.bias", (o,))]
+    out += [("query_embed.weight", (Q, d)), ("input_proj.weight", (d, 512, 1, 1)), ("input_proj.bias", (d,))]
+    b = "backbone.0.body"
+    out += [(f"{b}.conv1.weight", (64, 3, 7, 7))] + _bn_keys(f"{b}.bn1", 64)
+    cin = 64
+    for li, (w, n, s) in enumerate(_RESNET50_STAGES, start=1):
+        for k in range(n):
+            p = f"{b}.layer{li}.{k}"
+            out += [(f"{p}.conv1.weight", (w, cin, 1, 1))] + _bn_keys(f"{p}.bn1", w)
+            out += [(f"{p}.conv2.weight", (w, w, 3, 3))] + _bn_keys(f"{p}.bn2", w)
+            out += [(f"{p}.conv3.weight", (4 * w, w, 1, 1))] + _bn_keys(f"{p}.bn3", 4 * w)
+            if k == 0:
+                out += [(f"{p}.downsample.0.weight", (4 * w, cin, 1, 1))] + _bn_keys(f"{p}.downsample.1", 4 * w)
+            cin = 4 * w
+    out += [("backbone.0.s8_latern.weight", (256, 512, 1, 1)),
+            ("backbone.0.s16_latern.weight", (256, 1024, 3, 3)),
+            ("backbone.0.output_conv.weight", (512, 512, 3, 3)),
+            ("backbone.0.output_conv.bias", (512,))]
+    if cfg.sigma_head:
+        for j, (o, i) in enumerate([(d, d), (d, d), (1, d)]):
+            out += [(f"sigma_embed.layers.{j}.weight", (o, i)), (f"sigma_embed.layers.{j}.bias", (o,))]
+    return out
+
+
+def random_weights(cfg: SpeConfig, seed: int = 0):
+    """Deterministic random-init weights (dict key -> float32 ndarray).
+
+    Conv weights are He-normal, linear/attention weights Xavier-uniform (the reference's
+    `_reset_parameters`, REV/models/transformer.py:45-48), FrozenBN stats non-trivial and
+    the residual-branch gain (bn3 weight) damped so activations stay O(1) through 13
+    bottlenecks without batch statistics."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    w = {}
+    for key, shape in param_shapes(cfg):
+        if key.endswith("running_mean"):
+            a = rng.normal(0.0, 0.1, shape)
+        elif key.endswith("running_var"):
+            a = rng.uniform(0.5, 1.5, shape)
+        elif len(shape) == 4:
+            fan_in = shape[1] * shape[2] * shape[3]
+            a = rng.normal(0.0, np.sqrt(2.0 / fan_in), shape)
+        elif len(shape) == 2:
+            lim = np.sqrt(6.0 / (shape[0] + shape[1]))
+            a = rng.uniform(-lim, lim, shape)
+            if key == "query_embed.weight":
+                a = rng.normal(0.0, 1.0, shape)
+        else:  # 1-D: BN/LN affine or bias
+            if ".bn" in key or "downsample.1" in key:
+                if key.endswith("weight"):
+                    gain = 0.25 if (".bn3" in key) else 1.0
+                    a = gain * rng.uniform(0.5, 1.0, shape)
+                else:
+                    a = rng.normal(0.0, 0.05, shape)
+            elif "norm" in key and key.endswith("weight"):
+                a = 1.0 + rng.normal(0.0, 0.1, shape)
+            else:
+                a = rng.normal(0.0, 0.02, shape)
+        w[key] = np.ascontiguousarray(a, dtype=np.float32)
+    return w
+
+
+def random_pose(rng, n):
+    q = rng.normal(0.0, 1.0, (n, 4))
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    z = rng.uniform(3.0, 30.0, n)
+    t = np.stack([rng.normal(0.0, 0.3, n), rng.normal(0.0, 0.3, n), z], axis=1)
+    return q, t
+
+
+def clip_bbox_val(bbox, image_size=(Camera.nu, Camera.nv)):
+    """1.2x max-side square around the landmark box, clipped to the image
+    (REV/datasets/speed.py:246-260)."""
+    x1, y1, x2, y2 = bbox
+    scale = max(x2 - x1, y2 - y1) * 1.2
+    xc, yc, h = (x1 + x2) / 2, (y1 + y2) / 2, scale / 2
+    c = np.asarray([xc - h, yc - h, xc + h, yc + h], dtype=np.float64)
+    c[0::2] = c[0::2].clip(0, image_size[0])
+    c[1::2] = c[1::2].clip(0, image_size[1])
+    return c
+
+
+def synthetic_batch(cfg: SpeConfig, B: int, seed: int = 0, dtype=np.float32):
+    """B synthetic SPEED crops. Returns dict with images [B,3,S,S] (ImageNet-normalised),
+    quat [B,4], tvec [B,3], landmarks [B,11,2] (image px), clip_bbox [B,4]."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    S = cfg.input_size
+    W = world_points()
+    q, t = random_pose(rng, B)
+    lm = np.stack([project(W, q[i], t[i]) for i in range(B)])
+    boxes = np.stack([clip_bbox_val([l[:, 0].min(), l[:, 1].min(), l[:, 0].max(), l[:, 1].max()]) for l in lm])
+    ys, xs = np.meshgrid(np.arange(S, dtype=np.float32) + 0.5, np.arange(S, dtype=np.float32) + 0.5, indexing="ij")
+    imgs = np.empty((B, 3, S, S), dtype=np.float32)
+    for i in range(B):
+        x1, y1, x2, y2 = boxes[i]
+        sx, sy = S / max(x2 - x1, 1e-3), S / max(y2 - y1, 1e-3)
+        g = rng.normal(30.0, 10.0, (S, S)).astype(np.float32)
+        sig = max(4.0 * sx, 1.5)
+        for (u, v) in lm[i]:
+            cx, cy = (u - x1) * sx, (v - y1) * sy
+            g += 200.0 * np.exp(-((xs - cx) ** 2 + (ys - cy) ** 2) / (2 * sig * sig))
+        g = np.clip(np.round(g), 0, 255) / 255.0
+        for c in range(3):
+            imgs[i, c] = (g - IMAGENET_MEAN[c]) / IMAGENET_STD[c]
+    return {"images": imgs.astype(dtype), "quat": q, "tvec": t, "landmarks": lm, "clip_bbox": boxes}

@@ -1,0 +1,69 @@
+"""CPU: libspe.so loads, exports every symbol include/spe.h declares, and the host-side
+parameter registry speaks the reference's state_dict key space (no GPU compute here)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+from spe import _lib
+from spe.config import SpeConfig
+from spe.synthetic import param_shapes
+
+
+def _header_symbols():
+    src = open(os.path.join(REPO, "include", "spe.h")).read()
+    return sorted(set(re.findall(r"^\w[\w\s\*]*?\b(spe_\w+)\s*\(", src, re.M)))
+
+
+def test_exports_every_declared_symbol():
+    L = _lib.lib()
+    declared = _header_symbols()
+    assert set(declared) == set(_lib.EXPORTS)
+    for name in declared:
+        assert hasattr(L, name), name
+    assert L.spe_abi_version() == 1
+
+
+def _create(cfg, dtype=_lib.SPE_DTYPE_BF16):
+    L = _lib.lib()
+    c = _lib.ModelConfig(cfg.input_size, cfg.num_queries, cfg.enc_layers, cfg.dec_layers, cfg.hidden_dim,
+                         cfg.nheads, cfg.dim_feedforward, int(cfg.sigma_head), dtype)
+    h = ctypes.c_void_p()
+    rc = L.spe_model_create(ctypes.byref(c), ctypes.byref(h))
+    return rc, h
+
+
+@pytest.mark.parametrize("cfg", [SpeConfig(), SpeConfig(input_size=640, num_queries=40),
+                                 SpeConfig(sigma_head=True), SpeConfig(enc_layers=4, dec_layers=4)])
+def test_param_registry_matches_reference_keys(cfg):
+    L = _lib.lib()
+    rc, h = _create(cfg)
+    assert rc == 0
+    names = [L.spe_model_param_name(h, i).decode() for i in range(L.spe_model_num_params(h))]
+    assert names == [k for k, _ in param_shapes(cfg)]
+    if not cfg.sigma_head and cfg.enc_layers == 6 and cfg.dec_layers == 6:
+        assert len(names) == 412          # the reference's REV DETR state_dict
+    assert L.spe_model_workspace_bytes(h, 8) > 0
+    L.spe_model_destroy(h)
+
+
+def test_param_errors():
+    L = _lib.lib()
+    rc, h = _create(SpeConfig())
+    a = np.zeros(10, np.float32)
+    assert L.spe_model_set_param(h, b"no.such.key", a.ctypes.data_as(ctypes.c_void_p), 10) == -4
+    assert L.spe_model_set_param(h, b"cls_embed.bias", a.ctypes.data_as(ctypes.c_void_p), 10) == -4
+    b = np.zeros(12, np.float32)
+    assert L.spe_model_set_param(h, b"cls_embed.bias", b.ctypes.data_as(ctypes.c_void_p), 12) == 0
+    assert L.spe_model_finalize(h) == -3                     # missing parameters
+    assert b"missing parameter" in L.spe_last_error()
+    L.spe_model_destroy(h)
+
+
+def test_bad_configs_rejected():
+    assert _create(SpeConfig(hidden_dim=128, nheads=4))[0] == -1
+    assert _create(SpeConfig(input_size=420))[0] == -1
+    assert _create(SpeConfig(num_queries=100))[0] == -1

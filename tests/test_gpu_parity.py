@@ -1,0 +1,145 @@
+"""GPU parity: the HIP path (through libspe.so's C ABI) against the reference's golden outputs
+and the CPU oracles, on seeded inputs.
+
+Tolerances (written here on purpose):
+  fp32 parity mode   pred_points |d| <= 1e-4 (crop-normalised; BASELINE.json keypoint
+                     tolerance), pred_logits |d| <= 2e-3 abs, PostProcess px <= 0.05 px
+  bf16 throughput    pred_points |d| <= 2e-2, logits |d| <= 0.25 (bf16 storage, 8-bit mantissa)
+  solver             status / n_corr / corr_label / inlier masks bit-exact vs oracle/pnp_ref.c,
+                     pose |dq| <= 1e-5, |dt|/|t| <= 1e-6 (both fp64, rounding only)
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN
+from helpers import solver_stress_set
+from spe.config import SpeConfig, Camera, world_points
+from spe.synthetic import random_weights, synthetic_batch
+
+pytestmark = pytest.mark.gpu
+
+_models = {}
+
+
+def _model(cfg, dtype, wseed):
+    from spe.models import DETR
+    key = (cfg, dtype, wseed)
+    if key not in _models:
+        m = DETR(cfg, dtype=dtype)
+        m.load_state_dict(random_weights(cfg, wseed))
+        _models[key] = m
+    return _models[key]
+
+
+def _golden(tag):
+    g = np.load(os.path.join(GOLDEN, f"model_{tag}.npz"))
+    cfg = SpeConfig(**json.loads(str(g["config"])))
+    return g, cfg
+
+
+@pytest.mark.parametrize("tag", ["s128_q11_l2", "s224_q30_l4", "s416_q11_l6"])
+def test_forward_fp32_matches_reference(gpu_device, tag):
+    g, cfg = _golden(tag)
+    b = synthetic_batch(cfg, int(g["batch"]), int(g["image_seed"]))
+    m = _model(cfg, "fp32", int(g["weight_seed"]))
+    img = torch.from_numpy(b["images"]).to(gpu_device)
+    clip = torch.from_numpy(b["clip_bbox"]).float().to(gpu_device)
+    o = m(img, clip_bbox=clip)
+    torch.cuda.synchronize()
+    pts = o["pred_points"].cpu().numpy()
+    lg = o["pred_logits"].cpu().numpy()
+    assert np.abs(pts - g["pred_points"]).max() <= 1e-4
+    assert np.abs(lg - g["pred_logits"]).max() <= 2e-3
+    assert np.abs(o["points_px"].cpu().numpy() - g["pp_points"]).max() <= 0.05
+    assert np.abs(o["probs"].cpu().numpy() - g["pp_probs"]).max() <= 1e-3
+
+
+@pytest.mark.parametrize("tag", ["s128_q11_l2", "s416_q11_l6"])
+def test_forward_bf16_close_to_reference(gpu_device, tag):
+    g, cfg = _golden(tag)
+    b = synthetic_batch(cfg, int(g["batch"]), int(g["image_seed"]))
+    m = _model(cfg, "bf16", int(g["weight_seed"]))
+    o = m(torch.from_numpy(b["images"]).to(gpu_device))
+    torch.cuda.synchronize()
+    assert np.isfinite(o["pred_points"].cpu().numpy()).all()
+    assert np.abs(o["pred_points"].cpu().numpy() - g["pred_points"]).max() <= 2e-2
+    assert np.abs(o["pred_logits"].cpu().numpy() - g["pred_logits"]).max() <= 0.25
+
+
+def test_forward_batch_independence(gpu_device):
+    """Each image's outputs do not depend on the other images in the batch (sharding property)."""
+    cfg = SpeConfig(input_size=128, num_queries=11, enc_layers=2, dec_layers=2)
+    m = _model(cfg, "fp32", 7)
+    b = synthetic_batch(cfg, 5, 123)
+    img = torch.from_numpy(b["images"]).to(gpu_device)
+    full = m(img)["pred_points"].cpu().numpy()
+    part = m(img[2:4].contiguous())["pred_points"].cpu().numpy()
+    np.testing.assert_array_equal(full[2:4], part)
+
+
+def _solve(mode, pts, probs, sig, repro=20.0):
+    from spe.solver import PoseSolver
+    s = PoseSolver(mode=mode, repro=repro)
+    dev = torch.device("cuda:0")
+    o = s.solve_batch(torch.from_numpy(pts).to(dev), torch.from_numpy(probs).to(dev),
+                      torch.from_numpy(sig).to(dev) if sig is not None else None)
+    torch.cuda.synchronize()
+    return {k: v.cpu().numpy() for k, v in o.items()}
+
+
+@pytest.mark.parametrize("mode", [0, 1, 2, 3])
+def test_solver_matches_oracle(gpu_device, mode):
+    import pnp_ref
+    pts, probs, q, t, sig = solver_stress_set(256, seed=10 + mode)
+    sig_in = sig if mode == 2 else None
+    repro = 25.0 if mode == 2 else 20.0
+    h = _solve(mode, pts, probs, sig_in, repro)
+    o = pnp_ref.pnp_batch(pts, probs, Camera.K, world_points(), mode=mode, repro=repro, sigmas=sig_in)
+    np.testing.assert_array_equal(h["status"], o["status"])
+    np.testing.assert_array_equal(h["n_corr"], o["n_corr"])
+    np.testing.assert_array_equal(h["corr_label"], o["corr_label"])
+    np.testing.assert_array_equal(h["inlier_mask"].astype(np.uint32), o["inlier_mask"])
+    ok = (o["status"] == 0) | (o["status"] == 3)
+    assert ok.sum() > 200
+    dq = np.abs(np.abs((h["quat"].astype(np.float64) * o["quat"]).sum(1)) - 1)
+    assert dq[ok].max() <= 1e-5
+    dt = np.linalg.norm(h["tvec"] - o["tvec"], axis=1) / np.maximum(np.linalg.norm(o["tvec"], axis=1), 1e-9)
+    assert dt[ok].max() <= 1e-6
+    assert np.all(h["quat"][~ok] == 0) and np.all(h["tvec"][~ok] == 0)
+
+
+def test_solver_known_answer(gpu_device):
+    with open(os.path.join(GOLDEN, "pnp_kat_wz_real.json")) as f:
+        kat = json.load(f)["images"]
+    import pnp_ref
+    pts = np.stack([np.asarray(im["landmarks"], np.float32) for im in kat])
+    probs = np.full((len(kat), 11, 12), 0.01, np.float32)
+    probs[:, np.arange(11), np.arange(11)] = 0.89
+    for mode in (0, 1, 3):
+        h = _solve(mode, pts, probs, None)
+        for i, im in enumerate(kat):
+            s_t, s_q = pnp_ref.speed_score(h["quat"][i], h["tvec"][i], im["q_vbs2tango"], im["r_Vo2To_vbs_true"])
+            assert h["status"][i] == 0 and s_t < 2e-6 and s_q < 2e-3
+
+
+def test_speed_score_kernel(gpu_device):
+    import pnp_ref
+    from spe.speed_eval import device_speed_score
+    rng = np.random.default_rng(5)
+    B = 64
+    q = rng.normal(size=(B, 4)).astype(np.float32)
+    q[:8] = 0
+    t = rng.normal(size=(B, 3))
+    t[:8] = 0
+    qg = rng.normal(size=(B, 4)); qg /= np.linalg.norm(qg, axis=1, keepdims=True)
+    tg = rng.normal(size=(B, 3)) + [0, 0, 10]
+    d = gpu_device
+    s_t, s_q = device_speed_score(torch.from_numpy(q).to(d), torch.from_numpy(t).to(d), torch.from_numpy(qg).to(d),
+                                  torch.from_numpy(tg).to(d))
+    for i in range(B):
+        a, b = pnp_ref.speed_score(q[i].astype(np.float64), t[i], qg[i], tg[i])
+        assert abs(s_t[i].item() - a) < 1e-12 and abs(s_q[i].item() - b) < 1e-9
