@@ -36,6 +36,9 @@ def parse():
     p.add_argument("--layers", type=int, default=6)
     p.add_argument("--solver", default="epnp", choices=["epnp", "epnp_lm", "ransac_p3p_lm", "epnp_ransac_sigma"])
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--weights", default="label-diverse", choices=["label-diverse", "random"],
+                   help="label-diverse: random init made query-diverse so the solver sees >= 4 "
+                        "correspondences like a trained model (spe.synthetic.bench_weights)")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     return p.parse_args()
@@ -91,7 +94,8 @@ def main():
     from spe.models import DETR
     from spe.pipeline import PosePipeline
     from spe.solver import build_solver
-    from spe.synthetic import random_weights, synthetic_batch
+    import numpy as np
+    from spe.synthetic import bench_weights, random_weights, synthetic_batch
     from spe import _lib
 
     rank, world, local = sd.init_distributed_mode()
@@ -99,8 +103,19 @@ def main():
     dev = torch.device("cuda", local)
     cfg = SpeConfig(input_size=args.size, num_queries=args.queries, enc_layers=args.layers, dec_layers=args.layers)
     B = args.batch
+
+    def hs_fn(w, images):
+        # calibration pass of the HIP model itself (see spe.synthetic.bench_weights)
+        m = DETR(cfg, dtype=args.dtype)
+        m.load_state_dict(w)
+        out = []
+        for i in range(0, len(images), 8):
+            out.append(m(torch.from_numpy(images[i:i + 8]).to(dev), return_hs=True)["hs"].cpu().numpy())
+        del m
+        return np.concatenate(out)
+
     model = DETR(cfg, dtype=args.dtype)
-    model.load_state_dict(random_weights(cfg, 0))
+    model.load_state_dict(bench_weights(cfg, 0, hs_fn) if args.weights == "label-diverse" else random_weights(cfg, 0))
     solver = build_solver(argparse.Namespace(solver=args.solver, repro=20))
     pipe = PosePipeline(model, solver, B, device=dev)
     data = synthetic_batch(cfg, B, seed=1000 + rank)
@@ -189,7 +204,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.dtype,
-        "data": "synthetic (seeded SPEED-shaped crops, random-init weights; no checkpoint in the reference)",
+        "data": f"synthetic (seeded SPEED-shaped crops; {args.weights} random-init weights, "
+                "no checkpoint exists in the reference)",
         "config": {"workload": f"BASELINE config 2: ResNet50-s8 + {args.layers}/{args.layers} DETR, "
                                f"{args.queries} queries, {args.size}x{args.size}, solver={args.solver}",
                    "global_batch": B * world, "per_gpu_batch": B, "input_size": args.size,

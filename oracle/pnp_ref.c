@@ -43,6 +43,89 @@ static unsigned rng_next(rng_t* r) {
 }
 static int rng_uniform(rng_t* r, int a, int b) { return a == b ? a : (int)(rng_next(r) % (unsigned)(b - a) + a); }
 
+/* ------------------------------------------------------------------ deterministic math
+ * The inlier decisions and the RANSAC iteration count are index outputs that must agree bit for
+ * bit between this checker and the device solver.  libm (glibc) and the GPU's device library
+ * round transcendental functions differently in the last ulp, so every transcendental on the
+ * decision path is evaluated here with a fixed sequence of IEEE add/mul/div/sqrt (and the file
+ * is compiled with -ffp-contract=off on both sides).  Accuracy is ~1 ulp; OpenCV itself uses
+ * libm, so agreement with OpenCV stays at rounding level (unpinned there anyway). */
+static double det_rint(double x) { return rint(x); } /* exact IEEE operation */
+
+static void det_sincos(double x, double* s_out, double* c_out) {
+  const double INV_PIO2 = 6.36619772367581382433e-01;
+  const double PIO2_1 = 1.57079632673412561417e+00, PIO2_1T = 6.07710050650619224932e-11;
+  double k = det_rint(x * INV_PIO2);
+  double r = (x - k * PIO2_1) - k * PIO2_1T;
+  double z = r * r;
+  /* Taylor coefficients (-1)^n / (2n+1)!  and  (-1)^n / (2n)!, Horner in z = r^2 */
+  const double SC[10] = {1.0, -1.0 / 6.0, 1.0 / 120.0, -1.0 / 5040.0, 1.0 / 362880.0, -1.0 / 39916800.0,
+                                1.0 / 6227020800.0, -1.0 / 1307674368000.0, 1.0 / 355687428096000.0,
+                                -1.0 / 121645100408832000.0};
+  const double CC[10] = {1.0, -1.0 / 2.0, 1.0 / 24.0, -1.0 / 720.0, 1.0 / 40320.0, -1.0 / 3628800.0,
+                                1.0 / 479001600.0, -1.0 / 87178291200.0, 1.0 / 20922789888000.0,
+                                -1.0 / 6402373705728000.0};
+  double s = SC[9], c = CC[9];
+  for (int i = 8; i >= 0; --i) { s = s * z + SC[i]; c = c * z + CC[i]; }
+  s *= r;
+  long q = ((long)k) & 3;
+  if (q == 0) { *s_out = s; *c_out = c; }
+  else if (q == 1) { *s_out = c; *c_out = -s; }
+  else if (q == 2) { *s_out = -s; *c_out = -c; }
+  else { *s_out = -c; *c_out = s; }
+}
+static double det_sin(double x) { double s, c; det_sincos(x, &s, &c); return s; }
+static double det_cos(double x) { double s, c; det_sincos(x, &s, &c); return c; }
+
+/* asin for |y| <= 0.5 by its Taylor series (terms decrease faster than 4^-n) */
+static double det_asin_small(double y) {
+  double y2 = y * y, term = y, sum = y;
+  for (int n = 1; n < 30; ++n) {
+    term = term * y2 * ((2.0 * n - 1.0) * (2.0 * n - 1.0)) / ((2.0 * n) * (2.0 * n + 1.0));
+    sum += term;
+  }
+  return sum;
+}
+
+static double det_acos(double x) {
+  const double PI = 3.14159265358979311600e+00, PIO2 = 1.57079632679489655800e+00;
+  if (x >= 1.0) return 0.0;
+  if (x <= -1.0) return PI;
+  if (x <= 0.5 && x >= -0.5) return PIO2 - det_asin_small(x);
+  if (x > 0.5) return 2.0 * det_asin_small(sqrt((1.0 - x) * 0.5));
+  return PI - 2.0 * det_asin_small(sqrt((1.0 + x) * 0.5));
+}
+
+static double det_cbrt(double x) {
+  if (x == 0.0) return 0.0;
+  double a = fabs(x);
+  int e;
+  double m = frexp(a, &e); /* a = m 2^e, m in [0.5, 1) */
+  int r = ((e % 3) + 3) % 3;
+  m = ldexp(m, r);         /* m in [0.5, 4) */
+  e -= r;
+  double y = 0.75 + 0.25 * m;
+  for (int i = 0; i < 10; ++i) y = y - (y * y * y - m) / (3.0 * y * y);
+  y = ldexp(y, e / 3);
+  return x < 0 ? -y : y;
+}
+
+static double det_log(double x) { /* x > 0 */
+  const double LN2_HI = 6.93147180369123816490e-01, LN2_LO = 1.90821492927058770002e-10;
+  int e;
+  double m = frexp(x, &e);
+  if (m < 7.07106781186547524401e-01) { m *= 2.0; e -= 1; }
+  double s = (m - 1.0) / (m + 1.0), s2 = s * s, term = s, sum = s;
+  for (int n = 1; n < 14; ++n) { term *= s2; sum += term / (2.0 * n + 1.0); }
+  return (double)e * LN2_HI + ((double)e * LN2_LO + 2.0 * sum);
+}
+
+static double det_pow10i(int k) {
+  double v = 1.0;
+  for (int i = 0; i < (k > 0 ? k : -k); ++i) v *= 10.0;
+  return k >= 0 ? v : 1.0 / v;
+}
+
 /* ------------------------------------------------------------------ small linear algebra */
 /* cyclic Jacobi eigen-decomposition of a symmetric n x n matrix (row-major, destroyed).
  * evec[i*n + k] = component i of eigenvector k.  Eigenvalues returned unsorted. */
@@ -200,7 +283,9 @@ static void rodrigues_r2R(const double* r, double* R) {
     for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0);
     return;
   }
-  double c = cos(th), s = sin(th), c1 = 1. - c, it = 1. / th;
+  double c, s;
+  det_sincos(th, &s, &c);
+  double c1 = 1. - c, it = 1. / th;
   double x = r[0] * it, y = r[1] * it, z = r[2] * it;
   double rrt[9] = {x * x, x * y, x * z, x * y, y * y, y * z, x * z, y * z, z * z};
   double rx[9] = {0, -z, y, z, 0, -x, -y, x, 0};
@@ -215,7 +300,9 @@ static void rodrigues_jac(const double* r, double* J) {
     memcpy(J, J0, sizeof J0);
     return;
   }
-  double c = cos(th), s = sin(th), c1 = 1. - c, it = 1. / th;
+  double c, s;
+  det_sincos(th, &s, &c);
+  double c1 = 1. - c, it = 1. / th;
   double x = r[0] * it, y = r[1] * it, z = r[2] * it;
   double rrt[9] = {x * x, x * y, x * z, x * y, y * y, y * z, x * z, y * z, z * z};
   double rx[9] = {0, -z, y, z, 0, -x, -y, x, 0};
@@ -234,7 +321,7 @@ static void rodrigues_R2r(const double* R, double* r) {
   double s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
   double c = (R[0] + R[4] + R[8] - 1) * 0.5;
   c = c > 1. ? 1. : (c < -1. ? -1. : c);
-  double theta = acos(c);
+  double theta = det_acos(c);
   if (s < 1e-5) {
     if (c > 0) {
       r[0] = r[1] = r[2] = 0;
@@ -299,17 +386,17 @@ static int solve_deg3(double a, double b, double c, double d, double* x0, double
   double Q3 = Q * Q * Q, D = Q3 + R * R, b_a_3 = (1. / 3.) * b_a;
   if (Q == 0) {
     if (R == 0) { *x0 = *x1 = *x2 = -b_a_3; return 3; }
-    *x0 = pow(2 * R, 1 / 3.0) - b_a_3;
+    *x0 = (2 * R >= 0 ? det_cbrt(2 * R) : NAN) - b_a_3; /* pow(<0, 1/3.) is NaN in OpenCV's code */
     return 1;
   }
   if (D <= 0) {
-    double theta = acos(R / sqrt(-Q3)), sq = sqrt(-Q);
-    *x0 = 2 * sq * cos(theta / 3.0) - b_a_3;
-    *x1 = 2 * sq * cos((theta + 2 * M_PI) / 3.0) - b_a_3;
-    *x2 = 2 * sq * cos((theta + 4 * M_PI) / 3.0) - b_a_3;
+    double theta = det_acos(R / sqrt(-Q3)), sq = sqrt(-Q);
+    *x0 = 2 * sq * det_cos(theta / 3.0) - b_a_3;
+    *x1 = 2 * sq * det_cos((theta + 2 * M_PI) / 3.0) - b_a_3;
+    *x2 = 2 * sq * det_cos((theta + 4 * M_PI) / 3.0) - b_a_3;
     return 3;
   }
-  double AD = pow(fabs(R) + sqrt(D), 1.0 / 3.0) * (R > 0 ? 1 : (R < 0 ? -1 : 0));
+  double AD = det_cbrt(fabs(R) + sqrt(D)) * (R > 0 ? 1 : (R < 0 ? -1 : 0));
   double BD = (AD == 0) ? 0 : -Q / AD;
   *x0 = AD + BD - b_a_3;
   return 1;
@@ -835,7 +922,7 @@ static void lm_refine(const cam_t* k, int n, const double* wld, const double* im
     }
     double errNorm;
     for (;;) { /* step + CHECK_ERR, retrying with larger lambda */
-      double lambda = exp(lambdaLg10 * log(10.));
+      double lambda = det_pow10i(lambdaLg10);
       double S[36], dx[6];
       memcpy(S, JtJ, sizeof S);
       for (int i = 0; i < 6; ++i) S[i * 6 + i] *= 1. + lambda;
@@ -923,11 +1010,13 @@ static double ransac_update(double p, double ep, int mp, int maxIters) {
   p = p > 0 ? p : 0; p = p < 1 ? p : 1;
   ep = ep > 0 ? ep : 0; ep = ep < 1 ? ep : 1;
   double num = 1. - p > DBL_MIN ? 1. - p : DBL_MIN;
-  double denom = 1. - pow(1. - ep, mp);
+  double pw = 1.0;
+  for (int i = 0; i < mp; ++i) pw *= 1. - ep;
+  double denom = 1. - pw;
   if (denom < DBL_MIN) return 0;
-  num = log(num);
-  denom = log(denom);
-  return (denom >= 0 || -num >= maxIters * (-denom)) ? maxIters : (int)lrint(num / denom);
+  num = det_log(num);
+  denom = det_log(denom);
+  return (denom >= 0 || -num >= maxIters * (-denom)) ? maxIters : (int)det_rint(num / denom);
 }
 
 /* kernel: 0 = P3P (4-point samples), 1 = EPnP (5-point samples).  Returns 1 on consensus.

@@ -1,7 +1,9 @@
-// Device-side restatement of the pose-solver arithmetic (OpenCV 4.4 p3p / epnp / RANSAC /
-// LevMarq, Blender mat3_to_quat) used by pnp.hip.  Same published algorithms as the CPU
-// checker in oracle/pnp_ref.c (kept as a separate copy: the product never links the oracle).
-// Every function is executed by one lane; pnp.hip supplies the wave-level parallelism.
+// Device-side pose-solver arithmetic (OpenCV 4.4 p3p / epnp / LevMarq restated, Blender
+// mat3_to_quat, deterministic transcendental helpers) used by pnp.hip.  Same published
+// algorithms and the same IEEE operation sequence as the CPU checker oracle/pnp_ref.c (a
+// separate copy: the product never links the oracle); both are compiled with
+// -ffp-contract=off so integer / index outputs (inlier sets, iteration counts) agree bit for bit.
+// Every function here runs on one lane; pnp.hip provides the wave-level parallelism.
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -16,6 +18,89 @@ PNP_FN unsigned rng_next(rng_t* r) {
   return (unsigned)r->state;
 }
 PNP_FN int rng_uniform(rng_t* r, int a, int b) { return a == b ? a : (int)(rng_next(r) % (unsigned)(b - a) + a); }
+
+/* ------------------------------------------------------------------ deterministic math
+ * The inlier decisions and the RANSAC iteration count are index outputs that must agree bit for
+ * bit between this checker and the device solver.  libm (glibc) and the GPU's device library
+ * round transcendental functions differently in the last ulp, so every transcendental on the
+ * decision path is evaluated here with a fixed sequence of IEEE add/mul/div/sqrt (and the file
+ * is compiled with -ffp-contract=off on both sides).  Accuracy is ~1 ulp; OpenCV itself uses
+ * libm, so agreement with OpenCV stays at rounding level (unpinned there anyway). */
+PNP_FN double det_rint(double x) { return rint(x); } /* exact IEEE operation */
+
+PNP_FN void det_sincos(double x, double* s_out, double* c_out) {
+  const double INV_PIO2 = 6.36619772367581382433e-01;
+  const double PIO2_1 = 1.57079632673412561417e+00, PIO2_1T = 6.07710050650619224932e-11;
+  double k = det_rint(x * INV_PIO2);
+  double r = (x - k * PIO2_1) - k * PIO2_1T;
+  double z = r * r;
+  /* Taylor coefficients (-1)^n / (2n+1)!  and  (-1)^n / (2n)!, Horner in z = r^2 */
+  const double SC[10] = {1.0, -1.0 / 6.0, 1.0 / 120.0, -1.0 / 5040.0, 1.0 / 362880.0, -1.0 / 39916800.0,
+                                1.0 / 6227020800.0, -1.0 / 1307674368000.0, 1.0 / 355687428096000.0,
+                                -1.0 / 121645100408832000.0};
+  const double CC[10] = {1.0, -1.0 / 2.0, 1.0 / 24.0, -1.0 / 720.0, 1.0 / 40320.0, -1.0 / 3628800.0,
+                                1.0 / 479001600.0, -1.0 / 87178291200.0, 1.0 / 20922789888000.0,
+                                -1.0 / 6402373705728000.0};
+  double s = SC[9], c = CC[9];
+  for (int i = 8; i >= 0; --i) { s = s * z + SC[i]; c = c * z + CC[i]; }
+  s *= r;
+  long q = ((long)k) & 3;
+  if (q == 0) { *s_out = s; *c_out = c; }
+  else if (q == 1) { *s_out = c; *c_out = -s; }
+  else if (q == 2) { *s_out = -s; *c_out = -c; }
+  else { *s_out = -c; *c_out = s; }
+}
+PNP_FN double det_sin(double x) { double s, c; det_sincos(x, &s, &c); return s; }
+PNP_FN double det_cos(double x) { double s, c; det_sincos(x, &s, &c); return c; }
+
+/* asin for |y| <= 0.5 by its Taylor series (terms decrease faster than 4^-n) */
+PNP_FN double det_asin_small(double y) {
+  double y2 = y * y, term = y, sum = y;
+  for (int n = 1; n < 30; ++n) {
+    term = term * y2 * ((2.0 * n - 1.0) * (2.0 * n - 1.0)) / ((2.0 * n) * (2.0 * n + 1.0));
+    sum += term;
+  }
+  return sum;
+}
+
+PNP_FN double det_acos(double x) {
+  const double PI = 3.14159265358979311600e+00, PIO2 = 1.57079632679489655800e+00;
+  if (x >= 1.0) return 0.0;
+  if (x <= -1.0) return PI;
+  if (x <= 0.5 && x >= -0.5) return PIO2 - det_asin_small(x);
+  if (x > 0.5) return 2.0 * det_asin_small(sqrt((1.0 - x) * 0.5));
+  return PI - 2.0 * det_asin_small(sqrt((1.0 + x) * 0.5));
+}
+
+PNP_FN double det_cbrt(double x) {
+  if (x == 0.0) return 0.0;
+  double a = fabs(x);
+  int e;
+  double m = frexp(a, &e); /* a = m 2^e, m in [0.5, 1) */
+  int r = ((e % 3) + 3) % 3;
+  m = ldexp(m, r);         /* m in [0.5, 4) */
+  e -= r;
+  double y = 0.75 + 0.25 * m;
+  for (int i = 0; i < 10; ++i) y = y - (y * y * y - m) / (3.0 * y * y);
+  y = ldexp(y, e / 3);
+  return x < 0 ? -y : y;
+}
+
+PNP_FN double det_log(double x) { /* x > 0 */
+  const double LN2_HI = 6.93147180369123816490e-01, LN2_LO = 1.90821492927058770002e-10;
+  int e;
+  double m = frexp(x, &e);
+  if (m < 7.07106781186547524401e-01) { m *= 2.0; e -= 1; }
+  double s = (m - 1.0) / (m + 1.0), s2 = s * s, term = s, sum = s;
+  for (int n = 1; n < 14; ++n) { term *= s2; sum += term / (2.0 * n + 1.0); }
+  return (double)e * LN2_HI + ((double)e * LN2_LO + 2.0 * sum);
+}
+
+PNP_FN double det_pow10i(int k) {
+  double v = 1.0;
+  for (int i = 0; i < (k > 0 ? k : -k); ++i) v *= 10.0;
+  return k >= 0 ? v : 1.0 / v;
+}
 
 /* ------------------------------------------------------------------ small linear algebra */
 /* cyclic Jacobi eigen-decomposition of a symmetric n x n matrix (row-major, destroyed).
@@ -174,7 +259,9 @@ PNP_FN void rodrigues_r2R(const double* r, double* R) {
     for (int i = 0; i < 9; ++i) R[i] = (i % 4 == 0);
     return;
   }
-  double c = cos(th), s = sin(th), c1 = 1. - c, it = 1. / th;
+  double c, s;
+  det_sincos(th, &s, &c);
+  double c1 = 1. - c, it = 1. / th;
   double x = r[0] * it, y = r[1] * it, z = r[2] * it;
   double rrt[9] = {x * x, x * y, x * z, x * y, y * y, y * z, x * z, y * z, z * z};
   double rx[9] = {0, -z, y, z, 0, -x, -y, x, 0};
@@ -189,7 +276,9 @@ PNP_FN void rodrigues_jac(const double* r, double* J) {
     memcpy(J, J0, sizeof J0);
     return;
   }
-  double c = cos(th), s = sin(th), c1 = 1. - c, it = 1. / th;
+  double c, s;
+  det_sincos(th, &s, &c);
+  double c1 = 1. - c, it = 1. / th;
   double x = r[0] * it, y = r[1] * it, z = r[2] * it;
   double rrt[9] = {x * x, x * y, x * z, x * y, y * y, y * z, x * z, y * z, z * z};
   double rx[9] = {0, -z, y, z, 0, -x, -y, x, 0};
@@ -208,7 +297,7 @@ PNP_FN void rodrigues_R2r(const double* R, double* r) {
   double s = sqrt((rx * rx + ry * ry + rz * rz) * 0.25);
   double c = (R[0] + R[4] + R[8] - 1) * 0.5;
   c = c > 1. ? 1. : (c < -1. ? -1. : c);
-  double theta = acos(c);
+  double theta = det_acos(c);
   if (s < 1e-5) {
     if (c > 0) {
       r[0] = r[1] = r[2] = 0;
@@ -273,17 +362,17 @@ PNP_FN int solve_deg3(double a, double b, double c, double d, double* x0, double
   double Q3 = Q * Q * Q, D = Q3 + R * R, b_a_3 = (1. / 3.) * b_a;
   if (Q == 0) {
     if (R == 0) { *x0 = *x1 = *x2 = -b_a_3; return 3; }
-    *x0 = pow(2 * R, 1 / 3.0) - b_a_3;
+    *x0 = (2 * R >= 0 ? det_cbrt(2 * R) : NAN) - b_a_3; /* pow(<0, 1/3.) is NaN in OpenCV's code */
     return 1;
   }
   if (D <= 0) {
-    double theta = acos(R / sqrt(-Q3)), sq = sqrt(-Q);
-    *x0 = 2 * sq * cos(theta / 3.0) - b_a_3;
-    *x1 = 2 * sq * cos((theta + 2 * 3.14159265358979323846) / 3.0) - b_a_3;
-    *x2 = 2 * sq * cos((theta + 4 * 3.14159265358979323846) / 3.0) - b_a_3;
+    double theta = det_acos(R / sqrt(-Q3)), sq = sqrt(-Q);
+    *x0 = 2 * sq * det_cos(theta / 3.0) - b_a_3;
+    *x1 = 2 * sq * det_cos((theta + 2 * 3.14159265358979323846) / 3.0) - b_a_3;
+    *x2 = 2 * sq * det_cos((theta + 4 * 3.14159265358979323846) / 3.0) - b_a_3;
     return 3;
   }
-  double AD = pow(fabs(R) + sqrt(D), 1.0 / 3.0) * (R > 0 ? 1 : (R < 0 ? -1 : 0));
+  double AD = det_cbrt(fabs(R) + sqrt(D)) * (R > 0 ? 1 : (R < 0 ? -1 : 0));
   double BD = (AD == 0) ? 0 : -Q / AD;
   *x0 = AD + BD - b_a_3;
   return 1;
@@ -809,7 +898,7 @@ PNP_FN void lm_refine(const cam_t* k, int n, const double* wld, const double* im
     }
     double errNorm;
     for (;;) { /* step + CHECK_ERR, retrying with larger lambda */
-      double lambda = exp(lambdaLg10 * log(10.));
+      double lambda = det_pow10i(lambdaLg10);
       double S[36], dx[6];
       memcpy(S, JtJ, sizeof S);
       for (int i = 0; i < 6; ++i) S[i * 6 + i] *= 1. + lambda;
@@ -897,86 +986,13 @@ PNP_FN double ransac_update(double p, double ep, int mp, int maxIters) {
   p = p > 0 ? p : 0; p = p < 1 ? p : 1;
   ep = ep > 0 ? ep : 0; ep = ep < 1 ? ep : 1;
   double num = 1. - p > DBL_MIN ? 1. - p : DBL_MIN;
-  double denom = 1. - pow(1. - ep, mp);
+  double pw = 1.0;
+  for (int i = 0; i < mp; ++i) pw *= 1. - ep;
+  double denom = 1. - pw;
   if (denom < DBL_MIN) return 0;
-  num = log(num);
-  denom = log(denom);
-  return (denom >= 0 || -num >= maxIters * (-denom)) ? maxIters : (int)lrint(num / denom);
-}
-
-/* kernel: 0 = P3P (4-point samples), 1 = EPnP (5-point samples).  Returns 1 on consensus.
- * rvec/tvec: consensus model refit on inliers (EPnP), or — on failure — the last hypothesis
- * written by the kernel (OpenCV shares the callback's rvec/tvec buffers), has_last says
- * whether any hypothesis was written. */
-PNP_FN int ransac(const cam_t* k, int n, const float* wld_f, const float* img_f, int kernel, float thresh, int max_iters,
-                  double conf, double* rvec, double* tvec, unsigned char* mask, int* has_last) {
-  const int mp = kernel == 0 ? 4 : 5;
-  rng_t rng = {(uint64_t)-1};
-  int niters = max_iters > 1 ? max_iters : 1, maxGood = 0;
-  unsigned char best[MAXN], cur[MAXN];
-  double best_r[3], best_t[3];
-  float thr2 = (float)((double)thresh * (double)thresh);
-  *has_last = 0;
-  for (int iter = 0; iter < niters; ++iter) {
-    int idx[5];
-    for (int i = 0; i < mp; ++i) {
-      for (;;) {
-        int v = rng_uniform(&rng, 0, n), j;
-        idx[i] = v;
-        for (j = 0; j < i; ++j) if (v == idx[j]) break;
-        if (j == i) break;
-      }
-    }
-    float si[10], sw[15];
-    for (int i = 0; i < mp; ++i) {
-      si[2 * i] = img_f[2 * idx[i]]; si[2 * i + 1] = img_f[2 * idx[i] + 1];
-      for (int c = 0; c < 3; ++c) sw[3 * i + c] = wld_f[3 * idx[i] + c];
-    }
-    double r[3], t[3];
-    int ok;
-    if (kernel == 0) {
-      ok = p3p_solve4(k, si, sw, r, t);
-    } else {
-      double wd[15], id[10];
-      for (int i = 0; i < 15; ++i) wd[i] = sw[i];
-      for (int i = 0; i < 10; ++i) id[i] = si[i];
-      epnp_solve(k, 5, wd, id, 1, r, t);
-      ok = 1;
-    }
-    if (!ok) continue;
-    memcpy(rvec, r, sizeof r);
-    memcpy(tvec, t, sizeof t);
-    *has_last = 1;
-    double R[9];
-    rodrigues_r2R(r, R);
-    int good = 0;
-    for (int i = 0; i < n; ++i) {
-      float uv[2];
-      project_f(k, R, t, wld_f + 3 * i, uv);
-      cur[i] = sq_err_f(img_f + 2 * i, uv) <= thr2;
-      good += cur[i];
-    }
-    if (good > (maxGood > mp - 1 ? maxGood : mp - 1)) {
-      memcpy(best, cur, n);
-      memcpy(best_r, r, sizeof r);
-      memcpy(best_t, t, sizeof t);
-      maxGood = good;
-      niters = (int)ransac_update(conf, (double)(n - good) / n, mp, niters);
-    }
-  }
-  if (maxGood <= 0) return 0;
-  memcpy(mask, best, n);
-  /* refit on inliers with EPnP (double inputs) */
-  double wd[3 * MAXN], id[2 * MAXN];
-  int m = 0;
-  for (int i = 0; i < n; ++i)
-    if (best[i]) {
-      for (int c = 0; c < 3; ++c) wd[3 * m + c] = wld_f[3 * i + c];
-      id[2 * m] = img_f[2 * i]; id[2 * m + 1] = img_f[2 * i + 1];
-      m++;
-    }
-  epnp_solve(k, m, wd, id, 0, rvec, tvec);
-  return 1;
+  num = det_log(num);
+  denom = det_log(denom);
+  return (denom >= 0 || -num >= maxIters * (-denom)) ? maxIters : (int)det_rint(num / denom);
 }
 
 /* ------------------------------------------------------------------ Blender 2.81 mat3_to_quat */

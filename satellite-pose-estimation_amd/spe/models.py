@@ -85,7 +85,7 @@ class DETR(nn.Module):
         return self._ws
 
     # ---------------------------------------------------------------- forward
-    def forward(self, samples, clip_bbox=None, stream=None):
+    def forward(self, samples, clip_bbox=None, stream=None, return_hs=False):
         """REV/models/detr_speed.py:59-92.  Returns pred_logits [B,Q,12], pred_points [B,Q,2]
         (+ pred_sigmas as log-sigma when the sigma head is configured).  Passing `clip_bbox`
         ([B,4] device fp32) also runs the fused PostProcess and adds `probs` / `points_px`."""
@@ -107,13 +107,16 @@ class DETR(nn.Module):
         if self.cfg.sigma_head:
             out["pred_sigmas"] = torch.empty(B, Q, 2, device=dev)
             out["sigmas"] = torch.empty(B, Q, 2, device=dev)
+        if return_hs:
+            out["hs"] = torch.empty(B, Q, self.cfg.hidden_dim, device=dev)
         if clip_bbox is not None:
             clip_bbox = clip_bbox.to(device=dev, dtype=torch.float32).contiguous()
             out["probs"] = torch.empty(B, Q, 12, device=dev)
             out["points_px"] = torch.empty(B, Q, 2, device=dev)
         o = _lib.ForwardOutputs(_lib.ptr(out["pred_logits"]), _lib.ptr(out["pred_points"]), _lib.ptr(clip_bbox),
                                 _lib.ptr(out.get("probs")), _lib.ptr(out.get("points_px")),
-                                _lib.ptr(out.get("pred_sigmas")), _lib.ptr(out.get("sigmas")), None)
+                                _lib.ptr(out.get("pred_sigmas")), _lib.ptr(out.get("sigmas")),
+                                _lib.ptr(out.get("hs")))
         ws = self.workspace(B, dev)
         _lib.check(_lib.lib().spe_forward(self._h, _lib.stream_ptr(stream), _lib.ptr(images), B, _lib.ptr(ws),
                                           ws.numel(), ctypes.byref(o)), "spe_forward")

@@ -1,0 +1,98 @@
+"""GPU: end-to-end evaluate() path (model -> fused PostProcess -> batched solver -> score) and
+its agreement with the reference-style per-image path and the CPU oracles."""
+import argparse
+
+import numpy as np
+import pytest
+import torch
+
+from spe.config import SpeConfig, Camera, world_points
+from spe.synthetic import bench_weights, synthetic_batch
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def small_model(gpu_device):
+    from spe.models import DETR
+    cfg = SpeConfig(input_size=128, num_queries=11, enc_layers=2, dec_layers=2)
+
+    def hs_fn(w, images):
+        m = DETR(cfg, dtype="fp32")
+        m.load_state_dict(w)
+        return m(torch.from_numpy(images).to(gpu_device), return_hs=True)["hs"].cpu().numpy()
+
+    w = bench_weights(cfg, 3, hs_fn)
+    m = DETR(cfg, dtype="fp32")
+    m.load_state_dict(w)
+    return cfg, w, m
+
+
+def test_label_diverse_weights_feed_the_solver(gpu_device, small_model):
+    cfg, w, m = small_model
+    b = synthetic_batch(cfg, 16, 21)
+    o = m(torch.from_numpy(b["images"]).to(gpu_device), clip_bbox=torch.from_numpy(b["clip_bbox"]).float().to(gpu_device))
+    labels = o["probs"].argmax(-1).cpu().numpy()
+    n_fg = np.array([len(set(l.tolist()) - {11}) for l in labels])
+    assert (n_fg >= 4).mean() >= 0.5
+
+
+def test_batched_solver_equals_per_image_solver(gpu_device, small_model):
+    """solve_batch over the fused PostProcess outputs == reference-style per-image solver calls
+    on PostProcess's numpy dicts == CPU oracle."""
+    import pnp_ref
+    from spe.models import PostProcess
+    from spe.solver import SimplePoseSolver, SolverError
+    cfg, w, m = small_model
+    b = synthetic_batch(cfg, 12, 22)
+    img = torch.from_numpy(b["images"]).to(gpu_device)
+    clip = torch.from_numpy(b["clip_bbox"]).float().to(gpu_device)
+    o = m(img, clip_bbox=clip)
+    solver = SimplePoseSolver(argparse.Namespace(repro=20))
+    batched = solver.solve_batch(o["points_px"], o["probs"])
+    pp = PostProcess()(o, [c for c in b["clip_bbox"]])
+    ref = pnp_ref.pnp_batch(np.stack([r["points"] for r in pp]), np.stack([r["logits"] for r in pp]), Camera.K,
+                            world_points(), mode=pnp_ref.MODE_RANSAC_P3P_LM)
+    st = batched["status"].cpu().numpy()
+    np.testing.assert_array_equal(st, ref["status"])
+    for i, r in enumerate(pp):
+        try:
+            q, t = solver(r["points"], r["logits"])
+        except (IndexError, SolverError):
+            assert st[i] in (1, 2, 4)
+            continue
+        np.testing.assert_allclose(q, batched["quat"][i].double().cpu().numpy(), atol=1e-7)
+        np.testing.assert_allclose(t, batched["tvec"][i].cpu().numpy(), rtol=1e-9, atol=1e-9)
+        np.testing.assert_allclose(t, ref["tvec"][i], rtol=1e-6, atol=1e-6)
+
+
+def test_evaluate_matches_reference_style_speedeval(gpu_device, small_model):
+    from spe.engine import evaluate
+    from spe.misc import NestedTensor
+    from spe.models import PostProcess
+    from spe.solver import build_solver
+    from spe.speed_eval import SpeedEval
+    cfg, w, m = small_model
+    b = synthetic_batch(cfg, 10, 23)
+    names = [f"img{i:03d}.jpg" for i in range(10)]
+    gt = [{"filename": n, "q_vbs2tango": b["quat"][i].tolist(), "r_Vo2To_vbs_true": b["tvec"][i].tolist()}
+          for i, n in enumerate(names)]
+    loader = []
+    for s in range(0, 10, 4):
+        x = torch.from_numpy(b["images"][s:s + 4])
+        tg = [{"filename": names[i], "clip_bbox": torch.as_tensor(b["clip_bbox"][i])} for i in range(s, min(s + 4, 10))]
+        loader.append((NestedTensor(x, torch.zeros(x.shape[0], 128, 128, dtype=torch.bool)), tg))
+    solver = build_solver(argparse.Namespace(repro=20, solver="ransac_p3p_lm"))
+    stats, ev = evaluate(m, None, {"points": PostProcess()}, loader, gt, solver, gpu_device, None)
+    # reference-style path: PostProcess dicts -> per-image solver -> SpeedEval.update
+    ev2 = SpeedEval(gt, solver)
+    for x, tg in loader:
+        out = m(x.tensors.to(gpu_device))
+        pp = PostProcess()(out, [t["clip_bbox"] for t in tg])
+        ev2.update({t["filename"]: r for t, r in zip(tg, pp)})
+    ev2.summarize()
+    for n in names:
+        a, c = ev.log[n], ev2.log[n]
+        assert a["quat_pr"] == c["quat_pr"] and a["tvec_pr"] == c["tvec_pr"]
+        assert abs(a["score"] - c["score"]) < 1e-7
+    assert stats["speed_eval_pose"] == ev2.stats

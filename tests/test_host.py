@@ -1,0 +1,120 @@
+"""CPU: host-side logic of the drop-in surface (no GPU compute).
+
+SpeedEval log schema / rounding / failure mapping (REV/datasets/speed.py:337-421),
+speed_score (REV/utils/speed_eval.py:245-262), NestedTensor batching (REV/utils/misc.py:287-333),
+and the data-parallel record exchange over a world_size-2 gloo group.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+import pnp_ref
+from spe import dist as sd
+from spe.misc import NestedTensor, nested_tensor_from_tensor_list, collate_fn
+from spe.speed_eval import SpeedEval, speed_score
+from spe.solver import SolverError
+
+
+class _StubSolver:
+    """Returns a fixed pose, or raises what the reference's cv2 / indexing raises."""
+
+    def __init__(self):
+        self.calls = 0
+
+    def __call__(self, points, logits):
+        self.calls += 1
+        if logits.shape[0] == 1:
+            raise IndexError("no fg")
+        if logits.shape[0] == 2:
+            raise SolverError("cv2")
+        return np.array([1.0, 0, 0, 0]), np.array([0.0, 0.0, 10.0])
+
+
+def _gt():
+    return [{"filename": f"img{i}.jpg", "q_vbs2tango": [1.0, 0, 0, 0], "r_Vo2To_vbs_true": [0.0, 0.0, 10.0 + i]}
+            for i in range(3)]
+
+
+def test_speed_score_matches_oracle():
+    rng = np.random.default_rng(0)
+    for _ in range(50):
+        q, qg = rng.normal(size=4), rng.normal(size=4)
+        t, tg = rng.normal(size=3), rng.normal(size=3) + 5
+        assert np.allclose(speed_score(q, t, qg / np.linalg.norm(qg), tg),
+                           pnp_ref.speed_score(q, t, qg / np.linalg.norm(qg), tg))
+
+
+def test_speedeval_update_and_summary_format():
+    ev = SpeedEval(_gt(), _StubSolver())
+    ev.update({"img0.jpg": {"points": np.full((11, 2), 1.234567, np.float32), "logits": np.full((11, 12), 0.1234567)},
+               "img1.jpg": {"points": np.zeros((1, 2)), "logits": np.zeros((1, 12))},
+               "img2.jpg": {"points": np.zeros((2, 2)), "logits": np.zeros((2, 12))}})
+    rec = ev.log["img0.jpg"]
+    # float32 points round in float32 exactly as np.around does in the reference
+    assert rec["points"][0] == [float(np.float32(1.23))] * 2 and rec["logits"][0][0] == 0.123457
+    assert rec["score"] == 0.0
+    # failures -> zero pose -> s_t = 1, s_q = pi
+    for fn in ("img1.jpg", "img2.jpg"):
+        assert ev.log[fn]["quat_pr"] == [0.0] * 4 and ev.log[fn]["score_tvec"] == 1.0
+        assert ev.log[fn]["score_quat"] == pytest.approx(np.pi, abs=1e-7)
+    s = ev.summarize()
+    mean_t = np.mean([r["score_tvec"] for r in ev.log.values()])
+    assert s.startswith("tvec score: {:.6f}, quat score: ".format(mean_t))
+    # reference quirk: "median" of the already-averaged scalar equals the mean
+    assert "median tvec: {:.6f},".format(mean_t) in s
+    assert "median tvec abs:[" in s
+
+
+def test_nested_tensor_contract():
+    a, b = torch.ones(3, 4, 5), torch.ones(3, 6, 2)
+    nt = nested_tensor_from_tensor_list([a, b])
+    assert nt.tensors.shape == (2, 3, 6, 5)
+    assert not nt.mask[0, :4, :5].any() and nt.mask[0, 4:, :].all() and nt.mask[1, :, 2:].all()
+    x, targets = collate_fn([(a, {"f": 1}), (a, {"f": 2})])
+    assert isinstance(x, NestedTensor) and not x.mask.any() and len(targets) == 2
+
+
+def test_shard_covers_everything():
+    for n in (1, 7, 64, 256):
+        for w in (1, 2, 3, 8):
+            parts = [sd.shard(n, r, w) for r in range(w)]
+            assert parts[0][0] == 0 and parts[-1][1] == n
+            assert all(parts[i][1] == parts[i + 1][0] for i in range(w - 1))
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    r, w, _ = sd.init_distributed_mode(backend="gloo")
+    B = 4
+    quat = torch.full((B, 4), float(r))
+    tvec = torch.full((B, 3), 10.0 * r, dtype=torch.float64)
+    s_t = torch.full((B,), 0.1 * r, dtype=torch.float64)
+    s_q = torch.full((B,), 0.2 * r, dtype=torch.float64)
+    status = torch.full((B,), r, dtype=torch.int32)
+    rec = sd.all_gather_records(sd.pack_records(quat, tvec, s_t, s_q, status))
+    log = sd.all_gather_log({f"img{r}_{i}": {"score": float(r)} for i in range(2)})
+    if r == 0:
+        out.put((rec.numpy().tolist(), sorted(log)))
+    torch.distributed.destroy_process_group()
+
+
+def test_gloo_world2_record_exchange():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 29500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    rec, keys = q.get(timeout=120)
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    rec = np.asarray(rec)
+    assert rec.shape == (8, sd.RECORD_LEN)
+    assert (rec[:4, 0] == 0).all() and (rec[4:, 0] == 1).all() and (rec[4:, 9] == 1).all()
+    assert keys == ["img0_0", "img0_1", "img1_0", "img1_1"]
