@@ -14,8 +14,13 @@
 // tile is fed straight back as the B operand of O^T = V^T . P^T without leaving registers.
 // K tiles [64 keys][32] and V^T tiles [32][64 keys] are staged through XOR-swizzled LDS,
 // double-buffered (register prefetch of tile t+1 overlaps the MFMAs of tile t).
-// bf16: v_mfma_f32_32x32x16_bf16 (2 per 32x32 S tile, 2 per PV step).
-// fp32: v_mfma_f32_32x32x2_f32 (exact f32; parity mode).
+//
+// head_dim 32 makes the softmax the bottleneck (one exp per 128 MFMA flops), so the bf16 path
+// spends as little VALU per score as possible: Q is pre-scaled by softmax_scale*log2(e) (scores
+// come out in the exp2 domain), the running max only triggers an O/l rescale when some lane's
+// max actually grew (wave-uniform branch), and the row sums l are accumulated by the matrix
+// pipe (ones . P^T MFMA, which also normalises with exactly the bf16 P the numerator uses).
+// bf16: v_mfma_f32_32x32x16_bf16.  fp32 (parity mode): v_mfma_f32_32x32x2_f32, exact f32.
 #include "spe_common.h"
 #include "spe_kernels.h"
 
@@ -24,6 +29,7 @@ namespace {
 constexpr int NT = 256;
 constexpr int KT = 64;                 // keys per tile
 constexpr float LOG2E = 1.4426950408889634f;
+constexpr float NEG_BIG = -1.0e30f;    // finite "minus infinity" (exp2 of it underflows to 0)
 
 // ---------------------------------------------------------------- bf16 LDS image
 // K tile: 64 rows x 64 B (4 chunks); chunk slot c ^ ((row >> 2) & 3)
@@ -95,42 +101,25 @@ struct Stage {
   }
 };
 
-// Online-softmax bookkeeping on a lane's 32 scores (two 32-key sub-tiles, 16 each).
-// Returns alpha (rescale of the running state); s[] becomes exp2(s - m_new).
-SPE_DEV float softmax_tile(f32x16& s0, f32x16& s1, float& m, float& l, float sl2, int key_base, int Tk, int hh) {
-  const bool tail = key_base + KT > Tk;
-  float mx = -INFINITY;
+// mask keys past Tk (last tile only) and return the lane-pair max of the 32 scores
+SPE_DEV float tile_max(f32x16& s0, f32x16& s1, int key_base, int Tk, int hh) {
+  if (key_base + KT > Tk) {
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    const int kr = (r & 3) + 8 * (r >> 2) + 4 * hh;
-    float a = s0[r] * sl2, b = s1[r] * sl2;
-    if (tail) {
-      if (key_base + kr >= Tk) a = -INFINITY;
-      if (key_base + 32 + kr >= Tk) b = -INFINITY;
+    for (int r = 0; r < 16; ++r) {
+      const int kr = (r & 3) + 8 * (r >> 2) + 4 * hh;
+      if (key_base + kr >= Tk) s0[r] = NEG_BIG;
+      if (key_base + 32 + kr >= Tk) s1[r] = NEG_BIG;
     }
-    s0[r] = a;
-    s1[r] = b;
-    mx = fmaxf(mx, fmaxf(a, b));
   }
-  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-  const float mn = fmaxf(m, mx);
-  const float alpha = exp2f(m - mn);
-  float sum = 0.f;
+  float mx = NEG_BIG;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) {
-    s0[r] = exp2f(s0[r] - mn);
-    s1[r] = exp2f(s1[r] - mn);
-    sum += s0[r] + s1[r];
-  }
-  l = l * alpha + sum;
-  m = mn;
-  return alpha;
+  for (int r = 0; r < 16; ++r) mx = __builtin_fmaxf(mx, __builtin_fmaxf(s0[r], s1[r]));
+  return __builtin_fmaxf(mx, __shfl_xor(mx, 32, 64));
 }
 
-template <typename T>
-__global__ __launch_bounds__(NT, 2) void attn_kernel(AttnArgs a) {
-  constexpr int ES = sizeof(T);
-  constexpr int KBYTES = KT * 32 * ES, VBYTES = 32 * KT * ES;
+// ------------------------------------------------------------------ bf16 kernel
+__global__ __launch_bounds__(NT, 2) void attn_bf16_kernel(AttnArgs a) {
+  constexpr int KBYTES = KT * 32 * 2, VBYTES = 32 * KT * 2;
   __shared__ __attribute__((aligned(16))) char smem[2 * (KBYTES + VBYTES)];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int hh = lane >> 5, r32 = lane & 31;
@@ -140,26 +129,30 @@ __global__ __launch_bounds__(NT, 2) void attn_kernel(AttnArgs a) {
   const int b = bh / a.H, h = bh - b * a.H;
   const int q = qb * 128 + wid * 32 + r32;
   const bool wave_live = qb * 128 + wid * 32 < a.Tq;
-  const float sl2 = a.scale * LOG2E;
 
-  // query fragment (B operand of S^T = K . Q^T)
-  u32x4 qf[ES == 2 ? 2 : 4];
+  // query fragment (B operand of S^T = K . Q^T), pre-scaled into the exp2 domain
+  bf16x8 qf[2];
   {
-    const T* qp = (const T*)a.q + (size_t)(b * a.Tq + (q < a.Tq ? q : 0)) * a.ldq + h * 32;
+    const float sl2 = a.scale * LOG2E;
+    const bf16* qp = (const bf16*)a.q + (size_t)(b * a.Tq + (q < a.Tq ? q : 0)) * a.ldq + h * 32;
 #pragma unroll
-    for (int i = 0; i < (ES == 2 ? 2 : 4); ++i) {
-      const int d0 = (ES == 2) ? (16 * i + 8 * hh) : (16 * hh + 4 * i);
-      qf[i] = q < a.Tq ? ld16(qp + d0) : u32x4{0, 0, 0, 0};
+    for (int i = 0; i < 2; ++i) {
+      float f[8];
+      unpack16<bf16>(q < a.Tq ? ld16(qp + 16 * i + 8 * hh) : u32x4{0, 0, 0, 0}, f);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) f[e] *= sl2;
+      qf[i] = __builtin_bit_cast(bf16x8, pack16<bf16>(f));
     }
   }
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u});
 
   f32x16 o;
 #pragma unroll
   for (int r = 0; r < 16; ++r) o[r] = 0.f;
-  float m = -INFINITY, l = 0.f;
+  float m = NEG_BIG, l = 0.f;
 
   const int ntiles = (a.Tk + KT - 1) / KT;
-  Stage<T> st;
+  Stage<bf16> st;
   st.load(a, b, h, 0, tid);
   st.store(smem, smem + KBYTES, tid);
   __syncthreads();
@@ -172,60 +165,137 @@ __global__ __launch_bounds__(NT, 2) void attn_kernel(AttnArgs a) {
       f32x16 s0, s1;
 #pragma unroll
       for (int r = 0; r < 16; ++r) { s0[r] = 0.f; s1[r] = 0.f; }
-      if constexpr (ES == 2) {
 #pragma unroll
-        for (int sub = 0; sub < 2; ++sub) {
-          const int key = sub * 32 + r32;
-          bf16x8 k0 = __builtin_bit_cast(bf16x8, ld16(kl + k_off_bf16(key, hh)));
-          bf16x8 k1 = __builtin_bit_cast(bf16x8, ld16(kl + k_off_bf16(key, 2 + hh)));
-          f32x16& s = sub ? s1 : s0;
-          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, __builtin_bit_cast(bf16x8, qf[0]), s, 0, 0, 0);
-          s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, __builtin_bit_cast(bf16x8, qf[1]), s, 0, 0, 0);
-        }
-      } else {
+      for (int sub = 0; sub < 2; ++sub) {
+        const int key = sub * 32 + r32;
+        bf16x8 k0 = __builtin_bit_cast(bf16x8, ld16(kl + k_off_bf16(key, hh)));
+        bf16x8 k1 = __builtin_bit_cast(bf16x8, ld16(kl + k_off_bf16(key, 2 + hh)));
+        f32x16& s = sub ? s1 : s0;
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf[0], s, 0, 0, 0);
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[1], s, 0, 0, 0);
+      }
+      const float mx = tile_max(s0, s1, kt * KT, a.Tk, hh);
+      if (__any(mx > m)) {                         // wave-uniform: rescale only when a max grew
+        const float mn = __builtin_fmaxf(m, mx);
+        const float alpha = __builtin_amdgcn_exp2f(m - mn);
 #pragma unroll
-        for (int sub = 0; sub < 2; ++sub) {
-          const int key = sub * 32 + r32;
-          f32x16& s = sub ? s1 : s0;
+        for (int r = 0; r < 16; ++r) o[r] *= alpha;
+        l *= alpha;
+        m = mn;
+      }
+      f32x16 ls;
 #pragma unroll
-          for (int c = 0; c < 4; ++c) {
-            f32x4 kv = __builtin_bit_cast(f32x4, ld16(kl + k_off_f32(key, 4 * hh + c)));
-            f32x4 qv = __builtin_bit_cast(f32x4, qf[c]);
+      for (int r = 0; r < 16; ++r) ls[r] = 0.f;
 #pragma unroll
-            for (int e = 0; e < 4; ++e) s = __builtin_amdgcn_mfma_f32_32x32x2f32(kv[e], qv[e], s, 0, 0, 0);
-          }
+      for (int sub = 0; sub < 2; ++sub) {
+        f32x16& p = sub ? s1 : s0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(p[r] - m);
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          u32x4 pw{pack_bf16x2(p[8 * ks + 0], p[8 * ks + 1]), pack_bf16x2(p[8 * ks + 2], p[8 * ks + 3]),
+                   pack_bf16x2(p[8 * ks + 4], p[8 * ks + 5]), pack_bf16x2(p[8 * ks + 6], p[8 * ks + 7])};
+          const bf16x8 pb = __builtin_bit_cast(bf16x8, pw);
+          const int u0 = (sub * 32 + 16 * ks + 4 * hh) >> 2;   // 8-byte unit = 4 keys
+          u32x2 v0 = ld8(vl + v_off_bf16(r32, u0));
+          u32x2 v1 = ld8(vl + v_off_bf16(r32, u0 + 2));
+          u32x4 va{v0.x, v0.y, v1.x, v1.y};
+          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, va), pb, o, 0, 0, 0);
+          ls = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pb, ls, 0, 0, 0);   // column sums of P^T
         }
       }
-      const float alpha = softmax_tile(s0, s1, m, l, sl2, kt * KT, a.Tk, hh);
+      l += ls[0];
+    }
+    if (more) st.store(smem + ((kt + 1) & 1) * (KBYTES + VBYTES), smem + ((kt + 1) & 1) * (KBYTES + VBYTES) + KBYTES, tid);
+    __syncthreads();
+  }
+
+  if (!wave_live || q >= a.Tq) return;
+  const float inv = 1.f / l;            // l already sums all 64 keys of every tile
+  bf16* op = (bf16*)a.o + (size_t)(b * a.Tq + q) * a.ldo + h * 32;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int d0 = 8 * g + 4 * hh;
+    st8(op + d0, u32x2{pack_bf16x2(o[4 * g] * inv, o[4 * g + 1] * inv), pack_bf16x2(o[4 * g + 2] * inv, o[4 * g + 3] * inv)});
+  }
+}
+
+// ------------------------------------------------------------------ fp32 (parity) kernel
+__global__ __launch_bounds__(NT, 2) void attn_f32_kernel(AttnArgs a) {
+  constexpr int KBYTES = KT * 32 * 4, VBYTES = 32 * KT * 4;
+  __shared__ __attribute__((aligned(16))) char smem[2 * (KBYTES + VBYTES)];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int hh = lane >> 5, r32 = lane & 31;
+  const int qblocks = (a.Tq + 127) / 128;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = bid / qblocks, qb = bid - bh * qblocks;
+  const int b = bh / a.H, h = bh - b * a.H;
+  const int q = qb * 128 + wid * 32 + r32;
+  const bool wave_live = qb * 128 + wid * 32 < a.Tq;
+  const float sl2 = a.scale * LOG2E;
+
+  u32x4 qf[4];
+  {
+    const float* qp = (const float*)a.q + (size_t)(b * a.Tq + (q < a.Tq ? q : 0)) * a.ldq + h * 32;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) qf[i] = q < a.Tq ? ld16(qp + 16 * hh + 4 * i) : u32x4{0, 0, 0, 0};
+  }
+  f32x16 o;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) o[r] = 0.f;
+  float m = NEG_BIG, l = 0.f;
+
+  const int ntiles = (a.Tk + KT - 1) / KT;
+  Stage<float> st;
+  st.load(a, b, h, 0, tid);
+  st.store(smem, smem + KBYTES, tid);
+  __syncthreads();
+  for (int kt = 0; kt < ntiles; ++kt) {
+    char* kl = smem + (kt & 1) * (KBYTES + VBYTES);
+    char* vl = kl + KBYTES;
+    const bool more = kt + 1 < ntiles;
+    if (more) st.load(a, b, h, kt + 1, tid);
+    if (wave_live) {
+      f32x16 s0, s1;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { s0[r] = 0.f; s1[r] = 0.f; }
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        const int key = sub * 32 + r32;
+        f32x16& s = sub ? s1 : s0;
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          f32x4 kv = __builtin_bit_cast(f32x4, ld16(kl + k_off_f32(key, 4 * hh + c)));
+          f32x4 qv = __builtin_bit_cast(f32x4, qf[c]);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) s = __builtin_amdgcn_mfma_f32_32x32x2f32(kv[e], qv[e], s, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { s0[r] *= sl2; s1[r] *= sl2; }
+      const float mx = tile_max(s0, s1, kt * KT, a.Tk, hh);
+      const float mn = __builtin_fmaxf(m, mx);
+      const float alpha = exp2f(m - mn);
+      float sum = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        s0[r] = exp2f(s0[r] - mn);
+        s1[r] = exp2f(s1[r] - mn);
+        sum += s0[r] + s1[r];
+      }
+      l = l * alpha + sum;
+      m = mn;
 #pragma unroll
       for (int r = 0; r < 16; ++r) o[r] *= alpha;
-      if constexpr (ES == 2) {
 #pragma unroll
-        for (int sub = 0; sub < 2; ++sub) {
-          const f32x16& p = sub ? s1 : s0;
+      for (int sub = 0; sub < 2; ++sub) {
+        const f32x16& p = sub ? s1 : s0;
 #pragma unroll
-          for (int ks = 0; ks < 2; ++ks) {
-            u32x4 pb{pack_bf16x2(p[8 * ks + 0], p[8 * ks + 1]), pack_bf16x2(p[8 * ks + 2], p[8 * ks + 3]),
-                     pack_bf16x2(p[8 * ks + 4], p[8 * ks + 5]), pack_bf16x2(p[8 * ks + 6], p[8 * ks + 7])};
-            const int u0 = (sub * 32 + 16 * ks + 4 * hh) >> 2;   // 8-byte unit = 4 keys
-            u32x2 v0 = ld8(vl + v_off_bf16(r32, u0));
-            u32x2 v1 = ld8(vl + v_off_bf16(r32, u0 + 2));
-            u32x4 va{v0.x, v0.y, v1.x, v1.y};
-            o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, va), __builtin_bit_cast(bf16x8, pb),
-                                                        o, 0, 0, 0);
-          }
-        }
-      } else {
+        for (int i = 0; i < 4; ++i) {
+          // keys 8i + 4hh + (0..3) of this sub-tile = chunk 2i + hh
+          f32x4 vv = __builtin_bit_cast(f32x4, ld16(vl + v_off_f32(r32, sub * 8 + 2 * i + hh)));
 #pragma unroll
-        for (int sub = 0; sub < 2; ++sub) {
-          const f32x16& p = sub ? s1 : s0;
-#pragma unroll
-          for (int i = 0; i < 4; ++i) {
-            // keys 8i + 4hh + (0..3) of this sub-tile = chunk 2i + hh
-            f32x4 vv = __builtin_bit_cast(f32x4, ld16(vl + v_off_f32(r32, sub * 8 + 2 * i + hh)));
-#pragma unroll
-            for (int e = 0; e < 4; ++e) o = __builtin_amdgcn_mfma_f32_32x32x2f32(vv[e], p[4 * i + e], o, 0, 0, 0);
-          }
+          for (int e = 0; e < 4; ++e) o = __builtin_amdgcn_mfma_f32_32x32x2f32(vv[e], p[4 * i + e], o, 0, 0, 0);
         }
       }
     }
@@ -234,18 +304,13 @@ __global__ __launch_bounds__(NT, 2) void attn_kernel(AttnArgs a) {
   }
 
   if (!wave_live || q >= a.Tq) return;
-  const float lt = l + __shfl_xor(l, 32, 64);
+  const float lt = l + __shfl_xor(l, 32, 64);    // each lane of the pair summed its 32 keys
   const float inv = 1.f / lt;
-  T* op = (T*)a.o + (size_t)(b * a.Tq + q) * a.ldo + h * 32;
+  float* op = (float*)a.o + (size_t)(b * a.Tq + q) * a.ldo + h * 32;
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
-    const int d0 = 8 * g + 4 * hh;
     float v[4] = {o[4 * g] * inv, o[4 * g + 1] * inv, o[4 * g + 2] * inv, o[4 * g + 3] * inv};
-    if constexpr (ES == 2) {
-      st8(op + d0, u32x2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])});
-    } else {
-      st16(op + d0, pack16<float>(v));
-    }
+    st16(op + 8 * g + 4 * hh, pack16<float>(v));
   }
 }
 
@@ -257,8 +322,8 @@ int spe_launch_attention(const AttnArgs& a, int dtype, hipStream_t s) {
   if ((a.ldq % ce) || (a.ldk % ce) || (a.ldo % 4)) return -5;
   dim3 grid(a.B * a.H * ((a.Tq + 127) / 128)), block(NT);
   if (dtype == SPE_DTYPE_BF16)
-    hipLaunchKernelGGL(attn_kernel<bf16>, grid, block, 0, s, a);
+    hipLaunchKernelGGL(attn_bf16_kernel, grid, block, 0, s, a);
   else
-    hipLaunchKernelGGL(attn_kernel<float>, grid, block, 0, s, a);
+    hipLaunchKernelGGL(attn_f32_kernel, grid, block, 0, s, a);
   return (int)hipGetLastError();
 }

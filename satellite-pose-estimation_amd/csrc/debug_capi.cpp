@@ -1,0 +1,43 @@
+// Kernel-level test hooks (declared in include/spe.h, "kernel test hooks"): thin C entry points
+// that launch one kernel family on caller-provided device buffers, so tests/ can check each
+// kernel against a plain torch reference of the same op at awkward shapes (edges, ragged
+// tiles, strides) — the forward pass alone would hide a wrong-but-normalised intermediate.
+#include <hip/hip_runtime.h>
+
+#include "../../include/spe.h"
+#include "model_state.h"
+
+extern "C" {
+
+int spe_debug_gemm(void* stream, int dtype, int mode, const void* A, int lda, const void* P, int ldp, int prow,
+                   int H, int W, int Cin, int KH, int KW, int stride, int pad, const void* Bw, int ldb, int M, int N,
+                   int K, const float* bias, const void* R, int ldr, int relu, void* C, int ldc, int out_f32, int vt_T,
+                   int vt_B) {
+  GemmArgs g{};
+  g.A = A; g.lda = lda; g.P = P; g.ldp = ldp; g.prow = prow;
+  g.H = H; g.W = W; g.Cin = Cin; g.KH = KH; g.KW = KW; g.stride = stride; g.pad = pad;
+  g.Ho = mode == GEMM_CONV ? (H + 2 * pad - KH) / stride + 1 : 0;
+  g.Wo = mode == GEMM_CONV ? (W + 2 * pad - KW) / stride + 1 : 0;
+  g.B = Bw; g.ldb = ldb; g.M = M; g.N = N; g.K = K;
+  g.bias = bias; g.R = R; g.ldr = ldr; g.relu = relu; g.C = C; g.ldc = ldc; g.out_f32 = out_f32;
+  g.vt_T = vt_T; g.vt_B = vt_B;
+  int rc = spe_launch_gemm(g, dtype, mode, (hipStream_t)stream);
+  return rc < 0 ? spe_fail(SPE_E_LAUNCH, "gemm launch rejected its arguments") : rc;
+}
+
+int spe_debug_attention(void* stream, int dtype, const void* q, int ldq, const void* k, int ldk, const void* vt,
+                        void* o, int ldo, int B, int H, int Tq, int Tk, float scale) {
+  AttnArgs a{};
+  a.q = q; a.ldq = ldq; a.k = k; a.ldk = ldk; a.vt = vt; a.o = o; a.ldo = ldo;
+  a.B = B; a.H = H; a.Tq = Tq; a.Tk = Tk; a.scale = scale;
+  int rc = spe_launch_attention(a, dtype, (hipStream_t)stream);
+  return rc < 0 ? spe_fail(SPE_E_LAUNCH, "attention launch rejected its arguments") : rc;
+}
+
+int spe_debug_layernorm(void* stream, int dtype, const void* x, const float* gamma, const float* beta, void* out,
+                        float* out_f32, int M, int D) {
+  int rc = spe_launch_layernorm(x, gamma, beta, out, out_f32, M, D, dtype, (hipStream_t)stream);
+  return rc < 0 ? spe_fail(SPE_E_LAUNCH, "layernorm launch rejected its arguments") : rc;
+}
+
+}  // extern "C"

@@ -1,0 +1,181 @@
+"""GPU: each kernel family against a plain torch fp32 reference of the same op, through the
+C ABI test hooks, at ragged / edge shapes (partial tiles, strides, channel slices).
+
+Tolerances: fp32 storage (exact-f32 MFMA) max|d| <= 1e-4 * scale; bf16 storage: inputs are
+pre-rounded to bf16 so only accumulation order and the bf16 output rounding remain,
+max|d| <= 1e-2 * scale (scale = max|reference|, at least 1).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+import torch.nn.functional as F
+
+from spe import _lib
+
+pytestmark = pytest.mark.gpu
+
+DT = {"bf16": (_lib.SPE_DTYPE_BF16, torch.bfloat16, 1e-2), "fp32": (_lib.SPE_DTYPE_F32, torch.float32, 1e-4)}
+
+
+def _p(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def _close(got, ref, tol):
+    scale = max(1.0, ref.abs().max().item())
+    err = (got.float() - ref.float()).abs().max().item()
+    assert err <= tol * scale, (err, scale)
+
+
+def _gemm(dtype, mode, A, W, M, N, K, lda, ldb, C, ldc, bias=None, R=None, ldr=0, relu=0, P=None, ldp=0, prow=1,
+          conv=(0, 0, 0, 1, 1, 1, 0), out_f32=0, vt=(0, 0)):
+    L = _lib.lib()
+    H, Wd, Cin, KH, KW, stride, pad = conv
+    rc = L.spe_debug_gemm(None, DT[dtype][0], mode, _p(A), lda, _p(P), ldp, prow, H, Wd, Cin, KH, KW, stride, pad,
+                          _p(W), ldb, M, N, K, _p(bias), _p(R), ldr, relu, _p(C), ldc, out_f32, vt[0], vt[1])
+    assert rc == 0, L.spe_last_error()
+    torch.cuda.synchronize()
+
+
+def _padded_weight(Wt, ldb, dt):
+    N, K = Wt.shape
+    Wp = torch.zeros(N, ldb, dtype=dt, device=Wt.device)
+    Wp[:, :K] = Wt.to(dt)
+    return Wp
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+@pytest.mark.parametrize("M,N,K", [(300, 200, 256), (128, 64, 64), (77, 520, 2048), (5, 12, 192)])
+def test_gemm_linear_epilogue(gpu_device, dtype, M, N, K):
+    _, dt, tol = DT[dtype]
+    g = torch.Generator(device="cpu").manual_seed(M * 7 + N)
+    A = torch.randn(M, K, generator=g).to(gpu_device, dt)
+    Wt = (torch.randn(N, K, generator=g) / K ** 0.5).to(gpu_device, dt)
+    ldb = (K + 63) // 64 * 64
+    Wp = _padded_weight(Wt, ldb, dt)
+    bias = torch.randn(N, generator=g).to(gpu_device)
+    R = torch.randn(M, N + 8, generator=g).to(gpu_device, dt)
+    C = torch.zeros(M, N + 8, dtype=dt, device=gpu_device)
+    _gemm(dtype, 0, A, Wp, M, N, K, K, ldb, C, N + 8, bias=bias, R=R, ldr=N + 8, relu=1)
+    ref = torch.relu(A.float() @ Wt.float().t() + bias + R[:, :N].float())
+    _close(C[:, :N], ref, tol)
+    assert (C[:, N:] == 0).all()                       # nothing written past N
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_gemm_linear_add_and_f32_out(gpu_device, dtype):
+    _, dt, tol = DT[dtype]
+    M, N, K, prow = 250, 96, 256, 25
+    g = torch.Generator(device="cpu").manual_seed(3)
+    A = torch.randn(M, K, generator=g).to(gpu_device, dt)
+    P = torch.randn(prow, K, generator=g).to(gpu_device, dt)
+    Wt = (torch.randn(N, K, generator=g) / 16).to(gpu_device, dt)
+    Wp = _padded_weight(Wt, 256, dt)
+    C = torch.zeros(M, N, device=gpu_device)
+    _gemm(dtype, 1, A, Wp, M, N, K, K, 256, C, N, P=P, ldp=K, prow=prow, out_f32=1)
+    Aplus = (A.float() + P.float().repeat(M // prow, 1)).to(dt).float()   # the add is rounded to T
+    _close(C, Aplus @ Wt.float().t(), tol)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+@pytest.mark.parametrize("B,H,W,Cin,Cout,k,s,p", [(2, 13, 11, 16, 72, 3, 2, 1), (1, 20, 20, 8, 64, 7, 2, 3),
+                                                  (3, 9, 9, 64, 130, 1, 2, 0), (2, 10, 10, 32, 40, 3, 1, 1)])
+def test_gemm_conv_nhwc(gpu_device, dtype, B, H, W, Cin, Cout, k, s, p):
+    _, dt, tol = DT[dtype]
+    g = torch.Generator(device="cpu").manual_seed(B * H + Cout)
+    x = torch.randn(B, Cin, H, W, generator=g).to(gpu_device, dt)
+    w = (torch.randn(Cout, Cin, k, k, generator=g) / (Cin * k * k) ** 0.5).to(gpu_device, dt)
+    bias = torch.randn(Cout, generator=g).to(gpu_device)
+    ref = F.conv2d(x.float(), w.float(), bias, stride=s, padding=p)
+    Ho, Wo = ref.shape[2], ref.shape[3]
+    K = k * k * Cin
+    ldb = (K + 63) // 64 * 64
+    Wp = _padded_weight(w.permute(0, 2, 3, 1).reshape(Cout, K), ldb, dt)
+    xn = x.permute(0, 2, 3, 1).contiguous()
+    C = torch.zeros(B * Ho * Wo, Cout, dtype=dt, device=gpu_device)
+    _gemm(dtype, 2, xn, Wp, B * Ho * Wo, Cout, K, 0, ldb, C, Cout, bias=bias, conv=(H, W, Cin, k, k, s, p))
+    _close(C, ref.permute(0, 2, 3, 1).reshape(-1, Cout), tol)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+@pytest.mark.parametrize("T", [16, 11])
+def test_gemm_head_transposed_store(gpu_device, dtype, T):
+    _, dt, tol = DT[dtype]
+    B, K, N = 3, 256, 512                              # two groups of 256 (like the cross-attn V of 2 layers)
+    M = B * T
+    g = torch.Generator(device="cpu").manual_seed(T)
+    A = torch.randn(M, K, generator=g).to(gpu_device, dt)
+    Wt = (torch.randn(N, K, generator=g) / 16).to(gpu_device, dt)
+    bias = torch.randn(N, generator=g).to(gpu_device)
+    C = torch.zeros(2 * B * 256 * T, dtype=dt, device=gpu_device)
+    _gemm(dtype, 0, A, _padded_weight(Wt, 256, dt), M, N, K, K, 256, C, 8, bias=bias, vt=(T, B))
+    ref = (A.float() @ Wt.float().t() + bias).view(B, T, 2, 256).permute(2, 0, 3, 1).reshape(-1)
+    _close(C, ref, tol)
+
+
+def _attn_ref(q, k, v, scale):
+    a = torch.softmax((q.float() @ k.float().transpose(-1, -2)) * scale, -1)
+    return a @ v.float()
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+@pytest.mark.parametrize("B,H,Tq,Tk", [(2, 8, 200, 200), (3, 8, 11, 330), (1, 8, 11, 11), (1, 2, 300, 64)])
+def test_attention(gpu_device, dtype, B, H, Tq, Tk):
+    code, dt, tol = DT[dtype]
+    g = torch.Generator(device="cpu").manual_seed(Tq + Tk)
+    ld = H * 32 + 16                                   # row stride wider than the heads
+    Q = (torch.randn(B * Tq, ld, generator=g) * 2).to(gpu_device, dt)
+    K = (torch.randn(B * Tk, ld, generator=g) * 2).to(gpu_device, dt)
+    V = torch.randn(B, H, Tk, 32, generator=g).to(gpu_device, dt)
+    VT = V.transpose(-1, -2).contiguous()
+    O = torch.zeros(B * Tq, H * 32, dtype=dt, device=gpu_device)
+    scale = 32 ** -0.5
+    rc = _lib.lib().spe_debug_attention(None, code, _p(Q), ld, _p(K), ld, _p(VT), _p(O), H * 32, B, H, Tq, Tk, scale)
+    assert rc == 0
+    torch.cuda.synchronize()
+    q = Q[:, : H * 32].view(B, Tq, H, 32).transpose(1, 2)
+    k = K[:, : H * 32].view(B, Tk, H, 32).transpose(1, 2)
+    if dtype == "bf16":
+        q = (q.float() * scale * 1.4426950408889634).to(dt).float() / (scale * 1.4426950408889634)
+    ref = _attn_ref(q, k, V, scale).transpose(1, 2).reshape(B * Tq, H * 32)
+    _close(O, ref, 2e-2 if dtype == "bf16" else 1e-5)
+
+
+def test_attention_large_score_range(gpu_device):
+    """Scores spanning > 100 in log space force rescales of the running max late in the sweep."""
+    code, dt, _ = DT["bf16"]
+    B, H, T = 1, 8, 256
+    g = torch.Generator(device="cpu").manual_seed(0)
+    Q = torch.randn(B * T, 256, generator=g).to(gpu_device, dt)
+    K = torch.randn(B * T, 256, generator=g)
+    K[200:] *= 12.0                                    # late keys dominate
+    K = K.to(gpu_device, dt)
+    V = torch.randn(B, H, T, 32, generator=g).to(gpu_device, dt)
+    O = torch.zeros(B * T, 256, dtype=dt, device=gpu_device)
+    scale = 32 ** -0.5
+    assert _lib.lib().spe_debug_attention(None, code, _p(Q), 256, _p(K), 256, _p(V.transpose(-1, -2).contiguous()),
+                                          _p(O), 256, B, H, T, T, scale) == 0
+    torch.cuda.synchronize()
+    q = Q.view(B, T, H, 32).transpose(1, 2)
+    q = (q.float() * scale * 1.4426950408889634).to(dt).float() / (scale * 1.4426950408889634)
+    ref = _attn_ref(q, K.view(B, T, H, 32).transpose(1, 2), V, scale).transpose(1, 2).reshape(B * T, 256)
+    _close(O, ref, 2e-2)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+def test_layernorm(gpu_device, dtype):
+    code, dt, tol = DT[dtype]
+    M = 333
+    g = torch.Generator(device="cpu").manual_seed(1)
+    x = (torch.randn(M, 256, generator=g) * 3 + 1).to(gpu_device, dt)
+    gam = torch.randn(256, generator=g).to(gpu_device)
+    bet = torch.randn(256, generator=g).to(gpu_device)
+    out = torch.zeros(M, 256, dtype=dt, device=gpu_device)
+    out32 = torch.zeros(M, 256, device=gpu_device)
+    assert _lib.lib().spe_debug_layernorm(None, code, _p(x), _p(gam), _p(bet), _p(out), _p(out32), M, 256) == 0
+    torch.cuda.synchronize()
+    ref = F.layer_norm(x.float(), (256,), gam, bet, 1e-5)
+    _close(out32, ref, 1e-5)
+    _close(out, ref, tol)
