@@ -169,9 +169,90 @@ static void jacobi_eig(int n, double* a, double* ev, double* evec) {
 
 /* eigen-decomposition sorted by descending eigenvalue; vt[k*n + i] = component i of vector k
  * (the row layout of OpenCV's cvSVD(..., CV_SVD_U_T) on a symmetric PSD matrix). */
+/* Jacobi rotation angle for pivot (p, q); identity when a_pq vanishes */
+static void jacobi_cs(double app, double aqq, double apq, double* c, double* s) {
+  if (fabs(apq) < 1e-300) { *c = 1.0; *s = 0.0; return; }
+  double theta = (aqq - app) / (2 * apq);
+  double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1));
+  *c = 1 / sqrt(t * t + 1);
+  *s = t * *c;
+}
+
+/* round r of the 12-player round-robin: 6 disjoint pivot pairs (p < q) covering 0..11 */
+static void rr_pairs(int r, int* P, int* Q) {
+  int a = 11, b = r;
+  P[0] = b < a ? b : a; Q[0] = b < a ? a : b;
+  for (int i = 1; i < 6; ++i) {
+    a = (r + i) % 11; b = (r + 11 - i) % 11;
+    P[i] = a < b ? a : b; Q[i] = a < b ? b : a;
+  }
+}
+
+/* Round-parallel cyclic Jacobi for the 12x12 EPnP normal matrix M^T M: the 6 rotations of a
+ * round are computed from one snapshot and applied as a column pass then a row pass.  This
+ * is the order the device solver runs with 64 lanes cooperating (csrc/pnp.hip), and the
+ * sequential form here performs exactly the same IEEE operations.  evec: column k = vector k. */
+static void jacobi12_rr(double* a, double* ev, double* evec) {
+  const int n = 12;
+  double tmp[144];
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) evec[i * n + j] = (i == j);
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    double off = 0, diag = 0;
+    for (int i = 0; i < n; ++i) {
+      diag += a[i * n + i] * a[i * n + i];
+      for (int j = i + 1; j < n; ++j) off += a[i * n + j] * a[i * n + j];
+    }
+    if (off <= 1e-30 * diag || off == 0) break;
+    for (int r = 0; r < 11; ++r) {
+      int P[6], Q[6];
+      double C[6], S[6];
+      rr_pairs(r, P, Q);
+      for (int k = 0; k < 6; ++k) jacobi_cs(a[P[k] * n + P[k]], a[Q[k] * n + Q[k]], a[P[k] * n + Q[k]], &C[k], &S[k]);
+      memcpy(tmp, a, sizeof tmp);
+      for (int k = 0; k < 6; ++k)
+        for (int i = 0; i < n; ++i) {
+          const double x = a[i * n + P[k]], y = a[i * n + Q[k]];
+          tmp[i * n + P[k]] = C[k] * x - S[k] * y;
+          tmp[i * n + Q[k]] = S[k] * x + C[k] * y;
+        }
+      for (int k = 0; k < 6; ++k)
+        for (int j = 0; j < n; ++j) {
+          const double x = tmp[P[k] * n + j], y = tmp[Q[k] * n + j];
+          a[P[k] * n + j] = C[k] * x - S[k] * y;
+          a[Q[k] * n + j] = S[k] * x + C[k] * y;
+        }
+      for (int k = 0; k < 6; ++k)
+        for (int i = 0; i < n; ++i) {
+          const double x = evec[i * n + P[k]], y = evec[i * n + Q[k]];
+          evec[i * n + P[k]] = C[k] * x - S[k] * y;
+          evec[i * n + Q[k]] = S[k] * x + C[k] * y;
+        }
+    }
+  }
+  for (int i = 0; i < n; ++i) ev[i] = a[i * n + i];
+}
+
+/* sort an eigen-decomposition by descending eigenvalue into vt rows (stable insertion sort) */
+static void eig_sort_desc(int n, const double* ev, const double* evec, double* w, double* vt) {
+  int idx[12];
+  for (int i = 0; i < n; ++i) idx[i] = i;
+  for (int i = 1; i < n; ++i)
+    for (int j = i; j > 0 && ev[idx[j - 1]] < ev[idx[j]]; --j) { int t = idx[j]; idx[j] = idx[j - 1]; idx[j - 1] = t; }
+  for (int k = 0; k < n; ++k) {
+    w[k] = ev[idx[k]];
+    for (int i = 0; i < n; ++i) vt[k * n + i] = evec[i * n + idx[k]];
+  }
+}
+
 static void sym_eig_desc(int n, const double* A, double* w, double* vt) {
   double a[144], ev[12], evec[144];
   memcpy(a, A, sizeof(double) * n * n);
+  if (n == 12) {
+    jacobi12_rr(a, ev, evec);
+    eig_sort_desc(n, ev, evec, w, vt);
+    return;
+  }
   jacobi_eig(n, a, ev, evec);
   int idx[12];
   for (int i = 0; i < n; ++i) idx[i] = i;
@@ -751,31 +832,53 @@ static void epnp_gauss_newton(const double* L, const double* rho, double* betas)
 }
 
 /* EPnP pose from n >= 4 correspondences (pixel points given as double, OpenCV us[] convention) */
+/* EPnP in three stages (setup -> M^T M + 12x12 eigen-decomposition -> betas / pose) so the
+ * device solver can run the middle stage with a whole wave (csrc/pnp.hip) on the same math. */
+static void epnp_setup(epnp_t* e, const cam_t* k, int n, const double* wld, const double* img_norm) {
+  e->n = n;
+  e->fu = k->fx; e->fv = k->fy; e->uc = k->cx; e->vc = k->cy;
+  for (int i = 0; i < n; ++i) {
+    for (int j = 0; j < 3; ++j) e->pws[3 * i + j] = wld[3 * i + j];
+    e->us[2 * i] = img_norm[2 * i] * e->fu + e->uc;
+    e->us[2 * i + 1] = img_norm[2 * i + 1] * e->fv + e->vc;
+  }
+  epnp_control_points(e);
+  epnp_barycentric(e);
+}
+
+/* one entry (a, b) of M^T M, accumulated over the correspondences in order */
+static double epnp_mtm_entry(const epnp_t* e, int a, int b) {
+  double acc = 0;
+  for (int i = 0; i < e->n; ++i) {
+    const double* as = e->alphas + 4 * i;
+    const double u = e->us[2 * i], v = e->us[2 * i + 1];
+    const int ja = a / 3, ca = a % 3, jb = b / 3, cb = b % 3;
+    const double m1a = ca == 0 ? as[ja] * e->fu : (ca == 1 ? 0.0 : as[ja] * (e->uc - u));
+    const double m1b = cb == 0 ? as[jb] * e->fu : (cb == 1 ? 0.0 : as[jb] * (e->uc - u));
+    const double m2a = ca == 0 ? 0.0 : (ca == 1 ? as[ja] * e->fv : as[ja] * (e->vc - v));
+    const double m2b = cb == 0 ? 0.0 : (cb == 1 ? as[jb] * e->fv : as[jb] * (e->vc - v));
+    acc += m1a * m1b + m2a * m2b;
+  }
+  return acc;
+}
+
+static void epnp_finish(epnp_t* e, const double* ut, double* R, double* t);
+
 static void epnp_pose(const cam_t* k, int n, const double* wld, const double* img_norm, double* R, double* t) {
   epnp_t e;
-  e.n = n;
-  e.fu = k->fx; e.fv = k->fy; e.uc = k->cx; e.vc = k->cy;
-  for (int i = 0; i < n; ++i) {
-    for (int j = 0; j < 3; ++j) e.pws[3 * i + j] = wld[3 * i + j];
-    e.us[2 * i] = img_norm[2 * i] * e.fu + e.uc;
-    e.us[2 * i + 1] = img_norm[2 * i + 1] * e.fv + e.vc;
-  }
-  epnp_control_points(&e);
-  epnp_barycentric(&e);
-  double mtm[144] = {0};
-  for (int i = 0; i < n; ++i) {
-    double M1[12], M2[12];
-    const double* as = e.alphas + 4 * i;
-    double u = e.us[2 * i], v = e.us[2 * i + 1];
-    for (int j = 0; j < 4; ++j) {
-      M1[3 * j] = as[j] * e.fu; M1[3 * j + 1] = 0.0; M1[3 * j + 2] = as[j] * (e.uc - u);
-      M2[3 * j] = 0.0; M2[3 * j + 1] = as[j] * e.fv; M2[3 * j + 2] = as[j] * (e.vc - v);
-    }
-    for (int a = 0; a < 12; ++a)
-      for (int b = 0; b < 12; ++b) mtm[a * 12 + b] += M1[a] * M1[b] + M2[a] * M2[b];
-  }
+  epnp_setup(&e, k, n, wld, img_norm);
+  double mtm[144];
+  for (int a = 0; a < 12; ++a)
+    for (int b = 0; b < 12; ++b) mtm[a * 12 + b] = epnp_mtm_entry(&e, a, b);
   double d[12], ut[144];
   sym_eig_desc(12, mtm, d, ut);
+  epnp_finish(&e, ut, R, t);
+}
+
+static void epnp_finish(epnp_t* e_, const double* ut, double* R, double* t) {
+  epnp_t e = *e_;
+  const int n = e.n;
+  (void)n;
   const double* v[4] = {ut + 12 * 11, ut + 12 * 10, ut + 12 * 9, ut + 12 * 8};
   double dv[4][6][3];
   for (int i = 0; i < 4; ++i) {

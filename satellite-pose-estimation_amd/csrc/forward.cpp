@@ -326,8 +326,8 @@ int spe_pnp_batch(void* stream, const float* points_px, const float* probs, cons
   if (!points_px || !probs || !K || !world || !quat || !tvec || B < 0 || Q <= 0 || Q > 64 || C < 2 || C > 17)
     return fail(SPE_E_ARG, "bad argument");
   if (mode < SPE_PNP_EPNP || mode > SPE_PNP_EPNP_LM) return fail(SPE_E_ARG, "bad solver mode");
-  if (ransac_iters < 1 || ransac_iters > 256 || !(confidence > 0 && confidence < 1))
-    return fail(SPE_E_ARG, "ransac_iters must be in [1,256], confidence in (0,1)");
+  if (ransac_iters < 1 || ransac_iters > 255 || !(confidence > 0 && confidence < 1))
+    return fail(SPE_E_ARG, "ransac_iters must be in [1,255], confidence in (0,1)");
   PnpArgs a{};
   a.points = points_px; a.probs = probs; a.sigmas = sigmas;
   a.B = B; a.Q = Q; a.C = C; a.K = K; a.world = world; a.mode = mode; a.repro = repro;

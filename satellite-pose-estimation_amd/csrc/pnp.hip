@@ -11,10 +11,14 @@
 //                  its float32 inlier count is evaluated lane-parallel, then the adaptive
 //                  iteration count / best-model update is replayed in order — identical to the
 //                  serial loop because a hypothesis never depends on earlier ones.
-//   refit + refine EPnP on the consensus set (12x12 MtM eigen-decomposition, Gauss-Newton
-//                  betas), then CvLevMarq (<= 20 iters) for the REV path or the sigma-weighted
-//                  Huber LM for the UNC path; Rodrigues; Blender mat3_to_quat (float32).
+//   EPnP           wave-cooperative: M^T M entries across lanes, the 12x12 eigen-decomposition
+//                  as a round-parallel Jacobi (6 disjoint rotations per round, column pass then
+//                  row pass through LDS), betas / Gauss-Newton / pose on lane 0
+//   refine         CvLevMarq (<= 20 iters) for the REV path or the sigma-weighted Huber LM for
+//                  the UNC path; Rodrigues; Blender mat3_to_quat (float32).
 // Status codes follow the reference's exception mapping (REV/datasets/speed.py:355-363).
+// Compiled with -ffp-contract=off: together with pnp_math.h's deterministic transcendentals the
+// index outputs (correspondences, inlier sets) match oracle/pnp_ref.c bit for bit.
 #include "spe_common.h"
 #include "pnp_math.h"
 #include "spe_pnp.h"
@@ -23,6 +27,105 @@ namespace {
 
 constexpr int WAVE = 64;
 constexpr int MAXIT = 256;
+
+struct EpnpShared {
+  epnp_t e;
+  double a[144], v[144], tmp[144];
+  double c[6], s[6];
+  int P[6], Q[6], pair_of[12], is_p[12];
+  int stop;
+};
+
+// Round-parallel Jacobi on sh.a (12x12, LDS) with eigenvectors in sh.v: the same IEEE operation
+// sequence as jacobi12_rr() (pnp_math.h / oracle), with the 144 element updates spread over lanes.
+__device__ void jacobi12_rr_wave(EpnpShared& sh, int lane) {
+  for (int e = lane; e < 144; e += WAVE) sh.v[e] = (e / 12 == e % 12) ? 1.0 : 0.0;
+  __syncthreads();
+  for (int sweep = 0; sweep < 60; ++sweep) {
+    if (lane == 0) {
+      double off = 0, diag = 0;
+      for (int i = 0; i < 12; ++i) {
+        diag += sh.a[i * 12 + i] * sh.a[i * 12 + i];
+        for (int j = i + 1; j < 12; ++j) off += sh.a[i * 12 + j] * sh.a[i * 12 + j];
+      }
+      sh.stop = (off <= 1e-30 * diag || off == 0);
+    }
+    __syncthreads();
+    if (sh.stop) break;
+    for (int r = 0; r < 11; ++r) {
+      if (lane < 6) {
+        int P[6], Q[6];
+        rr_pairs(r, P, Q);
+        const int p = P[lane], q = Q[lane];
+        double c, s;
+        jacobi_cs(sh.a[p * 12 + p], sh.a[q * 12 + q], sh.a[p * 12 + q], &c, &s);
+        sh.c[lane] = c; sh.s[lane] = s; sh.P[lane] = p; sh.Q[lane] = q;
+        sh.pair_of[p] = lane; sh.pair_of[q] = lane;
+        sh.is_p[p] = 1; sh.is_p[q] = 0;
+      }
+      __syncthreads();
+      double vnew[3];
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        const int e = lane + WAVE * t;
+        if (e < 144) {
+          const int i = e / 12, j = e % 12, kk = sh.pair_of[j];
+          const double c = sh.c[kk], s = sh.s[kk];
+          const double x = sh.a[i * 12 + sh.P[kk]], y = sh.a[i * 12 + sh.Q[kk]];
+          sh.tmp[e] = sh.is_p[j] ? c * x - s * y : s * x + c * y;
+          const double vx = sh.v[i * 12 + sh.P[kk]], vy = sh.v[i * 12 + sh.Q[kk]];
+          vnew[t] = sh.is_p[j] ? c * vx - s * vy : s * vx + c * vy;
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int t = 0; t < 3; ++t) {
+        const int e = lane + WAVE * t;
+        if (e < 144) {
+          const int i = e / 12, j = e % 12, kk = sh.pair_of[i];
+          const double c = sh.c[kk], s = sh.s[kk];
+          const double x = sh.tmp[sh.P[kk] * 12 + j], y = sh.tmp[sh.Q[kk] * 12 + j];
+          sh.a[e] = sh.is_p[i] ? c * x - s * y : s * x + c * y;
+          sh.v[e] = vnew[t];
+        }
+      }
+      __syncthreads();
+    }
+  }
+}
+
+// solvePnPGeneric(EPNP) on the correspondences selected by `mask` (all lanes call; the pose is
+// valid on lane 0).  img_is_float: round the undistorted coordinates to float32 (OpenCV keeps
+// the input depth: float inputs on the direct path, double on the RANSAC refit).
+__device__ void epnp_solve_wave(EpnpShared& sh, const cam_t* k, const float* img_f, const float* wld_f, int nl,
+                                uint32_t mask, int img_is_float, double* rvec, double* tvec, int lane) {
+  if (lane == 0) {
+    double wd[3 * MAXN], nrm[2 * MAXN];
+    int m = 0;
+    for (int i = 0; i < nl; ++i)
+      if (mask & (1u << i)) {
+        for (int c = 0; c < 3; ++c) wd[3 * m + c] = wld_f[3 * i + c];
+        double un = ((double)img_f[2 * i] - k->cx) * (1. / k->fx);
+        double vn = ((double)img_f[2 * i + 1] - k->cy) * (1. / k->fy);
+        if (img_is_float) { un = (float)un; vn = (float)vn; }
+        nrm[2 * m] = un; nrm[2 * m + 1] = vn;
+        m++;
+      }
+    epnp_setup(&sh.e, k, m, wd, nrm);
+  }
+  __syncthreads();
+  for (int e = lane; e < 144; e += WAVE) sh.a[e] = epnp_mtm_entry(&sh.e, e / 12, e % 12);
+  __syncthreads();
+  jacobi12_rr_wave(sh, lane);
+  if (lane == 0) {
+    double ev[12], w[12], ut[144], R[9];
+    for (int i = 0; i < 12; ++i) ev[i] = sh.a[i * 12 + i];
+    eig_sort_desc(12, ev, sh.v, w, ut);
+    epnp_finish(&sh.e, ut, R, tvec);
+    rodrigues_R2r(R, rvec);
+  }
+  __syncthreads();
+}
 
 __global__ __launch_bounds__(WAVE) void pnp_kernel(PnpArgs a) {
   const int b = blockIdx.x;
@@ -35,6 +138,7 @@ __global__ __launch_bounds__(WAVE) void pnp_kernel(PnpArgs a) {
   __shared__ int s_ok[MAXIT], s_good[MAXIT];
   __shared__ uint32_t s_mask[MAXIT];
   __shared__ double s_rt[MAXIT][6];
+  __shared__ EpnpShared s_ep;
 
   const cam_t k = {a.K[0], a.K[4], a.K[2], a.K[5]};
   const int Q = a.Q, C = a.C;
@@ -72,6 +176,7 @@ __global__ __launch_bounds__(WAVE) void pnp_kernel(PnpArgs a) {
   }
   __syncthreads();
   const int nl = s_nl;
+  const uint32_t all = nl >= 32 ? 0xffffffffu : ((1u << nl) - 1);
 
   double rvec[3] = {0, 0, 0}, t[3] = {0, 0, 0};
   int status = SPE_PNP_OK;
@@ -83,38 +188,31 @@ __global__ __launch_bounds__(WAVE) void pnp_kernel(PnpArgs a) {
   } else if (nl < 4) {
     status = SPE_PNP_CV_ERROR;
   } else if (a.mode == SPE_PNP_EPNP || a.mode == SPE_PNP_EPNP_LM) {
-    if (lane == 0) {
+    epnp_solve_wave(s_ep, &k, s_img, s_wld, nl, all, 1, rvec, t, lane);
+    if (lane == 0 && a.mode == SPE_PNP_EPNP_LM) {
       double wd[3 * MAXN], id[2 * MAXN];
       for (int i = 0; i < 3 * nl; ++i) wd[i] = s_wld[i];
       for (int i = 0; i < 2 * nl; ++i) id[i] = s_img[i];
-      epnp_solve(&k, nl, wd, id, 1, rvec, t);
-      if (a.mode == SPE_PNP_EPNP_LM) lm_refine(&k, nl, wd, id, rvec, t);
-      inl = (nl >= 32) ? 0xffffffffu : ((1u << nl) - 1);
-      have_pose = true;
+      lm_refine(&k, nl, wd, id, rvec, t);
     }
+    inl = all;
+    have_pose = true;
   } else {
     const int kernel = (a.mode == SPE_PNP_RANSAC_P3P_LM || nl == 4) ? 0 : 1;
     const int mp = kernel == 0 ? 4 : 5;
     bool ok = false;
     if (nl == mp) {
       // model_points == npoints: direct solve on all points (solvepnp.cpp)
-      if (lane == 0) {
-        if (kernel == 0) {
-          ok = p3p_solve4(&k, s_img, s_wld, rvec, t) != 0;
-        } else {
-          double wd[15], id[10];
-          for (int i = 0; i < 15; ++i) wd[i] = s_wld[i];
-          for (int i = 0; i < 10; ++i) id[i] = s_img[i];
-          epnp_solve(&k, 5, wd, id, 1, rvec, t);
-          ok = true;
-        }
-        s_ok[0] = ok;
-        s_mask[0] = (1u << nl) - 1;
+      if (kernel == 0) {
+        if (lane == 0) s_ok[0] = p3p_solve4(&k, s_img, s_wld, rvec, t) != 0;
+      } else {
+        epnp_solve_wave(s_ep, &k, s_img, s_wld, nl, all, 1, rvec, t, lane);
+        if (lane == 0) s_ok[0] = 1;
       }
       __syncthreads();
       ok = s_ok[0];
       if (!ok) status = SPE_PNP_UNPINNED;
-      inl = s_mask[0];
+      inl = all;
     } else {
       const int iters = a.ransac_iters < MAXIT ? a.ransac_iters : MAXIT;
       // 1. subset stream of cv::RNG((uint64)-1), drawn in order
@@ -171,7 +269,7 @@ __global__ __launch_bounds__(WAVE) void pnp_kernel(PnpArgs a) {
         for (int c = 0; c < 3; ++c) { s_rt[it][c] = r[c]; s_rt[it][3 + c] = tt[c]; }
       }
       __syncthreads();
-      // 3. serial replay of the adaptive loop; refit + refine on lane 0
+      // 3. serial replay of the adaptive loop (lane 0)
       if (lane == 0) {
         int niters = iters > 1 ? iters : 1, maxGood = 0, best = -1, last = -1;
         for (int it = 0; it < niters; ++it) {
@@ -184,30 +282,24 @@ __global__ __launch_bounds__(WAVE) void pnp_kernel(PnpArgs a) {
           }
         }
         if (maxGood > 0) {
-          inl = s_mask[best];
-          double wd[3 * MAXN], id[2 * MAXN];
-          int m = 0;
-          for (int i = 0; i < nl; ++i)
-            if (inl & (1u << i)) {
-              for (int c = 0; c < 3; ++c) wd[3 * m + c] = s_wld[3 * i + c];
-              id[2 * m] = s_img[2 * i]; id[2 * m + 1] = s_img[2 * i + 1];
-              m++;
-            }
-          epnp_solve(&k, m, wd, id, 0, rvec, t);
-          s_ok[0] = 1;
+          s_mask[MAXIT - 1] = s_mask[best];
+          s_ok[MAXIT - 1] = 1;
         } else if (last >= 0) {
           for (int c = 0; c < 3; ++c) { rvec[c] = s_rt[last][c]; t[c] = s_rt[last][3 + c]; }
-          s_ok[0] = 2;
+          s_ok[MAXIT - 1] = 2;
         } else {
-          s_ok[0] = 0;
+          s_ok[MAXIT - 1] = 0;
         }
-        s_mask[0] = inl;
       }
       __syncthreads();
-      ok = s_ok[0] == 1;
-      if (s_ok[0] == 2) status = SPE_PNP_RANSAC_FALLBACK;
-      if (s_ok[0] == 0) status = SPE_PNP_UNPINNED;
-      inl = s_mask[0];
+      const int verdict = s_ok[MAXIT - 1];
+      ok = verdict == 1;
+      if (ok) {
+        inl = s_mask[MAXIT - 1];
+        epnp_solve_wave(s_ep, &k, s_img, s_wld, nl, inl, 0, rvec, t, lane);   // refit on the consensus set
+      }
+      if (verdict == 2) status = SPE_PNP_RANSAC_FALLBACK;
+      if (verdict == 0) status = SPE_PNP_UNPINNED;
     }
     if (ok && lane == 0) {
       double wi[3 * MAXN], ii[2 * MAXN], sg[2 * MAXN];
@@ -267,7 +359,7 @@ __global__ void score_kernel(const float* __restrict__ quat, const double* __res
 
 int spe_launch_pnp(const PnpArgs& a, hipStream_t s) {
   if (a.B <= 0) return 0;
-  if (a.Q > WAVE || a.C < 2 || a.C - 1 > MAXN) return -7;
+  if (a.Q > WAVE || a.C < 2 || a.C - 1 > MAXN || a.ransac_iters > MAXIT - 1) return -7;
   hipLaunchKernelGGL(pnp_kernel, dim3(a.B), dim3(WAVE), 0, s, a);
   return (int)hipGetLastError();
 }

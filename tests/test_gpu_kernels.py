@@ -56,9 +56,10 @@ def test_gemm_linear_epilogue(gpu_device, dtype, M, N, K):
     ldb = (K + 63) // 64 * 64
     Wp = _padded_weight(Wt, ldb, dt)
     bias = torch.randn(N, generator=g).to(gpu_device)
-    R = torch.randn(M, N + 8, generator=g).to(gpu_device, dt)
-    C = torch.zeros(M, N + 8, dtype=dt, device=gpu_device)
-    _gemm(dtype, 0, A, Wp, M, N, K, K, ldb, C, N + 8, bias=bias, R=R, ldr=N + 8, relu=1)
+    ld = (N + 8 + 7) // 8 * 8                          # row strides must keep 16-byte alignment
+    R = torch.randn(M, ld, generator=g).to(gpu_device, dt)
+    C = torch.zeros(M, ld, dtype=dt, device=gpu_device)
+    _gemm(dtype, 0, A, Wp, M, N, K, K, ldb, C, ld, bias=bias, R=R, ldr=ld, relu=1)
     ref = torch.relu(A.float() @ Wt.float().t() + bias + R[:, :N].float())
     _close(C[:, :N], ref, tol)
     assert (C[:, N:] == 0).all()                       # nothing written past N
@@ -94,9 +95,10 @@ def test_gemm_conv_nhwc(gpu_device, dtype, B, H, W, Cin, Cout, k, s, p):
     ldb = (K + 63) // 64 * 64
     Wp = _padded_weight(w.permute(0, 2, 3, 1).reshape(Cout, K), ldb, dt)
     xn = x.permute(0, 2, 3, 1).contiguous()
-    C = torch.zeros(B * Ho * Wo, Cout, dtype=dt, device=gpu_device)
-    _gemm(dtype, 2, xn, Wp, B * Ho * Wo, Cout, K, 0, ldb, C, Cout, bias=bias, conv=(H, W, Cin, k, k, s, p))
-    _close(C, ref.permute(0, 2, 3, 1).reshape(-1, Cout), tol)
+    ldc = (Cout + 7) // 8 * 8
+    C = torch.zeros(B * Ho * Wo, ldc, dtype=dt, device=gpu_device)
+    _gemm(dtype, 2, xn, Wp, B * Ho * Wo, Cout, K, 0, ldb, C, ldc, bias=bias, conv=(H, W, Cin, k, k, s, p))
+    _close(C[:, :Cout], ref.permute(0, 2, 3, 1).reshape(-1, Cout), tol)
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "fp32"])
