@@ -68,6 +68,25 @@ GemmArgs linear_args(const Conv& c, const void* A, int lda, int M, void* C, int 
   return g;
 }
 
+// Fused linear1 -> ReLU -> linear2 -> +residual -> LayerNorm over x (in place), bf16 models.
+int run_ffn(spe_model* m, const char* kind, const Conv& l1, const Conv& l2, const float* g, const float* b,
+            void* x, int M, hipStream_t s) {
+  FfnArgs a{};
+  a.x = x; a.ldx = l1.K;
+  a.w1 = l1.w; a.ld1 = l1.Kpad; a.b1 = l1.bias;
+  a.w2 = l2.w; a.ld2 = l2.Kpad; a.b2 = l2.bias;
+  a.gamma = g; a.beta = b;
+  a.y = x; a.ldy = l1.K;
+  a.M = M; a.D = l1.K; a.F = l1.N;
+  const double flops = 4.0 * M * (double)l1.K * l1.N;
+  const double bytes = 2.0 * M * l1.K * m->esz + 2.0 * (double)l1.K * l1.N * m->esz;
+  return run_other(m, kind, flops, bytes, s, [&] { return spe_launch_ffn_ln(a, s); });
+}
+
+bool use_fused_ffn(const spe_model* m) {
+  return m->cfg.dtype == SPE_DTYPE_BF16 && m->cfg.hidden_dim == 256 && m->cfg.dim_feedforward % 32 == 0;
+}
+
 GemmArgs conv_args(const Conv& c, const void* X, int B, int H, int W, void* Y, int ldc) {
   GemmArgs g{};
   g.A = X;
@@ -210,17 +229,21 @@ int spe_forward(spe_model* m, void* stream, const float* images, int B, void* wo
       CK(run_gemm(m, "gemm.enc.o", g, GEMM_LINEAR, s));
     }
     CK(run_other(m, "ln.enc", 0.0, (double)Mt * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.tmp), e.n1g, e.n1b, P(w.src), nullptr, Mt, d, dt, s); }));
-    {
-      GemmArgs g = linear_args(e.l1, P(w.src), d, Mt, P(w.ffn), ff);
-      g.relu = 1;
-      CK(run_gemm(m, "gemm.enc.ffn1", g, GEMM_LINEAR, s));
+    if (use_fused_ffn(m)) {
+      CK(run_ffn(m, "ffn.enc", e.l1, e.l2, e.n2g, e.n2b, P(w.src), Mt, s));
+    } else {
+      {
+        GemmArgs g = linear_args(e.l1, P(w.src), d, Mt, P(w.ffn), ff);
+        g.relu = 1;
+        CK(run_gemm(m, "gemm.enc.ffn1", g, GEMM_LINEAR, s));
+      }
+      {
+        GemmArgs g = linear_args(e.l2, P(w.ffn), ff, Mt, P(w.tmp), d);
+        g.R = P(w.src); g.ldr = d;
+        CK(run_gemm(m, "gemm.enc.ffn2", g, GEMM_LINEAR, s));
+      }
+      CK(run_other(m, "ln.enc", 0.0, (double)Mt * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.tmp), e.n2g, e.n2b, P(w.src), nullptr, Mt, d, dt, s); }));
     }
-    {
-      GemmArgs g = linear_args(e.l2, P(w.ffn), ff, Mt, P(w.tmp), d);
-      g.R = P(w.src); g.ldr = d;
-      CK(run_gemm(m, "gemm.enc.ffn2", g, GEMM_LINEAR, s));
-    }
-    CK(run_other(m, "ln.enc", 0.0, (double)Mt * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.tmp), e.n2g, e.n2b, P(w.src), nullptr, Mt, d, dt, s); }));
   }
   // memory = src.  Cross-attention K (memory + pos) and V^T (memory) for all decoder layers.
   {
@@ -284,17 +307,21 @@ int spe_forward(spe_model* m, void* stream, const float* images, int B, void* wo
       CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR, s));
     }
     CK(run_other(m, "ln.dec", 0.0, (double)Mq * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.dtmp), e.n2g, e.n2b, P(w.tgt), nullptr, Mq, d, dt, s); }));
-    {
-      GemmArgs g = linear_args(e.l1, P(w.tgt), d, Mq, P(w.dffn), ff);
-      g.relu = 1;
-      CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR, s));
+    if (use_fused_ffn(m)) {
+      CK(run_ffn(m, "ffn.dec", e.l1, e.l2, e.n3g, e.n3b, P(w.tgt), Mq, s));
+    } else {
+      {
+        GemmArgs g = linear_args(e.l1, P(w.tgt), d, Mq, P(w.dffn), ff);
+        g.relu = 1;
+        CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR, s));
+      }
+      {
+        GemmArgs g = linear_args(e.l2, P(w.dffn), ff, Mq, P(w.dtmp), d);
+        g.R = P(w.tgt); g.ldr = d;
+        CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR, s));
+      }
+      CK(run_other(m, "ln.dec", 0.0, (double)Mq * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.dtmp), e.n3g, e.n3b, P(w.tgt), nullptr, Mq, d, dt, s); }));
     }
-    {
-      GemmArgs g = linear_args(e.l2, P(w.dffn), ff, Mq, P(w.dtmp), d);
-      g.R = P(w.tgt); g.ldr = d;
-      CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR, s));
-    }
-    CK(run_other(m, "ln.dec", 0.0, (double)Mq * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.dtmp), e.n3g, e.n3b, P(w.tgt), nullptr, Mq, d, dt, s); }));
   }
   float* hs = out->hs ? out->hs : (float*)P(w.hs);
   CK(run_other(m, "ln.dec", 0.0, (double)Mq * d * (m->esz + 4), s, [&] { return spe_launch_layernorm(P(w.tgt), m->dng, m->dnb, nullptr, hs, Mq, d, dt, s); }));

@@ -30,7 +30,8 @@ constexpr int MAXIT = 256;
 
 struct EpnpShared {
   epnp_t e;
-  double a[144], v[144], tmp[144];
+  double a[144], v[144], tmp[144], ut[144];
+  double L[60], rho[6], err[4], Rs[4][9], ts[4][3];
   double c[6], s[6];
   int P[6], Q[6], pair_of[12], is_p[12];
   int stop;
@@ -118,11 +119,19 @@ __device__ void epnp_solve_wave(EpnpShared& sh, const cam_t* k, const float* img
   __syncthreads();
   jacobi12_rr_wave(sh, lane);
   if (lane == 0) {
-    double ev[12], w[12], ut[144], R[9];
+    double ev[12], w[12];
     for (int i = 0; i < 12; ++i) ev[i] = sh.a[i * 12 + i];
-    eig_sort_desc(12, ev, sh.v, w, ut);
-    epnp_finish(&sh.e, ut, R, tvec);
-    rodrigues_R2r(R, rvec);
+    eig_sort_desc(12, ev, sh.v, w, sh.ut);
+    epnp_L_rho(&sh.e, sh.ut, sh.L, sh.rho);
+  }
+  __syncthreads();
+  if (lane >= 1 && lane <= 3)   // the three beta approximations (epnp_finish) on three lanes
+    sh.err[lane] = epnp_approx(&sh.e, sh.ut, sh.L, sh.rho, lane, sh.Rs[lane], sh.ts[lane]);
+  __syncthreads();
+  if (lane == 0) {
+    const int N = epnp_pick(sh.err);
+    for (int i = 0; i < 3; ++i) tvec[i] = sh.ts[N][i];
+    rodrigues_R2r(sh.Rs[N], rvec);
   }
   __syncthreads();
 }

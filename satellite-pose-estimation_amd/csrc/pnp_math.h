@@ -852,10 +852,9 @@ PNP_FN void epnp_pose(const cam_t* k, int n, const double* wld, const double* im
   epnp_finish(&e, ut, R, t);
 }
 
-PNP_FN void epnp_finish(epnp_t* e_, const double* ut, double* R, double* t) {
-  epnp_t e = *e_;
-  const int n = e.n;
-  (void)n;
+/* L_6x10 and rho from the four null-space vectors (OpenCV compute_L_6x10 / compute_rho) */
+PNP_FN void epnp_L_rho(const epnp_t* ep, const double* ut, double* L, double* rho) {
+  const double(*cws)[3] = ep->cws;
   const double* v[4] = {ut + 12 * 11, ut + 12 * 10, ut + 12 * 9, ut + 12 * 8};
   double dv[4][6][3];
   for (int i = 0; i < 4; ++i) {
@@ -866,7 +865,6 @@ PNP_FN void epnp_finish(epnp_t* e_, const double* ut, double* R, double* t) {
       if (b > 3) { a++; b = a + 1; }
     }
   }
-  double L[60], rho[6];
   for (int i = 0; i < 6; ++i) {
     double* row = L + 10 * i;
     row[0] = dot3(dv[0][i], dv[0][i]);
@@ -880,49 +878,59 @@ PNP_FN void epnp_finish(epnp_t* e_, const double* ut, double* R, double* t) {
     row[8] = 2.0f * dot3(dv[2][i], dv[3][i]);
     row[9] = dot3(dv[3][i], dv[3][i]);
   }
-  rho[0] = dist2(e.cws[0], e.cws[1]); rho[1] = dist2(e.cws[0], e.cws[2]); rho[2] = dist2(e.cws[0], e.cws[3]);
-  rho[3] = dist2(e.cws[1], e.cws[2]); rho[4] = dist2(e.cws[1], e.cws[3]); rho[5] = dist2(e.cws[2], e.cws[3]);
+  rho[0] = dist2(cws[0], cws[1]); rho[1] = dist2(cws[0], cws[2]); rho[2] = dist2(cws[0], cws[3]);
+  rho[3] = dist2(cws[1], cws[2]); rho[4] = dist2(cws[1], cws[3]); rho[5] = dist2(cws[2], cws[3]);
+}
 
-  double betas[4][4] = {{0}}, err[4] = {0}, Rs[4][9], ts[4][3];
-  { /* approx 1: [B11 B12 B13 B14] */
+/* beta approximation `which` (1: [B11 B12 B13 B14], 2: [B11 B12 B22], 3: [B11 B12 B22 B13 B23]),
+ * Gauss-Newton refinement, pose and mean reprojection error.  The three are independent, so the
+ * device solver runs them on three lanes. */
+PNP_FN double epnp_approx(const epnp_t* e0, const double* ut, const double* L, const double* rho, int which, double* R,
+                          double* t) {
+  epnp_t e = *e0;
+  double bb[4] = {0, 0, 0, 0};
+  if (which == 1) {
     double A[24], x[4];
     for (int i = 0; i < 6; ++i) { A[i * 4] = L[10 * i]; A[i * 4 + 1] = L[10 * i + 1]; A[i * 4 + 2] = L[10 * i + 3]; A[i * 4 + 3] = L[10 * i + 6]; }
     lstsq_pinv(6, 4, A, rho, x);
-    double* bb = betas[1];
     if (x[0] < 0) { bb[0] = sqrt(-x[0]); bb[1] = -x[1] / bb[0]; bb[2] = -x[2] / bb[0]; bb[3] = -x[3] / bb[0]; }
     else { bb[0] = sqrt(x[0]); bb[1] = x[1] / bb[0]; bb[2] = x[2] / bb[0]; bb[3] = x[3] / bb[0]; }
-    epnp_gauss_newton(L, rho, bb);
-    err[1] = epnp_R_and_t(&e, ut, bb, Rs[1], ts[1]);
-  }
-  { /* approx 2: [B11 B12 B22] */
+  } else if (which == 2) {
     double A[18], x[3];
     for (int i = 0; i < 6; ++i) { A[i * 3] = L[10 * i]; A[i * 3 + 1] = L[10 * i + 1]; A[i * 3 + 2] = L[10 * i + 2]; }
     lstsq_pinv(6, 3, A, rho, x);
-    double* bb = betas[2];
     if (x[0] < 0) { bb[0] = sqrt(-x[0]); bb[1] = (x[2] < 0) ? sqrt(-x[2]) : 0.0; }
     else { bb[0] = sqrt(x[0]); bb[1] = (x[2] > 0) ? sqrt(x[2]) : 0.0; }
     if (x[1] < 0) bb[0] = -bb[0];
     bb[2] = 0.0; bb[3] = 0.0;
-    epnp_gauss_newton(L, rho, bb);
-    err[2] = epnp_R_and_t(&e, ut, bb, Rs[2], ts[2]);
-  }
-  { /* approx 3: [B11 B12 B22 B13 B23] */
+  } else {
     double A[30], x[5];
     for (int i = 0; i < 6; ++i)
       for (int c = 0; c < 5; ++c) A[i * 5 + c] = L[10 * i + c];
     lstsq_pinv(6, 5, A, rho, x);
-    double* bb = betas[3];
     if (x[0] < 0) { bb[0] = sqrt(-x[0]); bb[1] = (x[2] < 0) ? sqrt(-x[2]) : 0.0; }
     else { bb[0] = sqrt(x[0]); bb[1] = (x[2] > 0) ? sqrt(x[2]) : 0.0; }
     if (x[1] < 0) bb[0] = -bb[0];
     bb[2] = x[3] / bb[0];
     bb[3] = 0.0;
-    epnp_gauss_newton(L, rho, bb);
-    err[3] = epnp_R_and_t(&e, ut, bb, Rs[3], ts[3]);
   }
+  epnp_gauss_newton(L, rho, bb);
+  return epnp_R_and_t(&e, ut, bb, R, t);
+}
+
+/* OpenCV's choice among the three: N = 1; if err2 < err1 N = 2; if err3 < errN N = 3 */
+PNP_FN int epnp_pick(const double* err /* [1..3] */) {
   int N = 1;
   if (err[2] < err[1]) N = 2;
   if (err[3] < err[N]) N = 3;
+  return N;
+}
+
+PNP_FN void epnp_finish(epnp_t* e, const double* ut, double* R, double* t) {
+  double L[60], rho[6], err[4] = {0, 0, 0, 0}, Rs[4][9], ts[4][3];
+  epnp_L_rho(e, ut, L, rho);
+  for (int w = 1; w <= 3; ++w) err[w] = epnp_approx(e, ut, L, rho, w, Rs[w], ts[w]);
+  const int N = epnp_pick(err);
   memcpy(R, Rs[N], sizeof(double) * 9);
   memcpy(t, ts[N], sizeof(double) * 3);
 }

@@ -32,6 +32,20 @@ struct AttnArgs {
 };
 int spe_launch_attention(const AttnArgs& a, int dtype, hipStream_t s);
 
+// Fused FFN + residual + LayerNorm (bf16 only): y = LN(x + W2 relu(W1 x + b1) + b2).
+// x / y may alias (each block reads and writes only its own rows).
+struct FfnArgs {
+  const void* x; int ldx;          // [M][256] bf16 (input and residual)
+  const void* w1; int ld1;         // [F][ld1] bf16 (linear1.weight, K padded)
+  const float* b1;                 // [F]
+  const void* w2; int ld2;         // [256][ld2] bf16 (linear2.weight)
+  const float* b2;                 // [256]
+  const float* gamma; const float* beta;   // LayerNorm affine [256]
+  void* y; int ldy;                // [M][256] bf16
+  int M, D, F;
+};
+int spe_launch_ffn_ln(const FfnArgs& a, hipStream_t s);
+
 int spe_launch_pack_input(const float* img, void* out, int B, int S, int dtype, hipStream_t s);
 int spe_launch_maxpool3s2(const void* in, void* out, int B, int H, int W, int C, int Ho, int Wo,
                           int dtype, hipStream_t s);

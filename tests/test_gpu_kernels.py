@@ -11,6 +11,7 @@ import numpy as np
 import pytest
 import torch
 import torch.nn.functional as F
+import torch.nn.functional as F_
 
 from spe import _lib
 
@@ -164,6 +165,33 @@ def test_attention_large_score_range(gpu_device):
     q = (q.float() * scale * 1.4426950408889634).to(dt).float() / (scale * 1.4426950408889634)
     ref = _attn_ref(q, K.view(B, T, H, 32).transpose(1, 2), V, scale).transpose(1, 2).reshape(B * T, 256)
     _close(O, ref, 2e-2)
+
+
+@pytest.mark.parametrize("M,F,inplace", [(333, 2048, True), (128, 64, False), (1000, 2048, False), (5, 32, True)])
+def test_fused_ffn(gpu_device, M, F, inplace):
+    """bf16 fused linear1 -> ReLU -> linear2 -> +x -> LayerNorm against torch fp32 on bf16-rounded
+    operands; the hidden activation is rounded to bf16 on chip exactly as the unfused path stores it."""
+    dt, D = torch.bfloat16, 256
+    g = torch.Generator(device="cpu").manual_seed(M + F)
+    ld = D + 8 if not inplace else D
+    x = (torch.randn(M, ld, generator=g) * 2).to(gpu_device, dt)
+    w1 = (torch.randn(F, D, generator=g) / D ** 0.5).to(gpu_device, dt)
+    b1 = (torch.randn(F, generator=g) * 0.1).to(gpu_device)
+    w2 = (torch.randn(D, F, generator=g) / F ** 0.5).to(gpu_device, dt)
+    b2 = (torch.randn(D, generator=g) * 0.1).to(gpu_device)
+    gam = (torch.randn(D, generator=g) * 0.5 + 1).to(gpu_device)
+    bet = (torch.randn(D, generator=g) * 0.1).to(gpu_device)
+    xs = x[:, :D].float()
+    h = torch.relu(xs @ w1.float().t() + b1).to(dt).float()
+    ref = F_.layer_norm(xs + h @ w2.float().t() + b2, (D,), gam, bet, 1e-5)
+    y = x if inplace else torch.full((M, ld), 7.0, dtype=dt, device=gpu_device)
+    rc = _lib.lib().spe_debug_ffn(None, _p(x), ld, _p(w1), D, _p(b1), _p(w2), F, _p(b2), _p(gam), _p(bet), _p(y), ld,
+                                  M, D, F)
+    assert rc == 0, _lib.lib().spe_last_error()
+    torch.cuda.synchronize()
+    _close(y[:, :D], ref, 3e-2)
+    if not inplace:
+        assert (y[:, D:] == 7.0).all()                 # nothing written past D
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "fp32"])
