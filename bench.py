@@ -41,6 +41,8 @@ def parse():
                         "correspondences like a trained model (spe.synthetic.bench_weights)")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--launch-table", default=None,
+                   help="write every launch of the profiled step (kind, ms, flops, bytes, roofline floor) as JSON")
     return p.parse_args()
 
 
@@ -144,13 +146,20 @@ def main():
     tot = {}
     kb = ctypes.create_string_buffer(64)
     ms, fl, by = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+    table = []
     for i in range(n):
         L.spe_model_profile_get(model._h, i, kb, 64, ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(by))
         k = kb.value.decode()
         t = tot.setdefault(k, [0.0, 0])
         t[0] += ms.value
         t[1] += 1
+        floor_ms = 1e3 * max(fl.value / (PEAK[args.dtype]["mfma"] * 1e12), by.value / (PEAK["hbm"] * 1e9))
+        table.append({"i": i, "kind": k, "ms": ms.value, "flops": fl.value, "bytes": by.value,
+                      "floor_ms": floor_ms, "frac": floor_ms / max(ms.value, 1e-9)})
     dominant = max(tot, key=lambda k: tot[k][0])
+    if args.launch_table and rank == 0:
+        with open(args.launch_table, "w") as f:
+            json.dump(table, f, indent=0)
 
     # ---- timed region: K steps, dominant kernel bracketed with HIP events on its stream
     if world > 1:
@@ -183,7 +192,7 @@ def main():
         return
     total_images = B * world * args.steps
     avg_ms = k_ms / max(k_n, 1)
-    mfma_bound = dominant.startswith(("conv", "gemm", "attn"))
+    mfma_bound = dominant.startswith(("conv", "gemm", "attn", "ffn"))
     if mfma_bound:
         achieved = (k_fl / max(k_n, 1)) / (avg_ms * 1e-3) / 1e12
         peak = PEAK[args.dtype]["mfma"]

@@ -27,44 +27,69 @@
 namespace {
 
 constexpr int NT = 256;
-constexpr int KT = 64;                 // keys per tile
+constexpr int KT = 64;                 // keys per softmax step (and per staged tile, fp32)
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float NEG_BIG = -1.0e30f;    // finite "minus infinity" (exp2 of it underflows to 0)
+constexpr float RESCALE_SLACK = 8.0f;  // log2 units (bf16 path)
 
 // ---------------------------------------------------------------- bf16 LDS image
-// K tile: 64 rows x 64 B (4 chunks); chunk slot c ^ ((row >> 2) & 3)
-SPE_DEV int k_off_bf16(int key, int c) { return key * 64 + ((c ^ ((key >> 2) & 3)) << 4); }
-// V^T tile: 32 rows (d) x 128 B (16 units of 8 B); unit slot u ^ ((d >> 1) & 15)
-SPE_DEV int v_off_bf16(int d, int u) { return d * 128 + ((u ^ ((d >> 1) & 15)) << 3); }
+// Padded (not XOR-swizzled) rows, so every fragment read is lane base + immediate offset with
+// no per-read address VALU.  K tile: rows of 64 B + 16 B pad: the 16 keys of one ds_read_b128
+// lane group start 20 banks apart mod 64 -> 16 distinct 4-bank groups (conflict-free).
+constexpr int KROW = 80;
+SPE_DEV int k_off_bf16(int key, int c) { return key * KROW + (c << 4); }
+// V^T tile: 32 rows (d) of KT keys + 16 B pad (row = 36 dwords: the 16 rows of each
+// ds_read_b128 lane group start on distinct 4-bank groups).  Within every 16-key group the two
+// middle quads are swapped (keys 0-3, 8-11, 4-7, 12-15), which is the k order the P^T operand
+// has straight out of the S^T accumulator: each PV MFMA's A operand is ONE 16-byte read.
+constexpr int VROW = KT * 2 + 16;
+SPE_DEV int v_quad_off(int d, int quad) {            // quad = 4-key unit index within the row
+  const int g = quad >> 2, qi = quad & 3;
+  const int pos = (qi == 1) ? 2 : (qi == 2) ? 1 : qi;
+  return d * VROW + g * 32 + pos * 8;
+}
 // ---------------------------------------------------------------- fp32 LDS image
 SPE_DEV int k_off_f32(int key, int c) { return key * 128 + ((c ^ (key & 7)) << 4); }       // 8 chunks
 SPE_DEV int v_off_f32(int d, int c) { return d * 256 + ((c ^ (d & 15)) << 4); }            // 16 chunks
 
-template <typename T>
+template <typename T, int KTT>
 struct Stage {
   static constexpr int ES = sizeof(T);
-  static constexpr int KCH = 64 * 32 * ES / 16 / NT;   // K chunks per thread (1 bf16, 2 f32)
-  static constexpr int VCH = 32 * 64 * ES / 16 / NT;   // V^T chunks per thread
+  static constexpr int KCH = KTT * 32 * ES / 16 / NT;  // K chunks per thread
+  static constexpr int VCH = 32 * KTT * ES / 16 / NT;  // V^T chunks per thread
   u32x4 kr[KCH], vr[VCH];
 
   SPE_DEV void load(const AttnArgs& a, int b, int h, int kt, int tid) {
     constexpr int CE = 16 / ES;
     constexpr int KCPR = 32 / CE;     // K chunks per key row
-    constexpr int VCPR = 64 / CE;     // V^T chunks per d row
+    constexpr int VCPR = KTT / CE;    // V^T chunks per d row
     const T* kbase = (const T*)a.k + (size_t)b * a.Tk * a.ldk + h * 32;
     const T* vbase = (const T*)a.vt + (size_t)(b * a.H + h) * 32 * a.Tk;
+    if ((kt + 1) * KTT <= a.Tk && (a.Tk % CE) == 0) {     // whole tile in range (wave-uniform)
+#pragma unroll
+      for (int i = 0; i < KCH; ++i) {
+        const int idx = tid + i * NT, key = idx / KCPR, c = idx % KCPR;
+        kr[i] = ld16(kbase + (size_t)(kt * KTT + key) * a.ldk + c * CE);
+      }
+#pragma unroll
+      for (int i = 0; i < VCH; ++i) {
+        const int idx = tid + i * NT, d = idx / VCPR, c = idx % VCPR;
+        vr[i] = ld16(vbase + (size_t)d * a.Tk + kt * KTT + c * CE);
+      }
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < KCH; ++i) {
       int idx = tid + i * NT;
       int key = idx / KCPR, c = idx % KCPR;
-      int kk = kt * KT + key;
+      int kk = kt * KTT + key;
       kr[i] = kk < a.Tk ? ld16(kbase + (size_t)kk * a.ldk + c * CE) : u32x4{0, 0, 0, 0};
     }
 #pragma unroll
     for (int i = 0; i < VCH; ++i) {
       int idx = tid + i * NT;
       int d = idx / VCPR, c = idx % VCPR;
-      int k0 = kt * KT + c * CE;
+      int k0 = kt * KTT + c * CE;
       const T* src = vbase + (size_t)d * a.Tk + k0;
       if (k0 + CE <= a.Tk && ((a.Tk % CE) == 0)) {
         vr[i] = ld16(src);
@@ -80,7 +105,7 @@ struct Stage {
   SPE_DEV void store(char* kl, char* vl, int tid) const {
     constexpr int CE = 16 / ES;
     constexpr int KCPR = 32 / CE;
-    constexpr int VCPR = 64 / CE;
+    constexpr int VCPR = KTT / CE;
 #pragma unroll
     for (int i = 0; i < KCH; ++i) {
       int idx = tid + i * NT;
@@ -92,8 +117,8 @@ struct Stage {
       int idx = tid + i * NT;
       int d = idx / VCPR, c = idx % VCPR;
       if constexpr (ES == 2) {
-        st8(vl + v_off_bf16(d, 2 * c), u32x2{vr[i].x, vr[i].y});
-        st8(vl + v_off_bf16(d, 2 * c + 1), u32x2{vr[i].z, vr[i].w});
+        st8(vl + v_quad_off(d, 2 * c), u32x2{vr[i].x, vr[i].y});
+        st8(vl + v_quad_off(d, 2 * c + 1), u32x2{vr[i].z, vr[i].w});
       } else {
         st16(vl + v_off_f32(d, c), vr[i]);
       }
@@ -111,15 +136,22 @@ SPE_DEV float tile_max(f32x16& s0, f32x16& s1, int key_base, int Tk, int hh) {
       if (key_base + 32 + kr >= Tk) s1[r] = NEG_BIG;
     }
   }
-  float mx = NEG_BIG;
+  // two independent v_max3 chains (the file is built with -fno-honor-nans, so no canonicalizes)
+  float ma = __builtin_fmaxf(s0[0], s1[0]), mb = __builtin_fmaxf(s0[1], s1[1]);
 #pragma unroll
-  for (int r = 0; r < 16; ++r) mx = __builtin_fmaxf(mx, __builtin_fmaxf(s0[r], s1[r]));
-  return __builtin_fmaxf(mx, __shfl_xor(mx, 32, 64));
+  for (int r = 2; r < 16; r += 2) {
+    ma = __builtin_fmaxf(__builtin_fmaxf(ma, s0[r]), s1[r]);
+    mb = __builtin_fmaxf(__builtin_fmaxf(mb, s0[r + 1]), s1[r + 1]);
+  }
+  const float mx = __builtin_fmaxf(ma, mb);
+  // lane <-> lane^32 exchange without an LDS round trip
+  const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
+  return __builtin_fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
 }
 
 // ------------------------------------------------------------------ bf16 kernel
-__global__ __launch_bounds__(NT, 2) void attn_bf16_kernel(AttnArgs a) {
-  constexpr int KBYTES = KT * 32 * 2, VBYTES = 32 * KT * 2;
+__global__ __launch_bounds__(NT, 4) void attn_bf16_kernel(AttnArgs a) {
+  constexpr int KBYTES = KT * KROW, VBYTES = 32 * VROW;
   __shared__ __attribute__((aligned(16))) char smem[2 * (KBYTES + VBYTES)];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int hh = lane >> 5, r32 = lane & 31;
@@ -144,74 +176,94 @@ __global__ __launch_bounds__(NT, 2) void attn_bf16_kernel(AttnArgs a) {
       qf[i] = __builtin_bit_cast(bf16x8, pack16<bf16>(f));
     }
   }
-  const bf16x8 ones = __builtin_bit_cast(bf16x8, u32x4{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u});
+  u32x4 ones_u{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};
+  asm volatile("" : "+v"(ones_u));      // keep in VGPRs (else rematerialised from SGPRs per use)
+  const bf16x8 ones = __builtin_bit_cast(bf16x8, ones_u);
 
-  f32x16 o;
+  // o: O^T accumulator; ls: running row sum (ones . P^T, every element equal), rescaled with o.
+  f32x16 o, ls;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) o[r] = 0.f;
-  float m = NEG_BIG, l = 0.f;
+  for (int r = 0; r < 16; ++r) { o[r] = 0.f; ls[r] = 0.f; }
+  float m = NEG_BIG;
 
+  // Two-slot LDS ring, one barrier per 64-key step: tile kt+1 travels global -> registers
+  // during step kt and is written to the other slot after it.  (A three-slot ring that
+  // prefetches the next step's K fragments measured slower: its extra live registers cost
+  // either spills or a wave of occupancy.)
   const int ntiles = (a.Tk + KT - 1) / KT;
-  Stage<bf16> st;
+  constexpr int SLOT = KBYTES + VBYTES;
+  Stage<bf16, KT> st;
   st.load(a, b, h, 0, tid);
   st.store(smem, smem + KBYTES, tid);
   __syncthreads();
   for (int kt = 0; kt < ntiles; ++kt) {
-    char* kl = smem + (kt & 1) * (KBYTES + VBYTES);
-    char* vl = kl + KBYTES;
+    const char* kl = smem + (kt & 1) * SLOT;
+    const char* vl = kl + KBYTES;
     const bool more = kt + 1 < ntiles;
     if (more) st.load(a, b, h, kt + 1, tid);
     if (wave_live) {
+      // every fragment read of this step is issued up front; V lands during QK^T + softmax
+      u32x4 kf[2][2], vf[2][2];
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        kf[sub][0] = ld16(kl + k_off_bf16(sub * 32 + r32, hh));
+        kf[sub][1] = ld16(kl + k_off_bf16(sub * 32 + r32, 2 + hh));
+      }
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)      // keys sub*32 + 16ks + {4hh..+3, 8+4hh..+3}
+          vf[sub][ks] = ld16(vl + r32 * VROW + (2 * sub + ks) * 32 + hh * 16);
       f32x16 s0, s1;
 #pragma unroll
       for (int r = 0; r < 16; ++r) { s0[r] = 0.f; s1[r] = 0.f; }
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub) {
-        const int key = sub * 32 + r32;
-        bf16x8 k0 = __builtin_bit_cast(bf16x8, ld16(kl + k_off_bf16(key, hh)));
-        bf16x8 k1 = __builtin_bit_cast(bf16x8, ld16(kl + k_off_bf16(key, 2 + hh)));
         f32x16& s = sub ? s1 : s0;
-        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf[0], s, 0, 0, 0);
-        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[1], s, 0, 0, 0);
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[sub][0]), qf[0], s, 0, 0, 0);
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[sub][1]), qf[1], s, 0, 0, 0);
       }
       const float mx = tile_max(s0, s1, kt * KT, a.Tk, hh);
-      if (__any(mx > m)) {                         // wave-uniform: rescale only when a max grew
+      // Lazy rescale (wave-uniform): keep the stale max until some lane's max grew by more than
+      // RESCALE_SLACK (p <= 2^8 then, harmless in fp32 accumulators and bf16 P).  With an exact
+      // "grew at all" test, 32 queries per wave re-fire the rescale on about half the tiles.
+      if (__any(mx > m + RESCALE_SLACK)) {
         const float mn = __builtin_fmaxf(m, mx);
         const float alpha = __builtin_amdgcn_exp2f(m - mn);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) o[r] *= alpha;
-        l *= alpha;
+        for (int r = 0; r < 16; ++r) { o[r] *= alpha; ls[r] *= alpha; }
         m = mn;
       }
-      f32x16 ls;
+      // p = exp2(s - m): packed subtracts (v_pk_add_f32, two scores per instruction)
+      const f32x2 nm = {-m, -m};
 #pragma unroll
-      for (int r = 0; r < 16; ++r) ls[r] = 0.f;
+      for (int r = 0; r < 16; r += 2) {
+        const f32x2 t0 = f32x2{s0[r], s0[r + 1]} + nm;
+        const f32x2 t1 = f32x2{s1[r], s1[r + 1]} + nm;
+        s0[r] = __builtin_amdgcn_exp2f(t0.x);
+        s0[r + 1] = __builtin_amdgcn_exp2f(t0.y);
+        s1[r] = __builtin_amdgcn_exp2f(t1.x);
+        s1[r + 1] = __builtin_amdgcn_exp2f(t1.y);
+      }
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub) {
-        f32x16& p = sub ? s1 : s0;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) p[r] = __builtin_amdgcn_exp2f(p[r] - m);
+        const f32x16& p = sub ? s1 : s0;
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
           u32x4 pw{pack_bf16x2(p[8 * ks + 0], p[8 * ks + 1]), pack_bf16x2(p[8 * ks + 2], p[8 * ks + 3]),
                    pack_bf16x2(p[8 * ks + 4], p[8 * ks + 5]), pack_bf16x2(p[8 * ks + 6], p[8 * ks + 7])};
           const bf16x8 pb = __builtin_bit_cast(bf16x8, pw);
-          const int u0 = (sub * 32 + 16 * ks + 4 * hh) >> 2;   // 8-byte unit = 4 keys
-          u32x2 v0 = ld8(vl + v_off_bf16(r32, u0));
-          u32x2 v1 = ld8(vl + v_off_bf16(r32, u0 + 2));
-          u32x4 va{v0.x, v0.y, v1.x, v1.y};
-          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, va), pb, o, 0, 0, 0);
+          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, vf[sub][ks]), pb, o, 0, 0, 0);
           ls = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pb, ls, 0, 0, 0);   // column sums of P^T
         }
       }
-      l += ls[0];
     }
-    if (more) st.store(smem + ((kt + 1) & 1) * (KBYTES + VBYTES), smem + ((kt + 1) & 1) * (KBYTES + VBYTES) + KBYTES, tid);
+    if (more) st.store(smem + ((kt + 1) & 1) * SLOT, smem + ((kt + 1) & 1) * SLOT + KBYTES, tid);
     __syncthreads();
   }
 
   if (!wave_live || q >= a.Tq) return;
-  const float inv = 1.f / l;            // l already sums all 64 keys of every tile
+  const float inv = 1.f / ls[0];        // ls sums all 64 keys of every tile
   bf16* op = (bf16*)a.o + (size_t)(b * a.Tq + q) * a.ldo + h * 32;
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
@@ -246,7 +298,7 @@ __global__ __launch_bounds__(NT, 2) void attn_f32_kernel(AttnArgs a) {
   float m = NEG_BIG, l = 0.f;
 
   const int ntiles = (a.Tk + KT - 1) / KT;
-  Stage<float> st;
+  Stage<float, KT> st;
   st.load(a, b, h, 0, tid);
   st.store(smem, smem + KBYTES, tid);
   __syncthreads();

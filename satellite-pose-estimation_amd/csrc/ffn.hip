@@ -28,11 +28,14 @@ constexpr int D = 256;
 constexpr int W1_BYTES = HC * D * 2;    // 16 KiB: W1[j][d], 32 rows of 512 B
 constexpr int W2_BYTES = D * HC * 2;    // 16 KiB: W2[n][j], 256 rows of 64 B
 constexpr int STAGE = W1_BYTES + W2_BYTES;
+constexpr int FMAX = 4096;              // largest dim_feedforward (b1 staged in LDS)
 
 // W1 chunk: 16-byte chunk c (of 32 per row) lives at slot c ^ (row & 15)
 SPE_DEV int w1_off(int row, int c) { return row * 512 + ((c ^ (row & 15)) << 4); }
-// W2 chunk: 8-byte unit u (of 8 per row) lives at slot u ^ (2 * ((row >> 2) & 3))
-SPE_DEV int w2_off(int row, int u) { return row * 64 + ((u ^ (((row >> 2) & 3) << 1)) << 3); }
+// W2 chunk: 8-byte unit u (of 8 per row) lives at slot u ^ ((row >> 1) & 7): the 16 rows one
+// ds_read_b64 / ds_read2_b64 lane group touches land on 16 distinct 8-byte bank pairs
+SPE_DEV int w2_key(int row) { return (row >> 1) & 7; }
+SPE_DEV int w2_off(int row, int u) { return row * 64 + ((u ^ w2_key(row)) << 3); }
 
 struct Staged {
   u32x4 w1[4], w2[4];
@@ -58,14 +61,21 @@ struct Staged {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int idx = tid + i * NT, row = idx >> 2, c = idx & 3;
-      st16(st + W1_BYTES + w2_off(row, 2 * c), w2[i]);   // units 2c, 2c+1 stay adjacent
+      // units 2c, 2c+1 land in one aligned slot pair, swapped when the row key is odd
+      const bool swap = w2_key(row) & 1;
+      const u32x4 v = swap ? u32x4{w2[i].z, w2[i].w, w2[i].x, w2[i].y} : w2[i];
+      st16(st + W1_BYTES + (w2_off(row, 2 * c) & ~15), v);
     }
   }
 };
 
 __global__ __launch_bounds__(NT, 1) void ffn_ln_kernel(FfnArgs a) {
   __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
+  __shared__ __attribute__((aligned(16))) float sb1[FMAX];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // b1 lives in LDS: a global load inside the chunk loop would make the wave wait (vmcnt is
+  // in-order) for the next chunk's weight prefetch issued just before it.
+  for (int i = tid; i < a.F; i += NT) sb1[i] = a.b1[i];
   const int g = lane >> 4, c16 = lane & 15;
   const int m0 = blockIdx.x * BM + wid * 32;
 
@@ -92,6 +102,21 @@ __global__ __launch_bounds__(NT, 1) void ffn_ln_kernel(FfnArgs a) {
     const char* st = smem + (ch & 1) * STAGE;
     const bool more = ch + 1 < nchunks;
     if (more) stg.load(a, ch + 1, tid);
+    // All of this chunk's LDS operand reads are issued up front (one wave per SIMD: nothing else
+    // hides LDS latency); the phase-2 W2 reads land while the phase-1 MFMAs run.
+    u32x4 wa[8][2];
+    u32x2 wlo[16], whi[16];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb) wa[ks][jb] = ld16(st + w1_off(16 * jb + c16, 4 * ks + g));
+#pragma unroll
+    for (int nb = 0; nb < 16; ++nb) {
+      const int row = 16 * nb + c16;
+      wlo[nb] = ld8(st + W1_BYTES + w2_off(row, g));        // j = 4g .. 4g+3
+      whi[nb] = ld8(st + W1_BYTES + w2_off(row, 4 + g));    // j = 16+4g .. +3
+    }
+    __builtin_amdgcn_sched_barrier(0);
     // ---- H^T chunk: [32 j][32 m] = W1[j] . x[m]
     f32x4 h[2][2];
 #pragma unroll
@@ -100,14 +125,14 @@ __global__ __launch_bounds__(NT, 1) void ffn_ln_kernel(FfnArgs a) {
     for (int ks = 0; ks < 8; ++ks) {
 #pragma unroll
       for (int jb = 0; jb < 2; ++jb) {
-        const bf16x8 wa = __builtin_bit_cast(bf16x8, ld16(st + w1_off(16 * jb + c16, 4 * ks + g)));
-        h[jb][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, xf[0][ks], h[jb][0], 0, 0, 0);
-        h[jb][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, xf[1][ks], h[jb][1], 0, 0, 0);
+        const bf16x8 w = __builtin_bit_cast(bf16x8, wa[ks][jb]);
+        h[jb][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, xf[0][ks], h[jb][0], 0, 0, 0);
+        h[jb][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, xf[1][ks], h[jb][1], 0, 0, 0);
       }
     }
     // ---- bias + ReLU, repack as the K=32 B operand: element e <- hidden 4g+e (e<4), 16+4g+e-4
-    const f32x4 b1a = *reinterpret_cast<const f32x4*>(a.b1 + ch * HC + 4 * g);
-    const f32x4 b1b = *reinterpret_cast<const f32x4*>(a.b1 + ch * HC + 16 + 4 * g);
+    const f32x4 b1a = *reinterpret_cast<const f32x4*>(sb1 + ch * HC + 4 * g);
+    const f32x4 b1b = *reinterpret_cast<const f32x4*>(sb1 + ch * HC + 16 + 4 * g);
     bf16x8 hb[2];
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb) {
@@ -122,10 +147,7 @@ __global__ __launch_bounds__(NT, 1) void ffn_ln_kernel(FfnArgs a) {
     // ---- out^T[n][m] += W2[n][chunk j] . H^T[j][m]
 #pragma unroll
     for (int nb = 0; nb < 16; ++nb) {
-      const int row = 16 * nb + c16;
-      const u32x2 lo = ld8(st + W1_BYTES + w2_off(row, g));        // j = 4g .. 4g+3
-      const u32x2 hi = ld8(st + W1_BYTES + w2_off(row, 4 + g));    // j = 16+4g .. +3
-      const bf16x8 wb = __builtin_bit_cast(bf16x8, u32x4{lo.x, lo.y, hi.x, hi.y});
+      const bf16x8 wb = __builtin_bit_cast(bf16x8, u32x4{wlo[nb].x, wlo[nb].y, whi[nb].x, whi[nb].y});
       acc[nb][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb, hb[0], acc[nb][0], 0, 0, 0);
       acc[nb][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb, hb[1], acc[nb][1], 0, 0, 0);
     }
@@ -187,7 +209,7 @@ __global__ __launch_bounds__(NT, 1) void ffn_ln_kernel(FfnArgs a) {
 
 int spe_launch_ffn_ln(const FfnArgs& a, hipStream_t s) {
   if (a.M <= 0) return 0;
-  if (a.D != D || a.F % HC || (a.ldx % 8) || (a.ldy % 8) || (a.ld1 % 8) || (a.ld2 % 8)) return -5;
+  if (a.D != D || a.F % HC || a.F > FMAX || (a.ldx % 8) || (a.ldy % 8) || (a.ld1 % 8) || (a.ld2 % 8)) return -5;
   hipLaunchKernelGGL(ffn_ln_kernel, dim3((a.M + BM - 1) / BM), dim3(NT), 0, s, a);
   return (int)hipGetLastError();
 }

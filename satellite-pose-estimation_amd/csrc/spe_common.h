@@ -49,9 +49,11 @@ template <typename T> SPE_DEV u32x4 pack16(const float* f);
 template <> SPE_DEV u32x4 pack16<float>(const float* f) {
   return u32x4{__float_as_uint(f[0]), __float_as_uint(f[1]), __float_as_uint(f[2]), __float_as_uint(f[3])};
 }
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+// two floats -> two RNE bf16 in one v_cvt_pk_bf16_f32 (two scalar casts + shift/or cost 4 VALU)
 SPE_DEV uint32_t pack_bf16x2(float lo, float hi) {
-  bf16 a = (bf16)lo, b = (bf16)hi;
-  return (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{lo, hi}, bf16x2));
 }
 template <> SPE_DEV u32x4 pack16<bf16>(const float* f) {
   return u32x4{pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]), pack_bf16x2(f[6], f[7])};

@@ -12,7 +12,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libspe.so")
+LIB_PATH = os.environ.get("SPE_LIB_PATH") or os.path.join(_HERE, "libspe.so")   # override: kernel A/B builds
 
 P = ctypes.c_void_p
 I = ctypes.c_int

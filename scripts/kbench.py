@@ -1,0 +1,71 @@
+"""Per-kernel microbenchmark at the bench workload's shapes (B=64, 416x416 -> 2704 tokens),
+through the C-ABI kernel test hooks.  Run alone for timings, or under rocprofv3 --pmc for
+counters of one kernel family.
+
+usage: python scripts/kbench.py [attn|ffn|all] [--iters 20]
+"""
+import argparse
+import ctypes
+import os
+import sys
+
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(REPO, "satellite-pose-estimation_amd"))
+from spe import _lib  # noqa: E402
+
+
+def p(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def timeit(fn, iters):
+    fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("which", nargs="?", default="all")
+    ap.add_argument("--iters", type=int, default=20)
+    ap.add_argument("--batch", type=int, default=64)
+    a = ap.parse_args()
+    L = _lib.lib()
+    dev = torch.device("cuda", 0)
+    B, H, T, D, F = a.batch, 8, 2704, 256, 2048
+    g = torch.Generator(device="cpu").manual_seed(0)
+    if a.which in ("attn", "all"):
+        qk = torch.randn(B * T, 512, generator=g).to(dev, torch.bfloat16)
+        vt = torch.randn(B, H, 32, T, generator=g).to(dev, torch.bfloat16)
+        o = torch.empty(B * T, D, dtype=torch.bfloat16, device=dev)
+        kp = ctypes.c_void_p(qk.data_ptr() + 256 * 2)
+        fn = lambda: L.spe_debug_attention(None, 0, p(qk), 512, kp, 512, p(vt), p(o), D, B, H, T, T, 32 ** -0.5)
+        ms = timeit(fn, a.iters)
+        fl = 4.0 * B * H * T * T * 32
+        print(f"attn.enc  {ms:.3f} ms  {fl / ms / 1e9:.1f} TF/s")
+    if a.which in ("ffn", "all"):
+        x = torch.randn(B * T, D, generator=g).to(dev, torch.bfloat16)
+        w1 = (torch.randn(F, D, generator=g) / 16).to(dev, torch.bfloat16)
+        w2 = (torch.randn(D, F, generator=g) / 45).to(dev, torch.bfloat16)
+        b1 = torch.zeros(F, device=dev)
+        b2 = torch.zeros(D, device=dev)
+        gm = torch.ones(D, device=dev)
+        bt = torch.zeros(D, device=dev)
+        y = torch.empty_like(x)
+        fn = lambda: L.spe_debug_ffn(None, p(x), D, p(w1), D, p(b1), p(w2), F, p(b2), p(gm), p(bt), p(y), D,
+                                     B * T, D, F)
+        ms = timeit(fn, a.iters)
+        fl = 4.0 * B * T * D * F
+        print(f"ffn.enc   {ms:.3f} ms  {fl / ms / 1e9:.1f} TF/s")
+
+
+if __name__ == "__main__":
+    main()
