@@ -129,12 +129,14 @@ int spe_model_profile_get(const spe_model* m, int i, char* kind, int kind_len, d
 /* Kernel test hooks: launch one kernel family on caller buffers (tests/test_gpu_kernels.py).
  * gemm: C[M,N] = A . W^T (+bias, +R, ReLU) with mode 0 linear (A[m*lda+k]), 1 linear + P[(m%prow)
  * *ldp+k] added to A, 2 implicit-GEMM conv over NHWC A [*,H,W,Cin]; W is [N][ldb] (ldb % 64 == 0);
- * vt_T > 0 stores head-transposed C[((n/256)*vt_B + m/vt_T)*256 + n%256][m%vt_T].
+ * vt_T > 0 stores head-transposed C[((n/256)*vt_B + m/vt_T)*256 + n%256][m%vt_T]; r_period > 0
+ * reads the residual row-periodically, R[(m % r_period)*ldr + n].  bf16 problems that fill the chip
+ * with 256-row tiles run the direct-to-LDS kernel (gemm2.hip), the rest the 128x128 kernel.
  * attention: per (b,h) softmax(scale Q K^T) V with Q/K rows b*T+i at column h*32, V^T [B][H][32][Tk]. */
 int spe_debug_gemm(void* stream, int dtype, int mode, const void* A, int lda, const void* P, int ldp, int prow, int H,
                    int W, int Cin, int KH, int KW, int stride, int pad, const void* Bw, int ldb, int M, int N, int K,
                    const float* bias, const void* R, int ldr, int relu, void* C, int ldc, int out_f32, int vt_T,
-                   int vt_B);
+                   int vt_B, int r_period);
 int spe_debug_attention(void* stream, int dtype, const void* q, int ldq, const void* k, int ldk, const void* vt,
                         void* o, int ldo, int B, int H, int Tq, int Tk, float scale);
 int spe_debug_layernorm(void* stream, int dtype, const void* x, const float* gamma, const float* beta, void* out,

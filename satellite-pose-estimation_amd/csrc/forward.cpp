@@ -46,7 +46,8 @@ int run_other(spe_model* m, const char* kind, double flops, double bytes, hipStr
 int run_gemm(spe_model* m, const char* kind, const GemmArgs& g, int mode, hipStream_t s) {
   const double E = m->esz;
   const double a_elems = mode == GEMM_CONV ? (double)(g.M / (g.Ho * g.Wo)) * g.H * g.W * g.Cin : (double)g.M * g.K;
-  const double bytes = (a_elems + (double)g.N * g.K + (double)g.M * g.N * (g.R ? 2 : 1)) * E +
+  const double r_rows = g.R ? (g.r_period > 0 ? (double)g.r_period : (double)g.M) : 0.0;
+  const double bytes = (a_elems + (double)g.N * g.K + (double)g.M * g.N + r_rows * g.N) * E +
                        (mode == GEMM_LINEAR_ADD ? (double)g.prow * g.K * E : 0.0);
   return run_other(m, kind, 2.0 * g.M * g.N * g.K, bytes, s,
                    [&] { return spe_launch_gemm(g, m->cfg.dtype, mode, s); });
@@ -85,6 +86,17 @@ int run_ffn(spe_model* m, const char* kind, const Conv& l1, const Conv& l2, cons
 
 bool use_fused_ffn(const spe_model* m) {
   return m->cfg.dtype == SPE_DTYPE_BF16 && m->cfg.hidden_dim == 256 && m->cfg.dim_feedforward % 32 == 0;
+}
+
+// `(x + pos) . W^T`: fp32 models add pos to the A operand as the reference does; bf16 models
+// add the precomputed pos . W^T as a row-periodic residual (see gemm2.hip).
+int add_pos(const spe_model* m, GemmArgs& g, const void* pos, int ldp, int period, const void* posw, int ldw) {
+  if (m->esz == 2 && posw) {
+    g.R = posw; g.ldr = ldw; g.r_period = period;
+    return GEMM_LINEAR;
+  }
+  g.P = pos; g.ldp = ldp; g.prow = period;
+  return GEMM_LINEAR_ADD;
 }
 
 GemmArgs conv_args(const Conv& c, const void* X, int B, int H, int W, void* Y, int ldc) {
@@ -206,8 +218,8 @@ int spe_forward(spe_model* m, void* stream, const float* images, int B, void* wo
   for (const Enc& e : m->enc) {
     {
       GemmArgs g = linear_args(e.qk, P(w.src), d, Mt, P(w.qkv), 3 * d);
-      g.P = m->pos; g.ldp = d; g.prow = T;
-      CK(run_gemm(m, "gemm.enc.qk", g, GEMM_LINEAR_ADD, s));
+      const int mode = add_pos(m, g, m->pos, d, T, e.pos_qk, 2 * d);
+      CK(run_gemm(m, "gemm.enc.qk", g, mode, s));
     }
     {
       GemmArgs g = linear_args(e.v, P(w.src), d, Mt, P(w.vt), 8);
@@ -248,8 +260,8 @@ int spe_forward(spe_model* m, void* stream, const float* images, int B, void* wo
   // memory = src.  Cross-attention K (memory + pos) and V^T (memory) for all decoder layers.
   {
     GemmArgs g = linear_args(m->crossK, P(w.src), d, Mt, P(w.ck), L * d);
-    g.P = m->pos; g.ldp = d; g.prow = T;
-    CK(run_gemm(m, "gemm.cross_kv", g, GEMM_LINEAR_ADD, s));
+    const int mode = add_pos(m, g, m->pos, d, T, m->pos_crossK, L * d);
+    CK(run_gemm(m, "gemm.cross_kv", g, mode, s));
   }
   {
     GemmArgs g = linear_args(m->crossV, P(w.src), d, Mt, P(w.cvt), 8);
@@ -264,8 +276,8 @@ int spe_forward(spe_model* m, void* stream, const float* images, int B, void* wo
     const Dec& e = m->dec[l];
     {
       GemmArgs g = linear_args(e.sqk, P(w.tgt), d, Mq, P(w.dqkv), 3 * d);
-      g.P = m->qpos; g.ldp = d; g.prow = Q;
-      CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR_ADD, s));
+      const int mode = add_pos(m, g, m->qpos, d, Q, e.qpos_sqk, 2 * d);
+      CK(run_gemm(m, "gemm.dec", g, mode, s));
     }
     {
       GemmArgs g = linear_args(e.sv, P(w.tgt), d, Mq, P(w.dvt), 8);
@@ -289,8 +301,8 @@ int spe_forward(spe_model* m, void* stream, const float* images, int B, void* wo
     CK(run_other(m, "ln.dec", 0.0, (double)Mq * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.dtmp), e.n1g, e.n1b, P(w.tgt), nullptr, Mq, d, dt, s); }));
     {
       GemmArgs g = linear_args(e.cq, P(w.tgt), d, Mq, P(w.dqc), d);
-      g.P = m->qpos; g.ldp = d; g.prow = Q;
-      CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR_ADD, s));
+      const int mode = add_pos(m, g, m->qpos, d, Q, e.qpos_cq, d);
+      CK(run_gemm(m, "gemm.dec", g, mode, s));
     }
     {
       AttnArgs a{};

@@ -244,21 +244,14 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs g) {
     float v[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = ct[rr * EPI_LD + cg + e] + bv[e];
-    if (g.R) {
-      const T* rp = (const T*)g.R + (size_t)m * g.ldr + n;
+    if (g.R) {                                     // residual, or row-periodic add (pos . W^T)
+      const T* rp = (const T*)g.R + (size_t)(g.r_period > 0 ? m % g.r_period : m) * g.ldr + n;
       if (full) {
-        if constexpr (sizeof(T) == 2) {
-          float f[8];
-          unpack16<T>(ld16(rp), f);
+        float f[8];
+        unpack16<T>(ld16(rp), f);
+        if constexpr (sizeof(T) == 4) unpack16<T>(ld16(rp + 4), f + 4);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += f[e];
-        } else {
-          float f[8];
-          unpack16<T>(ld16(rp), f);
-          unpack16<T>(ld16(rp + 4), f + 4);
-#pragma unroll
-          for (int e = 0; e < 8; ++e) v[e] += f[e];
-        }
+        for (int e = 0; e < 8; ++e) v[e] += f[e];
       } else {
         for (int e = 0; e < 8 && n + e < g.N; ++e) v[e] += to_f32(rp[e]);
       }
@@ -314,5 +307,9 @@ int spe_launch_gemm(const GemmArgs& g, int dtype, int mode, hipStream_t s) {
   if (mode == GEMM_CONV && (g.Cin % ce)) return -3;
   if (g.ldb % 64) return -4;                                 // weights padded to 64 elements
   if ((g.lda % ce) || (g.ldc % (g.out_f32 ? 4 : ce)) || (g.R && (g.ldr % ce))) return -5;
+  if (dtype == SPE_DTYPE_BF16) {                 // 256-row tiles when they fill the chip
+    const int rc = spe_launch_gemm2(g, mode, s);
+    if (rc != 1) return rc;
+  }
   return dtype == SPE_DTYPE_BF16 ? launch_t<bf16>(g, mode, s) : launch_t<float>(g, mode, s);
 }

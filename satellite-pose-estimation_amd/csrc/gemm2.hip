@@ -1,0 +1,296 @@
+// Large-tile bf16 GEMM / implicit-GEMM convolution for gfx950 with direct-to-LDS staging.
+//
+// Serves the bf16 throughput path of every big contraction (ResNet-50 convs, neck convs,
+// transformer projections; REV/models/backbone.py:114-149, REV/models/transformer.py:137-191)
+// when the problem fills the chip with 256-row tiles; small or fp32 problems stay on gemm.hip.
+//
+//   C[M,N] = A[M,K] . W[N,K]^T  (+bias[n]) (+R[m or m % r_period, n]) (ReLU)
+//
+// * Tile 256 x BN (BN = 256 / 128 / 64 by N), 512 threads = 8 waves, wave tile
+//   (256/WM) x (BN/WN) of 16x16x32 bf16 MFMA fragments.  K-step = 64 bf16 = one 128-byte line
+//   per row.
+// * Staging: __builtin_amdgcn_global_load_lds (16 B per lane) straight into LDS, no VGPR
+//   round trip and no ds_write.  One wave-instruction fills 8 rows x 128 B linearly, so the
+//   XOR swizzle (16-byte chunk c of row r at slot c ^ (r & 7), conflict-free fragment reads)
+//   is applied on the SOURCE address (lane slot s loads global chunk s ^ (r & 7)) and again on
+//   the read.  Rows past M / N, columns past K and conv padding taps load from a zero line.
+// * Pipeline: two LDS stages; stage k+1's loads are issued before stage k is consumed and
+//   retired with a counted `s_waitcnt vmcnt(loads per stage)` + raw s_barrier (never
+//   __syncthreads, whose fence would drain the in-flight stage).  All LDS is one array.
+// * The `+ pos` of the attention projections is NOT applied to A here: by linearity
+//   (x + pos) W^T = x W^T + (pos W^T), the runtime precomputes pos W^T once per model and the
+//   epilogue adds it as a row-periodic residual (r_period = tokens per image).
+// * The residual tile is fetched into registers before the K loop (it is independent of the
+//   contraction), so the epilogue never waits on HBM.
+// * Epilogue: accumulators -> fp32 LDS tile in 64-row passes -> bias / residual / ReLU ->
+//   16-byte row stores (or the head-transposed V^T store).
+#include "spe_common.h"
+#include "spe_kernels.h"
+
+namespace {
+
+constexpr int BM = 256, BK = 64, NT = 512;
+__device__ __attribute__((aligned(64))) uint32_t g_zero_line[16];   // zero-filled source line
+
+SPE_DEV int swz(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
+
+template <int BN> struct Cfg;
+template <> struct Cfg<256> { static constexpr int WM = 2, WN = 4; };
+template <> struct Cfg<128> { static constexpr int WM = 4, WN = 2; };
+template <> struct Cfg<64> { static constexpr int WM = 4, WN = 2; };
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+template <int N>
+SPE_DEV void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+template <int BN, int MODE>
+__global__ __launch_bounds__(NT, 1) void gemm2_kernel(GemmArgs g) {
+  constexpr int WM = Cfg<BN>::WM, WN = Cfg<BN>::WN;
+  constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
+  constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
+  constexpr int IA = BM / 64, IB = BN / 64;            // glds instructions per wave per stage
+  constexpr int LOADS = IA + IB;
+  constexpr int EPI_ROWS = 64, EPI_LD = BN + 4;
+  constexpr int SMEM = (2 * STAGE > EPI_ROWS * EPI_LD * 4) ? 2 * STAGE : EPI_ROWS * EPI_LD * 4;
+  __shared__ __attribute__((aligned(1024))) char smem[SMEM];
+
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid / WN, wc = wid % WN;
+  const int tilesN = (g.N + BN - 1) / BN;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (t / tilesN) * BM, n0 = (t % tilesN) * BN;
+  const int nk = (g.K + BK - 1) / BK;
+
+  // ---- per-lane load descriptors.  Instruction i of wave w fills rows (w*I + i)*8 + lane/8.
+  const int lrow = lane >> 3;                    // row within the 8-row group
+  const int chunk = (lane & 7) ^ lrow;           // global 16-byte chunk this lane fetches
+  const char* zero = reinterpret_cast<const char*>(g_zero_line);
+  const char* abase[IA];
+  int aih[IA], aiw[IA];
+  bool arow[IA];
+#pragma unroll
+  for (int i = 0; i < IA; ++i) {
+    const int m = m0 + (wid * IA + i) * 8 + lrow;
+    arow[i] = m < g.M;
+    const int mm = arow[i] ? m : 0;
+    if constexpr (MODE == GEMM_CONV) {
+      const int hw = g.Ho * g.Wo;
+      const int b = mm / hw, r = mm - b * hw;
+      const int oh = r / g.Wo, ow = r - oh * g.Wo;
+      aih[i] = oh * g.stride - g.pad;
+      aiw[i] = ow * g.stride - g.pad;
+      abase[i] = (const char*)g.A + (size_t)b * g.H * g.W * g.Cin * 2;
+    } else {
+      abase[i] = (const char*)g.A + (size_t)mm * g.lda * 2;
+      aih[i] = aiw[i] = 0;
+    }
+  }
+  const char* bbase[IB];
+#pragma unroll
+  for (int i = 0; i < IB; ++i) {
+    const int n = n0 + (wid * IB + i) * 8 + lrow;
+    bbase[i] = n < g.N ? (const char*)g.B + ((size_t)n * g.ldb + chunk * 8) * 2 : nullptr;
+  }
+
+  auto issue = [&](int ks, int buf) {
+    char* st = smem + buf * STAGE;
+    const int k = ks * BK + chunk * 8;
+    const bool kv = k < g.K;
+    if constexpr (MODE == GEMM_CONV) {
+      const int kpos = k / g.Cin, ci = k - kpos * g.Cin;
+      const int kh = kpos / g.KW, kw = kpos - kh * g.KW;
+#pragma unroll
+      for (int i = 0; i < IA; ++i) {
+        const int ih = aih[i] + kh, iw = aiw[i] + kw;
+        const bool v = kv && arow[i] && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+        const char* src = v ? abase[i] + ((size_t)(ih * g.W + iw) * g.Cin + ci) * 2 : zero;
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(st + (wid * IA + i) * 1024), 16, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < IA; ++i) {
+        const char* src = (kv && arow[i]) ? abase[i] + (size_t)k * 2 : zero;
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(st + (wid * IA + i) * 1024), 16, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {
+      const char* src = bbase[i] ? bbase[i] + (size_t)ks * BK * 2 : zero;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(st + A_BYTES + (wid * IB + i) * 1024), 16, 0, 0);
+    }
+  };
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // ---- residual tile prefetch: this thread's epilogue rows x 8 columns, in registers
+  constexpr int TPR = BN / 8;                   // epilogue threads per row (8 columns each)
+  constexpr int RSTEP = NT / TPR, RPT = EPI_ROWS / RSTEP, NPASS = BM / EPI_ROWS;
+  const int ecg = (tid % TPR) * 8, en = n0 + ecg, ert = tid / TPR;
+  const bool efull = en + 8 <= g.N;
+  // (BN = 256: only the first half here, the rest after the K loop, or the K loop would spill)
+  constexpr int NPRE = BN == 256 ? NPASS / 2 : NPASS;
+  u32x4 rres[NPASS][RPT];
+  auto fetch_res = [&](int pp) {
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+      rres[pp][q] = u32x4{0, 0, 0, 0};
+      const int m = m0 + pp * EPI_ROWS + ert + q * RSTEP;
+      if (g.R && g.vt_T == 0 && efull && m < g.M) {
+        const int rm = g.r_period > 0 ? m % g.r_period : m;
+        rres[pp][q] = ld16((const bf16*)g.R + (size_t)rm * g.ldr + en);
+      }
+    }
+  };
+#pragma unroll
+  for (int pp = 0; pp < NPRE; ++pp) fetch_res(pp);
+
+  const int fg = lane >> 4, fr = lane & 15;
+  issue(0, 0);
+  for (int ks = 0; ks < nk; ++ks) {
+    if (ks + 1 < nk) {
+      issue(ks + 1, (ks + 1) & 1);
+      wait_vmcnt<LOADS>();                      // retire stage ks, keep ks+1 in flight
+    } else {
+      wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();               // every wave's stage-ks lines have landed
+    const char* st = smem + (ks & 1) * STAGE;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      u32x4 af[FM], bfr[FN];
+#pragma unroll
+      for (int i = 0; i < FM; ++i) af[i] = ld16(st + swz(wr * TM + i * 16 + fr, 4 * kk + fg));
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bfr[j] = ld16(st + A_BYTES + swz(wc * TN + j * 16 + fr, 4 * kk + fg));
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[i]),
+                                                               __builtin_bit_cast(bf16x8, bfr[j]), acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();               // stage ks fully read: its buffer may be refilled
+  }
+
+  // ---- epilogue in 64-row passes through an fp32 LDS tile
+#pragma unroll
+  for (int pp = NPRE; pp < NPASS; ++pp) fetch_res(pp);
+  float* ct = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int pass = 0; pass < NPASS; ++pass) {
+    const int r0 = pass * EPI_ROWS;
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+      const int rb = wr * TM + i * 16;            // fragment rows [rb, rb+16)
+      if (rb >= r0 && rb < r0 + EPI_ROWS) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            ct[(rb - r0 + fg * 4 + r) * EPI_LD + wc * TN + j * 16 + fr] = acc[i][j][r];
+      }
+    }
+    __syncthreads();
+    if (g.vt_T > 0) {
+      // head-transposed store: column n = grp*256 + hd -> C[((grp*vt_B + b)*256 + hd)*T + tok]
+      for (int it = tid; it < (EPI_ROWS / 8) * BN; it += NT) {
+        const int col = it % BN, rg = (it / BN) * 8, n = n0 + col, m = m0 + r0 + rg;
+        if (n >= g.N || m >= g.M) continue;
+        float bv = g.bias ? g.bias[n] : 0.f;
+        float v[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] = ct[(rg + e) * EPI_LD + col] + bv;
+        const int grp = n >> 8, hd = n & 255;
+        const int b = m / g.vt_T, tok = m - b * g.vt_T;
+        if ((g.vt_T & 7) == 0 && m + 8 <= g.M) {
+          st16((bf16*)g.C + ((size_t)(grp * g.vt_B + b) * 256 + hd) * g.vt_T + tok, pack16<bf16>(v));
+        } else {
+          for (int e = 0; e < 8 && m + e < g.M; ++e) {
+            const int me = m + e, be = me / g.vt_T, te = me - be * g.vt_T;
+            ((bf16*)g.C)[((size_t)(grp * g.vt_B + be) * 256 + hd) * g.vt_T + te] = from_f32<bf16>(v[e]);
+          }
+        }
+      }
+    } else {
+      const int cg = ecg, n = en;
+      if (n < g.N) {
+        const bool full = efull;
+        float bv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) bv[e] = (g.bias && n + e < g.N) ? g.bias[n + e] : 0.f;
+#pragma unroll
+        for (int q = 0; q < RPT; ++q) {
+          const int rr = ert + q * RSTEP, m = m0 + r0 + rr;
+          if (m >= g.M) continue;
+          float v[8];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) v[e] = ct[rr * EPI_LD + cg + e] + bv[e];
+          if (g.R) {
+            if (full) {
+              float f[8];
+              unpack16<bf16>(rres[pass][q], f);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) v[e] += f[e];
+            } else {
+              const bf16* rp = (const bf16*)g.R + (size_t)(g.r_period > 0 ? m % g.r_period : m) * g.ldr + n;
+              for (int e = 0; e < 8 && n + e < g.N; ++e) v[e] += to_f32(rp[e]);
+            }
+          }
+          if (g.relu) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+          }
+          if (g.out_f32) {
+            float* cp = (float*)g.C + (size_t)m * g.ldc + n;
+            if (full) {
+              st16(cp, pack16<float>(v));
+              st16(cp + 4, pack16<float>(v + 4));
+            } else {
+              for (int e = 0; e < 8 && n + e < g.N; ++e) cp[e] = v[e];
+            }
+          } else {
+            bf16* cp = (bf16*)g.C + (size_t)m * g.ldc + n;
+            if (full) {
+              st16(cp, pack16<bf16>(v));
+            } else {
+              for (int e = 0; e < 8 && n + e < g.N; ++e) cp[e] = from_f32<bf16>(v[e]);
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int BN>
+int launch_bn(const GemmArgs& g, int mode, hipStream_t s) {
+  const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
+  dim3 grid(tiles), block(NT);
+  if (mode == GEMM_CONV)
+    hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_CONV>), grid, block, 0, s, g);
+  else
+    hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_LINEAR>), grid, block, 0, s, g);
+  return (int)hipGetLastError();
+}
+
+}  // namespace
+
+// Returns 1 when the problem is not for this kernel (caller falls back to gemm.hip).
+int spe_launch_gemm2(const GemmArgs& g, int mode, hipStream_t s) {
+  if (mode != GEMM_LINEAR && mode != GEMM_CONV) return 1;
+  if (g.M <= 0 || g.N <= 0) return 0;
+  if (g.K % 8 || g.ldb % 64 || g.lda % 8 || (mode == GEMM_CONV && g.Cin % 8)) return 1;
+  if (g.out_f32 ? (g.ldc % 4) : (g.ldc % 8)) return 1;
+  if (g.R && g.ldr % 8) return 1;
+  const int bn = g.N <= 64 ? 64 : g.N <= 128 ? 128 : 256;
+  const int tiles = ((g.M + BM - 1) / BM) * ((g.N + bn - 1) / bn);
+  if (tiles < 256) return 1;                     // too few tiles to fill 256 CUs: 128x128 kernel
+  return bn == 64 ? launch_bn<64>(g, mode, s) : bn == 128 ? launch_bn<128>(g, mode, s) : launch_bn<256>(g, mode, s);
+}

@@ -25,11 +25,14 @@ struct Block {
 struct Enc {
   Conv qk, v, o, l1, l2;
   float *n1g, *n1b, *n2g, *n2b;
+  void* pos_qk = nullptr;   // bf16 models: pos . W_qk^T [tokens][512] (row-periodic residual)
 };
 
 struct Dec {
   Conv sqk, sv, so, cq, co, l1, l2;
   float *n1g, *n1b, *n2g, *n2b, *n3g, *n3b;
+  void* qpos_sqk = nullptr; // bf16 models: query_pos . W_sqk^T [Q][512]
+  void* qpos_cq = nullptr;  // bf16 models: query_pos . W_cq^T [Q][256]
 };
 
 struct Ws {                // workspace layout (byte offsets)
@@ -69,6 +72,7 @@ struct spe_model {
   std::vector<Dec> dec;
   void* pos = nullptr;     // [tokens][256] T
   void* qpos = nullptr;    // [Q][256] T
+  void* pos_crossK = nullptr;  // bf16 models: pos . W_crossK^T [tokens][L*256]
   float *dng = nullptr, *dnb = nullptr;
   HeadArgs head{};
   Profiler prof;

@@ -295,6 +295,18 @@ int build_device(spe_model* m) {
   const int fs = c.input_size / 8;
   m->pos = upload_T(m, sine_pos(fs, fs, d));
   m->qpos = upload_T(m, m->host["query_embed.weight"]);
+  if (m->esz == 2) {
+    // bf16 throughput path: the `+ pos` of the q/k projections is applied as (pos . W^T), a
+    // row-periodic residual filled by spe_model_finalize (gemm2.hip header); fp32 keeps the
+    // reference's (x + pos) . W^T order for exact parity.
+    const size_t T = (size_t)fs * fs, Q = c.num_queries;
+    for (auto& e : m->enc) e.pos_qk = dalloc(m, T * 2 * d * 2);
+    m->pos_crossK = dalloc(m, T * c.dec_layers * d * 2);
+    for (auto& e : m->dec) {
+      e.qpos_sqk = dalloc(m, Q * 2 * d * 2);
+      e.qpos_cq = dalloc(m, Q * d * 2);
+    }
+  }
   m->dng = upload_key(m, "transformer.decoder.norm.weight");
   m->dnb = upload_key(m, "transformer.decoder.norm.bias");
 
@@ -422,6 +434,24 @@ int spe_model_finalize(spe_model* m) {
   build_device(m);
   e = hipDeviceSynchronize();
   if (e != hipSuccess || m->upload_err) return fail(e != hipSuccess ? (int)e : m->upload_err, "weight upload failed");
+  if (m->esz == 2) {
+    const int d = m->cfg.hidden_dim, fs = m->cfg.input_size / 8, T = fs * fs, Q = m->cfg.num_queries;
+    auto proj = [&](const void* A, int rows, const Conv& w, void* out) {
+      GemmArgs g{};
+      g.A = A; g.lda = d; g.B = w.w; g.ldb = w.Kpad;
+      g.M = rows; g.N = w.N; g.K = w.K; g.C = out; g.ldc = w.N;
+      return spe_launch_gemm(g, SPE_DTYPE_BF16, GEMM_LINEAR, nullptr);
+    };
+    int rc = 0;
+    for (auto& l : m->enc) rc |= proj(m->pos, T, l.qk, l.pos_qk);
+    rc |= proj(m->pos, T, m->crossK, m->pos_crossK);
+    for (auto& l : m->dec) {
+      rc |= proj(m->qpos, Q, l.sqk, l.qpos_sqk);
+      rc |= proj(m->qpos, Q, l.cq, l.qpos_cq);
+    }
+    e = hipDeviceSynchronize();
+    if (rc || e != hipSuccess) return fail(SPE_E_LAUNCH, "positional projection precompute failed");
+  }
   m->host.clear();
   m->finalized = true;
   return 0;

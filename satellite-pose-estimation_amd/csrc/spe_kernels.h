@@ -19,8 +19,10 @@ struct GemmArgs {
   void* C; int ldc;                // output [m*ldc + n]
   int out_f32;                     // store fp32 instead of T
   int vt_T, vt_B;                  // >0: head-transposed store (see gemm.hip)
+  int r_period;                    // >0: residual row = m % r_period (row-periodic add, e.g. pos . W^T)
 };
 int spe_launch_gemm(const GemmArgs& g, int dtype, int mode, hipStream_t s);
+int spe_launch_gemm2(const GemmArgs& g, int mode, hipStream_t s);   // 1 = not applicable
 
 struct AttnArgs {
   const void* q; int ldq;          // query row b*Tq+i, head h at columns [h*32, h*32+32)

@@ -31,11 +31,11 @@ def _close(got, ref, tol):
 
 
 def _gemm(dtype, mode, A, W, M, N, K, lda, ldb, C, ldc, bias=None, R=None, ldr=0, relu=0, P=None, ldp=0, prow=1,
-          conv=(0, 0, 0, 1, 1, 1, 0), out_f32=0, vt=(0, 0)):
+          conv=(0, 0, 0, 1, 1, 1, 0), out_f32=0, vt=(0, 0), r_period=0):
     L = _lib.lib()
     H, Wd, Cin, KH, KW, stride, pad = conv
     rc = L.spe_debug_gemm(None, DT[dtype][0], mode, _p(A), lda, _p(P), ldp, prow, H, Wd, Cin, KH, KW, stride, pad,
-                          _p(W), ldb, M, N, K, _p(bias), _p(R), ldr, relu, _p(C), ldc, out_f32, vt[0], vt[1])
+                          _p(W), ldb, M, N, K, _p(bias), _p(R), ldr, relu, _p(C), ldc, out_f32, vt[0], vt[1], r_period)
     assert rc == 0, L.spe_last_error()
     torch.cuda.synchronize()
 
@@ -114,6 +114,79 @@ def test_gemm_head_transposed_store(gpu_device, dtype, T):
     bias = torch.randn(N, generator=g).to(gpu_device)
     C = torch.zeros(2 * B * 256 * T, dtype=dt, device=gpu_device)
     _gemm(dtype, 0, A, _padded_weight(Wt, 256, dt), M, N, K, K, 256, C, 8, bias=bias, vt=(T, B))
+    ref = (A.float() @ Wt.float().t() + bias).view(B, T, 2, 256).permute(2, 0, 3, 1).reshape(-1)
+    _close(C, ref, tol)
+
+
+# ---- large-tile (256-row, direct-to-LDS) kernel: bf16 problems with >= 256 tiles
+
+@pytest.mark.parametrize("N,K", [(256, 256), (64, 192), (128, 520), (512, 256), (200, 64)])
+def test_gemm_large_tile_linear(gpu_device, N, K):
+    _, dt, tol = DT["bf16"]
+    M = 256 * 256 + 77                                  # >= 256 tiles of 256 rows, ragged tail
+    if N > 256:
+        M = 256 * 130 + 5
+    g = torch.Generator(device="cpu").manual_seed(N + K)
+    A = torch.randn(M, K + 8, generator=g).to(gpu_device, dt)        # lda > K
+    Wt = (torch.randn(N, K, generator=g) / K ** 0.5).to(gpu_device, dt)
+    ldb = (K + 63) // 64 * 64
+    bias = torch.randn(N, generator=g).to(gpu_device)
+    ld = (N + 8 + 7) // 8 * 8
+    R = torch.randn(M, ld, generator=g).to(gpu_device, dt)
+    C = torch.zeros(M, ld, dtype=dt, device=gpu_device)
+    _gemm("bf16", 0, A, _padded_weight(Wt, ldb, dt), M, N, K, K + 8, ldb, C, ld, bias=bias, R=R, ldr=ld, relu=1)
+    ref = A[:, :K].float() @ Wt.float().t() + bias + R[:, :N].float()
+    _close(C[:, :N], torch.relu(ref), tol)
+    assert (C[:, N:] == 0).all()
+
+
+@pytest.mark.parametrize("M", [256 * 256 + 77, 300])
+def test_gemm_row_periodic_residual(gpu_device, M):
+    """C = A W^T + b + R[m % period]: the (x + pos) W^T = x W^T + pos W^T rewrite of the
+    attention q/k projections (both kernels: M = 300 stays on the 128x128 one)."""
+    _, dt, tol = DT["bf16"]
+    N, K, period = 512, 256, 2704 if M > 1000 else 11
+    g = torch.Generator(device="cpu").manual_seed(M)
+    A = torch.randn(M, K, generator=g).to(gpu_device, dt)
+    Wt = (torch.randn(N, K, generator=g) / 16).to(gpu_device, dt)
+    bias = torch.randn(N, generator=g).to(gpu_device)
+    Rp = torch.randn(period, N, generator=g).to(gpu_device, dt)
+    C = torch.zeros(M, N, dtype=dt, device=gpu_device)
+    _gemm("bf16", 0, A, _padded_weight(Wt, 256, dt), M, N, K, K, 256, C, N, bias=bias, R=Rp, ldr=N, r_period=period)
+    ref = A.float() @ Wt.float().t() + bias + Rp.float()[torch.arange(M, device=gpu_device) % period]
+    _close(C, ref, tol)
+
+
+@pytest.mark.parametrize("Cin,Cout,k,s,p", [(64, 64, 3, 1, 1), (64, 128, 1, 1, 0), (32, 256, 3, 2, 1), (8, 64, 7, 2, 3)])
+def test_gemm_large_tile_conv(gpu_device, Cin, Cout, k, s, p):
+    _, dt, tol = DT["bf16"]
+    B = 4
+    H = 130 if s == 1 else 258
+    g = torch.Generator(device="cpu").manual_seed(Cin * k + Cout)
+    x = torch.randn(B, Cin, H, H, generator=g).to(gpu_device, dt)
+    w = (torch.randn(Cout, Cin, k, k, generator=g) / (Cin * k * k) ** 0.5).to(gpu_device, dt)
+    bias = torch.randn(Cout, generator=g).to(gpu_device)
+    ref = F.conv2d(x.float(), w.float(), bias, stride=s, padding=p)
+    Ho = ref.shape[2]
+    K = k * k * Cin
+    ldb = (K + 63) // 64 * 64
+    Wp = _padded_weight(w.permute(0, 2, 3, 1).reshape(Cout, K), ldb, dt)
+    C = torch.zeros(B * Ho * Ho, Cout, dtype=dt, device=gpu_device)
+    _gemm("bf16", 2, x.permute(0, 2, 3, 1).contiguous(), Wp, B * Ho * Ho, Cout, K, 0, ldb, C, Cout, bias=bias,
+          conv=(H, H, Cin, k, k, s, p))
+    _close(C, ref.permute(0, 2, 3, 1).reshape(-1, Cout), tol)
+
+
+def test_gemm_large_tile_head_transposed(gpu_device):
+    _, dt, tol = DT["bf16"]
+    B, T, K, N = 25, 2704, 256, 512
+    M = B * T
+    g = torch.Generator(device="cpu").manual_seed(5)
+    A = torch.randn(M, K, generator=g).to(gpu_device, dt)
+    Wt = (torch.randn(N, K, generator=g) / 16).to(gpu_device, dt)
+    bias = torch.randn(N, generator=g).to(gpu_device)
+    C = torch.zeros(2 * B * 256 * T, dtype=dt, device=gpu_device)
+    _gemm("bf16", 0, A, _padded_weight(Wt, 256, dt), M, N, K, K, 256, C, 8, bias=bias, vt=(T, B))
     ref = (A.float() @ Wt.float().t() + bias).view(B, T, 2, 256).permute(2, 0, 3, 1).reshape(-1)
     _close(C, ref, tol)
 
