@@ -127,6 +127,26 @@ __global__ __launch_bounds__(NT, 1) void gemm2_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // BN = 64 tiles store straight from the accumulators (see the direct epilogue below); the
+  // wider tiles stage their output through LDS for 16-byte row stores, which measured faster
+  // for the store-heavy 256-wide shapes.
+  constexpr bool DIRECT = BN == 64;
+  const int fg = lane >> 4, fr = lane & 15;
+  u32x2 dres[DIRECT ? FM : 1][FN];
+  if constexpr (DIRECT) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j) {
+        dres[i][j] = u32x2{0, 0};
+        const int m = m0 + wr * TM + 16 * i + fr, n = n0 + wc * TN + 16 * j + 4 * fg;
+        if (g.R && m < g.M && n + 4 <= g.N) {
+          const int rm = g.r_period > 0 ? m % g.r_period : m;
+          dres[i][j] = ld8((const bf16*)g.R + (size_t)rm * g.ldr + n);
+        }
+      }
+  }
+
   // ---- residual tile prefetch: this thread's epilogue rows x 8 columns, in registers
   constexpr int TPR = BN / 8;                   // epilogue threads per row (8 columns each)
   constexpr int RSTEP = NT / TPR, RPT = EPI_ROWS / RSTEP, NPASS = BM / EPI_ROWS;
@@ -140,7 +160,7 @@ __global__ __launch_bounds__(NT, 1) void gemm2_kernel(GemmArgs g) {
     for (int q = 0; q < RPT; ++q) {
       rres[pp][q] = u32x4{0, 0, 0, 0};
       const int m = m0 + pp * EPI_ROWS + ert + q * RSTEP;
-      if (g.R && g.vt_T == 0 && efull && m < g.M) {
+      if (!DIRECT && g.R && g.vt_T == 0 && efull && m < g.M) {
         const int rm = g.r_period > 0 ? m % g.r_period : m;
         rres[pp][q] = ld16((const bf16*)g.R + (size_t)rm * g.ldr + en);
       }
@@ -149,7 +169,6 @@ __global__ __launch_bounds__(NT, 1) void gemm2_kernel(GemmArgs g) {
 #pragma unroll
   for (int pp = 0; pp < NPRE; ++pp) fetch_res(pp);
 
-  const int fg = lane >> 4, fr = lane & 15;
   issue(0, 0);
   for (int ks = 0; ks < nk; ++ks) {
     if (ks + 1 < nk) {
@@ -171,11 +190,60 @@ __global__ __launch_bounds__(NT, 1) void gemm2_kernel(GemmArgs g) {
       for (int i = 0; i < FM; ++i)
 #pragma unroll
         for (int j = 0; j < FN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[i]),
-                                                               __builtin_bit_cast(bf16x8, bfr[j]), acc[i][j], 0, 0, 0);
+          // DIRECT: MFMA(W, A) = C^T fragments -> a lane owns 4 consecutive columns of one row
+          acc[i][j] = DIRECT ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bfr[j]),
+                                                                      __builtin_bit_cast(bf16x8, af[i]), acc[i][j], 0, 0, 0)
+                             : __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[i]),
+                                                                      __builtin_bit_cast(bf16x8, bfr[j]), acc[i][j], 0, 0, 0);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();               // stage ks fully read: its buffer may be refilled
+  }
+
+  if constexpr (DIRECT) {
+    // lane holds C[m = 16i + fr][n = 16j + 4fg + r], r = 0..3 -> 8-byte stores
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + wc * TN + 16 * j + 4 * fg;
+      if (n >= g.N) continue;
+      const bool full = n + 4 <= g.N;
+      float bv[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) bv[r] = (g.bias && n + r < g.N) ? g.bias[n + r] : 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const int m = m0 + wr * TM + 16 * i + fr;
+        if (m >= g.M) continue;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bv[r];
+        if (g.R) {
+          if (full) {
+            v[0] += __uint_as_float(dres[i][j].x << 16);
+            v[1] += __uint_as_float(dres[i][j].x & 0xffff0000u);
+            v[2] += __uint_as_float(dres[i][j].y << 16);
+            v[3] += __uint_as_float(dres[i][j].y & 0xffff0000u);
+          } else {
+            const bf16* rp = (const bf16*)g.R + (size_t)(g.r_period > 0 ? m % g.r_period : m) * g.ldr + n;
+            for (int r = 0; r < 4 && n + r < g.N; ++r) v[r] += to_f32(rp[r]);
+          }
+        }
+        if (g.relu) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        }
+        if (g.out_f32) {
+          float* cp = (float*)g.C + (size_t)m * g.ldc + n;
+          if (full) st16(cp, pack16<float>(v));
+          else for (int r = 0; r < 4 && n + r < g.N; ++r) cp[r] = v[r];
+        } else {
+          bf16* cp = (bf16*)g.C + (size_t)m * g.ldc + n;
+          if (full) st8(cp, u32x2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])});
+          else for (int r = 0; r < 4 && n + r < g.N; ++r) cp[r] = from_f32<bf16>(v[r]);
+        }
+      }
+    }
+    return;
   }
 
   // ---- epilogue in 64-row passes through an fp32 LDS tile
@@ -289,7 +357,7 @@ int spe_launch_gemm2(const GemmArgs& g, int mode, hipStream_t s) {
   if (g.K % 8 || g.ldb % 64 || g.lda % 8 || (mode == GEMM_CONV && g.Cin % 8)) return 1;
   if (g.out_f32 ? (g.ldc % 4) : (g.ldc % 8)) return 1;
   if (g.R && g.ldr % 8) return 1;
-  const int bn = g.N <= 64 ? 64 : g.N <= 128 ? 128 : 256;
+  const int bn = (g.N <= 64 && g.vt_T == 0) ? 64 : g.N <= 128 ? 128 : 256;   // BN 64 has no V^T store
   const int tiles = ((g.M + BM - 1) / BM) * ((g.N + bn - 1) / bn);
   if (tiles < 256) return 1;                     // too few tiles to fill 256 CUs: 128x128 kernel
   return bn == 64 ? launch_bn<64>(g, mode, s) : bn == 128 ? launch_bn<128>(g, mode, s) : launch_bn<256>(g, mode, s);
