@@ -192,6 +192,9 @@ __global__ __launch_bounds__(NT, 1) void ffn_ln_kernel(FfnArgs a) {
     const float rs = rsqrtf(q * (1.f / D) + 1e-5f);
     if (!live) continue;
     bf16* yr = (bf16*)a.y + (size_t)m * a.ldy;
+    // optional second output y + pos (the encoder's last layer: the cross-attention K input)
+    const bf16* pr = a.ypos ? (const bf16*)a.pos + (size_t)(m % a.pos_period) * D : nullptr;
+    bf16* ypr = a.ypos ? (bf16*)a.ypos + (size_t)m * a.ldy : nullptr;
 #pragma unroll
     for (int nb = 0; nb < 16; ++nb) {
       const int n = 16 * nb + 4 * g;
@@ -201,6 +204,11 @@ __global__ __launch_bounds__(NT, 1) void ffn_ln_kernel(FfnArgs a) {
 #pragma unroll
       for (int r = 0; r < 4; ++r) o[r] = (acc[nb][mb][r] - mean) * rs * ga[r] + be[r];
       st8(yr + n, u32x2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])});
+      if (ypr) {
+        const u32x2 pv = ld8(pr + n);
+        st8(ypr + n, u32x2{pack_bf16x2(o[0] + __uint_as_float(pv.x << 16), o[1] + __uint_as_float(pv.x & 0xffff0000u)),
+                           pack_bf16x2(o[2] + __uint_as_float(pv.y << 16), o[3] + __uint_as_float(pv.y & 0xffff0000u))});
+      }
     }
   }
 }
@@ -209,6 +217,7 @@ __global__ __launch_bounds__(NT, 1) void ffn_ln_kernel(FfnArgs a) {
 
 int spe_launch_ffn_ln(const FfnArgs& a, hipStream_t s) {
   if (a.M <= 0) return 0;
+  if (a.ypos && (!a.pos || a.pos_period <= 0)) return -5;
   if (a.D != D || a.F % HC || a.F > FMAX || (a.ldx % 8) || (a.ldy % 8) || (a.ld1 % 8) || (a.ld2 % 8)) return -5;
   hipLaunchKernelGGL(ffn_ln_kernel, dim3((a.M + BM - 1) / BM), dim3(NT), 0, s, a);
   return (int)hipGetLastError();

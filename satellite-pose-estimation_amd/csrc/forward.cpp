@@ -71,8 +71,9 @@ GemmArgs linear_args(const Conv& c, const void* A, int lda, int M, void* C, int 
 
 // Fused linear1 -> ReLU -> linear2 -> +residual -> LayerNorm over x (in place), bf16 models.
 int run_ffn(spe_model* m, const char* kind, const Conv& l1, const Conv& l2, const float* g, const float* b,
-            void* x, int M, hipStream_t s) {
+            void* x, int M, hipStream_t s, const void* pos = nullptr, void* ypos = nullptr, int period = 0) {
   FfnArgs a{};
+  a.pos = pos; a.ypos = ypos; a.pos_period = period;
   a.x = x; a.ldx = l1.K;
   a.w1 = l1.w; a.ld1 = l1.Kpad; a.b1 = l1.bias;
   a.w2 = l2.w; a.ld2 = l2.Kpad; a.b2 = l2.bias;
@@ -242,7 +243,9 @@ int spe_forward(spe_model* m, void* stream, const float* images, int B, void* wo
     }
     CK(run_other(m, "ln.enc", 0.0, (double)Mt * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.tmp), e.n1g, e.n1b, P(w.src), nullptr, Mt, d, dt, s); }));
     if (use_fused_ffn(m)) {
-      CK(run_ffn(m, "ffn.enc", e.l1, e.l2, e.n2g, e.n2b, P(w.src), Mt, s));
+      const bool last = &e == &m->enc.back();     // last layer also emits memory + pos
+      CK(run_ffn(m, "ffn.enc", e.l1, e.l2, e.n2g, e.n2b, P(w.src), Mt, s, last ? m->pos : nullptr,
+                 last ? P(w.srcpos) : nullptr, T));
     } else {
       {
         GemmArgs g = linear_args(e.l1, P(w.src), d, Mt, P(w.ffn), ff);
@@ -259,8 +262,11 @@ int spe_forward(spe_model* m, void* stream, const float* images, int B, void* wo
   }
   // memory = src.  Cross-attention K (memory + pos) and V^T (memory) for all decoder layers.
   {
-    GemmArgs g = linear_args(m->crossK, P(w.src), d, Mt, P(w.ck), L * d);
-    const int mode = add_pos(m, g, m->pos, d, T, m->pos_crossK, L * d);
+    // bf16 fused path: the last FFN wrote memory + pos (rounded once, like the reference's
+    // fp32 add) -> plain GEMM; its 8 MB pos.W^T table would not stay L2-resident
+    const bool have_srcpos = use_fused_ffn(m) && !m->enc.empty();
+    GemmArgs g = linear_args(m->crossK, P(have_srcpos ? w.srcpos : w.src), d, Mt, P(w.ck), L * d);
+    const int mode = have_srcpos ? GEMM_LINEAR : add_pos(m, g, m->pos, d, T, m->pos_crossK, L * d);
     CK(run_gemm(m, "gemm.cross_kv", g, mode, s));
   }
   {

@@ -63,8 +63,8 @@ struct ALoader {
     const int k = kstep * BKE + (tid & 7) * CE;
     const bool kv = k < g.K;
     if (MODE == GEMM_CONV) {
-      int kpos = k / g.Cin, ci = k - kpos * g.Cin;
-      int kh = kpos / g.KW, kw = kpos - kh * g.KW;
+      int kh, kw, ci;
+      conv_k_decode(k, g.Cin, g.KW, g.KH * g.KW, kh, kw, ci);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         int ih = ih0[i] + kh, iw = iw0[i] + kw;
@@ -169,6 +169,14 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs g) {
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // epilogue bias, fetched before the K loop (in the epilogue it would add an HBM round trip)
+  float bv[8];
+  {
+    const int n = n0 + (tid & 15) * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bv[e] = (g.bias && n + e < g.N) ? g.bias[n + e] : 0.f;
+  }
+
   u32x4 ra[4], rb[4];
   al.load(g, 0, tid, ra);
   load_b<T>(g, n0, 0, tid, rb);
@@ -234,9 +242,6 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs g) {
   const int cg = (tid & 15) * 8;
   const int n = n0 + cg;
   if (n >= g.N) return;
-  float bv[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) bv[e] = (g.bias && n + e < g.N) ? g.bias[n + e] : 0.f;
   const bool full = n + 8 <= g.N;
   for (int rr = tid >> 4; rr < BM; rr += 16) {
     const int m = m0 + rr;

@@ -98,8 +98,8 @@ __global__ __launch_bounds__(NT, 1) void gemm2_kernel(GemmArgs g) {
     const int k = ks * BK + chunk * 8;
     const bool kv = k < g.K;
     if constexpr (MODE == GEMM_CONV) {
-      const int kpos = k / g.Cin, ci = k - kpos * g.Cin;
-      const int kh = kpos / g.KW, kw = kpos - kh * g.KW;
+      int kh, kw, ci;
+      conv_k_decode(k, g.Cin, g.KW, g.KH * g.KW, kh, kw, ci);
 #pragma unroll
       for (int i = 0; i < IA; ++i) {
         const int ih = aih[i] + kh, iw = aiw[i] + kw;
@@ -133,7 +133,16 @@ __global__ __launch_bounds__(NT, 1) void gemm2_kernel(GemmArgs g) {
   constexpr bool DIRECT = BN == 64;
   const int fg = lane >> 4, fr = lane & 15;
   u32x2 dres[DIRECT ? FM : 1][FN];
+  f32x4 dbias[DIRECT ? FN : 1];
   if constexpr (DIRECT) {
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      const int n = n0 + wc * TN + 16 * j + 4 * fg;
+      dbias[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (g.bias && n + 4 <= g.N) dbias[j] = *reinterpret_cast<const f32x4*>(g.bias + n);
+      else if (g.bias)
+        for (int r = 0; r < 4; ++r) dbias[j][r] = n + r < g.N ? g.bias[n + r] : 0.f;
+    }
 #pragma unroll
     for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -168,6 +177,16 @@ __global__ __launch_bounds__(NT, 1) void gemm2_kernel(GemmArgs g) {
   };
 #pragma unroll
   for (int pp = 0; pp < NPRE; ++pp) fetch_res(pp);
+  // the bias too: a load in the epilogue would cost one more HBM round trip per tile
+  float ebias[8];
+  if (!DIRECT && g.bias && efull) {
+    const f32x4 b0 = *reinterpret_cast<const f32x4*>(g.bias + en), b1 = *reinterpret_cast<const f32x4*>(g.bias + en + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { ebias[e] = b0[e]; ebias[4 + e] = b1[e]; }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) ebias[e] = (!DIRECT && g.bias && en + e < g.N) ? g.bias[en + e] : 0.f;
+  }
 
   issue(0, 0);
   for (int ks = 0; ks < nk; ++ks) {
@@ -207,9 +226,7 @@ __global__ __launch_bounds__(NT, 1) void gemm2_kernel(GemmArgs g) {
       const int n = n0 + wc * TN + 16 * j + 4 * fg;
       if (n >= g.N) continue;
       const bool full = n + 4 <= g.N;
-      float bv[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) bv[r] = (g.bias && n + r < g.N) ? g.bias[n + r] : 0.f;
+      const f32x4 bv = dbias[j];                  // loaded before the K loop
 #pragma unroll
       for (int i = 0; i < FM; ++i) {
         const int m = m0 + wr * TM + 16 * i + fr;
@@ -289,9 +306,7 @@ __global__ __launch_bounds__(NT, 1) void gemm2_kernel(GemmArgs g) {
       const int cg = ecg, n = en;
       if (n < g.N) {
         const bool full = efull;
-        float bv[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) bv[e] = (g.bias && n + e < g.N) ? g.bias[n + e] : 0.f;
+        const float* bv = ebias;
 #pragma unroll
         for (int q = 0; q < RPT; ++q) {
           const int rr = ert + q * RSTEP, m = m0 + r0 + rr;

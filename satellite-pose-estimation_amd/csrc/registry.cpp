@@ -160,12 +160,15 @@ Conv make_conv(spe_model* m, const std::string& wkey, const std::string& bnkey, 
   const int cp = cin_pad > 0 ? cin_pad : (int)cin;
   const int K = (int)(kh * kw * cp);
   std::vector<float> rows((size_t)cout * K, 0.f);
+  const bool cblk = conv_channel_blocked(cp, (int)(kh * kw));   // K order: spe_kernels.h
   for (int64_t co = 0; co < cout; ++co)
     for (int64_t ci = 0; ci < cin; ++ci)
       for (int64_t y = 0; y < kh; ++y)
-        for (int64_t x = 0; x < kw; ++x)
-          rows[(size_t)co * K + (y * kw + x) * cp + ci] =
-              (float)(spec_w[((co * cin + ci) * kh + y) * kw + x] * scale[co]);
+        for (int64_t x = 0; x < kw; ++x) {
+          const int64_t tap = y * kw + x;
+          const int64_t k = cblk ? ((ci / 64) * kh * kw + tap) * 64 + ci % 64 : tap * cp + ci;
+          rows[(size_t)co * K + k] = (float)(spec_w[((co * cin + ci) * kh + y) * kw + x] * scale[co]);
+        }
   std::vector<float> bias(shift.begin(), shift.end());
   Conv c;
   c.N = (int)cout; c.K = K; c.Kpad = pad64(K); c.Cin = cp; c.KH = (int)kh; c.KW = (int)kw; c.stride = stride; c.pad = pad;
@@ -351,6 +354,7 @@ Ws spe_plan(const spe_model* m, int B) {
   w.cat = take((size_t)B * H8 * H8 * 512 * E);
   w.neck = take((size_t)B * H8 * H8 * 512 * E);
   w.src = take((size_t)B * T * d * E);
+  w.srcpos = take((size_t)B * T * d * E);   // memory + pos (bf16 fused path: cross-attention K input)
   w.qkv = take((size_t)B * T * 3 * d * E);
   w.vt = take((size_t)B * T * d * E);
   w.ao = take((size_t)B * T * d * E);

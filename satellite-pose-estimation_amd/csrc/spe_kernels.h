@@ -22,6 +22,26 @@ struct GemmArgs {
   int r_period;                    // >0: residual row = m % r_period (row-periodic add, e.g. pos . W^T)
 };
 int spe_launch_gemm(const GemmArgs& g, int dtype, int mode, hipStream_t s);
+
+// Implicit-GEMM conv K order.  Multi-tap convs with Cin % 64 == 0 use channel-block-major order
+// k = ((ci / 64) * KH*KW + tap) * 64 + ci % 64, so one 64-channel slice of the input window is
+// reused by all taps in consecutive K-steps (L2-resident) instead of the whole Cin-deep window
+// being streamed once per tap; other convs use k = tap * Cin + ci.  Weights are packed to match
+// (registry.cpp make_conv).
+__host__ __device__ inline bool conv_channel_blocked(int Cin, int taps) { return (Cin & 63) == 0 && taps > 1; }
+__device__ __forceinline__ void conv_k_decode(int k, int Cin, int KW, int taps, int& kh, int& kw, int& ci) {
+  int tap;
+  if (conv_channel_blocked(Cin, taps)) {
+    const int cb = k / (64 * taps), rem = k - cb * 64 * taps;
+    tap = rem >> 6;
+    ci = cb * 64 + (rem & 63);
+  } else {
+    tap = k / Cin;
+    ci = k - tap * Cin;
+  }
+  kh = tap / KW;
+  kw = tap - kh * KW;
+}
 int spe_launch_gemm2(const GemmArgs& g, int mode, hipStream_t s);   // 1 = not applicable
 
 struct AttnArgs {
@@ -45,6 +65,8 @@ struct FfnArgs {
   const float* gamma; const float* beta;   // LayerNorm affine [256]
   void* y; int ldy;                // [M][256] bf16
   int M, D, F;
+  const void* pos; void* ypos;     // optional: ypos = y + pos[m % pos_period] (bf16 [M][256])
+  int pos_period;
 };
 int spe_launch_ffn_ln(const FfnArgs& a, hipStream_t s);
 

@@ -65,6 +65,37 @@ def main():
         ms = timeit(fn, a.iters)
         fl = 4.0 * B * T * D * F
         print(f"ffn.enc   {ms:.3f} ms  {fl / ms / 1e9:.1f} TF/s")
+    if a.which in ("gemm", "all"):
+        # name, mode, M, N, K, residual rows (0 none, -1 full, >0 period), conv geometry
+        cases = [("l1.c3 1x1+res", 0, B * 104 * 104, 256, 64, -1, None),
+                 ("l1.c3 1x1 nores", 0, B * 104 * 104, 256, 64, 0, None),
+                 ("l1.c3 N128+res", 0, B * 104 * 104, 128, 64, -1, None),
+                 ("l1.c1 1x1", 0, B * 104 * 104, 64, 256, 0, None),
+                 ("enc.qk +posW", 0, B * T, 512, 256, T, None),
+                 ("cross_k +posW", 0, B * T, 1536, 256, T, None),
+                 ("enc.o +res", 0, B * T, 256, 256, -1, None),
+                 ("neck s16 3x3", 2, B * T, 256, 9 * 1024, 0, (52, 52, 1024, 3, 3, 1, 1)),
+                 ("l1 3x3", 2, B * 104 * 104, 64, 9 * 64, 0, (104, 104, 64, 3, 3, 1, 1))]
+        for name, mode, M, N, K, rr, conv in cases:
+            if conv:
+                H, W, Cin, KH, KW, st, pd = conv
+                A = torch.randn(B, H, W, Cin, generator=g).to(dev, torch.bfloat16)
+            else:
+                H = W = Cin = 0; KH = KW = st = 1; pd = 0
+                A = torch.randn(M, K, generator=g).to(dev, torch.bfloat16)
+            ldb = (K + 63) // 64 * 64
+            Wt = (torch.randn(N, ldb, generator=g) / K ** 0.5).to(dev, torch.bfloat16)
+            bias = torch.zeros(N, device=dev)
+            R = None if rr == 0 else torch.randn(M if rr < 0 else rr, N, generator=g).to(dev, torch.bfloat16)
+            C = torch.empty(M, N, dtype=torch.bfloat16, device=dev)
+            rp = 0 if rr <= 0 else rr
+            fn = lambda: L.spe_debug_gemm(None, 0, mode, p(A), K if not conv else 0, None, 0, 1, H, W, Cin, KH, KW,
+                                          st, pd, p(Wt), ldb, M, N, K, p(bias), p(R) if R is not None else None,
+                                          N, 1, p(C), N, 0, 0, 0, rp)
+            ms = timeit(fn, a.iters)
+            abytes = (B * H * W * Cin if conv else M * K) * 2
+            byts = abytes + N * ldb * 2 + M * N * 2 + (0 if R is None else R.numel() * 2)
+            print(f"{name:16s} {ms:.3f} ms  {2.0 * M * N * K / ms / 1e9:7.1f} TF/s  {byts / ms / 1e9:6.2f} TB/s")
 
 
 if __name__ == "__main__":

@@ -47,6 +47,16 @@ def _padded_weight(Wt, ldb, dt):
     return Wp
 
 
+def _pack_conv(w):
+    """[Cout][Cin][kh][kw] -> [Cout][K] in the kernels' K order (spe_kernels.h conv_k_decode):
+    channel-block-major ([Cin/64][kh][kw][64]) for multi-tap convs with Cin % 64 == 0, else
+    [kh][kw][Cin]."""
+    Cout, Cin, kh, kw = w.shape
+    if Cin % 64 == 0 and kh * kw > 1:
+        return w.reshape(Cout, Cin // 64, 64, kh, kw).permute(0, 1, 3, 4, 2).reshape(Cout, -1)
+    return w.permute(0, 2, 3, 1).reshape(Cout, -1)
+
+
 @pytest.mark.parametrize("dtype", ["bf16", "fp32"])
 @pytest.mark.parametrize("M,N,K", [(300, 200, 256), (128, 64, 64), (77, 520, 2048), (5, 12, 192)])
 def test_gemm_linear_epilogue(gpu_device, dtype, M, N, K):
@@ -83,7 +93,8 @@ def test_gemm_linear_add_and_f32_out(gpu_device, dtype):
 
 @pytest.mark.parametrize("dtype", ["bf16", "fp32"])
 @pytest.mark.parametrize("B,H,W,Cin,Cout,k,s,p", [(2, 13, 11, 16, 72, 3, 2, 1), (1, 20, 20, 8, 64, 7, 2, 3),
-                                                  (3, 9, 9, 64, 130, 1, 2, 0), (2, 10, 10, 32, 40, 3, 1, 1)])
+                                                  (3, 9, 9, 64, 130, 1, 2, 0), (2, 10, 10, 32, 40, 3, 1, 1),
+                                                  (2, 12, 12, 128, 96, 3, 1, 1), (1, 9, 9, 192, 64, 3, 2, 1)])
 def test_gemm_conv_nhwc(gpu_device, dtype, B, H, W, Cin, Cout, k, s, p):
     _, dt, tol = DT[dtype]
     g = torch.Generator(device="cpu").manual_seed(B * H + Cout)
@@ -94,7 +105,7 @@ def test_gemm_conv_nhwc(gpu_device, dtype, B, H, W, Cin, Cout, k, s, p):
     Ho, Wo = ref.shape[2], ref.shape[3]
     K = k * k * Cin
     ldb = (K + 63) // 64 * 64
-    Wp = _padded_weight(w.permute(0, 2, 3, 1).reshape(Cout, K), ldb, dt)
+    Wp = _padded_weight(_pack_conv(w), ldb, dt)
     xn = x.permute(0, 2, 3, 1).contiguous()
     ldc = (Cout + 7) // 8 * 8
     C = torch.zeros(B * Ho * Wo, ldc, dtype=dt, device=gpu_device)
@@ -157,7 +168,8 @@ def test_gemm_row_periodic_residual(gpu_device, M):
     _close(C, ref, tol)
 
 
-@pytest.mark.parametrize("Cin,Cout,k,s,p", [(64, 64, 3, 1, 1), (64, 128, 1, 1, 0), (32, 256, 3, 2, 1), (8, 64, 7, 2, 3)])
+@pytest.mark.parametrize("Cin,Cout,k,s,p", [(64, 64, 3, 1, 1), (64, 128, 1, 1, 0), (32, 256, 3, 2, 1), (8, 64, 7, 2, 3),
+                                            (128, 256, 3, 2, 1)])
 def test_gemm_large_tile_conv(gpu_device, Cin, Cout, k, s, p):
     _, dt, tol = DT["bf16"]
     B = 4
@@ -170,7 +182,7 @@ def test_gemm_large_tile_conv(gpu_device, Cin, Cout, k, s, p):
     Ho = ref.shape[2]
     K = k * k * Cin
     ldb = (K + 63) // 64 * 64
-    Wp = _padded_weight(w.permute(0, 2, 3, 1).reshape(Cout, K), ldb, dt)
+    Wp = _padded_weight(_pack_conv(w), ldb, dt)
     C = torch.zeros(B * Ho * Ho, Cout, dtype=dt, device=gpu_device)
     _gemm("bf16", 2, x.permute(0, 2, 3, 1).contiguous(), Wp, B * Ho * Ho, Cout, K, 0, ldb, C, Cout, bias=bias,
           conv=(H, H, Cin, k, k, s, p))
