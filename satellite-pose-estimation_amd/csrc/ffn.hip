@@ -7,7 +7,7 @@
 // [rows x 2048] hidden activation never leaves registers: per 128-row block each wave owns 32
 // rows and keeps its x rows (as MFMA B fragments) and its 256 output columns (as transposed
 // accumulators out^T[n][m]) in registers while the block streams W1/W2 in chunks of 32 hidden
-// units through LDS:
+// units through a three-slot LDS ring filled by global_load_lds (two chunks in flight):
 //     H^T[j][m] = W1[j][:] . x[m][:]                 16x16x32 MFMAs, K = 256
 //     out^T[n][m] += W2[n][j] . relu(H^T + b1)[j][m]   16x16x32 MFMAs, K = 32; the H^T accumulator
 //                                                    is re-packed in registers as the B operand
@@ -28,56 +28,53 @@ constexpr int D = 256;
 constexpr int W1_BYTES = HC * D * 2;    // 16 KiB: W1[j][d], 32 rows of 512 B
 constexpr int W2_BYTES = D * HC * 2;    // 16 KiB: W2[n][j], 256 rows of 64 B
 constexpr int STAGE = W1_BYTES + W2_BYTES;
+constexpr int NSTAGE = 3;               // ring: chunk ch in use, ch+1 landing, ch+2 in flight
 constexpr int FMAX = 4096;              // largest dim_feedforward (b1 staged in LDS)
+constexpr int LOADS = (W1_BYTES + W2_BYTES) / 1024 / 4;   // DMA wave-instructions per wave per chunk
 
-// W1 chunk: 16-byte chunk c (of 32 per row) lives at slot c ^ (row & 15)
-SPE_DEV int w1_off(int row, int c) { return row * 512 + ((c ^ (row & 15)) << 4); }
-// W2 chunk: 8-byte unit u (of 8 per row) lives at slot u ^ ((row >> 1) & 7): the 16 rows one
-// ds_read_b64 / ds_read2_b64 lane group touches land on 16 distinct 8-byte bank pairs
-SPE_DEV int w2_key(int row) { return (row >> 1) & 7; }
-SPE_DEV int w2_off(int row, int u) { return row * 64 + ((u ^ w2_key(row)) << 3); }
+// Hidden-unit order inside a chunk.  Phase 1 computes H^T in two 16-row MFMA blocks; LDS row
+// R of the W1 stage holds hidden unit P(R) = 8*((R&15)>>2) + 4*(R>>4) + (R&3), so lane group g
+// ends up owning the 8 CONSECUTIVE hidden units 8g..8g+7 of the chunk: its B operand for phase
+// 2 packs in order, its bias is one 32-byte read and its W2 A operand is one 16-byte read.
+SPE_DEV int w1_src_row(int R) { return 8 * ((R & 15) >> 2) + 4 * (R >> 4) + (R & 3); }
+// W1 stage: 16-byte chunk c of LDS row R at slot c ^ (R & 15) (conflict-free ds_read_b128)
+SPE_DEV int w1_off(int R, int c) { return R * 512 + ((c ^ (R & 15)) << 4); }
+// W2 stage: 16-byte chunk c (hidden 8c..8c+7) of row n at slot c ^ key(n), key = -(n>>2) & 3:
+// each ds_read_b128 lane group's 16 reads hit 16 distinct 16-byte bank groups
+SPE_DEV int w2_key(int n) { return (4 - ((n >> 2) & 3)) & 3; }
+SPE_DEV int w2_off(int n, int c) { return n * 64 + ((c ^ w2_key(n)) << 4); }
 
-struct Staged {
-  u32x4 w1[4], w2[4];
-  SPE_DEV void load(const FfnArgs& a, int chunk, int tid) {
-    const char* W1 = (const char*)a.w1 + (size_t)(chunk * HC) * a.ld1 * 2;
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+template <int N>
+SPE_DEV void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+
+// One chunk's weights, global -> LDS directly (global_load_lds, 16 B per lane, linear LDS
+// image per wave-instruction; the swizzles above are applied on the source side).
+SPE_DEV void issue_chunk(const FfnArgs& a, int ch, char* st, int wid, int lane) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {               // 32 rows x 32 chunks
-      const int idx = tid + i * NT, row = idx >> 5, c = idx & 31;
-      w1[i] = ld16(W1 + ((size_t)row * a.ld1 + c * 8) * 2);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {               // 256 rows x 4 chunks of 16 B
-      const int idx = tid + i * NT, row = idx >> 2, c = idx & 3;
-      w2[i] = ld16((const char*)a.w2 + ((size_t)row * a.ld2 + chunk * HC + c * 8) * 2);
-    }
+  for (int i = 0; i < 4; ++i) {                 // W1: 16 instructions x 2 rows of 512 B
+    const int ins = wid * 4 + i, R = 2 * ins + (lane >> 5), c = (lane & 31) ^ (R & 15);
+    const char* src = (const char*)a.w1 + ((size_t)(ch * HC + w1_src_row(R)) * a.ld1 + c * 8) * 2;
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(st + ins * 1024), 16, 0, 0);
   }
-  SPE_DEV void store(char* st, int tid) const {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int idx = tid + i * NT, row = idx >> 5, c = idx & 31;
-      st16(st + w1_off(row, c), w1[i]);
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int idx = tid + i * NT, row = idx >> 2, c = idx & 3;
-      // units 2c, 2c+1 land in one aligned slot pair, swapped when the row key is odd
-      const bool swap = w2_key(row) & 1;
-      const u32x4 v = swap ? u32x4{w2[i].z, w2[i].w, w2[i].x, w2[i].y} : w2[i];
-      st16(st + W1_BYTES + (w2_off(row, 2 * c) & ~15), v);
-    }
+  for (int i = 0; i < 4; ++i) {                 // W2: 16 instructions x 16 rows of 64 B
+    const int ins = wid * 4 + i, n = 16 * ins + (lane >> 2), c = (lane & 3) ^ w2_key(n);
+    const char* src = (const char*)a.w2 + ((size_t)n * a.ld2 + ch * HC + c * 8) * 2;
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(st + W1_BYTES + ins * 1024), 16, 0, 0);
   }
-};
+}
 
 __global__ __launch_bounds__(NT, 1) void ffn_ln_kernel(FfnArgs a) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE];
-  __shared__ __attribute__((aligned(16))) float sb1[FMAX];
+  // one LDS array (a second __shared__ object beside in-flight global_load_lds can make the
+  // compiler drain vmcnt before LDS reads): [NSTAGE weight stages][b1]
+  __shared__ __attribute__((aligned(1024))) char lds[NSTAGE * STAGE + FMAX * 4];
+  float* sb1 = reinterpret_cast<float*>(lds + NSTAGE * STAGE);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  // b1 lives in LDS: a global load inside the chunk loop would make the wave wait (vmcnt is
-  // in-order) for the next chunk's weight prefetch issued just before it.
-  for (int i = tid; i < a.F; i += NT) sb1[i] = a.b1[i];
   const int g = lane >> 4, c16 = lane & 15;
   const int m0 = blockIdx.x * BM + wid * 32;
+  const int nchunks = a.F / HC;
+  for (int i = tid; i < a.F; i += NT) sb1[i] = a.b1[i];
 
   // x rows of this wave as B fragments: xf[mb][ks] = x[m0 + 16mb + c16][32ks + 8g .. +7]
   bf16x8 xf[2][8];
@@ -92,32 +89,44 @@ __global__ __launch_bounds__(NT, 1) void ffn_ln_kernel(FfnArgs a) {
   f32x4 acc[16][2];
 #pragma unroll
   for (int nb = 0; nb < 16; ++nb) { acc[nb][0] = f32x4{0, 0, 0, 0}; acc[nb][1] = f32x4{0, 0, 0, 0}; }
+  // x (and b1) must have landed before the weight DMA starts: vmcnt is in-order, and with a load
+  // of x still pending at the loop entry the compiler's merged wait state would drain every
+  // in-flight chunk at the first MFMA of each step.  (An asm use of every x register makes the
+  // compiler itself retire those loads here; an inline-asm s_waitcnt is invisible to it.)
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) asm volatile("" ::"v"(xf[mb][ks]));
+  wait_vmcnt<0>();
+  issue_chunk(a, 0, lds, wid, lane);
+  if (nchunks > 1) issue_chunk(a, 1, lds + STAGE, wid, lane);
 
-  const int nchunks = a.F / HC;
-  Staged stg;
-  stg.load(a, 0, tid);
-  stg.store(smem, tid);
-  __syncthreads();
+  int slot = 0;
   for (int ch = 0; ch < nchunks; ++ch) {
-    const char* st = smem + (ch & 1) * STAGE;
-    const bool more = ch + 1 < nchunks;
-    if (more) stg.load(a, ch + 1, tid);
-    // All of this chunk's LDS operand reads are issued up front (one wave per SIMD: nothing else
-    // hides LDS latency); the phase-2 W2 reads land while the phase-1 MFMAs run.
-    u32x4 wa[8][2];
-    u32x2 wlo[16], whi[16];
+    // retire chunk ch (this wave's loads; chunk ch+1 may stay in flight), then the barrier makes
+    // every wave's part visible and guarantees slot (ch+2)%3 -- read in step ch-1 -- is free
+    if (ch + 1 < nchunks) wait_vmcnt<LOADS>();
+    else wait_vmcnt<0>();
+    // raw barrier: __syncthreads' fence would also drain the chunk still in flight
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const int slot2 = slot == 0 ? 2 : slot - 1;    // (ch + 2) % 3
+    const char* st = lds + slot * STAGE;
+    slot = slot == 2 ? 0 : slot + 1;
+    // all of this chunk's fragment reads up front (one wave per SIMD: nothing else hides LDS
+    // latency); the W2 reads land while the phase-1 MFMAs run
+    u32x4 wa[8][2], wb[16];
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks)
 #pragma unroll
       for (int jb = 0; jb < 2; ++jb) wa[ks][jb] = ld16(st + w1_off(16 * jb + c16, 4 * ks + g));
 #pragma unroll
-    for (int nb = 0; nb < 16; ++nb) {
-      const int row = 16 * nb + c16;
-      wlo[nb] = ld8(st + W1_BYTES + w2_off(row, g));        // j = 4g .. 4g+3
-      whi[nb] = ld8(st + W1_BYTES + w2_off(row, 4 + g));    // j = 16+4g .. +3
-    }
+    for (int nb = 0; nb < 16; ++nb) wb[nb] = ld16(st + W1_BYTES + w2_off(16 * nb + c16, g));
+    // chunk ch+2's loads go out after this chunk's LDS reads: issued before them, the compiler
+    // (which cannot tell the DMA's slot from the read's) would drain them first
+    if (ch + 2 < nchunks) issue_chunk(a, ch + 2, lds + slot2 * STAGE, wid, lane);
     __builtin_amdgcn_sched_barrier(0);
-    // ---- H^T chunk: [32 j][32 m] = W1[j] . x[m]
+    // ---- H^T chunk: [32 j][32 m] = W1[j] . x[m]   (LDS row 16jb + 4g + r = hidden 8g + 4jb + r)
     f32x4 h[2][2];
 #pragma unroll
     for (int jb = 0; jb < 2; ++jb) { h[jb][0] = f32x4{0, 0, 0, 0}; h[jb][1] = f32x4{0, 0, 0, 0}; }
@@ -130,9 +139,9 @@ __global__ __launch_bounds__(NT, 1) void ffn_ln_kernel(FfnArgs a) {
         h[jb][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, xf[1][ks], h[jb][1], 0, 0, 0);
       }
     }
-    // ---- bias + ReLU, repack as the K=32 B operand: element e <- hidden 4g+e (e<4), 16+4g+e-4
-    const f32x4 b1a = *reinterpret_cast<const f32x4*>(sb1 + ch * HC + 4 * g);
-    const f32x4 b1b = *reinterpret_cast<const f32x4*>(sb1 + ch * HC + 16 + 4 * g);
+    // ---- bias + ReLU, pack as the K=32 B operand: element e <-> hidden 8g + e of the chunk
+    const f32x4 b1a = *reinterpret_cast<const f32x4*>(sb1 + ch * HC + 8 * g);
+    const f32x4 b1b = *reinterpret_cast<const f32x4*>(sb1 + ch * HC + 8 * g + 4);
     bf16x8 hb[2];
 #pragma unroll
     for (int mb = 0; mb < 2; ++mb) {
@@ -144,15 +153,13 @@ __global__ __launch_bounds__(NT, 1) void ffn_ln_kernel(FfnArgs a) {
       }
       hb[mb] = __builtin_bit_cast(bf16x8, pack16<bf16>(v));
     }
-    // ---- out^T[n][m] += W2[n][chunk j] . H^T[j][m]
+    // ---- out^T[n][m] += W2[n][chunk 8g..8g+7] . H^T[8g..8g+7][m]
 #pragma unroll
     for (int nb = 0; nb < 16; ++nb) {
-      const bf16x8 wb = __builtin_bit_cast(bf16x8, u32x4{wlo[nb].x, wlo[nb].y, whi[nb].x, whi[nb].y});
-      acc[nb][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb, hb[0], acc[nb][0], 0, 0, 0);
-      acc[nb][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wb, hb[1], acc[nb][1], 0, 0, 0);
+      const bf16x8 w = __builtin_bit_cast(bf16x8, wb[nb]);
+      acc[nb][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, hb[0], acc[nb][0], 0, 0, 0);
+      acc[nb][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, hb[1], acc[nb][1], 0, 0, 0);
     }
-    if (more) stg.store(smem + ((ch + 1) & 1) * STAGE, tid);
-    __syncthreads();
   }
 
   // ---- epilogue: + b2 + residual, LayerNorm over n, bf16 store.  Lane holds, for each of its
