@@ -23,6 +23,9 @@ REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "satellite-pose-estimation_amd"))
 
 PEAK = {"bf16": {"mfma": 2500.0}, "fp32": {"mfma": 157.3}, "hbm": 8000.0}   # TFLOP/s, GB/s (MI355X_MICROARCH.md)
+# profiler symbol of each launch class (to match profiles/*kernel_stats.csv rows)
+KIND_SYMBOL = {"attn.enc": "attn_bf16_kernel<0>", "attn.dec_self": "attn_bf16_kernel<1>",
+               "attn.dec_cross": "attn_bf16_kernel<1>", "ffn.enc": "ffn_ln_kernel", "ffn.dec": "ffn_ln_kernel"}
 
 
 def parse():
@@ -107,14 +110,17 @@ def main():
     B = args.batch
 
     def hs_fn(w, images):
-        # calibration pass of the HIP model itself (see spe.synthetic.bench_weights)
+        # calibration pass of the HIP model itself (see spe.synthetic.bench_weights), run at the
+        # bench batch size so every launch in this process has the timed shape (profiler
+        # per-kernel averages then match the in-bench event timings)
         m = DETR(cfg, dtype=args.dtype)
         m.load_state_dict(w)
-        out = []
-        for i in range(0, len(images), 8):
-            out.append(m(torch.from_numpy(images[i:i + 8]).to(dev), return_hs=True)["hs"].cpu().numpy())
+        n = len(images)
+        reps = (B + n - 1) // n
+        x = torch.from_numpy(np.concatenate([images] * reps)[:B]).to(dev)
+        hs = m(x, return_hs=True)["hs"].cpu().numpy()[:n]
         del m
-        return np.concatenate(out)
+        return hs
 
     model = DETR(cfg, dtype=args.dtype)
     model.load_state_dict(bench_weights(cfg, 0, hs_fn) if args.weights == "label-diverse" else random_weights(cfg, 0))
@@ -219,7 +225,8 @@ def main():
                                f"{args.queries} queries, {args.size}x{args.size}, solver={args.solver}",
                    "global_batch": B * world, "per_gpu_batch": B, "input_size": args.size,
                    "num_queries": args.queries, "parallelism": f"dp{world} (image sharding)"},
-        "roofline": {"kernel": dominant, "bound": "mfma" if mfma_bound else "hbm", "achieved": achieved,
+        "roofline": {"kernel": dominant, "kernel_symbol": KIND_SYMBOL.get(dominant, dominant),
+                     "bound": "mfma" if mfma_bound else "hbm", "achieved": achieved,
                      "peak": peak, "unit": unit, "frac": achieved / peak,
                      "traffic": traffic_for(dominant), "launches": k_n, "avg_launch_ms": avg_ms,
                      "algorithmic_flops_per_launch": k_fl / max(k_n, 1),

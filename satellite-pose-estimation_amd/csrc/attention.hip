@@ -150,6 +150,9 @@ SPE_DEV float tile_max(f32x16& s0, f32x16& s1, int key_base, int Tk, int hh) {
 }
 
 // ------------------------------------------------------------------ bf16 kernel
+// ROLE only separates the symbols of the token-query (encoder self-attention) and the
+// object-query (decoder) launches so profiler summaries report them apart; the code is shared.
+template <int ROLE>
 __global__ __launch_bounds__(NT, 4) void attn_bf16_kernel(AttnArgs a) {
   constexpr int KBYTES = KT * KROW, VBYTES = 32 * VROW;
   __shared__ __attribute__((aligned(16))) char smem[2 * (KBYTES + VBYTES)];
@@ -374,7 +377,10 @@ int spe_launch_attention(const AttnArgs& a, int dtype, hipStream_t s) {
   if ((a.ldq % ce) || (a.ldk % ce) || (a.ldo % 4)) return -5;
   dim3 grid(a.B * a.H * ((a.Tq + 127) / 128)), block(NT);
   if (dtype == SPE_DTYPE_BF16)
-    hipLaunchKernelGGL(attn_bf16_kernel, grid, block, 0, s, a);
+    if (a.Tq >= 128)
+      hipLaunchKernelGGL(attn_bf16_kernel<0>, grid, block, 0, s, a);
+    else
+      hipLaunchKernelGGL(attn_bf16_kernel<1>, grid, block, 0, s, a);
   else
     hipLaunchKernelGGL(attn_f32_kernel, grid, block, 0, s, a);
   return (int)hipGetLastError();
