@@ -43,10 +43,11 @@ int spe_debug_layernorm(void* stream, int dtype, const void* x, const float* gam
 
 int spe_debug_ffn(void* stream, const void* x, int ldx, const void* w1, int ld1, const float* b1, const void* w2,
                   int ld2, const float* b2, const float* gamma, const float* beta, void* y, int ldy, int M, int D,
-                  int F) {
+                  int F, float* partial, int splits) {
   FfnArgs a{};
   a.x = x; a.ldx = ldx; a.w1 = w1; a.ld1 = ld1; a.b1 = b1; a.w2 = w2; a.ld2 = ld2; a.b2 = b2;
   a.gamma = gamma; a.beta = beta; a.y = y; a.ldy = ldy; a.M = M; a.D = D; a.F = F;
+  a.partial = partial; a.splits = splits;
   int rc = spe_launch_ffn_ln(a, (hipStream_t)stream);
   return rc < 0 ? spe_fail(SPE_E_LAUNCH, "ffn launch rejected its arguments") : rc;
 }

@@ -72,8 +72,13 @@ __global__ __launch_bounds__(NT, 1) void ffn_ln_kernel(FfnArgs a) {
   float* sb1 = reinterpret_cast<float*>(lds + NSTAGE * STAGE);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int g = lane >> 4, c16 = lane & 15;
-  const int m0 = blockIdx.x * BM + wid * 32;
-  const int nchunks = a.F / HC;
+  // split-F mode (few rows, e.g. the decoder's B*Q): block = (row tile, hidden-unit range);
+  // the partial out^T of each range goes to a.partial and ffn_reduce_ln_kernel finishes
+  const int S = a.partial ? a.splits : 1;
+  const int split = blockIdx.x % S;
+  const int m0 = (blockIdx.x / S) * BM + wid * 32;
+  const int cps = a.F / HC / S;
+  const int cbeg = split * cps, nchunks = cbeg + cps;   // chunk range [cbeg, nchunks)
   for (int i = tid; i < a.F; i += NT) sb1[i] = a.b1[i];
 
   // x rows of this wave as B fragments: xf[mb][ks] = x[m0 + 16mb + c16][32ks + 8g .. +7]
@@ -98,11 +103,11 @@ __global__ __launch_bounds__(NT, 1) void ffn_ln_kernel(FfnArgs a) {
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) asm volatile("" ::"v"(xf[mb][ks]));
   wait_vmcnt<0>();
-  issue_chunk(a, 0, lds, wid, lane);
-  if (nchunks > 1) issue_chunk(a, 1, lds + STAGE, wid, lane);
+  issue_chunk(a, cbeg, lds, wid, lane);
+  if (cbeg + 1 < nchunks) issue_chunk(a, cbeg + 1, lds + STAGE, wid, lane);
 
   int slot = 0;
-  for (int ch = 0; ch < nchunks; ++ch) {
+  for (int ch = cbeg; ch < nchunks; ++ch) {
     // retire chunk ch (this wave's loads; chunk ch+1 may stay in flight), then the barrier makes
     // every wave's part visible and guarantees slot (ch+2)%3 -- read in step ch-1 -- is free
     if (ch + 1 < nchunks) wait_vmcnt<LOADS>();
@@ -160,6 +165,18 @@ __global__ __launch_bounds__(NT, 1) void ffn_ln_kernel(FfnArgs a) {
       acc[nb][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, hb[0], acc[nb][0], 0, 0, 0);
       acc[nb][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, hb[1], acc[nb][1], 0, 0, 0);
     }
+  }
+
+  if (a.partial) {                              // split-F: raw partial sums, finished elsewhere
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+      const int m = m0 + 16 * mb + c16;
+      if (m >= a.M) continue;
+      float* pr = a.partial + ((size_t)split * a.M + m) * D;
+#pragma unroll
+      for (int nb = 0; nb < 16; ++nb) st16(pr + 16 * nb + 4 * g, __builtin_bit_cast(u32x4, acc[nb][mb]));
+    }
+    return;
   }
 
   // ---- epilogue: + b2 + residual, LayerNorm over n, bf16 store.  Lane holds, for each of its
@@ -220,12 +237,60 @@ __global__ __launch_bounds__(NT, 1) void ffn_ln_kernel(FfnArgs a) {
   }
 }
 
+// split-F finish: y = LN(x + sum_s partial[s] + b2) (+ pos copy), one wave per row
+__global__ __launch_bounds__(256) void ffn_reduce_ln_kernel(FfnArgs a) {
+  const int lane = threadIdx.x & 63, m = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= a.M) return;
+  const int n = 4 * lane;
+  f32x4 v = *reinterpret_cast<const f32x4*>(a.b2 + n);
+  for (int s = 0; s < a.splits; ++s) v += *reinterpret_cast<const f32x4*>(a.partial + ((size_t)s * a.M + m) * D + n);
+  const u32x2 rv = ld8((const bf16*)a.x + (size_t)m * a.ldx + n);
+  v[0] += __uint_as_float(rv.x << 16); v[1] += __uint_as_float(rv.x & 0xffff0000u);
+  v[2] += __uint_as_float(rv.y << 16); v[3] += __uint_as_float(rv.y & 0xffff0000u);
+  const float mean = wave_sum(v[0] + v[1] + v[2] + v[3]) * (1.f / D);
+  float q = 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) q += (v[r] - mean) * (v[r] - mean);
+  const float rs = rsqrtf(wave_sum(q) * (1.f / D) + 1e-5f);
+  const f32x4 ga = *reinterpret_cast<const f32x4*>(a.gamma + n), be = *reinterpret_cast<const f32x4*>(a.beta + n);
+  float o[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) o[r] = (v[r] - mean) * rs * ga[r] + be[r];
+  st8((bf16*)a.y + (size_t)m * a.ldy + n, u32x2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])});
+  if (a.ypos) {
+    const u32x2 pv = ld8((const bf16*)a.pos + (size_t)(m % a.pos_period) * D + n);
+    st8((bf16*)a.ypos + (size_t)m * a.ldy + n,
+        u32x2{pack_bf16x2(o[0] + __uint_as_float(pv.x << 16), o[1] + __uint_as_float(pv.x & 0xffff0000u)),
+              pack_bf16x2(o[2] + __uint_as_float(pv.y << 16), o[3] + __uint_as_float(pv.y & 0xffff0000u))});
+  }
+}
+
 }  // namespace
 
-int spe_launch_ffn_ln(const FfnArgs& a, hipStream_t s) {
+// Rows below this many full row tiles per CU-wave run split-F (two launches, fp32 partials).
+constexpr int SPLIT_ROWS = 128 * 64;
+
+int spe_ffn_splits(int M, int F) {
+  if (M >= SPLIT_ROWS) return 1;
+  int s = 1;
+  while (s < 32 && (F / HC) % (2 * s) == 0 && ((M + BM - 1) / BM) * s < 256) s *= 2;
+  return s;
+}
+
+int spe_launch_ffn_ln(const FfnArgs& a0, hipStream_t s) {
+  FfnArgs a = a0;
   if (a.M <= 0) return 0;
   if (a.ypos && (!a.pos || a.pos_period <= 0)) return -5;
   if (a.D != D || a.F % HC || a.F > FMAX || (a.ldx % 8) || (a.ldy % 8) || (a.ld1 % 8) || (a.ld2 % 8)) return -5;
-  hipLaunchKernelGGL(ffn_ln_kernel, dim3((a.M + BM - 1) / BM), dim3(NT), 0, s, a);
+  if (!a.partial) a.splits = 1;
+  if (a.partial && (a.splits < 1 || (a.F / HC) % a.splits)) return -5;
+  const int tiles = (a.M + BM - 1) / BM;
+  if (a.partial && a.splits > 1) {
+    hipLaunchKernelGGL(ffn_ln_kernel, dim3(tiles * a.splits), dim3(NT), 0, s, a);
+    hipLaunchKernelGGL(ffn_reduce_ln_kernel, dim3((a.M + 3) / 4), dim3(256), 0, s, a);
+  } else {
+    a.partial = nullptr;
+    hipLaunchKernelGGL(ffn_ln_kernel, dim3(tiles), dim3(NT), 0, s, a);
+  }
   return (int)hipGetLastError();
 }

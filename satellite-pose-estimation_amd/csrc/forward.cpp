@@ -71,9 +71,12 @@ GemmArgs linear_args(const Conv& c, const void* A, int lda, int M, void* C, int 
 
 // Fused linear1 -> ReLU -> linear2 -> +residual -> LayerNorm over x (in place), bf16 models.
 int run_ffn(spe_model* m, const char* kind, const Conv& l1, const Conv& l2, const float* g, const float* b,
-            void* x, int M, hipStream_t s, const void* pos = nullptr, void* ypos = nullptr, int period = 0) {
+            void* x, int M, hipStream_t s, const void* pos = nullptr, void* ypos = nullptr, int period = 0,
+            float* partial = nullptr) {
   FfnArgs a{};
   a.pos = pos; a.ypos = ypos; a.pos_period = period;
+  a.splits = partial ? spe_ffn_splits(M, l1.N) : 1;
+  a.partial = a.splits > 1 ? partial : nullptr;
   a.x = x; a.ldx = l1.K;
   a.w1 = l1.w; a.ld1 = l1.Kpad; a.b1 = l1.bias;
   a.w2 = l2.w; a.ld2 = l2.Kpad; a.b2 = l2.bias;
@@ -326,7 +329,8 @@ int spe_forward(spe_model* m, void* stream, const float* images, int B, void* wo
     }
     CK(run_other(m, "ln.dec", 0.0, (double)Mq * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.dtmp), e.n2g, e.n2b, P(w.tgt), nullptr, Mq, d, dt, s); }));
     if (use_fused_ffn(m)) {
-      CK(run_ffn(m, "ffn.dec", e.l1, e.l2, e.n3g, e.n3b, P(w.tgt), Mq, s));
+      CK(run_ffn(m, "ffn.dec", e.l1, e.l2, e.n3g, e.n3b, P(w.tgt), Mq, s, nullptr, nullptr, 0,
+                 (float*)P(w.dffnpart)));
     } else {
       {
         GemmArgs g = linear_args(e.l1, P(w.tgt), d, Mq, P(w.dffn), ff);

@@ -38,7 +38,7 @@ struct Dec {
 struct Ws {                // workspace layout (byte offsets)
   size_t x0, stem, pool, bufA, bufB, t1, t2, ds, xs8, up, cat, neck;
   size_t src, srcpos, qkv, vt, ao, tmp, ffn, ck, cvt;
-  size_t tgt, dtmp, dqkv, dvt, dao, dqc, dffn, hs;
+  size_t tgt, dtmp, dqkv, dvt, dao, dqc, dffn, dffnpart, hs;
   size_t total;
 };
 

@@ -369,6 +369,7 @@ Ws spe_plan(const spe_model* m, int B) {
   w.dao = take((size_t)B * Q * d * E);
   w.dqc = take((size_t)B * Q * d * E);
   w.dffn = take((size_t)B * Q * ff * E);
+  w.dffnpart = take((size_t)std::max(1, spe_ffn_splits((int)(B * Q), (int)ff)) * B * Q * d * 4);   // split-F partials
   w.hs = take((size_t)B * Q * d * 4);
   w.total = off;
   return w;

@@ -67,8 +67,10 @@ struct FfnArgs {
   int M, D, F;
   const void* pos; void* ypos;     // optional: ypos = y + pos[m % pos_period] (bf16 [M][256])
   int pos_period;
+  int splits; float* partial;      // optional split over F for few rows: fp32 [splits][M][256] workspace
 };
 int spe_launch_ffn_ln(const FfnArgs& a, hipStream_t s);
+int spe_ffn_splits(int M, int F);  // split count spe_launch_ffn_ln would use for M rows (1 = none)
 
 int spe_launch_pack_input(const float* img, void* out, int B, int S, int dtype, hipStream_t s);
 int spe_launch_maxpool3s2(const void* in, void* out, int B, int H, int W, int C, int Ho, int Wo,

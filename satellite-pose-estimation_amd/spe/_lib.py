@@ -79,7 +79,7 @@ def lib():
     L.spe_debug_gemm.argtypes = [P, I, I, P, I, P, I, I] + [I] * 7 + [P, I, I, I, I, P, P, I, I, P, I, I, I, I, I]
     L.spe_debug_attention.argtypes = [P, I, P, I, P, I, P, P, I, I, I, I, I, F]
     L.spe_debug_layernorm.argtypes = [P, I, P, P, P, P, P, I, I]
-    L.spe_debug_ffn.argtypes = [P, P, I, P, I, P, P, I, P, P, P, P, I, I, I, I]
+    L.spe_debug_ffn.argtypes = [P, P, I, P, I, P, P, I, P, P, P, P, I, I, I, I, P, I]
     if L.spe_abi_version() != 1:
         raise ImportError("libspe.so ABI version mismatch")
     _lib = L

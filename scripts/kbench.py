@@ -61,7 +61,7 @@ def main():
         bt = torch.zeros(D, device=dev)
         y = torch.empty_like(x)
         fn = lambda: L.spe_debug_ffn(None, p(x), D, p(w1), D, p(b1), p(w2), F, p(b2), p(gm), p(bt), p(y), D,
-                                     B * T, D, F)
+                                     B * T, D, F, None, 0)
         ms = timeit(fn, a.iters)
         fl = 4.0 * B * T * D * F
         print(f"ffn.enc   {ms:.3f} ms  {fl / ms / 1e9:.1f} TF/s")

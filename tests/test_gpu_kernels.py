@@ -252,8 +252,10 @@ def test_attention_large_score_range(gpu_device):
     _close(O, ref, 2e-2)
 
 
-@pytest.mark.parametrize("M,F,inplace", [(333, 2048, True), (128, 64, False), (1000, 2048, False), (5, 32, True)])
-def test_fused_ffn(gpu_device, M, F, inplace):
+@pytest.mark.parametrize("M,F,inplace,splits", [(333, 2048, True, 0), (128, 64, False, 0), (1000, 2048, False, 0),
+                                                (5, 32, True, 0), (704, 2048, True, 16), (300, 2048, False, 32),
+                                                (77, 128, False, 2)])
+def test_fused_ffn(gpu_device, M, F, inplace, splits):
     """bf16 fused linear1 -> ReLU -> linear2 -> +x -> LayerNorm against torch fp32 on bf16-rounded
     operands; the hidden activation is rounded to bf16 on chip exactly as the unfused path stores it."""
     dt, D = torch.bfloat16, 256
@@ -270,8 +272,9 @@ def test_fused_ffn(gpu_device, M, F, inplace):
     h = torch.relu(xs @ w1.float().t() + b1).to(dt).float()
     ref = F_.layer_norm(xs + h @ w2.float().t() + b2, (D,), gam, bet, 1e-5)
     y = x if inplace else torch.full((M, ld), 7.0, dtype=dt, device=gpu_device)
+    part = torch.empty(max(splits, 1), M, D, device=gpu_device) if splits else None
     rc = _lib.lib().spe_debug_ffn(None, _p(x), ld, _p(w1), D, _p(b1), _p(w2), F, _p(b2), _p(gam), _p(bet), _p(y), ld,
-                                  M, D, F)
+                                  M, D, F, _p(part), splits)
     assert rc == 0, _lib.lib().spe_last_error()
     torch.cuda.synchronize()
     _close(y[:, :D], ref, 3e-2)
