@@ -365,6 +365,137 @@ int launch_bn(const GemmArgs& g, int mode, hipStream_t s) {
 
 }  // namespace
 
+namespace {
+
+// ---------------------------------------------------------------- few-row GEMM (decoder, M = B*Q)
+// 64x64 tile, 4 waves (2x2, 32x32 each), the WHOLE K extent (<= 256) staged by one round of
+// global_load_lds: a single memory round trip per tile instead of one per 64-deep K-step, which
+// is what bounds these latency-limited problems.  Stores straight from the accumulators (C^T
+// fragments for row-major output, C fragments for the head-transposed V^T store).
+constexpr int SM_T = 64, SM_NT = 256, SM_KMAX = 256;
+
+template <bool VT>
+__global__ __launch_bounds__(SM_NT) void gemm_small_kernel(GemmArgs g) {
+  constexpr int ROWB = SM_KMAX * 2;                  // 512 B LDS row (K = 256 bf16)
+  __shared__ __attribute__((aligned(1024))) char lds[2 * SM_T * ROWB];   // A tile | W tile
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tilesN = (g.N + SM_T - 1) / SM_T;
+  const int m0 = (blockIdx.x / tilesN) * SM_T, n0 = (blockIdx.x % tilesN) * SM_T;
+  const char* zero = reinterpret_cast<const char*>(g_zero_line);
+  // 64 wave-instructions of 1 KB (2 rows x 512 B); wave w issues 8 for A then 8 for W.  LDS row
+  // r, 16-byte chunk c lives at slot c ^ (r & 15) (conflict-free fragment reads): lane slot s
+  // fetches source chunk s ^ (r & 15).
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int ins = wid * 16 + i, isB = ins >= 32, r = 2 * (ins & 31) + (lane >> 5);
+    const int c = (lane & 31) ^ (r & 15), k = c * 8;
+    const char* src = zero;
+    if (!isB) {
+      const int m = m0 + r;
+      if (m < g.M && k < g.K) src = (const char*)g.A + ((size_t)m * g.lda + k) * 2;
+    } else {
+      const int n = n0 + r;
+      if (n < g.N && k < g.K) src = (const char*)g.B + ((size_t)n * g.ldb + k) * 2;
+    }
+    __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(lds + ins * 1024), 16, 0, 0);
+  }
+  const int fg = lane >> 4, fr = lane & 15, wr = wid >> 1, wc = wid & 1;
+  // epilogue operands fetched while the tile is in flight
+  f32x4 bias[2];
+  u32x2 res[2][2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    bias[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < 2; ++i) res[i][j] = u32x2{0, 0};
+    if constexpr (!VT) {
+      const int n = n0 + wc * 32 + 16 * j + 4 * fg;
+      if (g.bias && n + 4 <= g.N) bias[j] = *reinterpret_cast<const f32x4*>(g.bias + n);
+      else if (g.bias)
+        for (int r = 0; r < 4; ++r) bias[j][r] = n + r < g.N ? g.bias[n + r] : 0.f;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int m = m0 + wr * 32 + 16 * i + fr;
+        if (g.R && m < g.M && n + 4 <= g.N)
+          res[i][j] = ld8((const bf16*)g.R + (size_t)(g.r_period > 0 ? m % g.r_period : m) * g.ldr + n);
+      }
+    }
+  }
+  wait_vmcnt<0>();
+  __syncthreads();
+  f32x4 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int nks = (g.K + 31) / 32;
+  for (int kk = 0; kk < nks; ++kk) {
+    u32x4 af[2], wf[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int ra = wr * 32 + 16 * i + fr, rb = wc * 32 + 16 * i + fr, c = 4 * kk + fg;
+      af[i] = ld16(lds + ra * ROWB + ((c ^ (ra & 15)) << 4));
+      wf[i] = ld16(lds + SM_T * ROWB + rb * ROWB + ((c ^ (rb & 15)) << 4));
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const bf16x8 a = __builtin_bit_cast(bf16x8, af[i]), b = __builtin_bit_cast(bf16x8, wf[j]);
+        acc[i][j] = VT ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[i][j], 0, 0, 0)
+                       : __builtin_amdgcn_mfma_f32_16x16x32_bf16(b, a, acc[i][j], 0, 0, 0);
+      }
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if constexpr (VT) {
+        // C fragment: 4 consecutive tokens m = .. + 4fg + r of column n
+        const int n = n0 + wc * 32 + 16 * j + fr, m = m0 + wr * 32 + 16 * i + 4 * fg;
+        if (n >= g.N) continue;
+        const float bv = g.bias ? g.bias[n] : 0.f;
+        const int grp = n >> 8, hd = n & 255;
+        for (int r = 0; r < 4 && m + r < g.M; ++r) {
+          const int me = m + r, be = me / g.vt_T, te = me - be * g.vt_T;
+          ((bf16*)g.C)[((size_t)(grp * g.vt_B + be) * 256 + hd) * g.vt_T + te] = from_f32<bf16>(acc[i][j][r] + bv);
+        }
+      } else {
+        // C^T fragment: 4 consecutive columns n = .. + 4fg + r of row m
+        const int m = m0 + wr * 32 + 16 * i + fr, n = n0 + wc * 32 + 16 * j + 4 * fg;
+        if (m >= g.M || n >= g.N) continue;
+        const bool full = n + 4 <= g.N;
+        float v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bias[j][r];
+        if (g.R) {
+          if (full) {
+            v[0] += __uint_as_float(res[i][j].x << 16);
+            v[1] += __uint_as_float(res[i][j].x & 0xffff0000u);
+            v[2] += __uint_as_float(res[i][j].y << 16);
+            v[3] += __uint_as_float(res[i][j].y & 0xffff0000u);
+          } else {
+            const bf16* rp = (const bf16*)g.R + (size_t)(g.r_period > 0 ? m % g.r_period : m) * g.ldr + n;
+            for (int r = 0; r < 4 && n + r < g.N; ++r) v[r] += to_f32(rp[r]);
+          }
+        }
+        if (g.relu)
+          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        if (g.out_f32) {
+          float* cp = (float*)g.C + (size_t)m * g.ldc + n;
+          if (full) st16(cp, pack16<float>(v));
+          else for (int r = 0; r < 4 && n + r < g.N; ++r) cp[r] = v[r];
+        } else {
+          bf16* cp = (bf16*)g.C + (size_t)m * g.ldc + n;
+          if (full) st8(cp, u32x2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])});
+          else for (int r = 0; r < 4 && n + r < g.N; ++r) cp[r] = from_f32<bf16>(v[r]);
+        }
+      }
+    }
+}
+
+}  // namespace
+
 // Returns 1 when the problem is not for this kernel (caller falls back to gemm.hip).
 int spe_launch_gemm2(const GemmArgs& g, int mode, hipStream_t s) {
   if (mode != GEMM_LINEAR && mode != GEMM_CONV) return 1;
@@ -372,6 +503,12 @@ int spe_launch_gemm2(const GemmArgs& g, int mode, hipStream_t s) {
   if (g.K % 8 || g.ldb % 64 || g.lda % 8 || (mode == GEMM_CONV && g.Cin % 8)) return 1;
   if (g.out_f32 ? (g.ldc % 4) : (g.ldc % 8)) return 1;
   if (g.R && g.ldr % 8) return 1;
+  if (mode == GEMM_LINEAR && g.M <= 4096 && g.K <= SM_KMAX) {   // few rows: one-shot K, 64x64 tiles
+    const int tiles = ((g.M + SM_T - 1) / SM_T) * ((g.N + SM_T - 1) / SM_T);
+    if (g.vt_T > 0) hipLaunchKernelGGL(gemm_small_kernel<true>, dim3(tiles), dim3(SM_NT), 0, s, g);
+    else hipLaunchKernelGGL(gemm_small_kernel<false>, dim3(tiles), dim3(SM_NT), 0, s, g);
+    return (int)hipGetLastError();
+  }
   const int bn = (g.N <= 64 && g.vt_T == 0) ? 64 : g.N <= 128 ? 128 : 256;   // BN 64 has no V^T store
   const int tiles = ((g.M + BM - 1) / BM) * ((g.N + bn - 1) / bn);
   if (tiles < 256) return 1;                     // too few tiles to fill 256 CUs: 128x128 kernel
