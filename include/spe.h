@@ -136,7 +136,9 @@ int spe_model_profile_get(const spe_model* m, int i, char* kind, int kind_len, d
 int spe_debug_gemm(void* stream, int dtype, int mode, const void* A, int lda, const void* P, int ldp, int prow, int H,
                    int W, int Cin, int KH, int KW, int stride, int pad, const void* Bw, int ldb, int M, int N, int K,
                    const float* bias, const void* R, int ldr, int relu, void* C, int ldc, int out_f32, int vt_T,
-                   int vt_B, int r_period);
+                   int vt_B, int r_period, const float* ln_g, const float* ln_b);
+/* (ln_g/ln_b non-null: post-norm LayerNorm over each output row fused into the epilogue; bf16,
+ * N == 256 and enough rows for the large-tile kernel, else SPE_E_LAUNCH) */
 int spe_debug_attention(void* stream, int dtype, const void* q, int ldq, const void* k, int ldk, const void* vt,
                         void* o, int ldo, int B, int H, int Tq, int Tk, float scale);
 int spe_debug_layernorm(void* stream, int dtype, const void* x, const float* gamma, const float* beta, void* out,

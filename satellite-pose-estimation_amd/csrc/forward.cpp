@@ -240,11 +240,18 @@ int spe_forward(spe_model* m, void* stream, const float* images, int B, void* wo
       CK(run_attn(m, "attn.enc", a, s));
     }
     {
+      // out-proj + residual; bf16 large batches fuse norm1 into the GEMM epilogue, in place over src
       GemmArgs g = linear_args(e.o, P(w.ao), d, Mt, P(w.tmp), d);
       g.R = P(w.src); g.ldr = d;
-      CK(run_gemm(m, "gemm.enc.o", g, GEMM_LINEAR, s));
+      GemmArgs gf = g;
+      gf.C = P(w.src); gf.ln_g = e.n1g; gf.ln_b = e.n1b;
+      if (m->esz == 2 && spe_gemm_ln_fusable(gf)) {
+        CK(run_gemm(m, "gemm.enc.o", gf, GEMM_LINEAR, s));
+      } else {
+        CK(run_gemm(m, "gemm.enc.o", g, GEMM_LINEAR, s));
+        CK(run_other(m, "ln.enc", 0.0, (double)Mt * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.tmp), e.n1g, e.n1b, P(w.src), nullptr, Mt, d, dt, s); }));
+      }
     }
-    CK(run_other(m, "ln.enc", 0.0, (double)Mt * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.tmp), e.n1g, e.n1b, P(w.src), nullptr, Mt, d, dt, s); }));
     if (use_fused_ffn(m)) {
       const bool last = &e == &m->enc.back();     // last layer also emits memory + pos
       CK(run_ffn(m, "ffn.enc", e.l1, e.l2, e.n2g, e.n2b, P(w.src), Mt, s, last ? m->pos : nullptr,

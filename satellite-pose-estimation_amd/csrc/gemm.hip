@@ -312,6 +312,7 @@ int spe_launch_gemm(const GemmArgs& g, int dtype, int mode, hipStream_t s) {
   if (mode == GEMM_CONV && (g.Cin % ce)) return -3;
   if (g.ldb % 64) return -4;                                 // weights padded to 64 elements
   if ((g.lda % ce) || (g.ldc % (g.out_f32 ? 4 : ce)) || (g.R && (g.ldr % ce))) return -5;
+  if (g.ln_g && dtype != SPE_DTYPE_BF16) return -5;   // fused LayerNorm: large-tile bf16 kernel only
   if (dtype == SPE_DTYPE_BF16) {                 // 256-row tiles when they fill the chip
     const int rc = spe_launch_gemm2(g, mode, s);
     if (rc != 1) return rc;

@@ -44,7 +44,9 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 template <int N>
 SPE_DEV void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
-template <int BN, int MODE>
+// LN: fused post-norm LayerNorm epilogue (a separate instantiation: its 16 extra live
+// registers would push the plain 256-wide kernel into spills)
+template <int BN, int MODE, bool LN>
 __global__ __launch_bounds__(NT, 1) void gemm2_kernel(GemmArgs g) {
   constexpr int WM = Cfg<BN>::WM, WN = Cfg<BN>::WN;
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
@@ -187,6 +189,14 @@ __global__ __launch_bounds__(NT, 1) void gemm2_kernel(GemmArgs g) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) ebias[e] = (!DIRECT && g.bias && en + e < g.N) ? g.bias[en + e] : 0.f;
   }
+  float elg[LN ? 8 : 1], elb[LN ? 8 : 1];        // fused LayerNorm affine (this thread's 8 columns)
+  if constexpr (LN) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      elg[e] = en + e < g.N ? g.ln_g[en + e] : 0.f;
+      elb[e] = en + e < g.N ? g.ln_b[en + e] : 0.f;
+    }
+  }
 
   issue(0, 0);
   for (int ks = 0; ks < nk; ++ks) {
@@ -325,6 +335,24 @@ __global__ __launch_bounds__(NT, 1) void gemm2_kernel(GemmArgs g) {
               for (int e = 0; e < 8 && n + e < g.N; ++e) v[e] += to_f32(rp[e]);
             }
           }
+          if constexpr (LN) {
+            // fused post-norm LayerNorm (N == BN == 256): a row's 32 column groups are the 32
+            // lanes of one half-wave, so the row statistics are five xor-shuffles away
+            float sm = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) sm += v[e];
+#pragma unroll
+            for (int o = 1; o < 32; o <<= 1) sm += __shfl_xor(sm, o, 64);
+            const float mean = sm * (1.f / 256);
+            float sq = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) sq += (v[e] - mean) * (v[e] - mean);
+#pragma unroll
+            for (int o = 1; o < 32; o <<= 1) sq += __shfl_xor(sq, o, 64);
+            const float rs = rsqrtf(sq * (1.f / 256) + 1e-5f);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = (v[e] - mean) * rs * elg[e] + elb[e];
+          }
           if (g.relu) {
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
@@ -356,10 +384,17 @@ template <int BN>
 int launch_bn(const GemmArgs& g, int mode, hipStream_t s) {
   const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
   dim3 grid(tiles), block(NT);
-  if (mode == GEMM_CONV)
-    hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_CONV>), grid, block, 0, s, g);
-  else
-    hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_LINEAR>), grid, block, 0, s, g);
+  if (mode == GEMM_CONV) {
+    hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_CONV, false>), grid, block, 0, s, g);
+  } else {
+    if constexpr (BN == 256) {
+      if (g.ln_g) {
+        hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_LINEAR, true>), grid, block, 0, s, g);
+        return (int)hipGetLastError();
+      }
+    }
+    hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_LINEAR, false>), grid, block, 0, s, g);
+  }
   return (int)hipGetLastError();
 }
 
@@ -496,6 +531,12 @@ __global__ __launch_bounds__(SM_NT) void gemm_small_kernel(GemmArgs g) {
 
 }  // namespace
 
+bool spe_gemm_ln_fusable(const GemmArgs& g) {
+  const int tiles = (g.M + BM - 1) / BM;
+  return g.N == 256 && g.vt_T == 0 && tiles >= 256 && g.K % 8 == 0 && g.ldb % 64 == 0 && g.lda % 8 == 0 &&
+         g.ldc % 8 == 0 && (!g.R || g.ldr % 8 == 0);
+}
+
 // Returns 1 when the problem is not for this kernel (caller falls back to gemm.hip).
 int spe_launch_gemm2(const GemmArgs& g, int mode, hipStream_t s) {
   if (mode != GEMM_LINEAR && mode != GEMM_CONV) return 1;
@@ -503,6 +544,10 @@ int spe_launch_gemm2(const GemmArgs& g, int mode, hipStream_t s) {
   if (g.K % 8 || g.ldb % 64 || g.lda % 8 || (mode == GEMM_CONV && g.Cin % 8)) return 1;
   if (g.out_f32 ? (g.ldc % 4) : (g.ldc % 8)) return 1;
   if (g.R && g.ldr % 8) return 1;
+  if (g.ln_g) {                                  // fused LayerNorm needs whole rows in one 256-wide tile
+    if (g.N != 256 || g.vt_T > 0 || mode != GEMM_LINEAR || !spe_gemm_ln_fusable(g)) return -5;
+    return launch_bn<256>(g, mode, s);
+  }
   if (mode == GEMM_LINEAR && g.M <= 4096 && g.K <= SM_KMAX) {   // few rows: one-shot K, 64x64 tiles
     const int tiles = ((g.M + SM_T - 1) / SM_T) * ((g.N + SM_T - 1) / SM_T);
     if (g.vt_T > 0) hipLaunchKernelGGL(gemm_small_kernel<true>, dim3(tiles), dim3(SM_NT), 0, s, g);

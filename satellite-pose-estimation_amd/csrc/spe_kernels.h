@@ -20,7 +20,9 @@ struct GemmArgs {
   int out_f32;                     // store fp32 instead of T
   int vt_T, vt_B;                  // >0: head-transposed store (see gemm.hip)
   int r_period;                    // >0: residual row = m % r_period (row-periodic add, e.g. pos . W^T)
+  const float* ln_g; const float* ln_b;   // optional fused post-norm LayerNorm over N == 256 (bf16, large M)
 };
+bool spe_gemm_ln_fusable(const GemmArgs& g);   // the large-tile kernel can fuse ln_g/ln_b for g
 int spe_launch_gemm(const GemmArgs& g, int dtype, int mode, hipStream_t s);
 
 // Implicit-GEMM conv K order.  Multi-tap convs with Cin % 64 == 0 use channel-block-major order

@@ -76,7 +76,7 @@ def lib():
     L.spe_model_profile_end.argtypes = [P]
     L.spe_model_profile_get.argtypes = [P, I, ctypes.c_char_p, I, ctypes.POINTER(D), ctypes.POINTER(D),
                                         ctypes.POINTER(D)]
-    L.spe_debug_gemm.argtypes = [P, I, I, P, I, P, I, I] + [I] * 7 + [P, I, I, I, I, P, P, I, I, P, I, I, I, I, I]
+    L.spe_debug_gemm.argtypes = [P, I, I, P, I, P, I, I] + [I] * 7 + [P, I, I, I, I, P, P, I, I, P, I, I, I, I, I, P, P]
     L.spe_debug_attention.argtypes = [P, I, P, I, P, I, P, P, I, I, I, I, I, F]
     L.spe_debug_layernorm.argtypes = [P, I, P, P, P, P, P, I, I]
     L.spe_debug_ffn.argtypes = [P, P, I, P, I, P, P, I, P, P, P, P, I, I, I, I, P, I]

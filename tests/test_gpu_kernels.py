@@ -31,11 +31,12 @@ def _close(got, ref, tol):
 
 
 def _gemm(dtype, mode, A, W, M, N, K, lda, ldb, C, ldc, bias=None, R=None, ldr=0, relu=0, P=None, ldp=0, prow=1,
-          conv=(0, 0, 0, 1, 1, 1, 0), out_f32=0, vt=(0, 0), r_period=0):
+          conv=(0, 0, 0, 1, 1, 1, 0), out_f32=0, vt=(0, 0), r_period=0, ln=(None, None)):
     L = _lib.lib()
     H, Wd, Cin, KH, KW, stride, pad = conv
     rc = L.spe_debug_gemm(None, DT[dtype][0], mode, _p(A), lda, _p(P), ldp, prow, H, Wd, Cin, KH, KW, stride, pad,
-                          _p(W), ldb, M, N, K, _p(bias), _p(R), ldr, relu, _p(C), ldc, out_f32, vt[0], vt[1], r_period)
+                          _p(W), ldb, M, N, K, _p(bias), _p(R), ldr, relu, _p(C), ldc, out_f32, vt[0], vt[1], r_period,
+                          _p(ln[0]), _p(ln[1]))
     assert rc == 0, L.spe_last_error()
     torch.cuda.synchronize()
 
@@ -149,6 +150,31 @@ def test_gemm_large_tile_linear(gpu_device, N, K):
     ref = A[:, :K].float() @ Wt.float().t() + bias + R[:, :N].float()
     _close(C[:, :N], torch.relu(ref), tol)
     assert (C[:, N:] == 0).all()
+
+
+@pytest.mark.parametrize("inplace", [True, False])
+def test_gemm_fused_layernorm(gpu_device, inplace):
+    """out-proj + residual + LayerNorm in one launch (encoder norm1), optionally in place over R."""
+    _, dt, tol = DT["bf16"]
+    M, N, K = 256 * 256 + 77, 256, 256
+    g = torch.Generator(device="cpu").manual_seed(11)
+    A = torch.randn(M, K, generator=g).to(gpu_device, dt)
+    Wt = (torch.randn(N, K, generator=g) / 16).to(gpu_device, dt)
+    bias = torch.randn(N, generator=g).to(gpu_device)
+    R = (torch.randn(M, N, generator=g) * 2).to(gpu_device, dt)
+    gam = (torch.randn(N, generator=g) * 0.5 + 1).to(gpu_device)
+    bet = torch.randn(N, generator=g).to(gpu_device)
+    pre = A.float() @ Wt.float().t() + bias + R.float()
+    ref = F.layer_norm(pre, (N,), gam, bet, 1e-5)
+    C = R if inplace else torch.zeros(M, N, dtype=dt, device=gpu_device)
+    _gemm("bf16", 0, A, _padded_weight(Wt, 256, dt), M, N, K, K, 256, C, N, bias=bias, R=R, ldr=N, ln=(gam, bet))
+    _close(C, ref, 3e-2)
+    # not fusable (too few rows for the large-tile kernel): the hook must refuse, not ignore
+    L = _lib.lib()
+    small = torch.zeros(100, N, dtype=dt, device=gpu_device)
+    rc = L.spe_debug_gemm(None, 0, 0, _p(A), K, None, 0, 1, 0, 0, 0, 1, 1, 1, 0, _p(_padded_weight(Wt, 256, dt)), 256,
+                          100, N, K, _p(bias), None, N, 0, _p(small), N, 0, 0, 0, 0, _p(gam), _p(bet))
+    assert rc != 0
 
 
 @pytest.mark.parametrize("M", [256 * 256 + 77, 300])
