@@ -44,9 +44,21 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 template <int N>
 SPE_DEV void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
 
+// raw workgroup barrier (no vmcnt drain) that LDS reads / DMA issues are not moved across
+SPE_DEV void bar_raw() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// K from which a 256-wide linear GEMM takes the 4-phase half-tile schedule (P8 below).  Measured
+// (B=64 bench shapes): +10-12 % on long-K linear problems (8192^3, K = 9216); slower for K <= 256
+// (the deeper prologue) and for the implicit-GEMM convolutions, which keep the 2-stage loop.
+constexpr int P8_MIN_K = 1024;
+
 // LN: fused post-norm LayerNorm epilogue (a separate instantiation: its 16 extra live
 // registers would push the plain 256-wide kernel into spills)
-template <int BN, int MODE, bool LN>
+template <int BN, int MODE, bool LN, bool P8K = false>
 __global__ __launch_bounds__(NT, 1) void gemm2_kernel(GemmArgs g) {
   constexpr int WM = Cfg<BN>::WM, WN = Cfg<BN>::WN;
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
@@ -64,7 +76,17 @@ __global__ __launch_bounds__(NT, 1) void gemm2_kernel(GemmArgs g) {
   const int m0 = (t / tilesN) * BM, n0 = (t % tilesN) * BN;
   const int nk = (g.K + BK - 1) / BK;
 
-  // ---- per-lane load descriptors.  Instruction i of wave w fills rows (w*I + i)*8 + lane/8.
+  // P8 (256x256 tiles): the K-step is split into 4 phases over half-tiles (A rows 0-127 / 128-255,
+  // W rows 0-127 / 128-255).  A wave's 128x64 output is then two 64-row halves (one in each A
+  // half-tile) x two 32-column halves, so every phase multiplies one A half by one W half and a
+  // half-tile's buffer can be refilled as soon as its phase has been read.
+  constexpr bool P8 = BN == 256 && P8K;
+  // first row of load instruction i (IA = IB = 4 when P8) and of fragment i / j
+  auto ld_row = [&](int i, int I) { return P8 ? (i >> 1) * 128 + wid * 16 + (i & 1) * 8 : (wid * I + i) * 8; };
+  auto frag_row = [&](int i) { return P8 ? (i >> 2) * 128 + wr * 64 + (i & 3) * 16 : wr * TM + i * 16; };
+  auto frag_col = [&](int j) { return P8 ? (j >> 1) * 128 + wc * 32 + (j & 1) * 16 : wc * TN + j * 16; };
+
+  // ---- per-lane load descriptors.  Instruction i of wave w fills rows ld_row(i) + lane/8.
   const int lrow = lane >> 3;                    // row within the 8-row group
   const int chunk = (lane & 7) ^ lrow;           // global 16-byte chunk this lane fetches
   const char* zero = reinterpret_cast<const char*>(g_zero_line);
@@ -73,7 +95,7 @@ __global__ __launch_bounds__(NT, 1) void gemm2_kernel(GemmArgs g) {
   bool arow[IA];
 #pragma unroll
   for (int i = 0; i < IA; ++i) {
-    const int m = m0 + (wid * IA + i) * 8 + lrow;
+    const int m = m0 + ld_row(i, IA) + lrow;
     arow[i] = m < g.M;
     const int mm = arow[i] ? m : 0;
     if constexpr (MODE == GEMM_CONV) {
@@ -91,37 +113,63 @@ __global__ __launch_bounds__(NT, 1) void gemm2_kernel(GemmArgs g) {
   const char* bbase[IB];
 #pragma unroll
   for (int i = 0; i < IB; ++i) {
-    const int n = n0 + (wid * IB + i) * 8 + lrow;
+    const int n = n0 + ld_row(i, IB) + lrow;
     bbase[i] = n < g.N ? (const char*)g.B + ((size_t)n * g.ldb + chunk * 8) * 2 : nullptr;
   }
 
-  auto issue = [&](int ks, int buf) {
+  // Convolution K position of a K-step.  Channel-blocked order (Cin % 64 == 0, see
+  // conv_k_decode) makes a whole K-step one (channel block, tap): it is tracked incrementally in
+  // scalar registers instead of being divided out per lane.
+  const int taps = g.KH * g.KW;
+  const bool kblocked = MODE == GEMM_CONV && conv_channel_blocked(g.Cin, taps);
+  struct KPos { int cb, kh, kw; };
+  auto kadv = [&](KPos p) {
+    if (++p.kw == g.KW) {
+      p.kw = 0;
+      if (++p.kh == g.KH) { p.kh = 0; ++p.cb; }
+    }
+    return p;
+  };
+  // issue A instructions [ia0, ia1) and W instructions [ib0, ib1) of K-step ks (K position kp)
+  // into stage buf (constant ranges after inlining; K-steps past the end load the zero line)
+  auto issue_rng =[&](int ks, const KPos& kp, int buf, int ia0, int ia1, int ib0, int ib1) {
     char* st = smem + buf * STAGE;
     const int k = ks * BK + chunk * 8;
     const bool kv = k < g.K;
     if constexpr (MODE == GEMM_CONV) {
       int kh, kw, ci;
-      conv_k_decode(k, g.Cin, g.KW, g.KH * g.KW, kh, kw, ci);
+      if (kblocked) {
+        kh = kp.kh; kw = kp.kw; ci = kp.cb * 64 + chunk * 8;
+      } else if (taps == 1) {
+        kh = kw = 0; ci = k;
+      } else {
+        conv_k_decode(k, g.Cin, g.KW, taps, kh, kw, ci);
+      }
 #pragma unroll
       for (int i = 0; i < IA; ++i) {
+        if (i < ia0 || i >= ia1) continue;
         const int ih = aih[i] + kh, iw = aiw[i] + kw;
         const bool v = kv && arow[i] && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
         const char* src = v ? abase[i] + ((size_t)(ih * g.W + iw) * g.Cin + ci) * 2 : zero;
-        __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(st + (wid * IA + i) * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(st + ld_row(i, IA) * 128), 16, 0, 0);
       }
     } else {
 #pragma unroll
       for (int i = 0; i < IA; ++i) {
+        if (i < ia0 || i >= ia1) continue;
         const char* src = (kv && arow[i]) ? abase[i] + (size_t)k * 2 : zero;
-        __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(st + (wid * IA + i) * 1024), 16, 0, 0);
+        __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(st + ld_row(i, IA) * 128), 16, 0, 0);
       }
     }
 #pragma unroll
     for (int i = 0; i < IB; ++i) {
-      const char* src = bbase[i] ? bbase[i] + (size_t)ks * BK * 2 : zero;
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(st + A_BYTES + (wid * IB + i) * 1024), 16, 0, 0);
+      if (i < ib0 || i >= ib1) continue;
+      const char* src = (bbase[i] && ks * BK < g.K) ? bbase[i] + (size_t)ks * BK * 2 : zero;
+      __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(st + A_BYTES + ld_row(i, IB) * 128), 16, 0, 0);
     }
   };
+  auto issue = [&](int ks, const KPos& kp, int buf) { issue_rng(ks, kp, buf, 0, IA, 0, IB); };
+  const KPos kp0{0, 0, 0};
 
   f32x4 acc[FM][FN];
 #pragma unroll
@@ -164,7 +212,8 @@ __global__ __launch_bounds__(NT, 1) void gemm2_kernel(GemmArgs g) {
   const int ecg = (tid % TPR) * 8, en = n0 + ecg, ert = tid / TPR;
   const bool efull = en + 8 <= g.N;
   // (BN = 256: only the first half here, the rest after the K loop, or the K loop would spill)
-  constexpr int NPRE = BN == 256 ? NPASS / 2 : NPASS;
+  // (P8: none before the loop, its phases hold more fragments live)
+  constexpr int NPRE = P8 ? 0 : BN == 256 ? NPASS / 2 : NPASS;
   u32x4 rres[NPASS][RPT];
   auto fetch_res = [&](int pp) {
 #pragma unroll
@@ -198,10 +247,90 @@ __global__ __launch_bounds__(NT, 1) void gemm2_kernel(GemmArgs g) {
     }
   }
 
-  issue(0, 0);
+  if constexpr (P8) {
+    // Half-tile stream, 2 glds per half per wave.  Issue order per K-step: A0 W0 W1 A1; the
+    // halves of K-step t+2 go into the stage t is using two phases after t read them, and each
+    // K-step's wait leaves 3 halves (6 loads) in flight.
+    //   phase 1: read W0, A0 | issue A1(t+1)          | A0 x W0
+    //   phase 2: read W1     |                        | A0 x W1
+    //   phase 3: read A1     | issue A0, W0 (t+2)     | A1 x W1
+    //   phase 4:             | issue W1(t+2), vmcnt(6) retires all of t+1 | A1 x W0
+    KPos kp1 = kadv(kp0), kp2 = kadv(kp1);       // K positions of steps ks+1, ks+2
+    issue(0, kp0, 0);
+    issue_rng(1, kp1, 1, 0, 2, 0, 4);
+    wait_vmcnt<6>();
+    bar_raw();
+    u32x4 fa[8][2], fb[4][2];                    // [fragment][kk]
+    auto read_a = [&](const char* st, int i0) {
+#pragma unroll
+      for (int i = i0; i < i0 + 4; ++i)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) fa[i][kk] = ld16(st + swz(frag_row(i) + fr, 4 * kk + fg));
+    };
+    auto read_b = [&](const char* st, int j0) {
+#pragma unroll
+      for (int j = j0; j < j0 + 2; ++j)
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) fb[j][kk] = ld16(st + A_BYTES + swz(frag_col(j) + fr, 4 * kk + fg));
+    };
+    auto mma = [&](int i0, int j0) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = i0; i < i0 + 4; ++i)
+#pragma unroll
+          for (int j = j0; j < j0 + 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, fa[i][kk]),
+                                                                __builtin_bit_cast(bf16x8, fb[j][kk]), acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+      bar_raw();
+    };
+    // The waves of row group 1 (one per SIMD) run one barrier behind group 0, so on every SIMD
+    // one wave reads fragments while the other multiplies.  Under that stagger a barrier orders
+    // the two groups only one phase apart, hence: a half is restaged >= 2 phases after the phase
+    // that read it, and read >= 1 phase after the phase whose vmcnt retired it.
+    if (wr == 1) bar_raw();
+    for (int ks = 0; ks < nk; ++ks) {
+      const int cur = ks & 1;
+      const char* st = smem + cur * STAGE;
+      // phase 1
+      read_b(st, 0);
+      __builtin_amdgcn_sched_barrier(0);
+      read_a(st, 0);
+      issue_rng(ks + 1, kp1, cur ^ 1, 2, 4, 0, 0);
+      bar_raw();
+      mma(0, 0);
+      // phase 2
+      read_b(st, 2);
+      bar_raw();
+      mma(0, 2);
+      // phase 3
+      read_a(st, 4);
+      issue_rng(ks + 2, kp2, cur, 0, 2, 0, 2);
+      bar_raw();
+      mma(4, 2);
+      // phase 4
+      issue_rng(ks + 2, kp2, cur, 0, 0, 2, 4);
+      wait_vmcnt<6>();
+      bar_raw();
+      mma(4, 0);
+      kp1 = kp2;
+      kp2 = kadv(kp2);
+    }
+    if (wr == 0) bar_raw();                      // close the stagger
+    wait_vmcnt<0>();                             // the zero-line loads past the end, before the
+    bar_raw();                                   // epilogue reuses the LDS
+  } else {
+  issue(0, kp0, 0);
+  KPos kpn = kadv(kp0);                          // K position of step ks+1
   for (int ks = 0; ks < nk; ++ks) {
     if (ks + 1 < nk) {
-      issue(ks + 1, (ks + 1) & 1);
+      issue(ks + 1, kpn, (ks + 1) & 1);
+      kpn = kadv(kpn);
       wait_vmcnt<LOADS>();                      // retire stage ks, keep ks+1 in flight
     } else {
       wait_vmcnt<0>();
@@ -227,6 +356,7 @@ __global__ __launch_bounds__(NT, 1) void gemm2_kernel(GemmArgs g) {
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();               // stage ks fully read: its buffer may be refilled
+  }
   }
 
   if constexpr (DIRECT) {
@@ -282,13 +412,13 @@ __global__ __launch_bounds__(NT, 1) void gemm2_kernel(GemmArgs g) {
     const int r0 = pass * EPI_ROWS;
 #pragma unroll
     for (int i = 0; i < FM; ++i) {
-      const int rb = wr * TM + i * 16;            // fragment rows [rb, rb+16)
+      const int rb = frag_row(i);                 // fragment rows [rb, rb+16)
       if (rb >= r0 && rb < r0 + EPI_ROWS) {
 #pragma unroll
         for (int j = 0; j < FN; ++j)
 #pragma unroll
           for (int r = 0; r < 4; ++r)
-            ct[(rb - r0 + fg * 4 + r) * EPI_LD + wc * TN + j * 16 + fr] = acc[i][j][r];
+            ct[(rb - r0 + fg * 4 + r) * EPI_LD + frag_col(j) + fr] = acc[i][j][r];
       }
     }
     __syncthreads();
@@ -390,6 +520,12 @@ int launch_bn(const GemmArgs& g, int mode, hipStream_t s) {
     if constexpr (BN == 256) {
       if (g.ln_g) {
         hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_LINEAR, true>), grid, block, 0, s, g);
+        return (int)hipGetLastError();
+      }
+    }
+    if constexpr (BN == 256) {
+      if (g.K >= P8_MIN_K) {
+        hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_LINEAR, false, true>), grid, block, 0, s, g);
         return (int)hipGetLastError();
       }
     }

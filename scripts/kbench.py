@@ -37,6 +37,7 @@ def main():
     ap.add_argument("which", nargs="?", default="all")
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--batch", type=int, default=64)
+    ap.add_argument("--only", default="")
     a = ap.parse_args()
     L = _lib.lib()
     dev = torch.device("cuda", 0)
@@ -75,7 +76,17 @@ def main():
                  ("cross_k +posW", 0, B * T, 1536, 256, T, None),
                  ("enc.o +res", 0, B * T, 256, 256, -1, None),
                  ("neck s16 3x3", 2, B * T, 256, 9 * 1024, 0, (52, 52, 1024, 3, 3, 1, 1)),
-                 ("l1 3x3", 2, B * 104 * 104, 64, 9 * 64, 0, (104, 104, 64, 3, 3, 1, 1))]
+                 ("l1 3x3", 2, B * 104 * 104, 64, 9 * 64, 0, (104, 104, 64, 3, 3, 1, 1)),
+                 ("l2 3x3", 2, B * T, 128, 9 * 128, 0, (52, 52, 128, 3, 3, 1, 1)),
+                 ("l3 3x3", 2, B * 676, 256, 9 * 256, 0, (26, 26, 256, 3, 3, 1, 1)),
+                 ("l3.c3 1x1+res", 0, B * 676, 1024, 256, -1, None),
+                 ("l3.c1 1x1", 0, B * 676, 256, 1024, 0, None),
+                 ("l2.c3 1x1+res", 0, B * T, 512, 128, -1, None),
+                 ("l2.c1 1x1", 0, B * T, 128, 512, 0, None),
+                 ("sq8192 linear", 0, 8192, 8192, 8192, 0, None),
+                 ("neck as linear", 0, B * T, 256, 9 * 1024, 0, None)]
+        if a.only:
+            cases = [c for c in cases if a.only in c[0]]
         for name, mode, M, N, K, rr, conv in cases:
             if conv:
                 H, W, Cin, KH, KW, st, pd = conv

@@ -132,7 +132,8 @@ def test_gemm_head_transposed_store(gpu_device, dtype, T):
 
 # ---- large-tile (256-row, direct-to-LDS) kernel: bf16 problems with >= 256 tiles
 
-@pytest.mark.parametrize("N,K", [(256, 256), (64, 192), (128, 520), (512, 256), (200, 64)])
+@pytest.mark.parametrize("N,K", [(256, 256), (64, 192), (128, 520), (512, 256), (200, 64),
+                                 (256, 1088), (300, 1000)])   # K >= 1024: the 4-phase half-tile loop
 def test_gemm_large_tile_linear(gpu_device, N, K):
     _, dt, tol = DT["bf16"]
     M = 256 * 256 + 77                                  # >= 256 tiles of 256 rows, ragged tail
