@@ -31,6 +31,9 @@ constexpr int KT = 64;                 // keys per softmax step (and per staged 
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float NEG_BIG = -1.0e30f;    // finite "minus infinity" (exp2 of it underflows to 0)
 constexpr float RESCALE_SLACK = 8.0f;  // log2 units (bf16 path)
+#ifndef SPE_ATTN_OCC
+#define SPE_ATTN_OCC 3
+#endif
 
 // ---------------------------------------------------------------- bf16 LDS image
 // Padded (not XOR-swizzled) rows, so every fragment read is lane base + immediate offset with
@@ -153,7 +156,7 @@ SPE_DEV float tile_max(f32x16& s0, f32x16& s1, int key_base, int Tk, int hh) {
 // ROLE only separates the symbols of the token-query (encoder self-attention) and the
 // object-query (decoder) launches so profiler summaries report them apart; the code is shared.
 template <int ROLE>
-__global__ __launch_bounds__(NT, 4) void attn_bf16_kernel(AttnArgs a) {
+__global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn_bf16_kernel(AttnArgs a) {
   constexpr int KBYTES = KT * KROW, VBYTES = 32 * VROW;
   __shared__ __attribute__((aligned(16))) char smem[2 * (KBYTES + VBYTES)];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -185,9 +188,12 @@ __global__ __launch_bounds__(NT, 4) void attn_bf16_kernel(AttnArgs a) {
 
   // o: O^T accumulator; ls: running row sum (ones . P^T, every element equal), rescaled with o.
   f32x16 o, ls;
+  // negm: -m in every element, the accumulator the score MFMAs start from, so the scores come
+  // out already shifted by the running max (s - m) and p = exp2 of them costs no subtract.
+  f32x16 negm;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) { o[r] = 0.f; ls[r] = 0.f; }
-  float m = NEG_BIG;
+  for (int r = 0; r < 16; ++r) { o[r] = 0.f; ls[r] = 0.f; negm[r] = 0.f; }
+  float m = 0.f;                        // set from the first tile (forced rescale at kt == 0)
 
   // Two-slot LDS ring, one barrier per 64-key step: tile kt+1 travels global -> registers
   // during step kt and is written to the other slot after it.  (A three-slot ring that
@@ -217,36 +223,33 @@ __global__ __launch_bounds__(NT, 4) void attn_bf16_kernel(AttnArgs a) {
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)      // keys sub*32 + 16ks + {4hh..+3, 8+4hh..+3}
           vf[sub][ks] = ld16(vl + r32 * VROW + (2 * sub + ks) * 32 + hh * 16);
-      f32x16 s0, s1;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) { s0[r] = 0.f; s1[r] = 0.f; }
+      f32x16 s0, s1;                    // s - m
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub) {
         f32x16& s = sub ? s1 : s0;
-        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[sub][0]), qf[0], s, 0, 0, 0);
+        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[sub][0]), qf[0], negm, 0, 0, 0);
         s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[sub][1]), qf[1], s, 0, 0, 0);
       }
-      const float mx = tile_max(s0, s1, kt * KT, a.Tk, hh);
+      const float mx = tile_max(s0, s1, kt * KT, a.Tk, hh);   // relative to m
       // Lazy rescale (wave-uniform): keep the stale max until some lane's max grew by more than
       // RESCALE_SLACK (p <= 2^8 then, harmless in fp32 accumulators and bf16 P).  With an exact
       // "grew at all" test, 32 queries per wave re-fire the rescale on about half the tiles.
-      if (__any(mx > m + RESCALE_SLACK)) {
-        const float mn = __builtin_fmaxf(m, mx);
-        const float alpha = __builtin_amdgcn_exp2f(m - mn);
+      // The first tile always sets m to its own max (o and l are still zero then).
+      if (kt == 0 || __any(mx > RESCALE_SLACK)) {
+        const float d = kt == 0 ? mx : __builtin_fmaxf(mx, 0.f);
+        if (kt != 0) {
+          const float alpha = __builtin_amdgcn_exp2f(-d);
 #pragma unroll
-        for (int r = 0; r < 16; ++r) { o[r] *= alpha; ls[r] *= alpha; }
-        m = mn;
+          for (int r = 0; r < 16; ++r) { o[r] *= alpha; ls[r] *= alpha; }
+        }
+        m += d;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { s0[r] -= d; s1[r] -= d; negm[r] = -m; }
       }
-      // p = exp2(s - m): packed subtracts (v_pk_add_f32, two scores per instruction)
-      const f32x2 nm = {-m, -m};
 #pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        const f32x2 t0 = f32x2{s0[r], s0[r + 1]} + nm;
-        const f32x2 t1 = f32x2{s1[r], s1[r + 1]} + nm;
-        s0[r] = __builtin_amdgcn_exp2f(t0.x);
-        s0[r + 1] = __builtin_amdgcn_exp2f(t0.y);
-        s1[r] = __builtin_amdgcn_exp2f(t1.x);
-        s1[r + 1] = __builtin_amdgcn_exp2f(t1.y);
+      for (int r = 0; r < 16; ++r) {
+        s0[r] = __builtin_amdgcn_exp2f(s0[r]);
+        s1[r] = __builtin_amdgcn_exp2f(s1[r]);
       }
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub) {
