@@ -149,6 +149,14 @@ int spe_debug_layernorm(void* stream, int dtype, const void* x, const float* gam
 int spe_debug_ffn(void* stream, const void* x, int ldx, const void* w1, int ld1, const float* b1, const void* w2,
                   int ld2, const float* b2, const float* gamma, const float* beta, void* y, int ldy, int M, int D,
                   int F, float* partial, int splits);
+/* xattn (bf16 only, the decoder cross-attention against the memory): for image b, query q and
+ * head h, u[b*Q+q][h*256 .. +256] = softmax_t(q'[b*Q+q][h*256 ..] . k[b*T+t]) . v[b*T+t] with the
+ * scores already in the exp2 domain.  k, v: rows b*T+t of 256.  wv non-null ([256][256] bf16,
+ * bv fp32): o[b*Q+q][h*32 + j] = wv[h*32 + j] . u_h + bv[h*32 + j] is written instead of u.
+ * splits <= 0 picks the launch's own key split; partial_scratch: fp32, splits * B * 8Q * 258. */
+int spe_debug_xattn(void* stream, const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* u,
+                    int ldu, const void* wv, const float* bv, void* o, int ldo, int B, int Q, int T, int splits,
+                    float* partial_scratch);
 
 #ifdef __cplusplus
 }

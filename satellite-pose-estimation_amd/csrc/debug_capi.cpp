@@ -53,4 +53,18 @@ int spe_debug_ffn(void* stream, const void* x, int ldx, const void* w1, int ld1,
   return rc < 0 ? spe_fail(SPE_E_LAUNCH, "ffn launch rejected its arguments") : rc;
 }
 
+int spe_debug_xattn(void* stream, const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* u,
+                    int ldu, const void* wv, const float* bv, void* o, int ldo, int B, int Q, int T, int splits,
+                    float* partial_scratch) {
+  XattnArgs a{};
+  a.q = q; a.ldq = ldq; a.k = k; a.ldk = ldk; a.v = v; a.ldv = ldv; a.u = u; a.ldu = ldu;
+  a.wv = wv; a.bv = bv; a.o = o; a.ldo = ldo;
+  a.B = B; a.Q = Q; a.T = T; a.splits = splits > 0 ? splits : spe_xattn_splits(B, Q, T);
+  const size_t rows = (size_t)a.splits * B * 8 * Q;
+  a.pm = partial_scratch; a.pl = partial_scratch ? partial_scratch + rows : nullptr;
+  a.pu = partial_scratch ? partial_scratch + 2 * rows : nullptr;
+  const int rc = spe_launch_xattn(a, (hipStream_t)stream);
+  return rc < 0 ? spe_fail(SPE_E_LAUNCH, "xattn launch rejected its arguments") : rc;
+}
+
 }  // extern "C"

@@ -270,7 +270,10 @@ int spe_forward(spe_model* m, void* stream, const float* images, int B, void* wo
       CK(run_other(m, "ln.enc", 0.0, (double)Mt * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.tmp), e.n2g, e.n2b, P(w.src), nullptr, Mt, d, dt, s); }));
     }
   }
-  // memory = src.  Cross-attention K (memory + pos) and V^T (memory) for all decoder layers.
+  // memory = src.  Unless the layers attend to memory + pos / memory directly (xattn path),
+  // project the cross-attention K (memory + pos) and V^T (memory) for all decoder layers.
+  const bool xa = spe_use_xattn(m);
+  if (!xa) {
   {
     // bf16 fused path: the last FFN wrote memory + pos (rounded once, like the reference's
     // fp32 add) -> plain GEMM; its 8 MB pos.W^T table would not stay L2-resident
@@ -283,6 +286,7 @@ int spe_forward(spe_model* m, void* stream, const float* images, int B, void* wo
     GemmArgs g = linear_args(m->crossV, P(w.src), d, Mt, P(w.cvt), 8);
     g.vt_T = T; g.vt_B = B;
     CK(run_gemm(m, "gemm.cross_kv", g, GEMM_LINEAR, s));
+  }
   }
 
   // ---------------- decoder (REV/models/transformer.py:100-129,218-239)
@@ -315,6 +319,23 @@ int spe_forward(spe_model* m, void* stream, const float* images, int B, void* wo
       CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR, s));
     }
     CK(run_other(m, "ln.dec", 0.0, (double)Mq * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.dtmp), e.n1g, e.n1b, P(w.tgt), nullptr, Mq, d, dt, s); }));
+    if (xa) {
+      // q' = (tgt + query_pos) . Wqk^T + bqk: the query-side fold of Wq and Wk (xattn.hip)
+      GemmArgs g = linear_args(e.xq, P(w.tgt), d, Mq, P(w.xq), 8 * d);
+      g.R = e.xq_r; g.ldr = 8 * d; g.r_period = Q;
+      CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR, s));
+      XattnArgs x{};
+      x.q = P(w.xq); x.ldq = 8 * d;
+      x.k = P(w.srcpos); x.ldk = d;
+      x.v = P(w.src); x.ldv = d;
+      x.wv = e.xv.w; x.bv = e.xv.bias;
+      x.o = P(w.dao); x.ldo = d;
+      x.B = B; x.Q = Q; x.T = T; x.splits = spe_xattn_splits(B, Q, T);
+      x.pm = (float*)P(w.xpm); x.pl = (float*)P(w.xpl); x.pu = (float*)P(w.xpu);
+      const double fl = 4.0 * B * 8.0 * Q * (double)T * d + 2.0 * Mq * 8.0 * d * 32;
+      const double by = 2.0 * B * (double)T * d * m->esz + 2.0 * Mq * 8.0 * d * m->esz;
+      CK(run_other(m, "attn.dec_cross", fl, by, s, [&] { return spe_launch_xattn(x, s); }));
+    } else {
     {
       GemmArgs g = linear_args(e.cq, P(w.tgt), d, Mq, P(w.dqc), d);
       const int mode = add_pos(m, g, m->qpos, d, Q, e.qpos_cq, d);
@@ -328,6 +349,7 @@ int spe_forward(spe_model* m, void* stream, const float* images, int B, void* wo
       a.o = P(w.dao); a.ldo = d;
       a.B = B; a.H = c.nheads; a.Tq = Q; a.Tk = T; a.scale = scale;
       CK(run_attn(m, "attn.dec_cross", a, s));
+    }
     }
     {
       GemmArgs g = linear_args(e.co, P(w.dao), d, Mq, P(w.dtmp), d);

@@ -33,12 +33,17 @@ struct Dec {
   float *n1g, *n1b, *n2g, *n2b, *n3g, *n3b;
   void* qpos_sqk = nullptr; // bf16 models: query_pos . W_sqk^T [Q][512]
   void* qpos_cq = nullptr;  // bf16 models: query_pos . W_cq^T [Q][256]
+  // cross-attention against the memory (spe_use_xattn, xattn.hip): q' = tgt . Wqk^T + xq_r
+  // with Wq/Wk folded per head at finalize; xv = the value projection rows of in_proj
+  Conv xq, xv;
+  void* xq_r = nullptr;     // [Q][8*256] bf16: query_pos . Wqk^T + bqk (scaled)
 };
 
 struct Ws {                // workspace layout (byte offsets)
   size_t x0, stem, pool, bufA, bufB, t1, t2, ds, xs8, up, cat, neck;
   size_t src, srcpos, qkv, vt, ao, tmp, ffn, ck, cvt;
   size_t tgt, dtmp, dqkv, dvt, dao, dqc, dffn, dffnpart, hs;
+  size_t xq, xu, xpm, xpl, xpu;           // cross-attention against the memory (xattn.hip)
   size_t total;
 };
 
@@ -79,4 +84,12 @@ struct spe_model {
 };
 
 int spe_fail(int code, const std::string& msg);
+
+// bf16 models take the decoder cross-attention against the memory itself (xattn.hip) when the
+// last encoder layer can emit memory + pos (fused FFN)
+inline bool spe_use_xattn(const spe_model* m) {
+  const auto& c = m->cfg;
+  return c.dtype == SPE_DTYPE_BF16_ && c.hidden_dim == 256 && c.nheads == 8 && c.dim_feedforward % 32 == 0 &&
+         c.enc_layers > 0;
+}
 Ws spe_plan(const spe_model* m, int B);

@@ -4,6 +4,7 @@
 // workspace planning.  The launch sequence lives in forward.cpp.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -224,6 +225,52 @@ std::vector<float> sine_pos(int h, int w, int d) {
   return out;
 }
 
+// Cross-attention of decoder layer p folded for xattn.hip (header there).  Per head h
+// (hd = 32 dims, s = softmax scale * log2 e):
+//   Wqk[h*256 + n][k] = s * sum_i Wk[h*32+i][n] Wq[h*32+i][k]     (q' = x . Wqk^T + bqk)
+//   bqk[h*256 + n]    = s * sum_i bq[h*32+i] Wk[h*32+i][n]         (bk drops out of the softmax)
+//   xq_r[q][j]        = query_pos[q] . Wqk[j] + bqk[j]             (the `+ query_pos` of the query)
+// Sums in double, stored bf16 (the reference's fp32 chain differs by the usual bf16 rounding).
+// Wv (+bv) stays a plain [256][256] matrix: it is applied per row after the weighted sum.
+void fold_cross_attention(spe_model* m, const std::string& p, Dec& e) {
+  const auto& c = m->cfg;
+  const int d = c.hidden_dim, H = c.nheads, hd = d / H, Q = c.num_queries, HD = H * d;
+  std::vector<float> wqk((size_t)HD * d, 0.f), rqk((size_t)Q * HD, 0.f);
+  if (m->dmem) {                                   // pass 2 only: pass 1 just sizes the block
+    const auto& W = m->host[p + ".multihead_attn.in_proj_weight"];
+    const auto& Bi = m->host[p + ".multihead_attn.in_proj_bias"];
+    const auto& qe = m->host["query_embed.weight"];
+    const double sc = 1.0 / std::sqrt((double)hd) * 1.4426950408889634;
+    std::vector<double> acc((size_t)d), bqk((size_t)HD, 0.0);
+    for (int h = 0; h < H; ++h)
+      for (int n = 0; n < d; ++n) {
+        std::fill(acc.begin(), acc.end(), 0.0);
+        double bsum = 0.0;
+        for (int i = 0; i < hd; ++i) {
+          const double wk = W[(size_t)(d + h * hd + i) * d + n];
+          const float* wq = &W[(size_t)(h * hd + i) * d];
+          for (int k = 0; k < d; ++k) acc[k] += wk * wq[k];
+          bsum += wk * Bi[h * hd + i];
+        }
+        float* dst = &wqk[((size_t)h * d + n) * d];
+        for (int k = 0; k < d; ++k) dst[k] = (float)(acc[k] * sc);
+        bqk[(size_t)h * d + n] = bsum * sc;
+      }
+    for (int q = 0; q < Q; ++q)
+      for (int j = 0; j < HD; ++j) {
+        double sum = bqk[j];
+        const float* wr = &wqk[(size_t)j * d];
+        for (int k = 0; k < d; ++k) sum += (double)qe[(size_t)q * d + k] * wr[k];
+        rqk[(size_t)q * HD + j] = (float)sum;
+      }
+  }
+  e.xq.N = HD; e.xq.K = d; e.xq.Kpad = pad64(d); e.xq.Cin = d;
+  e.xq.w = upload_rows(m, wqk, HD, d, e.xq.Kpad);
+  e.xq.bias = nullptr;
+  e.xq_r = upload_T(m, rqk);
+  e.xv = make_linear(m, p + ".multihead_attn.in_proj_weight", p + ".multihead_attn.in_proj_bias", 2 * d, d, d);
+}
+
 int build_device(spe_model* m) {
   const auto& c = m->cfg;
   const int d = c.hidden_dim, ff = c.dim_feedforward, Q = c.num_queries;
@@ -278,6 +325,7 @@ int build_device(spe_model* m) {
     e.n1g = upload_key(m, p + ".norm1.weight"); e.n1b = upload_key(m, p + ".norm1.bias");
     e.n2g = upload_key(m, p + ".norm2.weight"); e.n2b = upload_key(m, p + ".norm2.bias");
     e.n3g = upload_key(m, p + ".norm3.weight"); e.n3b = upload_key(m, p + ".norm3.bias");
+    if (spe_use_xattn(m)) fold_cross_attention(m, p, e);
     m->dec.push_back(e);
     const auto& w = m->host[p + ".multihead_attn.in_proj_weight"];
     const auto& bb = m->host[p + ".multihead_attn.in_proj_bias"];
@@ -287,7 +335,9 @@ int build_device(spe_model* m) {
     vb.insert(vb.end(), bb.begin() + 2 * d, bb.begin() + 3 * d);
   }
   // all decoder layers' cross-attention K/V projections of the (fixed) memory, batched
-  m->crossK.N = m->crossV.N = c.dec_layers * d;
+  // (not needed when the cross-attention runs against the memory itself)
+  if (spe_use_xattn(m)) { kall.clear(); vall.clear(); kb.clear(); vb.clear(); }
+  m->crossK.N = m->crossV.N = spe_use_xattn(m) ? 0 : c.dec_layers * d;
   m->crossK.K = m->crossV.K = d;
   m->crossK.Kpad = m->crossV.Kpad = pad64(d);
   m->crossK.w = upload_rows(m, kall, m->crossK.N, d, m->crossK.Kpad);
@@ -304,10 +354,10 @@ int build_device(spe_model* m) {
     // reference's (x + pos) . W^T order for exact parity.
     const size_t T = (size_t)fs * fs, Q = c.num_queries;
     for (auto& e : m->enc) e.pos_qk = dalloc(m, T * 2 * d * 2);
-    m->pos_crossK = dalloc(m, T * c.dec_layers * d * 2);
+    m->pos_crossK = spe_use_xattn(m) ? nullptr : dalloc(m, T * c.dec_layers * d * 2);
     for (auto& e : m->dec) {
       e.qpos_sqk = dalloc(m, Q * 2 * d * 2);
-      e.qpos_cq = dalloc(m, Q * d * 2);
+      e.qpos_cq = spe_use_xattn(m) ? nullptr : dalloc(m, Q * d * 2);
     }
   }
   m->dng = upload_key(m, "transformer.decoder.norm.weight");
@@ -360,8 +410,15 @@ Ws spe_plan(const spe_model* m, int B) {
   w.ao = take((size_t)B * T * d * E);
   w.tmp = take((size_t)B * T * d * E);
   w.ffn = take((size_t)B * T * ff * E);
-  w.ck = take((size_t)B * T * L * d * E);
-  w.cvt = take((size_t)B * T * L * d * E);
+  const bool xa = spe_use_xattn(m);
+  w.ck = take(xa ? 0 : (size_t)B * T * L * d * E);
+  w.cvt = take(xa ? 0 : (size_t)B * T * L * d * E);
+  const size_t R = 8 * Q, XS = xa ? (size_t)spe_xattn_splits(B, (int)Q, (int)T) : 0;
+  w.xq = take(xa ? (size_t)B * Q * 8 * d * E : 0);
+  w.xu = take(xa ? (size_t)B * Q * 8 * d * E : 0);
+  w.xpm = take(XS > 1 ? XS * B * R * 4 : 0);
+  w.xpl = take(XS > 1 ? XS * B * R * 4 : 0);
+  w.xpu = take(XS > 1 ? XS * B * R * d * 4 : 0);
   w.tgt = take((size_t)B * Q * d * E);
   w.dtmp = take((size_t)B * Q * d * E);
   w.dqkv = take((size_t)B * Q * 3 * d * E);
@@ -449,10 +506,10 @@ int spe_model_finalize(spe_model* m) {
     };
     int rc = 0;
     for (auto& l : m->enc) rc |= proj(m->pos, T, l.qk, l.pos_qk);
-    rc |= proj(m->pos, T, m->crossK, m->pos_crossK);
+    if (m->pos_crossK) rc |= proj(m->pos, T, m->crossK, m->pos_crossK);
     for (auto& l : m->dec) {
       rc |= proj(m->qpos, Q, l.sqk, l.qpos_sqk);
-      rc |= proj(m->qpos, Q, l.cq, l.qpos_cq);
+      if (l.qpos_cq) rc |= proj(m->qpos, Q, l.cq, l.qpos_cq);
     }
     e = hipDeviceSynchronize();
     if (rc || e != hipSuccess) return fail(SPE_E_LAUNCH, "positional projection precompute failed");

@@ -56,6 +56,22 @@ struct AttnArgs {
 };
 int spe_launch_attention(const AttnArgs& a, int dtype, hipStream_t s);
 
+// Decoder cross-attention against the encoder memory (bf16 path, xattn.hip): per image b and
+// attention row r = q * 8 + h, u[b][q][h] = softmax(q'[b][q][h] . K^T) . V with K = memory +
+// pos [T][256], V = memory [T][256], q' pre-scaled into the exp2 domain.
+struct XattnArgs {
+  const void* q; int ldq;          // q' rows b*Q + q, head h at columns [h*256, h*256 + 256)
+  const void* k; int ldk;          // memory + pos, rows b*T + t
+  const void* v; int ldv;          // memory, rows b*T + t
+  void* u; int ldu;                // output rows b*Q + q, head h at columns [h*256, h*256 + 256)
+  const void* wv; const float* bv; // optional: o_h = Wv_h u_h + bv_h written instead of u
+  void* o; int ldo;                //   o rows b*Q + q, head h at columns [h*32, h*32 + 32)
+  int B, Q, T, splits, tiles_per_split;
+  float *pm, *pl, *pu;             // key-split partials [B][splits][8Q] (pu: x 256), required
+};
+int spe_xattn_splits(int B, int Q, int T);
+int spe_launch_xattn(const XattnArgs& a, hipStream_t s);
+
 // Fused FFN + residual + LayerNorm (bf16 only): y = LN(x + W2 relu(W1 x + b1) + b2).
 // x / y may alias (each block reads and writes only its own rows).
 struct FfnArgs {

@@ -29,7 +29,7 @@ EXPORTS = ["spe_abi_version", "spe_last_error", "spe_model_create", "spe_model_d
            "spe_model_num_params", "spe_model_param_name", "spe_model_finalize", "spe_model_workspace_bytes",
            "spe_forward", "spe_postprocess", "spe_pnp_batch", "spe_speed_score", "spe_model_profile_begin",
            "spe_model_profile_end", "spe_model_profile_get", "spe_debug_gemm", "spe_debug_attention",
-           "spe_debug_layernorm", "spe_debug_ffn"]
+           "spe_debug_layernorm", "spe_debug_ffn", "spe_debug_xattn"]
 
 
 class ModelConfig(ctypes.Structure):
@@ -80,6 +80,7 @@ def lib():
     L.spe_debug_attention.argtypes = [P, I, P, I, P, I, P, P, I, I, I, I, I, F]
     L.spe_debug_layernorm.argtypes = [P, I, P, P, P, P, P, I, I]
     L.spe_debug_ffn.argtypes = [P, P, I, P, I, P, P, I, P, P, P, P, I, I, I, I, P, I]
+    L.spe_debug_xattn.argtypes = [P, P, I, P, I, P, I, P, I, P, P, P, I, I, I, I, I, P]
     if L.spe_abi_version() != 1:
         raise ImportError("libspe.so ABI version mismatch")
     _lib = L

@@ -66,6 +66,25 @@ def main():
         ms = timeit(fn, a.iters)
         fl = 4.0 * B * T * D * F
         print(f"ffn.enc   {ms:.3f} ms  {fl / ms / 1e9:.1f} TF/s")
+    if a.which in ("xattn", "all"):
+        Q = 11
+        q = (torch.randn(B * Q, 8 * D, generator=g) / 16).to(dev, torch.bfloat16)
+        k = torch.randn(B * T, D, generator=g).to(dev, torch.bfloat16)
+        v = torch.randn(B * T, D, generator=g).to(dev, torch.bfloat16)
+        wv = (torch.randn(D, D, generator=g) / 16).to(dev, torch.bfloat16)
+        bv = torch.zeros(D, device=dev)
+        u = torch.empty(B * Q, 8 * D, dtype=torch.bfloat16, device=dev)
+        o = torch.empty(B * Q, D, dtype=torch.bfloat16, device=dev)
+        part = torch.empty(256 * B * 8 * Q * 258, device=dev)
+        for sp in (0, 2, 8):
+            fn = lambda: L.spe_debug_xattn(None, p(q), 8 * D, p(k), D, p(v), D, None, 0, p(wv), p(bv), p(o), D,
+                                           B, Q, T, sp, p(part))
+            ms = timeit(fn, a.iters)
+            fn_u = lambda: L.spe_debug_xattn(None, p(q), 8 * D, p(k), D, p(v), D, p(u), 8 * D, None, None, None,
+                                             0, B, Q, T, sp, p(part))
+            ms_u = timeit(fn_u, a.iters)
+            byts = 2 * B * T * D * 2                      # K and V reads
+            print(f"xattn splits={sp}: {ms:.3f} ms with Wv, {ms_u:.3f} ms u only ({byts / ms_u / 1e9:.2f} TB/s)")
     if a.which in ("gemm", "all"):
         # name, mode, M, N, K, residual rows (0 none, -1 full, >0 period), conv geometry
         cases = [("l1.c3 1x1+res", 0, B * 104 * 104, 256, 64, -1, None),

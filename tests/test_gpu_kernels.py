@@ -309,6 +309,47 @@ def test_fused_ffn(gpu_device, M, F, inplace, splits):
         assert (y[:, D:] == 7.0).all()                 # nothing written past D
 
 
+@pytest.mark.parametrize("B,Q,T,splits,amp", [(3, 11, 200, 1, 1.0), (2, 11, 203, 3, 1.0), (1, 17, 136, 2, 1.0),
+                                              (2, 11, 2704, 0, 1.0), (2, 5, 640, 4, 12.0), (64, 11, 2704, 0, 1.0)])
+def test_cross_attention_memory(gpu_device, B, Q, T, splits, amp):
+    """decoder cross-attention against the memory (xattn.hip): u = softmax_2(q' . K^T) . V per
+    (image, query, head) row, against torch fp32 on the same bf16 operands.  amp = 12 spreads the
+    scores over ~100 log2 units (many lazy-rescale branches taken, split partials merged far apart).
+    Tolerance: P is rounded to bf16 (2^-9 relative) before the value product; 1e-2 * scale."""
+    dt, D = torch.bfloat16, 256
+    g = torch.Generator(device="cpu").manual_seed(B * T + Q)
+    ldq, ldv = 8 * D + 8, D + 8
+    q = (torch.randn(B * Q, ldq, generator=g) * amp / 16).to(gpu_device, dt)
+    k = torch.randn(B * T, D, generator=g).to(gpu_device, dt)
+    v = torch.randn(B * T, ldv, generator=g).to(gpu_device, dt)          # strided rows
+    if amp > 1:
+        k[5] *= 4                                           # one key far above the rest
+    wv = (torch.randn(D, D, generator=g) / 16).to(gpu_device, dt)
+    bv = torch.randn(D, generator=g).to(gpu_device)
+    u = torch.full((B * Q, ldq), 7.0, dtype=dt, device=gpu_device)
+    o = torch.full((B * Q, D + 8), 7.0, dtype=dt, device=gpu_device)
+    S = splits if splits > 0 else 256                     # the launch's own split count is below 256
+    part = torch.empty(S * B * 8 * Q * 258, device=gpu_device)
+    L = _lib.lib()
+    rc = L.spe_debug_xattn(None, _p(q), ldq, _p(k), D, _p(v), ldv, _p(u), ldq, None, None, None, 0, B, Q, T,
+                           splits, _p(part))
+    assert rc == 0, L.spe_last_error()
+    rc = L.spe_debug_xattn(None, _p(q), ldq, _p(k), D, _p(v), ldv, None, 0, _p(wv), _p(bv), _p(o), D + 8, B, Q,
+                           T, splits, _p(part))
+    assert rc == 0, L.spe_last_error()
+    torch.cuda.synchronize()
+    qh = q[:, :8 * D].float().view(B, Q * 8, D)
+    s = torch.einsum("brd,btd->brt", qh, k.float().view(B, T, D))
+    p = torch.softmax(s * 0.6931471805599453, dim=-1)
+    ref = torch.einsum("brt,btd->brd", p, v[:, :D].float().view(B, T, D))   # [B][Q*8][D], rows q*8 + h
+    _close(u[:, :8 * D], ref.reshape(B * Q, 8 * D), 1e-2)
+    assert (u[:, 8 * D:] == 7.0).all()
+    # o_h = Wv_h u_h + bv_h: the value projection after the weighted sum (u itself unrounded)
+    ref_o = torch.einsum("bqhn,hjn->bqhj", ref.view(B, Q, 8, D), wv.float().view(8, 32, D)) + bv.view(8, 32)
+    _close(o[:, :D], ref_o.reshape(B * Q, D), 1e-2)
+    assert (o[:, D:] == 7.0).all()
+
+
 @pytest.mark.parametrize("dtype", ["bf16", "fp32"])
 def test_layernorm(gpu_device, dtype):
     code, dt, tol = DT[dtype]
