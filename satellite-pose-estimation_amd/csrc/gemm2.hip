@@ -692,6 +692,8 @@ int spe_launch_gemm2(const GemmArgs& g, int mode, hipStream_t s) {
   }
   const int bn = (g.N <= 64 && g.vt_T == 0) ? 64 : g.N <= 128 ? 128 : 256;   // BN 64 has no V^T store
   const int tiles = ((g.M + BM - 1) / BM) * ((g.N + bn - 1) / bn);
-  if (tiles < 256) return 1;                     // too few tiles to fill 256 CUs: 128x128 kernel
+  // too few tiles for the large-tile kernel: the 128x128 kernel.  (169 tiles of 256x256 on the
+  // layer3 convs, M = B*26*26, still beat 676 tiles of the 128x128 kernel by 12-18 %.)
+  if (tiles < 128) return 1;
   return bn == 64 ? launch_bn<64>(g, mode, s) : bn == 128 ? launch_bn<128>(g, mode, s) : launch_bn<256>(g, mode, s);
 }
