@@ -28,16 +28,36 @@ KIND_SYMBOL = {"attn.enc": "attn_bf16_kernel<0>", "attn.dec_self": "attn_bf16_ke
                "attn.dec_cross": "attn_bf16_kernel<1>", "ffn.enc": "ffn_ln_kernel", "ffn.dec": "ffn_ln_kernel"}
 
 
+# BASELINE.json configs: per-GPU shapes (configs 3-5 are quoted at bs=256 over 8 GPUs = 32/GPU)
+PRESETS = {
+    2: dict(batch=64, size=416, queries=11, layers=6, solver="epnp", sigma_head=0),
+    3: dict(batch=32, size=416, queries=11, layers=6, solver="ransac_p3p_lm", sigma_head=0),
+    4: dict(batch=32, size=416, queries=11, layers=6, solver="epnp_ransac_sigma", sigma_head=1),
+    5: dict(batch=32, size=640, queries=40, layers=6, solver="ransac_p3p_lm", sigma_head=0),
+}
+CONFIG_NAME = {
+    2: "BASELINE config 2: ResNet50-s8 + {L}/{L} DETR, {Q} queries, {S}x{S}, solver={solver}",
+    3: "BASELINE config 3: ResNet50-s8 + {L}/{L} DETR, {Q} queries, {S}x{S}, RANSAC-P3P + LM refine (solver={solver})",
+    4: "BASELINE config 4: ResNet50-s8 + {L}/{L} DETR + sigma head, {Q} queries, {S}x{S}, sigma-weighted "
+       "EPnP-RANSAC + self-assessment filter (solver={solver})",
+    5: "BASELINE config 5: ResNet50-s8 + {L}/{L} DETR, {Q} queries, {S}x{S} (train_resnet50s8_query40), "
+       "bf16 attention, solver={solver}",
+}
+
+
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
-    p.add_argument("--batch", type=int, default=64, help="images per GPU per step")
-    p.add_argument("--size", type=int, default=416)
-    p.add_argument("--queries", type=int, default=11)
-    p.add_argument("--layers", type=int, default=6)
-    p.add_argument("--solver", default="epnp", choices=["epnp", "epnp_lm", "ransac_p3p_lm", "epnp_ransac_sigma"])
+    p.add_argument("--config", type=int, default=2, choices=sorted(PRESETS),
+                   help="BASELINE.json configs[k-1] preset (2 = the headline metric's workload); explicit flags override")
+    p.add_argument("--batch", type=int, default=None, help="images per GPU per step")
+    p.add_argument("--size", type=int, default=None)
+    p.add_argument("--queries", type=int, default=None)
+    p.add_argument("--layers", type=int, default=None)
+    p.add_argument("--solver", default=None, choices=["epnp", "epnp_lm", "ransac_p3p_lm", "epnp_ransac_sigma"])
+    p.add_argument("--sigma-head", type=int, default=None, choices=[0, 1])
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--weights", default="label-diverse", choices=["label-diverse", "random"],
                    help="label-diverse: random init made query-diverse so the solver sees >= 4 "
@@ -46,18 +66,25 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--launch-table", default=None,
                    help="write every launch of the profiled step (kind, ms, flops, bytes, roofline floor) as JSON")
-    return p.parse_args()
+    a = p.parse_args()
+    for k, v in PRESETS[a.config].items():
+        if getattr(a, k) is None:
+            setattr(a, k, v)
+    return a
 
 
-def cpu_baseline(cfg, seconds):
+def cpu_baseline(cfg, seconds, solver="epnp"):
     """Oracle port (torch-fp32 CPU model + C solver) timed on this host's cores on a bounded
-    sample of the same workload: single 416x416 images, repeated until `seconds` elapse."""
+    sample of the same workload: single images of the bench's shape, repeated until `seconds`
+    elapse."""
     import torch
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import model_ref
     import pnp_ref
     from spe.config import Camera, world_points
     from spe.synthetic import random_weights, synthetic_batch
+    mode = {"epnp": pnp_ref.MODE_EPNP, "epnp_lm": pnp_ref.MODE_EPNP_LM, "ransac_p3p_lm": pnp_ref.MODE_RANSAC_P3P_LM,
+            "epnp_ransac_sigma": pnp_ref.MODE_EPNP_RANSAC_SIGMA}[solver]
     threads = min(16, os.cpu_count() or 1)
     torch.set_num_threads(threads)
     w = random_weights(cfg, 0)
@@ -67,14 +94,17 @@ def cpu_baseline(cfg, seconds):
     with torch.no_grad():
         while True:
             o = model_ref.forward(b["images"], w, cfg)
-            pp = model_ref.postprocess(o["pred_logits"], o["pred_points"], b["clip_bbox"])
-            pnp_ref.pnp_batch(pp[0]["points"][None], pp[0]["logits"][None], K, W, mode=pnp_ref.MODE_EPNP)
+            pp = model_ref.postprocess(o["pred_logits"], o["pred_points"], b["clip_bbox"], o.get("pred_sigmas"))
+            sg = pp[0]["sigmas"][None] if "sigmas" in pp[0] else None
+            pnp_ref.pnp_batch(pp[0]["points"][None], pp[0]["logits"][None], K, W, mode=mode,
+                              repro=25.0 if mode == pnp_ref.MODE_EPNP_RANSAC_SIGMA else 20.0, sigmas=sg)
             n += 1
             if time.perf_counter() - t0 >= seconds:
                 break
     dt = time.perf_counter() - t0
     return {"value": n / dt, "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{n} single-image passes (416x416, Q=11, 6/6, fp32 torch-CPU model + C EPnP oracle) in {dt:.1f}s"}
+            "sample": f"{n} single-image passes ({cfg.input_size}x{cfg.input_size}, Q={cfg.num_queries}, "
+                      f"{cfg.enc_layers}/{cfg.dec_layers}, fp32 torch-CPU model + C {solver} oracle) in {dt:.1f}s"}
 
 
 def traffic_for(kind):
@@ -106,7 +136,8 @@ def main():
     rank, world, local = sd.init_distributed_mode()
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
-    cfg = SpeConfig(input_size=args.size, num_queries=args.queries, enc_layers=args.layers, dec_layers=args.layers)
+    cfg = SpeConfig(input_size=args.size, num_queries=args.queries, enc_layers=args.layers, dec_layers=args.layers,
+                    sigma_head=bool(args.sigma_head))
     B = args.batch
 
     def hs_fn(w, images):
@@ -208,7 +239,7 @@ def main():
         peak = PEAK["hbm"]
         unit = "GB/s"
     result = {
-        "metric": "images/sec end-to-end (backbone->kpts->PnP) at 416x416; SPEED pose score",
+        "metric": f"images/sec end-to-end (backbone->kpts->PnP) at {args.size}x{args.size}; SPEED pose score",
         "value": total_images / elapsed,
         "unit": "images/s",
         "n_gpus": world,
@@ -221,8 +252,8 @@ def main():
         "dtype": args.dtype,
         "data": f"synthetic (seeded SPEED-shaped crops; {args.weights} random-init weights, "
                 "no checkpoint exists in the reference)",
-        "config": {"workload": f"BASELINE config 2: ResNet50-s8 + {args.layers}/{args.layers} DETR, "
-                               f"{args.queries} queries, {args.size}x{args.size}, solver={args.solver}",
+        "config": {"workload": CONFIG_NAME[args.config].format(L=args.layers, Q=args.queries, S=args.size,
+                                                                solver=args.solver),
                    "global_batch": B * world, "per_gpu_batch": B, "input_size": args.size,
                    "num_queries": args.queries, "parallelism": f"dp{world} (image sharding)"},
         "roofline": {"kernel": dominant, "kernel_symbol": KIND_SYMBOL.get(dominant, dominant),
@@ -235,8 +266,10 @@ def main():
         "speed_score_mean_random_weights": score,
         "solver_status_counts": {str(s): int((status == s).sum()) for s in range(5)},
     }
+    if "assess" in out:
+        result["self_assessment_reliable"] = int(out["assess"]["reliable"].sum().item())
     if world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds)
+        result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds, args.solver)
     print(json.dumps(result))
     if world > 1:
         dist.destroy_process_group()

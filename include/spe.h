@@ -112,6 +112,19 @@ int spe_pnp_batch(void* stream, const float* points_px, const float* probs, cons
                   int ransac_iters, double confidence, float* quat, double* tvec, double* rvec, int32_t* status,
                   int32_t* n_corr, int32_t* corr_label, uint32_t* inlier_mask);
 
+/* Self-assessment filter over the sigma solver's output (BASELINE config 4).  No reference code
+ * exists: the UNC README (ROOT/README.md:15-20) names the mechanism and the commented gate
+ * `s_ > 0.5 and sig.mean() < 5` (UNC/utils/speed_eval_ceres.py:110-114) is its only trace, so
+ * the rule is defined here (parity unpinned): over the RANSAC inliers of each image,
+ * mean_sigma = mean sigma (both axes); n_confident = #inliers with score > score_th and mean
+ * sigma < sigma_th; reliable = pose solved (status 0 or 3) and n_confident >= min_inliers and
+ * mean_sigma < sigma_th.  Inputs are spe_forward's probs/sigmas and spe_pnp_batch's status /
+ * corr_label / inlier_mask; all device pointers. */
+int spe_self_assess(void* stream, const float* probs, const float* sigmas, const int32_t* status,
+                    const int32_t* corr_label, const uint32_t* inlier_mask, int batch, int num_queries,
+                    int num_classes, float score_th, float sigma_th, int min_inliers, float* mean_sigma,
+                    int32_t* n_confident, uint8_t* reliable);
+
 /* speed_score per image (REV/utils/speed_eval.py:245-262), device pointers. */
 int spe_speed_score(void* stream, const float* quat, const double* tvec, const double* q_gt, const double* t_gt,
                     int batch, double* s_t, double* s_q);

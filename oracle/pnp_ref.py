@@ -97,3 +97,41 @@ def select_correspondences(points, probs):
         labs.append(lab)
         pts.append(arr[best, :2])
     return labs, np.asarray(pts, np.float32).reshape(-1, 2)
+
+
+def self_assess(probs, sigmas, status, corr_label, inlier_mask, score_th=0.5, sigma_th=5.0, min_inliers=4):
+    """Self-assessment filter (BASELINE config 4).  No reference code exists (parity unpinned):
+    the rule restates include/spe.h spe_self_assess, built on the commented per-keypoint gate
+    `s_ > 0.5 and sig.mean() < 5` of UNC/utils/speed_eval_ceres.py:110-114 and on the
+    reference's selection (best-score query per label, REV/utils/speed_eval.py:152-200).
+    Per image: (mean_sigma f32, n_confident int, reliable bool)."""
+    B, Q, C = probs.shape
+    ms = np.zeros(B, np.float32)
+    nc = np.zeros(B, np.int32)
+    rel = np.zeros(B, bool)
+    for b in range(B):
+        best_q, best_s = {}, {}
+        for q in range(Q):
+            lab = int(probs[b, q].argmax())
+            if lab == C - 1:
+                continue
+            sc = probs[b, q, lab]
+            if lab not in best_q or sc > best_s[lab]:
+                best_q[lab], best_s[lab] = q, sc
+        inl = int(inlier_mask[b]) & 0xFFFFFFFF if int(status[b]) in (ST_OK, ST_RANSAC_FALLBACK) else 0
+        ssum, n, conf = np.float32(0), 0, 0
+        for j in range(MAXN):
+            if not (inl >> j) & 1:
+                continue
+            lab = int(corr_label[b, j])
+            if lab < 0 or lab not in best_q:
+                continue
+            sx, sy = sigmas[b, best_q[lab]].astype(np.float32)
+            ssum = np.float32(ssum + np.float32(sx + sy))
+            n += 1
+            if best_s[lab] > np.float32(score_th) and np.float32(0.5) * np.float32(sx + sy) < np.float32(sigma_th):
+                conf += 1
+        ms[b] = np.float32(ssum / np.float32(2 * n)) if n else np.float32(np.inf)
+        nc[b] = conf
+        rel[b] = n > 0 and conf >= min_inliers and ms[b] < np.float32(sigma_th)
+    return ms, nc, rel

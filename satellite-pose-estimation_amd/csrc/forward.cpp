@@ -416,6 +416,18 @@ int spe_pnp_batch(void* stream, const float* points_px, const float* probs, cons
   return 0;
 }
 
+int spe_self_assess(void* stream, const float* probs, const float* sigmas, const int32_t* status,
+                    const int32_t* corr_label, const uint32_t* inlier_mask, int B, int Q, int C, float score_th,
+                    float sigma_th, int min_inliers, float* mean_sigma, int32_t* n_confident, uint8_t* reliable) {
+  if (!probs || !sigmas || !status || !corr_label || !inlier_mask || !mean_sigma || !n_confident || !reliable || B < 0 ||
+      Q <= 0 || Q > 64 || C < 2 || C > 17 || min_inliers < 0)
+    return fail(SPE_E_ARG, "bad argument");
+  SelfAssessArgs a{probs, sigmas, status, corr_label, inlier_mask, B, Q, C, score_th, sigma_th, min_inliers,
+                   mean_sigma, n_confident, reliable};
+  CK(spe_launch_self_assess(a, (hipStream_t)stream));
+  return 0;
+}
+
 int spe_speed_score(void* stream, const float* quat, const double* tvec, const double* q_gt, const double* t_gt, int B,
                     double* s_t, double* s_q) {
   if (!quat || !tvec || !q_gt || !t_gt || !s_t || !s_q || B < 0) return fail(SPE_E_ARG, "bad argument");

@@ -364,7 +364,61 @@ __global__ void score_kernel(const float* __restrict__ quat, const double* __res
   s_q[b] = 2 * acos(d < 1 ? d : 1);
 }
 
+// Self-assessment filter (BASELINE config 4).  The reference has no code for it: the UNC README
+// (ROOT/README.md:15-20) describes a mechanism that "filters out unreliable pose estimation
+// results" from the predicted keypoint sigmas, and the only code trace is the commented per-
+// keypoint gate `s_ > 0.5 and sig.mean() < 5` (UNC/utils/speed_eval_ceres.py:110-114).  Defined
+// here (parity unpinned): with the solver's correspondence selection
+// re-derived from probs (same argmax / first-on-ties rule as pnp_kernel), over the RANSAC
+// inliers j of image b:
+//     mean_sigma[b] = mean over inliers and both axes of sigma[sel(j)]
+//     confident(j)  = score(sel(j)) > score_th  and  mean(sigma[sel(j)]) < sigma_th
+//     reliable[b]   = status in {0, 3} and #confident inliers >= min_inliers and mean_sigma < sigma_th
+// One thread per image (Q <= 64, C <= 17): the whole pass is a few hundred loads.
+__global__ void self_assess_kernel(SelfAssessArgs a) {
+  const int b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= a.B) return;
+  const int Q = a.Q, C = a.C;
+  int best_q[MAXN];
+  float best_s[MAXN];
+  for (int l = 0; l < MAXN; ++l) { best_q[l] = -1; best_s[l] = 0.f; }
+  for (int q = 0; q < Q; ++q) {
+    const float* p = a.probs + ((size_t)b * Q + q) * C;
+    int lab = 0;
+    float sc = p[0];
+    for (int c = 1; c < C; ++c)
+      if (p[c] > sc) { sc = p[c]; lab = c; }
+    if (lab == C - 1) continue;
+    if (best_q[lab] < 0 || sc > best_s[lab]) { best_q[lab] = q; best_s[lab] = sc; }
+  }
+  const int st = a.status[b];
+  const uint32_t inl = (st == SPE_PNP_OK || st == SPE_PNP_RANSAC_FALLBACK) ? a.inlier_mask[b] : 0u;
+  float ssum = 0.f;
+  int n = 0, nconf = 0;
+  for (int j = 0; j < MAXN; ++j) {
+    if (!(inl & (1u << j))) continue;
+    const int lab = a.corr_label[MAXN * b + j];
+    if (lab < 0 || lab >= MAXN || best_q[lab] < 0) continue;
+    const int q = best_q[lab];
+    const float sx = a.sigmas[((size_t)b * Q + q) * 2], sy = a.sigmas[((size_t)b * Q + q) * 2 + 1];
+    ssum += sx + sy;
+    n++;
+    if (best_s[lab] > a.score_th && 0.5f * (sx + sy) < a.sigma_th) nconf++;
+  }
+  const float ms = n ? ssum / (2.f * n) : INFINITY;
+  a.mean_sigma[b] = ms;
+  a.n_confident[b] = nconf;
+  a.reliable[b] = (n > 0 && nconf >= a.min_inliers && ms < a.sigma_th) ? 1 : 0;
+}
+
 }  // namespace
+
+int spe_launch_self_assess(const SelfAssessArgs& a, hipStream_t s) {
+  if (a.B <= 0) return 0;
+  if (a.Q > WAVE || a.C < 2 || a.C - 1 > MAXN) return -7;
+  hipLaunchKernelGGL(self_assess_kernel, dim3((a.B + 127) / 128), dim3(128), 0, s, a);
+  return (int)hipGetLastError();
+}
 
 int spe_launch_pnp(const PnpArgs& a, hipStream_t s) {
   if (a.B <= 0) return 0;

@@ -24,5 +24,20 @@ struct PnpArgs {
   uint32_t* inlier_mask;   // [B] or null (bit i = correspondence i)
 };
 int spe_launch_pnp(const PnpArgs& a, hipStream_t s);
+
+struct SelfAssessArgs {
+  const float* probs;         // [B][Q][C]
+  const float* sigmas;        // [B][Q][2]
+  const int32_t* status;      // [B]     (pnp_kernel outputs)
+  const int32_t* corr_label;  // [B][16]
+  const uint32_t* inlier_mask;// [B]
+  int B, Q, C;
+  float score_th, sigma_th;
+  int min_inliers;
+  float* mean_sigma;          // [B]
+  int32_t* n_confident;       // [B]
+  uint8_t* reliable;          // [B]
+};
+int spe_launch_self_assess(const SelfAssessArgs& a, hipStream_t s);
 int spe_launch_score(const float* quat, const double* tvec, const double* q_gt, const double* t_gt, int B,
                      double* s_t, double* s_q, hipStream_t s);

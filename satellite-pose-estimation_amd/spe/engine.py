@@ -28,7 +28,9 @@ def evaluate(model, criterion, postprocessors, data_loader, gt_file, solver, dev
         q_gt = torch.tensor([g["quat"] for g in gt], dtype=torch.float64, device=device)
         t_gt = torch.tensor([g["tvec"] for g in gt], dtype=torch.float64, device=device)
         s_t, s_q = device_speed_score(poses["quat"], poses["tvec"], q_gt, t_gt)
-        evaluator.update_batch(filenames, outputs["points_px"], outputs["probs"], poses, s_t, s_q)
+        sig = outputs.get("sigmas")
+        assess = solver.self_assess(outputs["probs"], sig, poses) if sig is not None else None
+        evaluator.update_batch(filenames, outputs["points_px"], outputs["probs"], poses, s_t, s_q, sig, assess)
     evaluator.log = spe_dist.all_gather_log(evaluator.log)
     evaluator.summarize()
     stats = {"speed_eval_pose": evaluator.stats}

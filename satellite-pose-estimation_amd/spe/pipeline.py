@@ -14,8 +14,10 @@ from .speed_eval import device_speed_score
 
 
 class PosePipeline:
-    def __init__(self, model: DETR, solver: PoseSolver, batch: int, device="cuda", use_graph: bool = False):
+    def __init__(self, model: DETR, solver: PoseSolver, batch: int, device="cuda", use_graph: bool = False,
+                 self_assess: bool = True):
         self.model, self.solver, self.B = model, solver, batch
+        self.self_assess = self_assess
         self.device = torch.device(device)
         S, Q = model.cfg.input_size, model.cfg.num_queries
         dev = self.device
@@ -36,7 +38,10 @@ class PosePipeline:
         sig = fo.get("sigmas")
         poses = self.solver.solve_batch(fo["points_px"], fo["probs"], sig)
         s_t, s_q = device_speed_score(poses["quat"], poses["tvec"], self.q_gt, self.t_gt)
-        return {"forward": fo, "poses": poses, "s_t": s_t, "s_q": s_q}
+        out = {"forward": fo, "poses": poses, "s_t": s_t, "s_q": s_q}
+        if sig is not None and self.self_assess:
+            out["assess"] = self.solver.self_assess(fo["probs"], sig, poses)   # config-4 filter
+        return out
 
     def load(self, images, clip_bbox, q_gt=None, t_gt=None):
         self.images.copy_(images, non_blocking=True)

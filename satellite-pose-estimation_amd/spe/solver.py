@@ -67,6 +67,23 @@ class PoseSolver:
             _lib.ptr(out["corr_label"]), _lib.ptr(out["inlier_mask"])), "spe_pnp_batch")
         return out
 
+    def self_assess(self, probs, sigmas, poses, score_th=0.5, sigma_th=5.0, min_inliers=4, stream=None):
+        """Self-assessment filter over a solve_batch result (BASELINE config 4; definition and
+        its unpinned status: include/spe.h spe_self_assess, after the commented gate of
+        UNC/utils/speed_eval_ceres.py:110-114).  Returns device tensors mean_sigma [B] f32,
+        n_confident [B] i32, reliable [B] bool."""
+        B, Q, C = probs.shape
+        dev = probs.device
+        out = dict(mean_sigma=torch.empty(B, device=dev), n_confident=torch.empty(B, dtype=torch.int32, device=dev),
+                   reliable=torch.empty(B, dtype=torch.uint8, device=dev))
+        _lib.check(_lib.lib().spe_self_assess(
+            _lib.stream_ptr(stream), _lib.ptr(probs.contiguous()), _lib.ptr(sigmas.contiguous()),
+            _lib.ptr(poses["status"]), _lib.ptr(poses["corr_label"]), _lib.ptr(poses["inlier_mask"]), B, Q, C,
+            float(score_th), float(sigma_th), int(min_inliers), _lib.ptr(out["mean_sigma"]),
+            _lib.ptr(out["n_confident"]), _lib.ptr(out["reliable"])), "spe_self_assess")
+        out["reliable"] = out["reliable"].bool()
+        return out
+
     def find_index(self, logits):
         return logits.argmax(1), logits.max(1)
 

@@ -94,10 +94,15 @@ class SpeedEval:
             s_t, s_q = speed_score(quat_pr, tvec_pr, gt["quat"], gt["tvec"])
             self._record(filename, ret["points"], ret["logits"], quat_pr, tvec_pr, s_t, s_q)
 
-    def update_batch(self, filenames, points_px, probs, poses, s_t=None, s_q=None):
+    def update_batch(self, filenames, points_px, probs, poses, s_t=None, s_q=None, sigmas=None, assess=None):
         """Hot-path variant: `poses` is the dict returned by solver.solve_batch (device), optional
         device scores from device_speed_score.  Failed images carry zero poses (status != 0
-        except RANSAC_FALLBACK), exactly as update() produces them."""
+        except RANSAC_FALLBACK), exactly as update() produces them.  With the sigma head the
+        record also carries "sigma" (UNC/src/data/speed/speed_dataset.py:437, 8 dp) and, when
+        `assess` (solver.self_assess output) is given, the self-assessment verdict."""
+        sg = sigmas.detach().cpu().numpy() if sigmas is not None else None
+        ms = assess["mean_sigma"].cpu().numpy() if assess is not None else None
+        rl = assess["reliable"].cpu().numpy() if assess is not None else None
         pts = points_px.detach().cpu().numpy()
         prb = probs.detach().cpu().numpy()
         quat = poses["quat"].double().cpu().numpy()
@@ -111,6 +116,11 @@ class SpeedEval:
             else:
                 a, b = float(st_dev[i]), float(sq_dev[i])
             self._record(fn, pts[i], prb[i], quat[i], tvec[i], a, b)
+            if sg is not None:
+                self.log[fn]["sigma"] = np.around(sg[i], decimals=8).tolist()
+            if rl is not None:
+                self.log[fn]["mean_sigma"] = float(np.around(ms[i], decimals=8))
+                self.log[fn]["reliable"] = bool(rl[i])
 
     def summarize(self):
         """REV/datasets/speed.py:382-421, including its quirk: the "median" fields are taken of
@@ -131,4 +141,8 @@ class SpeedEval:
         tvec_abs_median = np.median(tvec_abs, 0).tolist()
         self.stats += ("mean tvec abs: [{:.6f}, {:.6f}, {:.6f}], median tvec abs:"
                        "[{:.6f}, {:.6f}, {:.6f}]").format(*(tvec_abs_mean + tvec_abs_median))
+        if any("reliable" in it for it in items):
+            kept = [it["score"] for it in items if it.get("reliable")]
+            self.stats += "; self-assessment: {:d}/{:d} reliable, final score (reliable): {}".format(
+                len(kept), len(items), "{:.6f}".format(float(np.mean(kept))) if kept else "n/a")
         return self.stats

@@ -112,6 +112,31 @@ def test_solver_matches_oracle(gpu_device, mode):
     assert np.all(h["quat"][~ok] == 0) and np.all(h["tvec"][~ok] == 0)
 
 
+@pytest.mark.parametrize("sigma_th,score_th,min_inl", [(5.0, 0.5, 4), (10.0, 0.3, 4), (12.0, 0.0, 6)])
+def test_self_assessment_matches_oracle(gpu_device, sigma_th, score_th, min_inl):
+    """Config-4 self-assessment filter (definition unpinned: include/spe.h spe_self_assess) on
+    the sigma solver's own output; integer outputs bit-exact, mean sigma to f32 rounding."""
+    import pnp_ref
+    from spe.solver import PoseSolver
+    pts, probs, q, t, sig = solver_stress_set(256, seed=77)
+    s = PoseSolver(mode=2, repro=25.0)
+    dev = torch.device("cuda:0")
+    pd, sd = torch.from_numpy(probs).to(dev), torch.from_numpy(sig).to(dev)
+    poses = s.solve_batch(torch.from_numpy(pts).to(dev), pd, sd)
+    h = s.self_assess(pd, sd, poses, score_th=score_th, sigma_th=sigma_th, min_inliers=min_inl)
+    torch.cuda.synchronize()
+    p = {k: v.cpu().numpy() for k, v in poses.items()}
+    ms, nc, rel = pnp_ref.self_assess(probs, sig, p["status"], p["corr_label"], p["inlier_mask"].astype(np.uint32),
+                                      score_th, sigma_th, min_inl)
+    hm = h["mean_sigma"].cpu().numpy()
+    np.testing.assert_array_equal(h["n_confident"].cpu().numpy(), nc)
+    np.testing.assert_array_equal(h["reliable"].cpu().numpy(), rel)
+    fin = np.isfinite(ms)
+    np.testing.assert_array_equal(np.isfinite(hm), fin)
+    np.testing.assert_allclose(hm[fin], ms[fin], rtol=1e-6)
+    assert 0 < rel.sum() < len(rel) or sigma_th == 5.0
+
+
 def test_solver_known_answer(gpu_device):
     with open(os.path.join(GOLDEN, "pnp_kat_wz_real.json")) as f:
         kat = json.load(f)["images"]
