@@ -10,6 +10,8 @@
 #include <cstdio>
 #include <cstring>
 #include <functional>
+#include <map>
+#include <mutex>
 
 #include "model_state.h"
 #include "spe_pnp.h"
@@ -397,6 +399,26 @@ int spe_postprocess(void* stream, const float* logits, const float* points, cons
   return 0;
 }
 
+// Device scratch for the EPnP-RANSAC hypothesis records (sigma mode): one buffer per device,
+// grown on demand and kept for the process lifetime, so steady-state calls allocate nothing (a
+// first call with a larger batch allocates and must therefore happen outside graph capture).
+static HypRec* hyp_scratch(size_t n) {
+  static std::mutex mu;
+  static std::map<int, std::pair<HypRec*, size_t>> bufs;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> g(mu);
+  auto& e = bufs[dev];
+  if (e.second < n) {
+    if (e.first) (void)hipFree(e.first);
+    e.first = nullptr;
+    e.second = 0;
+    if (hipMalloc((void**)&e.first, n * sizeof(HypRec)) != hipSuccess) return nullptr;
+    e.second = n;
+  }
+  return e.first;
+}
+
 int spe_pnp_batch(void* stream, const float* points_px, const float* probs, const float* sigmas, int B, int Q, int C,
                   const double* K, const double* world, int mode, float repro, int ransac_iters, double confidence,
                   float* quat, double* tvec, double* rvec, int32_t* status, int32_t* n_corr, int32_t* corr_label,
@@ -412,6 +434,11 @@ int spe_pnp_batch(void* stream, const float* points_px, const float* probs, cons
   a.ransac_iters = ransac_iters; a.confidence = confidence;
   a.quat = quat; a.tvec = tvec; a.rvec = rvec; a.status = status; a.n_corr = n_corr;
   a.corr_label = corr_label; a.inlier_mask = inlier_mask;
+  if (mode == SPE_PNP_EPNP_RANSAC_SIGMA && B > 0) {
+    a.hyp = hyp_scratch((size_t)B * ransac_iters);
+    a.hyp_stride = ransac_iters;
+    if (!a.hyp) return fail(SPE_E_LAUNCH, "hypothesis scratch allocation failed");
+  }
   CK(spe_launch_pnp(a, (hipStream_t)stream));
   return 0;
 }

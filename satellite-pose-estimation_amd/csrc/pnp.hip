@@ -136,13 +136,123 @@ __device__ void epnp_solve_wave(EpnpShared& sh, const cam_t* k, const float* img
   __syncthreads();
 }
 
+// Correspondence selection (REV/utils/speed_eval.py:152-206): lane-parallel argmax over the C
+// class probabilities, then (lane 0) first-seen label order with the best-score query per label.
+struct SelShared {
+  int lab[WAVE];
+  float score[WAVE];
+  int nl, order[MAXN], bestq[MAXN];
+  float img[2 * MAXN], wld[3 * MAXN], sig[2 * MAXN];
+};
+
+__device__ void select_correspondences(const PnpArgs& a, int b, int lane, SelShared& sh) {
+  const int Q = a.Q, C = a.C;
+  for (int q = lane; q < Q; q += WAVE) {
+    const float* p = a.probs + ((size_t)b * Q + q) * C;
+    int lab = 0;
+    float sc = p[0];
+    for (int c = 1; c < C; ++c)
+      if (p[c] > sc) { sc = p[c]; lab = c; }
+    if (q < WAVE) { sh.lab[q] = lab; sh.score[q] = sc; }
+  }
+  __syncthreads();
+  if (lane == 0) {
+    int nl = 0;
+    float best_s[MAXN];
+    for (int q = 0; q < Q && q < WAVE; ++q) {
+      const int lab = sh.lab[q];
+      if (lab == C - 1) continue;
+      int j;
+      for (j = 0; j < nl; ++j) if (sh.order[j] == lab) break;
+      if (j == nl) { if (nl < MAXN) { sh.order[nl] = lab; sh.bestq[nl] = q; best_s[nl] = sh.score[q]; nl++; } }
+      else if (sh.score[q] > best_s[j]) { sh.bestq[j] = q; best_s[j] = sh.score[q]; }
+    }
+    sh.nl = nl;
+    for (int j = 0; j < nl; ++j) {
+      const int q = sh.bestq[j];
+      sh.img[2 * j] = a.points[((size_t)b * Q + q) * 2];
+      sh.img[2 * j + 1] = a.points[((size_t)b * Q + q) * 2 + 1];
+      for (int c = 0; c < 3; ++c) sh.wld[3 * j + c] = (float)a.world[3 * sh.order[j] + c];
+      sh.sig[2 * j] = a.sigmas ? a.sigmas[((size_t)b * Q + q) * 2] : 1.f;
+      sh.sig[2 * j + 1] = a.sigmas ? a.sigmas[((size_t)b * Q + q) * 2 + 1] : 1.f;
+    }
+  }
+  __syncthreads();
+}
+
+// The cv::RNG((uint64)-1) subset stream of OpenCV's RANSACPointSetRegistrator: `mp` distinct
+// indices in [0, nl) per iteration, rejection-sampled, iterations drawn in order.
+__device__ void draw_subset(rng_t* rng, int nl, int mp, int* idx) {
+  for (int i = 0; i < mp; ++i) {
+    for (;;) {
+      int v = rng_uniform(rng, 0, nl), j;
+      idx[i] = v;
+      for (j = 0; j < i; ++j) if (v == idx[j]) break;
+      if (j == i) break;
+    }
+  }
+}
+
+// RANSAC uses EPnP hypotheses (5-point model): sigma mode with more than 5 correspondences
+SPE_DEV bool epnp_ransac_path(const PnpArgs& a, int nl) { return a.mode == SPE_PNP_EPNP_RANSAC_SIGMA && nl > 5; }
+
+// EPnP-RANSAC hypotheses, one wave per (image, iteration): the 12x12 eigen-decomposition of a
+// 5-point EPnP runs wave-cooperatively (jacobi12_rr_wave) instead of serially on one lane of the
+// image's wave, so the ~100 hypotheses of an image run concurrently across the chip.  Same IEEE
+// operation sequence as the serial per-lane form (jacobi12_rr == the oracle's), so inlier sets
+// stay bit-identical.  Results go to a[b][it] records; pnp_kernel replays the adaptive loop.
+__global__ __launch_bounds__(WAVE) void pnp_hyp_kernel(PnpArgs a, int iters) {
+  const int b = blockIdx.x / iters, it = blockIdx.x - b * iters;
+  const int lane = threadIdx.x;
+  __shared__ SelShared sel;
+  __shared__ float h_img[10], h_wld[15];
+  __shared__ double h_rt[6];
+  __shared__ EpnpShared s_ep;
+  select_correspondences(a, b, lane, sel);
+  const int nl = sel.nl;
+  if (!epnp_ransac_path(a, nl)) return;              // wave-uniform
+  if (lane == 0) {
+    rng_t rng = {(uint64_t)-1};
+    int idx[5];
+    for (int j = 0; j <= it; ++j) draw_subset(&rng, nl, 5, idx);
+    for (int i = 0; i < 5; ++i) {
+      h_img[2 * i] = sel.img[2 * idx[i]]; h_img[2 * i + 1] = sel.img[2 * idx[i] + 1];
+      for (int c = 0; c < 3; ++c) h_wld[3 * i + c] = sel.wld[3 * idx[i] + c];
+    }
+  }
+  __syncthreads();
+  const cam_t k = {a.K[0], a.K[4], a.K[2], a.K[5]};
+  double r[3], tt[3];
+  epnp_solve_wave(s_ep, &k, h_img, h_wld, 5, 0x1Fu, 1, r, tt, lane);
+  if (lane == 0) for (int c = 0; c < 3; ++c) { h_rt[c] = r[c]; h_rt[3 + c] = tt[c]; }
+  __syncthreads();
+  for (int c = 0; c < 3; ++c) { r[c] = h_rt[c]; tt[c] = h_rt[3 + c]; }
+  const float thr2 = (float)((double)a.repro * (double)a.repro);
+  bool in = false;
+  if (lane < nl) {
+    double R[9];
+    rodrigues_r2R(r, R);
+    float uv[2];
+    project_f(&k, R, tt, sel.wld + 3 * lane, uv);
+    in = sq_err_f(sel.img + 2 * lane, uv) <= thr2;
+  }
+  const uint64_t m = __ballot(in);
+  if (lane == 0) {
+    HypRec& h = a.hyp[(size_t)b * a.hyp_stride + it];
+    for (int c = 0; c < 6; ++c) h.rt[c] = h_rt[c];
+    h.mask = (uint32_t)m;
+    h.good = __popcll(m);
+    h.ok = 1;
+  }
+}
+
 __global__ __launch_bounds__(WAVE) void pnp_kernel(PnpArgs a) {
   const int b = blockIdx.x;
   const int lane = threadIdx.x;
-  __shared__ int s_lab[WAVE];
-  __shared__ float s_score[WAVE];
-  __shared__ int s_nl, s_order[MAXN], s_bestq[MAXN];
-  __shared__ float s_img[2 * MAXN], s_wld[3 * MAXN], s_sig[2 * MAXN];
+  __shared__ SelShared sel;
+  float* const s_img = sel.img;
+  float* const s_wld = sel.wld;
+  float* const s_sig = sel.sig;
   __shared__ unsigned char s_idx[MAXIT][5];
   __shared__ int s_ok[MAXIT], s_good[MAXIT];
   __shared__ uint32_t s_mask[MAXIT];
@@ -150,41 +260,9 @@ __global__ __launch_bounds__(WAVE) void pnp_kernel(PnpArgs a) {
   __shared__ EpnpShared s_ep;
 
   const cam_t k = {a.K[0], a.K[4], a.K[2], a.K[5]};
-  const int Q = a.Q, C = a.C;
 
-  // ---- correspondence selection
-  for (int q = lane; q < Q; q += WAVE) {
-    const float* p = a.probs + ((size_t)b * Q + q) * C;
-    int lab = 0;
-    float sc = p[0];
-    for (int c = 1; c < C; ++c)
-      if (p[c] > sc) { sc = p[c]; lab = c; }
-    if (q < WAVE) { s_lab[q] = lab; s_score[q] = sc; }
-  }
-  __syncthreads();
-  if (lane == 0) {
-    int nl = 0;
-    float best_s[MAXN];
-    for (int q = 0; q < Q && q < WAVE; ++q) {
-      const int lab = s_lab[q];
-      if (lab == C - 1) continue;
-      int j;
-      for (j = 0; j < nl; ++j) if (s_order[j] == lab) break;
-      if (j == nl) { if (nl < MAXN) { s_order[nl] = lab; s_bestq[nl] = q; best_s[nl] = s_score[q]; nl++; } }
-      else if (s_score[q] > best_s[j]) { s_bestq[j] = q; best_s[j] = s_score[q]; }
-    }
-    s_nl = nl;
-    for (int j = 0; j < nl; ++j) {
-      const int q = s_bestq[j];
-      s_img[2 * j] = a.points[((size_t)b * Q + q) * 2];
-      s_img[2 * j + 1] = a.points[((size_t)b * Q + q) * 2 + 1];
-      for (int c = 0; c < 3; ++c) s_wld[3 * j + c] = (float)a.world[3 * s_order[j] + c];
-      s_sig[2 * j] = a.sigmas ? a.sigmas[((size_t)b * Q + q) * 2] : 1.f;
-      s_sig[2 * j + 1] = a.sigmas ? a.sigmas[((size_t)b * Q + q) * 2 + 1] : 1.f;
-    }
-  }
-  __syncthreads();
-  const int nl = s_nl;
+  select_correspondences(a, b, lane, sel);
+  const int nl = sel.nl;
   const uint32_t all = nl >= 32 ? 0xffffffffu : ((1u << nl) - 1);
 
   double rvec[3] = {0, 0, 0}, t[3] = {0, 0, 0};
@@ -225,25 +303,28 @@ __global__ __launch_bounds__(WAVE) void pnp_kernel(PnpArgs a) {
     } else {
       const int iters = a.ransac_iters < MAXIT ? a.ransac_iters : MAXIT;
       // 1. subset stream of cv::RNG((uint64)-1), drawn in order
-      if (lane == 0) {
+      const bool pre = kernel == 1 && a.hyp != nullptr;   // hypotheses precomputed by pnp_hyp_kernel
+      if (lane == 0 && !pre) {
         rng_t rng = {(uint64_t)-1};
         for (int it = 0; it < iters; ++it) {
           int idx[5];
-          for (int i = 0; i < mp; ++i) {
-            for (;;) {
-              int v = rng_uniform(&rng, 0, nl), j;
-              idx[i] = v;
-              for (j = 0; j < i; ++j) if (v == idx[j]) break;
-              if (j == i) break;
-            }
-            s_idx[it][i] = (unsigned char)idx[i];
-          }
+          draw_subset(&rng, nl, mp, idx);
+          for (int i = 0; i < mp; ++i) s_idx[it][i] = (unsigned char)idx[i];
         }
       }
       __syncthreads();
       // 2. hypotheses + float32 inlier sets, lane-parallel
       const float thr2 = (float)((double)a.repro * (double)a.repro);
-      for (int it = lane; it < iters; it += WAVE) {
+      if (pre) {
+        for (int it = lane; it < iters; it += WAVE) {
+          const HypRec& h = a.hyp[(size_t)b * a.hyp_stride + it];
+          s_ok[it] = h.ok;
+          s_good[it] = h.good;
+          s_mask[it] = h.mask;
+          for (int c = 0; c < 6; ++c) s_rt[it][c] = h.rt[c];
+        }
+      }
+      for (int it = pre ? iters : lane; it < iters; it += WAVE) {
         float si[10], sw[15];
         for (int i = 0; i < mp; ++i) {
           const int j = s_idx[it][i];
@@ -340,7 +421,7 @@ __global__ __launch_bounds__(WAVE) void pnp_kernel(PnpArgs a) {
   if (a.status) a.status[b] = status;
   if (a.n_corr) a.n_corr[b] = nl;
   if (a.inlier_mask) a.inlier_mask[b] = inl;
-  if (a.corr_label) for (int j = 0; j < MAXN; ++j) a.corr_label[MAXN * b + j] = j < nl ? s_order[j] : -1;
+  if (a.corr_label) for (int j = 0; j < MAXN; ++j) a.corr_label[MAXN * b + j] = j < nl ? sel.order[j] : -1;
 }
 
 // SPEED score (REV/utils/speed_eval.py:245-262): q sign-normalised, s_t = |dt|/|t_gt|,
@@ -423,6 +504,10 @@ int spe_launch_self_assess(const SelfAssessArgs& a, hipStream_t s) {
 int spe_launch_pnp(const PnpArgs& a, hipStream_t s) {
   if (a.B <= 0) return 0;
   if (a.Q > WAVE || a.C < 2 || a.C - 1 > MAXN || a.ransac_iters > MAXIT - 1) return -7;
+  if (a.hyp) {
+    if (a.hyp_stride < a.ransac_iters) return -7;
+    hipLaunchKernelGGL(pnp_hyp_kernel, dim3(a.B * a.ransac_iters), dim3(WAVE), 0, s, a, a.ransac_iters);
+  }
   hipLaunchKernelGGL(pnp_kernel, dim3(a.B), dim3(WAVE), 0, s, a);
   return (int)hipGetLastError();
 }

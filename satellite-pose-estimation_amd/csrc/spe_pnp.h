@@ -4,6 +4,13 @@
 #include <stdint.h>
 #include "../../include/spe.h"
 
+// One EPnP-RANSAC hypothesis (pnp_hyp_kernel -> pnp_kernel)
+struct HypRec {
+  double rt[6];            // rvec, tvec
+  uint32_t mask;           // float32 inlier set over the correspondences
+  int good, ok, pad;
+};
+
 struct PnpArgs {
   const float* points;     // [B][Q][2] image px (PostProcess output)
   const float* probs;      // [B][Q][C] softmax probabilities
@@ -22,6 +29,8 @@ struct PnpArgs {
   int32_t* n_corr;         // [B] or null
   int32_t* corr_label;     // [B][16] or null
   uint32_t* inlier_mask;   // [B] or null (bit i = correspondence i)
+  HypRec* hyp;             // [B][hyp_stride] scratch for the EPnP-RANSAC hypotheses (sigma mode) or null
+  int hyp_stride;
 };
 int spe_launch_pnp(const PnpArgs& a, hipStream_t s);
 
