@@ -62,6 +62,8 @@ def parse():
     p.add_argument("--weights", default="label-diverse", choices=["label-diverse", "random"],
                    help="label-diverse: random init made query-diverse so the solver sees >= 4 "
                         "correspondences like a trained model (spe.synthetic.bench_weights)")
+    p.add_argument("--no-overlap", action="store_true",
+                   help="run the solver on the forward's stream (default: solver of batch i overlaps the forward of i+1)")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--launch-table", default=None,
@@ -156,7 +158,7 @@ def main():
     model = DETR(cfg, dtype=args.dtype)
     model.load_state_dict(bench_weights(cfg, 0, hs_fn) if args.weights == "label-diverse" else random_weights(cfg, 0))
     solver = build_solver(argparse.Namespace(solver=args.solver, repro=20))
-    pipe = PosePipeline(model, solver, B, device=dev)
+    pipe = PosePipeline(model, solver, B, device=dev, overlap=not args.no_overlap)
     data = synthetic_batch(cfg, B, seed=1000 + rank)
     pipe.load(torch.from_numpy(data["images"]).to(dev), torch.from_numpy(data["clip_bbox"]).float().to(dev),
               torch.from_numpy(data["quat"]).to(dev), torch.from_numpy(data["tvec"]).to(dev))
@@ -165,9 +167,11 @@ def main():
     def step():
         out = pipe.run()
         if world > 1:
-            rec = sd.pack_records(out["poses"]["quat"], out["poses"]["tvec"], out["s_t"], out["s_q"],
-                                  out["poses"]["status"])
-            sd.all_gather_records(rec)
+            # on the solver's stream: the record exchange waits for this batch's poses only
+            with torch.cuda.stream(out.get("stream") or torch.cuda.current_stream()):
+                rec = sd.pack_records(out["poses"]["quat"], out["poses"]["tvec"], out["s_t"], out["s_q"],
+                                      out["poses"]["status"])
+                sd.all_gather_records(rec)
         return out
 
     for _ in range(max(args.warmup, 1)):

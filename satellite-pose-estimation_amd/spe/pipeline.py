@@ -15,9 +15,15 @@ from .speed_eval import device_speed_score
 
 class PosePipeline:
     def __init__(self, model: DETR, solver: PoseSolver, batch: int, device="cuda", use_graph: bool = False,
-                 self_assess: bool = True):
+                 self_assess: bool = True, overlap: bool = False):
         self.model, self.solver, self.B = model, solver, batch
         self.self_assess = self_assess
+        # overlap: the solver / score / self-assessment of batch i run on a second HIP stream
+        # while the forward of batch i+1 runs on the caller's stream (the solver occupies one
+        # wave per image, far from filling the chip, and its latency is fp64-bound).  Results of
+        # a run() are then complete only after wait(out) (or a device synchronize).
+        self.overlap = overlap and not use_graph
+        self.solve_stream = torch.cuda.Stream(device=device) if self.overlap else None
         self.device = torch.device(device)
         S, Q = model.cfg.input_size, model.cfg.num_queries
         dev = self.device
@@ -33,15 +39,33 @@ class PosePipeline:
         self.out = None
         _ = Q
 
-    def _body(self):
-        fo = self.model(self.images, clip_bbox=self.clip_bbox)
+    def _solve(self, fo, stream=None):
         sig = fo.get("sigmas")
-        poses = self.solver.solve_batch(fo["points_px"], fo["probs"], sig)
-        s_t, s_q = device_speed_score(poses["quat"], poses["tvec"], self.q_gt, self.t_gt)
+        poses = self.solver.solve_batch(fo["points_px"], fo["probs"], sig, stream=stream)
+        s_t, s_q = device_speed_score(poses["quat"], poses["tvec"], self.q_gt, self.t_gt, stream=stream)
         out = {"forward": fo, "poses": poses, "s_t": s_t, "s_q": s_q}
         if sig is not None and self.self_assess:
-            out["assess"] = self.solver.self_assess(fo["probs"], sig, poses)   # config-4 filter
+            out["assess"] = self.solver.self_assess(fo["probs"], sig, poses, stream=stream)   # config-4 filter
         return out
+
+    def _body(self):
+        fo = self.model(self.images, clip_bbox=self.clip_bbox)
+        if not self.overlap:
+            return self._solve(fo)
+        s1 = self.solve_stream
+        s1.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s1):
+            for t in fo.values():
+                t.record_stream(s1)          # forward outputs are consumed on the solver stream
+            out = self._solve(fo, stream=s1)
+        out["stream"] = s1
+        return out
+
+    def wait(self, out=None):
+        """Make the caller's stream wait for a run()'s solver work (no-op without overlap)."""
+        out = out if out is not None else self.out
+        if out is not None and out.get("stream") is not None:
+            torch.cuda.current_stream().wait_stream(out["stream"])
 
     def load(self, images, clip_bbox, q_gt=None, t_gt=None):
         self.images.copy_(images, non_blocking=True)

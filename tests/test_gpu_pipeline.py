@@ -96,3 +96,30 @@ def test_evaluate_matches_reference_style_speedeval(gpu_device, small_model):
         assert a["quat_pr"] == c["quat_pr"] and a["tvec_pr"] == c["tvec_pr"]
         assert abs(a["score"] - c["score"]) < 1e-7
     assert stats["speed_eval_pose"] == ev2.stats
+
+
+@pytest.mark.parametrize("solver_name", ["epnp", "ransac_p3p_lm"])
+def test_overlapped_pipeline_equals_serial(gpu_device, small_model, solver_name):
+    """Solver of batch i on the second stream while the forward of batch i+1 runs: after wait(),
+    every batch's poses / scores equal the single-stream pipeline's (same inputs, same kernels)."""
+    from spe.pipeline import PosePipeline
+    from spe.solver import build_solver
+    cfg, w, m = small_model
+    B = 8
+    solver = build_solver(argparse.Namespace(solver=solver_name, repro=20))
+    batches = [synthetic_batch(cfg, B, 40 + i) for i in range(3)]
+    res = {}
+    for ov in (False, True):
+        pipe = PosePipeline(m, solver, B, device=gpu_device, overlap=ov)
+        outs = []
+        for b in batches:
+            pipe.load(torch.from_numpy(b["images"]).to(gpu_device), torch.from_numpy(b["clip_bbox"]).float().to(gpu_device))
+            outs.append(pipe.run())
+        for o in outs:
+            pipe.wait(o)
+        res[ov] = [(o["poses"]["status"].cpu().numpy(), o["poses"]["tvec"].cpu().numpy(), o["s_t"].cpu().numpy())
+                   for o in outs]
+    for (s0, t0, e0), (s1, t1, e1) in zip(res[False], res[True]):
+        np.testing.assert_array_equal(s0, s1)
+        np.testing.assert_array_equal(t0, t1)
+        np.testing.assert_array_equal(e0, e1)
