@@ -24,8 +24,8 @@ sys.path.insert(0, os.path.join(REPO, "satellite-pose-estimation_amd"))
 
 PEAK = {"bf16": {"mfma": 2500.0}, "fp32": {"mfma": 157.3}, "hbm": 8000.0}   # TFLOP/s, GB/s (MI355X_MICROARCH.md)
 # profiler symbol of each launch class (to match profiles/*kernel_stats.csv rows)
-KIND_SYMBOL = {"attn.enc": "attn_bf16_kernel<0>", "attn.dec_self": "attn_bf16_kernel<1>",
-               "attn.dec_cross": "attn_bf16_kernel<1>", "ffn.enc": "ffn_ln_kernel", "ffn.dec": "ffn_ln_kernel"}
+KIND_SYMBOL = {"attn.enc": "attn16_kernel<0, __bf16>", "attn.dec_self": "attn16_kernel<1, __bf16>",
+               "attn.dec_cross": "xattn_kernel", "ffn.enc": "ffn_ln_kernel", "ffn.dec": "ffn_ln_kernel"}
 
 
 # BASELINE.json configs: per-GPU shapes (configs 3-5 are quoted at bs=256 over 8 GPUs = 32/GPU)
@@ -33,7 +33,7 @@ PRESETS = {
     2: dict(batch=64, size=416, queries=11, layers=6, solver="epnp", sigma_head=0),
     3: dict(batch=32, size=416, queries=11, layers=6, solver="ransac_p3p_lm", sigma_head=0),
     4: dict(batch=32, size=416, queries=11, layers=6, solver="epnp_ransac_sigma", sigma_head=1),
-    5: dict(batch=32, size=640, queries=40, layers=6, solver="ransac_p3p_lm", sigma_head=0),
+    5: dict(batch=32, size=640, queries=40, layers=6, solver="ransac_p3p_lm", sigma_head=0, attn_dtype="fp16"),
 }
 CONFIG_NAME = {
     2: "BASELINE config 2: ResNet50-s8 + {L}/{L} DETR, {Q} queries, {S}x{S}, solver={solver}",
@@ -41,7 +41,7 @@ CONFIG_NAME = {
     4: "BASELINE config 4: ResNet50-s8 + {L}/{L} DETR + sigma head, {Q} queries, {S}x{S}, sigma-weighted "
        "EPnP-RANSAC + self-assessment filter (solver={solver})",
     5: "BASELINE config 5: ResNet50-s8 + {L}/{L} DETR, {Q} queries, {S}x{S} (train_resnet50s8_query40), "
-       "bf16 attention, solver={solver}",
+       "{A} MFMA encoder attention, solver={solver}",
 }
 
 
@@ -59,6 +59,8 @@ def parse():
     p.add_argument("--solver", default=None, choices=["epnp", "epnp_lm", "ransac_p3p_lm", "epnp_ransac_sigma"])
     p.add_argument("--sigma-head", type=int, default=None, choices=[0, 1])
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--attn-dtype", dest="attn_dtype", default=None, choices=["bf16", "fp16"],
+                   help="encoder self-attention operand type (bf16 models; config 5 preset: fp16)")
     p.add_argument("--weights", default="label-diverse", choices=["label-diverse", "random"],
                    help="label-diverse: random init made query-diverse so the solver sees >= 4 "
                         "correspondences like a trained model (spe.synthetic.bench_weights)")
@@ -72,6 +74,8 @@ def parse():
     for k, v in PRESETS[a.config].items():
         if getattr(a, k) is None:
             setattr(a, k, v)
+    if a.attn_dtype is None or a.dtype == "fp32":
+        a.attn_dtype = a.dtype
     return a
 
 
@@ -109,17 +113,26 @@ def cpu_baseline(cfg, seconds, solver="epnp"):
                       f"{cfg.enc_layers}/{cfg.dec_layers}, fp32 torch-CPU model + C {solver} oracle) in {dt:.1f}s"}
 
 
-def traffic_for(kind):
-    """HBM bytes per launch of `kind` from a committed PMC summary (profiles/pmc_*.json), or None."""
+def traffic_for(kind, grid, attn_dtype):
+    """HBM bytes per launch of `kind` from a committed PMC summary (profiles/pmc_*.json), or None.
+    Only a summary measured on the same launch (kind, grid size in threads, operand type) counts."""
     best = None
     for f in sorted(glob.glob(os.path.join(REPO, "profiles", "pmc_*.json"))):
         try:
             d = json.load(open(f))
         except Exception:
             continue
-        if d.get("kind") == kind and "hbm_bytes_per_launch" in d:
+        if (d.get("kind") == kind and "hbm_bytes_per_launch" in d and grid is not None and d.get("grid") == grid
+                and d.get("attn_dtype", "bf16") == attn_dtype):
             best = d["hbm_bytes_per_launch"]
     return best
+
+
+def launch_grid(kind, B, cfg):
+    """rocprofv3 Grid_Size (threads) of one launch of `kind` at this workload, where known."""
+    if kind == "attn.enc":
+        return B * cfg.nheads * ((cfg.tokens + 127) // 128) * 256
+    return None
 
 
 def main():
@@ -146,7 +159,7 @@ def main():
         # calibration pass of the HIP model itself (see spe.synthetic.bench_weights), run at the
         # bench batch size so every launch in this process has the timed shape (profiler
         # per-kernel averages then match the in-bench event timings)
-        m = DETR(cfg, dtype=args.dtype)
+        m = DETR(cfg, dtype=args.dtype, attn_dtype=args.attn_dtype)
         m.load_state_dict(w)
         n = len(images)
         reps = (B + n - 1) // n
@@ -155,7 +168,7 @@ def main():
         del m
         return hs
 
-    model = DETR(cfg, dtype=args.dtype)
+    model = DETR(cfg, dtype=args.dtype, attn_dtype=args.attn_dtype)
     model.load_state_dict(bench_weights(cfg, 0, hs_fn) if args.weights == "label-diverse" else random_weights(cfg, 0))
     solver = build_solver(argparse.Namespace(solver=args.solver, repro=20))
     pipe = PosePipeline(model, solver, B, device=dev, overlap=not args.no_overlap)
@@ -257,13 +270,15 @@ def main():
         "data": f"synthetic (seeded SPEED-shaped crops; {args.weights} random-init weights, "
                 "no checkpoint exists in the reference)",
         "config": {"workload": CONFIG_NAME[args.config].format(L=args.layers, Q=args.queries, S=args.size,
-                                                                solver=args.solver),
+                                                                solver=args.solver, A=args.attn_dtype),
                    "global_batch": B * world, "per_gpu_batch": B, "input_size": args.size,
-                   "num_queries": args.queries, "parallelism": f"dp{world} (image sharding)"},
-        "roofline": {"kernel": dominant, "kernel_symbol": KIND_SYMBOL.get(dominant, dominant),
+                   "num_queries": args.queries, "attention_dtype": args.attn_dtype,
+                   "parallelism": f"dp{world} (image sharding)"},
+        "roofline": {"kernel": dominant, "kernel_symbol": KIND_SYMBOL.get(dominant, dominant).replace(
+                         "<0, __bf16>", "<0, _Float16>" if args.attn_dtype == "fp16" else "<0, __bf16>"),
                      "bound": "mfma" if mfma_bound else "hbm", "achieved": achieved,
                      "peak": peak, "unit": unit, "frac": achieved / peak,
-                     "traffic": traffic_for(dominant), "launches": k_n, "avg_launch_ms": avg_ms,
+                     "traffic": traffic_for(dominant, launch_grid(dominant, B, cfg), args.attn_dtype), "launches": k_n, "avg_launch_ms": avg_ms,
                      "algorithmic_flops_per_launch": k_fl / max(k_n, 1),
                      "algorithmic_bytes_per_launch": k_by / max(k_n, 1)},
         "kernel_time_ms_per_step": {k: v[0] for k, v in sorted(tot.items(), key=lambda kv: -kv[1][0])},

@@ -18,7 +18,7 @@
 extern "C" {
 #endif
 
-#define SPE_ABI_VERSION 1
+#define SPE_ABI_VERSION 2
 
 enum {
   SPE_E_ARG = -1,        /* bad argument / size */
@@ -29,7 +29,7 @@ enum {
   SPE_E_LAUNCH = -6      /* kernel launch rejected its shapes */
 };
 
-enum { SPE_DTYPE_BF16_ = 0, SPE_DTYPE_F32_ = 1 };
+enum { SPE_DTYPE_BF16_ = 0, SPE_DTYPE_F32_ = 1, SPE_DTYPE_F16_ = 2 };
 
 /* Solver modes.
  *  SPE_PNP_EPNP              cv2.solvePnPGeneric(EPNP) on all selected points
@@ -64,6 +64,8 @@ typedef struct {
   int dim_feedforward;  /* --dim_feedforward (2048) */
   int sigma_head;       /* 1: UNC-style sigma head (sigma_embed.layers.*) */
   int dtype;            /* SPE_DTYPE_BF16_ (bf16 storage, fp32 accumulate) or SPE_DTYPE_F32_ */
+  int attn_dtype;       /* encoder self-attention operands (q, k, V^T): 0 = as dtype; SPE_DTYPE_F16_ =
+                         * fp16 (bf16 models only; BASELINE config 5's "fp16 MFMA attention") */
 } spe_model_config;
 
 typedef struct {
@@ -149,8 +151,8 @@ int spe_model_profile_get(const spe_model* m, int i, char* kind, int kind_len, d
 int spe_debug_gemm(void* stream, int dtype, int mode, const void* A, int lda, const void* P, int ldp, int prow, int H,
                    int W, int Cin, int KH, int KW, int stride, int pad, const void* Bw, int ldb, int M, int N, int K,
                    const float* bias, const void* R, int ldr, int relu, void* C, int ldc, int out_f32, int vt_T,
-                   int vt_B, int r_period, const float* ln_g, const float* ln_b);
-/* (ln_g/ln_b non-null: post-norm LayerNorm over each output row fused into the epilogue; bf16,
+                   int vt_B, int r_period, const float* ln_g, const float* ln_b, int out_f16);
+/* (out_f16: bf16 launches store fp16 instead of bf16.  ln_g/ln_b non-null: post-norm LayerNorm over each output row fused into the epilogue; bf16,
  * N == 256 and enough rows for the large-tile kernel, else SPE_E_LAUNCH) */
 int spe_debug_attention(void* stream, int dtype, const void* q, int ldq, const void* k, int ldk, const void* vt,
                         void* o, int ldo, int B, int H, int Tq, int Tk, float scale);

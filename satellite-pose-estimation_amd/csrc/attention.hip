@@ -20,7 +20,8 @@
 // come out in the exp2 domain), the running max only triggers an O/l rescale when some lane's
 // max actually grew (wave-uniform branch), and the row sums l are accumulated by the matrix
 // pipe (ones . P^T MFMA, which also normalises with exactly the bf16 P the numerator uses).
-// bf16: v_mfma_f32_32x32x16_bf16.  fp32 (parity mode): v_mfma_f32_32x32x2_f32, exact f32.
+// bf16: v_mfma_f32_32x32x16_bf16; fp16 operands (config 5): v_mfma_f32_32x32x16_f16 (same
+// kernel, AT<f16> traits).  fp32 (parity mode): v_mfma_f32_32x32x2_f32, exact f32.
 #include "spe_common.h"
 #include "spe_kernels.h"
 
@@ -152,11 +153,31 @@ SPE_DEV float tile_max(f32x16& s0, f32x16& s1, int key_base, int Tk, int hh) {
   return __builtin_fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
 }
 
+// 16-bit operand traits: bf16 (default) or fp16 (BASELINE config 5's "fp16 MFMA attention":
+// the encoder q/k projection and V^T are then stored as fp16 by their GEMM epilogues).  P is
+// packed with v_cvt_pkrtz_f16_f32 for fp16 (one instruction per two values, like
+// v_cvt_pk_bf16_f32; round-toward-zero costs < 1 fp16 ulp = 2^-10, below bf16's RNE 2^-9).
+template <typename TI> struct AT;
+template <> struct AT<bf16> {
+  typedef bf16x8 v8;
+  static constexpr uint32_t ONE2 = 0x3F803F80u;
+  static SPE_DEV uint32_t pk(float a, float b) { return pack_bf16x2(a, b); }
+  static SPE_DEV f32x16 mfma(v8 a, v8 b, f32x16 c) { return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0); }
+};
+template <> struct AT<f16> {
+  typedef f16x8 v8;
+  static constexpr uint32_t ONE2 = 0x3C003C00u;
+  static SPE_DEV uint32_t pk(float a, float b) { return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(a, b)); }
+  static SPE_DEV f32x16 mfma(v8 a, v8 b, f32x16 c) { return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0); }
+};
+
 // ------------------------------------------------------------------ bf16 kernel
 // ROLE only separates the symbols of the token-query (encoder self-attention) and the
 // object-query (decoder) launches so profiler summaries report them apart; the code is shared.
-template <int ROLE>
-__global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn_bf16_kernel(AttnArgs a) {
+template <int ROLE, typename TI>
+__global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn16_kernel(AttnArgs a) {
+  typedef AT<TI> A;
+  typedef typename A::v8 v8;
   constexpr int KBYTES = KT * KROW, VBYTES = 32 * VROW;
   __shared__ __attribute__((aligned(16))) char smem[2 * (KBYTES + VBYTES)];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -169,22 +190,22 @@ __global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn_bf16_kernel(AttnArgs a)
   const bool wave_live = qb * 128 + wid * 32 < a.Tq;
 
   // query fragment (B operand of S^T = K . Q^T), pre-scaled into the exp2 domain
-  bf16x8 qf[2];
+  v8 qf[2];
   {
     const float sl2 = a.scale * LOG2E;
-    const bf16* qp = (const bf16*)a.q + (size_t)(b * a.Tq + (q < a.Tq ? q : 0)) * a.ldq + h * 32;
+    const TI* qp = (const TI*)a.q + (size_t)(b * a.Tq + (q < a.Tq ? q : 0)) * a.ldq + h * 32;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       float f[8];
-      unpack16<bf16>(q < a.Tq ? ld16(qp + 16 * i + 8 * hh) : u32x4{0, 0, 0, 0}, f);
+      unpack16<TI>(q < a.Tq ? ld16(qp + 16 * i + 8 * hh) : u32x4{0, 0, 0, 0}, f);
 #pragma unroll
       for (int e = 0; e < 8; ++e) f[e] *= sl2;
-      qf[i] = __builtin_bit_cast(bf16x8, pack16<bf16>(f));
+      qf[i] = __builtin_bit_cast(v8, pack16<TI>(f));
     }
   }
-  u32x4 ones_u{0x3F803F80u, 0x3F803F80u, 0x3F803F80u, 0x3F803F80u};
+  u32x4 ones_u{A::ONE2, A::ONE2, A::ONE2, A::ONE2};
   asm volatile("" : "+v"(ones_u));      // keep in VGPRs (else rematerialised from SGPRs per use)
-  const bf16x8 ones = __builtin_bit_cast(bf16x8, ones_u);
+  const v8 ones = __builtin_bit_cast(v8, ones_u);
 
   // o: O^T accumulator; ls: running row sum (ones . P^T, every element equal), rescaled with o.
   f32x16 o, ls;
@@ -201,7 +222,7 @@ __global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn_bf16_kernel(AttnArgs a)
   // either spills or a wave of occupancy.)
   const int ntiles = (a.Tk + KT - 1) / KT;
   constexpr int SLOT = KBYTES + VBYTES;
-  Stage<bf16, KT> st;
+  Stage<TI, KT> st;
   st.load(a, b, h, 0, tid);
   st.store(smem, smem + KBYTES, tid);
   __syncthreads();
@@ -231,8 +252,8 @@ __global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn_bf16_kernel(AttnArgs a)
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub) {
         f32x16& s = sub ? s1 : s0;
-        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[sub][0]), qf[0], negm, 0, 0, 0);
-        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, kf[sub][1]), qf[1], s, 0, 0, 0);
+        s = A::mfma(__builtin_bit_cast(v8, kf[sub][0]), qf[0], negm);
+        s = A::mfma(__builtin_bit_cast(v8, kf[sub][1]), qf[1], s);
       }
 #ifdef SPE_X_NOMAX
       const float mx = kt == 0 ? s0[0] : 0.f;
@@ -269,12 +290,12 @@ __global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn_bf16_kernel(AttnArgs a)
         const f32x16& p = sub ? s1 : s0;
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks) {
-          u32x4 pw{pack_bf16x2(p[8 * ks + 0], p[8 * ks + 1]), pack_bf16x2(p[8 * ks + 2], p[8 * ks + 3]),
-                   pack_bf16x2(p[8 * ks + 4], p[8 * ks + 5]), pack_bf16x2(p[8 * ks + 6], p[8 * ks + 7])};
-          const bf16x8 pb = __builtin_bit_cast(bf16x8, pw);
-          o = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, vf[sub][ks]), pb, o, 0, 0, 0);
+          u32x4 pw{A::pk(p[8 * ks + 0], p[8 * ks + 1]), A::pk(p[8 * ks + 2], p[8 * ks + 3]),
+                   A::pk(p[8 * ks + 4], p[8 * ks + 5]), A::pk(p[8 * ks + 6], p[8 * ks + 7])};
+          const v8 pb = __builtin_bit_cast(v8, pw);
+          o = A::mfma(__builtin_bit_cast(v8, vf[sub][ks]), pb, o);
 #ifndef SPE_X_NOLS
-          ls = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ones, pb, ls, 0, 0, 0);   // column sums of P^T
+          ls = A::mfma(ones, pb, ls);   // column sums of P^T
 #endif
         }
       }
@@ -397,14 +418,19 @@ __global__ __launch_bounds__(NT, 2) void attn_f32_kernel(AttnArgs a) {
 
 int spe_launch_attention(const AttnArgs& a, int dtype, hipStream_t s) {
   if (a.B <= 0 || a.Tq <= 0 || a.Tk <= 0) return 0;
-  const int ce = dtype == SPE_DTYPE_BF16 ? 8 : 4;
+  const int ce = dtype == SPE_DTYPE_F32 ? 4 : 8;
   if ((a.ldq % ce) || (a.ldk % ce) || (a.ldo % 4)) return -5;
   dim3 grid(a.B * a.H * ((a.Tq + 127) / 128)), block(NT);
-  if (dtype == SPE_DTYPE_BF16)
+  if (dtype == SPE_DTYPE_F16)
     if (a.Tq >= 128)
-      hipLaunchKernelGGL(attn_bf16_kernel<0>, grid, block, 0, s, a);
+      hipLaunchKernelGGL((attn16_kernel<0, f16>), grid, block, 0, s, a);
     else
-      hipLaunchKernelGGL(attn_bf16_kernel<1>, grid, block, 0, s, a);
+      hipLaunchKernelGGL((attn16_kernel<1, f16>), grid, block, 0, s, a);
+  else if (dtype == SPE_DTYPE_BF16)
+    if (a.Tq >= 128)
+      hipLaunchKernelGGL((attn16_kernel<0, bf16>), grid, block, 0, s, a);
+    else
+      hipLaunchKernelGGL((attn16_kernel<1, bf16>), grid, block, 0, s, a);
   else
     hipLaunchKernelGGL(attn_f32_kernel, grid, block, 0, s, a);
   return (int)hipGetLastError();

@@ -12,7 +12,7 @@ extern "C" {
 int spe_debug_gemm(void* stream, int dtype, int mode, const void* A, int lda, const void* P, int ldp, int prow,
                    int H, int W, int Cin, int KH, int KW, int stride, int pad, const void* Bw, int ldb, int M, int N,
                    int K, const float* bias, const void* R, int ldr, int relu, void* C, int ldc, int out_f32, int vt_T,
-                   int vt_B, int r_period, const float* ln_g, const float* ln_b) {
+                   int vt_B, int r_period, const float* ln_g, const float* ln_b, int out_f16) {
   GemmArgs g{};
   g.A = A; g.lda = lda; g.P = P; g.ldp = ldp; g.prow = prow;
   g.H = H; g.W = W; g.Cin = Cin; g.KH = KH; g.KW = KW; g.stride = stride; g.pad = pad;
@@ -23,6 +23,7 @@ int spe_debug_gemm(void* stream, int dtype, int mode, const void* A, int lda, co
   g.vt_T = vt_T; g.vt_B = vt_B;
   g.r_period = r_period;
   g.ln_g = ln_g; g.ln_b = ln_b;
+  g.out_f16 = out_f16;
   int rc = spe_launch_gemm(g, dtype, mode, (hipStream_t)stream);
   return rc < 0 ? spe_fail(SPE_E_LAUNCH, "gemm launch rejected its arguments") : rc;
 }

@@ -55,10 +55,10 @@ int run_gemm(spe_model* m, const char* kind, const GemmArgs& g, int mode, hipStr
                    [&] { return spe_launch_gemm(g, m->cfg.dtype, mode, s); });
 }
 
-int run_attn(spe_model* m, const char* kind, const AttnArgs& a, hipStream_t s) {
+int run_attn(spe_model* m, const char* kind, const AttnArgs& a, int dtype, hipStream_t s) {
   const double flops = 4.0 * a.B * a.H * (double)a.Tq * a.Tk * 32;
   const double bytes = (double)a.B * a.H * 32 * (2.0 * a.Tq + 2.0 * a.Tk) * m->esz;
-  return run_other(m, kind, flops, bytes, s, [&] { return spe_launch_attention(a, m->cfg.dtype, s); });
+  return run_other(m, kind, flops, bytes, s, [&] { return spe_launch_attention(a, dtype, s); });
 }
 
 GemmArgs linear_args(const Conv& c, const void* A, int lda, int M, void* C, int ldc) {
@@ -221,15 +221,20 @@ int spe_forward(spe_model* m, void* stream, const float* images, int B, void* wo
   // ---------------- encoder (REV/models/transformer.py:154-167)
   const float scale = 1.0f / std::sqrt(32.0f);
   const int Mt = B * T;
+  // fp16 encoder attention operands (bf16 models, attn_dtype = SPE_DTYPE_F16_): the q/k and V^T
+  // projections store fp16, the attention runs fp16 MFMAs; everything else stays bf16
+  const int f16attn = c.attn_dtype == SPE_DTYPE_F16_ && dt == SPE_DTYPE_BF16;
   for (const Enc& e : m->enc) {
     {
       GemmArgs g = linear_args(e.qk, P(w.src), d, Mt, P(w.qkv), 3 * d);
+      g.out_f16 = f16attn;
       const int mode = add_pos(m, g, m->pos, d, T, e.pos_qk, 2 * d);
       CK(run_gemm(m, "gemm.enc.qk", g, mode, s));
     }
     {
       GemmArgs g = linear_args(e.v, P(w.src), d, Mt, P(w.vt), 8);
       g.vt_T = T; g.vt_B = B;
+      g.out_f16 = f16attn;
       CK(run_gemm(m, "gemm.enc.v", g, GEMM_LINEAR, s));
     }
     {
@@ -239,7 +244,7 @@ int spe_forward(spe_model* m, void* stream, const float* images, int B, void* wo
       a.vt = P(w.vt);
       a.o = P(w.ao); a.ldo = d;
       a.B = B; a.H = c.nheads; a.Tq = T; a.Tk = T; a.scale = scale;
-      CK(run_attn(m, "attn.enc", a, s));
+      CK(run_attn(m, "attn.enc", a, f16attn ? SPE_DTYPE_F16 : dt, s));
     }
     {
       // out-proj + residual; bf16 large batches fuse norm1 into the GEMM epilogue, in place over src
@@ -313,7 +318,7 @@ int spe_forward(spe_model* m, void* stream, const float* images, int B, void* wo
       a.vt = P(w.dvt);
       a.o = P(w.dao); a.ldo = d;
       a.B = B; a.H = c.nheads; a.Tq = Q; a.Tk = Q; a.scale = scale;
-      CK(run_attn(m, "attn.dec_self", a, s));
+      CK(run_attn(m, "attn.dec_self", a, dt, s));
     }
     {
       GemmArgs g = linear_args(e.so, P(w.dao), d, Mq, P(w.dtmp), d);
@@ -350,7 +355,7 @@ int spe_forward(spe_model* m, void* stream, const float* images, int B, void* wo
       a.vt = (char*)P(w.cvt) + (size_t)l * B * d * T * m->esz;
       a.o = P(w.dao); a.ldo = d;
       a.B = B; a.H = c.nheads; a.Tq = Q; a.Tk = T; a.scale = scale;
-      CK(run_attn(m, "attn.dec_cross", a, s));
+      CK(run_attn(m, "attn.dec_cross", a, dt, s));
     }
     }
     {

@@ -224,7 +224,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs g) {
       if ((g.vt_T & 7) == 0 && m + 8 <= g.M) {
         char* cp = (char*)g.C + (rowbase + tok) * sizeof(T);
         if constexpr (sizeof(T) == 2) {
-          st16(cp, pack16<T>(v));
+          st16(cp, pack_out8(v, g.out_f16));
         } else {
           st16(cp, pack16<T>(v));
           st16(cp + 16, pack16<T>(v + 4));
@@ -232,7 +232,9 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs g) {
       } else {
         for (int e = 0; e < 8 && m + e < g.M; ++e) {
           const int me = m + e, be = me / g.vt_T, te = me - be * g.vt_T;
-          ((T*)g.C)[((size_t)(grp * g.vt_B + be) * 256 + hd) * g.vt_T + te] = from_f32<T>(v[e]);
+          const size_t idx = ((size_t)(grp * g.vt_B + be) * 256 + hd) * g.vt_T + te;
+          if constexpr (sizeof(T) == 2) store_out1(g.C, idx, v[e], g.out_f16);
+          else ((T*)g.C)[idx] = from_f32<T>(v[e]);
         }
       }
     }
@@ -277,13 +279,16 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs g) {
       T* cp = (T*)g.C + (size_t)m * g.ldc + n;
       if (full) {
         if constexpr (sizeof(T) == 2) {
-          st16(cp, pack16<T>(v));
+          st16(cp, pack_out8(v, g.out_f16));
         } else {
           st16(cp, pack16<T>(v));
           st16(cp + 4, pack16<T>(v + 4));
         }
       } else {
-        for (int e = 0; e < 8 && n + e < g.N; ++e) cp[e] = from_f32<T>(v[e]);
+        for (int e = 0; e < 8 && n + e < g.N; ++e) {
+          if constexpr (sizeof(T) == 2) store_out1(cp, e, v[e], g.out_f16);
+          else cp[e] = from_f32<T>(v[e]);
+        }
       }
     }
   }

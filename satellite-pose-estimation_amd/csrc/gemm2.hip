@@ -395,8 +395,8 @@ __global__ __launch_bounds__(NT, 1) void gemm2_kernel(GemmArgs g) {
           else for (int r = 0; r < 4 && n + r < g.N; ++r) cp[r] = v[r];
         } else {
           bf16* cp = (bf16*)g.C + (size_t)m * g.ldc + n;
-          if (full) st8(cp, u32x2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])});
-          else for (int r = 0; r < 4 && n + r < g.N; ++r) cp[r] = from_f32<bf16>(v[r]);
+          if (full) st8(cp, u32x2{pack_out2(v[0], v[1], g.out_f16), pack_out2(v[2], v[3], g.out_f16)});
+          else for (int r = 0; r < 4 && n + r < g.N; ++r) store_out1(cp, r, v[r], g.out_f16);
         }
       }
     }
@@ -434,11 +434,11 @@ __global__ __launch_bounds__(NT, 1) void gemm2_kernel(GemmArgs g) {
         const int grp = n >> 8, hd = n & 255;
         const int b = m / g.vt_T, tok = m - b * g.vt_T;
         if ((g.vt_T & 7) == 0 && m + 8 <= g.M) {
-          st16((bf16*)g.C + ((size_t)(grp * g.vt_B + b) * 256 + hd) * g.vt_T + tok, pack16<bf16>(v));
+          st16((bf16*)g.C + ((size_t)(grp * g.vt_B + b) * 256 + hd) * g.vt_T + tok, pack_out8(v, g.out_f16));
         } else {
           for (int e = 0; e < 8 && m + e < g.M; ++e) {
             const int me = m + e, be = me / g.vt_T, te = me - be * g.vt_T;
-            ((bf16*)g.C)[((size_t)(grp * g.vt_B + be) * 256 + hd) * g.vt_T + te] = from_f32<bf16>(v[e]);
+            store_out1(g.C, ((size_t)(grp * g.vt_B + be) * 256 + hd) * g.vt_T + te, v[e], g.out_f16);
           }
         }
       }
@@ -498,9 +498,9 @@ __global__ __launch_bounds__(NT, 1) void gemm2_kernel(GemmArgs g) {
           } else {
             bf16* cp = (bf16*)g.C + (size_t)m * g.ldc + n;
             if (full) {
-              st16(cp, pack16<bf16>(v));
+              st16(cp, pack_out8(v, g.out_f16));
             } else {
-              for (int e = 0; e < 8 && n + e < g.N; ++e) cp[e] = from_f32<bf16>(v[e]);
+              for (int e = 0; e < 8 && n + e < g.N; ++e) store_out1(cp, e, v[e], g.out_f16);
             }
           }
         }
@@ -629,7 +629,7 @@ __global__ __launch_bounds__(SM_NT) void gemm_small_kernel(GemmArgs g) {
         const int grp = n >> 8, hd = n & 255;
         for (int r = 0; r < 4 && m + r < g.M; ++r) {
           const int me = m + r, be = me / g.vt_T, te = me - be * g.vt_T;
-          ((bf16*)g.C)[((size_t)(grp * g.vt_B + be) * 256 + hd) * g.vt_T + te] = from_f32<bf16>(acc[i][j][r] + bv);
+          store_out1(g.C, ((size_t)(grp * g.vt_B + be) * 256 + hd) * g.vt_T + te, acc[i][j][r] + bv, g.out_f16);
         }
       } else {
         // C^T fragment: 4 consecutive columns n = .. + 4fg + r of row m
@@ -658,8 +658,8 @@ __global__ __launch_bounds__(SM_NT) void gemm_small_kernel(GemmArgs g) {
           else for (int r = 0; r < 4 && n + r < g.N; ++r) cp[r] = v[r];
         } else {
           bf16* cp = (bf16*)g.C + (size_t)m * g.ldc + n;
-          if (full) st8(cp, u32x2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])});
-          else for (int r = 0; r < 4 && n + r < g.N; ++r) cp[r] = from_f32<bf16>(v[r]);
+          if (full) st8(cp, u32x2{pack_out2(v[0], v[1], g.out_f16), pack_out2(v[2], v[3], g.out_f16)});
+          else for (int r = 0; r < 4 && n + r < g.N; ++r) store_out1(cp, r, v[r], g.out_f16);
         }
       }
     }

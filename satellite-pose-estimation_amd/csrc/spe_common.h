@@ -59,6 +59,30 @@ template <> SPE_DEV u32x4 pack16<bf16>(const float* f) {
   return u32x4{pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3]), pack_bf16x2(f[4], f[5]), pack_bf16x2(f[6], f[7])};
 }
 
+// fp16 storage (encoder attention operands in the fp16-attention mode, BASELINE config 5)
+typedef _Float16 f16;
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+template <> SPE_DEV f16 from_f32<f16>(float x) { return (f16)x; }
+SPE_DEV uint32_t pack_f16x2(float lo, float hi) {                 // RNE
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{lo, hi}, f16x2));
+}
+template <> SPE_DEV void unpack16<f16>(u32x4 v, float* f) {
+  const f16x8 h = __builtin_bit_cast(f16x8, v);
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f[i] = (float)h[i];
+}
+template <> SPE_DEV u32x4 pack16<f16>(const float* f) {
+  return u32x4{pack_f16x2(f[0], f[1]), pack_f16x2(f[2], f[3]), pack_f16x2(f[4], f[5]), pack_f16x2(f[6], f[7])};
+}
+// 16-bit GEMM outputs: bf16 unless the launch asked for fp16 (GemmArgs::out_f16)
+SPE_DEV uint32_t pack_out2(float lo, float hi, bool f16o) { return f16o ? pack_f16x2(lo, hi) : pack_bf16x2(lo, hi); }
+SPE_DEV u32x4 pack_out8(const float* f, bool f16o) { return f16o ? pack16<f16>(f) : pack16<bf16>(f); }
+SPE_DEV void store_out1(void* base, size_t i, float v, bool f16o) {
+  if (f16o) reinterpret_cast<f16*>(base)[i] = (f16)v;
+  else reinterpret_cast<bf16*>(base)[i] = (bf16)v;
+}
+
 SPE_DEV float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

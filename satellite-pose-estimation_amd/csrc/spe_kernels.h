@@ -4,7 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-enum { SPE_DTYPE_BF16 = 0, SPE_DTYPE_F32 = 1 };
+enum { SPE_DTYPE_BF16 = 0, SPE_DTYPE_F32 = 1, SPE_DTYPE_F16 = 2 };   // F16: attention operands only
 enum { GEMM_LINEAR = 0, GEMM_LINEAR_ADD = 1, GEMM_CONV = 2 };
 
 struct GemmArgs {
@@ -18,6 +18,7 @@ struct GemmArgs {
   int relu;
   void* C; int ldc;                // output [m*ldc + n]
   int out_f32;                     // store fp32 instead of T
+  int out_f16;                     // bf16 models: store fp16 instead of bf16 (fp16 attention operands)
   int vt_T, vt_B;                  // >0: head-transposed store (see gemm.hip)
   int r_period;                    // >0: residual row = m % r_period (row-periodic add, e.g. pos . W^T)
   const float* ln_g; const float* ln_b;   // optional fused post-norm LayerNorm over N == 256 (bf16, large M)

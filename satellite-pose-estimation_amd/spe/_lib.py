@@ -20,7 +20,7 @@ I64 = ctypes.c_int64
 F = ctypes.c_float
 D = ctypes.c_double
 
-SPE_DTYPE_BF16, SPE_DTYPE_F32 = 0, 1
+SPE_DTYPE_BF16, SPE_DTYPE_F32, SPE_DTYPE_F16 = 0, 1, 2
 SPE_PNP_EPNP, SPE_PNP_RANSAC_P3P_LM, SPE_PNP_EPNP_RANSAC_SIGMA, SPE_PNP_EPNP_LM = 0, 1, 2, 3
 SPE_PNP_OK, SPE_PNP_NO_FG, SPE_PNP_CV_ERROR, SPE_PNP_RANSAC_FALLBACK, SPE_PNP_UNPINNED = 0, 1, 2, 3, 4
 
@@ -34,7 +34,8 @@ EXPORTS = ["spe_abi_version", "spe_last_error", "spe_model_create", "spe_model_d
 
 class ModelConfig(ctypes.Structure):
     _fields_ = [("input_size", I), ("num_queries", I), ("enc_layers", I), ("dec_layers", I), ("hidden_dim", I),
-                ("nheads", I), ("dim_feedforward", I), ("sigma_head", I), ("dtype", I)]
+                ("nheads", I), ("dim_feedforward", I), ("sigma_head", I), ("dtype", I),
+                ("attn_dtype", I)]
 
 
 class ForwardOutputs(ctypes.Structure):
@@ -77,12 +78,12 @@ def lib():
     L.spe_model_profile_end.argtypes = [P]
     L.spe_model_profile_get.argtypes = [P, I, ctypes.c_char_p, I, ctypes.POINTER(D), ctypes.POINTER(D),
                                         ctypes.POINTER(D)]
-    L.spe_debug_gemm.argtypes = [P, I, I, P, I, P, I, I] + [I] * 7 + [P, I, I, I, I, P, P, I, I, P, I, I, I, I, I, P, P]
+    L.spe_debug_gemm.argtypes = [P, I, I, P, I, P, I, I] + [I] * 7 + [P, I, I, I, I, P, P, I, I, P, I, I, I, I, I, P, P, I]
     L.spe_debug_attention.argtypes = [P, I, P, I, P, I, P, P, I, I, I, I, I, F]
     L.spe_debug_layernorm.argtypes = [P, I, P, P, P, P, P, I, I]
     L.spe_debug_ffn.argtypes = [P, P, I, P, I, P, P, I, P, P, P, P, I, I, I, I, P, I]
     L.spe_debug_xattn.argtypes = [P, P, I, P, I, P, I, P, I, P, P, P, I, I, I, I, I, P]
-    if L.spe_abi_version() != 1:
+    if L.spe_abi_version() != 2:
         raise ImportError("libspe.so ABI version mismatch")
     _lib = L
     return L

@@ -26,14 +26,19 @@ class DETR(nn.Module):
     """Keypoint-set predictor (REV/models/detr_speed.py:32-100), HIP implementation.
 
     dtype "bf16": bf16 storage / MFMA with fp32 accumulation, softmax, LayerNorm and heads
-    (throughput path).  dtype "fp32": exact-f32 MFMA everywhere (parity path)."""
+    (throughput path).  dtype "fp32": exact-f32 MFMA everywhere (parity path).
+    attn_dtype "fp16" (bf16 models): the encoder self-attention's q/k/V operands are stored
+    and multiplied in fp16 (BASELINE config 5, "fp16 MFMA attention")."""
 
-    def __init__(self, cfg: SpeConfig, dtype: str = "bf16", aux_loss: bool = False):
+    def __init__(self, cfg: SpeConfig, dtype: str = "bf16", aux_loss: bool = False, attn_dtype: str = None):
         super().__init__()
         self.cfg = cfg
         self.num_queries = cfg.num_queries
         self.aux_loss = aux_loss
         self.dtype = dtype
+        if attn_dtype not in (None, dtype, "fp16") or (attn_dtype == "fp16" and dtype != "bf16"):
+            raise ValueError(f"attn_dtype {attn_dtype!r}: None, the model dtype, or 'fp16' for bf16 models")
+        self.attn_dtype = attn_dtype or dtype
         self._pending = {}
         self._handle = None
         self._ws = None
@@ -41,7 +46,8 @@ class DETR(nn.Module):
         L = _lib.lib()
         c = _lib.ModelConfig(cfg.input_size, cfg.num_queries, cfg.enc_layers, cfg.dec_layers, cfg.hidden_dim,
                              cfg.nheads, cfg.dim_feedforward, int(cfg.sigma_head),
-                             _lib.SPE_DTYPE_BF16 if dtype == "bf16" else _lib.SPE_DTYPE_F32)
+                             _lib.SPE_DTYPE_BF16 if dtype == "bf16" else _lib.SPE_DTYPE_F32,
+                             _lib.SPE_DTYPE_F16 if self.attn_dtype == "fp16" else 0)
         h = ctypes.c_void_p()
         _lib.check(L.spe_model_create(ctypes.byref(c), ctypes.byref(h)), "spe_model_create")
         self._h = h
@@ -166,5 +172,6 @@ def build_model(args, dtype: str = None):
     inference hot path and is returned as None (out of scope)."""
     cfg = SpeConfig.from_args(args)
     dtype = dtype or getattr(args, "dtype", "bf16")
-    model = DETR(cfg, dtype=dtype, aux_loss=bool(getattr(args, "aux_loss", False)))
+    model = DETR(cfg, dtype=dtype, aux_loss=bool(getattr(args, "aux_loss", False)),
+                 attn_dtype=getattr(args, "attn_dtype", None))
     return model, None, {"points": PostProcess()}

@@ -8,4 +8,4 @@ timeout -k 10 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun
   python3 bench.py --steps ${BENCH_STEPS:-5} --warmup 2 --no-cpu-baseline > gpurun_out/prof_$TAG/bench_under_rocprof.log 2>&1 \
   || { echo "rocprof run failed"; tail -30 gpurun_out/prof_$TAG/bench_under_rocprof.log; exit 5; }
 find gpurun_out/prof_$TAG -name "*stats*" | head
-tail -1 gpurun_out/prof_$TAG/bench_under_rocprof.log | cut -c1-400
+grep "^{\"metric\"" gpurun_out/prof_$TAG/bench_under_rocprof.log | cut -c1-400

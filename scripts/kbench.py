@@ -121,7 +121,7 @@ def main():
             rp = 0 if rr <= 0 else rr
             fn = lambda: L.spe_debug_gemm(None, 0, mode, p(A), K if not conv else 0, None, 0, 1, H, W, Cin, KH, KW,
                                           st, pd, p(Wt), ldb, M, N, K, p(bias), p(R) if R is not None else None,
-                                          N, 1, p(C), N, 0, 0, 0, rp, None, None)
+                                          N, 1, p(C), N, 0, 0, 0, rp, None, None, 0)
             ms = timeit(fn, a.iters)
             abytes = (B * H * W * Cin if conv else M * K) * 2
             byts = abytes + N * ldb * 2 + M * N * 2 + (0 if R is None else R.numel() * 2)

@@ -17,7 +17,8 @@ from spe import _lib
 
 pytestmark = pytest.mark.gpu
 
-DT = {"bf16": (_lib.SPE_DTYPE_BF16, torch.bfloat16, 1e-2), "fp32": (_lib.SPE_DTYPE_F32, torch.float32, 1e-4)}
+DT = {"bf16": (_lib.SPE_DTYPE_BF16, torch.bfloat16, 1e-2), "fp32": (_lib.SPE_DTYPE_F32, torch.float32, 1e-4),
+      "fp16": (_lib.SPE_DTYPE_F16, torch.float16, 2e-3)}
 
 
 def _p(t):
@@ -31,12 +32,12 @@ def _close(got, ref, tol):
 
 
 def _gemm(dtype, mode, A, W, M, N, K, lda, ldb, C, ldc, bias=None, R=None, ldr=0, relu=0, P=None, ldp=0, prow=1,
-          conv=(0, 0, 0, 1, 1, 1, 0), out_f32=0, vt=(0, 0), r_period=0, ln=(None, None)):
+          conv=(0, 0, 0, 1, 1, 1, 0), out_f32=0, vt=(0, 0), r_period=0, ln=(None, None), out_f16=0):
     L = _lib.lib()
     H, Wd, Cin, KH, KW, stride, pad = conv
     rc = L.spe_debug_gemm(None, DT[dtype][0], mode, _p(A), lda, _p(P), ldp, prow, H, Wd, Cin, KH, KW, stride, pad,
                           _p(W), ldb, M, N, K, _p(bias), _p(R), ldr, relu, _p(C), ldc, out_f32, vt[0], vt[1], r_period,
-                          _p(ln[0]), _p(ln[1]))
+                          _p(ln[0]), _p(ln[1]), out_f16)
     assert rc == 0, L.spe_last_error()
     torch.cuda.synchronize()
 
@@ -174,7 +175,7 @@ def test_gemm_fused_layernorm(gpu_device, inplace):
     L = _lib.lib()
     small = torch.zeros(100, N, dtype=dt, device=gpu_device)
     rc = L.spe_debug_gemm(None, 0, 0, _p(A), K, None, 0, 1, 0, 0, 0, 1, 1, 1, 0, _p(_padded_weight(Wt, 256, dt)), 256,
-                          100, N, K, _p(bias), None, N, 0, _p(small), N, 0, 0, 0, 0, _p(gam), _p(bet))
+                          100, N, K, _p(bias), None, N, 0, _p(small), N, 0, 0, 0, 0, _p(gam), _p(bet), 0)
     assert rc != 0
 
 
@@ -230,12 +231,37 @@ def test_gemm_large_tile_head_transposed(gpu_device):
     _close(C, ref, tol)
 
 
+@pytest.mark.parametrize("M,N,vt", [(256 * 256 + 40, 512, False), (300, 512, False), (5000, 256, False),
+                                     (64 * 676, 256, True), (2 * 256, 256, True), (20 * 256, 256, True)])
+def test_gemm_fp16_output(gpu_device, M, N, vt):
+    """out_f16: bf16 GEMMs (large-tile, few-row and 128x128 kernels) storing fp16, row-major or
+    head-transposed V^T -- the operands of the fp16 encoder attention (BASELINE config 5)."""
+    g = torch.Generator(device="cpu").manual_seed(M + N)
+    K = 256
+    A = torch.randn(M, K, generator=g).to(gpu_device, torch.bfloat16)
+    Wt = (torch.randn(N, K, generator=g) / 16).to(gpu_device, torch.bfloat16)
+    bias = torch.randn(N, generator=g).to(gpu_device)
+    ref = A.float() @ Wt.float().t() + bias
+    if vt:
+        T = 676 if M % 676 == 0 else 256
+        B = M // T
+        C = torch.zeros(B * N * T, dtype=torch.float16, device=gpu_device)
+        _gemm("bf16", 0, A, _padded_weight(Wt, 256, torch.bfloat16), M, N, K, K, 256, C, 8, bias=bias, vt=(T, B),
+              out_f16=1)
+        ref = ref.view(B, T, N // 256, 256).permute(2, 0, 3, 1).reshape(-1)
+    else:
+        C = torch.zeros(M, N, dtype=torch.float16, device=gpu_device)
+        _gemm("bf16", 0, A, _padded_weight(Wt, 256, torch.bfloat16), M, N, K, K, 256, C, N, bias=bias, out_f16=1)
+    assert torch.isfinite(C.float()).all()
+    _close(C, ref, 2e-3)
+
+
 def _attn_ref(q, k, v, scale):
     a = torch.softmax((q.float() @ k.float().transpose(-1, -2)) * scale, -1)
     return a @ v.float()
 
 
-@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+@pytest.mark.parametrize("dtype", ["bf16", "fp16", "fp32"])
 @pytest.mark.parametrize("B,H,Tq,Tk", [(2, 8, 200, 200), (3, 8, 11, 330), (1, 8, 11, 11), (1, 2, 300, 64)])
 def test_attention(gpu_device, dtype, B, H, Tq, Tk):
     code, dt, tol = DT[dtype]
@@ -245,17 +271,18 @@ def test_attention(gpu_device, dtype, B, H, Tq, Tk):
     K = (torch.randn(B * Tk, ld, generator=g) * 2).to(gpu_device, dt)
     V = torch.randn(B, H, Tk, 32, generator=g).to(gpu_device, dt)
     VT = V.transpose(-1, -2).contiguous()
-    O = torch.zeros(B * Tq, H * 32, dtype=dt, device=gpu_device)
+    # 16-bit operand kernels (bf16 / fp16) write bf16: the out-projection GEMM reads bf16
+    O = torch.zeros(B * Tq, H * 32, dtype=torch.float32 if dtype == "fp32" else torch.bfloat16, device=gpu_device)
     scale = 32 ** -0.5
     rc = _lib.lib().spe_debug_attention(None, code, _p(Q), ld, _p(K), ld, _p(VT), _p(O), H * 32, B, H, Tq, Tk, scale)
     assert rc == 0
     torch.cuda.synchronize()
     q = Q[:, : H * 32].view(B, Tq, H, 32).transpose(1, 2)
     k = K[:, : H * 32].view(B, Tk, H, 32).transpose(1, 2)
-    if dtype == "bf16":
+    if dtype != "fp32":                                # the kernel rounds the prescaled q to 16 bits
         q = (q.float() * scale * 1.4426950408889634).to(dt).float() / (scale * 1.4426950408889634)
     ref = _attn_ref(q, k, V, scale).transpose(1, 2).reshape(B * Tq, H * 32)
-    _close(O, ref, 2e-2 if dtype == "bf16" else 1e-5)
+    _close(O, ref, {"bf16": 2e-2, "fp16": 1e-2, "fp32": 1e-5}[dtype])
 
 
 def test_attention_large_score_range(gpu_device):

@@ -4,7 +4,8 @@ and the CPU oracles, on seeded inputs.
 Tolerances (written here on purpose):
   fp32 parity mode   pred_points |d| <= 1e-4 (crop-normalised; BASELINE.json keypoint
                      tolerance), pred_logits |d| <= 2e-3 abs, PostProcess px <= 0.05 px
-  bf16 throughput    pred_points |d| <= 2e-2, logits |d| <= 0.25 (bf16 storage, 8-bit mantissa)
+  bf16 throughput    pred_points |d| <= 2e-2, logits |d| <= 0.25 (bf16 storage, 8-bit mantissa;
+                     same bound with fp16 encoder-attention operands)
   solver             status / n_corr / corr_label / inlier masks bit-exact vs oracle/pnp_ref.c,
                      pose |dq| <= 1e-5, |dt|/|t| <= 1e-6 (both fp64, rounding only)
 """
@@ -25,11 +26,11 @@ pytestmark = pytest.mark.gpu
 _models = {}
 
 
-def _model(cfg, dtype, wseed):
+def _model(cfg, dtype, wseed, attn_dtype=None):
     from spe.models import DETR
-    key = (cfg, dtype, wseed)
+    key = (cfg, dtype, wseed, attn_dtype)
     if key not in _models:
-        m = DETR(cfg, dtype=dtype)
+        m = DETR(cfg, dtype=dtype, attn_dtype=attn_dtype)
         m.load_state_dict(random_weights(cfg, wseed))
         _models[key] = m
     return _models[key]
@@ -58,11 +59,13 @@ def test_forward_fp32_matches_reference(gpu_device, tag):
     assert np.abs(o["probs"].cpu().numpy() - g["pp_probs"]).max() <= 1e-3
 
 
-@pytest.mark.parametrize("tag", ["s128_q11_l2", "s416_q11_l6"])
-def test_forward_bf16_close_to_reference(gpu_device, tag):
+@pytest.mark.parametrize("attn_dtype", [None, "fp16"])
+@pytest.mark.parametrize("tag", ["s128_q11_l2", "s224_q30_l4", "s416_q11_l6"])
+def test_forward_bf16_close_to_reference(gpu_device, tag, attn_dtype):
+    """bf16 throughput mode, with bf16 or fp16 (config 5) encoder-attention operands."""
     g, cfg = _golden(tag)
     b = synthetic_batch(cfg, int(g["batch"]), int(g["image_seed"]))
-    m = _model(cfg, "bf16", int(g["weight_seed"]))
+    m = _model(cfg, "bf16", int(g["weight_seed"]), attn_dtype)
     o = m(torch.from_numpy(b["images"]).to(gpu_device))
     torch.cuda.synchronize()
     assert np.isfinite(o["pred_points"].cpu().numpy()).all()
