@@ -66,6 +66,10 @@ def parse():
                         "correspondences like a trained model (spe.synthetic.bench_weights)")
     p.add_argument("--no-overlap", action="store_true",
                    help="run the solver on the forward's stream (default: solver of batch i overlaps the forward of i+1)")
+    p.add_argument("--raw-frames", action="store_true",
+                   help="start every step from 1920x1200 8-bit frames + detector boxes in HBM: the "
+                        "validation transform (crop, cv2-cubic resize, normalise; spe.datasets) runs "
+                        "on the device inside the timed step")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--launch-table", default=None,
@@ -171,10 +175,18 @@ def main():
     model = DETR(cfg, dtype=args.dtype, attn_dtype=args.attn_dtype)
     model.load_state_dict(bench_weights(cfg, 0, hs_fn) if args.weights == "label-diverse" else random_weights(cfg, 0))
     solver = build_solver(argparse.Namespace(solver=args.solver, repro=20))
-    pipe = PosePipeline(model, solver, B, device=dev, overlap=not args.no_overlap)
-    data = synthetic_batch(cfg, B, seed=1000 + rank)
-    pipe.load(torch.from_numpy(data["images"]).to(dev), torch.from_numpy(data["clip_bbox"]).float().to(dev),
-              torch.from_numpy(data["quat"]).to(dev), torch.from_numpy(data["tvec"]).to(dev))
+    if args.raw_frames:
+        from spe.synthetic import synthetic_frames
+        data = synthetic_frames(B, seed=1000 + rank)
+        H, W = data["frames"].shape[1:3]
+        pipe = PosePipeline(model, solver, B, device=dev, overlap=not args.no_overlap, raw_frames=(H, W, 1))
+        pipe.load_frames(torch.from_numpy(data["frames"]).to(dev), torch.from_numpy(data["bbox_xxyy"]).to(dev),
+                         torch.from_numpy(data["quat"]).to(dev), torch.from_numpy(data["tvec"]).to(dev))
+    else:
+        pipe = PosePipeline(model, solver, B, device=dev, overlap=not args.no_overlap)
+        data = synthetic_batch(cfg, B, seed=1000 + rank)
+        pipe.load(torch.from_numpy(data["images"]).to(dev), torch.from_numpy(data["clip_bbox"]).float().to(dev),
+                  torch.from_numpy(data["quat"]).to(dev), torch.from_numpy(data["tvec"]).to(dev))
     torch.cuda.synchronize()
 
     def step():
@@ -267,8 +279,8 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.dtype,
-        "data": f"synthetic (seeded SPEED-shaped crops; {args.weights} random-init weights, "
-                "no checkpoint exists in the reference)",
+        "data": f"synthetic (seeded SPEED-shaped {'1920x1200 8-bit frames + detector boxes, on-device val transform' if args.raw_frames else 'crops'}; "
+                f"{args.weights} random-init weights, no checkpoint exists in the reference)",
         "config": {"workload": CONFIG_NAME[args.config].format(L=args.layers, Q=args.queries, S=args.size,
                                                                 solver=args.solver, A=args.attn_dtype),
                    "global_batch": B * world, "per_gpu_batch": B, "input_size": args.size,

@@ -98,6 +98,16 @@ int64_t spe_model_workspace_bytes(const spe_model* m, int batch);
 int spe_forward(spe_model* m, void* stream, const float* images, int batch, void* workspace, int64_t workspace_bytes,
                 const spe_forward_outputs* out);
 
+/* Validation input pipeline on the device (SpeedTrain.__getitem__ with train=False,
+ * REV/datasets/speed.py:209-233): generate_clip_bbox_val (:246-258), Pillow crop,
+ * A.Resize(S, S, cv2.INTER_CUBIC) (make_transforms(train=False), :295-299), F.to_tensor and
+ * Normalize (:25-41).  frames: device uint8 [B,H,W] (channels = 1: grayscale, replicated to RGB
+ * like Image.convert('RGB')) or [B,H,W,3]; bbox_xxyy: device fp64 [B,4] detector boxes;
+ * images: fp32 [B,3,S,S] (spe_forward's input); clip_bbox: fp32 [B,4] (PostProcess's box);
+ * status (nullable): [B] 0 ok, 1 empty crop (the reference raises; zeros written). */
+int spe_preprocess(void* stream, const uint8_t* frames, int batch, int height, int width, int channels,
+                   const double* bbox_xxyy, int size, float* images, float* clip_bbox, int32_t* status);
+
 /* PostProcess alone (REV/models/detr_speed.py:266-293). */
 int spe_postprocess(void* stream, const float* logits, const float* points, const float* clip_bbox, int batch,
                     int num_queries, float* probs, float* points_px);

@@ -397,6 +397,16 @@ int spe_forward(spe_model* m, void* stream, const float* images, int B, void* wo
   return 0;
 }
 
+int spe_preprocess(void* stream, const uint8_t* frames, int batch, int height, int width, int channels,
+                   const double* bbox_xxyy, int size, float* images, float* clip_bbox, int32_t* status) {
+  if (!frames || !bbox_xxyy || !images || !clip_bbox || batch < 0 || height <= 0 || width <= 0 || size <= 0 ||
+      (channels != 1 && channels != 3))
+    return fail(SPE_E_ARG, "bad argument");
+  CK(spe_launch_preprocess(frames, batch, height, width, channels, bbox_xxyy, size, images, clip_bbox, status,
+                           (hipStream_t)stream));
+  return 0;
+}
+
 int spe_postprocess(void* stream, const float* logits, const float* points, const float* clip_bbox, int B, int Q,
                     float* probs, float* points_px) {
   if (!logits || !points || !clip_bbox || !probs || !points_px || B < 0 || Q <= 0) return fail(SPE_E_ARG, "bad argument");

@@ -91,6 +91,8 @@ struct FfnArgs {
 int spe_launch_ffn_ln(const FfnArgs& a, hipStream_t s);
 int spe_ffn_splits(int M, int F);  // split count spe_launch_ffn_ln would use for M rows (1 = none)
 
+int spe_launch_preprocess(const uint8_t* frames, int B, int H, int W, int C, const double* bbox, int S,
+                          float* images, float* clip_bbox, int32_t* status, hipStream_t s);
 int spe_launch_pack_input(const float* img, void* out, int B, int S, int dtype, hipStream_t s);
 int spe_launch_maxpool3s2(const void* in, void* out, int B, int H, int W, int C, int Ho, int Wo,
                           int dtype, hipStream_t s);

@@ -1,6 +1,7 @@
 """Whole-batch device pipeline of the evaluate() hot loop (REV/engine.py:91-123 without the
-logging-only criterion): images -> backbone/transformer/heads + fused PostProcess -> batched
-PnP -> SPEED scores, all on one HIP stream with no host round trip.  Optionally captured
+logging-only criterion): [raw frames -> validation transform (spe.datasets, optional)] ->
+images -> backbone/transformer/heads + fused PostProcess -> batched PnP -> SPEED scores, all
+on the device with no host round trip.  Optionally captured
 into a HIP graph (torch.cuda.CUDAGraph drives hipStreamBeginCapture on ROCm): spe_forward,
 spe_pnp_batch and spe_speed_score never allocate or synchronise.
 """
@@ -15,7 +16,7 @@ from .speed_eval import device_speed_score
 
 class PosePipeline:
     def __init__(self, model: DETR, solver: PoseSolver, batch: int, device="cuda", use_graph: bool = False,
-                 self_assess: bool = True, overlap: bool = False):
+                 self_assess: bool = True, overlap: bool = False, raw_frames=None):
         self.model, self.solver, self.B = model, solver, batch
         self.self_assess = self_assess
         # overlap: the solver / score / self-assessment of batch i run on a second HIP stream
@@ -34,6 +35,17 @@ class PosePipeline:
         self.q_gt[:, 0] = 1
         self.t_gt[:, 2] = 10
         model.workspace(batch, dev)
+        # raw_frames = (H, W, C): each run() starts from uint8 frames + detector boxes resident in
+        # HBM (load_frames) and runs the validation transform on the device first
+        self.frames = self.bbox = self.transform = None
+        if raw_frames is not None:
+            from .datasets import SpeedValTransform
+            H, W, C = raw_frames
+            self.frames = torch.zeros((batch, H, W) + ((C,) if C == 3 else ()), dtype=torch.uint8, device=dev)
+            self.bbox = torch.zeros(batch, 4, dtype=torch.float64, device=dev)
+            self.transform = SpeedValTransform(S)
+            self.pp_out = {"images": self.images, "clip_bbox": self.clip_bbox,
+                           "status": torch.zeros(batch, dtype=torch.int32, device=dev)}
         self.use_graph = use_graph
         self.graph = None
         self.out = None
@@ -49,6 +61,8 @@ class PosePipeline:
         return out
 
     def _body(self):
+        if self.transform is not None:
+            self.transform(self.frames, self.bbox, out=self.pp_out)
         fo = self.model(self.images, clip_bbox=self.clip_bbox)
         if not self.overlap:
             return self._solve(fo)
@@ -70,6 +84,14 @@ class PosePipeline:
     def load(self, images, clip_bbox, q_gt=None, t_gt=None):
         self.images.copy_(images, non_blocking=True)
         self.clip_bbox.copy_(clip_bbox, non_blocking=True)
+        if q_gt is not None:
+            self.q_gt.copy_(q_gt, non_blocking=True)
+            self.t_gt.copy_(t_gt, non_blocking=True)
+
+    def load_frames(self, frames, bbox_xxyy, q_gt=None, t_gt=None):
+        """Raw-frame mode: uint8 frames [B,H,W(,3)] + detector boxes [B,4] (fp64)."""
+        self.frames.copy_(frames, non_blocking=True)
+        self.bbox.copy_(torch.as_tensor(bbox_xxyy, dtype=torch.float64), non_blocking=True)
         if q_gt is not None:
             self.q_gt.copy_(q_gt, non_blocking=True)
             self.t_gt.copy_(t_gt, non_blocking=True)

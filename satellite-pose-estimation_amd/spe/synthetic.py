@@ -6,6 +6,8 @@
 * `random_weights(cfg, seed)` - deterministic random-init weights in that key space
   (there is no trained checkpoint in the reference tree), with non-trivial FrozenBN
   statistics so the BN folding path is exercised.
+* `synthetic_frames(B, seed)` - full 1920x1200 8-bit frames + detector boxes, the input of
+  the on-device validation transform (spe.datasets.SpeedValTransform).
 * `synthetic_batch(cfg, B, seed)` - SPEED-shaped crops: GT pose, projected landmarks,
   val-rule clip box (REV/datasets/speed.py:246-260), rendered crop, ImageNet
   normalisation (REV/datasets/speed.py:25-41).
@@ -155,6 +157,33 @@ def synthetic_batch(cfg: SpeConfig, B: int, seed: int = 0, dtype=np.float32):
         for c in range(3):
             imgs[i, c] = (g - IMAGENET_MEAN[c]) / IMAGENET_STD[c]
     return {"images": imgs.astype(dtype), "quat": q, "tvec": t, "landmarks": lm, "clip_bbox": boxes}
+
+
+def synthetic_frames(B: int, seed: int = 0, height: int = Camera.nv, width: int = Camera.nu, channels: int = 1):
+    """B synthetic full SPEED frames (8-bit grayscale like the dataset, or replicated RGB):
+    background noise N(30, 10) plus a Gaussian blob (sigma 4 px) at every projected landmark of
+    a random pose.  Returns frames uint8 [B,H,W] (or [B,H,W,3]), bbox_xxyy [B,4] (landmark
+    box, the annotation field REV/datasets/speed.py:216 reads), quat, tvec, landmarks."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    W = world_points()
+    q, t = random_pose(rng, B)
+    lm = np.stack([project(W, q[i], t[i]) for i in range(B)])
+    frames = np.empty((B, height, width), np.uint8)
+    r = 16
+    oy, ox = np.meshgrid(np.arange(-r, r + 1), np.arange(-r, r + 1), indexing="ij")
+    for i in range(B):
+        g = rng.normal(30.0, 10.0, (height, width)).astype(np.float32)
+        for (u, v) in lm[i]:
+            cx, cy = int(np.floor(u)), int(np.floor(v))
+            ys, xs = cy + oy, cx + ox
+            ok = (ys >= 0) & (ys < height) & (xs >= 0) & (xs < width)
+            d2 = (xs - u) ** 2 + (ys - v) ** 2
+            g[ys[ok], xs[ok]] += (200.0 * np.exp(-d2 / (2 * 4.0 ** 2)))[ok]
+        frames[i] = np.clip(np.round(g), 0, 255).astype(np.uint8)
+    bbox = np.stack([[l[:, 0].min(), l[:, 1].min(), l[:, 0].max(), l[:, 1].max()] for l in lm])
+    if channels == 3:
+        frames = np.repeat(frames[..., None], 3, -1)
+    return {"frames": frames, "bbox_xxyy": bbox, "quat": q, "tvec": t, "landmarks": lm}
 
 
 # ---------------------------------------------------------------------------- bench weights

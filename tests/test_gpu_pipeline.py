@@ -123,3 +123,28 @@ def test_overlapped_pipeline_equals_serial(gpu_device, small_model, solver_name)
         np.testing.assert_array_equal(s0, s1)
         np.testing.assert_array_equal(t0, t1)
         np.testing.assert_array_equal(e0, e1)
+
+
+def test_pipeline_from_raw_frames(gpu_device, small_model):
+    """Raw-frame mode (device validation transform -> model -> solver) == the same pipeline fed
+    with the oracle's preprocessed images and clip boxes: identical poses and statuses."""
+    import preprocess_ref as pr
+    from spe.pipeline import PosePipeline
+    from spe.solver import build_solver
+    from spe.synthetic import synthetic_frames
+    cfg, w, m = small_model
+    B = 6
+    d = synthetic_frames(B, seed=31)
+    solver = build_solver(argparse.Namespace(solver="ransac_p3p_lm", repro=20))
+    raw = PosePipeline(m, solver, B, device=gpu_device, raw_frames=d["frames"].shape[1:3] + (1,))
+    raw.load_frames(torch.from_numpy(d["frames"]).to(gpu_device), torch.from_numpy(d["bbox_xxyy"]).to(gpu_device))
+    a = raw.run()
+    torch.cuda.synchronize()
+    ref = pr.preprocess(d["frames"], d["bbox_xxyy"], cfg.input_size)
+    assert np.array_equal(raw.images.cpu().numpy(), ref["images"])
+    pre = PosePipeline(m, solver, B, device=gpu_device)
+    pre.load(torch.from_numpy(ref["images"]).to(gpu_device), torch.from_numpy(ref["clip_bbox"]).float().to(gpu_device))
+    b = pre.run()
+    torch.cuda.synchronize()
+    for k in ("status", "quat", "tvec"):
+        assert torch.equal(a["poses"][k], b["poses"][k]), k
