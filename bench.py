@@ -66,6 +66,9 @@ def parse():
                         "correspondences like a trained model (spe.synthetic.bench_weights)")
     p.add_argument("--no-overlap", action="store_true",
                    help="run the solver on the forward's stream (default: solver of batch i overlaps the forward of i+1)")
+    p.add_argument("--no-overlap-decode", action="store_true",
+                   help="keep each batch's decoder + heads on the forward's stream (default: batch i's "
+                        "decoder runs on its own stream beside batch i+1's backbone/encoder, two workspaces)")
     p.add_argument("--raw-frames", action="store_true",
                    help="start every step from 1920x1200 8-bit frames + detector boxes in HBM: the "
                         "validation transform (crop, cv2-cubic resize, normalise; spe.datasets) runs "
@@ -179,11 +182,13 @@ def main():
         from spe.synthetic import synthetic_frames
         data = synthetic_frames(B, seed=1000 + rank)
         H, W = data["frames"].shape[1:3]
-        pipe = PosePipeline(model, solver, B, device=dev, overlap=not args.no_overlap, raw_frames=(H, W, 1))
+        pipe = PosePipeline(model, solver, B, device=dev, overlap=not args.no_overlap,
+                            overlap_decode=not (args.no_overlap_decode or args.no_overlap), raw_frames=(H, W, 1))
         pipe.load_frames(torch.from_numpy(data["frames"]).to(dev), torch.from_numpy(data["bbox_xxyy"]).to(dev),
                          torch.from_numpy(data["quat"]).to(dev), torch.from_numpy(data["tvec"]).to(dev))
     else:
-        pipe = PosePipeline(model, solver, B, device=dev, overlap=not args.no_overlap)
+        pipe = PosePipeline(model, solver, B, device=dev, overlap=not args.no_overlap,
+                            overlap_decode=not (args.no_overlap_decode or args.no_overlap))
         data = synthetic_batch(cfg, B, seed=1000 + rank)
         pipe.load(torch.from_numpy(data["images"]).to(dev), torch.from_numpy(data["clip_bbox"]).float().to(dev),
                   torch.from_numpy(data["quat"]).to(dev), torch.from_numpy(data["tvec"]).to(dev))

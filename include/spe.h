@@ -97,6 +97,14 @@ int64_t spe_model_workspace_bytes(const spe_model* m, int batch);
  * images: device [B,3,S,S] fp32, ImageNet-normalised (REV/datasets/speed.py:25-41). */
 int spe_forward(spe_model* m, void* stream, const float* images, int batch, void* workspace, int64_t workspace_bytes,
                 const spe_forward_outputs* out);
+/* The same pass split in two stages that may run on different streams: ENCODE = backbone +
+ * neck + input_proj + encoder (images -> memory, kept in `workspace`), DECODE = decoder + heads +
+ * PostProcess (memory in `workspace` -> out).  spe_forward == both stages in order.  A caller
+ * that overlaps batch i's DECODE with batch i+1's ENCODE gives each in-flight batch its own
+ * workspace. */
+enum { SPE_STAGE_ENCODE = 1, SPE_STAGE_DECODE = 2 };
+int spe_forward_stages(spe_model* m, void* stream, const float* images, int batch, void* workspace,
+                       int64_t workspace_bytes, const spe_forward_outputs* out, int stages);
 
 /* Validation input pipeline on the device (SpeedTrain.__getitem__ with train=False,
  * REV/datasets/speed.py:209-233): generate_clip_bbox_val (:246-258), Pillow crop,

@@ -136,8 +136,15 @@ extern "C" {
 
 int spe_forward(spe_model* m, void* stream, const float* images, int B, void* workspace, int64_t ws_bytes,
                 const spe_forward_outputs* out) {
-  if (!m || !images || !workspace || !out || !out->logits || !out->points || B <= 0)
-    return fail(SPE_E_ARG, "null argument");
+  return spe_forward_stages(m, stream, images, B, workspace, ws_bytes, out, SPE_STAGE_ENCODE | SPE_STAGE_DECODE);
+}
+
+int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, void* workspace, int64_t ws_bytes,
+                       const spe_forward_outputs* out, int stages) {
+  if (!m || !workspace || B <= 0 || (stages & ~(SPE_STAGE_ENCODE | SPE_STAGE_DECODE)) || !stages)
+    return fail(SPE_E_ARG, "bad argument");
+  if ((stages & SPE_STAGE_ENCODE) && !images) return fail(SPE_E_ARG, "null images");
+  if ((stages & SPE_STAGE_DECODE) && (!out || !out->logits || !out->points)) return fail(SPE_E_ARG, "null outputs");
   if (!m->finalized) return fail(SPE_E_STATE, "model not finalized");
   const Ws w = spe_plan(m, B);
   if ((int64_t)w.total > ws_bytes) return fail(SPE_E_WORKSPACE, "workspace too small");
@@ -148,6 +155,11 @@ int spe_forward(spe_model* m, void* stream, const float* images, int B, void* wo
   char* ws = (char*)workspace;
   auto P = [&](size_t off) { return (void*)(ws + off); };
 
+  const int F = S / 8, T = F * F;
+  const float scale = 1.0f / std::sqrt(32.0f);
+  const int Mt = B * T;
+  const bool xa = spe_use_xattn(m);
+  if (stages & SPE_STAGE_ENCODE) {
   // ---------------- backbone (REV/models/backbone.py:133-149)
   CK(run_other(m, "eltwise.pack", 0.0, (double)B * S * S * (12 + 8 * m->esz), s, [&] { return spe_launch_pack_input(images, P(w.x0), B, S, dt, s); }));
   {
@@ -197,7 +209,6 @@ int spe_forward(spe_model* m, void* stream, const float* images, int B, void* wo
     cur = outbuf;
   }
   const size_t xs16 = cur;                              // [B, S/16, S/16, 1024]
-  const int F = S / 8, T = F * F;
   {  // s8_latern 1x1 512->256 into channels [0,256) of the concat buffer
     GemmArgs g = linear_args(m->s8, P(w.xs8), 512, B * T, P(w.cat), 512);
     g.bias = nullptr;
@@ -219,8 +230,6 @@ int spe_forward(spe_model* m, void* stream, const float* images, int B, void* wo
   }
 
   // ---------------- encoder (REV/models/transformer.py:154-167)
-  const float scale = 1.0f / std::sqrt(32.0f);
-  const int Mt = B * T;
   // fp16 encoder attention operands (bf16 models, attn_dtype = SPE_DTYPE_F16_): the q/k and V^T
   // projections store fp16, the attention runs fp16 MFMAs; everything else stays bf16
   const int f16attn = c.attn_dtype == SPE_DTYPE_F16_ && dt == SPE_DTYPE_BF16;
@@ -279,7 +288,6 @@ int spe_forward(spe_model* m, void* stream, const float* images, int B, void* wo
   }
   // memory = src.  Unless the layers attend to memory + pos / memory directly (xattn path),
   // project the cross-attention K (memory + pos) and V^T (memory) for all decoder layers.
-  const bool xa = spe_use_xattn(m);
   if (!xa) {
   {
     // bf16 fused path: the last FFN wrote memory + pos (rounded once, like the reference's
@@ -296,7 +304,13 @@ int spe_forward(spe_model* m, void* stream, const float* images, int B, void* wo
   }
   }
 
+  }  // SPE_STAGE_ENCODE
+  if (!(stages & SPE_STAGE_DECODE)) return 0;
+
   // ---------------- decoder (REV/models/transformer.py:100-129,218-239)
+  // (reads only the memory -- src, srcpos, or ck / cvt -- that the encode stage left in the
+  // workspace, so the two stages may run on different streams, e.g. batch i's decoder beside
+  // batch i+1's backbone with two workspaces)
   const int Mq = B * Q;
   CK((int)hipMemsetAsync(P(w.tgt), 0, (size_t)Mq * d * m->esz, s));
   for (int l = 0; l < L; ++l) {

@@ -21,13 +21,14 @@ F = ctypes.c_float
 D = ctypes.c_double
 
 SPE_DTYPE_BF16, SPE_DTYPE_F32, SPE_DTYPE_F16 = 0, 1, 2
+SPE_STAGE_ENCODE, SPE_STAGE_DECODE = 1, 2
 SPE_PNP_EPNP, SPE_PNP_RANSAC_P3P_LM, SPE_PNP_EPNP_RANSAC_SIGMA, SPE_PNP_EPNP_LM = 0, 1, 2, 3
 SPE_PNP_OK, SPE_PNP_NO_FG, SPE_PNP_CV_ERROR, SPE_PNP_RANSAC_FALLBACK, SPE_PNP_UNPINNED = 0, 1, 2, 3, 4
 
 # every symbol include/spe.h declares (checked by tests/test_capi.py)
 EXPORTS = ["spe_abi_version", "spe_last_error", "spe_model_create", "spe_model_destroy", "spe_model_set_param",
            "spe_model_num_params", "spe_model_param_name", "spe_model_finalize", "spe_model_workspace_bytes",
-           "spe_forward", "spe_preprocess", "spe_postprocess", "spe_pnp_batch", "spe_self_assess", "spe_speed_score", "spe_model_profile_begin",
+           "spe_forward", "spe_forward_stages", "spe_preprocess", "spe_postprocess", "spe_pnp_batch", "spe_self_assess", "spe_speed_score", "spe_model_profile_begin",
            "spe_model_profile_end", "spe_model_profile_get", "spe_debug_gemm", "spe_debug_attention",
            "spe_debug_layernorm", "spe_debug_ffn", "spe_debug_xattn"]
 
@@ -70,6 +71,7 @@ def lib():
     L.spe_model_workspace_bytes.argtypes = [P, I]
     L.spe_model_workspace_bytes.restype = I64
     L.spe_forward.argtypes = [P, P, P, I, P, I64, ctypes.POINTER(ForwardOutputs)]
+    L.spe_forward_stages.argtypes = [P, P, P, I, P, I64, ctypes.POINTER(ForwardOutputs), I]
     L.spe_postprocess.argtypes = [P, P, P, P, I, I, P, P]
     L.spe_preprocess.argtypes = [P, P, I, I, I, I, P, I, P, P, P]
     L.spe_pnp_batch.argtypes = [P, P, P, P, I, I, I, P, P, I, F, I, D, P, P, P, P, P, P, P]

@@ -90,7 +90,44 @@ class DETR(nn.Module):
             self._ws_batch = B
         return self._ws
 
+    def new_workspace(self, B, device):
+        """A separate workspace for another in-flight batch (encode/decode overlap)."""
+        return torch.empty(int(_lib.lib().spe_model_workspace_bytes(self._h, B)), dtype=torch.uint8, device=device)
+
     # ---------------------------------------------------------------- forward
+    def _outputs(self, B, dev, clip_bbox, return_hs):
+        Q = self.cfg.num_queries
+        out = {"pred_logits": torch.empty(B, Q, 12, device=dev), "pred_points": torch.empty(B, Q, 2, device=dev)}
+        if self.cfg.sigma_head:
+            out["pred_sigmas"] = torch.empty(B, Q, 2, device=dev)
+            out["sigmas"] = torch.empty(B, Q, 2, device=dev)
+        if return_hs:
+            out["hs"] = torch.empty(B, Q, self.cfg.hidden_dim, device=dev)
+        if clip_bbox is not None:
+            out["probs"] = torch.empty(B, Q, 12, device=dev)
+            out["points_px"] = torch.empty(B, Q, 2, device=dev)
+        o = _lib.ForwardOutputs(_lib.ptr(out["pred_logits"]), _lib.ptr(out["pred_points"]), _lib.ptr(clip_bbox),
+                                _lib.ptr(out.get("probs")), _lib.ptr(out.get("points_px")),
+                                _lib.ptr(out.get("pred_sigmas")), _lib.ptr(out.get("sigmas")),
+                                _lib.ptr(out.get("hs")))
+        return out, o
+
+    def encode(self, images, ws, stream=None):
+        """Encode stage (backbone, neck, input_proj, encoder): images -> memory kept in `ws`."""
+        B = images.shape[0]
+        _lib.check(_lib.lib().spe_forward_stages(self._h, _lib.stream_ptr(stream), _lib.ptr(images), B, _lib.ptr(ws),
+                                                 ws.numel(), None, _lib.SPE_STAGE_ENCODE), "spe_forward_stages")
+
+    def decode(self, B, ws, clip_bbox=None, stream=None, return_hs=False):
+        """Decode stage (decoder, heads, fused PostProcess) of the memory an encode() left in `ws`."""
+        dev = ws.device
+        if clip_bbox is not None:
+            clip_bbox = clip_bbox.to(device=dev, dtype=torch.float32).contiguous()
+        out, o = self._outputs(B, dev, clip_bbox, return_hs)
+        _lib.check(_lib.lib().spe_forward_stages(self._h, _lib.stream_ptr(stream), None, B, _lib.ptr(ws), ws.numel(),
+                                                 ctypes.byref(o), _lib.SPE_STAGE_DECODE), "spe_forward_stages")
+        return out
+
     def forward(self, samples, clip_bbox=None, stream=None, return_hs=False):
         """REV/models/detr_speed.py:59-92.  Returns pred_logits [B,Q,12], pred_points [B,Q,2]
         (+ pred_sigmas as log-sigma when the sigma head is configured).  Passing `clip_bbox`
@@ -108,21 +145,9 @@ class DETR(nn.Module):
         if C != 3 or H != S or W != S:
             raise ValueError(f"expected [B,3,{S},{S}] input, got {tuple(images.shape)}")
         dev = images.device
-        Q = self.cfg.num_queries
-        out = {"pred_logits": torch.empty(B, Q, 12, device=dev), "pred_points": torch.empty(B, Q, 2, device=dev)}
-        if self.cfg.sigma_head:
-            out["pred_sigmas"] = torch.empty(B, Q, 2, device=dev)
-            out["sigmas"] = torch.empty(B, Q, 2, device=dev)
-        if return_hs:
-            out["hs"] = torch.empty(B, Q, self.cfg.hidden_dim, device=dev)
         if clip_bbox is not None:
             clip_bbox = clip_bbox.to(device=dev, dtype=torch.float32).contiguous()
-            out["probs"] = torch.empty(B, Q, 12, device=dev)
-            out["points_px"] = torch.empty(B, Q, 2, device=dev)
-        o = _lib.ForwardOutputs(_lib.ptr(out["pred_logits"]), _lib.ptr(out["pred_points"]), _lib.ptr(clip_bbox),
-                                _lib.ptr(out.get("probs")), _lib.ptr(out.get("points_px")),
-                                _lib.ptr(out.get("pred_sigmas")), _lib.ptr(out.get("sigmas")),
-                                _lib.ptr(out.get("hs")))
+        out, o = self._outputs(B, dev, clip_bbox, return_hs)
         ws = self.workspace(B, dev)
         _lib.check(_lib.lib().spe_forward(self._h, _lib.stream_ptr(stream), _lib.ptr(images), B, _lib.ptr(ws),
                                           ws.numel(), ctypes.byref(o)), "spe_forward")

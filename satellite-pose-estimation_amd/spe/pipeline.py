@@ -16,14 +16,19 @@ from .speed_eval import device_speed_score
 
 class PosePipeline:
     def __init__(self, model: DETR, solver: PoseSolver, batch: int, device="cuda", use_graph: bool = False,
-                 self_assess: bool = True, overlap: bool = False, raw_frames=None):
+                 self_assess: bool = True, overlap: bool = False, raw_frames=None, overlap_decode: bool = False):
         self.model, self.solver, self.B = model, solver, batch
         self.self_assess = self_assess
         # overlap: the solver / score / self-assessment of batch i run on a second HIP stream
         # while the forward of batch i+1 runs on the caller's stream (the solver occupies one
         # wave per image, far from filling the chip, and its latency is fp64-bound).  Results of
         # a run() are then complete only after wait(out) (or a device synchronize).
-        self.overlap = overlap and not use_graph
+        # overlap_decode (implies overlap): the forward is split at the encoder memory
+        # (spe_forward_stages) and batch i's decoder + heads run on a third stream beside batch
+        # i+1's backbone/encoder; two workspaces alternate between in-flight batches.  The
+        # decoder is ~55 launches of few-row kernels that leave most CUs idle on their own.
+        self.overlap_decode = overlap_decode and not use_graph
+        self.overlap = (overlap or self.overlap_decode) and not use_graph
         self.solve_stream = torch.cuda.Stream(device=device) if self.overlap else None
         self.device = torch.device(device)
         S, Q = model.cfg.input_size, model.cfg.num_queries
@@ -35,6 +40,16 @@ class PosePipeline:
         self.q_gt[:, 0] = 1
         self.t_gt[:, 2] = 10
         model.workspace(batch, dev)
+        if self.overlap_decode:
+            self.dec_stream = torch.cuda.Stream(device=device)
+            self.ws2 = [model.workspace(batch, dev), model.new_workspace(batch, dev)]
+            # per-slot snapshots of what the later stages read (a load() for the next batch may
+            # overwrite the staging buffers while this batch's decoder / solver still run)
+            self.slot_clip = [torch.zeros(batch, 4, device=dev) for _ in range(2)]
+            self.slot_q = [torch.zeros(batch, 4, dtype=torch.float64, device=dev) for _ in range(2)]
+            self.slot_t = [torch.zeros(batch, 3, dtype=torch.float64, device=dev) for _ in range(2)]
+            self.dec_done = [None, None]
+            self.calls = 0
         # raw_frames = (H, W, C): each run() starts from uint8 frames + detector boxes resident in
         # HBM (load_frames) and runs the validation transform on the device first
         self.frames = self.bbox = self.transform = None
@@ -51,16 +66,48 @@ class PosePipeline:
         self.out = None
         _ = Q
 
-    def _solve(self, fo, stream=None):
+    def _solve(self, fo, stream=None, q_gt=None, t_gt=None):
         sig = fo.get("sigmas")
         poses = self.solver.solve_batch(fo["points_px"], fo["probs"], sig, stream=stream)
-        s_t, s_q = device_speed_score(poses["quat"], poses["tvec"], self.q_gt, self.t_gt, stream=stream)
+        q_gt = self.q_gt if q_gt is None else q_gt
+        t_gt = self.t_gt if t_gt is None else t_gt
+        s_t, s_q = device_speed_score(poses["quat"], poses["tvec"], q_gt, t_gt, stream=stream)
         out = {"forward": fo, "poses": poses, "s_t": s_t, "s_q": s_q}
         if sig is not None and self.self_assess:
             out["assess"] = self.solver.self_assess(fo["probs"], sig, poses, stream=stream)   # config-4 filter
         return out
 
+    def _body_staged(self):
+        main = torch.cuda.current_stream()
+        slot = self.calls % 2
+        self.calls += 1
+        if self.transform is not None:
+            self.transform(self.frames, self.bbox, out=self.pp_out)
+        if self.dec_done[slot] is not None:
+            main.wait_event(self.dec_done[slot])      # batch i-2's decoder is done with this workspace
+        self.slot_clip[slot].copy_(self.clip_bbox)
+        self.slot_q[slot].copy_(self.q_gt)
+        self.slot_t[slot].copy_(self.t_gt)
+        self.model.encode(self.images, self.ws2[slot], stream=main)
+        d = self.dec_stream
+        d.wait_stream(main)
+        with torch.cuda.stream(d):
+            fo = self.model.decode(self.B, self.ws2[slot], clip_bbox=self.slot_clip[slot], stream=d)
+            ev = torch.cuda.Event()
+            ev.record(d)
+            self.dec_done[slot] = ev
+        s1 = self.solve_stream
+        s1.wait_stream(d)
+        with torch.cuda.stream(s1):
+            for t in fo.values():
+                t.record_stream(s1)
+            out = self._solve(fo, stream=s1, q_gt=self.slot_q[slot], t_gt=self.slot_t[slot])
+        out["stream"] = s1
+        return out
+
     def _body(self):
+        if self.overlap_decode:
+            return self._body_staged()
         if self.transform is not None:
             self.transform(self.frames, self.bbox, out=self.pp_out)
         fo = self.model(self.images, clip_bbox=self.clip_bbox)

@@ -148,3 +148,35 @@ def test_pipeline_from_raw_frames(gpu_device, small_model):
     torch.cuda.synchronize()
     for k in ("status", "quat", "tvec"):
         assert torch.equal(a["poses"][k], b["poses"][k]), k
+
+
+def test_pipeline_overlap_decode_matches_serial(gpu_device, small_model):
+    """Decoder of batch i on its own stream beside the encoder of batch i+1 (two workspaces,
+    per-slot snapshots of clip boxes / ground truth): every batch's poses and scores equal the
+    serial pipeline's, over consecutive batches that reuse both workspace slots."""
+    from spe.pipeline import PosePipeline
+    from spe.solver import build_solver
+    cfg, w, m = small_model
+    B = 8
+    solver = build_solver(argparse.Namespace(solver="ransac_p3p_lm", repro=20))
+    serial = PosePipeline(m, solver, B, device=gpu_device)
+    staged = PosePipeline(m, solver, B, device=gpu_device, overlap_decode=True)
+    batches = [synthetic_batch(cfg, B, 500 + k) for k in range(4)]
+    dev = gpu_device
+
+    def load(p, b):
+        p.load(torch.from_numpy(b["images"]).to(dev), torch.from_numpy(b["clip_bbox"]).float().to(dev),
+               torch.from_numpy(b["quat"]).to(dev), torch.from_numpy(b["tvec"]).to(dev))
+
+    outs = []
+    for b in batches:                    # enqueue all batches back to back, no host sync between
+        load(staged, b)
+        outs.append(staged.run())
+    torch.cuda.synchronize()
+    for b, o in zip(batches, outs):
+        load(serial, b)
+        r = serial.run()
+        torch.cuda.synchronize()
+        for k in ("status", "quat", "tvec"):
+            assert torch.equal(o["poses"][k], r["poses"][k]), k
+        assert torch.equal(o["s_t"], r["s_t"]) and torch.equal(o["s_q"], r["s_q"])
