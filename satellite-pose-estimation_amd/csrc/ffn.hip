@@ -4,14 +4,16 @@
 //
 // i.e. linear1 -> ReLU -> linear2 -> residual -> norm2 of TransformerEncoderLayer.forward_post
 // (REV/models/transformer.py:164-167) and norm3 of the decoder layer (:235-238).  The
-// [rows x 2048] hidden activation never leaves registers: per 128-row block each wave owns 32
-// rows and keeps its x rows (as MFMA B fragments) and its 256 output columns (as transposed
+// [rows x 2048] hidden activation never leaves registers: per 192-row block each wave owns 48
+// rows (32 in the split-F form) and keeps its x rows (as MFMA B fragments) and its 256 output columns (as transposed
 // accumulators out^T[n][m]) in registers while the block streams W1/W2 in chunks of 32 hidden
 // units through a three-slot LDS ring filled by global_load_lds (two chunks in flight):
 //     H^T[j][m] = W1[j][:] . x[m][:]                 16x16x32 MFMAs, K = 256
 //     out^T[n][m] += W2[n][j] . relu(H^T + b1)[j][m]   16x16x32 MFMAs, K = 32; the H^T accumulator
 //                                                    is re-packed in registers as the B operand
 //                                                    (k order permuted; W2 reads follow it)
+// Each wave owns 16*MB rows (48 by default): every wave streams the whole chunk of weights
+// from LDS, so more rows per wave means more MFMA work per LDS byte and per barrier.
 // The epilogue adds b2 and the residual, does the row LayerNorm with two lane shuffles
 // (each row's 256 columns live in 4 lanes) and stores bf16 in place over x.
 // Versus two GEMM launches + a LayerNorm launch this removes the 2 x rows x 2048 x 2 B round
@@ -19,10 +21,12 @@
 #include "spe_common.h"
 #include "spe_kernels.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int NT = 256;
-constexpr int BM = 128;                 // rows per block (32 per wave)
+constexpr int BM = 128;                 // rows per block of the split-F (few-row) form: 32 per wave
 constexpr int HC = 32;                  // hidden units per chunk
 constexpr int D = 256;
 constexpr int W1_BYTES = HC * D * 2;    // 16 KiB: W1[j][d], 32 rows of 512 B
@@ -65,7 +69,11 @@ SPE_DEV void issue_chunk(const FfnArgs& a, int ch, char* st, int wid, int lane) 
   }
 }
 
+// MB = 16-row MFMA blocks per wave (rows per wave = 16 MB, per block = 64 MB): more rows per
+// wave = more MFMA work per byte of weights read from LDS (every wave reads the whole chunk).
+template <int MB>
 __global__ __launch_bounds__(NT, 1) void ffn_ln_kernel(FfnArgs a) {
+  constexpr int RB = 64 * MB;           // rows per block
   // one LDS array (a second __shared__ object beside in-flight global_load_lds can make the
   // compiler drain vmcnt before LDS reads): [NSTAGE weight stages][b1]
   __shared__ __attribute__((aligned(1024))) char lds[NSTAGE * STAGE + FMAX * 4];
@@ -76,30 +84,32 @@ __global__ __launch_bounds__(NT, 1) void ffn_ln_kernel(FfnArgs a) {
   // the partial out^T of each range goes to a.partial and ffn_reduce_ln_kernel finishes
   const int S = a.partial ? a.splits : 1;
   const int split = blockIdx.x % S;
-  const int m0 = (blockIdx.x / S) * BM + wid * 32;
+  const int m0 = (blockIdx.x / S) * RB + wid * 16 * MB;
   const int cps = a.F / HC / S;
   const int cbeg = split * cps, nchunks = cbeg + cps;   // chunk range [cbeg, nchunks)
   for (int i = tid; i < a.F; i += NT) sb1[i] = a.b1[i];
 
   // x rows of this wave as B fragments: xf[mb][ks] = x[m0 + 16mb + c16][32ks + 8g .. +7]
-  bf16x8 xf[2][8];
+  bf16x8 xf[MB][8];
 #pragma unroll
-  for (int mb = 0; mb < 2; ++mb) {
+  for (int mb = 0; mb < MB; ++mb) {
     const int m = m0 + 16 * mb + c16;
     const bf16* xr = (const bf16*)a.x + (size_t)(m < a.M ? m : 0) * a.ldx;
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks)
       xf[mb][ks] = __builtin_bit_cast(bf16x8, m < a.M ? ld16(xr + 32 * ks + 8 * g) : u32x4{0, 0, 0, 0});
   }
-  f32x4 acc[16][2];
+  f32x4 acc[16][MB];
 #pragma unroll
-  for (int nb = 0; nb < 16; ++nb) { acc[nb][0] = f32x4{0, 0, 0, 0}; acc[nb][1] = f32x4{0, 0, 0, 0}; }
+  for (int nb = 0; nb < 16; ++nb)
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) acc[nb][mb] = f32x4{0, 0, 0, 0};
   // x (and b1) must have landed before the weight DMA starts: vmcnt is in-order, and with a load
   // of x still pending at the loop entry the compiler's merged wait state would drain every
   // in-flight chunk at the first MFMA of each step.  (An asm use of every x register makes the
   // compiler itself retire those loads here; an inline-asm s_waitcnt is invisible to it.)
 #pragma unroll
-  for (int mb = 0; mb < 2; ++mb)
+  for (int mb = 0; mb < MB; ++mb)
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) asm volatile("" ::"v"(xf[mb][ks]));
   wait_vmcnt<0>();
@@ -132,24 +142,27 @@ __global__ __launch_bounds__(NT, 1) void ffn_ln_kernel(FfnArgs a) {
     if (ch + 2 < nchunks) issue_chunk(a, ch + 2, lds + slot2 * STAGE, wid, lane);
     __builtin_amdgcn_sched_barrier(0);
     // ---- H^T chunk: [32 j][32 m] = W1[j] . x[m]   (LDS row 16jb + 4g + r = hidden 8g + 4jb + r)
-    f32x4 h[2][2];
+    f32x4 h[2][MB];
 #pragma unroll
-    for (int jb = 0; jb < 2; ++jb) { h[jb][0] = f32x4{0, 0, 0, 0}; h[jb][1] = f32x4{0, 0, 0, 0}; }
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) h[jb][mb] = f32x4{0, 0, 0, 0};
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) {
 #pragma unroll
       for (int jb = 0; jb < 2; ++jb) {
         const bf16x8 w = __builtin_bit_cast(bf16x8, wa[ks][jb]);
-        h[jb][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, xf[0][ks], h[jb][0], 0, 0, 0);
-        h[jb][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, xf[1][ks], h[jb][1], 0, 0, 0);
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb)
+          h[jb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, xf[mb][ks], h[jb][mb], 0, 0, 0);
       }
     }
     // ---- bias + ReLU, pack as the K=32 B operand: element e <-> hidden 8g + e of the chunk
     const f32x4 b1a = *reinterpret_cast<const f32x4*>(sb1 + ch * HC + 8 * g);
     const f32x4 b1b = *reinterpret_cast<const f32x4*>(sb1 + ch * HC + 8 * g + 4);
-    bf16x8 hb[2];
+    bf16x8 hb[MB];
 #pragma unroll
-    for (int mb = 0; mb < 2; ++mb) {
+    for (int mb = 0; mb < MB; ++mb) {
       float v[8];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
@@ -162,14 +175,15 @@ __global__ __launch_bounds__(NT, 1) void ffn_ln_kernel(FfnArgs a) {
 #pragma unroll
     for (int nb = 0; nb < 16; ++nb) {
       const bf16x8 w = __builtin_bit_cast(bf16x8, wb[nb]);
-      acc[nb][0] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, hb[0], acc[nb][0], 0, 0, 0);
-      acc[nb][1] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, hb[1], acc[nb][1], 0, 0, 0);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb)
+        acc[nb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, hb[mb], acc[nb][mb], 0, 0, 0);
     }
   }
 
   if (a.partial) {                              // split-F: raw partial sums, finished elsewhere
 #pragma unroll
-    for (int mb = 0; mb < 2; ++mb) {
+    for (int mb = 0; mb < MB; ++mb) {
       const int m = m0 + 16 * mb + c16;
       if (m >= a.M) continue;
       float* pr = a.partial + ((size_t)split * a.M + m) * D;
@@ -180,9 +194,9 @@ __global__ __launch_bounds__(NT, 1) void ffn_ln_kernel(FfnArgs a) {
   }
 
   // ---- epilogue: + b2 + residual, LayerNorm over n, bf16 store.  Lane holds, for each of its
-  // two rows m = m0 + 16mb + c16, columns n = 16nb + 4g + r (r = 0..3, nb = 0..15).
+  // MB rows m = m0 + 16mb + c16, columns n = 16nb + 4g + r (r = 0..3, nb = 0..15).
 #pragma unroll
-  for (int mb = 0; mb < 2; ++mb) {
+  for (int mb = 0; mb < MB; ++mb) {
     const int m = m0 + 16 * mb + c16;
     const bool live = m < a.M;
     const bf16* xr = (const bf16*)a.x + (size_t)(live ? m : 0) * a.ldx;
@@ -284,13 +298,18 @@ int spe_launch_ffn_ln(const FfnArgs& a0, hipStream_t s) {
   if (a.D != D || a.F % HC || a.F > FMAX || (a.ldx % 8) || (a.ldy % 8) || (a.ld1 % 8) || (a.ld2 % 8)) return -5;
   if (!a.partial) a.splits = 1;
   if (a.partial && (a.splits < 1 || (a.F / HC) % a.splits)) return -5;
-  const int tiles = (a.M + BM - 1) / BM;
   if (a.partial && a.splits > 1) {
-    hipLaunchKernelGGL(ffn_ln_kernel, dim3(tiles * a.splits), dim3(NT), 0, s, a);
+    const int tiles = (a.M + BM - 1) / BM;
+    hipLaunchKernelGGL(ffn_ln_kernel<2>, dim3(tiles * a.splits), dim3(NT), 0, s, a);
     hipLaunchKernelGGL(ffn_reduce_ln_kernel, dim3((a.M + 3) / 4), dim3(256), 0, s, a);
   } else {
     a.partial = nullptr;
-    hipLaunchKernelGGL(ffn_ln_kernel, dim3(tiles), dim3(NT), 0, s, a);
+    // 48 rows per wave (MB = 3, 493 VGPR+AGPR, no spills) measured 9 % faster than 32 (kbench,
+    // B = 64 encoder FFN: 0.48 vs 0.53 ms); 64 rows spill.  SPE_FFN_MB overrides for A/B runs.
+    static const int mb = [] { const char* e = getenv("SPE_FFN_MB"); return e ? atoi(e) : 3; }();
+    if (mb == 3) hipLaunchKernelGGL(ffn_ln_kernel<3>, dim3((a.M + 191) / 192), dim3(NT), 0, s, a);
+    else if (mb == 4) hipLaunchKernelGGL(ffn_ln_kernel<4>, dim3((a.M + 255) / 256), dim3(NT), 0, s, a);
+    else hipLaunchKernelGGL(ffn_ln_kernel<2>, dim3((a.M + 127) / 128), dim3(NT), 0, s, a);
   }
   return (int)hipGetLastError();
 }

@@ -27,6 +27,8 @@
 #include "spe_common.h"
 #include "spe_kernels.h"
 
+#include <cstdlib>
+
 namespace {
 
 constexpr int BM = 256, BK = 64, NT = 512;
@@ -58,15 +60,18 @@ constexpr int P8_MIN_K = 1024;
 
 // LN: fused post-norm LayerNorm epilogue (a separate instantiation: its 16 extra live
 // registers would push the plain 256-wide kernel into spills)
-template <int BN, int MODE, bool LN, bool P8K = false>
-__global__ __launch_bounds__(NT, 1) void gemm2_kernel(GemmArgs g) {
+// NST = LDS stages: 2 (double-buffered K loop, one workgroup per CU) or 1 (load, wait,
+// multiply per K-step, LDS and registers sized for two resident workgroups per CU, so one
+// workgroup's epilogue and load latency overlap the other's work: short-K linear problems)
+template <int BN, int MODE, bool LN, bool P8K = false, int NST = 2>
+__global__ __launch_bounds__(NT, NST == 1 ? 4 : 1) void gemm2_kernel(GemmArgs g) {
   constexpr int WM = Cfg<BN>::WM, WN = Cfg<BN>::WN;
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
   constexpr int A_BYTES = BM * 128, STAGE = (BM + BN) * 128;
   constexpr int IA = BM / 64, IB = BN / 64;            // glds instructions per wave per stage
   constexpr int LOADS = IA + IB;
   constexpr int EPI_ROWS = 64, EPI_LD = BN + 4;
-  constexpr int SMEM = (2 * STAGE > EPI_ROWS * EPI_LD * 4) ? 2 * STAGE : EPI_ROWS * EPI_LD * 4;
+  constexpr int SMEM = (NST * STAGE > EPI_ROWS * EPI_LD * 4) ? NST * STAGE : EPI_ROWS * EPI_LD * 4;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -213,7 +218,7 @@ __global__ __launch_bounds__(NT, 1) void gemm2_kernel(GemmArgs g) {
   const bool efull = en + 8 <= g.N;
   // (BN = 256: only the first half here, the rest after the K loop, or the K loop would spill)
   // (P8: none before the loop, its phases hold more fragments live)
-  constexpr int NPRE = P8 ? 0 : BN == 256 ? NPASS / 2 : NPASS;
+  constexpr int NPRE = (P8 || NST == 1) ? 0 : BN == 256 ? NPASS / 2 : NPASS;
   u32x4 rres[NPASS][RPT];
   auto fetch_res = [&](int pp) {
 #pragma unroll
@@ -324,6 +329,32 @@ __global__ __launch_bounds__(NT, 1) void gemm2_kernel(GemmArgs g) {
     if (wr == 0) bar_raw();                      // close the stagger
     wait_vmcnt<0>();                             // the zero-line loads past the end, before the
     bar_raw();                                   // epilogue reuses the LDS
+  } else if constexpr (NST == 1) {
+    KPos kpc = kp0;
+    for (int ks = 0; ks < nk; ++ks) {
+      issue(ks, kpc, 0);
+      kpc = kadv(kpc);
+      wait_vmcnt<0>();
+      __builtin_amdgcn_s_barrier();             // every wave's stage-ks lines have landed
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        u32x4 af[FM], bfr[FN];
+#pragma unroll
+        for (int i = 0; i < FM; ++i) af[i] = ld16(smem + swz(wr * TM + i * 16 + fr, 4 * kk + fg));
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bfr[j] = ld16(smem + A_BYTES + swz(wc * TN + j * 16 + fr, 4 * kk + fg));
+#pragma unroll
+        for (int i = 0; i < FM; ++i)
+#pragma unroll
+          for (int j = 0; j < FN; ++j)
+            acc[i][j] = DIRECT ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bfr[j]),
+                                                                        __builtin_bit_cast(bf16x8, af[i]), acc[i][j], 0, 0, 0)
+                               : __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[i]),
+                                                                        __builtin_bit_cast(bf16x8, bfr[j]), acc[i][j], 0, 0, 0);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();             // stage read: the next K-step may refill it
+    }
   } else {
   issue(0, kp0, 0);
   KPos kpn = kadv(kp0);                          // K position of step ks+1
@@ -534,6 +565,28 @@ int launch_bn(const GemmArgs& g, int mode, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// one-stage 256x128 tiles, two workgroups per CU (see NST above)
+int launch_st1(const GemmArgs& g, hipStream_t s) {
+  const int tiles = ((g.M + BM - 1) / BM) * ((g.N + 127) / 128);
+  hipLaunchKernelGGL((gemm2_kernel<128, GEMM_LINEAR, false, false, 1>), dim3(tiles), dim3(NT), 0, s, g);
+  return (int)hipGetLastError();
+}
+// Short-K linear problems take the one-stage kernel when the grid holds >= 2 tiles per
+// workgroup slot.  Measured at the B = 64 bench shapes (kbench): 256x128 + residual 0.118 ->
+// 0.097 ms, 256x256 + residual (K = 64) 0.194 -> 0.182, q/k projection + pos.W^T 0.121 ->
+// 0.113, layer2/3 conv3 + residual -7 / -8 %; a plain K = 64, N = 256 store got slower
+// (0.129 -> 0.138) and stays on the two-stage kernel.  SPE_GEMM_ST1_K overrides the K bound
+// (0 disables) for A/B runs.
+int st1_max_k() {
+  static const int v = [] { const char* e = getenv("SPE_GEMM_ST1_K"); return e ? atoi(e) : 256; }();
+  return v;
+}
+bool use_st1(const GemmArgs& g, int mode) {
+  if (mode != GEMM_LINEAR || g.K > st1_max_k() || g.N < 128 || g.ln_g) return false;
+  if (!g.R && g.vt_T == 0 && g.N >= 256) return false;
+  return ((g.M + BM - 1) / BM) * ((g.N + 127) / 128) >= 512;
+}
+
 }  // namespace
 
 namespace {
@@ -690,6 +743,7 @@ int spe_launch_gemm2(const GemmArgs& g, int mode, hipStream_t s) {
     else hipLaunchKernelGGL(gemm_small_kernel<false>, dim3(tiles), dim3(SM_NT), 0, s, g);
     return (int)hipGetLastError();
   }
+  if (use_st1(g, mode)) return launch_st1(g, s);
   const int bn = (g.N <= 64 && g.vt_T == 0) ? 64 : g.N <= 128 ? 128 : 256;   // BN 64 has no V^T store
   const int tiles = ((g.M + BM - 1) / BM) * ((g.N + bn - 1) / bn);
   // too few tiles for the large-tile kernel: the 128x128 kernel.  (169 tiles of 256x256 on the

@@ -256,6 +256,43 @@ def test_gemm_fp16_output(gpu_device, M, N, vt):
     _close(C, ref, 2e-3)
 
 
+@pytest.mark.parametrize("M,N,K,mode", [(256 * 600 + 5, 256, 64, "res"), (256 * 1100 + 100, 128, 256, "relu"),
+                                         (300 * 512, 512, 256, "periodic"), (64 * 2704, 256, 256, "vt")])
+def test_gemm_one_stage_large(gpu_device, M, N, K, mode):
+    """Sizes that take the one-stage, two-workgroups-per-CU kernel (short K, >= 512 tiles of
+    256x128): residual, ReLU, row-periodic residual (the q/k projection's pos.W^T) and the
+    head-transposed V^T store, against an fp32 torch reference."""
+    g = torch.Generator(device="cpu").manual_seed(M + K)
+    dt = torch.bfloat16
+    A = torch.randn(M, K, generator=g).to(gpu_device, dt)
+    Wt = (torch.randn(N, K, generator=g) / K ** 0.5).to(gpu_device, dt)
+    bias = torch.randn(N, generator=g).to(gpu_device)
+    ref = A.float() @ Wt.float().t() + bias
+    W = _padded_weight(Wt, (K + 63) // 64 * 64, dt)
+    ldb = W.shape[1]
+    if mode == "vt":
+        T = 2704
+        B = M // T
+        C = torch.zeros(B * N * T, dtype=dt, device=gpu_device)
+        _gemm("bf16", 0, A, W, M, N, K, K, ldb, C, 8, bias=bias, vt=(T, B))
+        ref = ref.view(B, T, N // 256, 256).permute(2, 0, 3, 1).reshape(-1)
+    else:
+        C = torch.zeros(M, N, dtype=dt, device=gpu_device)
+        if mode == "res":
+            R = torch.randn(M, N, generator=g).to(gpu_device, dt)
+            _gemm("bf16", 0, A, W, M, N, K, K, ldb, C, N, bias=bias, R=R, ldr=N, relu=1)
+            ref = torch.relu(ref + R.float())
+        elif mode == "relu":
+            _gemm("bf16", 0, A, W, M, N, K, K, ldb, C, N, bias=bias, relu=1)
+            ref = torch.relu(ref)
+        else:
+            P = 512
+            R = torch.randn(P, N, generator=g).to(gpu_device, dt)
+            _gemm("bf16", 0, A, W, M, N, K, K, ldb, C, N, bias=bias, R=R, ldr=N, r_period=P)
+            ref = ref + R.float().repeat(M // P, 1)
+    _close(C, ref, 2e-2)
+
+
 def _attn_ref(q, k, v, scale):
     a = torch.softmax((q.float() @ k.float().transpose(-1, -2)) * scale, -1)
     return a @ v.float()
