@@ -24,8 +24,11 @@ sys.path.insert(0, os.path.join(REPO, "satellite-pose-estimation_amd"))
 
 PEAK = {"bf16": {"mfma": 2500.0}, "fp32": {"mfma": 157.3}, "hbm": 8000.0}   # TFLOP/s, GB/s (MI355X_MICROARCH.md)
 # profiler symbol of each launch class (to match profiles/*kernel_stats.csv rows)
-KIND_SYMBOL = {"attn.enc": "attn16_kernel<0, __bf16>", "attn.dec_self": "attn16_kernel<1, __bf16>",
-               "attn.dec_cross": "xattn_kernel", "ffn.enc": "ffn_ln_kernel", "ffn.dec": "ffn_ln_kernel"}
+# (rocprofv3 prints the attention kernels mangled: it does not demangle the __bf16 / _Float16
+# template arguments, DF16b / DF16_)
+KIND_SYMBOL = {"attn.enc": "_ZN12_GLOBAL__N_113attn16_kernelILi0EDF16bEEv8AttnArgs",
+               "attn.dec_self": "_ZN12_GLOBAL__N_113attn16_kernelILi1EDF16bEEv8AttnArgs",
+               "attn.dec_cross": "xattn_kernel", "ffn.enc": "ffn_ln_kernel<3>", "ffn.dec": "ffn_ln_kernel<2>"}
 
 
 # BASELINE.json configs: per-GPU shapes (configs 3-5 are quoted at bs=256 over 8 GPUs = 32/GPU)
@@ -292,7 +295,7 @@ def main():
                    "num_queries": args.queries, "attention_dtype": args.attn_dtype,
                    "parallelism": f"dp{world} (image sharding)"},
         "roofline": {"kernel": dominant, "kernel_symbol": KIND_SYMBOL.get(dominant, dominant).replace(
-                         "<0, __bf16>", "<0, _Float16>" if args.attn_dtype == "fp16" else "<0, __bf16>"),
+                         "DF16b", "DF16_" if args.attn_dtype == "fp16" else "DF16b"),
                      "bound": "mfma" if mfma_bound else "hbm", "achieved": achieved,
                      "peak": peak, "unit": unit, "frac": achieved / peak,
                      "traffic": traffic_for(dominant, launch_grid(dominant, B, cfg), args.attn_dtype), "launches": k_n, "avg_launch_ms": avg_ms,
