@@ -18,7 +18,7 @@
 extern "C" {
 #endif
 
-#define SPE_ABI_VERSION 2
+#define SPE_ABI_VERSION 3
 
 enum {
   SPE_E_ARG = -1,        /* bad argument / size */
@@ -77,6 +77,8 @@ typedef struct {
   float* log_sigmas;      /* [B,Q,2]  sigma head raw output (nullable) */
   float* sigmas;          /* [B,Q,2]  exp(log_sigmas) (nullable) */
   float* hs;              /* [B,Q,256] last decoder layer after decoder_norm (nullable) */
+  float* aux_logits;      /* [dec_layers-1,B,Q,12] aux outputs (nullable; aux_loss=True, */
+  float* aux_points;      /* [dec_layers-1,B,Q,2]   REV/models/detr_speed.py:88-99)       */
 } spe_forward_outputs;
 
 int spe_abi_version(void);
@@ -115,6 +117,17 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int batc
  * status (nullable): [B] 0 ok, 1 empty crop (the reference raises; zeros written). */
 int spe_preprocess(void* stream, const uint8_t* frames, int batch, int height, int width, int channels,
                    const double* bbox_xxyy, int size, float* images, float* clip_bbox, int32_t* status);
+
+/* SetCriterion.forward with its HungarianMatcher (REV/models/detr_speed.py:214-261,
+ * REV/models/matcher.py:60-88) for `layers` decoder layers (aux first, last layer last), the
+ * logging half of evaluate() (REV/engine.py:99-112).  Device pointers: logits [L,B,Q,C] (C = 12),
+ * points [L,B,Q,2], tgt_labels int32 [B,T], tgt_points [B,T,2] (crop-normalised), match int32
+ * [L,B,T] (query matched to each target), losses fp64 [L,4] = loss_ce, class_error,
+ * cardinality_error, loss_points.  num_points: targets per rank averaged over ranks, >= 1
+ * (REV/models/detr_speed.py:235-244).  Q <= 64, T <= min(Q, 32). */
+int spe_criterion(void* stream, const float* logits, const float* points, const int32_t* tgt_labels,
+                  const float* tgt_points, int layers, int batch, int num_queries, int num_classes, int num_targets,
+                  float cost_class, float cost_pts, float eos_coef, double num_points, int32_t* match, double* losses);
 
 /* PostProcess alone (REV/models/detr_speed.py:266-293). */
 int spe_postprocess(void* stream, const float* logits, const float* points, const float* clip_bbox, int batch,

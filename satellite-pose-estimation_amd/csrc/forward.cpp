@@ -394,6 +394,19 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       }
       CK(run_other(m, "ln.dec", 0.0, (double)Mq * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.dtmp), e.n3g, e.n3b, P(w.tgt), nullptr, Mq, d, dt, s); }));
     }
+    if (out->aux_logits && out->aux_points && l + 1 < L) {
+      // aux output of layer l: the shared decoder_norm (REV/models/transformer.py:117-124) and
+      // the same heads (REV/models/detr_speed.py:83-99), into the aux slices
+      float* hs_aux = (float*)P(w.hs);
+      CK(run_other(m, "ln.dec", 0.0, (double)Mq * d * (m->esz + 4), s, [&] { return spe_launch_layernorm(P(w.tgt), m->dng, m->dnb, nullptr, hs_aux, Mq, d, dt, s); }));
+      HeadArgs ha = m->head;
+      ha.hs = hs_aux; ha.B = B; ha.Q = Q;
+      ha.clip_bbox = nullptr; ha.probs = nullptr; ha.points_px = nullptr;
+      ha.log_sigmas = nullptr; ha.sigmas = nullptr;
+      ha.logits = out->aux_logits + (size_t)l * Mq * 12;
+      ha.points = out->aux_points + (size_t)l * Mq * 2;
+      CK(run_other(m, "heads", 0.0, (double)Mq * d * 4, s, [&] { return spe_launch_heads(ha, s); }));
+    }
   }
   float* hs = out->hs ? out->hs : (float*)P(w.hs);
   CK(run_other(m, "ln.dec", 0.0, (double)Mq * d * (m->esz + 4), s, [&] { return spe_launch_layernorm(P(w.tgt), m->dng, m->dnb, nullptr, hs, Mq, d, dt, s); }));
@@ -408,6 +421,42 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   h.log_sigmas = out->log_sigmas; h.sigmas = out->sigmas;
   if (!c.sigma_head) { h.log_sigmas = nullptr; h.sigmas = nullptr; }
   CK(run_other(m, "heads", 0.0, (double)Mq * d * 4, s, [&] { return spe_launch_heads(h, s); }));
+  return 0;
+}
+
+// Device scratch of the criterion's per-image partial sums (grown on demand, kept; steady-state
+// calls allocate nothing -- a first call with a larger batch must happen outside graph capture)
+static double* crit_scratch(size_t n) {
+  static std::mutex mu;
+  static std::map<int, std::pair<double*, size_t>> bufs;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> g(mu);
+  auto& e = bufs[dev];
+  if (e.second < n) {
+    if (e.first) (void)hipFree(e.first);
+    e.first = nullptr;
+    e.second = 0;
+    if (hipMalloc((void**)&e.first, n * sizeof(double)) != hipSuccess) return nullptr;
+    e.second = n;
+  }
+  return e.first;
+}
+
+int spe_criterion(void* stream, const float* logits, const float* points, const int32_t* tgt_labels,
+                  const float* tgt_points, int layers, int batch, int num_queries, int num_classes, int num_targets,
+                  float cost_class, float cost_pts, float eos_coef, double num_points, int32_t* match, double* losses) {
+  if (!logits || !points || !tgt_labels || !tgt_points || !match || !losses || layers < 1 || batch < 0 ||
+      num_queries < 1 || num_queries > 64 || num_targets < 1 || num_targets > 32 || num_targets > num_queries ||
+      num_classes < 2 || num_classes > 32 || !(num_points > 0))
+    return fail(SPE_E_ARG, "bad argument");
+  CritArgs a{logits, points, tgt_labels, tgt_points, layers, batch, num_queries, num_classes, num_targets,
+             cost_class, cost_pts, eos_coef, num_points, match, nullptr, losses};
+  if (batch > 0) {
+    a.partial = crit_scratch((size_t)layers * batch * 5);
+    if (!a.partial) return fail(SPE_E_LAUNCH, "criterion scratch allocation failed");
+  }
+  CK(spe_launch_criterion(a, (hipStream_t)stream));
   return 0;
 }
 

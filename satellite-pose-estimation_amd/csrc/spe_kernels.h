@@ -119,5 +119,20 @@ struct HeadArgs {
   float* sigmas;                   // [B][Q][2] exp (nullable)
 };
 int spe_launch_heads(const HeadArgs& a, hipStream_t s);
+
+// Set criterion (criterion.hip): Hungarian matching + losses for L layers of B images.
+struct CritArgs {
+  const float* logits;             // [L][B][Q][C]
+  const float* points;             // [L][B][Q][2]
+  const int32_t* tgt_labels;       // [B][T]
+  const float* tgt_points;         // [B][T][2]
+  int L, B, Q, C, T;
+  float cost_class, cost_pts, eos_coef;
+  double num_points;               // loss_points normaliser
+  int32_t* match;                  // [L][B][T] matched query per target (out)
+  double* partial;                 // [L][B][5] scratch
+  double* losses;                  // [L][4] loss_ce, class_error, cardinality_error, loss_points (out)
+};
+int spe_launch_criterion(const CritArgs& a, hipStream_t s);
 int spe_launch_postprocess(const float* logits, const float* points, const float* clip_bbox, int B, int Q,
                            float* probs, float* points_px, hipStream_t s);

@@ -2,8 +2,10 @@
 
 Per batch: one device pass (model + fused PostProcess), one batched solver launch and one
 D2H copy of the pose records, instead of the reference's per-image Python solver loop.
-The criterion (Hungarian matcher + losses, REV/engine.py:99-112) only feeds logging and is
-skipped when None (it is out of the inference scope).
+The criterion (Hungarian matcher + losses, REV/engine.py:99-112) runs on the device
+(spe.models.SetCriterion) when given; its losses are logged like the reference's
+MetricLogger: per-batch values averaged over batches, weighted ("loss", "loss_ce", ...) and
+"<k>_unscaled", plus "class_error".
 """
 from __future__ import annotations
 
@@ -16,13 +18,33 @@ from .speed_eval import SpeedEval, device_speed_score
 @torch.no_grad()
 def evaluate(model, criterion, postprocessors, data_loader, gt_file, solver, device, output_dir=None):
     evaluator = SpeedEval(gt_file, solver)
+    meters = {}
+
+    def log(k, v):
+        s = meters.setdefault(k, [0.0, 0])
+        s[0] += float(v)
+        s[1] += 1
+
     for samples, targets in data_loader:
         samples = samples.to(device)
         filenames = [t["filename"] for t in targets]
         clip = torch.stack([torch.as_tensor(t["clip_bbox"], dtype=torch.float32) for t in targets]).to(device)
         outputs = model(samples, clip_bbox=clip)
         if criterion is not None:
-            criterion(outputs, [{k: v.to(device) for k, v in t.items() if torch.is_tensor(v)} for t in targets])
+            ld = criterion(outputs, [{k: v.to(device) for k, v in t.items() if torch.is_tensor(v)} for t in targets])
+            ld = {k: float(v) for k, v in ld.items()}
+            if spe_dist.is_dist():                            # utils.reduce_dict (REV/engine.py:103)
+                vals = torch.tensor([ld[k] for k in sorted(ld)], dtype=torch.float64, device=device)
+                torch.distributed.all_reduce(vals)
+                ld = dict(zip(sorted(ld), (vals / torch.distributed.get_world_size()).tolist()))
+            wd = criterion.weight_dict
+            scaled = {k: v * wd[k] for k, v in ld.items() if k in wd}
+            log("loss", sum(scaled.values()))
+            for k, v in scaled.items():
+                log(k, v)
+            for k, v in ld.items():
+                log(k + "_unscaled", v)
+            log("class_error", ld["class_error"])
         poses = solver.solve_batch(outputs["points_px"], outputs["probs"], outputs.get("sigmas"))
         gt = [evaluator.ground_truth[f] for f in filenames]
         q_gt = torch.tensor([g["quat"] for g in gt], dtype=torch.float64, device=device)
@@ -33,5 +55,6 @@ def evaluate(model, criterion, postprocessors, data_loader, gt_file, solver, dev
         evaluator.update_batch(filenames, outputs["points_px"], outputs["probs"], poses, s_t, s_q, sig, assess)
     evaluator.log = spe_dist.all_gather_log(evaluator.log)
     evaluator.summarize()
-    stats = {"speed_eval_pose": evaluator.stats}
+    stats = {k: s / max(n, 1) for k, (s, n) in meters.items()}
+    stats["speed_eval_pose"] = evaluator.stats
     return stats, evaluator

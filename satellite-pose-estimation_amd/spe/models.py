@@ -106,10 +106,15 @@ class DETR(nn.Module):
         if clip_bbox is not None:
             out["probs"] = torch.empty(B, Q, 12, device=dev)
             out["points_px"] = torch.empty(B, Q, 2, device=dev)
+        aux_l = aux_p = None
+        if self.aux_loss and self.cfg.dec_layers > 1:       # REV/models/detr_speed.py:88-99
+            aux_l = torch.empty(self.cfg.dec_layers - 1, B, Q, 12, device=dev)
+            aux_p = torch.empty(self.cfg.dec_layers - 1, B, Q, 2, device=dev)
+            out["aux_outputs"] = [{"pred_logits": a, "pred_points": p} for a, p in zip(aux_l, aux_p)]
         o = _lib.ForwardOutputs(_lib.ptr(out["pred_logits"]), _lib.ptr(out["pred_points"]), _lib.ptr(clip_bbox),
                                 _lib.ptr(out.get("probs")), _lib.ptr(out.get("points_px")),
                                 _lib.ptr(out.get("pred_sigmas")), _lib.ptr(out.get("sigmas")),
-                                _lib.ptr(out.get("hs")))
+                                _lib.ptr(out.get("hs")), _lib.ptr(aux_l), _lib.ptr(aux_p))
         return out, o
 
     def encode(self, images, ws, stream=None):
@@ -162,6 +167,59 @@ class DETR(nn.Module):
             pass
 
 
+class SetCriterion(nn.Module):
+    """REV/models/detr_speed.py:103-261 with the HungarianMatcher of REV/models/matcher.py:35-88,
+    on the device (spe_criterion, csrc/criterion.hip): one launch matches and scores the last
+    layer and every aux layer.  Returns the reference's loss dict (loss_ce, class_error,
+    loss_points, cardinality_error, and *_i for aux layer i without class_error) as 0-d device
+    tensors; `weight_dict` as REV/models/detr_speed.py:319-327 builds it.  The matching of the
+    last call is kept in `last_match` ([L,B,T] query per target; layer L-1 = last)."""
+
+    def __init__(self, num_classes: int = 11, cost_class: float = 1.0, cost_pts: float = 5.0,
+                 eos_coef: float = 0.1, pts_loss_coef: float = 5.0, dec_layers: int = 6, aux_loss: bool = True):
+        super().__init__()
+        self.num_classes, self.cost_class, self.cost_pts, self.eos_coef = num_classes, cost_class, cost_pts, eos_coef
+        self.weight_dict = {"loss_ce": 1, "loss_points": pts_loss_coef}
+        if aux_loss:
+            for i in range(dec_layers - 1):
+                self.weight_dict.update({f"loss_ce_{i}": 1, f"loss_points_{i}": pts_loss_coef})
+        self.last_match = None
+
+    @torch.no_grad()
+    def forward(self, outputs, targets, stream=None):
+        layers = [(a["pred_logits"], a["pred_points"]) for a in outputs.get("aux_outputs", [])]
+        layers.append((outputs["pred_logits"], outputs["pred_points"]))
+        logits = torch.stack([l for l, _ in layers]).float().contiguous()
+        points = torch.stack([p for _, p in layers]).float().contiguous()
+        L, B, Q, C = logits.shape
+        dev = logits.device
+        labels = torch.stack([t["labels"] for t in targets]).to(dev, torch.int32).contiguous()
+        tpts = torch.stack([t["landmarks"] for t in targets]).to(dev, torch.float32).contiguous()
+        T = labels.shape[1]
+        num_points = float(B * T)                         # REV/models/detr_speed.py:235-244
+        from . import dist as spe_dist
+        if spe_dist.is_dist():
+            n = torch.tensor([num_points], dtype=torch.float64, device=dev)
+            torch.distributed.all_reduce(n)
+            num_points = float(n.item()) / torch.distributed.get_world_size()
+        num_points = max(num_points, 1.0)
+        match = torch.empty(L, B, T, dtype=torch.int32, device=dev)
+        res = torch.empty(L, 4, dtype=torch.float64, device=dev)
+        _lib.check(_lib.lib().spe_criterion(_lib.stream_ptr(stream), _lib.ptr(logits), _lib.ptr(points), _lib.ptr(labels),
+                                            _lib.ptr(tpts), L, B, Q, C, T, self.cost_class, self.cost_pts,
+                                            self.eos_coef, num_points, _lib.ptr(match), _lib.ptr(res)), "spe_criterion")
+        self.last_match = match
+        losses = {}
+        for l in range(L):
+            sfx = "" if l == L - 1 else f"_{l}"
+            losses["loss_ce" + sfx] = res[l, 0]
+            if l == L - 1:
+                losses["class_error"] = res[l, 1]
+            losses["cardinality_error" + sfx] = res[l, 2]
+            losses["loss_points" + sfx] = res[l, 3]
+        return losses
+
+
 class PostProcess(nn.Module):
     """REV/models/detr_speed.py:264-293 (and the sigma variant,
     UNC/src/zoo/rtdetr/rtdetr_postprocessor.py:44-78): softmax over the 12 classes and
@@ -193,10 +251,15 @@ class PostProcess(nn.Module):
 
 def build_model(args, dtype: str = None):
     """REV/models/__init__.py:5-6 / detr_speed.py:296-336.  Returns (model, criterion,
-    postprocessors).  The training criterion (Hungarian matcher + losses) is outside the
-    inference hot path and is returned as None (out of scope)."""
+    postprocessors); the criterion is the device SetCriterion with the reference's argparse
+    defaults (set_cost_class 1, set_cost_pts 5, eos_coef 0.1, pts_loss_coef 5)."""
     cfg = SpeConfig.from_args(args)
     dtype = dtype or getattr(args, "dtype", "bf16")
-    model = DETR(cfg, dtype=dtype, aux_loss=bool(getattr(args, "aux_loss", False)),
-                 attn_dtype=getattr(args, "attn_dtype", None))
-    return model, None, {"points": PostProcess()}
+    aux = bool(getattr(args, "aux_loss", False))
+    model = DETR(cfg, dtype=dtype, aux_loss=aux, attn_dtype=getattr(args, "attn_dtype", None))
+    criterion = SetCriterion(cost_class=float(getattr(args, "set_cost_class", 1.0)),
+                             cost_pts=float(getattr(args, "set_cost_pts", 5.0)),
+                             eos_coef=float(getattr(args, "eos_coef", 0.1)),
+                             pts_loss_coef=float(getattr(args, "pts_loss_coef", 5.0)),
+                             dec_layers=cfg.dec_layers, aux_loss=aux)
+    return model, criterion, {"points": PostProcess()}
