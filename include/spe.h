@@ -129,6 +129,14 @@ int spe_criterion(void* stream, const float* logits, const float* points, const 
                   const float* tgt_points, int layers, int batch, int num_queries, int num_classes, int num_targets,
                   float cost_class, float cost_pts, float eos_coef, double num_points, int32_t* match, double* losses);
 
+/* Multi-checkpoint ensemble front end (Multi_Mean_PoseSolver, REV/utils/speed_eval.py:42-100;
+ * REV/gen_submission_multi.py:145-186): fuses M models' PostProcess outputs per image -- labels
+ * in first-seen order, per label the mean of its points after the 3-sigma filter -- into
+ * fused_points [B,C-1,2] + one-hot fused_probs [B,C-1,C], the input spe_pnp_batch then solves
+ * (RANSAC_P3P_LM, like the reference).  points [M,B,Q,2] px, probs [M,B,Q,C]; M * Q <= 256. */
+int spe_ensemble_fuse(void* stream, const float* points_px, const float* probs, int models, int batch,
+                      int num_queries, int num_classes, float* fused_points, float* fused_probs);
+
 /* PostProcess alone (REV/models/detr_speed.py:266-293). */
 int spe_postprocess(void* stream, const float* logits, const float* points, const float* clip_bbox, int batch,
                     int num_queries, float* probs, float* points_px);

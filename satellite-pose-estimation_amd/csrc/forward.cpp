@@ -460,6 +460,16 @@ int spe_criterion(void* stream, const float* logits, const float* points, const 
   return 0;
 }
 
+int spe_ensemble_fuse(void* stream, const float* points_px, const float* probs, int models, int batch,
+                      int num_queries, int num_classes, float* fused_points, float* fused_probs) {
+  if (!points_px || !probs || !fused_points || !fused_probs || models < 1 || batch < 0 || num_queries < 1 ||
+      num_classes < 2 || num_classes > 17 || (int64_t)models * num_queries > 256)
+    return fail(SPE_E_ARG, "bad argument");
+  EnsembleArgs a{points_px, probs, models, batch, num_queries, num_classes, fused_points, fused_probs};
+  CK(spe_launch_ensemble_fuse(a, (hipStream_t)stream));
+  return 0;
+}
+
 int spe_preprocess(void* stream, const uint8_t* frames, int batch, int height, int width, int channels,
                    const double* bbox_xxyy, int size, float* images, float* clip_bbox, int32_t* status) {
   if (!frames || !bbox_xxyy || !images || !clip_bbox || batch < 0 || height <= 0 || width <= 0 || size <= 0 ||

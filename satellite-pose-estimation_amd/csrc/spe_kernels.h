@@ -134,5 +134,16 @@ struct CritArgs {
   double* losses;                  // [L][4] loss_ce, class_error, cardinality_error, loss_points (out)
 };
 int spe_launch_criterion(const CritArgs& a, hipStream_t s);
+
+// Multi-model keypoint fusion (ensemble.hip): M models' PostProcess outputs -> one fused
+// keypoint set per image in spe_pnp_batch's input layout.
+struct EnsembleArgs {
+  const float* points;             // [M][B][Q][2] image px
+  const float* probs;              // [M][B][Q][C]
+  int M, B, Q, C;
+  float* fused_points;             // [B][C-1][2]
+  float* fused_probs;              // [B][C-1][C] one-hot rows (background padding)
+};
+int spe_launch_ensemble_fuse(const EnsembleArgs& a, hipStream_t s);
 int spe_launch_postprocess(const float* logits, const float* points, const float* clip_bbox, int B, int Q,
                            float* probs, float* points_px, hipStream_t s);

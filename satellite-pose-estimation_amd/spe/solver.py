@@ -128,6 +128,40 @@ class EPnPSolver(PoseSolver):
         super().__init__(_lib.SPE_PNP_EPNP_LM if refine else _lib.SPE_PNP_EPNP, 20.0)
 
 
+class Multi_Mean_PoseSolver(PoseSolver):
+    """Multi-checkpoint ensemble (REV/utils/speed_eval.py:42-140): the M models' keypoints are
+    fused per label (mean after a 3-sigma filter, first-seen label order) on the device
+    (spe_ensemble_fuse) and solved like SimplePoseSolver (P3P-RANSAC + LM)."""
+
+    def __init__(self, args=None):
+        super().__init__(_lib.SPE_PNP_RANSAC_P3P_LM, getattr(args, "repro", 25) if args is not None else 25)
+
+    def fuse_batch(self, multi_points_px, multi_probs, stream=None):
+        """lists of M device tensors [B,Q,2] / [B,Q,C] -> fused points [B,C-1,2], probs [B,C-1,C]."""
+        pts = torch.stack(list(multi_points_px)).float().contiguous()
+        prb = torch.stack(list(multi_probs)).float().contiguous()
+        M, B, Q, C = prb.shape
+        fp = torch.empty(B, C - 1, 2, device=prb.device)
+        fr = torch.empty(B, C - 1, C, device=prb.device)
+        _lib.check(_lib.lib().spe_ensemble_fuse(_lib.stream_ptr(stream), _lib.ptr(pts), _lib.ptr(prb), M, B, Q, C,
+                                                _lib.ptr(fp), _lib.ptr(fr)), "spe_ensemble_fuse")
+        return fp, fr
+
+    def solve_batch_multi(self, multi_points_px, multi_probs, stream=None):
+        fp, fr = self.fuse_batch(multi_points_px, multi_probs, stream=stream)
+        return self.solve_batch(fp, fr, stream=stream)
+
+    def __call__(self, multi_points, multi_logits, device=None):
+        """One image, numpy lists in / numpy out, the reference's call (gen_submission)."""
+        assert isinstance(multi_points, list) and isinstance(multi_logits, list)
+        assert len(multi_points) == len(multi_logits)
+        dev = device or torch.device("cuda")
+        mp = [torch.from_numpy(np.asarray(p, np.float32)[None].copy()).to(dev) for p in multi_points]
+        ml = [torch.from_numpy(np.asarray(l, np.float32)[None].copy()).to(dev) for l in multi_logits]
+        fp, fr = self.fuse_batch(mp, ml)
+        return PoseSolver.__call__(self, fp[0].cpu().numpy(), fr[0].cpu().numpy(), device=dev)
+
+
 def build_solver(args=None):
     """REV/utils/speed_eval.py:21-22 (SimplePoseSolver); `args.solver` selects the variant."""
     name = getattr(args, "solver", "ransac_p3p_lm") if args is not None else "ransac_p3p_lm"
