@@ -49,6 +49,7 @@ class PosePipeline:
             self.slot_q = [torch.zeros(batch, 4, dtype=torch.float64, device=dev) for _ in range(2)]
             self.slot_t = [torch.zeros(batch, 3, dtype=torch.float64, device=dev) for _ in range(2)]
             self.dec_done = [None, None]
+            self.solve_done = [None, None]
             self.calls = 0
         # raw_frames = (H, W, C): each run() starts from uint8 frames + detector boxes resident in
         # HBM (load_frames) and runs the validation transform on the device first
@@ -85,6 +86,8 @@ class PosePipeline:
             self.transform(self.frames, self.bbox, out=self.pp_out)
         if self.dec_done[slot] is not None:
             main.wait_event(self.dec_done[slot])      # batch i-2's decoder is done with this workspace
+        if self.solve_done[slot] is not None:
+            main.wait_event(self.solve_done[slot])    # ... and its solver / score with the slot's snapshots
         self.slot_clip[slot].copy_(self.clip_bbox)
         self.slot_q[slot].copy_(self.q_gt)
         self.slot_t[slot].copy_(self.t_gt)
@@ -102,6 +105,9 @@ class PosePipeline:
             for t in fo.values():
                 t.record_stream(s1)
             out = self._solve(fo, stream=s1, q_gt=self.slot_q[slot], t_gt=self.slot_t[slot])
+            ev = torch.cuda.Event()
+            ev.record(s1)
+            self.solve_done[slot] = ev
         out["stream"] = s1
         return out
 
@@ -114,11 +120,14 @@ class PosePipeline:
         if not self.overlap:
             return self._solve(fo)
         s1 = self.solve_stream
+        # the ground truth is snapshotted on the caller's stream: a load() of the next batch may
+        # overwrite q_gt / t_gt while this batch's score still runs on the solver stream
+        q_gt, t_gt = self.q_gt.clone(), self.t_gt.clone()
         s1.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s1):
-            for t in fo.values():
-                t.record_stream(s1)          # forward outputs are consumed on the solver stream
-            out = self._solve(fo, stream=s1)
+            for t in list(fo.values()) + [q_gt, t_gt]:
+                t.record_stream(s1)          # consumed on the solver stream
+            out = self._solve(fo, stream=s1, q_gt=q_gt, t_gt=t_gt)
         out["stream"] = s1
         return out
 
