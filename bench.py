@@ -261,7 +261,7 @@ def main():
     score = float((out["s_t"] + out["s_q"]).mean().item())
     status = out["poses"]["status"].cpu()
     if rank != 0:
-        if world > 1:
+        if dist.is_initialized():
             dist.destroy_process_group()
         return
     total_images = B * world * args.steps
@@ -310,7 +310,7 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds, args.solver)
     print(json.dumps(result))
-    if world > 1:
+    if dist.is_initialized():
         dist.destroy_process_group()
 
 
