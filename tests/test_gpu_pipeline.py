@@ -101,7 +101,9 @@ def test_evaluate_matches_reference_style_speedeval(gpu_device, small_model):
 @pytest.mark.parametrize("solver_name", ["epnp", "ransac_p3p_lm"])
 def test_overlapped_pipeline_equals_serial(gpu_device, small_model, solver_name):
     """Solver of batch i on the second stream while the forward of batch i+1 runs: after wait(),
-    every batch's poses / scores equal the single-stream pipeline's (same inputs, same kernels)."""
+    every batch's poses / scores equal the single-stream pipeline's (same inputs, same kernels;
+    each batch loads its own ground truth, which the next load() overwrites while the previous
+    batch's score may still be queued)."""
     from spe.pipeline import PosePipeline
     from spe.solver import build_solver
     cfg, w, m = small_model
@@ -113,16 +115,16 @@ def test_overlapped_pipeline_equals_serial(gpu_device, small_model, solver_name)
         pipe = PosePipeline(m, solver, B, device=gpu_device, overlap=ov)
         outs = []
         for b in batches:
-            pipe.load(torch.from_numpy(b["images"]).to(gpu_device), torch.from_numpy(b["clip_bbox"]).float().to(gpu_device))
+            pipe.load(torch.from_numpy(b["images"]).to(gpu_device), torch.from_numpy(b["clip_bbox"]).float().to(gpu_device),
+                      torch.from_numpy(b["quat"]).to(gpu_device), torch.from_numpy(b["tvec"]).to(gpu_device))
             outs.append(pipe.run())
         for o in outs:
             pipe.wait(o)
-        res[ov] = [(o["poses"]["status"].cpu().numpy(), o["poses"]["tvec"].cpu().numpy(), o["s_t"].cpu().numpy())
-                   for o in outs]
-    for (s0, t0, e0), (s1, t1, e1) in zip(res[False], res[True]):
-        np.testing.assert_array_equal(s0, s1)
-        np.testing.assert_array_equal(t0, t1)
-        np.testing.assert_array_equal(e0, e1)
+        res[ov] = [(o["poses"]["status"].cpu().numpy(), o["poses"]["tvec"].cpu().numpy(), o["s_t"].cpu().numpy(),
+                    o["s_q"].cpu().numpy()) for o in outs]
+    for r0, r1 in zip(res[False], res[True]):
+        for x0, x1 in zip(r0, r1):
+            np.testing.assert_array_equal(x0, x1)
 
 
 def test_pipeline_from_raw_frames(gpu_device, small_model):
