@@ -16,8 +16,9 @@ REV/gen_submission_multi.py:145-186):
 numpy's reductions are restated operation for operation: an axis-0 mean of an [n, 2] float32
 array accumulates row by row in float32 and divides in float32; np.std of the 1-D fp64
 distances uses numpy's pairwise summation (sequential below 8 elements, 8 accumulators above).
-Deliberate divergence: when every point of a label coincides (std 0) the reference's inlier set
-is empty and its mean NaN; here the label keeps the plain mean.  The reference module imports
+When no point is closer than 3 std (every point of a label coincides, std 0, or all distances
+are equal) the reference's inlier set is empty and np.mean gives a NaN point; so does this
+restatement, and the NaN point then goes to the solver like the reference's.  The reference module imports
 cv2/mathutils and cannot be imported here, so this restatement is pinned by the known-answer
 cases in tests/test_ensemble.py only (parity unpinned against the reference code itself).
 """
@@ -66,7 +67,7 @@ def mean_and_filter(points):
     sd = np.sqrt(pairwise_sum((d - mu) ** 2) / len(d))
     keep = d < sd * 3
     if not keep.any():
-        return m                      # reference: mean of nothing -> NaN (see module docstring)
+        return np.full(2, np.nan, np.float32)    # np.mean of an empty selection (module docstring)
     return mean_rows_f32(p[keep])
 
 

@@ -102,7 +102,10 @@ __global__ __launch_bounds__(64) void ensemble_fuse_kernel(EnsembleArgs a) {
             }
             ++j;
           }
-      if (nk > 0) { fx = kx / (float)nk; fy = ky / (float)nk; }   // all coincide: keep the mean
+      // np.mean of an empty selection (every distance >= 3 std, e.g. coinciding points with
+      // std 0) is NaN, like the reference: 0 / 0 here
+      fx = kx / (float)nk;
+      fy = ky / (float)nk;
     }
     outp[2 * i] = fx;
     outp[2 * i + 1] = fy;

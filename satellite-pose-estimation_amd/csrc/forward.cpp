@@ -12,6 +12,7 @@
 #include <functional>
 #include <map>
 #include <mutex>
+#include <tuple>
 
 #include "model_state.h"
 #include "spe_pnp.h"
@@ -424,24 +425,34 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   return 0;
 }
 
-// Device scratch of the criterion's per-image partial sums (grown on demand, kept; steady-state
-// calls allocate nothing -- a first call with a larger batch must happen outside graph capture)
-static double* crit_scratch(size_t n) {
+// Device scratch of the solver's RANSAC hypothesis records and the criterion's per-image partial
+// sums: one buffer per (device, stream, kind), grown on demand and kept for the process lifetime,
+// so steady-state calls allocate nothing (a first call with a larger batch allocates and must
+// therefore happen outside graph capture).  Keying by stream is what makes concurrent calls safe:
+// calls on one stream are ordered by the stream, calls on different streams never share records.
+// A stream handle that is destroyed while its work is pending and then reissued by the runtime
+// would inherit the buffer; callers keep solver streams alive for as long as they use them.
+static void* stream_scratch(hipStream_t stream, int kind, size_t bytes) {
   static std::mutex mu;
-  static std::map<int, std::pair<double*, size_t>> bufs;
+  static std::map<std::tuple<int, hipStream_t, int>, std::pair<void*, size_t>> bufs;
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess) return nullptr;
   std::lock_guard<std::mutex> g(mu);
-  auto& e = bufs[dev];
-  if (e.second < n) {
-    if (e.first) (void)hipFree(e.first);
+  auto& e = bufs[std::make_tuple(dev, stream, kind)];
+  if (e.second < bytes) {
+    // the old buffer may still be read by work queued on this stream: free it in stream order
+    if (e.first) {
+      if (hipStreamSynchronize(stream) != hipSuccess) return nullptr;
+      (void)hipFree(e.first);
+    }
     e.first = nullptr;
     e.second = 0;
-    if (hipMalloc((void**)&e.first, n * sizeof(double)) != hipSuccess) return nullptr;
-    e.second = n;
+    if (hipMalloc(&e.first, bytes) != hipSuccess) return nullptr;
+    e.second = bytes;
   }
   return e.first;
 }
+enum { SCRATCH_CRITERION = 0, SCRATCH_HYP = 1 };
 
 int spe_criterion(void* stream, const float* logits, const float* points, const int32_t* tgt_labels,
                   const float* tgt_points, int layers, int batch, int num_queries, int num_classes, int num_targets,
@@ -453,7 +464,7 @@ int spe_criterion(void* stream, const float* logits, const float* points, const 
   CritArgs a{logits, points, tgt_labels, tgt_points, layers, batch, num_queries, num_classes, num_targets,
              cost_class, cost_pts, eos_coef, num_points, match, nullptr, losses};
   if (batch > 0) {
-    a.partial = crit_scratch((size_t)layers * batch * 5);
+    a.partial = (double*)stream_scratch((hipStream_t)stream, SCRATCH_CRITERION, (size_t)layers * batch * 5 * sizeof(double));
     if (!a.partial) return fail(SPE_E_LAUNCH, "criterion scratch allocation failed");
   }
   CK(spe_launch_criterion(a, (hipStream_t)stream));
@@ -487,26 +498,6 @@ int spe_postprocess(void* stream, const float* logits, const float* points, cons
   return 0;
 }
 
-// Device scratch for the EPnP-RANSAC hypothesis records (sigma mode): one buffer per device,
-// grown on demand and kept for the process lifetime, so steady-state calls allocate nothing (a
-// first call with a larger batch allocates and must therefore happen outside graph capture).
-static HypRec* hyp_scratch(size_t n) {
-  static std::mutex mu;
-  static std::map<int, std::pair<HypRec*, size_t>> bufs;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> g(mu);
-  auto& e = bufs[dev];
-  if (e.second < n) {
-    if (e.first) (void)hipFree(e.first);
-    e.first = nullptr;
-    e.second = 0;
-    if (hipMalloc((void**)&e.first, n * sizeof(HypRec)) != hipSuccess) return nullptr;
-    e.second = n;
-  }
-  return e.first;
-}
-
 int spe_pnp_batch(void* stream, const float* points_px, const float* probs, const float* sigmas, int B, int Q, int C,
                   const double* K, const double* world, int mode, float repro, int ransac_iters, double confidence,
                   float* quat, double* tvec, double* rvec, int32_t* status, int32_t* n_corr, int32_t* corr_label,
@@ -523,7 +514,7 @@ int spe_pnp_batch(void* stream, const float* points_px, const float* probs, cons
   a.quat = quat; a.tvec = tvec; a.rvec = rvec; a.status = status; a.n_corr = n_corr;
   a.corr_label = corr_label; a.inlier_mask = inlier_mask;
   if (mode == SPE_PNP_EPNP_RANSAC_SIGMA && B > 0) {
-    a.hyp = hyp_scratch((size_t)B * ransac_iters);
+    a.hyp = (HypRec*)stream_scratch((hipStream_t)stream, SCRATCH_HYP, (size_t)B * ransac_iters * sizeof(HypRec));
     a.hyp_stride = ransac_iters;
     if (!a.hyp) return fail(SPE_E_LAUNCH, "hypothesis scratch allocation failed");
   }

@@ -425,7 +425,7 @@ __global__ __launch_bounds__(WAVE) void pnp_kernel(PnpArgs a) {
 }
 
 // SPEED score (REV/utils/speed_eval.py:245-262): q sign-normalised, s_t = |dt|/|t_gt|,
-// s_q = 2 acos(min(|q.q_gt|, 1)); failures arrive as zero poses (REV/datasets/speed.py:355-363).
+// s_q = 2 acos(min(|q.q_gt|, 1)), NaN poses score NaN as on the host; failures arrive as zero poses (REV/datasets/speed.py:355-363).
 __global__ void score_kernel(const float* __restrict__ quat, const double* __restrict__ tvec,
                              const double* __restrict__ q_gt, const double* __restrict__ t_gt, int B,
                              double* __restrict__ s_t, double* __restrict__ s_q) {
@@ -442,7 +442,8 @@ __global__ void score_kernel(const float* __restrict__ quat, const double* __res
   }
   s_t[b] = sqrt(dn) / sqrt(gn);
   const double d = fabs(qp[0] * qg[0] + qp[1] * qg[1] + qp[2] * qg[2] + qp[3] * qg[3]);
-  s_q[b] = 2 * acos(d < 1 ? d : 1);
+  // Python's min(d, 1) keeps its first argument unless 1 < d, so a NaN dot product stays NaN
+  s_q[b] = 2 * acos(1 < d ? 1.0 : d);
 }
 
 // Self-assessment filter (BASELINE config 4).  The reference has no code for it: the UNC README

@@ -41,8 +41,7 @@ class DETR(nn.Module):
         self.attn_dtype = attn_dtype or dtype
         self._pending = {}
         self._handle = None
-        self._ws = None
-        self._ws_batch = 0
+        self._ws = {}          # (device, stream) -> (workspace, batch it was sized for)
         L = _lib.lib()
         c = _lib.ModelConfig(cfg.input_size, cfg.num_queries, cfg.enc_layers, cfg.dec_layers, cfg.hidden_dim,
                              cfg.nheads, cfg.dim_feedforward, int(cfg.sigma_head),
@@ -83,12 +82,20 @@ class DETR(nn.Module):
             _lib.check(_lib.lib().spe_model_finalize(self._h), "spe_model_finalize")
             self._handle = self._h
 
-    def workspace(self, B, device):
-        if self._ws is None or self._ws_batch < B:
+    def workspace(self, B, device, stream=None):
+        """The default workspace of forward() on `stream` (the current stream if None): one per
+        (device, stream), so forwards issued on different streams never share intermediates;
+        forwards on one stream are ordered by it.  Allocated from torch's caching allocator on
+        that stream, so a regrown workspace's old block is only reused in stream order."""
+        device = torch.device(device)
+        s = stream if stream is not None else torch.cuda.current_stream(device)
+        key = (device.index if device.index is not None else torch.cuda.current_device(), s.cuda_stream)
+        ws = self._ws.get(key)
+        if ws is None or ws[1] < B:
             nbytes = _lib.lib().spe_model_workspace_bytes(self._h, B)
-            self._ws = torch.empty(int(nbytes), dtype=torch.uint8, device=device)
-            self._ws_batch = B
-        return self._ws
+            with torch.cuda.stream(s):
+                self._ws[key] = ws = (torch.empty(int(nbytes), dtype=torch.uint8, device=device), B)
+        return ws[0]
 
     def new_workspace(self, B, device):
         """A separate workspace for another in-flight batch (encode/decode overlap)."""
@@ -153,7 +160,7 @@ class DETR(nn.Module):
         if clip_bbox is not None:
             clip_bbox = clip_bbox.to(device=dev, dtype=torch.float32).contiguous()
         out, o = self._outputs(B, dev, clip_bbox, return_hs)
-        ws = self.workspace(B, dev)
+        ws = self.workspace(B, dev, stream)
         _lib.check(_lib.lib().spe_forward(self._h, _lib.stream_ptr(stream), _lib.ptr(images), B, _lib.ptr(ws),
                                           ws.numel(), ctypes.byref(o)), "spe_forward")
         return out

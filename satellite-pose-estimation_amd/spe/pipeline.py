@@ -39,10 +39,13 @@ class PosePipeline:
         self.t_gt = torch.zeros(batch, 3, dtype=torch.float64, device=dev)
         self.q_gt[:, 0] = 1
         self.t_gt[:, 2] = 10
-        model.workspace(batch, dev)
+        if not overlap_decode:
+            model.workspace(batch, dev)           # sized outside any graph capture
         if self.overlap_decode:
             self.dec_stream = torch.cuda.Stream(device=device)
-            self.ws2 = [model.workspace(batch, dev), model.new_workspace(batch, dev)]
+            # the staged slots own their workspaces: a direct model(...) call or another
+            # pipeline on the same model never writes into a slot's encoder memory
+            self.ws2 = [model.new_workspace(batch, dev), model.new_workspace(batch, dev)]
             # per-slot snapshots of what the later stages read (a load() for the next batch may
             # overwrite the staging buffers while this batch's decoder / solver still run)
             self.slot_clip = [torch.zeros(batch, 4, device=dev) for _ in range(2)]

@@ -115,6 +115,30 @@ def test_solver_matches_oracle(gpu_device, mode):
     assert np.all(h["quat"][~ok] == 0) and np.all(h["tvec"][~ok] == 0)
 
 
+def test_sigma_solves_on_concurrent_streams(gpu_device):
+    """Two sigma-mode (EPnP-RANSAC hypothesis records in device scratch) solves of different
+    batches issued back to back on two streams, interleaved over several rounds: the scratch is
+    per (device, stream), so each result equals the same batch solved alone."""
+    from spe.solver import PoseSolver
+    dev = gpu_device
+    sets = [solver_stress_set(512, seed=s) for s in (21, 22)]
+    alone = [_solve(2, p, r, g, 25.0) for p, r, _, _, g in sets]
+    s = PoseSolver(mode=2, repro=25.0)
+    ins = [tuple(torch.from_numpy(a).to(dev) for a in (p, r, g)) for p, r, _, _, g in sets]
+    streams = [torch.cuda.Stream(device=dev) for _ in range(2)]
+    torch.cuda.synchronize()
+    outs = []
+    for _ in range(4):
+        for (p, r, g), st in zip(ins, streams):
+            with torch.cuda.stream(st):
+                outs.append(s.solve_batch(p, r, g, stream=st))
+    torch.cuda.synchronize()
+    for i, o in enumerate(outs):
+        ref = alone[i % 2]
+        for k in ("status", "n_corr", "corr_label", "inlier_mask", "quat", "tvec"):
+            np.testing.assert_array_equal(o[k].cpu().numpy(), ref[k], err_msg=f"{k} call {i}")
+
+
 @pytest.mark.parametrize("sigma_th,score_th,min_inl", [(5.0, 0.5, 4), (10.0, 0.3, 4), (12.0, 0.0, 6)])
 def test_self_assessment_matches_oracle(gpu_device, sigma_th, score_th, min_inl):
     """Config-4 self-assessment filter (definition unpinned: include/spe.h spe_self_assess) on
@@ -165,9 +189,20 @@ def test_speed_score_kernel(gpu_device):
     t[:8] = 0
     qg = rng.normal(size=(B, 4)); qg /= np.linalg.norm(qg, axis=1, keepdims=True)
     tg = rng.normal(size=(B, 3)) + [0, 0, 10]
+    # NaN poses (the solver reproduces OpenCV's NaN P3P root): the host min(|dot|, 1) keeps NaN
+    q[8] = np.nan
+    q[9, 2] = np.nan
+    t[10, 1] = np.nan
     d = gpu_device
     s_t, s_q = device_speed_score(torch.from_numpy(q).to(d), torch.from_numpy(t).to(d), torch.from_numpy(qg).to(d),
                                   torch.from_numpy(tg).to(d))
+    from spe.speed_eval import speed_score
     for i in range(B):
-        a, b = pnp_ref.speed_score(q[i].astype(np.float64), t[i], qg[i], tg[i])
-        assert abs(s_t[i].item() - a) < 1e-12 and abs(s_q[i].item() - b) < 1e-9
+        for a, b in (pnp_ref.speed_score(q[i].astype(np.float64), t[i], qg[i], tg[i]),
+                     speed_score(q[i], t[i], qg[i], tg[i])):
+            assert np.isnan(s_t[i].item()) == np.isnan(a) and np.isnan(s_q[i].item()) == np.isnan(b), i
+            if not np.isnan(a):
+                assert abs(s_t[i].item() - a) < 1e-12
+            if not np.isnan(b):
+                assert abs(s_q[i].item() - b) < 1e-9
+    assert np.isnan(s_q[8].item()) and np.isnan(s_q[9].item()) and np.isnan(s_t[10].item())
