@@ -18,8 +18,11 @@
 // head_dim 32 makes the softmax the bottleneck (one exp per 128 MFMA flops), so the bf16 path
 // spends as little VALU per score as possible: Q is pre-scaled by softmax_scale*log2(e) (scores
 // come out in the exp2 domain), the running max only triggers an O/l rescale when some lane's
-// max actually grew (wave-uniform branch), and the row sums l are accumulated by the matrix
-// pipe (ones . P^T MFMA, which also normalises with exactly the bf16 P the numerator uses).
+// max actually grew (wave-uniform branch), and the row sums l are f32 adds of p (each lane sums
+// its 32 keys, the lane pair is combined once at the end).  The chip runs this loop at its
+// power limit (~1.75-1.8 GHz), so what pays is energy per tile, not issue slots: a ones . P^T
+// MFMA for the sums (4 of 12 MFMAs) cost more than the 35 VALU adds that replace it
+// (scripts/lab/attn_lab.hip: 0.86 -> 0.81 ms at B = 64 on random inputs).
 // bf16: v_mfma_f32_32x32x16_bf16; fp16 operands (config 5): v_mfma_f32_32x32x16_f16 (same
 // kernel, AT<f16> traits).  fp32 (parity mode): v_mfma_f32_32x32x2_f32, exact f32.
 #include "spe_common.h"
@@ -33,7 +36,7 @@ constexpr float LOG2E = 1.4426950408889634f;
 constexpr float NEG_BIG = -1.0e30f;    // finite "minus infinity" (exp2 of it underflows to 0)
 constexpr float RESCALE_SLACK = 8.0f;  // log2 units (bf16 path)
 #ifndef SPE_ATTN_OCC
-#define SPE_ATTN_OCC 3
+#define SPE_ATTN_OCC 4
 #endif
 
 // ---------------------------------------------------------------- bf16 LDS image
@@ -160,13 +163,11 @@ SPE_DEV float tile_max(f32x16& s0, f32x16& s1, int key_base, int Tk, int hh) {
 template <typename TI> struct AT;
 template <> struct AT<bf16> {
   typedef bf16x8 v8;
-  static constexpr uint32_t ONE2 = 0x3F803F80u;
   static SPE_DEV uint32_t pk(float a, float b) { return pack_bf16x2(a, b); }
   static SPE_DEV f32x16 mfma(v8 a, v8 b, f32x16 c) { return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0); }
 };
 template <> struct AT<f16> {
   typedef f16x8 v8;
-  static constexpr uint32_t ONE2 = 0x3C003C00u;
   static SPE_DEV uint32_t pk(float a, float b) { return __builtin_bit_cast(uint32_t, __builtin_amdgcn_cvt_pkrtz(a, b)); }
   static SPE_DEV f32x16 mfma(v8 a, v8 b, f32x16 c) { return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0); }
 };
@@ -203,17 +204,14 @@ __global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn16_kernel(AttnArgs a) {
       qf[i] = __builtin_bit_cast(v8, pack16<TI>(f));
     }
   }
-  u32x4 ones_u{A::ONE2, A::ONE2, A::ONE2, A::ONE2};
-  asm volatile("" : "+v"(ones_u));      // keep in VGPRs (else rematerialised from SGPRs per use)
-  const v8 ones = __builtin_bit_cast(v8, ones_u);
-
-  // o: O^T accumulator; ls: running row sum (ones . P^T, every element equal), rescaled with o.
-  f32x16 o, ls;
+  // o: O^T accumulator; ls: this lane's running sum of p over its half of the keys.
+  f32x16 o;
+  float ls = 0.f;
   // negm: -m in every element, the accumulator the score MFMAs start from, so the scores come
   // out already shifted by the running max (s - m) and p = exp2 of them costs no subtract.
   f32x16 negm;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) { o[r] = 0.f; ls[r] = 0.f; negm[r] = 0.f; }
+  for (int r = 0; r < 16; ++r) { o[r] = 0.f; negm[r] = 0.f; }
   float m = 0.f;                        // set from the first tile (forced rescale at kt == 0)
 
   // Two-slot LDS ring, one barrier per 64-key step: tile kt+1 travels global -> registers
@@ -269,7 +267,8 @@ __global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn16_kernel(AttnArgs a) {
         if (kt != 0) {
           const float alpha = __builtin_amdgcn_exp2f(-d);
 #pragma unroll
-          for (int r = 0; r < 16; ++r) { o[r] *= alpha; ls[r] *= alpha; }
+          for (int r = 0; r < 16; ++r) o[r] *= alpha;
+          ls *= alpha;
         }
         m += d;
 #pragma unroll
@@ -285,6 +284,14 @@ __global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn16_kernel(AttnArgs a) {
         s1[r] = __builtin_amdgcn_exp2f(s1[r]);
 #endif
       }
+#ifndef SPE_X_NOLS
+      {
+        float t0 = 0.f, t1 = 0.f, t2 = 0.f, t3 = 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; r += 2) { t0 += s0[r]; t1 += s0[r + 1]; t2 += s1[r]; t3 += s1[r + 1]; }
+        ls += (t0 + t1) + (t2 + t3);
+      }
+#endif
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub) {
         const f32x16& p = sub ? s1 : s0;
@@ -294,9 +301,6 @@ __global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn16_kernel(AttnArgs a) {
                    A::pk(p[8 * ks + 4], p[8 * ks + 5]), A::pk(p[8 * ks + 6], p[8 * ks + 7])};
           const v8 pb = __builtin_bit_cast(v8, pw);
           o = A::mfma(__builtin_bit_cast(v8, vf[sub][ks]), pb, o);
-#ifndef SPE_X_NOLS
-          ls = A::mfma(ones, pb, ls);   // column sums of P^T
-#endif
         }
       }
     }
@@ -311,7 +315,7 @@ __global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn16_kernel(AttnArgs a) {
   }
 
   if (!wave_live || q >= a.Tq) return;
-  const float inv = 1.f / ls[0];        // ls sums all 64 keys of every tile
+  const float inv = 1.f / (ls + __shfl_xor(ls, 32, 64));   // the lane pair's two key halves
   bf16* op = (bf16*)a.o + (size_t)(b * a.Tq + q) * a.ldo + h * 32;
 #pragma unroll
   for (int g = 0; g < 4; ++g) {
