@@ -18,7 +18,7 @@
 extern "C" {
 #endif
 
-#define SPE_ABI_VERSION 3
+#define SPE_ABI_VERSION 4
 
 enum {
   SPE_E_ARG = -1,        /* bad argument / size */
@@ -80,6 +80,47 @@ typedef struct {
   float* aux_logits;      /* [dec_layers-1,B,Q,12] aux outputs (nullable; aux_loss=True, */
   float* aux_points;      /* [dec_layers-1,B,Q,2]   REV/models/detr_speed.py:88-99)       */
 } spe_forward_outputs;
+
+/* UNC RT-DETR keypoint model with the sigma head: RTDETR(PResNet-vd, HybridEncoder,
+ * RTDETRTransformer) (UNC/src/zoo/rtdetr/rtdetr.py:20-38, UNC/nn/backbone/presnet.py:156-265,
+ * UNC/src/zoo/rtdetr/hybrid_encoder.py:196-401, UNC/src/zoo/rtdetr/rtdetr_decoder.py:372-710) as
+ * the speed configs build it (UNC/configs/rtdetr_speed/rtdetr_r{18,50}vd_6x_speed_kl_*.yml). */
+typedef struct {
+  int depth;            /* PResNet depth, variant d: 18 (BasicBlock) or 50 (BottleNeck) */
+  int input_size;       /* eval_spatial_size (256); multiple of 32 */
+  int num_queries;      /* RTDETRTransformer.num_queries (30), <= 64 */
+  int dec_layers;       /* num_decoder_layers (3) */
+  int enc_ff;           /* HybridEncoder.dim_feedforward (1024, GELU) */
+  int dec_ff;           /* RTDETRTransformer.dim_feedforward (1024, ReLU) */
+  int csp_hidden;       /* CSPRepLayer hidden channels = 256 * expansion (128 for expansion 0.5) */
+  int num_classes;      /* 11 (+1 no-object logit) */
+  int dtype;            /* SPE_DTYPE_BF16_ or SPE_DTYPE_F32_ */
+} spe_rtdetr_config;
+
+typedef struct {
+  float* logits;          /* [B,Q,C+1] pred_logits of the last decoder layer (required) */
+  float* points;          /* [B,Q,2]   pred_pts, refined reference points, crop-normalised (required) */
+  float* log_sigmas;      /* [B,Q,2]   pred_sigmas (raw sigma head, repeated to 2) (nullable) */
+  const float* clip_bbox; /* [B,4] (nullable) -> fused RTDETRPostProcessor: */
+  float* probs;           /*   [B,Q,C+1] softmax (rtdetr_postprocessor.py:44-76) */
+  float* points_px;       /*   [B,Q,2] image pixels */
+  float* sigmas;          /*   [B,Q,2] exp(pred_sigmas) */
+  float* aux_logits;      /* [L-1,B,Q,C+1] earlier decoder layers (nullable; aux_outputs) */
+  float* aux_points;      /* [L-1,B,Q,2] */
+  float* aux_log_sigmas;  /* [L-1,B,Q,2] */
+  float* enc_logits;      /* [B,Q,C+1] encoder top-k logits (nullable; last aux_outputs entry) */
+  float* enc_points;      /* [B,Q,2]   sigmoid(enc_bbox_head + anchors) of the selected tokens */
+  int32_t* topk;          /* [B,Q] selected encoder tokens, descending score (nullable) */
+} spe_rtdetr_outputs;
+
+/* Create an RT-DETR model handle.  The lifecycle entry points of spe_model (set_param with the
+ * reference's state_dict keys, num_params / param_name, finalize, workspace_bytes, destroy,
+ * profile_*) apply to it unchanged; BatchNorm2d num_batches_tracked buffers are not parameters. */
+int spe_rtdetr_create(const spe_rtdetr_config* cfg, spe_model** out);
+/* RTDETR.forward in eval (+ RTDETRPostProcessor when clip_bbox is given).  images: device
+ * [B,3,S,S] fp32, ImageNet-normalised (UNC/src/data/speed/speed_dataset.py:40-66). */
+int spe_rtdetr_forward(spe_model* m, void* stream, const float* images, int batch, void* workspace,
+                       int64_t workspace_bytes, const spe_rtdetr_outputs* out);
 
 int spe_abi_version(void);
 const char* spe_last_error(void);
@@ -181,7 +222,8 @@ int spe_model_profile_get(const spe_model* m, int i, char* kind, int kind_len, d
                           double* bytes);
 
 /* Kernel test hooks: launch one kernel family on caller buffers (tests/test_gpu_kernels.py).
- * gemm: C[M,N] = A . W^T (+bias, +R, ReLU) with mode 0 linear (A[m*lda+k]), 1 linear + P[(m%prow)
+ * gemm: C[M,N] = act(A . W^T + bias + R) with act = act_code & 255 (0 none, 1 ReLU, 2 SiLU, 3
+ * exact GELU); bit 8 of act_code adds R after the activation instead; mode 0 linear (A[m*lda+k]), 1 linear + P[(m%prow)
  * *ldp+k] added to A, 2 implicit-GEMM conv over NHWC A [*,H,W,Cin]; W is [N][ldb] (ldb % 64 == 0);
  * vt_T > 0 stores head-transposed C[((n/256)*vt_B + m/vt_T)*256 + n%256][m%vt_T]; r_period > 0
  * reads the residual row-periodically, R[(m % r_period)*ldr + n].  bf16 problems that fill the chip
@@ -189,7 +231,7 @@ int spe_model_profile_get(const spe_model* m, int i, char* kind, int kind_len, d
  * attention: per (b,h) softmax(scale Q K^T) V with Q/K rows b*T+i at column h*32, V^T [B][H][32][Tk]. */
 int spe_debug_gemm(void* stream, int dtype, int mode, const void* A, int lda, const void* P, int ldp, int prow, int H,
                    int W, int Cin, int KH, int KW, int stride, int pad, const void* Bw, int ldb, int M, int N, int K,
-                   const float* bias, const void* R, int ldr, int relu, void* C, int ldc, int out_f32, int vt_T,
+                   const float* bias, const void* R, int ldr, int act_code, void* C, int ldc, int out_f32, int vt_T,
                    int vt_B, int r_period, const float* ln_g, const float* ln_b, int out_f16);
 /* (out_f16: bf16 launches store fp16 instead of bf16.  ln_g/ln_b non-null: post-norm LayerNorm over each output row fused into the epilogue; bf16,
  * N == 256 and enough rows for the large-tile kernel, else SPE_E_LAUNCH) */

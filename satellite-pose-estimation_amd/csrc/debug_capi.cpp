@@ -11,7 +11,7 @@ extern "C" {
 
 int spe_debug_gemm(void* stream, int dtype, int mode, const void* A, int lda, const void* P, int ldp, int prow,
                    int H, int W, int Cin, int KH, int KW, int stride, int pad, const void* Bw, int ldb, int M, int N,
-                   int K, const float* bias, const void* R, int ldr, int relu, void* C, int ldc, int out_f32, int vt_T,
+                   int K, const float* bias, const void* R, int ldr, int act_code, void* C, int ldc, int out_f32, int vt_T,
                    int vt_B, int r_period, const float* ln_g, const float* ln_b, int out_f16) {
   GemmArgs g{};
   g.A = A; g.lda = lda; g.P = P; g.ldp = ldp; g.prow = prow;
@@ -19,7 +19,7 @@ int spe_debug_gemm(void* stream, int dtype, int mode, const void* A, int lda, co
   g.Ho = mode == GEMM_CONV ? (H + 2 * pad - KH) / stride + 1 : 0;
   g.Wo = mode == GEMM_CONV ? (W + 2 * pad - KW) / stride + 1 : 0;
   g.B = Bw; g.ldb = ldb; g.M = M; g.N = N; g.K = K;
-  g.bias = bias; g.R = R; g.ldr = ldr; g.relu = relu; g.C = C; g.ldc = ldc; g.out_f32 = out_f32;
+  g.bias = bias; g.R = R; g.ldr = ldr; g.act = act_code & 255; g.res_post = (act_code >> 8) & 1; g.C = C; g.ldc = ldc; g.out_f32 = out_f32;
   g.vt_T = vt_T; g.vt_B = vt_B;
   g.r_period = r_period;
   g.ln_g = ln_g; g.ln_b = ln_b;

@@ -16,6 +16,7 @@
 
 #include "model_state.h"
 #include "spe_pnp.h"
+#include "launch.h"
 
 #define fail spe_fail
 
@@ -35,6 +36,9 @@ bool prof_match(const spe_model* m, const char* kind) {
   return m->prof.on && std::strncmp(kind, m->prof.filter.c_str(), m->prof.filter.size()) == 0;
 }
 
+}  // namespace
+
+// ---- launch helpers shared with rtdetr.cpp (launch.h)
 int run_other(spe_model* m, const char* kind, double flops, double bytes, hipStream_t s, const std::function<int()>& fn) {
   if (!prof_match(m, kind)) return fn();
   ProfRecord r{kind, kind, flops, bytes, next_event(m), next_event(m)};
@@ -74,8 +78,7 @@ GemmArgs linear_args(const Conv& c, const void* A, int lda, int M, void* C, int 
 
 // Fused linear1 -> ReLU -> linear2 -> +residual -> LayerNorm over x (in place), bf16 models.
 int run_ffn(spe_model* m, const char* kind, const Conv& l1, const Conv& l2, const float* g, const float* b,
-            void* x, int M, hipStream_t s, const void* pos = nullptr, void* ypos = nullptr, int period = 0,
-            float* partial = nullptr) {
+            void* x, int M, hipStream_t s, const void* pos, void* ypos, int period, float* partial) {
   FfnArgs a{};
   a.pos = pos; a.ypos = ypos; a.pos_period = period;
   a.splits = partial ? spe_ffn_splits(M, l1.N) : 1;
@@ -90,6 +93,8 @@ int run_ffn(spe_model* m, const char* kind, const Conv& l1, const Conv& l2, cons
   const double bytes = 2.0 * M * l1.K * m->esz + 2.0 * (double)l1.K * l1.N * m->esz;
   return run_other(m, kind, flops, bytes, s, [&] { return spe_launch_ffn_ln(a, s); });
 }
+
+namespace {
 
 bool use_fused_ffn(const spe_model* m) {
   return m->cfg.dtype == SPE_DTYPE_BF16 && m->cfg.hidden_dim == 256 && m->cfg.dim_feedforward % 32 == 0;
@@ -106,6 +111,8 @@ int add_pos(const spe_model* m, GemmArgs& g, const void* pos, int ldp, int perio
   return GEMM_LINEAR_ADD;
 }
 
+}  // namespace
+
 GemmArgs conv_args(const Conv& c, const void* X, int B, int H, int W, void* Y, int ldc) {
   GemmArgs g{};
   g.A = X;
@@ -119,6 +126,7 @@ GemmArgs conv_args(const Conv& c, const void* X, int B, int H, int W, void* Y, i
   return g;
 }
 
+namespace {
 #define CK(x)                                                                   \
   do {                                                                          \
     int _r = (x);                                                               \
@@ -165,7 +173,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   CK(run_other(m, "eltwise.pack", 0.0, (double)B * S * S * (12 + 8 * m->esz), s, [&] { return spe_launch_pack_input(images, P(w.x0), B, S, dt, s); }));
   {
     GemmArgs g = conv_args(m->stem, P(w.x0), B, S, S, P(w.stem), 64);
-    g.relu = 1;
+    g.act = ACT_RELU;
     CK(run_gemm(m, "conv.stem", g, GEMM_CONV, s));
   }
   int H = S / 2;
@@ -181,12 +189,12 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
     const int Ho = (H + 2 - 3) / blk.stride + 1;
     {  // conv1 1x1 + bn1 + relu
       GemmArgs g = linear_args(blk.c1, P(cur), cin, B * H * H, P(w.t1), blk.c1.N);
-      g.relu = 1;
+      g.act = ACT_RELU;
       CK(run_gemm(m, "conv.1x1", g, GEMM_LINEAR, s));
     }
     {  // conv2 3x3 (stride on the 3x3, ResNet v1.5) + bn2 + relu
       GemmArgs g = conv_args(blk.c2, P(w.t1), B, H, H, P(w.t2), blk.c2.N);
-      g.relu = 1;
+      g.act = ACT_RELU;
       CK(run_gemm(m, "conv.3x3", g, GEMM_CONV, s));
     }
     size_t res = cur;
@@ -202,7 +210,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
     }
     {  // conv3 1x1 + bn3 + residual + relu
       GemmArgs g = linear_args(blk.c3, P(w.t2), blk.c2.N, B * Ho * Ho, P(outbuf), blk.c3.N);
-      g.R = P(res); g.ldr = blk.c3.N; g.relu = 1;
+      g.R = P(res); g.ldr = blk.c3.N; g.act = ACT_RELU;
       CK(run_gemm(m, "conv.1x1", g, GEMM_LINEAR, s));
     }
     cin = blk.c3.N;
@@ -276,7 +284,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
     } else {
       {
         GemmArgs g = linear_args(e.l1, P(w.src), d, Mt, P(w.ffn), ff);
-        g.relu = 1;
+        g.act = ACT_RELU;
         CK(run_gemm(m, "gemm.enc.ffn1", g, GEMM_LINEAR, s));
       }
       {
@@ -385,7 +393,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
     } else {
       {
         GemmArgs g = linear_args(e.l1, P(w.tgt), d, Mq, P(w.dffn), ff);
-        g.relu = 1;
+        g.act = ACT_RELU;
         CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR, s));
       }
       {

@@ -251,7 +251,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs g) {
     float v[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = ct[rr * EPI_LD + cg + e] + bv[e];
-    if (g.R) {                                     // residual, or row-periodic add (pos . W^T)
+    auto add_res = [&]() {                         // residual, or row-periodic add (pos . W^T)
       const T* rp = (const T*)g.R + (size_t)(g.r_period > 0 ? m % g.r_period : m) * g.ldr + n;
       if (full) {
         float f[8];
@@ -262,11 +262,13 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs g) {
       } else {
         for (int e = 0; e < 8 && n + e < g.N; ++e) v[e] += to_f32(rp[e]);
       }
-    }
-    if (g.relu) {
+    };
+    if (g.R && !g.res_post) add_res();
+    if (g.act) {
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+      for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], g.act);
     }
+    if (g.R && g.res_post) add_res();
     if (g.out_f32) {
       float* cp = (float*)g.C + (size_t)m * g.ldc + n;
       if (full) {

@@ -405,7 +405,7 @@ __global__ __launch_bounds__(NT, NST == 1 ? 4 : 1) void gemm2_kernel(GemmArgs g)
         float v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bv[r];
-        if (g.R) {
+        auto add_res = [&]() {
           if (full) {
             v[0] += __uint_as_float(dres[i][j].x << 16);
             v[1] += __uint_as_float(dres[i][j].x & 0xffff0000u);
@@ -415,11 +415,13 @@ __global__ __launch_bounds__(NT, NST == 1 ? 4 : 1) void gemm2_kernel(GemmArgs g)
             const bf16* rp = (const bf16*)g.R + (size_t)(g.r_period > 0 ? m % g.r_period : m) * g.ldr + n;
             for (int r = 0; r < 4 && n + r < g.N; ++r) v[r] += to_f32(rp[r]);
           }
-        }
-        if (g.relu) {
+        };
+        if (g.R && !g.res_post) add_res();
+        if (g.act) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+          for (int r = 0; r < 4; ++r) v[r] = apply_act(v[r], g.act);
         }
+        if (g.R && g.res_post) add_res();
         if (g.out_f32) {
           float* cp = (float*)g.C + (size_t)m * g.ldc + n;
           if (full) st16(cp, pack16<float>(v));
@@ -485,7 +487,7 @@ __global__ __launch_bounds__(NT, NST == 1 ? 4 : 1) void gemm2_kernel(GemmArgs g)
           float v[8];
 #pragma unroll
           for (int e = 0; e < 8; ++e) v[e] = ct[rr * EPI_LD + cg + e] + bv[e];
-          if (g.R) {
+          auto add_res = [&]() {
             if (full) {
               float f[8];
               unpack16<bf16>(rres[pass][q], f);
@@ -495,7 +497,8 @@ __global__ __launch_bounds__(NT, NST == 1 ? 4 : 1) void gemm2_kernel(GemmArgs g)
               const bf16* rp = (const bf16*)g.R + (size_t)(g.r_period > 0 ? m % g.r_period : m) * g.ldr + n;
               for (int e = 0; e < 8 && n + e < g.N; ++e) v[e] += to_f32(rp[e]);
             }
-          }
+          };
+          if (g.R && !g.res_post) add_res();
           if constexpr (LN) {
             // fused post-norm LayerNorm (N == BN == 256): a row's 32 column groups are the 32
             // lanes of one half-wave, so the row statistics are five xor-shuffles away
@@ -514,10 +517,11 @@ __global__ __launch_bounds__(NT, NST == 1 ? 4 : 1) void gemm2_kernel(GemmArgs g)
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = (v[e] - mean) * rs * elg[e] + elb[e];
           }
-          if (g.relu) {
+          if (g.act) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
+            for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], g.act);
           }
+          if (g.R && g.res_post) add_res();
           if (g.out_f32) {
             float* cp = (float*)g.C + (size_t)m * g.ldc + n;
             if (full) {
@@ -692,7 +696,7 @@ __global__ __launch_bounds__(SM_NT) void gemm_small_kernel(GemmArgs g) {
         float v[4];
 #pragma unroll
         for (int r = 0; r < 4; ++r) v[r] = acc[i][j][r] + bias[j][r];
-        if (g.R) {
+        auto add_res = [&]() {
           if (full) {
             v[0] += __uint_as_float(res[i][j].x << 16);
             v[1] += __uint_as_float(res[i][j].x & 0xffff0000u);
@@ -702,9 +706,11 @@ __global__ __launch_bounds__(SM_NT) void gemm_small_kernel(GemmArgs g) {
             const bf16* rp = (const bf16*)g.R + (size_t)(g.r_period > 0 ? m % g.r_period : m) * g.ldr + n;
             for (int r = 0; r < 4 && n + r < g.N; ++r) v[r] += to_f32(rp[r]);
           }
-        }
-        if (g.relu)
-          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
+        };
+        if (g.R && !g.res_post) add_res();
+        if (g.act)
+          for (int r = 0; r < 4; ++r) v[r] = apply_act(v[r], g.act);
+        if (g.R && g.res_post) add_res();
         if (g.out_f32) {
           float* cp = (float*)g.C + (size_t)m * g.ldc + n;
           if (full) st16(cp, pack16<float>(v));

@@ -62,7 +62,45 @@ struct Profiler {
   size_t next_event = 0;
 };
 
+// ---- UNC RT-DETR (rtdetr_model.cpp)
+struct RtBlock {             // PResNet BasicBlock / BottleNeck; shortcut conv (first block of a stage)
+  Conv a, b, c, sc;          // variant d stride-2 shortcut: AvgPool2d(2, 2) + 1x1 folded into a 2x2/2 conv
+  bool has_sc = false, bottleneck = false;
+  int stride = 1, cin = 0, cout = 0;
+};
+struct RtCsp {               // CSPRepLayer, one RepVggBlock folded into one 3x3 conv (convert_to_deploy)
+  Conv c1, c2, rep, c3;
+  bool has_c3 = false;
+};
+struct RtDec {               // decoder layer + its score / box / sigma heads
+  Conv sqk, sv, so, soaw, oproj, l1, l2;   // soaw: sampling_offsets | attention_weights (N = 288)
+  float *n1g, *n1b, *n2g, *n2b, *n3g, *n3b;
+  HeadArgs head{};
+};
+struct RtModel {
+  spe_rtdetr_config cfg{};
+  int L = 0, lvl_s[3] = {0, 0, 0}, lvl_start[4] = {0, 0, 0, 0};
+  Conv stem[3];
+  std::vector<RtBlock> blocks;
+  int stage_first[4] = {0, 0, 0, 0}, stage_n[4] = {0, 0, 0, 0};
+  Conv in_proj[3];
+  Conv aqk, av, ao, al1, al2;          // AIFI encoder layer
+  float *an1g, *an1b, *an2g, *an2b;
+  void* aifi_pos = nullptr;             // [s2*s2][256] T, 2D sin-cos table
+  Conv lateral[2];
+  RtCsp fpn[2], pan[2];
+  Conv dec_in[3], enc_out, enc_score, vproj;   // vproj: every layer's value_proj, N = 256 * dec_layers
+  float *eo_g, *eo_b;
+  float* anchors = nullptr;             // [L][2] fp32, logit domain
+  HeadArgs enc_head{};                  // enc_bbox_head (+ anchors, sigmoid): the initial reference points
+  float *qp_w0 = nullptr, *qp_b0 = nullptr;   // query_pos_head layer 0 [512][2], [512]
+  Conv qp_l1;
+  std::vector<RtDec> dec;
+};
+
 struct spe_model {
+  int family = 0;            // 0: DETR (REV), 1: RT-DETR (UNC)
+  RtModel* rt = nullptr;
   spe_model_config cfg{};
   int esz = 2;
   std::vector<std::pair<std::string, std::vector<int64_t>>> spec;
@@ -84,6 +122,9 @@ struct spe_model {
 };
 
 int spe_fail(int code, const std::string& msg);
+// RT-DETR runtime hooks (rtdetr_model.cpp)
+int spe_rtdetr_build_device(spe_model* m);
+int64_t spe_rtdetr_workspace(const spe_model* m, int B);
 
 // bf16 models take the decoder cross-attention against the memory itself (xattn.hip) when the
 // last encoder layer can emit memory + pos (fused FFN)

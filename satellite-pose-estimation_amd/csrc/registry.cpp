@@ -10,10 +10,11 @@
 #include <cstring>
 
 #include "model_state.h"
+#include "registry.h"
 
 namespace {
-
 thread_local std::string g_err;
+}  // namespace
 
 uint16_t f2bf(float f) {
   uint32_t u;
@@ -22,8 +23,6 @@ uint16_t f2bf(float f) {
   u += 0x7fffu + ((u >> 16) & 1u);
   return (uint16_t)(u >> 16);
 }
-
-}  // namespace
 
 int spe_fail(int code, const std::string& msg) {
   g_err = msg;
@@ -92,6 +91,9 @@ std::vector<std::pair<std::string, std::vector<int64_t>>> build_spec(const spe_m
   return s;
 }
 
+}  // namespace
+
+// ---- packing helpers shared with the RT-DETR runtime (registry.h)
 void* dalloc(spe_model* m, size_t bytes) {
   size_t off = (m->dused + 255) & ~size_t(255);
   m->dused = off + bytes;
@@ -136,13 +138,43 @@ void* upload_T(spe_model* m, const std::vector<float>& v) {
 
 int pad64(int k) { return (k + 63) / 64 * 64; }
 
-// conv weight [Cout][Cin][KH][KW] (+FrozenBN) -> [Cout][KH][KW][Cin_pad] rows, folded bias
-Conv make_conv(spe_model* m, const std::string& wkey, const std::string& bnkey, const std::string& biaskey, int cin_pad,
-               int stride, int pad) {
-  const auto& spec_w = m->host[wkey];
-  int64_t cout = 0, cin = 0, kh = 0, kw = 0;
+// folded conv weight [cout][cin][kh][kw] (host fp32) -> [Cout][KH][KW][Cin_pad] rows in the
+// kernels' K order (spe_kernels.h conv_k_decode), bias fp32
+Conv pack_conv(spe_model* m, const std::vector<float>& w, const std::vector<float>& bias, int cout, int cin, int kh,
+               int kw, int cin_pad, int stride, int pad) {
+  const int cp = cin_pad > 0 ? cin_pad : cin;
+  const int K = kh * kw * cp;
+  std::vector<float> rows((size_t)cout * K, 0.f);
+  const bool cblk = conv_channel_blocked(cp, kh * kw);
+  if (m->dmem)                                     // pass 1 only sizes the device block
+    for (int co = 0; co < cout; ++co)
+      for (int ci = 0; ci < cin; ++ci)
+        for (int y = 0; y < kh; ++y)
+          for (int x = 0; x < kw; ++x) {
+            const int tap = y * kw + x;
+            const int k = cblk ? ((ci / 64) * kh * kw + tap) * 64 + ci % 64 : tap * cp + ci;
+            rows[(size_t)co * K + k] = w[(((size_t)co * cin + ci) * kh + y) * kw + x];
+          }
+  Conv c;
+  c.N = cout; c.K = K; c.Kpad = pad64(K); c.Cin = cp; c.KH = kh; c.KW = kw; c.stride = stride; c.pad = pad;
+  c.w = upload_rows(m, rows, c.N, c.K, c.Kpad);
+  c.bias = upload_f32(m, bias.data(), bias.size());
+  return c;
+}
+
+std::vector<int64_t> param_shape(const spe_model* m, const std::string& key) {
   for (auto& s : m->spec)
-    if (s.first == wkey) { cout = s.second[0]; cin = s.second[1]; kh = s.second[2]; kw = s.second[3]; }
+    if (s.first == key) return s.second;
+  return {};
+}
+
+// conv weight `wkey` [cout][cin][kh][kw] with an eval BatchNorm `bnkey` (weight, bias,
+// running_mean, running_var; eps 1e-5) and/or a conv bias folded in (double arithmetic)
+void fold_conv(spe_model* m, const std::string& wkey, const std::string& bnkey, const std::string& biaskey,
+               std::vector<float>& w, std::vector<float>& bias) {
+  const auto sh = param_shape(m, wkey);
+  const int64_t cout = sh[0], per = sh[1] * sh[2] * sh[3];
+  const auto& src = m->host[wkey];
   std::vector<double> scale(cout, 1.0), shift(cout, 0.0);
   if (!bnkey.empty()) {
     const auto& g = m->host[bnkey + ".weight"];
@@ -158,24 +190,20 @@ Conv make_conv(spe_model* m, const std::string& wkey, const std::string& bnkey, 
     const auto& bb = m->host[biaskey];
     for (int64_t c = 0; c < cout; ++c) shift[c] += bb[c];
   }
-  const int cp = cin_pad > 0 ? cin_pad : (int)cin;
-  const int K = (int)(kh * kw * cp);
-  std::vector<float> rows((size_t)cout * K, 0.f);
-  const bool cblk = conv_channel_blocked(cp, (int)(kh * kw));   // K order: spe_kernels.h
-  for (int64_t co = 0; co < cout; ++co)
-    for (int64_t ci = 0; ci < cin; ++ci)
-      for (int64_t y = 0; y < kh; ++y)
-        for (int64_t x = 0; x < kw; ++x) {
-          const int64_t tap = y * kw + x;
-          const int64_t k = cblk ? ((ci / 64) * kh * kw + tap) * 64 + ci % 64 : tap * cp + ci;
-          rows[(size_t)co * K + k] = (float)(spec_w[((co * cin + ci) * kh + y) * kw + x] * scale[co]);
-        }
-  std::vector<float> bias(shift.begin(), shift.end());
-  Conv c;
-  c.N = (int)cout; c.K = K; c.Kpad = pad64(K); c.Cin = cp; c.KH = (int)kh; c.KW = (int)kw; c.stride = stride; c.pad = pad;
-  c.w = upload_rows(m, rows, c.N, c.K, c.Kpad);
-  c.bias = upload_f32(m, bias.data(), bias.size());
-  return c;
+  w.assign((size_t)cout * per, 0.f);
+  if (!src.empty())
+    for (int64_t co = 0; co < cout; ++co)
+      for (int64_t i = 0; i < per; ++i) w[co * per + i] = (float)(src[co * per + i] * scale[co]);
+  bias.assign(shift.begin(), shift.end());
+}
+
+// conv weight [Cout][Cin][KH][KW] (+FrozenBN) -> [Cout][KH][KW][Cin_pad] rows, folded bias
+Conv make_conv(spe_model* m, const std::string& wkey, const std::string& bnkey, const std::string& biaskey, int cin_pad,
+               int stride, int pad) {
+  const auto sh = param_shape(m, wkey);
+  std::vector<float> w, bias;
+  fold_conv(m, wkey, bnkey, biaskey, w, bias);
+  return pack_conv(m, w, bias, (int)sh[0], (int)sh[1], (int)sh[2], (int)sh[3], cin_pad, stride, pad);
 }
 
 // linear rows [r0, r0+n) of a [*, K] weight + bias slice
@@ -202,6 +230,8 @@ float* upload_transposed(spe_model* m, const std::string& k, int out, int in) {
     for (int i = 0; i < in; ++i) t[(size_t)i * out + o] = v[(size_t)o * in + i];
   return upload_f32(m, t.data(), t.size());
 }
+
+namespace {
 
 // sine position table for an all-valid mask (REV/models/position_encoding.py:30-53),
 // [h*w][256] in token order h*W + w
@@ -460,6 +490,7 @@ void spe_model_destroy(spe_model* m) {
   if (!m) return;
   if (m->dmem) (void)hipFree(m->dmem);
   for (auto e : m->prof.pool) (void)hipEventDestroy(e);
+  delete m->rt;
   delete m;
 }
 
@@ -490,16 +521,19 @@ int spe_model_finalize(spe_model* m) {
   // pass 1 sizes the device block, pass 2 packs and uploads
   m->dmem = nullptr;
   m->dused = 0;
-  build_device(m);
+  auto build = [&] { return m->family == 1 ? spe_rtdetr_build_device(m) : build_device(m); };
+  int rc0 = build();
+  if (rc0) return rc0;
   m->dbytes = m->dused;
   hipError_t e = hipMalloc((void**)&m->dmem, m->dbytes);
   if (e != hipSuccess) return fail((int)e, "hipMalloc of weights failed");
   m->dused = 0;
   m->upload_err = 0;
-  build_device(m);
+  rc0 = build();
+  if (rc0) return rc0;
   e = hipDeviceSynchronize();
   if (e != hipSuccess || m->upload_err) return fail(e != hipSuccess ? (int)e : m->upload_err, "weight upload failed");
-  if (m->esz == 2) {
+  if (m->esz == 2 && m->family == 0) {
     const int d = m->cfg.hidden_dim, fs = m->cfg.input_size / 8, T = fs * fs, Q = m->cfg.num_queries;
     auto proj = [&](const void* A, int rows, const Conv& w, void* out) {
       GemmArgs g{};
@@ -524,6 +558,7 @@ int spe_model_finalize(spe_model* m) {
 
 int64_t spe_model_workspace_bytes(const spe_model* m, int batch) {
   if (!m || batch <= 0) return -1;
+  if (m->family == 1) return spe_rtdetr_workspace(m, batch);
   return (int64_t)spe_plan(m, batch).total;
 }
 

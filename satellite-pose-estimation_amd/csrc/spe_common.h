@@ -102,3 +102,11 @@ SPE_DEV int xcd_remap(int bid, int nwg) {
   const int xcd = bid & 7, idx = bid >> 3;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + idx;
 }
+
+// epilogue activation (ACT_* in spe_kernels.h); SiLU as torch's x / (1 + exp(-x)), GELU exact
+SPE_DEV float apply_act(float v, int act) {
+  if (act == 1) return fmaxf(v, 0.f);
+  if (act == 2) return v / (1.f + expf(-v));
+  if (act == 3) return 0.5f * v * (1.f + erff(v * 0.7071067811865476f));
+  return v;
+}

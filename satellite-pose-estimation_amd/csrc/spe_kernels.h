@@ -6,6 +6,9 @@
 
 enum { SPE_DTYPE_BF16 = 0, SPE_DTYPE_F32 = 1, SPE_DTYPE_F16 = 2 };   // F16: attention operands only
 enum { GEMM_LINEAR = 0, GEMM_LINEAR_ADD = 1, GEMM_CONV = 2 };
+// GEMM epilogue activations: ReLU (ResNet, DETR FFN), SiLU (UNC hybrid encoder ConvNormLayer,
+// hybrid_encoder.py:17-37), exact-erf GELU (UNC AIFI FFN, torch nn.GELU default)
+enum { ACT_NONE = 0, ACT_RELU = 1, ACT_SILU = 2, ACT_GELU = 3 };
 
 struct GemmArgs {
   const void* A; int lda;          // LINEAR*: A[m*lda + k]; CONV: NHWC input [B][H][W][Cin]
@@ -15,7 +18,8 @@ struct GemmArgs {
   int M, N, K;
   const float* bias;               // [N] or null
   const void* R; int ldr;          // residual [m*ldr + n] or null
-  int relu;
+  int act;                         // ACT_*: y = act(acc + bias + R), or act(acc + bias) + R
+  int res_post;                    //   with res_post (CSPRepLayer's silu(rep(x1)) + x2)
   void* C; int ldc;                // output [m*ldc + n]
   int out_f32;                     // store fp32 instead of T
   int out_f16;                     // bf16 models: store fp16 instead of bf16 (fp16 attention operands)
@@ -115,6 +119,8 @@ struct HeadArgs {
   float* points;                   // [B][Q][2] crop-normalised (sigmoid)
   float* probs;                    // [B][Q][12] softmax (nullable)
   float* points_px;                // [B][Q][2] image px (nullable)
+  const float* pt_add;             // [B*Q][2] added to the point MLP output before the sigmoid
+  int pt_add_invsig;               //   (nullable; RT-DETR: anchors, or inverse_sigmoid(ref) if set)
   float* log_sigmas;               // [B][Q][2] (nullable)
   float* sigmas;                   // [B][Q][2] exp (nullable)
 };
@@ -147,3 +153,33 @@ struct EnsembleArgs {
 int spe_launch_ensemble_fuse(const EnsembleArgs& a, hipStream_t s);
 int spe_launch_postprocess(const float* logits, const float* points, const float* clip_bbox, int B, int Q,
                            float* probs, float* points_px, hipStream_t s);
+
+// ---- UNC RT-DETR (rtdetr.hip, rtdetr_model.cpp)
+// nearest x2 (mode 0) / bicubic x0.5 (mode 1) resample of NHWC [B][H][W][C] (row stride ldi)
+// into [B][Ho][Wo] rows of stride ldo (a channel slice of a concat buffer)
+int spe_launch_resample2x(const void* in, int ldi, void* out, int ldo, int B, int H, int W, int C, int mode, int dtype,
+                          hipStream_t s);
+struct RtSelectArgs {
+  const float* logits; int C;      // enc_score_head [level-major rows][C] fp32
+  const void* memory; int ldm;     // output_memory (enc_output), level-major rows, T
+  const float* anchors;            // [L][2] per-image token anchors (logit domain)
+  int B, Q, D, levels;
+  int lvl_start[5];                // token offsets of the levels within an image, [levels] = L
+  int* topk;                       // [B][Q] selected token indices, descending score
+  void* target; int ldt;           // [B*Q][D] T gathered output_memory rows
+  float* target_f32;               // [B*Q][D] the same rows in fp32 (encoder box head input)
+  float* sel_logits;               // [B*Q][C]
+  float* sel_anchors;              // [B*Q][2]
+};
+int spe_launch_query_select(const RtSelectArgs& a, int dtype, hipStream_t s);
+int spe_launch_qpos_hidden(const float* ref, const float* w0, const float* b0, void* out, int rows, int H, int dtype,
+                           hipStream_t s);
+struct RtDeformArgs {
+  const void* value; int ldv;      // level-major rows [lvl_rows0[l] + b*H_l*W_l + y*W_l + x], T, heads h*32+c
+  const float* so_aw; int ld_so;   // [rows][2*H*NL*NP offsets | H*NL*NP attention logits] fp32
+  const float* ref;                // [rows][2] reference points (sigmoid domain)
+  void* out; int ldo;              // [rows][256] T
+  int rows, Q, heads, levels, points;
+  int lvl_h[4], lvl_w[4], lvl_rows0[4];
+};
+int spe_launch_msdeform(const RtDeformArgs& a, int dtype, hipStream_t s);

@@ -79,6 +79,48 @@ def test_gemm_linear_epilogue(gpu_device, dtype, M, N, K):
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+@pytest.mark.parametrize("act", [2, 3])
+@pytest.mark.parametrize("post", [0, 1])
+@pytest.mark.parametrize("M,N,K", [(300, 200, 256), (40000, 64, 128), (33000, 256, 512)])
+def test_gemm_activations(gpu_device, dtype, act, post, M, N, K):
+    """SiLU / exact GELU epilogues (UNC hybrid encoder ConvNormLayer, AIFI FFN), with the
+    residual added before the activation or after it (CSPRepLayer: silu(rep(x1)) + x2); shapes
+    reach the few-row, 256-row-tile and 128x128 kernels."""
+    _, dt, tol = DT[dtype]
+    g = torch.Generator(device="cpu").manual_seed(M + N + act)
+    A = torch.randn(M, K, generator=g).to(gpu_device, dt)
+    Wt = (torch.randn(N, K, generator=g) / K ** 0.5).to(gpu_device, dt)
+    ldb = (K + 63) // 64 * 64
+    bias = torch.randn(N, generator=g).to(gpu_device)
+    R = torch.randn(M, N, generator=g).to(gpu_device, dt)
+    C = torch.zeros(M, N, dtype=dt, device=gpu_device)
+    _gemm(dtype, 0, A, _padded_weight(Wt, ldb, dt), M, N, K, K, ldb, C, N, bias=bias, R=R, ldr=N, relu=act | (post << 8))
+    y = A.float() @ Wt.float().t() + bias
+    f = F.silu if act == 2 else F.gelu
+    ref = f(y) + R.float() if post else f(y + R.float())
+    _close(C, ref, tol)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+@pytest.mark.parametrize("B,H,Cin,Cout", [(2, 16, 64, 128), (64, 32, 256, 512)])
+def test_gemm_conv_avgpool_shortcut(gpu_device, dtype, B, H, Cin, Cout):
+    """PResNet-vd shortcut AvgPool2d(2, 2, ceil_mode) + 1x1 conv as one 2x2 stride-2 conv with
+    w/4 per tap (UNC/nn/backbone/presnet.py:88-101), channel-blocked K order (4 taps)."""
+    _, dt, tol = DT[dtype]
+    g = torch.Generator(device="cpu").manual_seed(B + Cin)
+    x = torch.randn(B, Cin, H, H, generator=g).to(gpu_device, dt)
+    w1 = (torch.randn(Cout, Cin, 1, 1, generator=g) / Cin ** 0.5).to(gpu_device)
+    ref = F.conv2d(F.avg_pool2d(x.float(), 2, 2, 0, ceil_mode=True), w1)
+    w = (w1 / 4).repeat(1, 1, 2, 2).to(dt)
+    K = 4 * Cin
+    Wp = _padded_weight(_pack_conv(w), K, dt)
+    C = torch.zeros(B * (H // 2) ** 2, Cout, dtype=dt, device=gpu_device)
+    _gemm(dtype, 2, x.permute(0, 2, 3, 1).contiguous(), Wp, C.shape[0], Cout, K, 0, K, C, Cout,
+          conv=(H, H, Cin, 2, 2, 2, 0))
+    _close(C, ref.permute(0, 2, 3, 1).reshape(-1, Cout), tol)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
 def test_gemm_linear_add_and_f32_out(gpu_device, dtype):
     _, dt, tol = DT[dtype]
     M, N, K, prow = 250, 96, 256, 25

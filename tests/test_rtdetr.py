@@ -82,3 +82,77 @@ def test_oracle_postprocess_matches_reference_formula():
     np.testing.assert_allclose(pp["points"][..., 0].numpy(), px, rtol=1e-6)
     np.testing.assert_allclose(pp["sigmas"].numpy(), np.exp(g["pred_sigmas"]), rtol=1e-6)
     np.testing.assert_allclose(pp["probs"].numpy().sum(-1), 1.0, rtol=1e-6)
+
+
+_hip_models = {}
+
+
+def _hip_model(cfg, dtype, wseed):
+    from spe.rtdetr import RTDETR
+    key = (cfg, dtype, wseed)
+    if key not in _hip_models:
+        m = RTDETR(cfg, dtype)
+        m.load_state_dict(random_rtdetr_weights(cfg, wseed))
+        _hip_models[key] = m
+    return _hip_models[key]
+
+
+def _hip_forward(tag, dtype, dev):
+    g, cfg = _golden(tag)
+    m = _hip_model(cfg, dtype, int(g["weight_seed"]))
+    b = synthetic_batch(SpeConfig(input_size=cfg.input_size), int(g["batch"]), int(g["image_seed"]))
+    o = m(torch.from_numpy(b["images"]).to(dev), clip_bbox=torch.from_numpy(g["clip_bbox"]).float().to(dev))
+    torch.cuda.synchronize()
+    return g, cfg, o
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tag", TAGS)
+def test_hip_fp32_matches_reference(gpu_device, tag):
+    g, cfg, o = _hip_forward(tag, "fp32", gpu_device)
+    np.testing.assert_array_equal(o["topk"].cpu().numpy(), g["topk_ind"])
+    c = lambda t: t.cpu().numpy()
+    assert np.abs(c(o["pred_pts"]) - g["pred_pts"]).max() <= 1e-4
+    assert np.abs(c(o["pred_logits"]) - g["pred_logits"]).max() <= 2e-3
+    assert np.abs(c(o["pred_sigmas"]) - g["pred_sigmas"]).max() <= 2e-3
+    aux = o["aux_outputs"]
+    assert np.abs(np.stack([c(a["pred_pts"]) for a in aux[:-1]]) - g["aux_pts"]).max() <= 1e-4
+    assert np.abs(np.stack([c(a["pred_logits"]) for a in aux[:-1]]) - g["aux_logits"]).max() <= 2e-3
+    assert np.abs(np.stack([c(a["pred_sigmas"]) for a in aux[:-1]]) - g["aux_sigmas"]).max() <= 2e-3
+    assert np.abs(c(aux[-1]["pred_pts"]) - g["enc_topk_bboxes"]).max() <= 1e-4
+    assert np.abs(c(aux[-1]["pred_logits"]) - g["enc_topk_logits"]).max() <= 2e-3
+    # fused RTDETRPostProcessor == the reference's formula on the reference's outputs
+    ref = rtdetr_ref.postprocess({k: torch.from_numpy(g[k]) for k in ("pred_logits", "pred_pts", "pred_sigmas")},
+                                 g["clip_bbox"])
+    assert np.abs(c(o["points_px"]) - ref["points"].numpy()).max() <= 0.05
+    assert np.abs(c(o["probs"]) - ref["probs"].numpy()).max() <= 1e-3
+    assert np.abs(c(o["sigmas"]) - ref["sigmas"].numpy()).max() <= 5e-3 * max(1.0, float(ref["sigmas"].max()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("tag", TAGS)
+def test_hip_bf16_close_to_reference(gpu_device, tag):
+    g, cfg, o = _hip_forward(tag, "bf16", gpu_device)
+    sel, ref_sel = o["topk"].cpu().numpy(), g["topk_ind"]
+    for b in range(sel.shape[0]):
+        assert len(set(sel[b]) & set(ref_sel[b])) >= 0.8 * cfg.num_queries
+        same = sel[b] == ref_sel[b]           # queries selected in the same rank
+        if same.sum() == 0:
+            continue
+        assert np.abs(o["pred_pts"][b].cpu().numpy()[same] - g["pred_pts"][b][same]).max() <= 3e-2
+        assert np.abs(o["pred_logits"][b].cpu().numpy()[same] - g["pred_logits"][b][same]).max() <= 0.3
+
+
+@pytest.mark.gpu
+def test_hip_batch_independence(gpu_device):
+    """Image i's outputs do not depend on the rest of the batch (per-image top-k, level-major
+    memory indexing)."""
+    g, cfg = _golden("r18_s128")
+    m = _hip_model(cfg, "fp32", int(g["weight_seed"]))
+    b = synthetic_batch(SpeConfig(input_size=cfg.input_size), 4, 9)
+    x = torch.from_numpy(b["images"]).to(gpu_device)
+    full = m(x)
+    part = m(x[1:3].contiguous())
+    torch.cuda.synchronize()
+    np.testing.assert_array_equal(full["topk"][1:3].cpu().numpy(), part["topk"].cpu().numpy())
+    assert (full["pred_pts"][1:3] - part["pred_pts"]).abs().max().item() <= 1e-5
