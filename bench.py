@@ -53,6 +53,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--model", default="detr", choices=["detr", "rtdetr_r18", "rtdetr_r50"],
+                   help="detr: the REV DETR keypoint model (BASELINE configs); rtdetr_*: the UNC RT-DETR sigma model "
+                        "(SURVEY 8f.4) at its speed config (256x256, 30 queries, 3 decoder layers, sigma-weighted "
+                        "EPnP-RANSAC + self-assessment)")
     p.add_argument("--config", type=int, default=2, choices=sorted(PRESETS),
                    help="BASELINE.json configs[k-1] preset (2 = the headline metric's workload); explicit flags override")
     p.add_argument("--batch", type=int, default=None, help="images per GPU per step")
@@ -81,6 +85,10 @@ def parse():
     p.add_argument("--launch-table", default=None,
                    help="write every launch of the profiled step (kind, ms, flops, bytes, roofline floor) as JSON")
     a = p.parse_args()
+    if a.model != "detr":
+        for k, v in dict(batch=64, size=256, queries=30, layers=3, solver="epnp_ransac_sigma", sigma_head=1).items():
+            if getattr(a, k) is None:
+                setattr(a, k, v)
     for k, v in PRESETS[a.config].items():
         if getattr(a, k) is None:
             setattr(a, k, v)
@@ -121,6 +129,37 @@ def cpu_baseline(cfg, seconds, solver="epnp"):
     return {"value": n / dt, "unit": "images/s", "cores": threads, "kind": "port",
             "sample": f"{n} single-image passes ({cfg.input_size}x{cfg.input_size}, Q={cfg.num_queries}, "
                       f"{cfg.enc_layers}/{cfg.dec_layers}, fp32 torch-CPU model + C {solver} oracle) in {dt:.1f}s"}
+
+
+def cpu_baseline_rtdetr(rcfg, seconds):
+    """Oracle port of the UNC RT-DETR model (torch-fp32 CPU restatement + C sigma-EPnP-RANSAC
+    solver) on single images, like cpu_baseline."""
+    import torch
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import pnp_ref
+    import rtdetr_ref
+    from spe.config import Camera, SpeConfig, world_points
+    from spe.rtdetr_spec import random_rtdetr_weights
+    from spe.synthetic import synthetic_batch
+    threads = min(16, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    w = random_rtdetr_weights(rcfg, 0)
+    b = synthetic_batch(SpeConfig(input_size=rcfg.input_size), 1, 99)
+    W, K = world_points(), Camera.K
+    n, t0 = 0, time.perf_counter()
+    with torch.no_grad():
+        while True:
+            o = rtdetr_ref.forward(b["images"], w, rcfg)
+            pp = rtdetr_ref.postprocess(o, b["clip_bbox"])
+            pnp_ref.pnp_batch(pp["points"].numpy(), pp["probs"].numpy(), K, W, mode=pnp_ref.MODE_EPNP_RANSAC_SIGMA,
+                              repro=25.0, sigmas=pp["sigmas"].numpy())
+            n += 1
+            if time.perf_counter() - t0 >= seconds:
+                break
+    dt = time.perf_counter() - t0
+    return {"value": n / dt, "unit": "images/s", "cores": threads, "kind": "port",
+            "sample": f"{n} single-image passes (RT-DETR r{rcfg.depth}vd {rcfg.input_size}x{rcfg.input_size}, "
+                      f"Q={rcfg.num_queries}, fp32 torch-CPU restatement + C epnp_ransac_sigma oracle) in {dt:.1f}s"}
 
 
 def traffic_for(kind, grid, attn_dtype):
@@ -178,8 +217,18 @@ def main():
         del m
         return hs
 
-    model = DETR(cfg, dtype=args.dtype, attn_dtype=args.attn_dtype)
-    model.load_state_dict(bench_weights(cfg, 0, hs_fn) if args.weights == "label-diverse" else random_weights(cfg, 0))
+    rcfg = None
+    if args.model != "detr":
+        from spe.rtdetr import RTDETR
+        from spe.rtdetr_spec import RtdetrConfig, random_rtdetr_weights
+        rcfg = RtdetrConfig(depth=18 if args.model == "rtdetr_r18" else 50, input_size=args.size,
+                            num_queries=args.queries, dec_layers=args.layers)
+        model = RTDETR(rcfg, dtype=args.dtype, aux_outputs=False)
+        model.load_state_dict(random_rtdetr_weights(rcfg, 0))
+        args.weights = "random"
+    else:
+        model = DETR(cfg, dtype=args.dtype, attn_dtype=args.attn_dtype)
+        model.load_state_dict(bench_weights(cfg, 0, hs_fn) if args.weights == "label-diverse" else random_weights(cfg, 0))
     solver = build_solver(argparse.Namespace(solver=args.solver, repro=20))
     if args.raw_frames:
         from spe.synthetic import synthetic_frames
@@ -191,7 +240,7 @@ def main():
                          torch.from_numpy(data["quat"]).to(dev), torch.from_numpy(data["tvec"]).to(dev))
     else:
         pipe = PosePipeline(model, solver, B, device=dev, overlap=not args.no_overlap,
-                            overlap_decode=not (args.no_overlap_decode or args.no_overlap))
+                            overlap_decode=rcfg is None and not (args.no_overlap_decode or args.no_overlap))
         data = synthetic_batch(cfg, B, seed=1000 + rank)
         pipe.load(torch.from_numpy(data["images"]).to(dev), torch.from_numpy(data["clip_bbox"]).float().to(dev),
                   torch.from_numpy(data["quat"]).to(dev), torch.from_numpy(data["tvec"]).to(dev))
@@ -266,7 +315,7 @@ def main():
         return
     total_images = B * world * args.steps
     avg_ms = k_ms / max(k_n, 1)
-    mfma_bound = dominant.startswith(("conv", "gemm", "attn", "ffn"))
+    mfma_bound = dominant.replace("rt.", "", 1).startswith(("conv", "gemm", "attn", "ffn", "aifi", "csp", "enc", "dec"))
     if mfma_bound:
         achieved = (k_fl / max(k_n, 1)) / (avg_ms * 1e-3) / 1e12
         peak = PEAK[args.dtype]["mfma"]
@@ -289,8 +338,11 @@ def main():
         "dtype": args.dtype,
         "data": f"synthetic (seeded SPEED-shaped {'1920x1200 8-bit frames + detector boxes, on-device val transform' if args.raw_frames else 'crops'}; "
                 f"{args.weights} random-init weights, no checkpoint exists in the reference)",
-        "config": {"workload": CONFIG_NAME[args.config].format(L=args.layers, Q=args.queries, S=args.size,
-                                                                solver=args.solver, A=args.attn_dtype),
+        "config": {"workload": (CONFIG_NAME[args.config].format(L=args.layers, Q=args.queries, S=args.size,
+                                                                 solver=args.solver, A=args.attn_dtype) if rcfg is None else
+                                f"UNC RT-DETR r{rcfg.depth}vd + HybridEncoder + {args.layers}-layer deformable decoder "
+                                f"with sigma head, {args.queries} queries, {args.size}x{args.size}, sigma-weighted "
+                                f"EPnP-RANSAC + self-assessment (solver={args.solver}; SURVEY 8f.4, not a BASELINE config)"),
                    "global_batch": B * world, "per_gpu_batch": B, "input_size": args.size,
                    "num_queries": args.queries, "attention_dtype": args.attn_dtype,
                    "parallelism": f"dp{world} (image sharding)"},
@@ -308,7 +360,8 @@ def main():
     if "assess" in out:
         result["self_assessment_reliable"] = int(out["assess"]["reliable"].sum().item())
     if world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(cfg, args.cpu_seconds, args.solver)
+        result["cpu_baseline"] = (cpu_baseline(cfg, args.cpu_seconds, args.solver) if rcfg is None
+                                  else cpu_baseline_rtdetr(rcfg, args.cpu_seconds))
     print(json.dumps(result))
     if dist.is_initialized():
         dist.destroy_process_group()

@@ -29,9 +29,9 @@ class RTDETR(nn.Module):
     dtype "bf16": bf16 storage / MFMA with fp32 accumulation, LayerNorm, softmax and heads;
     "fp32": exact-f32 MFMA everywhere (parity path)."""
 
-    def __init__(self, cfg: RtdetrConfig, dtype: str = "bf16"):
+    def __init__(self, cfg: RtdetrConfig, dtype: str = "bf16", aux_outputs: bool = True):
         super().__init__()
-        self.cfg, self.dtype = cfg, dtype
+        self.cfg, self.dtype, self.aux_outputs = cfg, dtype, aux_outputs
         self.num_queries = cfg.num_queries
         self._pending = {}
         self._ready = False
@@ -83,12 +83,13 @@ class RTDETR(nn.Module):
                 self._ws[key] = ws = (torch.empty(int(nbytes), dtype=torch.uint8, device=device), B)
         return ws[0]
 
-    def forward(self, samples, clip_bbox=None, stream=None, aux=True):
+    def forward(self, samples, clip_bbox=None, stream=None, aux=None):
         """rtdetr.py:36-53 in eval.  Returns pred_logits [B,Q,C+1], pred_pts [B,Q,2], pred_sigmas
         [B,Q,2] (raw) and, with aux, the reference's aux_outputs list.  Passing `clip_bbox`
         ([B,4] device) also runs the fused RTDETRPostProcessor: probs, points_px, sigmas."""
         if not self._ready:
             raise RuntimeError("RTDETR: load_state_dict() with every parameter before forward()")
+        aux = self.aux_outputs if aux is None else aux
         if isinstance(samples, (list, tuple)):
             samples = nested_tensor_from_tensor_list(list(samples))
         images = samples.tensors if isinstance(samples, NestedTensor) else samples
