@@ -4,8 +4,6 @@
 //   sigma head  MLP(256,256,1,3) repeated to 2, exp       UNC/src/zoo/rtdetr/rtdetr_decoder.py:295-297,367,
 //                                                         UNC/src/zoo/rtdetr/rtdetr_postprocessor.py:53
 //   PostProcess softmax(12) + crop->image px rescale      REV/models/detr_speed.py:266-293
-//   RT-DETR point refinement: sigmoid(MLP(hs) + inverse_sigmoid(ref)), or + anchors for the
-//   encoder's query selection             UNC/src/zoo/rtdetr/rtdetr_decoder.py:335-338,638
 // Only the last decoder layer feeds PostProcess; the aux layers only feed the training
 // criterion (REV/models/detr_speed.py:89-100) and are not evaluated on the inference path.
 // One workgroup (256 threads) per query row; weights are stored transposed [in][out] so the
@@ -53,8 +51,8 @@ __global__ __launch_bounds__(NT) void heads_kernel(HeadArgs a) {
   __syncthreads();
 
   // classification logits + softmax
-  if (a.cls_wt) dense_small(x, a.cls_wt, a.cls_b, out, D, 12, red);
-  if (a.cls_wt && threadIdx.x == 0) {
+  dense_small(x, a.cls_wt, a.cls_b, out, D, 12, red);
+  if (threadIdx.x == 0) {
     float mx = -INFINITY;
     for (int c = 0; c < 12; ++c) mx = fmaxf(mx, out[c]);
     float e[12], s = 0.f;
@@ -73,22 +71,8 @@ __global__ __launch_bounds__(NT) void heads_kernel(HeadArgs a) {
   __syncthreads();
   dense_small(h2, a.pt_w2t, a.pt_b2, out, D, 2, red);
   if (threadIdx.x == 0) {
-    float dx = out[0], dy = out[1];
-    if (a.pt_add) {             // RT-DETR: + anchor, or + inverse_sigmoid(ref) (UNC utils.py:10-12)
-      float ax = a.pt_add[(size_t)row * 2], ay = a.pt_add[(size_t)row * 2 + 1];
-      if (a.pt_add_invsig) {
-        auto invsig = [](float v) {
-          v = fminf(fmaxf(v, 0.f), 1.f);
-          return logf(fmaxf(v, 1e-5f) / fmaxf(1.f - v, 1e-5f));
-        };
-        ax = invsig(ax);
-        ay = invsig(ay);
-      }
-      dx = dx + ax;
-      dy = dy + ay;
-    }
-    const float px = 1.f / (1.f + expf(-dx));
-    const float py = 1.f / (1.f + expf(-dy));
+    const float px = 1.f / (1.f + expf(-out[0]));
+    const float py = 1.f / (1.f + expf(-out[1]));
     a.points[(size_t)row * 2 + 0] = px;
     a.points[(size_t)row * 2 + 1] = py;
     if (a.points_px && a.clip_bbox) {

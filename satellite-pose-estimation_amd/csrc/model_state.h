@@ -72,10 +72,15 @@ struct RtCsp {               // CSPRepLayer, one RepVggBlock folded into one 3x3
   Conv c1, c2, rep, c3;
   bool has_c3 = false;
 };
-struct RtDec {               // decoder layer + its score / box / sigma heads
+struct RtHead {              // score / box MLP / sigma MLP heads of one layer (rtdetr_decoder.py:298-372)
+  Conv h1, box1, sig1;       // h1: box.layers.0 | sigma.layers.0 stacked (N = 512, or 256 without sigma)
+  float *cls_w = nullptr, *cls_b = nullptr, *box_w2 = nullptr, *box_b2 = nullptr;
+  float *sig_w2 = nullptr, *sig_b2 = nullptr;   // last layers, fp32 [out][256]
+};
+struct RtDec {               // decoder layer + its heads
   Conv sqk, sv, so, soaw, oproj, l1, l2;   // soaw: sampling_offsets | attention_weights (N = 288)
   float *n1g, *n1b, *n2g, *n2b, *n3g, *n3b;
-  HeadArgs head{};
+  RtHead head;
 };
 struct RtModel {
   spe_rtdetr_config cfg{};
@@ -92,7 +97,7 @@ struct RtModel {
   Conv dec_in[3], enc_out, enc_score, vproj;   // vproj: every layer's value_proj, N = 256 * dec_layers
   float *eo_g, *eo_b;
   float* anchors = nullptr;             // [L][2] fp32, logit domain
-  HeadArgs enc_head{};                  // enc_bbox_head (+ anchors, sigmoid): the initial reference points
+  RtHead enc_head;                      // enc_bbox_head (+ anchors, sigmoid): the initial reference points
   float *qp_w0 = nullptr, *qp_b0 = nullptr;   // query_pos_head layer 0 [512][2], [512]
   Conv qp_l1;
   std::vector<RtDec> dec;

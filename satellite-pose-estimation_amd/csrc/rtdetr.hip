@@ -12,6 +12,11 @@
 //                  anchors; one workgroup per image
 //   qpos_hidden    query_pos_head layer 0 (MLP(2, 512, 256), rtdetr_decoder.py:459,298-300):
 //                  relu(W0 . ref + b0) with K = 2, written as the A operand of layer 1's GEMM
+//   head_finish    the last layers of the score / box / sigma heads (rtdetr_decoder.py:335-372):
+//                  logits = hs W_c^T + b_c, box = sigmoid(h2_box W_2^T + b_2 + inverse_sigmoid(ref))
+//                  (or + anchors for the encoder selection, :638), log-sigma = h2_sig w^T + b
+//                  repeated to 2, and the fused RTDETRPostProcessor; the heads' 256-wide hidden
+//                  layers run as GEMMs before it.  One wave per query row.
 //   msdeform       MSDeformableAttention core (rtdetr_decoder.py:105-196 + utils.py:15-64):
 //                  per (query, head) softmax over levels x points of the attention logits,
 //                  sampling location = ref + offset / (W_l, H_l), bilinear grid_sample
@@ -132,10 +137,7 @@ __global__ __launch_bounds__(SEL_NT) void query_select_kernel(RtSelectArgs a) {
     const size_t src = row_of(sel[k]), dst = (size_t)b * a.Q + k;
     const T* mr = (const T*)a.memory + src * a.ldm;
     T* tr = (T*)a.target + dst * a.ldt;
-    for (int c = tid; c < D; c += SEL_NT) {
-      tr[c] = mr[c];
-      a.target_f32[dst * D + c] = to_f32(mr[c]);
-    }
+    for (int c = tid; c < D; c += SEL_NT) tr[c] = mr[c];
     if (tid < a.C) a.sel_logits[dst * a.C + tid] = a.logits[src * a.C + tid];
     if (tid < 2) a.sel_anchors[dst * 2 + tid] = a.anchors[(size_t)sel[k] * 2 + tid];
   }
@@ -151,6 +153,67 @@ __global__ void qpos_hidden_kernel(const float* __restrict__ ref, const float* _
     const size_t r = i / H;
     const float v = ref[2 * r] * w0[2 * j] + ref[2 * r + 1] * w0[2 * j + 1] + b0[j];
     out[i] = from_f32<T>(fmaxf(v, 0.f));
+  }
+}
+
+
+// ---------------------------------------------------------------- head_finish
+template <typename T>
+__global__ __launch_bounds__(256) void head_finish_kernel(RtHeadArgs a) {
+  const int lane = threadIdx.x & 63, row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= a.rows) return;
+  const int C = a.C;
+  auto dot = [&](const float* x, const float* w) {       // 256-long, 4 per lane, wave reduction
+    const float4 xv = *reinterpret_cast<const float4*>(x + 4 * lane);
+    const float4 wv = *reinterpret_cast<const float4*>(w + 4 * lane);
+    return wave_sum(xv.x * wv.x + xv.y * wv.y + xv.z * wv.z + xv.w * wv.w);
+  };
+  auto dotT = [&](const T* x, const float* w) {
+    float f[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) f[e] = to_f32(x[4 * lane + e]);
+    const float4 wv = *reinterpret_cast<const float4*>(w + 4 * lane);
+    return wave_sum(f[0] * wv.x + f[1] * wv.y + f[2] * wv.z + f[3] * wv.w);
+  };
+  if (a.cls_w) {
+    float lg[16];
+    const float* hs = a.hs + (size_t)row * 256;
+    for (int c = 0; c < C; ++c) lg[c] = dot(hs, a.cls_w + (size_t)c * 256) + a.cls_b[c];
+    if (lane == 0) {
+      float mx = -INFINITY, e[16], sum = 0.f;
+      for (int c = 0; c < C; ++c) { a.logits[(size_t)row * C + c] = lg[c]; mx = fmaxf(mx, lg[c]); }
+      for (int c = 0; c < C; ++c) { e[c] = expf(lg[c] - mx); sum += e[c]; }
+      if (a.probs)
+        for (int c = 0; c < C; ++c) a.probs[(size_t)row * C + c] = e[c] / sum;
+    }
+  }
+  const T* h2 = (const T*)a.h2 + (size_t)row * a.ld_h2;
+  float dx = dotT(h2, a.box_w2) + a.box_b2[0];
+  float dy = dotT(h2, a.box_w2 + 256) + a.box_b2[1];
+  float sg = a.sig_w2 ? dotT(h2 + 256, a.sig_w2) + a.sig_b2[0] : 0.f;
+  if (lane != 0) return;
+  float ax = a.pt_add[(size_t)row * 2], ay = a.pt_add[(size_t)row * 2 + 1];
+  if (a.pt_add_invsig) {            // inverse_sigmoid (UNC/src/zoo/rtdetr/utils.py:10-12)
+    auto invsig = [](float v) {
+      v = fminf(fmaxf(v, 0.f), 1.f);
+      return logf(fmaxf(v, 1e-5f) / fmaxf(1.f - v, 1e-5f));
+    };
+    ax = invsig(ax);
+    ay = invsig(ay);
+  }
+  dx = dx + ax;
+  dy = dy + ay;
+  const float px = 1.f / (1.f + expf(-dx)), py = 1.f / (1.f + expf(-dy));
+  a.points[(size_t)row * 2] = px;
+  a.points[(size_t)row * 2 + 1] = py;
+  if (a.points_px && a.clip_bbox) {
+    const float* bb = a.clip_bbox + (size_t)(row / a.Q) * 4;
+    a.points_px[(size_t)row * 2] = px * (bb[2] - bb[0]) + bb[0];
+    a.points_px[(size_t)row * 2 + 1] = py * (bb[3] - bb[1]) + bb[1];
+  }
+  if (a.sig_w2) {
+    if (a.log_sigmas) { a.log_sigmas[(size_t)row * 2] = sg; a.log_sigmas[(size_t)row * 2 + 1] = sg; }
+    if (a.sigmas) { const float e = expf(sg); a.sigmas[(size_t)row * 2] = e; a.sigmas[(size_t)row * 2 + 1] = e; }
   }
 }
 
@@ -254,5 +317,14 @@ int spe_launch_msdeform(const RtDeformArgs& a, int dtype, hipStream_t s) {
   if (a.heads * 32 != 256 || a.heads * a.levels * a.points > 128 || a.levels > 4 || a.points > 4) return -5;
   if (dtype == SPE_DTYPE_BF16) hipLaunchKernelGGL(msdeform_kernel<bf16>, dim3(a.rows), dim3(256), 0, s, a);
   else hipLaunchKernelGGL(msdeform_kernel<float>, dim3(a.rows), dim3(256), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+int spe_launch_head_finish(const RtHeadArgs& a, int dtype, hipStream_t s) {
+  if (a.rows <= 0) return 0;
+  if (a.C > 16 || !a.points || !a.pt_add || !a.h2 || (a.cls_w && (!a.hs || !a.logits))) return -5;
+  const int blocks = (a.rows + 3) / 4;
+  if (dtype == SPE_DTYPE_BF16) hipLaunchKernelGGL(head_finish_kernel<bf16>, dim3(blocks), dim3(256), 0, s, a);
+  else hipLaunchKernelGGL(head_finish_kernel<float>, dim3(blocks), dim3(256), 0, s, a);
   return (int)hipGetLastError();
 }

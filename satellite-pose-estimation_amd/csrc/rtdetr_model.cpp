@@ -141,20 +141,22 @@ Conv stack_linears(spe_model* m, const std::vector<std::pair<std::string, std::s
   return c;
 }
 
-HeadArgs make_head(spe_model* m, const std::string& cls, const std::string& box, const std::string& sigma) {
-  HeadArgs h{};
-  h.D = 256;
-  if (!cls.empty()) {
-    h.cls_wt = upload_transposed(m, cls + ".weight", m->rt->cfg.num_classes + 1, 256);
-    h.cls_b = upload_key(m, cls + ".bias");
-  }
-  h.pt_w0t = upload_transposed(m, box + ".layers.0.weight", 256, 256); h.pt_b0 = upload_key(m, box + ".layers.0.bias");
-  h.pt_w1t = upload_transposed(m, box + ".layers.1.weight", 256, 256); h.pt_b1 = upload_key(m, box + ".layers.1.bias");
-  h.pt_w2t = upload_transposed(m, box + ".layers.2.weight", 2, 256); h.pt_b2 = upload_key(m, box + ".layers.2.bias");
+RtHead make_head(spe_model* m, const std::string& cls, const std::string& box, const std::string& sigma) {
+  RtHead h;
+  std::vector<std::pair<std::string, std::string>> first{{box + ".layers.0.weight", box + ".layers.0.bias"}};
+  if (!sigma.empty()) first.emplace_back(sigma + ".layers.0.weight", sigma + ".layers.0.bias");
+  h.h1 = stack_linears(m, first, 256);
+  h.box1 = make_linear(m, box + ".layers.1.weight", box + ".layers.1.bias", 0, 256, 256);
+  h.box_w2 = upload_key(m, box + ".layers.2.weight");
+  h.box_b2 = upload_key(m, box + ".layers.2.bias");
   if (!sigma.empty()) {
-    h.sg_w0t = upload_transposed(m, sigma + ".layers.0.weight", 256, 256); h.sg_b0 = upload_key(m, sigma + ".layers.0.bias");
-    h.sg_w1t = upload_transposed(m, sigma + ".layers.1.weight", 256, 256); h.sg_b1 = upload_key(m, sigma + ".layers.1.bias");
-    h.sg_w2t = upload_transposed(m, sigma + ".layers.2.weight", 1, 256); h.sg_b2 = upload_key(m, sigma + ".layers.2.bias");
+    h.sig1 = make_linear(m, sigma + ".layers.1.weight", sigma + ".layers.1.bias", 0, 256, 256);
+    h.sig_w2 = upload_key(m, sigma + ".layers.2.weight");
+    h.sig_b2 = upload_key(m, sigma + ".layers.2.bias");
+  }
+  if (!cls.empty()) {
+    h.cls_w = upload_key(m, cls + ".weight");
+    h.cls_b = upload_key(m, cls + ".bias");
   }
   return h;
 }
@@ -220,7 +222,7 @@ struct RtWs {
   size_t cat0, cat1, catp0, catp1, aqk, avt, aao, atmp, affn, aout;
   size_t x1, x2, y, inner1, p3, n4, n5;
   size_t mem, omem, elog, value;
-  size_t topk, tgt, tgt32, slog, sanc, refs, qh, qpos, dqk, dvt, dao, dtmp, t1d, t2d, soaw, dcr, dffn, hs, lsig, lgt;
+  size_t topk, tgt, slog, sanc, refs, qh, qpos, hh1, hh2, dqk, dvt, dao, dtmp, t1d, t2d, soaw, dcr, dffn, hs, lgt;
   size_t total;
 };
 
@@ -257,7 +259,8 @@ RtWs rt_plan(const spe_model* m, int B) {
   w.elog = take((size_t)B * L * (c.num_classes + 1) * 4);
   w.value = take((size_t)B * L * 256 * c.dec_layers * E);
   w.topk = take(BQ * 4);
-  w.tgt = take(BQ * 256 * E); w.tgt32 = take(BQ * 256 * 4);
+  w.tgt = take(BQ * 256 * E);
+  w.hh1 = take(BQ * 512 * E); w.hh2 = take(BQ * 512 * E);
   w.slog = take(BQ * (c.num_classes + 1) * 4); w.sanc = take(BQ * 2 * 4);
   w.refs = take((size_t)(c.dec_layers + 1) * BQ * 2 * 4);
   w.qh = take(BQ * 512 * E); w.qpos = take(BQ * 256 * E);
@@ -265,7 +268,7 @@ RtWs rt_plan(const spe_model* m, int B) {
   w.t1d = take(BQ * 256 * E); w.t2d = take(BQ * 256 * E);
   w.soaw = take(BQ * 288 * 4); w.dcr = take(BQ * 256 * E); w.dffn = take(BQ * c.dec_ff * E);
   w.hs = take(BQ * 256 * 4);
-  w.lsig = take(BQ * 2 * 4); w.lgt = take(BQ * (c.num_classes + 1) * 4);
+  w.lgt = take(BQ * (c.num_classes + 1) * 4);
   w.total = off;
   return w;
 }
@@ -446,6 +449,23 @@ int spe_rtdetr_forward(spe_model* m, void* stream, const float* images, int B, v
                      [&] { return spe_launch_layernorm(x, g, b, y, y32, M, d, dt, s); });
   };
 
+  // conv as an implicit GEMM, or a plain GEMM over NHWC rows when it is 1x1 / stride 1; the
+  // residual R (same row layout as the output) is added before the activation
+  auto cgemm = [&](const char* kind, const Conv& cv, const void* in, int Hin, void* outp, int ldc, int act,
+                   const void* R) {
+    GemmArgs g;
+    int mode = GEMM_CONV;
+    if (cv.KH == 1 && cv.KW == 1 && cv.stride == 1 && cv.pad == 0) {
+      g = linear_args(cv, in, cv.Cin, B * Hin * Hin, outp, ldc);
+      mode = GEMM_LINEAR;
+    } else {
+      g = conv_args(cv, in, B, Hin, Hin, outp, ldc);
+    }
+    g.act = act;
+    g.R = R; g.ldr = ldc;
+    return run_gemm(m, kind, g, mode, s);
+  };
+
   // ---------------- PResNet-vd (presnet.py:248-265)
   CK(run_other(m, "eltwise.pack", 0.0, (double)B * S * S * (12 + 8 * E), s,
                [&] { return spe_launch_pack_input(images, P(w.x0), B, S, dt, s); }));
@@ -473,25 +493,16 @@ int spe_rtdetr_forward(spe_model* m, void* stream, const float* images, int B, v
       const size_t outbuf = (last && st > 0) ? feat[st - 1] : (cur == w.bufA ? w.bufB : w.bufA);
       size_t res = cur;
       if (b.has_sc) {
-        GemmArgs g = conv_args(b.sc, P(cur), B, H, H, P(w.sc), b.cout);
-        CK(run_gemm(m, "rt.conv.short", g, GEMM_CONV, s));
+        CK(cgemm(b.stride == 2 ? "rt.conv.short" : "rt.conv.1x1", b.sc, P(cur), H, P(w.sc), b.cout, ACT_NONE, nullptr));
         res = w.sc;
       }
-      GemmArgs ga = conv_args(b.a, P(cur), B, H, H, P(w.t1), b.a.N);
-      ga.act = ACT_RELU;
-      CK(run_gemm(m, b.bottleneck ? "rt.conv.1x1" : "rt.conv.3x3", ga, GEMM_CONV, s));
-      const int Ha = ga.Ho;
+      CK(cgemm(b.bottleneck ? "rt.conv.1x1" : "rt.conv.3x3", b.a, P(cur), H, P(w.t1), b.a.N, ACT_RELU, nullptr));
+      const int Ha = (H + 2 * b.a.pad - b.a.KH) / b.a.stride + 1;
       if (b.bottleneck) {
-        GemmArgs gb = conv_args(b.b, P(w.t1), B, Ha, Ha, P(w.t2), b.b.N);
-        gb.act = ACT_RELU;
-        CK(run_gemm(m, "rt.conv.3x3", gb, GEMM_CONV, s));
-        GemmArgs gc = conv_args(b.c, P(w.t2), B, Ho, Ho, P(outbuf), b.cout);
-        gc.R = P(res); gc.ldr = b.cout; gc.act = ACT_RELU;
-        CK(run_gemm(m, "rt.conv.1x1", gc, GEMM_CONV, s));
+        CK(cgemm("rt.conv.3x3", b.b, P(w.t1), Ha, P(w.t2), b.b.N, ACT_RELU, nullptr));
+        CK(cgemm("rt.conv.1x1", b.c, P(w.t2), Ho, P(outbuf), b.cout, ACT_RELU, P(res)));
       } else {
-        GemmArgs gb = conv_args(b.b, P(w.t1), B, Ha, Ha, P(outbuf), b.cout);
-        gb.R = P(res); gb.ldr = b.cout; gb.act = ACT_RELU;
-        CK(run_gemm(m, "rt.conv.3x3", gb, GEMM_CONV, s));
+        CK(cgemm("rt.conv.3x3", b.b, P(w.t1), Ha, P(outbuf), b.cout, ACT_RELU, P(res)));
       }
       H = Ho;
       cur = outbuf;
@@ -617,18 +628,36 @@ int spe_rtdetr_forward(spe_model* m, void* stream, const float* images, int B, v
   for (int l = 0; l < 4; ++l) sa.lvl_start[l] = r.lvl_start[l];
   sa.topk = out->topk ? out->topk : (int*)P(w.topk);
   sa.target = P(w.tgt); sa.ldt = d;
-  sa.target_f32 = (float*)P(w.tgt32);
   sa.sel_logits = out->enc_logits ? out->enc_logits : (float*)P(w.slog);
   sa.sel_anchors = (float*)P(w.sanc);
   CK(run_other(m, "rt.select", 0.0, (double)ML * C * 4, s, [&] { return spe_launch_query_select(sa, dt, s); }));
+  // heads: the 256-wide hidden layers as GEMMs (box | sigma side by side), then head_finish
+  auto heads = [&](const RtHead& k, const void* x, const float* hs32, RtHeadArgs ha) -> int {
+    GemmArgs g1 = linear_args(k.h1, x, d, BQ, P(w.hh1), 2 * d);
+    g1.act = ACT_RELU;
+    int rc = run_gemm(m, "rt.heads", g1, GEMM_LINEAR, s);
+    if (rc) return rc;
+    GemmArgs g2 = linear_args(k.box1, P(w.hh1), 2 * d, BQ, P(w.hh2), 2 * d);
+    g2.act = ACT_RELU;
+    if ((rc = run_gemm(m, "rt.heads", g2, GEMM_LINEAR, s))) return rc;
+    if (k.sig_w2) {
+      GemmArgs g3 = linear_args(k.sig1, (char*)P(w.hh1) + d * E, 2 * d, BQ, (char*)P(w.hh2) + d * E, 2 * d);
+      g3.act = ACT_RELU;
+      if ((rc = run_gemm(m, "rt.heads", g3, GEMM_LINEAR, s))) return rc;
+    }
+    ha.rows = BQ; ha.Q = Q; ha.C = C;
+    ha.hs = hs32; ha.cls_w = k.cls_w; ha.cls_b = k.cls_b;
+    ha.h2 = P(w.hh2); ha.ld_h2 = 2 * d;
+    ha.box_w2 = k.box_w2; ha.box_b2 = k.box_b2; ha.sig_w2 = k.sig_w2; ha.sig_b2 = k.sig_b2;
+    return run_other(m, "rt.heads", 0.0, (double)BQ * d * 4, s, [&] { return spe_launch_head_finish(ha, dt, s); });
+  };
   float* refs = (float*)P(w.refs);
   auto ref_buf = [&](int i) { return refs + (size_t)i * BQ * 2; };
   {  // initial reference points: sigmoid(enc_bbox_head(target) + anchors) (= enc_topk_bboxes)
-    HeadArgs hh = r.enc_head;
-    hh.hs = (const float*)P(w.tgt32); hh.B = B; hh.Q = Q;
-    hh.pt_add = sa.sel_anchors; hh.pt_add_invsig = 0;
-    hh.points = out->enc_points ? out->enc_points : ref_buf(0);
-    CK(run_other(m, "rt.heads", 0.0, (double)BQ * d * 4, s, [&] { return spe_launch_heads(hh, s); }));
+    RtHeadArgs ha{};
+    ha.pt_add = sa.sel_anchors; ha.pt_add_invsig = 0;
+    ha.points = out->enc_points ? out->enc_points : ref_buf(0);
+    CK(heads(r.enc_head, P(w.tgt), nullptr, ha));
     if (out->enc_points)
       CK((int)hipMemcpyAsync(ref_buf(0), out->enc_points, (size_t)BQ * 2 * 4, hipMemcpyDeviceToDevice, s));
   }
@@ -689,24 +718,22 @@ int spe_rtdetr_forward(spe_model* m, void* stream, const float* images, int B, v
     tgt = (tgt == w.tgt) ? w.t1d : w.tgt;          // t1d is free again once the FFN residual is read
     CK(ln("rt.ln", P(w.dtmp), e.n3g, e.n3b, P(tgt), (float*)P(w.hs), BQ));
     // heads: score, refined points sigmoid(box MLP + inverse_sigmoid(ref)), sigma (+ PostProcess)
-    HeadArgs hh = e.head;
-    hh.hs = (const float*)P(w.hs); hh.B = B; hh.Q = Q;
-    hh.pt_add = ref; hh.pt_add_invsig = 1;
+    RtHeadArgs ha{};
+    ha.pt_add = ref; ha.pt_add_invsig = 1;
     const size_t aoff = (size_t)i * BQ;
     if (last) {
-      hh.logits = out->logits; hh.points = out->points;
-      hh.log_sigmas = out->log_sigmas ? out->log_sigmas : (float*)P(w.lsig);
-      hh.clip_bbox = out->clip_bbox;
-      hh.probs = out->clip_bbox ? out->probs : nullptr;
-      hh.points_px = out->clip_bbox ? out->points_px : nullptr;
-      hh.sigmas = out->clip_bbox ? out->sigmas : nullptr;
+      ha.logits = out->logits; ha.points = out->points;
+      ha.log_sigmas = out->log_sigmas;
+      ha.clip_bbox = out->clip_bbox;
+      ha.probs = out->clip_bbox ? out->probs : nullptr;
+      ha.points_px = out->clip_bbox ? out->points_px : nullptr;
+      ha.sigmas = out->clip_bbox ? out->sigmas : nullptr;
     } else {
-      hh.logits = out->aux_logits ? out->aux_logits + aoff * C : (float*)P(w.lgt);
-      hh.points = ref_buf(i + 1);
-      hh.log_sigmas = out->aux_log_sigmas ? out->aux_log_sigmas + aoff * 2 : (float*)P(w.lsig);
-      hh.clip_bbox = nullptr; hh.probs = nullptr; hh.points_px = nullptr; hh.sigmas = nullptr;
+      ha.logits = out->aux_logits ? out->aux_logits + aoff * C : (float*)P(w.lgt);
+      ha.points = ref_buf(i + 1);
+      ha.log_sigmas = out->aux_log_sigmas ? out->aux_log_sigmas + aoff * 2 : nullptr;
     }
-    CK(run_other(m, "rt.heads", 0.0, (double)BQ * d * 4, s, [&] { return spe_launch_heads(hh, s); }));
+    CK(heads(e.head, P(tgt), (const float*)P(w.hs), ha));
     if (!last && out->aux_points)
       CK((int)hipMemcpyAsync(out->aux_points + aoff * 2, ref_buf(i + 1), (size_t)BQ * 2 * 4, hipMemcpyDeviceToDevice, s));
   }

@@ -119,8 +119,6 @@ struct HeadArgs {
   float* points;                   // [B][Q][2] crop-normalised (sigmoid)
   float* probs;                    // [B][Q][12] softmax (nullable)
   float* points_px;                // [B][Q][2] image px (nullable)
-  const float* pt_add;             // [B*Q][2] added to the point MLP output before the sigmoid
-  int pt_add_invsig;               //   (nullable; RT-DETR: anchors, or inverse_sigmoid(ref) if set)
   float* log_sigmas;               // [B][Q][2] (nullable)
   float* sigmas;                   // [B][Q][2] exp (nullable)
 };
@@ -167,7 +165,6 @@ struct RtSelectArgs {
   int lvl_start[5];                // token offsets of the levels within an image, [levels] = L
   int* topk;                       // [B][Q] selected token indices, descending score
   void* target; int ldt;           // [B*Q][D] T gathered output_memory rows
-  float* target_f32;               // [B*Q][D] the same rows in fp32 (encoder box head input)
   float* sel_logits;               // [B*Q][C]
   float* sel_anchors;              // [B*Q][2]
 };
@@ -183,3 +180,17 @@ struct RtDeformArgs {
   int lvl_h[4], lvl_w[4], lvl_rows0[4];
 };
 int spe_launch_msdeform(const RtDeformArgs& a, int dtype, hipStream_t s);
+struct RtHeadArgs {
+  int rows, Q, C;
+  const float* hs;                 // [rows][256] fp32 layer output (score head input; null: no score head)
+  const float* cls_w; const float* cls_b;   // [C][256], [C]
+  const void* h2; int ld_h2;       // T: box hidden (cols 0..255), sigma hidden (cols 256..511)
+  const float* box_w2; const float* box_b2; // [2][256], [2]
+  const float* sig_w2; const float* sig_b2; // [1][256], [1] (null: no sigma head)
+  const float* pt_add; int pt_add_invsig;   // [rows][2]: anchors, or reference points (inverse_sigmoid)
+  float* logits; float* probs;     // [rows][C]
+  float* points;                   // [rows][2] sigmoid
+  const float* clip_bbox; float* points_px;
+  float* log_sigmas; float* sigmas;         // [rows][2]
+};
+int spe_launch_head_finish(const RtHeadArgs& a, int dtype, hipStream_t s);
