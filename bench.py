@@ -223,9 +223,20 @@ def main():
         from spe.rtdetr_spec import RtdetrConfig, random_rtdetr_weights
         rcfg = RtdetrConfig(depth=18 if args.model == "rtdetr_r18" else 50, input_size=args.size,
                             num_queries=args.queries, dec_layers=args.layers)
+        from spe.synthetic import diversify_class_head
+        w = random_rtdetr_weights(rcfg, 0)
+        if args.weights == "label-diverse":
+            # RT-DETR's queries are distinct encoder tokens already; only the last score head is
+            # drawn in the principal subspace of its input (spe.synthetic.diversify_class_head)
+            m = RTDETR(rcfg, dtype=args.dtype, aux_outputs=False)
+            m.load_state_dict(w)
+            calib = synthetic_batch(SpeConfig(input_size=args.size), 16, seed=4242)["images"]
+            x = torch.from_numpy(np.concatenate([calib] * ((B + 15) // 16))[:B]).to(dev)
+            hs = m(x, return_hs=True)["hs"].cpu().numpy()[:16]
+            del m
+            w = diversify_class_head(w, hs, head=f"decoder.dec_score_head.{rcfg.dec_layers - 1}")
         model = RTDETR(rcfg, dtype=args.dtype, aux_outputs=False)
-        model.load_state_dict(random_rtdetr_weights(rcfg, 0))
-        args.weights = "random"
+        model.load_state_dict(w)
     else:
         model = DETR(cfg, dtype=args.dtype, attn_dtype=args.attn_dtype)
         model.load_state_dict(bench_weights(cfg, 0, hs_fn) if args.weights == "label-diverse" else random_weights(cfg, 0))
@@ -315,7 +326,9 @@ def main():
         return
     total_images = B * world * args.steps
     avg_ms = k_ms / max(k_n, 1)
-    mfma_bound = dominant.replace("rt.", "", 1).startswith(("conv", "gemm", "attn", "ffn", "aifi", "csp", "enc", "dec"))
+    # bound by the class's own arithmetic intensity against the ridge point (2500 TF/s / 8 TB/s
+    # = 312 flop/B): the K <= 256 1x1 convs are HBM-bound, attention / FFN / 3x3 convs MFMA-bound
+    mfma_bound = k_fl * PEAK["hbm"] * 1e9 > k_by * PEAK[args.dtype]["mfma"] * 1e12
     if mfma_bound:
         achieved = (k_fl / max(k_n, 1)) / (avg_ms * 1e-3) / 1e12
         peak = PEAK[args.dtype]["mfma"]

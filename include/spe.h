@@ -111,6 +111,7 @@ typedef struct {
   float* enc_logits;      /* [B,Q,C+1] encoder top-k logits (nullable; last aux_outputs entry) */
   float* enc_points;      /* [B,Q,2]   sigmoid(enc_bbox_head + anchors) of the selected tokens */
   int32_t* topk;          /* [B,Q] selected encoder tokens, descending score (nullable) */
+  float* hs;              /* [B,Q,256] last decoder layer output, the heads' input (nullable) */
 } spe_rtdetr_outputs;
 
 /* Create an RT-DETR model handle.  The lifecycle entry points of spe_model (set_param with the

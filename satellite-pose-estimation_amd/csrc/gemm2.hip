@@ -63,7 +63,9 @@ constexpr int P8_MIN_K = 1024;
 // NST = LDS stages: 2 (double-buffered K loop, one workgroup per CU) or 1 (load, wait,
 // multiply per K-step, LDS and registers sized for two resident workgroups per CU, so one
 // workgroup's epilogue and load latency overlap the other's work: short-K linear problems)
-template <int BN, int MODE, bool LN, bool P8K = false, int NST = 2>
+// XA: extended epilogue (SiLU / GELU, residual after the activation) for the RT-DETR encoder.
+// A separate instantiation: the extra live state made the ReLU-only tiles spill (272 B/lane).
+template <int BN, int MODE, bool LN, bool P8K = false, int NST = 2, bool XA = false>
 __global__ __launch_bounds__(NT, NST == 1 ? 4 : 1) void gemm2_kernel(GemmArgs g) {
   constexpr int WM = Cfg<BN>::WM, WN = Cfg<BN>::WN;
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
@@ -416,12 +418,18 @@ __global__ __launch_bounds__(NT, NST == 1 ? 4 : 1) void gemm2_kernel(GemmArgs g)
             for (int r = 0; r < 4 && n + r < g.N; ++r) v[r] += to_f32(rp[r]);
           }
         };
-        if (g.R && !g.res_post) add_res();
-        if (g.act) {
+        const bool rpost = XA && g.res_post;
+        if (g.R && !rpost) add_res();
+        if constexpr (XA) {
+          if (g.act) {
 #pragma unroll
-          for (int r = 0; r < 4; ++r) v[r] = apply_act(v[r], g.act);
+            for (int r = 0; r < 4; ++r) v[r] = apply_act(v[r], g.act);
+          }
+        } else if (g.act) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
         }
-        if (g.R && g.res_post) add_res();
+        if (g.R && rpost) add_res();
         if (g.out_f32) {
           float* cp = (float*)g.C + (size_t)m * g.ldc + n;
           if (full) st16(cp, pack16<float>(v));
@@ -498,7 +506,8 @@ __global__ __launch_bounds__(NT, NST == 1 ? 4 : 1) void gemm2_kernel(GemmArgs g)
               for (int e = 0; e < 8 && n + e < g.N; ++e) v[e] += to_f32(rp[e]);
             }
           };
-          if (g.R && !g.res_post) add_res();
+          const bool rpost = XA && g.res_post;
+          if (g.R && !rpost) add_res();
           if constexpr (LN) {
             // fused post-norm LayerNorm (N == BN == 256): a row's 32 column groups are the 32
             // lanes of one half-wave, so the row statistics are five xor-shuffles away
@@ -517,11 +526,16 @@ __global__ __launch_bounds__(NT, NST == 1 ? 4 : 1) void gemm2_kernel(GemmArgs g)
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = (v[e] - mean) * rs * elg[e] + elb[e];
           }
-          if (g.act) {
+          if constexpr (XA) {
+            if (g.act) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], g.act);
+              for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], g.act);
+            }
+          } else if (g.act) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
           }
-          if (g.R && g.res_post) add_res();
+          if (g.R && rpost) add_res();
           if (g.out_f32) {
             float* cp = (float*)g.C + (size_t)m * g.ldc + n;
             if (full) {
@@ -549,6 +563,14 @@ template <int BN>
 int launch_bn(const GemmArgs& g, int mode, hipStream_t s) {
   const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
   dim3 grid(tiles), block(NT);
+  if (g.act > ACT_RELU || g.res_post) {
+    if (g.ln_g) return -1;
+    if (mode == GEMM_CONV)
+      hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_CONV, false, false, 2, true>), grid, block, 0, s, g);
+    else
+      hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_LINEAR, false, false, 2, true>), grid, block, 0, s, g);
+    return (int)hipGetLastError();
+  }
   if (mode == GEMM_CONV) {
     hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_CONV, false>), grid, block, 0, s, g);
   } else {
@@ -749,7 +771,7 @@ int spe_launch_gemm2(const GemmArgs& g, int mode, hipStream_t s) {
     else hipLaunchKernelGGL(gemm_small_kernel<false>, dim3(tiles), dim3(SM_NT), 0, s, g);
     return (int)hipGetLastError();
   }
-  if (use_st1(g, mode)) return launch_st1(g, s);
+  if (use_st1(g, mode) && g.act <= ACT_RELU && !g.res_post) return launch_st1(g, s);
   const int bn = (g.N <= 64 && g.vt_T == 0) ? 64 : g.N <= 128 ? 128 : 256;   // BN 64 has no V^T store
   const int tiles = ((g.M + BM - 1) / BM) * ((g.N + bn - 1) / bn);
   // too few tiles for the large-tile kernel: the 128x128 kernel.  (169 tiles of 256x256 on the

@@ -180,6 +180,311 @@ __device__ void select_correspondences(const PnpArgs& a, int b, int lane, SelSha
   __syncthreads();
 }
 
+// ---------------------------------------------------------------- wave-parallel refinement
+// CvLevMarq (lm_refine) and the sigma-weighted Huber LM (sigma_lm) of pnp_math.h with the
+// per-point work spread over lanes.  Every lane holds the (uniform) 6-vector state; lane j
+// projects correspondence j and writes its two residual / Jacobian rows to LDS at its rank
+// among the selected points; lane e then forms normal-equation entry e by the serial loop over
+// rows, in the serial code's row order and association, so g / H / the cost are the serial
+// code's values bit for bit.  The 6x6 step is a register Cholesky on every lane (the serial code
+// solves with a Jacobi pseudo-inverse in scratch memory, which dominated the solver's time);
+// when a pivot falls below 1e-10 of the largest diagonal the wave takes the serial
+// pseudo-inverse (lane 0) instead, so rank-deficient steps keep cv::solve(DECOMP_SVD) semantics.
+struct LmShared {
+  double J[2 * MAXN][6];
+  double r[2 * MAXN];        // residual rows (lm: proj - img; sigma: w * (proj - xn))
+  double w[2 * MAXN];        // sigma: per-row weight
+  double red[48];            // reduced normal equations: H[36], g[6], cost
+  double x[6];               // fallback step
+};
+
+// S x = b for symmetric S (lower triangle read); false when S is not safely positive definite
+__device__ __forceinline__ bool chol6_solve(const double* S, const double* b, double* x) {
+  double L[6][6], y[6];
+  double maxd = 0;
+#pragma unroll
+  for (int i = 0; i < 6; ++i) maxd = fmax(maxd, fabs(S[i * 7]));
+  const double thr = maxd * 1e-10;
+#pragma unroll
+  for (int j = 0; j < 6; ++j) {
+    double s = S[j * 6 + j];
+#pragma unroll
+    for (int p = 0; p < j; ++p) s -= L[j][p] * L[j][p];
+    if (!(s > thr)) return false;
+    L[j][j] = sqrt(s);
+    const double inv = 1.0 / L[j][j];
+#pragma unroll
+    for (int i = j + 1; i < 6; ++i) {
+      double t = S[i * 6 + j];
+#pragma unroll
+      for (int p = 0; p < j; ++p) t -= L[i][p] * L[j][p];
+      L[i][j] = t * inv;
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 6; ++i) {
+    double t = b[i];
+#pragma unroll
+    for (int p = 0; p < i; ++p) t -= L[i][p] * y[p];
+    y[i] = t / L[i][i];
+  }
+#pragma unroll
+  for (int i = 5; i >= 0; --i) {
+    double t = y[i];
+#pragma unroll
+    for (int p = i + 1; p < 6; ++p) t -= L[p][i] * x[p];
+    x[i] = t / L[i][i];
+  }
+  return true;
+}
+
+__device__ void solve6_wave(LmShared& sh, const double* S, const double* b, double* x, int lane) {
+  if (chol6_solve(S, b, x)) return;        // uniform: every lane holds the same S, b
+  if (lane == 0) sym_solve(6, S, b, sh.x);
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 6; ++i) x[i] = sh.x[i];
+  __syncthreads();
+}
+
+// One correspondence per lane: its world point, pixel observation and row rank (-1 = unused).
+struct LmPoint {
+  double M[3], obs[2], sig[2];
+  int row;
+};
+
+__device__ LmPoint lm_point(const float* img_f, const float* wld_f, const float* sig_f, int nl, uint32_t mask,
+                            int lane) {
+  LmPoint p{};
+  p.row = -1;
+  if (lane < nl && (mask >> lane) & 1u) {
+    p.row = __popc(mask & ((1u << lane) - 1u));
+    for (int c = 0; c < 3; ++c) p.M[c] = wld_f[3 * lane + c];
+    for (int c = 0; c < 2; ++c) { p.obs[c] = img_f[2 * lane + c]; p.sig[c] = sig_f ? sig_f[2 * lane + c] : 1.0; }
+  }
+  return p;
+}
+
+// project_jac for this lane's point (k: camera; unit camera for normalised coordinates)
+__device__ __forceinline__ void lm_project(const cam_t* k, const double* R, const double* dRdr, const double* t,
+                                           const LmPoint& pt, double* proj, double (*J)[6]) {
+  const double* M = pt.M;
+  double X = R[0] * M[0] + R[1] * M[1] + R[2] * M[2] + t[0];
+  double Y = R[3] * M[0] + R[4] * M[1] + R[5] * M[2] + t[1];
+  double Z = R[6] * M[0] + R[7] * M[1] + R[8] * M[2] + t[2];
+  double z = Z ? 1. / Z : 1;
+  double x = X * z, y = Y * z;
+  proj[0] = x * k->fx + k->cx;
+  proj[1] = y * k->fy + k->cy;
+  if (!J) return;
+#pragma unroll
+  for (int j = 0; j < 3; ++j) {
+    const double* d = dRdr + 9 * j;
+    double dX = d[0] * M[0] + d[1] * M[1] + d[2] * M[2];
+    double dY = d[3] * M[0] + d[4] * M[1] + d[5] * M[2];
+    double dZ = d[6] * M[0] + d[7] * M[1] + d[8] * M[2];
+    J[0][j] = k->fx * (z * dX - x * z * dZ);
+    J[1][j] = k->fy * (z * dY - y * z * dZ);
+  }
+  J[0][3] = k->fx * z; J[0][4] = 0; J[0][5] = -k->fx * x * z;
+  J[1][3] = 0; J[1][4] = k->fy * z; J[1][5] = -k->fy * y * z;
+}
+
+// lm_refine (pnp_math.h) over the selected correspondences, all lanes; result uniform
+__device__ void lm_refine_wave(LmShared& sh, const cam_t* k, const LmPoint& pt, int n, double* rvec, double* tvec,
+                               int lane) {
+  double param[6] = {rvec[0], rvec[1], rvec[2], tvec[0], tvec[1], tvec[2]}, prev[6];
+  double JtJ[36], JtErr[6];
+  int lambdaLg10 = -3, iters = 0;
+  double prevErrNorm = DBL_MAX;
+  const int m = 2 * n;
+  // rows of the current param: residual (+ Jacobian) of this lane's point
+  auto rows = [&](const double* p, bool jac) {
+    double R[9], dRdr[27], proj[2], J[2][6];
+    rodrigues_r2R(p, R);
+    if (jac) rodrigues_jac(p, dRdr);
+    if (pt.row >= 0) {
+      lm_project(k, R, dRdr, p + 3, pt, proj, jac ? J : nullptr);
+      for (int a = 0; a < 2; ++a) {
+        sh.r[2 * pt.row + a] = proj[a] - pt.obs[a];
+        if (jac)
+          for (int c = 0; c < 6; ++c) sh.J[2 * pt.row + a][c] = J[a][c];
+      }
+    }
+    __syncthreads();
+  };
+  auto err_norm = [&]() {     // serial sum of squares, every lane (LDS broadcast reads)
+    double s = 0;
+    for (int i = 0; i < m; ++i) { double r = sh.r[i]; s += r * r; }
+    return sqrt(s);
+  };
+  rows(param, true);
+  for (;;) {
+    if (lane < 42) {          // normal-equation entry per lane, serial row order
+      double s = 0;
+      if (lane < 36) {
+        const int a = lane / 6, b = lane % 6;
+        for (int i = 0; i < m; ++i) s += sh.J[i][a] * sh.J[i][b];
+      } else {
+        const int a = lane - 36;
+        for (int i = 0; i < m; ++i) s += sh.J[i][a] * sh.r[i];
+      }
+      sh.red[lane] = s;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int e = 0; e < 36; ++e) JtJ[e] = sh.red[e];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) JtErr[a] = sh.red[36 + a];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) prev[a] = param[a];
+    if (iters == 0) prevErrNorm = err_norm();
+    __syncthreads();
+    double errNorm;
+    for (;;) {
+      double lambda = det_pow10i(lambdaLg10);
+      double S[36], dx[6];
+#pragma unroll
+      for (int e = 0; e < 36; ++e) S[e] = JtJ[e];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) S[i * 6 + i] *= 1. + lambda;
+      solve6_wave(sh, S, JtErr, dx, lane);
+#pragma unroll
+      for (int i = 0; i < 6; ++i) param[i] = prev[i] - dx[i];
+      rows(param, false);
+      errNorm = err_norm();
+      __syncthreads();
+      if (errNorm > prevErrNorm && ++lambdaLg10 <= 16) continue;
+      break;
+    }
+    lambdaLg10 = lambdaLg10 - 1 > -16 ? lambdaLg10 - 1 : -16;
+    double dn = 0, pn = 0;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) { dn += (param[i] - prev[i]) * (param[i] - prev[i]); pn += prev[i] * prev[i]; }
+    double rel = sqrt(dn) / (sqrt(pn) + DBL_EPSILON);
+    if (++iters >= 20 || rel < FLT_EPSILON) break;
+    prevErrNorm = errNorm;
+    rows(param, true);
+  }
+  for (int c = 0; c < 3; ++c) { rvec[c] = param[c]; tvec[c] = param[3 + c]; }
+}
+
+// the pose on lane 0 (epnp_solve_wave / the RANSAC replay) -> every lane
+__device__ void bcast_pose(LmShared& sh, double* rvec, double* tvec, int lane) {
+  if (lane == 0)
+    for (int c = 0; c < 3; ++c) { sh.x[c] = rvec[c]; sh.x[3 + c] = tvec[c]; }
+  __syncthreads();
+  for (int c = 0; c < 3; ++c) { rvec[c] = sh.x[c]; tvec[c] = sh.x[3 + c]; }
+  __syncthreads();
+}
+
+// sigma_lm (pnp_math.h) over the selected correspondences, all lanes; result uniform
+__device__ void sigma_lm_wave(LmShared& sh, const cam_t* k, const LmPoint& pt, int n, double delta, double* rvec,
+                              double* tvec, int lane) {
+  const int m = 2 * n;
+  double xn[2] = {0, 0}, w[2] = {0, 0};
+  if (pt.row >= 0)
+    for (int a = 0; a < 2; ++a) {
+      xn[a] = (float)((pt.obs[a] - (a ? k->cy : k->cx)) * (1. / (a ? k->fy : k->fx)));
+      w[a] = 1. / (sqrt(pt.sig[a]) + 1e-6);
+      sh.w[2 * pt.row + a] = w[a];
+    }
+  __syncthreads();
+  double sum[2] = {0, 0};
+  for (int i = 0; i < n; ++i) { sum[0] += sh.w[2 * i]; sum[1] += sh.w[2 * i + 1]; }
+  __syncthreads();
+  if (pt.row >= 0)
+    for (int a = 0; a < 2; ++a) { w[a] /= sum[a]; sh.w[2 * pt.row + a] = w[a]; }
+  const cam_t unit = {1, 1, 0, 0};
+  double param[6] = {rvec[0], rvec[1], rvec[2], tvec[0], tvec[1], tvec[2]};
+  double mu = 1e-4, nu = 2;
+  double cost_prev = 0;
+  const double d2 = delta * delta;
+  for (int it = 0; it < 20; ++it) {
+    {
+      double R[9], dRdr[27], proj[2], J[2][6];
+      rodrigues_r2R(param, R);
+      rodrigues_jac(param, dRdr);
+      if (pt.row >= 0) {
+        lm_project(&unit, R, dRdr, param + 3, pt, proj, J);
+        for (int a = 0; a < 2; ++a) {
+          sh.r[2 * pt.row + a] = w[a] * (proj[a] - xn[a]);
+          for (int c = 0; c < 6; ++c) sh.J[2 * pt.row + a][c] = J[a][c];
+        }
+      }
+    }
+    __syncthreads();
+    if (lane < 43) {          // H[a][b] (36, not symmetric bitwise), g[a] (6), cost: serial row order
+      double s = 0;
+      for (int i = 0; i < m; ++i) {
+        const double r = sh.r[i], r2 = r * r, wi = sh.w[i];
+        double rho1 = 1;
+        if (r2 > d2) {
+          double q = sqrt(r2);
+          rho1 = delta / q;
+          if (lane == 42) s += 2 * delta * q - d2;
+        } else if (lane == 42) {
+          s += r2;
+        }
+        if (lane < 36) {
+          const int a = lane / 6, b = lane % 6;
+          const double ja = wi * sh.J[i][a];
+          s += rho1 * ja * wi * sh.J[i][b];
+        } else if (lane < 42) {
+          const double ja = wi * sh.J[i][lane - 36];
+          s += rho1 * ja * r;
+        }
+      }
+      sh.red[lane] = s;
+    }
+    __syncthreads();
+    double H[36], g[6], cost;
+#pragma unroll
+    for (int e = 0; e < 36; ++e) H[e] = sh.red[e];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) g[a] = sh.red[36 + a];
+    cost = sh.red[42];
+    __syncthreads();
+    if (it == 0) cost_prev = cost;
+    double S[36], dx[6], trial[6];
+#pragma unroll
+    for (int e = 0; e < 36; ++e) S[e] = H[e];
+#pragma unroll
+    for (int a = 0; a < 6; ++a) S[a * 6 + a] += mu * (H[a * 6 + a] > 1e-12 ? H[a * 6 + a] : 1e-12);
+    solve6_wave(sh, S, g, dx, lane);
+#pragma unroll
+    for (int a = 0; a < 6; ++a) trial[a] = param[a] - dx[a];
+    {
+      double R[9], proj[2];
+      rodrigues_r2R(trial, R);
+      if (pt.row >= 0) {
+        lm_project(&unit, R, nullptr, trial + 3, pt, proj, nullptr);
+        for (int a = 0; a < 2; ++a) sh.r[2 * pt.row + a] = w[a] * (proj[a] - xn[a]);
+      }
+    }
+    __syncthreads();
+    double cost_new = 0;
+    for (int i = 0; i < m; ++i) {
+      double r = sh.r[i], r2 = r * r;
+      cost_new += r2 > d2 ? 2 * delta * sqrt(r2) - d2 : r2;
+    }
+    __syncthreads();
+    if (cost_new < cost_prev) {
+#pragma unroll
+      for (int a = 0; a < 6; ++a) param[a] = trial[a];
+      double dn = 0, pn = 0;
+#pragma unroll
+      for (int a = 0; a < 6; ++a) { dn += dx[a] * dx[a]; pn += param[a] * param[a]; }
+      mu *= 1. / 3.; nu = 2;
+      if (cost_prev - cost_new < 1e-6 * cost_prev || sqrt(dn) < 1e-8 * (sqrt(pn) + 1e-8)) { cost_prev = cost_new; break; }
+      cost_prev = cost_new;
+    } else {
+      mu *= nu; nu *= 2;
+    }
+  }
+  for (int c = 0; c < 3; ++c) { rvec[c] = param[c]; tvec[c] = param[3 + c]; }
+}
+
 // The cv::RNG((uint64)-1) subset stream of OpenCV's RANSACPointSetRegistrator: `mp` distinct
 // indices in [0, nl) per iteration, rejection-sampled, iterations drawn in order.
 __device__ void draw_subset(rng_t* rng, int nl, int mp, int* idx) {
@@ -258,6 +563,7 @@ __global__ __launch_bounds__(WAVE) void pnp_kernel(PnpArgs a) {
   __shared__ uint32_t s_mask[MAXIT];
   __shared__ double s_rt[MAXIT][6];
   __shared__ EpnpShared s_ep;
+  __shared__ LmShared s_lm;
 
   const cam_t k = {a.K[0], a.K[4], a.K[2], a.K[5]};
 
@@ -276,11 +582,9 @@ __global__ __launch_bounds__(WAVE) void pnp_kernel(PnpArgs a) {
     status = SPE_PNP_CV_ERROR;
   } else if (a.mode == SPE_PNP_EPNP || a.mode == SPE_PNP_EPNP_LM) {
     epnp_solve_wave(s_ep, &k, s_img, s_wld, nl, all, 1, rvec, t, lane);
-    if (lane == 0 && a.mode == SPE_PNP_EPNP_LM) {
-      double wd[3 * MAXN], id[2 * MAXN];
-      for (int i = 0; i < 3 * nl; ++i) wd[i] = s_wld[i];
-      for (int i = 0; i < 2 * nl; ++i) id[i] = s_img[i];
-      lm_refine(&k, nl, wd, id, rvec, t);
+    if (a.mode == SPE_PNP_EPNP_LM) {
+      bcast_pose(s_lm, rvec, t, lane);
+      lm_refine_wave(s_lm, &k, lm_point(s_img, s_wld, nullptr, nl, all, lane), nl, rvec, t, lane);
     }
     inl = all;
     have_pose = true;
@@ -391,17 +695,12 @@ __global__ __launch_bounds__(WAVE) void pnp_kernel(PnpArgs a) {
       if (verdict == 2) status = SPE_PNP_RANSAC_FALLBACK;
       if (verdict == 0) status = SPE_PNP_UNPINNED;
     }
-    if (ok && lane == 0) {
-      double wi[3 * MAXN], ii[2 * MAXN], sg[2 * MAXN];
-      int m = 0;
-      for (int i = 0; i < nl; ++i)
-        if (inl & (1u << i)) {
-          for (int c = 0; c < 3; ++c) wi[3 * m + c] = s_wld[3 * i + c];
-          for (int c = 0; c < 2; ++c) { ii[2 * m + c] = s_img[2 * i + c]; sg[2 * m + c] = s_sig[2 * i + c]; }
-          m++;
-        }
-      if (a.mode == SPE_PNP_RANSAC_P3P_LM) lm_refine(&k, m, wi, ii, rvec, t);
-      else sigma_lm(&k, m, wi, ii, sg, 0.005, rvec, t);
+    if (ok) {                                     // wave-uniform
+      bcast_pose(s_lm, rvec, t, lane);
+      const LmPoint pt = lm_point(s_img, s_wld, s_sig, nl, inl, lane);
+      const int m = __popc(inl);
+      if (a.mode == SPE_PNP_RANSAC_P3P_LM) lm_refine_wave(s_lm, &k, pt, m, rvec, t, lane);
+      else sigma_lm_wave(s_lm, &k, pt, m, 0.005, rvec, t, lane);
     }
     have_pose = status == SPE_PNP_OK || status == SPE_PNP_RANSAC_FALLBACK;
   }

@@ -734,6 +734,8 @@ int spe_rtdetr_forward(spe_model* m, void* stream, const float* images, int B, v
       ha.log_sigmas = out->aux_log_sigmas ? out->aux_log_sigmas + aoff * 2 : nullptr;
     }
     CK(heads(e.head, P(tgt), (const float*)P(w.hs), ha));
+    if (last && out->hs)
+      CK((int)hipMemcpyAsync(out->hs, P(w.hs), (size_t)BQ * 256 * 4, hipMemcpyDeviceToDevice, s));
     if (!last && out->aux_points)
       CK((int)hipMemcpyAsync(out->aux_points + aoff * 2, ref_buf(i + 1), (size_t)BQ * 2 * 4, hipMemcpyDeviceToDevice, s));
   }

@@ -52,7 +52,7 @@ class RtdetrConfig(ctypes.Structure):
 class RtdetrOutputs(ctypes.Structure):
     _fields_ = [("logits", P), ("points", P), ("log_sigmas", P), ("clip_bbox", P), ("probs", P), ("points_px", P),
                 ("sigmas", P), ("aux_logits", P), ("aux_points", P), ("aux_log_sigmas", P), ("enc_logits", P),
-                ("enc_points", P), ("topk", P)]
+                ("enc_points", P), ("topk", P), ("hs", P)]
 
 
 class SpeError(RuntimeError):

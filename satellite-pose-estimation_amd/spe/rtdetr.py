@@ -83,10 +83,11 @@ class RTDETR(nn.Module):
                 self._ws[key] = ws = (torch.empty(int(nbytes), dtype=torch.uint8, device=device), B)
         return ws[0]
 
-    def forward(self, samples, clip_bbox=None, stream=None, aux=None):
+    def forward(self, samples, clip_bbox=None, stream=None, aux=None, return_hs=False):
         """rtdetr.py:36-53 in eval.  Returns pred_logits [B,Q,C+1], pred_pts [B,Q,2], pred_sigmas
         [B,Q,2] (raw) and, with aux, the reference's aux_outputs list.  Passing `clip_bbox`
-        ([B,4] device) also runs the fused RTDETRPostProcessor: probs, points_px, sigmas."""
+        ([B,4] device) also runs the fused RTDETRPostProcessor: probs, points_px, sigmas.
+        return_hs adds "hs" [B,Q,256], the last decoder layer's output (the heads' input)."""
         if not self._ready:
             raise RuntimeError("RTDETR: load_state_dict() with every parameter before forward()")
         aux = self.aux_outputs if aux is None else aux
@@ -115,10 +116,12 @@ class RTDETR(nn.Module):
             topk = torch.empty(B, Q, dtype=torch.int32, device=dev)
         else:
             al = ap = asg = el = ep = topk = None
+        if return_hs:
+            out["hs"] = torch.empty(B, Q, 256, **f)
         o = _lib.RtdetrOutputs(_lib.ptr(out["pred_logits"]), _lib.ptr(out["pred_pts"]), _lib.ptr(out["pred_sigmas"]),
                                _lib.ptr(clip_bbox), _lib.ptr(out.get("probs")), _lib.ptr(out.get("points_px")),
                                _lib.ptr(out.get("sigmas")), _lib.ptr(al), _lib.ptr(ap), _lib.ptr(asg), _lib.ptr(el),
-                               _lib.ptr(ep), _lib.ptr(topk))
+                               _lib.ptr(ep), _lib.ptr(topk), _lib.ptr(out.get("hs")))
         ws = self.workspace(B, dev, stream)
         _lib.check(_lib.lib().spe_rtdetr_forward(self._h, _lib.stream_ptr(stream), _lib.ptr(images), B, _lib.ptr(ws),
                                                  ws.numel(), ctypes.byref(o)), "spe_rtdetr_forward")

@@ -205,16 +205,17 @@ def sharpen_decoder(w, cfg: SpeConfig, factor: float = 64.0):
     return w
 
 
-def diversify_class_head(w, hs, seed: int = 1, k: int = 12, logit_scale: float = 6.0):
-    """hs: [N, d] decoder outputs (after decoder_norm) of a calibration batch."""
+def diversify_class_head(w, hs, seed: int = 1, k: int = 12, logit_scale: float = 6.0, head: str = "cls_embed"):
+    """hs: [N, d] decoder outputs (after decoder_norm) of a calibration batch; head: the class
+    head's state_dict prefix (RT-DETR: decoder.dec_score_head.<last layer>)."""
     hs = np.asarray(hs, np.float64).reshape(-1, hs.shape[-1])
     mu = hs.mean(0)
     _, S, Vt = np.linalg.svd(hs - mu, full_matrices=False)
     k = min(k, len(S))
-    G = np.random.Generator(np.random.PCG64(seed)).normal(size=(12, k))
+    G = np.random.Generator(np.random.PCG64(seed)).normal(size=(w[f"{head}.weight"].shape[0], k))
     W = G @ (Vt[:k] / np.maximum(S[:k, None], 1e-12)) * logit_scale * np.sqrt(hs.shape[0])
-    w["cls_embed.weight"] = W.astype(np.float32)
-    w["cls_embed.bias"] = (-W @ mu).astype(np.float32)
+    w[f"{head}.weight"] = W.astype(np.float32)
+    w[f"{head}.bias"] = (-W @ mu).astype(np.float32)
     return w
 
 

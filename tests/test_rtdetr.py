@@ -156,3 +156,19 @@ def test_hip_batch_independence(gpu_device):
     torch.cuda.synchronize()
     np.testing.assert_array_equal(full["topk"][1:3].cpu().numpy(), part["topk"].cpu().numpy())
     assert (full["pred_pts"][1:3] - part["pred_pts"]).abs().max().item() <= 1e-5
+
+
+@pytest.mark.gpu
+def test_hip_hs_output_feeds_score_head(gpu_device):
+    """The optional hs output is the last decoder layer's output: the reference's last score head
+    (rtdetr_decoder.py dec_score_head[-1]) applied to it gives pred_logits."""
+    g, cfg = _golden("r18_s128")
+    m = _hip_model(cfg, "fp32", int(g["weight_seed"]))
+    w = random_rtdetr_weights(cfg, int(g["weight_seed"]))
+    b = synthetic_batch(SpeConfig(input_size=cfg.input_size), int(g["batch"]), int(g["image_seed"]))
+    o = m(torch.from_numpy(b["images"]).to(gpu_device), return_hs=True)
+    torch.cuda.synchronize()
+    hs = o["hs"].cpu().numpy().astype(np.float64)
+    k = f"decoder.dec_score_head.{cfg.dec_layers - 1}"
+    logits = hs @ w[f"{k}.weight"].T.astype(np.float64) + w[f"{k}.bias"]
+    assert np.abs(logits - o["pred_logits"].cpu().numpy()).max() <= 1e-4
