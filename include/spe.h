@@ -254,6 +254,12 @@ int spe_debug_ffn(void* stream, const void* x, int ldx, const void* w1, int ld1,
 int spe_debug_xattn(void* stream, const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* u,
                     int ldu, const void* wv, const float* bv, void* o, int ldo, int B, int Q, int T, int splits,
                     float* partial_scratch);
+/* upconv (bf16 models' neck, replaces the upsample + conv pair of REV/models/backbone.py:141
+ * s16_latern(up16sto8s(xs16))): z [B*H*W][9*C] holds the per-tap products W_t . x at the low
+ * resolution (t = kh*3 + kw); out [B][2H][2W] rows of stride ldo receive conv3x3(pad 1) of the
+ * align_corners bilinear x2 upsample, i.e. sum over in-grid taps of the bilinear interpolation
+ * of z's tap block.  C % 8 == 0 (bf16) / C % 4 == 0 (fp32). */
+int spe_debug_upconv(void* stream, int dtype, const void* z, void* out, int ldo, int B, int H, int W, int C);
 
 #ifdef __cplusplus
 }

@@ -54,6 +54,12 @@ int spe_debug_ffn(void* stream, const void* x, int ldx, const void* w1, int ld1,
   return rc < 0 ? spe_fail(SPE_E_LAUNCH, "ffn launch rejected its arguments") : rc;
 }
 
+int spe_debug_upconv(void* stream, int dtype, const void* z, void* out, int ldo, int B, int H, int W, int C) {
+  if (!z || !out || B < 0 || H < 1 || W < 1 || C < 1) return spe_fail(SPE_E_ARG, "bad argument");
+  int rc = spe_launch_upconv_combine(z, out, ldo, B, H, W, C, dtype, (hipStream_t)stream);
+  return rc < 0 ? spe_fail(SPE_E_LAUNCH, "upconv launch rejected its arguments") : rc;
+}
+
 int spe_debug_xattn(void* stream, const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* u,
                     int ldu, const void* wv, const float* bv, void* o, int ldo, int B, int Q, int T, int splits,
                     float* partial_scratch) {

@@ -88,6 +88,59 @@ __global__ void upsample_kernel(const T* __restrict__ in, T* __restrict__ out, i
   }
 }
 
+// 3x3 / pad 1 conv over the align_corners bilinear x2 upsample of x, by linearity evaluated at
+// the low resolution: Z[p][t*C + c] = (W_t . x[p])[c] for each tap t = (dy+1)*3 + (dx+1) (one
+// GEMM with N = 9C), then
+//   out[Y][X][c] = sum_t [U = Y+dy, V = X+dx inside the 2h x 2w grid] bilerp(Z[.][t*C + c], U, V)
+// with bilerp the upsample kernel's weights above.  (REV/models/backbone.py:141
+// s16_latern(up16sto8s(xs16)): 4x fewer MFMA flops and no 2h x 2w x Cin intermediate.)
+// One thread per 8 output channels of one output pixel; fp32 sums, one rounding at the store.
+template <typename T>
+__global__ void upconv_combine_kernel(const T* __restrict__ z, T* __restrict__ out, int ldo, int B, int H, int W, int C) {
+  constexpr int CE = Chunk<T>::CE;
+  const int Ho = 2 * H, Wo = 2 * W, cch = C / CE;
+  const size_t ldz = (size_t)9 * C;
+  const float sy = Ho > 1 ? (float)(H - 1) / (float)(Ho - 1) : 0.f;
+  const float sx = Wo > 1 ? (float)(W - 1) / (float)(Wo - 1) : 0.f;
+  const size_t n = (size_t)B * Ho * Wo * cch;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const int c = (int)(i % cch);
+    size_t r = i / cch;
+    const int ox = (int)(r % Wo); r /= Wo;
+    const int oy = (int)(r % Ho);
+    const int b = (int)(r / Ho);
+    const T* zb = z + (size_t)b * H * W * ldz + c * CE;
+    float acc[CE];
+#pragma unroll
+    for (int e = 0; e < CE; ++e) acc[e] = 0.f;
+#pragma unroll
+    for (int dy = -1; dy <= 1; ++dy) {
+      const int U = oy + dy;
+      if (U < 0 || U >= Ho) continue;
+      const float fy = U * sy;
+      const int y0 = (int)fy, y1 = y0 + (y0 < H - 1);
+      const float ly = fy - y0, hy = 1.f - ly;
+#pragma unroll
+      for (int dx = -1; dx <= 1; ++dx) {
+        const int V = ox + dx;
+        if (V < 0 || V >= Wo) continue;
+        const float fx = V * sx;
+        const int x0 = (int)fx, x1 = x0 + (x0 < W - 1);
+        const float lx = fx - x0, hx = 1.f - lx;
+        const T* zt = zb + (size_t)((dy + 1) * 3 + dx + 1) * C;
+        float a[CE], bb[CE], cc[CE], d[CE];
+        unpack16<T>(ld16(zt + ((size_t)y0 * W + x0) * ldz), a);
+        unpack16<T>(ld16(zt + ((size_t)y0 * W + x1) * ldz), bb);
+        unpack16<T>(ld16(zt + ((size_t)y1 * W + x0) * ldz), cc);
+        unpack16<T>(ld16(zt + ((size_t)y1 * W + x1) * ldz), d);
+#pragma unroll
+        for (int e = 0; e < CE; ++e) acc[e] += hy * (hx * a[e] + lx * bb[e]) + ly * (hx * cc[e] + lx * d[e]);
+      }
+    }
+    st16(out + (((size_t)b * Ho + oy) * Wo + ox) * ldo + c * CE, pack16<T>(acc));
+  }
+}
+
 // D = 256: each lane owns 4 consecutive features.
 template <typename T>
 __global__ void layernorm_kernel(const T* __restrict__ x, const float* __restrict__ gamma, const float* __restrict__ beta,
@@ -152,6 +205,17 @@ int spe_launch_upsample2x(const void* in, void* out, int B, int H, int W, int C,
     hipLaunchKernelGGL(upsample_kernel<bf16>, grid_for(n, 256), 256, 0, s, (const bf16*)in, (bf16*)out, B, H, W, C);
   else
     hipLaunchKernelGGL(upsample_kernel<float>, grid_for(n, 256), 256, 0, s, (const float*)in, (float*)out, B, H, W, C);
+  return (int)hipGetLastError();
+}
+
+int spe_launch_upconv_combine(const void* z, void* out, int ldo, int B, int H, int W, int C, int dtype, hipStream_t s) {
+  const int ce = dtype == SPE_DTYPE_BF16 ? 8 : 4;
+  if (C % ce || ldo % ce || ldo < C) return -5;
+  const size_t n = (size_t)B * 4 * H * W * (C / ce);
+  if (dtype == SPE_DTYPE_BF16)
+    hipLaunchKernelGGL(upconv_combine_kernel<bf16>, grid_for(n, 256), 256, 0, s, (const bf16*)z, (bf16*)out, ldo, B, H, W, C);
+  else
+    hipLaunchKernelGGL(upconv_combine_kernel<float>, grid_for(n, 256), 256, 0, s, (const float*)z, (float*)out, ldo, B, H, W, C);
   return (int)hipGetLastError();
 }
 

@@ -223,11 +223,21 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
     g.bias = nullptr;
     CK(run_gemm(m, "conv.neck", g, GEMM_LINEAR, s));
   }
+  if (spe_use_upconv(m)) {
+    // s16_latern(up16sto8s(xs16)) at the low resolution: Z = xs16 . [W_t]^T for the 9 taps
+    // (w.up holds Z [B*(S/16)^2][9*256]), then the bilinear combine into channels [256,512)
+    const int h = S / 16, nz = m->s16taps.N;
+    GemmArgs g = linear_args(m->s16taps, P(xs16), 1024, B * h * h, P(w.up), nz);
+    CK(run_gemm(m, "conv.neck", g, GEMM_LINEAR, s));
+    const double by = ((double)B * h * h * nz + (double)B * 4 * h * h * 256) * m->esz;
+    CK(run_other(m, "eltwise.upconv", 0.0, by, s, [&] { return spe_launch_upconv_combine(P(w.up), (char*)P(w.cat) + 256 * m->esz, 512, B, h, h, 256, dt, s); }));
+  } else {
   CK(run_other(m, "eltwise.upsample", 0.0, (double)B * 1024 * 5 * (S / 16) * (S / 16) * m->esz, s, [&] { return spe_launch_upsample2x(P(xs16), P(w.up), B, S / 16, S / 16, 1024, dt, s); }));
   {  // s16_latern 3x3 1024->256 into channels [256,512)
     GemmArgs g = conv_args(m->s16, P(w.up), B, F, F, (char*)P(w.cat) + 256 * m->esz, 512);
     g.bias = nullptr;
     CK(run_gemm(m, "conv.neck", g, GEMM_CONV, s));
+  }
   }
   {  // output_conv 3x3 512->512 + bias
     GemmArgs g = conv_args(m->outc, P(w.cat), B, F, F, P(w.neck), 512);

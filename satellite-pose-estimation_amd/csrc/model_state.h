@@ -115,6 +115,7 @@ struct spe_model {
   size_t dbytes = 0, dused = 0;
   int upload_err = 0;
   Conv stem, s8, s16, outc, inproj, crossK, crossV;
+  Conv s16taps;            // bf16 models: s16_latern as 9 per-tap [256][1024] blocks (spe_use_upconv)
   std::vector<Block> blocks;
   std::vector<Enc> enc;
   std::vector<Dec> dec;
@@ -137,5 +138,10 @@ inline bool spe_use_xattn(const spe_model* m) {
   const auto& c = m->cfg;
   return c.dtype == SPE_DTYPE_BF16_ && c.hidden_dim == 256 && c.nheads == 8 && c.dim_feedforward % 32 == 0 &&
          c.enc_layers > 0;
+}
+// bf16 models evaluate s16_latern(up16sto8s(xs16)) at the low resolution (one per-tap GEMM +
+// upconv_combine); the fp32 parity mode keeps the reference's upsample-then-conv order
+inline bool spe_use_upconv(const spe_model* m) {
+  return m->cfg.dtype == SPE_DTYPE_BF16_ && m->cfg.input_size % 16 == 0;
 }
 Ws spe_plan(const spe_model* m, int B);

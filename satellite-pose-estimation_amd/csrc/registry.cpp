@@ -324,6 +324,25 @@ int build_device(spe_model* m) {
     }
   m->s8 = make_conv(m, "backbone.0.s8_latern.weight", "", "", 0, 1, 0);
   m->s16 = make_conv(m, "backbone.0.s16_latern.weight", "", "", 0, 1, 1);
+  m->s16taps = Conv{};
+  if (spe_use_upconv(m)) {
+    // per-tap rows for the low-resolution form of s16_latern(up16sto8s(x)) (elementwise.hip
+    // upconv_combine): row t*256 + co = weight[co][:][kh][kw], t = kh*3 + kw
+    const auto sh = param_shape(m, "backbone.0.s16_latern.weight");
+    const int co_n = (int)sh[0], ci_n = (int)sh[1];
+    std::vector<float> rows;
+    if (m->dmem) {
+      const auto& src = m->host["backbone.0.s16_latern.weight"];
+      rows.assign((size_t)9 * co_n * ci_n, 0.f);
+      for (int t = 0; t < 9; ++t)
+        for (int co = 0; co < co_n; ++co)
+          for (int ci = 0; ci < ci_n; ++ci)
+            rows[((size_t)t * co_n + co) * ci_n + ci] = src[((size_t)co * ci_n + ci) * 9 + t];
+    }
+    Conv& c = m->s16taps;
+    c.N = 9 * co_n; c.K = ci_n; c.Kpad = pad64(ci_n); c.Cin = ci_n;
+    c.w = upload_rows(m, rows, c.N, c.K, c.Kpad);
+  }
   m->outc = make_conv(m, "backbone.0.output_conv.weight", "", "backbone.0.output_conv.bias", 0, 1, 1);
   m->inproj = make_conv(m, "input_proj.weight", "", "input_proj.bias", 0, 1, 0);
 

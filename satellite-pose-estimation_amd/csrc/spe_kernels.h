@@ -101,6 +101,9 @@ int spe_launch_pack_input(const float* img, void* out, int B, int S, int dtype, 
 int spe_launch_maxpool3s2(const void* in, void* out, int B, int H, int W, int C, int Ho, int Wo,
                           int dtype, hipStream_t s);
 int spe_launch_upsample2x(const void* in, void* out, int B, int H, int W, int C, int dtype, hipStream_t s);
+// conv3x3(pad 1)(upsample2x(x)) from the per-tap low-resolution products z [B*H*W][9*C]
+// (elementwise.hip); out rows of stride ldo (a channel slice of a concat buffer)
+int spe_launch_upconv_combine(const void* z, void* out, int ldo, int B, int H, int W, int C, int dtype, hipStream_t s);
 int spe_launch_layernorm(const void* x, const float* gamma, const float* beta, void* out, float* out_f32,
                          int M, int D, int dtype, hipStream_t s);
 

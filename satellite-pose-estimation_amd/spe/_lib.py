@@ -30,7 +30,7 @@ EXPORTS = ["spe_abi_version", "spe_last_error", "spe_model_create", "spe_model_d
            "spe_model_num_params", "spe_model_param_name", "spe_model_finalize", "spe_model_workspace_bytes",
            "spe_forward", "spe_forward_stages", "spe_preprocess", "spe_criterion", "spe_ensemble_fuse", "spe_postprocess", "spe_pnp_batch", "spe_self_assess", "spe_speed_score", "spe_model_profile_begin",
            "spe_model_profile_end", "spe_model_profile_get", "spe_debug_gemm", "spe_debug_attention",
-           "spe_debug_layernorm", "spe_debug_ffn", "spe_debug_xattn", "spe_rtdetr_create", "spe_rtdetr_forward"]
+           "spe_debug_layernorm", "spe_debug_ffn", "spe_debug_xattn", "spe_debug_upconv", "spe_rtdetr_create", "spe_rtdetr_forward"]
 
 
 class ModelConfig(ctypes.Structure):
@@ -99,6 +99,7 @@ def lib():
     L.spe_debug_layernorm.argtypes = [P, I, P, P, P, P, P, I, I]
     L.spe_debug_ffn.argtypes = [P, P, I, P, I, P, P, I, P, P, P, P, I, I, I, I, P, I]
     L.spe_debug_xattn.argtypes = [P, P, I, P, I, P, I, P, I, P, P, P, I, I, I, I, I, P]
+    L.spe_debug_upconv.argtypes = [P, I, P, P, I, I, I, I, I]
     L.spe_rtdetr_create.argtypes = [ctypes.POINTER(RtdetrConfig), ctypes.POINTER(P)]
     L.spe_rtdetr_forward.argtypes = [P, P, P, I, P, I64, ctypes.POINTER(RtdetrOutputs)]
     if L.spe_abi_version() != 4:

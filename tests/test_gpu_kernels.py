@@ -471,3 +471,29 @@ def test_layernorm(gpu_device, dtype):
     ref = F.layer_norm(x.float(), (256,), gam, bet, 1e-5)
     _close(out32, ref, 1e-5)
     _close(out, ref, tol)
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32"])
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 26, 26, 1024, 256), (3, 5, 7, 64, 16), (1, 1, 3, 32, 8)])
+def test_upconv_low_resolution(gpu_device, dtype, B, H, W, Cin, Cout):
+    """bf16 neck: conv3x3(pad 1)(UpsamplingBilinear2d(x2)(x)) (REV/models/backbone.py:141) as one
+    per-tap GEMM at the low resolution + spe_debug_upconv's bilinear combine, written into a
+    channel slice of a wider concat buffer, against torch's upsample-then-conv in fp32."""
+    _, dt, tol = DT[dtype]
+    g = torch.Generator(device="cpu").manual_seed(B * H + Cin + W)
+    x = torch.randn(B, Cin, H, W, generator=g).to(gpu_device, dt)
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) / (Cin * 9) ** 0.5).to(gpu_device, dt)
+    ref = F.conv2d(F.interpolate(x.float(), scale_factor=2, mode="bilinear", align_corners=True), w.float(), padding=1)
+    taps = w.permute(2, 3, 0, 1).reshape(9 * Cout, Cin)              # row t*Cout + co, t = kh*3 + kw
+    ldb = (Cin + 63) // 64 * 64
+    M = B * H * W
+    Z = torch.zeros(M, 9 * Cout, dtype=dt, device=gpu_device)
+    _gemm(dtype, 0, x.permute(0, 2, 3, 1).contiguous(), _padded_weight(taps, ldb, dt), M, 9 * Cout, Cin, Cin, ldb, Z,
+          9 * Cout)
+    ldo = 2 * Cout + 8
+    out = torch.zeros(B * 4 * H * W, ldo, dtype=dt, device=gpu_device)
+    rc = _lib.lib().spe_debug_upconv(None, DT[dtype][0], _p(Z), _p(out[:, Cout:]), ldo, B, H, W, Cout)
+    assert rc == 0, _lib.lib().spe_last_error()
+    torch.cuda.synchronize()
+    _close(out[:, Cout:2 * Cout], ref.permute(0, 2, 3, 1).reshape(-1, Cout), tol)
+    assert (out[:, :Cout] == 0).all() and (out[:, 2 * Cout:] == 0).all()
