@@ -236,6 +236,9 @@ int spe_debug_gemm(void* stream, int dtype, int mode, const void* A, int lda, co
                    int vt_B, int r_period, const float* ln_g, const float* ln_b, int out_f16);
 /* (out_f16: bf16 launches store fp16 instead of bf16.  ln_g/ln_b non-null: post-norm LayerNorm over each output row fused into the epilogue; bf16,
  * N == 256 and enough rows for the large-tile kernel, else SPE_E_LAUNCH) */
+/* kernel family that served this thread's last gemm launch: 0 the 128x128 kernel, 1 the large-tile
+ * kernels (gemm2.hip), 2 the persistent streaming kernel for short-K problems (gemm_stream.hip) */
+int spe_debug_gemm_path(void);
 int spe_debug_attention(void* stream, int dtype, const void* q, int ldq, const void* k, int ldk, const void* vt,
                         void* o, int ldo, int B, int H, int Tq, int Tk, float scale);
 int spe_debug_layernorm(void* stream, int dtype, const void* x, const float* gamma, const float* beta, void* out,

@@ -28,6 +28,8 @@ int spe_debug_gemm(void* stream, int dtype, int mode, const void* A, int lda, co
   return rc < 0 ? spe_fail(SPE_E_LAUNCH, "gemm launch rejected its arguments") : rc;
 }
 
+int spe_debug_gemm_path(void) { return spe_gemm_last_path; }
+
 int spe_debug_attention(void* stream, int dtype, const void* q, int ldq, const void* k, int ldk, const void* vt,
                         void* o, int ldo, int B, int H, int Tq, int Tk, float scale) {
   AttnArgs a{};

@@ -312,6 +312,8 @@ int launch_t(const GemmArgs& g, int mode, hipStream_t s) {
 
 }  // namespace
 
+thread_local int spe_gemm_last_path = 0;
+
 int spe_launch_gemm(const GemmArgs& g, int dtype, int mode, hipStream_t s) {
   constexpr int CEb = 8, CEf = 4;
   const int ce = dtype == SPE_DTYPE_BF16 ? CEb : CEf;
@@ -321,8 +323,10 @@ int spe_launch_gemm(const GemmArgs& g, int dtype, int mode, hipStream_t s) {
   if ((g.lda % ce) || (g.ldc % (g.out_f32 ? 4 : ce)) || (g.R && (g.ldr % ce))) return -5;
   if (g.ln_g && dtype != SPE_DTYPE_BF16) return -5;   // fused LayerNorm: large-tile bf16 kernel only
   if (dtype == SPE_DTYPE_BF16) {                 // 256-row tiles when they fill the chip
+    spe_gemm_last_path = 1;
     const int rc = spe_launch_gemm2(g, mode, s);
     if (rc != 1) return rc;
   }
+  spe_gemm_last_path = 0;
   return dtype == SPE_DTYPE_BF16 ? launch_t<bf16>(g, mode, s) : launch_t<float>(g, mode, s);
 }

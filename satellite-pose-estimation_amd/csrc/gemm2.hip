@@ -761,6 +761,10 @@ int spe_launch_gemm2(const GemmArgs& g, int mode, hipStream_t s) {
   if (g.K % 8 || g.ldb % 64 || g.lda % 8 || (mode == GEMM_CONV && g.Cin % 8)) return 1;
   if (g.out_f32 ? (g.ldc % 4) : (g.ldc % 8)) return 1;
   if (g.R && g.ldr % 8) return 1;
+  {
+    const int rc = spe_launch_sgemm(g, mode, s);   // short-K streaming kernel (gemm_stream.hip)
+    if (rc != 1) return rc;
+  }
   if (g.ln_g) {                                  // fused LayerNorm needs whole rows in one 256-wide tile
     if (g.N != 256 || g.vt_T > 0 || mode != GEMM_LINEAR || !spe_gemm_ln_fusable(g)) return -5;
     return launch_bn<256>(g, mode, s);

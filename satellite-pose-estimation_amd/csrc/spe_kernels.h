@@ -50,6 +50,9 @@ __device__ __forceinline__ void conv_k_decode(int k, int Cin, int KW, int taps, 
   kw = tap - kh * KW;
 }
 int spe_launch_gemm2(const GemmArgs& g, int mode, hipStream_t s);   // 1 = not applicable
+int spe_launch_sgemm(const GemmArgs& g, int mode, hipStream_t s);   // 1 = not applicable
+// kernel family of this thread's last spe_launch_gemm: 0 gemm.hip, 1 gemm2.hip, 2 gemm_stream.hip
+extern thread_local int spe_gemm_last_path;
 
 struct AttnArgs {
   const void* q; int ldq;          // query row b*Tq+i, head h at columns [h*32, h*32+32)

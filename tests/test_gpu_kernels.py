@@ -497,3 +497,61 @@ def test_upconv_low_resolution(gpu_device, dtype, B, H, W, Cin, Cout):
     torch.cuda.synchronize()
     _close(out[:, Cout:2 * Cout], ref.permute(0, 2, 3, 1).reshape(-1, Cout), tol)
     assert (out[:, :Cout] == 0).all() and (out[:, 2 * Cout:] == 0).all()
+
+
+# (K, N, epilogue): the short-K linear problems of the bench (ResNet 1x1 convs, neck, encoder
+# projections) at sizes large enough for the persistent streaming kernel (gemm_stream.hip)
+SGEMM_CASES = [(64, 64, "relu"), (256, 64, "relu"), (256, 64, "plain"), (256, 128, "relu"), (256, 128, "res_relu"),
+               (512, 128, "relu"), (512, 64, "res_relu"), (512, 256, "bias"), (256, 1024, "res_relu"),
+               (256, 512, "res_periodic_f16"), (256, 256, "vt"), (256, 256, "vt_f16"), (256, 256, "res_ln")]
+
+
+@pytest.mark.parametrize("K,N,epi", SGEMM_CASES)
+def test_gemm_streaming_short_k(gpu_device, K, N, epi):
+    """Persistent weight-stationary kernel: W slice resident in LDS, row tiles streamed through
+    registers, epilogues (bias, residual before ReLU, row-periodic residual, fp16 store, V^T
+    store, fused LayerNorm) straight from the accumulators; ragged M (rows past M computed, not
+    stored), output strides wider than N, N split over workgroup slices."""
+    dt, tol = torch.bfloat16, 1e-2
+    T = 2704
+    M = 52 * T if epi.startswith("vt") else 140003
+    g = torch.Generator(device="cpu").manual_seed(K * 3 + N + len(epi))
+    A = torch.randn(M, K, generator=g).to(gpu_device, dt)
+    Wt = (torch.randn(N, K, generator=g) / K ** 0.5).to(gpu_device, dt)
+    bias = torch.randn(N, generator=g).to(gpu_device)
+    ldc = N + 8 if not epi.startswith("vt") else N
+    f16 = epi.endswith("f16")
+    C = torch.zeros(M, ldc, dtype=torch.float16 if f16 else dt, device=gpu_device)
+    y = A.float() @ Wt.float().t() + bias
+    kw = {}
+    if epi.startswith("res"):
+        if "periodic" in epi:
+            R = torch.randn(T, N, generator=g).to(gpu_device, dt)
+            kw = dict(R=R, ldr=N, r_period=T)
+            y = y + R.float().repeat(M // T + 1, 1)[:M]
+        else:
+            R = torch.randn(M, N, generator=g).to(gpu_device, dt)
+            kw = dict(R=R, ldr=N)
+            y = y + R.float()
+    if "relu" in epi:
+        kw["relu"] = 1
+        y = torch.relu(y)
+    if "ln" in epi:
+        gam = torch.randn(N, generator=g).to(gpu_device)
+        bet = torch.randn(N, generator=g).to(gpu_device)
+        kw["ln"] = (gam, bet)
+        y = F.layer_norm(y, (N,), gam, bet, 1e-5)
+    if epi.startswith("vt"):
+        B = M // T
+        C = torch.zeros(B * N * T, dtype=torch.float16 if f16 else dt, device=gpu_device)
+        _gemm("bf16", 0, A, _padded_weight(Wt, K, dt), M, N, K, K, K, C, 8, bias=bias, vt=(T, B), out_f16=int(f16))
+        got = C.view(N // 256, B, 256, T).permute(1, 3, 0, 2).reshape(M, N)
+    else:
+        _gemm("bf16", 0, A, _padded_weight(Wt, K, dt), M, N, K, K, K, C, ldc, bias=None if epi == "plain" else bias,
+              out_f16=int(f16), **kw)
+        got = C[:, :N]
+        assert (C[:, N:] == 0).all()
+        if epi == "plain":
+            y = y - bias
+    assert _lib.lib().spe_debug_gemm_path() == 2, "expected the streaming kernel"
+    _close(got, y, tol)
