@@ -32,7 +32,6 @@ constexpr int D = 256;
 constexpr int W1_BYTES = HC * D * 2;    // 16 KiB: W1[j][d], 32 rows of 512 B
 constexpr int W2_BYTES = D * HC * 2;    // 16 KiB: W2[n][j], 256 rows of 64 B
 constexpr int STAGE = W1_BYTES + W2_BYTES;
-constexpr int NSTAGE = 3;               // ring: chunk ch in use, ch+1 landing, ch+2 in flight
 constexpr int FMAX = 4096;              // largest dim_feedforward (b1 staged in LDS)
 constexpr int LOADS = (W1_BYTES + W2_BYTES) / 1024 / 4;   // DMA wave-instructions per wave per chunk
 
@@ -69,132 +68,11 @@ SPE_DEV void issue_chunk(const FfnArgs& a, int ch, char* st, int wid, int lane) 
   }
 }
 
-// MB = 16-row MFMA blocks per wave (rows per wave = 16 MB, per block = 64 MB): more rows per
-// wave = more MFMA work per byte of weights read from LDS (every wave reads the whole chunk).
+// epilogue shared by the FFN kernels: + b2 + residual, LayerNorm over n, bf16 store (and the
+// optional y + pos second output)
 template <int MB>
-__global__ __launch_bounds__(NT, 1) void ffn_ln_kernel(FfnArgs a) {
-  constexpr int RB = 64 * MB;           // rows per block
-  // one LDS array (a second __shared__ object beside in-flight global_load_lds can make the
-  // compiler drain vmcnt before LDS reads): [NSTAGE weight stages][b1]
-  __shared__ __attribute__((aligned(1024))) char lds[NSTAGE * STAGE + FMAX * 4];
-  float* sb1 = reinterpret_cast<float*>(lds + NSTAGE * STAGE);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int g = lane >> 4, c16 = lane & 15;
-  // split-F mode (few rows, e.g. the decoder's B*Q): block = (row tile, hidden-unit range);
-  // the partial out^T of each range goes to a.partial and ffn_reduce_ln_kernel finishes
-  const int S = a.partial ? a.splits : 1;
-  const int split = blockIdx.x % S;
-  const int m0 = (blockIdx.x / S) * RB + wid * 16 * MB;
-  const int cps = a.F / HC / S;
-  const int cbeg = split * cps, nchunks = cbeg + cps;   // chunk range [cbeg, nchunks)
-  for (int i = tid; i < a.F; i += NT) sb1[i] = a.b1[i];
-
-  // x rows of this wave as B fragments: xf[mb][ks] = x[m0 + 16mb + c16][32ks + 8g .. +7]
-  bf16x8 xf[MB][8];
-#pragma unroll
-  for (int mb = 0; mb < MB; ++mb) {
-    const int m = m0 + 16 * mb + c16;
-    const bf16* xr = (const bf16*)a.x + (size_t)(m < a.M ? m : 0) * a.ldx;
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks)
-      xf[mb][ks] = __builtin_bit_cast(bf16x8, m < a.M ? ld16(xr + 32 * ks + 8 * g) : u32x4{0, 0, 0, 0});
-  }
-  f32x4 acc[16][MB];
-#pragma unroll
-  for (int nb = 0; nb < 16; ++nb)
-#pragma unroll
-    for (int mb = 0; mb < MB; ++mb) acc[nb][mb] = f32x4{0, 0, 0, 0};
-  // x (and b1) must have landed before the weight DMA starts: vmcnt is in-order, and with a load
-  // of x still pending at the loop entry the compiler's merged wait state would drain every
-  // in-flight chunk at the first MFMA of each step.  (An asm use of every x register makes the
-  // compiler itself retire those loads here; an inline-asm s_waitcnt is invisible to it.)
-#pragma unroll
-  for (int mb = 0; mb < MB; ++mb)
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) asm volatile("" ::"v"(xf[mb][ks]));
-  wait_vmcnt<0>();
-  issue_chunk(a, cbeg, lds, wid, lane);
-  if (cbeg + 1 < nchunks) issue_chunk(a, cbeg + 1, lds + STAGE, wid, lane);
-
-  int slot = 0;
-  for (int ch = cbeg; ch < nchunks; ++ch) {
-    // retire chunk ch (this wave's loads; chunk ch+1 may stay in flight), then the barrier makes
-    // every wave's part visible and guarantees slot (ch+2)%3 -- read in step ch-1 -- is free
-    if (ch + 1 < nchunks) wait_vmcnt<LOADS>();
-    else wait_vmcnt<0>();
-    // raw barrier: __syncthreads' fence would also drain the chunk still in flight
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    const int slot2 = slot == 0 ? 2 : slot - 1;    // (ch + 2) % 3
-    const char* st = lds + slot * STAGE;
-    slot = slot == 2 ? 0 : slot + 1;
-    // all of this chunk's fragment reads up front (one wave per SIMD: nothing else hides LDS
-    // latency); the W2 reads land while the phase-1 MFMAs run
-    u32x4 wa[8][2], wb[16];
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks)
-#pragma unroll
-      for (int jb = 0; jb < 2; ++jb) wa[ks][jb] = ld16(st + w1_off(16 * jb + c16, 4 * ks + g));
-#pragma unroll
-    for (int nb = 0; nb < 16; ++nb) wb[nb] = ld16(st + W1_BYTES + w2_off(16 * nb + c16, g));
-    // chunk ch+2's loads go out after this chunk's LDS reads: issued before them, the compiler
-    // (which cannot tell the DMA's slot from the read's) would drain them first
-    if (ch + 2 < nchunks) issue_chunk(a, ch + 2, lds + slot2 * STAGE, wid, lane);
-    __builtin_amdgcn_sched_barrier(0);
-    // ---- H^T chunk: [32 j][32 m] = W1[j] . x[m]   (LDS row 16jb + 4g + r = hidden 8g + 4jb + r)
-    f32x4 h[2][MB];
-#pragma unroll
-    for (int jb = 0; jb < 2; ++jb)
-#pragma unroll
-      for (int mb = 0; mb < MB; ++mb) h[jb][mb] = f32x4{0, 0, 0, 0};
-#pragma unroll
-    for (int ks = 0; ks < 8; ++ks) {
-#pragma unroll
-      for (int jb = 0; jb < 2; ++jb) {
-        const bf16x8 w = __builtin_bit_cast(bf16x8, wa[ks][jb]);
-#pragma unroll
-        for (int mb = 0; mb < MB; ++mb)
-          h[jb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, xf[mb][ks], h[jb][mb], 0, 0, 0);
-      }
-    }
-    // ---- bias + ReLU, pack as the K=32 B operand: element e <-> hidden 8g + e of the chunk
-    const f32x4 b1a = *reinterpret_cast<const f32x4*>(sb1 + ch * HC + 8 * g);
-    const f32x4 b1b = *reinterpret_cast<const f32x4*>(sb1 + ch * HC + 8 * g + 4);
-    bf16x8 hb[MB];
-#pragma unroll
-    for (int mb = 0; mb < MB; ++mb) {
-      float v[8];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        v[r] = fmaxf(h[0][mb][r] + b1a[r], 0.f);
-        v[4 + r] = fmaxf(h[1][mb][r] + b1b[r], 0.f);
-      }
-      hb[mb] = __builtin_bit_cast(bf16x8, pack16<bf16>(v));
-    }
-    // ---- out^T[n][m] += W2[n][chunk 8g..8g+7] . H^T[8g..8g+7][m]
-#pragma unroll
-    for (int nb = 0; nb < 16; ++nb) {
-      const bf16x8 w = __builtin_bit_cast(bf16x8, wb[nb]);
-#pragma unroll
-      for (int mb = 0; mb < MB; ++mb)
-        acc[nb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, hb[mb], acc[nb][mb], 0, 0, 0);
-    }
-  }
-
-  if (a.partial) {                              // split-F: raw partial sums, finished elsewhere
-#pragma unroll
-    for (int mb = 0; mb < MB; ++mb) {
-      const int m = m0 + 16 * mb + c16;
-      if (m >= a.M) continue;
-      float* pr = a.partial + ((size_t)split * a.M + m) * D;
-#pragma unroll
-      for (int nb = 0; nb < 16; ++nb) st16(pr + 16 * nb + 4 * g, __builtin_bit_cast(u32x4, acc[nb][mb]));
-    }
-    return;
-  }
-
-  // ---- epilogue: + b2 + residual, LayerNorm over n, bf16 store.  Lane holds, for each of its
-  // MB rows m = m0 + 16mb + c16, columns n = 16nb + 4g + r (r = 0..3, nb = 0..15).
+SPE_DEV void ffn_epilogue(const FfnArgs& a, f32x4 (&acc)[16][MB], int m0, int g, int c16) {
+  // Lane holds, for each of its MB rows m = m0 + 16mb + c16, columns n = 16nb + 4g + r (r = 0..3, nb = 0..15).
 #pragma unroll
   for (int mb = 0; mb < MB; ++mb) {
     const int m = m0 + 16 * mb + c16;
@@ -249,6 +127,293 @@ __global__ __launch_bounds__(NT, 1) void ffn_ln_kernel(FfnArgs a) {
       }
     }
   }
+}
+
+// MB = 16-row MFMA blocks per wave (rows per wave = 16 MB, per block = 64 MB): more rows per
+// wave = more MFMA work per byte of weights read from LDS (every wave reads the whole chunk).
+template <int MB, int NSTAGE = 3>
+__global__ __launch_bounds__(NT, 1) void ffn_ln_kernel(FfnArgs a) {
+  constexpr int RB = 64 * MB;           // rows per block
+  // one LDS array (a second __shared__ object beside in-flight global_load_lds can make the
+  // compiler drain vmcnt before LDS reads): [NSTAGE weight stages][b1]
+  __shared__ __attribute__((aligned(1024))) char lds[NSTAGE * STAGE + FMAX * 4];
+  float* sb1 = reinterpret_cast<float*>(lds + NSTAGE * STAGE);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+  // split-F mode (few rows, e.g. the decoder's B*Q): block = (row tile, hidden-unit range);
+  // the partial out^T of each range goes to a.partial and ffn_reduce_ln_kernel finishes
+  const int S = a.partial ? a.splits : 1;
+  const int split = blockIdx.x % S;
+  const int m0 = (blockIdx.x / S) * RB + wid * 16 * MB;
+  const int cps = a.F / HC / S;
+  const int cbeg = split * cps, nchunks = cbeg + cps;   // chunk range [cbeg, nchunks)
+  for (int i = tid; i < a.F; i += NT) sb1[i] = a.b1[i];
+
+  // x rows of this wave as B fragments: xf[mb][ks] = x[m0 + 16mb + c16][32ks + 8g .. +7]
+  bf16x8 xf[MB][8];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    const int m = m0 + 16 * mb + c16;
+    const bf16* xr = (const bf16*)a.x + (size_t)(m < a.M ? m : 0) * a.ldx;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+      xf[mb][ks] = __builtin_bit_cast(bf16x8, m < a.M ? ld16(xr + 32 * ks + 8 * g) : u32x4{0, 0, 0, 0});
+  }
+  f32x4 acc[16][MB];
+#pragma unroll
+  for (int nb = 0; nb < 16; ++nb)
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) acc[nb][mb] = f32x4{0, 0, 0, 0};
+  // x (and b1) must have landed before the weight DMA starts: vmcnt is in-order, and with a load
+  // of x still pending at the loop entry the compiler's merged wait state would drain every
+  // in-flight chunk at the first MFMA of each step.  (An asm use of every x register makes the
+  // compiler itself retire those loads here; an inline-asm s_waitcnt is invisible to it.)
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) asm volatile("" ::"v"(xf[mb][ks]));
+  wait_vmcnt<0>();
+#pragma unroll
+  for (int i = 0; i < NSTAGE - 1; ++i)
+    if (cbeg + i < nchunks) issue_chunk(a, cbeg + i, lds + i * STAGE, wid, lane);
+
+  int slot = 0;
+  for (int ch = cbeg; ch < nchunks; ++ch) {
+    // retire chunk ch (this wave's loads; chunks ch+1 .. ch+NSTAGE-2 may stay in flight), then
+    // the barrier makes every wave's part visible and guarantees the slot of chunk
+    // ch+NSTAGE-1 -- read in step ch-1 -- is free
+    if (NSTAGE >= 4 && ch + 2 < nchunks) wait_vmcnt<2 * LOADS>();
+    else if (ch + 1 < nchunks) wait_vmcnt<LOADS>();
+    else wait_vmcnt<0>();
+    // raw barrier: __syncthreads' fence would also drain the chunk still in flight
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const int slot2 = slot == 0 ? NSTAGE - 1 : slot - 1;    // (ch + NSTAGE - 1) % NSTAGE
+    const char* st = lds + slot * STAGE;
+    slot = slot == NSTAGE - 1 ? 0 : slot + 1;
+    // all of this chunk's fragment reads up front (one wave per SIMD: nothing else hides LDS
+    // latency); the W2 reads land while the phase-1 MFMAs run
+    u32x4 wa[8][2], wb[16];
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb) wa[ks][jb] = ld16(st + w1_off(16 * jb + c16, 4 * ks + g));
+#pragma unroll
+    for (int nb = 0; nb < 16; ++nb) wb[nb] = ld16(st + W1_BYTES + w2_off(16 * nb + c16, g));
+    // chunk ch+2's loads go out after this chunk's LDS reads: issued before them, the compiler
+    // (which cannot tell the DMA's slot from the read's) would drain them first
+    if (ch + NSTAGE - 1 < nchunks) issue_chunk(a, ch + NSTAGE - 1, lds + slot2 * STAGE, wid, lane);
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- H^T chunk: [32 j][32 m] = W1[j] . x[m]   (LDS row 16jb + 4g + r = hidden 8g + 4jb + r)
+    f32x4 h[2][MB];
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) h[jb][mb] = f32x4{0, 0, 0, 0};
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) {
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb) {
+        const bf16x8 w = __builtin_bit_cast(bf16x8, wa[ks][jb]);
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb)
+          h[jb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, xf[mb][ks], h[jb][mb], 0, 0, 0);
+      }
+    }
+    // ---- bias + ReLU, pack as the K=32 B operand: element e <-> hidden 8g + e of the chunk
+    const f32x4 b1a = *reinterpret_cast<const f32x4*>(sb1 + ch * HC + 8 * g);
+    const f32x4 b1b = *reinterpret_cast<const f32x4*>(sb1 + ch * HC + 8 * g + 4);
+    bf16x8 hb[MB];
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = fmaxf(h[0][mb][r] + b1a[r], 0.f);
+        v[4 + r] = fmaxf(h[1][mb][r] + b1b[r], 0.f);
+      }
+      hb[mb] = __builtin_bit_cast(bf16x8, pack16<bf16>(v));
+    }
+    // ---- out^T[n][m] += W2[n][chunk 8g..8g+7] . H^T[8g..8g+7][m]
+#pragma unroll
+    for (int nb = 0; nb < 16; ++nb) {
+      const bf16x8 w = __builtin_bit_cast(bf16x8, wb[nb]);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb)
+        acc[nb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, hb[mb], acc[nb][mb], 0, 0, 0);
+    }
+  }
+
+  if (a.partial) {                              // split-F: raw partial sums, finished elsewhere
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      const int m = m0 + 16 * mb + c16;
+      if (m >= a.M) continue;
+      float* pr = a.partial + ((size_t)split * a.M + m) * D;
+#pragma unroll
+      for (int nb = 0; nb < 16; ++nb) st16(pr + 16 * nb + 4 * g, __builtin_bit_cast(u32x4, acc[nb][mb]));
+    }
+    return;
+  }
+
+  ffn_epilogue<MB>(a, acc, m0, g, c16);
+}
+
+// Cross-chunk software pipeline (encoder FFN, many rows): step c multiplies phase 2 of chunk c
+// (out^T += W2(c) . relu(H(c))) interleaved with phase 1 of chunk c+1 (H(c+1) = W1(c+1) . x), two
+// independent MFMA streams, so no MFMA waits on the phase-1 -> bias/ReLU -> phase-2 dependency
+// that stalls the one wave per SIMD in ffn_ln_kernel.  Four-slot ring: at step c chunk c+1 is
+// retired (chunk c+2 stays in flight) and chunk c+3 is issued into the slot chunk c-1 left.
+template <int MB>
+__global__ __launch_bounds__(NT, 1) void ffn_pipe_kernel(FfnArgs a) {
+  constexpr int NST = 4;
+  __shared__ __attribute__((aligned(1024))) char lds[NST * STAGE + FMAX * 4];
+  float* sb1 = reinterpret_cast<float*>(lds + NST * STAGE);
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int m0 = blockIdx.x * 64 * MB + wid * 16 * MB;
+  const int nch = a.F / HC;
+  for (int i = tid; i < a.F; i += NT) sb1[i] = a.b1[i];
+  bf16x8 xf[MB][8];
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb) {
+    const int m = m0 + 16 * mb + c16;
+    const bf16* xr = (const bf16*)a.x + (size_t)(m < a.M ? m : 0) * a.ldx;
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+      xf[mb][ks] = __builtin_bit_cast(bf16x8, m < a.M ? ld16(xr + 32 * ks + 8 * g) : u32x4{0, 0, 0, 0});
+  }
+  f32x4 acc[16][MB];
+#pragma unroll
+  for (int nb = 0; nb < 16; ++nb)
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) acc[nb][mb] = f32x4{0, 0, 0, 0};
+#pragma unroll
+  for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks) asm volatile("" ::"v"(xf[mb][ks]));
+  wait_vmcnt<0>();                               // (see ffn_ln_kernel: x retired before the DMA)
+#pragma unroll
+  for (int i = 0; i < NST - 1; ++i)
+    if (i < nch) issue_chunk(a, i, lds + i * STAGE, wid, lane);
+
+  u32x4 wa[8][2], wb[16];
+  f32x4 h[2][MB];
+  bf16x8 hb[MB];
+  auto read_w1 = [&](const char* st) {
+#pragma unroll
+    for (int ks = 0; ks < 8; ++ks)
+#pragma unroll
+      for (int jb = 0; jb < 2; ++jb) wa[ks][jb] = ld16(st + w1_off(16 * jb + c16, 4 * ks + g));
+  };
+  auto read_w2 = [&](const char* st) {
+#pragma unroll
+    for (int nb = 0; nb < 16; ++nb) wb[nb] = ld16(st + W1_BYTES + w2_off(16 * nb + c16, g));
+  };
+  auto p1 = [&](int i) {                         // phase-1 MFMA i of 16 MB: (ks, jb, mb)
+    const int ks = i / (2 * MB), jb = (i / MB) % 2, mb = i % MB;
+    h[jb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wa[ks][jb]), xf[mb][ks],
+                                                        h[jb][mb], 0, 0, 0);
+  };
+  auto p2 = [&](int i) {                         // phase-2 MFMA i of 16 MB: (nb, mb)
+    const int nb = i / MB, mb = i % MB;
+    acc[nb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wb[nb]), hb[mb],
+                                                          acc[nb][mb], 0, 0, 0);
+  };
+  auto zero_h = [&]() {
+#pragma unroll
+    for (int jb = 0; jb < 2; ++jb)
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) h[jb][mb] = f32x4{0, 0, 0, 0};
+  };
+  auto pack_h = [&](int ch) {                    // bias + ReLU, as the K = 32 B operand
+    const f32x4 b1a = *reinterpret_cast<const f32x4*>(sb1 + ch * HC + 8 * g);
+    const f32x4 b1b = *reinterpret_cast<const f32x4*>(sb1 + ch * HC + 8 * g + 4);
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+      float v[8];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        v[r] = fmaxf(h[0][mb][r] + b1a[r], 0.f);
+        v[4 + r] = fmaxf(h[1][mb][r] + b1b[r], 0.f);
+      }
+      hb[mb] = __builtin_bit_cast(bf16x8, pack16<bf16>(v));
+    }
+  };
+  auto sync = [&]() {                            // raw barrier: keep the in-flight chunks
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+  };
+
+  // prologue: chunk 0 retired, its phase 1 alone
+  if (nch > 2) wait_vmcnt<2 * LOADS>();
+  else if (nch > 1) wait_vmcnt<LOADS>();
+  else wait_vmcnt<0>();
+  sync();
+  read_w1(lds);
+  zero_h();
+#pragma unroll
+  for (int i = 0; i < 16 * MB; ++i) p1(i);
+  pack_h(0);
+
+  for (int c = 0; c + 1 < nch; ++c) {
+#ifndef SPE_X_FFN_NODMA
+    if (c + 2 < nch) wait_vmcnt<LOADS>();        // chunk c+1 landed, c+2 may stay in flight
+    else wait_vmcnt<0>();
+#endif
+#ifndef SPE_X_FFN_NOBAR
+    sync();
+#endif
+    const char* st = lds + (c % NST) * STAGE;
+    const char* st1 = lds + ((c + 1) % NST) * STAGE;
+#ifdef SPE_X_FFN_NOLDS
+    if (c == 0) {
+#endif
+    read_w2(st);
+    read_w1(st1);
+#ifdef SPE_X_FFN_NOLDS
+    }
+#endif
+#ifndef SPE_X_FFN_NODMA
+    if (c + 3 < nch) issue_chunk(a, c + 3, lds + ((c + 3) % NST) * STAGE, wid, lane);
+#endif
+    __builtin_amdgcn_sched_barrier(0);
+    zero_h();
+    // two phase-1 MFMAs per phase-2 MFMA until H(c+1) is complete, then the rest of phase 2
+    // beside its bias / ReLU / pack
+#pragma unroll
+    for (int i = 0; i < 8 * MB; ++i) {
+      p1(2 * i);
+      p1(2 * i + 1);
+      p2(i);
+    }
+    bf16x8 hb_next[MB];
+    {
+      const f32x4 b1a = *reinterpret_cast<const f32x4*>(sb1 + (c + 1) * HC + 8 * g);
+      const f32x4 b1b = *reinterpret_cast<const f32x4*>(sb1 + (c + 1) * HC + 8 * g + 4);
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) {
+        float v[8];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          v[r] = fmaxf(h[0][mb][r] + b1a[r], 0.f);
+          v[4 + r] = fmaxf(h[1][mb][r] + b1b[r], 0.f);
+        }
+        hb_next[mb] = __builtin_bit_cast(bf16x8, pack16<bf16>(v));
+      }
+    }
+#pragma unroll
+    for (int i = 8 * MB; i < 16 * MB; ++i) p2(i);
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) hb[mb] = hb_next[mb];
+  }
+  // last chunk: phase 2 alone
+  sync();
+  read_w2(lds + ((nch - 1) % NST) * STAGE);
+#pragma unroll
+  for (int i = 0; i < 16 * MB; ++i) p2(i);
+
+  ffn_epilogue<MB>(a, acc, m0, g, c16);
 }
 
 // split-F finish: y = LN(x + sum_s partial[s] + b2) (+ pos copy), one wave per row
@@ -307,7 +472,12 @@ int spe_launch_ffn_ln(const FfnArgs& a0, hipStream_t s) {
     // 48 rows per wave (MB = 3, 493 VGPR+AGPR, no spills) measured 9 % faster than 32 (kbench,
     // B = 64 encoder FFN: 0.48 vs 0.53 ms); 64 rows spill.  SPE_FFN_MB overrides for A/B runs.
     static const int mb = [] { const char* e = getenv("SPE_FFN_MB"); return e ? atoi(e) : 3; }();
-    if (mb == 3) hipLaunchKernelGGL(ffn_ln_kernel<3>, dim3((a.M + 191) / 192), dim3(NT), 0, s, a);
+    static const int nst = [] { const char* e = getenv("SPE_FFN_NST"); return e ? atoi(e) : 4; }();
+    static const int pipe = [] { const char* e = getenv("SPE_FFN_PIPE"); return e ? atoi(e) : 1; }();
+    if (pipe && mb == 3 && a.F / HC >= 2) hipLaunchKernelGGL(ffn_pipe_kernel<3>, dim3((a.M + 191) / 192), dim3(NT), 0, s, a);
+    else if (pipe && mb == 2 && a.F / HC >= 2) hipLaunchKernelGGL(ffn_pipe_kernel<2>, dim3((a.M + 127) / 128), dim3(NT), 0, s, a);
+    else if (mb == 3 && nst == 4) hipLaunchKernelGGL((ffn_ln_kernel<3, 4>), dim3((a.M + 191) / 192), dim3(NT), 0, s, a);
+    else if (mb == 3) hipLaunchKernelGGL(ffn_ln_kernel<3>, dim3((a.M + 191) / 192), dim3(NT), 0, s, a);
     else if (mb == 4) hipLaunchKernelGGL(ffn_ln_kernel<4>, dim3((a.M + 255) / 256), dim3(NT), 0, s, a);
     else hipLaunchKernelGGL(ffn_ln_kernel<2>, dim3((a.M + 127) / 128), dim3(NT), 0, s, a);
   }
