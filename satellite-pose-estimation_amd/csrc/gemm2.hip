@@ -776,7 +776,13 @@ int spe_launch_gemm2(const GemmArgs& g, int mode, hipStream_t s) {
     return (int)hipGetLastError();
   }
   if (use_st1(g, mode) && g.act <= ACT_RELU && !g.res_post) return launch_st1(g, s);
-  const int bn = (g.N <= 64 && g.vt_T == 0) ? 64 : g.N <= 128 ? 128 : 256;   // BN 64 has no V^T store
+  int bn = (g.N <= 64 && g.vt_T == 0) ? 64 : g.N <= 128 ? 128 : 256;   // BN 64 has no V^T store
+  {
+    // grids of 256-wide tiles that leave CUs idle in their last round: SPE_GEMM2_NARROW = the
+    // tile count below which convs take 128-wide tiles (A/B knob, default off)
+    static const int narrow = [] { const char* e = getenv("SPE_GEMM2_NARROW"); return e ? atoi(e) : 0; }();
+    if (bn == 256 && mode == GEMM_CONV && ((g.M + BM - 1) / BM) * ((g.N + 255) / 256) < narrow) bn = 128;
+  }
   const int tiles = ((g.M + BM - 1) / BM) * ((g.N + bn - 1) / bn);
   // too few tiles for the large-tile kernel: the 128x128 kernel.  (169 tiles of 256x256 on the
   // layer3 convs, M = B*26*26, still beat 676 tiles of the 128x128 kernel by 12-18 %.)
