@@ -68,6 +68,41 @@ SPE_DEV void issue_chunk(const FfnArgs& a, int ch, char* st, int wid, int lane) 
   }
 }
 
+// The same chunk DMA through buffer_load ... lds: the per-lane part of each source address is
+// a 32-bit voffset fixed for the kernel's life and the chunk's offset a scalar soffset, so a
+// chunk costs 8 issue slots and no address VALU (global_load_lds needs a 64-bit per-lane address
+// per instruction and chunk).  Out-of-range reads (num_records) return zero.
+typedef short short2_t __attribute__((ext_vector_type(2)));
+struct ChunkDma {
+  __amdgpu_buffer_rsrc_t r1, r2;
+  int vo1[4], vo2[4];
+  SPE_DEV void init(const FfnArgs& a, int wid, int lane) {
+    r1 = __builtin_amdgcn_make_buffer_rsrc((void*)a.w1, (short)0, a.F * a.ld1 * 2, 0x00020000);
+    r2 = __builtin_amdgcn_make_buffer_rsrc((void*)a.w2, (short)0, D * a.ld2 * 2, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ins = wid * 4 + i;
+      const int R = 2 * ins + (lane >> 5), c = (lane & 31) ^ (R & 15);
+      vo1[i] = (w1_src_row(R) * a.ld1 + c * 8) * 2;
+      const int n = 16 * ins + (lane >> 2), c2 = (lane & 3) ^ w2_key(n);
+      vo2[i] = (n * a.ld2 + c2 * 8) * 2;
+    }
+  }
+  SPE_DEV void issue(const FfnArgs& a, int ch, char* st, int wid) const {
+    const int so1 = ch * HC * a.ld1 * 2, so2 = ch * HC * 2;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r1, (lds_ptr_t)(st + (wid * 4 + i) * 1024), 16, vo1[i], so1, 0, 0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r2, (lds_ptr_t)(st + W1_BYTES + (wid * 4 + i) * 1024), 16, vo2[i], so2, 0, 0);
+  }
+};
+// ReLU of two packed bf16: negative values (sign bit set) are negative as int16
+SPE_DEV uint32_t relu_bf16x2(uint32_t v) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(short2_t, v), short2_t{0, 0}));
+}
+
 // epilogue shared by the FFN kernels: + b2 + residual, LayerNorm over n, bf16 store (and the
 // optional y + pos second output)
 template <int MB>
@@ -293,9 +328,11 @@ __global__ __launch_bounds__(NT, 1) void ffn_pipe_kernel(FfnArgs a) {
 #pragma unroll
     for (int ks = 0; ks < 8; ++ks) asm volatile("" ::"v"(xf[mb][ks]));
   wait_vmcnt<0>();                               // (see ffn_ln_kernel: x retired before the DMA)
+  ChunkDma dma;
+  dma.init(a, wid, lane);
 #pragma unroll
   for (int i = 0; i < NST - 1; ++i)
-    if (i < nch) issue_chunk(a, i, lds + i * STAGE, wid, lane);
+    if (i < nch) dma.issue(a, i, lds + i * STAGE, wid);
 
   u32x4 wa[8][2], wb[16];
   f32x4 h[2][MB];
@@ -320,24 +357,25 @@ __global__ __launch_bounds__(NT, 1) void ffn_pipe_kernel(FfnArgs a) {
     acc[nb][mb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wb[nb]), hb[mb],
                                                           acc[nb][mb], 0, 0, 0);
   };
-  auto zero_h = [&]() {
-#pragma unroll
-    for (int jb = 0; jb < 2; ++jb)
-#pragma unroll
-      for (int mb = 0; mb < MB; ++mb) h[jb][mb] = f32x4{0, 0, 0, 0};
-  };
-  auto pack_h = [&](int ch) {                    // bias + ReLU, as the K = 32 B operand
+  // H starts from b1 (the MFMAs accumulate onto the bias): h[jb][mb][r] <-> hidden 8g + 4jb + r
+  auto init_h = [&](int ch) {
     const f32x4 b1a = *reinterpret_cast<const f32x4*>(sb1 + ch * HC + 8 * g);
     const f32x4 b1b = *reinterpret_cast<const f32x4*>(sb1 + ch * HC + 8 * g + 4);
 #pragma unroll
     for (int mb = 0; mb < MB; ++mb) {
-      float v[8];
+      h[0][mb] = b1a;
+      h[1][mb] = b1b;
+    }
+  };
+  // ReLU after the bf16 rounding (same result: rounding keeps the sign), on packed pairs
+  auto pack_h = [&](bf16x8 (&out)[MB]) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        v[r] = fmaxf(h[0][mb][r] + b1a[r], 0.f);
-        v[4 + r] = fmaxf(h[1][mb][r] + b1b[r], 0.f);
-      }
-      hb[mb] = __builtin_bit_cast(bf16x8, pack16<bf16>(v));
+    for (int mb = 0; mb < MB; ++mb) {
+      const uint32_t w0 = relu_bf16x2(pack_bf16x2(h[0][mb][0], h[0][mb][1]));
+      const uint32_t w1 = relu_bf16x2(pack_bf16x2(h[0][mb][2], h[0][mb][3]));
+      const uint32_t w2 = relu_bf16x2(pack_bf16x2(h[1][mb][0], h[1][mb][1]));
+      const uint32_t w3 = relu_bf16x2(pack_bf16x2(h[1][mb][2], h[1][mb][3]));
+      out[mb] = __builtin_bit_cast(bf16x8, u32x4{w0, w1, w2, w3});
     }
   };
   auto sync = [&]() {                            // raw barrier: keep the in-flight chunks
@@ -351,10 +389,10 @@ __global__ __launch_bounds__(NT, 1) void ffn_pipe_kernel(FfnArgs a) {
   else wait_vmcnt<0>();
   sync();
   read_w1(lds);
-  zero_h();
+  init_h(0);
 #pragma unroll
   for (int i = 0; i < 16 * MB; ++i) p1(i);
-  pack_h(0);
+  pack_h(hb);
 
   for (int c = 0; c + 1 < nch; ++c) {
 #ifndef SPE_X_FFN_NODMA
@@ -375,10 +413,10 @@ __global__ __launch_bounds__(NT, 1) void ffn_pipe_kernel(FfnArgs a) {
     }
 #endif
 #ifndef SPE_X_FFN_NODMA
-    if (c + 3 < nch) issue_chunk(a, c + 3, lds + ((c + 3) % NST) * STAGE, wid, lane);
+    if (c + 3 < nch) dma.issue(a, c + 3, lds + ((c + 3) % NST) * STAGE, wid);
 #endif
     __builtin_amdgcn_sched_barrier(0);
-    zero_h();
+    init_h(c + 1);
     // two phase-1 MFMAs per phase-2 MFMA until H(c+1) is complete, then the rest of phase 2
     // beside its bias / ReLU / pack
 #pragma unroll
@@ -388,20 +426,7 @@ __global__ __launch_bounds__(NT, 1) void ffn_pipe_kernel(FfnArgs a) {
       p2(i);
     }
     bf16x8 hb_next[MB];
-    {
-      const f32x4 b1a = *reinterpret_cast<const f32x4*>(sb1 + (c + 1) * HC + 8 * g);
-      const f32x4 b1b = *reinterpret_cast<const f32x4*>(sb1 + (c + 1) * HC + 8 * g + 4);
-#pragma unroll
-      for (int mb = 0; mb < MB; ++mb) {
-        float v[8];
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          v[r] = fmaxf(h[0][mb][r] + b1a[r], 0.f);
-          v[4 + r] = fmaxf(h[1][mb][r] + b1b[r], 0.f);
-        }
-        hb_next[mb] = __builtin_bit_cast(bf16x8, pack16<bf16>(v));
-      }
-    }
+    pack_h(hb_next);
 #pragma unroll
     for (int i = 8 * MB; i < 16 * MB; ++i) p2(i);
 #pragma unroll
