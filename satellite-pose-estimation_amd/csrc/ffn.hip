@@ -42,10 +42,6 @@ constexpr int LOADS = (W1_BYTES + W2_BYTES) / 1024 / 4;   // DMA wave-instructio
 SPE_DEV int w1_src_row(int R) { return 8 * ((R & 15) >> 2) + 4 * (R >> 4) + (R & 3); }
 // W1 stage: 16-byte chunk c of LDS row R at slot c ^ (R & 15) (conflict-free ds_read_b128)
 SPE_DEV int w1_off(int R, int c) { return R * 512 + ((c ^ (R & 15)) << 4); }
-// 32x32x16 form (ffn32_kernel): D row R = 8i + 4hh + r of the H^T tile holds hidden unit
-// 16(i>>1) + 8hh + 4(i&1) + r, so lane half hh owns hidden 16ks + 8hh .. +7 of K-step ks in
-// the D registers 8ks .. 8ks+7: the phase-2 B operand packs straight from the accumulator
-SPE_DEV int w1_src_row32(int R) { const int i = R >> 3; return 16 * (i >> 1) + 8 * ((R >> 2) & 1) + 4 * (i & 1) + (R & 3); }
 // W2 stage: 16-byte chunk c (hidden 8c..8c+7) of row n at slot c ^ key(n), key = -(n>>2) & 3:
 // each ds_read_b128 lane group's 16 reads hit 16 distinct 16-byte bank groups
 SPE_DEV int w2_key(int n) { return (4 - ((n >> 2) & 3)) & 3; }
@@ -80,14 +76,14 @@ typedef short short2_t __attribute__((ext_vector_type(2)));
 struct ChunkDma {
   __amdgpu_buffer_rsrc_t r1, r2;
   int vo1[4], vo2[4];
-  SPE_DEV void init(const FfnArgs& a, int wid, int lane, bool p32 = false) {
+  SPE_DEV void init(const FfnArgs& a, int wid, int lane) {
     r1 = __builtin_amdgcn_make_buffer_rsrc((void*)a.w1, (short)0, a.F * a.ld1 * 2, 0x00020000);
     r2 = __builtin_amdgcn_make_buffer_rsrc((void*)a.w2, (short)0, D * a.ld2 * 2, 0x00020000);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int ins = wid * 4 + i;
       const int R = 2 * ins + (lane >> 5), c = (lane & 31) ^ (R & 15);
-      vo1[i] = ((p32 ? w1_src_row32(R) : w1_src_row(R)) * a.ld1 + c * 8) * 2;
+      vo1[i] = (w1_src_row(R) * a.ld1 + c * 8) * 2;
       const int n = 16 * ins + (lane >> 2), c2 = (lane & 3) ^ w2_key(n);
       vo2[i] = (n * a.ld2 + c2 * 8) * 2;
     }
@@ -445,183 +441,6 @@ __global__ __launch_bounds__(NT, 1) void ffn_pipe_kernel(FfnArgs a) {
   ffn_epilogue<MB>(a, acc, m0, g, c16);
 }
 
-// 32x32x16 MFMA form of the encoder FFN: half the MFMA instructions of the 16x16x32 kernels for
-// the same flops (each holds the wave's issue for 8 of its 32 cycles instead of 8 of 16), so one
-// wave per SIMD keeps more issue slots for its LDS reads and VALU.  Wave = 32 rows; per 32-unit
-// chunk: phase 1 H^T[32 j][32 m] = 16 MFMAs over K = 256 (A = W1 rows in LDS, B = x registers),
-// phase 2 out^T[256 n][32 m] += 8 n-blocks x 2 K-steps.  Same cross-chunk pipeline and ring as
-// ffn_pipe_kernel (phase 2 of chunk c beside phase 1 of chunk c+1).
-typedef __bf16 bf16x8_t __attribute__((ext_vector_type(8)));
-SPE_DEV f32x16 mfma32(u32x4 a, u32x4 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8_t, a), __builtin_bit_cast(bf16x8_t, b), c, 0, 0, 0);
-}
-
-__global__ __launch_bounds__(NT, 1) void ffn32_kernel(FfnArgs a) {
-  constexpr int NST = 4;
-  __shared__ __attribute__((aligned(1024))) char lds[NST * STAGE + FMAX * 4];
-  float* sb1 = reinterpret_cast<float*>(lds + NST * STAGE);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int hh = lane >> 5, l32 = lane & 31;
-  const int m0 = blockIdx.x * 128 + wid * 32;
-  const int nch = a.F / HC;
-  for (int i = tid; i < a.F; i += NT) sb1[i] = a.b1[i];
-  // x fragments: xf[ks] = x[m0 + l32][16ks + 8hh .. +7]
-  u32x4 xf[16];
-  {
-    const int m = m0 + l32;
-    const bf16* xr = (const bf16*)a.x + (size_t)(m < a.M ? m : 0) * a.ldx;
-#pragma unroll
-    for (int ks = 0; ks < 16; ++ks) xf[ks] = m < a.M ? ld16(xr + 16 * ks + 8 * hh) : u32x4{0, 0, 0, 0};
-#pragma unroll
-    for (int ks = 0; ks < 16; ++ks) asm volatile("" ::"v"(xf[ks]));
-  }
-  f32x16 acc[8];
-#pragma unroll
-  for (int nb = 0; nb < 8; ++nb)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[nb][r] = 0.f;
-  wait_vmcnt<0>();
-  ChunkDma dma;
-  dma.init(a, wid, lane, true);
-#pragma unroll
-  for (int i = 0; i < NST - 1; ++i)
-    if (i < nch) dma.issue(a, i, lds + i * STAGE, wid);
-
-  u32x4 wa[16], wb[8][2];
-  f32x16 h;
-  u32x4 hb[2];
-  auto read_w1 = [&](const char* st) {
-#pragma unroll
-    for (int ks = 0; ks < 16; ++ks) wa[ks] = ld16(st + w1_off(l32, 2 * ks + hh));
-  };
-  auto read_w2 = [&](const char* st) {
-#pragma unroll
-    for (int nb = 0; nb < 8; ++nb)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) wb[nb][ks] = ld16(st + W1_BYTES + w2_off(32 * nb + l32, 2 * ks + hh));
-  };
-  // h register r <-> D row (r&3) + 8(r>>2) + 4hh <-> hidden 16((r>>2)>>1) + 8hh + 4((r>>2)&1) + (r&3)
-  //              = 8 * (r >> 3) * 2 + 8hh + (r & 7): registers 8ks .. 8ks+7 = hidden 16ks + 8hh + e
-  auto init_h = [&](int ch) {
-    const float* bb = sb1 + ch * HC + 8 * hh;
-    const f32x4 b0 = *reinterpret_cast<const f32x4*>(bb), b1 = *reinterpret_cast<const f32x4*>(bb + 4);
-    const f32x4 b2 = *reinterpret_cast<const f32x4*>(bb + 16), b3 = *reinterpret_cast<const f32x4*>(bb + 20);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      h[r] = b0[r]; h[4 + r] = b1[r]; h[8 + r] = b2[r]; h[12 + r] = b3[r];
-    }
-  };
-  auto pack_h = [&](u32x4 (&out)[2]) {
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-      out[ks] = u32x4{relu_bf16x2(pack_bf16x2(h[8 * ks + 0], h[8 * ks + 1])), relu_bf16x2(pack_bf16x2(h[8 * ks + 2], h[8 * ks + 3])),
-                      relu_bf16x2(pack_bf16x2(h[8 * ks + 4], h[8 * ks + 5])), relu_bf16x2(pack_bf16x2(h[8 * ks + 6], h[8 * ks + 7]))};
-  };
-  auto sync = [&]() {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-  };
-
-  if (nch > 2) wait_vmcnt<2 * LOADS>();
-  else if (nch > 1) wait_vmcnt<LOADS>();
-  else wait_vmcnt<0>();
-  sync();
-  read_w1(lds);
-  init_h(0);
-#pragma unroll
-  for (int ks = 0; ks < 16; ++ks) h = mfma32(wa[ks], xf[ks], h);
-  pack_h(hb);
-
-  for (int c = 0; c + 1 < nch; ++c) {
-    if (c + 2 < nch) wait_vmcnt<LOADS>();
-    else wait_vmcnt<0>();
-    sync();
-    read_w2(lds + (c % NST) * STAGE);
-    read_w1(lds + ((c + 1) % NST) * STAGE);
-    if (c + 3 < nch) dma.issue(a, c + 3, lds + ((c + 3) % NST) * STAGE, wid);
-    __builtin_amdgcn_sched_barrier(0);
-    init_h(c + 1);
-    // phase 1 of chunk c+1 (16, one dependent chain) interleaved with phase 2 of chunk c (16)
-#ifdef SPE_FFN32_2CHAIN
-    f32x16 h2;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) h2[r] = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      if (i & 1) h2 = mfma32(wa[i], xf[i], h2);
-      else h = mfma32(wa[i], xf[i], h);
-      acc[i >> 1] = mfma32(wb[i >> 1][i & 1], hb[i & 1], acc[i >> 1]);
-    }
-#pragma unroll
-    for (int r = 0; r < 16; ++r) h[r] += h2[r];
-#else
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-      h = mfma32(wa[i], xf[i], h);
-      acc[i >> 1] = mfma32(wb[i >> 1][i & 1], hb[i & 1], acc[i >> 1]);
-    }
-#endif
-    pack_h(hb);
-  }
-  sync();
-  read_w2(lds + ((nch - 1) % NST) * STAGE);
-#pragma unroll
-  for (int i = 0; i < 16; ++i) acc[i >> 1] = mfma32(wb[i >> 1][i & 1], hb[i & 1], acc[i >> 1]);
-
-  // ---- epilogue: lane holds row m = m0 + l32, columns n = 32nb + 8i + 4hh + (0..3) in
-  // acc[nb][4i .. 4i+3]; the other half of the row is in lane ^ 32
-  const int m = m0 + l32;
-  const bool live = m < a.M;
-  const bf16* xr = (const bf16*)a.x + (size_t)(live ? m : 0) * a.ldx;
-  float s = 0.f;
-#pragma unroll
-  for (int nb = 0; nb < 8; ++nb)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int n = 32 * nb + 8 * i + 4 * hh;
-      const f32x4 b2 = *reinterpret_cast<const f32x4*>(a.b2 + n);
-      const u32x2 rv = live ? ld8(xr + n) : u32x2{0, 0};
-      acc[nb][4 * i + 0] += b2[0] + __uint_as_float(rv.x << 16);
-      acc[nb][4 * i + 1] += b2[1] + __uint_as_float(rv.x & 0xffff0000u);
-      acc[nb][4 * i + 2] += b2[2] + __uint_as_float(rv.y << 16);
-      acc[nb][4 * i + 3] += b2[3] + __uint_as_float(rv.y & 0xffff0000u);
-      s += acc[nb][4 * i] + acc[nb][4 * i + 1] + acc[nb][4 * i + 2] + acc[nb][4 * i + 3];
-    }
-  s += __shfl_xor(s, 32, 64);
-  const float mean = s * (1.f / D);
-  float q = 0.f;
-#pragma unroll
-  for (int nb = 0; nb < 8; ++nb)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const float dv = acc[nb][r] - mean;
-      q += dv * dv;
-    }
-  q += __shfl_xor(q, 32, 64);
-  const float rs = rsqrtf(q * (1.f / D) + 1e-5f);
-  if (!live) return;
-  bf16* yr = (bf16*)a.y + (size_t)m * a.ldy;
-  const bf16* pr = a.ypos ? (const bf16*)a.pos + (size_t)(m % a.pos_period) * D : nullptr;
-  bf16* ypr = a.ypos ? (bf16*)a.ypos + (size_t)m * a.ldy : nullptr;
-#pragma unroll
-  for (int nb = 0; nb < 8; ++nb)
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int n = 32 * nb + 8 * i + 4 * hh;
-      const f32x4 ga = *reinterpret_cast<const f32x4*>(a.gamma + n);
-      const f32x4 be = *reinterpret_cast<const f32x4*>(a.beta + n);
-      float o[4];
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = (acc[nb][4 * i + r] - mean) * rs * ga[r] + be[r];
-      st8(yr + n, u32x2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])});
-      if (ypr) {
-        const u32x2 pv = ld8(pr + n);
-        st8(ypr + n, u32x2{pack_bf16x2(o[0] + __uint_as_float(pv.x << 16), o[1] + __uint_as_float(pv.x & 0xffff0000u)),
-                           pack_bf16x2(o[2] + __uint_as_float(pv.y << 16), o[3] + __uint_as_float(pv.y & 0xffff0000u))});
-      }
-    }
-}
-
 // split-F finish: y = LN(x + sum_s partial[s] + b2) (+ pos copy), one wave per row
 __global__ __launch_bounds__(256) void ffn_reduce_ln_kernel(FfnArgs a) {
   const int lane = threadIdx.x & 63, m = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -679,9 +498,8 @@ int spe_launch_ffn_ln(const FfnArgs& a0, hipStream_t s) {
     // B = 64 encoder FFN: 0.48 vs 0.53 ms); 64 rows spill.  SPE_FFN_MB overrides for A/B runs.
     static const int mb = [] { const char* e = getenv("SPE_FFN_MB"); return e ? atoi(e) : 3; }();
     static const int nst = [] { const char* e = getenv("SPE_FFN_NST"); return e ? atoi(e) : 4; }();
-    static const int pipe = [] { const char* e = getenv("SPE_FFN_PIPE"); return e ? atoi(e) : 2; }();
-    if (pipe == 2 && a.F / HC >= 2) hipLaunchKernelGGL(ffn32_kernel, dim3((a.M + 127) / 128), dim3(NT), 0, s, a);
-    else if (pipe && mb == 3 && a.F / HC >= 2) hipLaunchKernelGGL(ffn_pipe_kernel<3>, dim3((a.M + 191) / 192), dim3(NT), 0, s, a);
+    static const int pipe = [] { const char* e = getenv("SPE_FFN_PIPE"); return e ? atoi(e) : 1; }();
+    if (pipe && mb == 3 && a.F / HC >= 2) hipLaunchKernelGGL(ffn_pipe_kernel<3>, dim3((a.M + 191) / 192), dim3(NT), 0, s, a);
     else if (pipe && mb == 2 && a.F / HC >= 2) hipLaunchKernelGGL(ffn_pipe_kernel<2>, dim3((a.M + 127) / 128), dim3(NT), 0, s, a);
     else if (mb == 3 && nst == 4) hipLaunchKernelGGL((ffn_ln_kernel<3, 4>), dim3((a.M + 191) / 192), dim3(NT), 0, s, a);
     else if (mb == 3) hipLaunchKernelGGL(ffn_ln_kernel<3>, dim3((a.M + 191) / 192), dim3(NT), 0, s, a);

@@ -474,7 +474,8 @@ def test_layernorm(gpu_device, dtype):
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "fp32"])
-@pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 26, 26, 1024, 256), (3, 5, 7, 64, 16), (1, 1, 3, 32, 8)])
+@pytest.mark.parametrize("B,H,W,Cin,Cout", [(2, 26, 26, 1024, 256), (3, 5, 7, 64, 16), (1, 1, 3, 32, 8),
+                                            (2, 5, 7, 64, 32), (1, 1, 3, 32, 64), (2, 40, 40, 128, 96)])
 def test_upconv_low_resolution(gpu_device, dtype, B, H, W, Cin, Cout):
     """bf16 neck: conv3x3(pad 1)(UpsamplingBilinear2d(x2)(x)) (REV/models/backbone.py:141) as one
     per-tap GEMM at the low resolution + spe_debug_upconv's bilinear combine, written into a
