@@ -28,7 +28,8 @@ __global__ void pack_input_kernel(const float* __restrict__ img, T* __restrict__
 }
 
 template <typename T>
-__global__ void maxpool_kernel(const T* __restrict__ in, T* __restrict__ out, int B, int H, int W, int C, int Ho, int Wo) {
+__global__ void maxpool_kernel(const T* __restrict__ in, T* __restrict__ out, int B, int H, int W, int C, int Ho, int Wo,
+                               int ldo) {
   constexpr int CE = Chunk<T>::CE;
   const int cch = C / CE;
   const size_t n = (size_t)B * Ho * Wo * cch;
@@ -53,7 +54,7 @@ __global__ void maxpool_kernel(const T* __restrict__ in, T* __restrict__ out, in
         for (int e = 0; e < CE; ++e) mx[e] = fmaxf(mx[e], f[e]);
       }
     }
-    st16(out + (((size_t)b * Ho + oh) * Wo + ow) * C + c * CE, pack16<T>(mx));
+    st16(out + (((size_t)b * Ho + oh) * Wo + ow) * ldo + c * CE, pack16<T>(mx));
   }
 }
 
@@ -186,14 +187,16 @@ int spe_launch_pack_input(const float* img, void* out, int B, int S, int dtype, 
   return (int)hipGetLastError();
 }
 
-int spe_launch_maxpool3s2(const void* in, void* out, int B, int H, int W, int C, int Ho, int Wo, int dtype, hipStream_t s) {
+int spe_launch_maxpool3s2(const void* in, void* out, int B, int H, int W, int C, int Ho, int Wo, int dtype, hipStream_t s,
+                          int ldo) {
   const int ce = dtype == SPE_DTYPE_BF16 ? 8 : 4;
-  if (C % ce) return -5;
+  if (ldo <= 0) ldo = C;
+  if (C % ce || ldo % ce || ldo < C) return -5;
   const size_t n = (size_t)B * Ho * Wo * (C / ce);
   if (dtype == SPE_DTYPE_BF16)
-    hipLaunchKernelGGL(maxpool_kernel<bf16>, grid_for(n, 256), 256, 0, s, (const bf16*)in, (bf16*)out, B, H, W, C, Ho, Wo);
+    hipLaunchKernelGGL(maxpool_kernel<bf16>, grid_for(n, 256), 256, 0, s, (const bf16*)in, (bf16*)out, B, H, W, C, Ho, Wo, ldo);
   else
-    hipLaunchKernelGGL(maxpool_kernel<float>, grid_for(n, 256), 256, 0, s, (const float*)in, (float*)out, B, H, W, C, Ho, Wo);
+    hipLaunchKernelGGL(maxpool_kernel<float>, grid_for(n, 256), 256, 0, s, (const float*)in, (float*)out, B, H, W, C, Ho, Wo, ldo);
   return (int)hipGetLastError();
 }
 

@@ -178,24 +178,41 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   }
   int H = S / 2;
   const int Hp = (H + 2 - 3) / 2 + 1;
-  CK(run_other(m, "eltwise.maxpool", 0.0, (double)B * 64 * (H * H + Hp * Hp) * m->esz, s, [&] { return spe_launch_maxpool3s2(P(w.stem), P(w.pool), B, H, H, 64, Hp, Hp, dt, s); }));
+  // bf16: layer1 block 0's conv3 + downsample run as one GEMM over [conv2 output | pool output]
+  // (Block::c3ds), so the max-pool writes the right half of that concatenation (w.ds region,
+  // row stride c3ds.K) and conv2 the left half
+  const Block& b0 = m->blocks[0];
+  const bool fuse0 = b0.c3ds.w != nullptr;
+  const int uld = fuse0 ? b0.c3ds.K : 64;
+  const size_t pool_at = fuse0 ? w.ds + (size_t)b0.c2.N * m->esz : w.pool;
+  CK(run_other(m, "eltwise.maxpool", 0.0, (double)B * 64 * (H * H + Hp * Hp) * m->esz, s, [&] { return spe_launch_maxpool3s2(P(w.stem), P(pool_at), B, H, H, 64, Hp, Hp, dt, s, uld); }));
   H = Hp;
-  size_t cur = w.pool;                                  // aliases bufA
-  int cin = 64;
+  size_t cur = pool_at;                                 // (w.pool aliases bufA)
+  int cin = 64, cur_ld = uld;
   for (size_t bi = 0; bi < m->blocks.size(); ++bi) {
     const Block& blk = m->blocks[bi];
+    const bool fused = bi == 0 && fuse0;
     // layer1: blocks 0-2, layer2: 3-6 (its output xs8 is kept for the neck), layer3: 7-12
     const size_t outbuf = (bi == 6) ? w.xs8 : (cur == w.bufA ? w.bufB : w.bufA);
     const int Ho = (H + 2 - 3) / blk.stride + 1;
     {  // conv1 1x1 + bn1 + relu
-      GemmArgs g = linear_args(blk.c1, P(cur), cin, B * H * H, P(w.t1), blk.c1.N);
+      GemmArgs g = linear_args(blk.c1, P(cur), cur_ld, B * H * H, P(w.t1), blk.c1.N);
       g.act = ACT_RELU;
       CK(run_gemm(m, "conv.1x1", g, GEMM_LINEAR, s));
     }
     {  // conv2 3x3 (stride on the 3x3, ResNet v1.5) + bn2 + relu
-      GemmArgs g = conv_args(blk.c2, P(w.t1), B, H, H, P(w.t2), blk.c2.N);
+      GemmArgs g = conv_args(blk.c2, P(w.t1), B, H, H, fused ? P(w.ds) : P(w.t2), fused ? uld : blk.c2.N);
       g.act = ACT_RELU;
       CK(run_gemm(m, "conv.3x3", g, GEMM_CONV, s));
+    }
+    if (fused) {  // relu(W3 t2 + Wds x + b3 + bds) over the concatenation
+      GemmArgs g = linear_args(blk.c3ds, P(w.ds), uld, B * Ho * Ho, P(outbuf), blk.c3ds.N);
+      g.act = ACT_RELU;
+      CK(run_gemm(m, "conv.1x1", g, GEMM_LINEAR, s));
+      cin = cur_ld = blk.c3.N;
+      H = Ho;
+      cur = outbuf;
+      continue;
     }
     size_t res = cur;
     if (blk.has_ds) {
@@ -213,7 +230,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       g.R = P(res); g.ldr = blk.c3.N; g.act = ACT_RELU;
       CK(run_gemm(m, "conv.1x1", g, GEMM_LINEAR, s));
     }
-    cin = blk.c3.N;
+    cin = cur_ld = blk.c3.N;
     H = Ho;
     cur = outbuf;
   }

@@ -319,6 +319,27 @@ int build_device(spe_model* m) {
       if (k == 0) {
         blk.has_ds = true;
         blk.ds = make_conv(m, p + ".downsample.0.weight", p + ".downsample.1", "", 0, blk.stride, 0);
+        if (blk.stride == 1 && m->esz == 2) {
+          // conv3 + downsample of a stride-1 first block as ONE K = w + cin GEMM over the
+          // channel concatenation [conv2 output | block input] (forward.cpp lays them out side by
+          // side): relu(W3 t2 + b3 + Wds x + bds) with no downsample output round trip
+          std::vector<float> w3, b3, wd, bd;
+          fold_conv(m, p + ".conv3.weight", p + ".bn3", "", w3, b3);
+          fold_conv(m, p + ".downsample.0.weight", p + ".downsample.1", "", wd, bd);
+          const int n = blk.c3.N, k3 = blk.c3.K, kd = blk.ds.K;
+          std::vector<float> rows((size_t)n * (k3 + kd));
+          if (m->dmem)
+            for (int r = 0; r < n; ++r) {
+              for (int c = 0; c < k3; ++c) rows[(size_t)r * (k3 + kd) + c] = w3[(size_t)r * k3 + c];
+              for (int c = 0; c < kd; ++c) rows[(size_t)r * (k3 + kd) + k3 + c] = wd[(size_t)r * kd + c];
+            }
+          std::vector<float> bias(n);
+          for (int r = 0; r < n; ++r) bias[r] = b3[r] + bd[r];
+          Conv& f = blk.c3ds;
+          f.N = n; f.K = k3 + kd; f.Kpad = pad64(f.K); f.Cin = f.K;
+          f.w = upload_rows(m, rows, f.N, f.K, f.Kpad);
+          f.bias = upload_f32(m, bias.data(), bias.size());
+        }
       }
       m->blocks.push_back(blk);
     }

@@ -102,7 +102,7 @@ int spe_launch_preprocess(const uint8_t* frames, int B, int H, int W, int C, con
                           float* images, float* clip_bbox, int32_t* status, hipStream_t s);
 int spe_launch_pack_input(const float* img, void* out, int B, int S, int dtype, hipStream_t s);
 int spe_launch_maxpool3s2(const void* in, void* out, int B, int H, int W, int C, int Ho, int Wo,
-                          int dtype, hipStream_t s);
+                          int dtype, hipStream_t s, int ldo = 0);   // ldo: output row stride (0 = C)
 int spe_launch_upsample2x(const void* in, void* out, int B, int H, int W, int C, int dtype, hipStream_t s);
 // conv3x3(pad 1)(upsample2x(x)) from the per-tap low-resolution products z [B*H*W][9*C]
 // (elementwise.hip); out rows of stride ldo (a channel slice of a concat buffer)
