@@ -88,6 +88,14 @@ struct ChunkDma {
       vo2[i] = (n * a.ld2 + c2 * 8) * 2;
     }
   }
+  // piece i of 8 (0-3: W1, 4-7: W2), for spreading a chunk's DMA between MFMAs
+  SPE_DEV void piece(const FfnArgs& a, int ch, char* st, int wid, int i) const {
+    if (i < 4)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r1, (lds_ptr_t)(st + (wid * 4 + i) * 1024), 16, vo1[i], ch * HC * a.ld1 * 2, 0, 0);
+    else
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r2, (lds_ptr_t)(st + W1_BYTES + (wid * 4 + i - 4) * 1024), 16, vo2[i - 4],
+                                               ch * HC * 2, 0, 0);
+  }
   SPE_DEV void issue(const FfnArgs& a, int ch, char* st, int wid) const {
     const int so1 = ch * HC * a.ld1 * 2, so2 = ch * HC * 2;
 #pragma unroll
@@ -299,14 +307,19 @@ __global__ __launch_bounds__(NT, 1) void ffn_ln_kernel(FfnArgs a) {
 // independent MFMA streams, so no MFMA waits on the phase-1 -> bias/ReLU -> phase-2 dependency
 // that stalls the one wave per SIMD in ffn_ln_kernel.  Four-slot ring: at step c chunk c+1 is
 // retired (chunk c+2 stays in flight) and chunk c+3 is issued into the slot chunk c-1 left.
-template <int MB>
+// SCHED: the step's 32 fragment reads are issued in consumption order a few MFMAs
+// ahead of their use and its 8 DMA pieces spread between the MFMAs, with the instruction order
+// pinned by sched_barrier: otherwise the compiler hoists every read to the top of the step and
+// the one wave per SIMD waits for all 32 KiB of them before its MFMAs can run.
+// PRE = reads issued ahead of the first MFMA (then one per MFMA triple).
+template <int MB, bool SCHED = false, int PRE = 6>
 __global__ __launch_bounds__(NT, 1) void ffn_pipe_kernel(FfnArgs a) {
   constexpr int NST = 4;
   __shared__ __attribute__((aligned(1024))) char lds[NST * STAGE + FMAX * 4];
   float* sb1 = reinterpret_cast<float*>(lds + NST * STAGE);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int g = lane >> 4, c16 = lane & 15;
-  const int m0 = blockIdx.x * 64 * MB + wid * 16 * MB;
+  const int m0 = a.row0 + blockIdx.x * 64 * MB + wid * 16 * MB;
   const int nch = a.F / HC;
   for (int i = tid; i < a.F; i += NT) sb1[i] = a.b1[i];
   bf16x8 xf[MB][8];
@@ -404,6 +417,54 @@ __global__ __launch_bounds__(NT, 1) void ffn_pipe_kernel(FfnArgs a) {
 #endif
     const char* st = lds + (c % NST) * STAGE;
     const char* st1 = lds + ((c + 1) % NST) * STAGE;
+    if constexpr (SCHED) {
+      // read r in consumption order: r < 24 -> block k = r / 3: W1(c+1) ks = k jb 0, W2(c) nb = k,
+      // W1(c+1) ks = k jb 1 (block k feeds interleaved steps MB*k .. MB*k + MB-1);
+      // r >= 24 -> W2(c) nb = r - 16 (the tail)
+      auto rd = [&](int r) {
+        if (r < 24) {
+          const int k = r / 3, q = r % 3;
+          if (q == 1) wb[k] = ld16(st + W1_BYTES + w2_off(16 * k + c16, g));
+          else wa[k][q >> 1] = ld16(st1 + w1_off(16 * (q >> 1) + c16, 4 * k + g));
+        } else {
+          wb[r - 16] = ld16(st + W1_BYTES + w2_off(16 * (r - 16) + c16, g));
+        }
+      };
+      // chunk c+3's pieces are issued unconditionally (a branch would split the MFMA block and
+      // the accumulators get copied across it): past the last chunk the buffer resource's range
+      // check makes them zero-fill the free slot (c+3) % 4, which nothing reads any more
+      char* dst = lds + ((c + 3) % NST) * STAGE;
+      init_h(c + 1);
+#pragma unroll
+      for (int r = 0; r < PRE; ++r) rd(r);
+      __builtin_amdgcn_sched_barrier(0);
+      // interleaved steps t: p1(2t), p1(2t+1), p2(t); 3 reads per MB steps, one DMA piece per MB
+      int issued = PRE;
+#pragma unroll
+      for (int t = 0; t < 8 * MB; ++t) {
+        const int upto = PRE + (3 * (t + 1) + MB - 1) / MB < 32 ? PRE + (3 * (t + 1) + MB - 1) / MB : 32;
+        for (; issued < upto; ++issued) rd(issued);
+        if (t % MB == 1 % MB) dma.piece(a, c + 3, dst, wid, t / MB);
+        p1(2 * t);
+        p1(2 * t + 1);
+        p2(t);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      bf16x8 hb_next[MB];
+      // tail: p2(8MB..16MB) in groups of MB (one W2 block each), the remaining reads and
+      // H(c+1)'s pack between them
+#pragma unroll
+      for (int t = 8 * MB; t < 16 * MB; t += MB) {
+        if (issued < 32) rd(issued++);
+#pragma unroll
+        for (int u = 0; u < MB; ++u) p2(t + u);
+        if (t == 9 * MB) pack_h(hb_next);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+#pragma unroll
+      for (int mb = 0; mb < MB; ++mb) hb[mb] = hb_next[mb];
+      continue;
+    }
 #ifdef SPE_X_FFN_NOLDS
     if (c == 0) {
 #endif
@@ -433,6 +494,7 @@ __global__ __launch_bounds__(NT, 1) void ffn_pipe_kernel(FfnArgs a) {
     for (int mb = 0; mb < MB; ++mb) hb[mb] = hb_next[mb];
   }
   // last chunk: phase 2 alone
+  if constexpr (SCHED) wait_vmcnt<0>();          // the zero-fill pieces past the end
   sync();
   read_w2(lds + ((nch - 1) % NST) * STAGE);
 #pragma unroll
@@ -483,6 +545,7 @@ int spe_ffn_splits(int M, int F) {
 
 int spe_launch_ffn_ln(const FfnArgs& a0, hipStream_t s) {
   FfnArgs a = a0;
+  a.row0 = 0;
   if (a.M <= 0) return 0;
   if (a.ypos && (!a.pos || a.pos_period <= 0)) return -5;
   if (a.D != D || a.F % HC || a.F > FMAX || (a.ldx % 8) || (a.ldy % 8) || (a.ld1 % 8) || (a.ld2 % 8)) return -5;
@@ -499,8 +562,33 @@ int spe_launch_ffn_ln(const FfnArgs& a0, hipStream_t s) {
     static const int mb = [] { const char* e = getenv("SPE_FFN_MB"); return e ? atoi(e) : 3; }();
     static const int nst = [] { const char* e = getenv("SPE_FFN_NST"); return e ? atoi(e) : 4; }();
     static const int pipe = [] { const char* e = getenv("SPE_FFN_PIPE"); return e ? atoi(e) : 1; }();
-    if (pipe && mb == 3 && a.F / HC >= 2) hipLaunchKernelGGL(ffn_pipe_kernel<3>, dim3((a.M + 191) / 192), dim3(NT), 0, s, a);
-    else if (pipe && mb == 2 && a.F / HC >= 2) hipLaunchKernelGGL(ffn_pipe_kernel<2>, dim3((a.M + 127) / 128), dim3(NT), 0, s, a);
+    // SPE_FFN_SCHED: 0 = compiler-scheduled pipe loop, 3 / 6 / 9 = pinned schedule with that
+    // many reads ahead (default 6)
+    static const int sched = [] { const char* e = getenv("SPE_FFN_SCHED"); return e ? atoi(e) : 6; }();
+    auto main_kernel = [&](int grid) {
+      if (sched == 3) hipLaunchKernelGGL((ffn_pipe_kernel<3, true, 3>), dim3(grid), dim3(NT), 0, s, a);
+      else if (sched == 9) hipLaunchKernelGGL((ffn_pipe_kernel<3, true, 9>), dim3(grid), dim3(NT), 0, s, a);
+      else if (sched) hipLaunchKernelGGL((ffn_pipe_kernel<3, true, 6>), dim3(grid), dim3(NT), 0, s, a);
+      else hipLaunchKernelGGL(ffn_pipe_kernel<3>, dim3(grid), dim3(NT), 0, s, a);
+    };
+    if (pipe && mb == 3 && a.F / HC >= 2) {
+      // One workgroup per CU (144 KiB of LDS), so the grid runs in rounds of #CU tiles.  When the
+      // last round would be partly idle and its rows fit one round of 128-row tiles, the whole
+      // rounds take 192-row tiles and the rest goes to a second launch of 128-row tiles: the
+      // last round then costs ~0.85 of a 192-row round (B = 64 encoder FFN: 0.445 -> 0.427 ms
+      // unpinned).  SPE_FFN_TAIL=0 disables it for A/B runs.
+      static const int tail = [] { const char* e = getenv("SPE_FFN_TAIL"); return e ? atoi(e) : 1; }();
+      const int tiles = (a.M + 191) / 192, ncu = spe_cu_count();
+      const int full = ncu > 0 ? tiles / ncu * ncu : 0, rest = a.M - full * 192;
+      if (tail && full > 0 && rest > 0 && (rest + 127) / 128 <= ncu) {
+        main_kernel(full);
+        a.row0 = full * 192;
+        if (sched) hipLaunchKernelGGL((ffn_pipe_kernel<2, true, 6>), dim3((rest + 127) / 128), dim3(NT), 0, s, a);
+        else hipLaunchKernelGGL(ffn_pipe_kernel<2>, dim3((rest + 127) / 128), dim3(NT), 0, s, a);
+      } else {
+        main_kernel(tiles);
+      }
+    } else if (pipe && mb == 2 && a.F / HC >= 2) hipLaunchKernelGGL(ffn_pipe_kernel<2>, dim3((a.M + 127) / 128), dim3(NT), 0, s, a);
     else if (mb == 3 && nst == 4) hipLaunchKernelGGL((ffn_ln_kernel<3, 4>), dim3((a.M + 191) / 192), dim3(NT), 0, s, a);
     else if (mb == 3) hipLaunchKernelGGL(ffn_ln_kernel<3>, dim3((a.M + 191) / 192), dim3(NT), 0, s, a);
     else if (mb == 4) hipLaunchKernelGGL(ffn_ln_kernel<4>, dim3((a.M + 255) / 256), dim3(NT), 0, s, a);

@@ -272,7 +272,9 @@ __global__ __launch_bounds__(256, OCC) void sgemm_kernel(GemmArgs g, int ns_coun
   }
 }
 
-int cu_count() {
+}  // namespace
+
+int spe_cu_count() {
   static const int n = [] {
     int dev = 0, c = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
@@ -283,6 +285,8 @@ int cu_count() {
   return n;
 }
 
+namespace {
+
 bool sgemm_enabled() {
   static const bool on = [] { const char* e = getenv("SPE_SGEMM"); return !e || atoi(e) != 0; }();
   return on;
@@ -291,7 +295,7 @@ bool sgemm_enabled() {
 template <int K, int BN, int RF, int OCC, int NB, bool HAS_R, int EPI>
 int launch_k(const GemmArgs& g, hipStream_t s) {
   const int row_tiles = (g.M + RF * 16 - 1) / (RF * 16), nsc = g.N / BN;
-  const int G = (cu_count() * OCC / nsc) * nsc;
+  const int G = (spe_cu_count() * OCC / nsc) * nsc;
   if ((long)row_tiles < 2L * (G / nsc) * 4) return 1;    // fewer than two tiles per wave
   hipLaunchKernelGGL((sgemm_kernel<K, BN, RF, OCC, NB, HAS_R, EPI>), dim3(G), dim3(256), 0, s, g, nsc, row_tiles);
   spe_gemm_last_path = 2;

@@ -51,6 +51,7 @@ __device__ __forceinline__ void conv_k_decode(int k, int Cin, int KW, int taps, 
 }
 int spe_launch_gemm2(const GemmArgs& g, int mode, hipStream_t s);   // 1 = not applicable
 int spe_launch_sgemm(const GemmArgs& g, int mode, hipStream_t s);   // 1 = not applicable
+int spe_cu_count();               // CUs of the current device (cached; 256 on MI355X)
 // kernel family of this thread's last spe_launch_gemm: 0 gemm.hip, 1 gemm2.hip, 2 gemm_stream.hip
 extern thread_local int spe_gemm_last_path;
 
@@ -94,6 +95,7 @@ struct FfnArgs {
   const void* pos; void* ypos;     // optional: ypos = y + pos[m % pos_period] (bf16 [M][256])
   int pos_period;
   int splits; float* partial;      // optional split over F for few rows: fp32 [splits][M][256] workspace
+  int row0;                        // first row of this launch's tiles (internal: the FFN tail launch)
 };
 int spe_launch_ffn_ln(const FfnArgs& a, hipStream_t s);
 int spe_ffn_splits(int M, int F);  // split count spe_launch_ffn_ln would use for M rows (1 = none)

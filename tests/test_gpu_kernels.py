@@ -387,7 +387,9 @@ def test_attention_large_score_range(gpu_device):
 
 @pytest.mark.parametrize("M,F,inplace,splits", [(333, 2048, True, 0), (128, 64, False, 0), (1000, 2048, False, 0),
                                                 (5, 32, True, 0), (704, 2048, True, 16), (300, 2048, False, 32),
-                                                (77, 128, False, 2), (17003, 2048, False, 0), (640, 1024, True, 0)])
+                                                (77, 128, False, 2), (17003, 2048, False, 0), (640, 1024, True, 0),
+                                                # whole 192-row rounds + a 128-row tail launch on 256 CUs
+                                                (54152, 2048, True, 0), (70000, 2048, False, 0)])
 def test_fused_ffn(gpu_device, M, F, inplace, splits):
     """bf16 fused linear1 -> ReLU -> linear2 -> +x -> LayerNorm against torch fp32 on bf16-rounded
     operands; the hidden activation is rounded to bf16 on chip exactly as the unfused path stores it."""
