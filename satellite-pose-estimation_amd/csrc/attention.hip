@@ -26,6 +26,7 @@
 // bf16: v_mfma_f32_32x32x16_bf16; fp16 operands (config 5): v_mfma_f32_32x32x16_f16 (same
 // kernel, AT<f16> traits).  fp32 (parity mode): v_mfma_f32_32x32x2_f32, exact f32.
 #include "spe_common.h"
+#include <type_traits>
 #include "spe_kernels.h"
 
 namespace {
@@ -175,10 +176,18 @@ template <> struct AT<f16> {
 // ------------------------------------------------------------------ bf16 kernel
 // ROLE only separates the symbols of the token-query (encoder self-attention) and the
 // object-query (decoder) launches so profiler summaries report them apart; the code is shared.
-template <int ROLE, typename TI>
+// TV: type of V^T and of P (the value product).  TV = fp16 also under bf16 q/k (the bf16
+// model's encoder, V^T stored fp16 by the v-projection epilogue): P is then packed as fp16
+// pairs, and the row sums are packed-fp16 adds of those same words (15 v_pk_add_f16 + one
+// v_dot2_f32_f16 per 64-key tile instead of 32 f32 adds; the tile's partial sum <= 32 * 2^8
+// fits fp16, and it is the rounded P the value product uses).
+template <int ROLE, typename TI, typename TV = TI>
 __global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn16_kernel(AttnArgs a) {
   typedef AT<TI> A;
+  typedef AT<TV> AV;
   typedef typename A::v8 v8;
+  typedef typename AV::v8 vv8;
+  constexpr bool HSUM = sizeof(TV) == 2 && !std::is_same<TV, bf16>::value;   // fp16 P: packed sums
   constexpr int KBYTES = KT * KROW, VBYTES = 32 * VROW;
   __shared__ __attribute__((aligned(16))) char smem[2 * (KBYTES + VBYTES)];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -285,24 +294,38 @@ __global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn16_kernel(AttnArgs a) {
 #endif
       }
 #ifndef SPE_X_NOLS
-      {
+      if constexpr (!HSUM) {
         float t0 = 0.f, t1 = 0.f, t2 = 0.f, t3 = 0.f;
 #pragma unroll
         for (int r = 0; r < 16; r += 2) { t0 += s0[r]; t1 += s0[r + 1]; t2 += s1[r]; t3 += s1[r + 1]; }
         ls += (t0 + t1) + (t2 + t3);
       }
 #endif
+      u32x4 pw[2][2];
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub) {
         const f32x16& p = sub ? s1 : s0;
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks) {
-          u32x4 pw{A::pk(p[8 * ks + 0], p[8 * ks + 1]), A::pk(p[8 * ks + 2], p[8 * ks + 3]),
-                   A::pk(p[8 * ks + 4], p[8 * ks + 5]), A::pk(p[8 * ks + 6], p[8 * ks + 7])};
-          const v8 pb = __builtin_bit_cast(v8, pw);
-          o = A::mfma(__builtin_bit_cast(v8, vf[sub][ks]), pb, o);
-        }
+        for (int ks = 0; ks < 2; ++ks)
+          pw[sub][ks] = u32x4{AV::pk(p[8 * ks + 0], p[8 * ks + 1]), AV::pk(p[8 * ks + 2], p[8 * ks + 3]),
+                              AV::pk(p[8 * ks + 4], p[8 * ks + 5]), AV::pk(p[8 * ks + 6], p[8 * ks + 7])};
       }
+#ifndef SPE_X_NOLS
+      if constexpr (HSUM) {
+        typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+        auto H2 = [](uint32_t w) { return __builtin_bit_cast(h2, w); };
+        h2 u[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          u[e] = (H2(pw[0][0][e]) + H2(pw[0][1][e])) + (H2(pw[1][0][e]) + H2(pw[1][1][e]));
+        ls = __builtin_amdgcn_fdot2((u[0] + u[1]) + (u[2] + u[3]), h2{(_Float16)1.f, (_Float16)1.f}, ls, false);
+      }
+#endif
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          o = AV::mfma(__builtin_bit_cast(vv8, vf[sub][ks]), __builtin_bit_cast(vv8, pw[sub][ks]), o);
     }
 #ifdef SPE_X_NOSTAGE
     if (more && kt == 0) st.store(smem + ((kt + 1) & 1) * SLOT, smem + ((kt + 1) & 1) * SLOT + KBYTES, tid);
@@ -430,6 +453,11 @@ int spe_launch_attention(const AttnArgs& a, int dtype, hipStream_t s) {
       hipLaunchKernelGGL((attn16_kernel<0, f16>), grid, block, 0, s, a);
     else
       hipLaunchKernelGGL((attn16_kernel<1, f16>), grid, block, 0, s, a);
+  else if (dtype == SPE_DTYPE_BF16_F16V)
+    if (a.Tq >= 128)
+      hipLaunchKernelGGL((attn16_kernel<0, bf16, f16>), grid, block, 0, s, a);
+    else
+      hipLaunchKernelGGL((attn16_kernel<1, bf16, f16>), grid, block, 0, s, a);
   else if (dtype == SPE_DTYPE_BF16)
     if (a.Tq >= 128)
       hipLaunchKernelGGL((attn16_kernel<0, bf16>), grid, block, 0, s, a);

@@ -422,6 +422,9 @@ __global__ __launch_bounds__(NT, 1) void ffn_pipe_kernel(FfnArgs a) {
       // W1(c+1) ks = k jb 1 (block k feeds interleaved steps MB*k .. MB*k + MB-1);
       // r >= 24 -> W2(c) nb = r - 16 (the tail)
       auto rd = [&](int r) {
+#ifdef SPE_X_FFN_NOLDS
+        if (c > 0) return;
+#endif
         if (r < 24) {
           const int k = r / 3, q = r % 3;
           if (q == 1) wb[k] = ld16(st + W1_BYTES + w2_off(16 * k + c16, g));
@@ -444,7 +447,9 @@ __global__ __launch_bounds__(NT, 1) void ffn_pipe_kernel(FfnArgs a) {
       for (int t = 0; t < 8 * MB; ++t) {
         const int upto = PRE + (3 * (t + 1) + MB - 1) / MB < 32 ? PRE + (3 * (t + 1) + MB - 1) / MB : 32;
         for (; issued < upto; ++issued) rd(issued);
+#ifndef SPE_X_FFN_NODMA
         if (t % MB == 1 % MB) dma.piece(a, c + 3, dst, wid, t / MB);
+#endif
         p1(2 * t);
         p1(2 * t + 1);
         p2(t);

@@ -8,6 +8,7 @@
 
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <map>
@@ -269,6 +270,12 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   // fp16 encoder attention operands (bf16 models, attn_dtype = SPE_DTYPE_F16_): the q/k and V^T
   // projections store fp16, the attention runs fp16 MFMAs; everything else stays bf16
   const int f16attn = c.attn_dtype == SPE_DTYPE_F16_ && dt == SPE_DTYPE_BF16;
+  // bf16 models otherwise keep bf16 q/k but store V^T as fp16: the attention's P is then fp16
+  // and its row sums packed-fp16 adds (attention.hip, TV).  fp16 has the finer mantissa; V and
+  // P stay far inside its range.  SPE_ATTN_F16V=0 keeps V^T and P bf16 (A/B knob).
+  static const int f16v_env = [] { const char* e = getenv("SPE_ATTN_F16V"); return e ? atoi(e) : 1; }();
+  const int f16v = !f16attn && dt == SPE_DTYPE_BF16 && f16v_env;
+  const int attn_dt = f16attn ? SPE_DTYPE_F16 : f16v ? SPE_DTYPE_BF16_F16V : dt;
   for (const Enc& e : m->enc) {
     {
       GemmArgs g = linear_args(e.qk, P(w.src), d, Mt, P(w.qkv), 3 * d);
@@ -279,7 +286,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
     {
       GemmArgs g = linear_args(e.v, P(w.src), d, Mt, P(w.vt), 8);
       g.vt_T = T; g.vt_B = B;
-      g.out_f16 = f16attn;
+      g.out_f16 = f16attn || f16v;
       CK(run_gemm(m, "gemm.enc.v", g, GEMM_LINEAR, s));
     }
     {
@@ -289,7 +296,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       a.vt = P(w.vt);
       a.o = P(w.ao); a.ldo = d;
       a.B = B; a.H = c.nheads; a.Tq = T; a.Tk = T; a.scale = scale;
-      CK(run_attn(m, "attn.enc", a, f16attn ? SPE_DTYPE_F16 : dt, s));
+      CK(run_attn(m, "attn.enc", a, attn_dt, s));
     }
     {
       // out-proj + residual; bf16 large batches fuse norm1 into the GEMM epilogue, in place over src

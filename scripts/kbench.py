@@ -38,6 +38,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--only", default="")
+    ap.add_argument("--attn-dtype", type=int, default=0, help="0 bf16, 2 fp16, 3 bf16 q/k + fp16 V^T/P")
     a = ap.parse_args()
     L = _lib.lib()
     dev = torch.device("cuda", 0)
@@ -45,10 +46,14 @@ def main():
     g = torch.Generator(device="cpu").manual_seed(0)
     if a.which in ("attn", "all"):
         qk = torch.randn(B * T, 512, generator=g).to(dev, torch.bfloat16)
-        vt = torch.randn(B, H, 32, T, generator=g).to(dev, torch.bfloat16)
+        vdt = torch.float16 if a.attn_dtype in (2, 3) else torch.bfloat16
+        if a.attn_dtype == 2:
+            qk = qk.to(torch.float16)
+        vt = torch.randn(B, H, 32, T, generator=g).to(dev, vdt)
         o = torch.empty(B * T, D, dtype=torch.bfloat16, device=dev)
         kp = ctypes.c_void_p(qk.data_ptr() + 256 * 2)
-        fn = lambda: L.spe_debug_attention(None, 0, p(qk), 512, kp, 512, p(vt), p(o), D, B, H, T, T, 32 ** -0.5)
+        fn = lambda: L.spe_debug_attention(None, a.attn_dtype, p(qk), 512, kp, 512, p(vt), p(o), D, B, H, T, T,
+                                           32 ** -0.5)
         ms = timeit(fn, a.iters)
         fl = 4.0 * B * H * T * T * 32
         print(f"attn.enc  {ms:.3f} ms  {fl / ms / 1e9:.1f} TF/s")

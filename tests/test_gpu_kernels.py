@@ -340,15 +340,24 @@ def _attn_ref(q, k, v, scale):
     return a @ v.float()
 
 
-@pytest.mark.parametrize("dtype", ["bf16", "fp16", "fp32"])
-@pytest.mark.parametrize("B,H,Tq,Tk", [(2, 8, 200, 200), (3, 8, 11, 330), (1, 8, 11, 11), (1, 2, 300, 64)])
+# attention-only operand mode of bf16 models' encoder: bf16 q/k, fp16 V^T and P (attention.hip TV)
+SPE_DTYPE_BF16_F16V = 3
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp16", "fp32", "bf16_f16v"])
+@pytest.mark.parametrize("B,H,Tq,Tk", [(2, 8, 200, 200), (3, 8, 11, 330), (1, 8, 11, 11), (1, 2, 300, 64),
+                                       (1, 8, 2704, 2704)])
 def test_attention(gpu_device, dtype, B, H, Tq, Tk):
-    code, dt, tol = DT[dtype]
+    if dtype == "bf16_f16v":
+        code, dt, vdt = SPE_DTYPE_BF16_F16V, torch.bfloat16, torch.float16
+    else:
+        code, dt, _ = DT[dtype]
+        vdt = dt
     g = torch.Generator(device="cpu").manual_seed(Tq + Tk)
     ld = H * 32 + 16                                   # row stride wider than the heads
     Q = (torch.randn(B * Tq, ld, generator=g) * 2).to(gpu_device, dt)
     K = (torch.randn(B * Tk, ld, generator=g) * 2).to(gpu_device, dt)
-    V = torch.randn(B, H, Tk, 32, generator=g).to(gpu_device, dt)
+    V = torch.randn(B, H, Tk, 32, generator=g).to(gpu_device, vdt)
     VT = V.transpose(-1, -2).contiguous()
     # 16-bit operand kernels (bf16 / fp16) write bf16: the out-projection GEMM reads bf16
     O = torch.zeros(B * Tq, H * 32, dtype=torch.float32 if dtype == "fp32" else torch.bfloat16, device=gpu_device)
@@ -361,19 +370,23 @@ def test_attention(gpu_device, dtype, B, H, Tq, Tk):
     if dtype != "fp32":                                # the kernel rounds the prescaled q to 16 bits
         q = (q.float() * scale * 1.4426950408889634).to(dt).float() / (scale * 1.4426950408889634)
     ref = _attn_ref(q, k, V, scale).transpose(1, 2).reshape(B * Tq, H * 32)
-    _close(O, ref, {"bf16": 2e-2, "fp16": 1e-2, "fp32": 1e-5}[dtype])
+    _close(O, ref, {"bf16": 2e-2, "fp16": 1e-2, "fp32": 1e-5, "bf16_f16v": 2e-2}[dtype])
 
 
-def test_attention_large_score_range(gpu_device):
+@pytest.mark.parametrize("mode", ["bf16", "bf16_f16v"])
+def test_attention_large_score_range(gpu_device, mode):
     """Scores spanning > 100 in log space force rescales of the running max late in the sweep."""
     code, dt, _ = DT["bf16"]
+    vdt = dt
+    if mode == "bf16_f16v":
+        code, vdt = SPE_DTYPE_BF16_F16V, torch.float16
     B, H, T = 1, 8, 256
     g = torch.Generator(device="cpu").manual_seed(0)
     Q = torch.randn(B * T, 256, generator=g).to(gpu_device, dt)
     K = torch.randn(B * T, 256, generator=g)
     K[200:] *= 12.0                                    # late keys dominate
     K = K.to(gpu_device, dt)
-    V = torch.randn(B, H, T, 32, generator=g).to(gpu_device, dt)
+    V = torch.randn(B, H, T, 32, generator=g).to(gpu_device, vdt)
     O = torch.zeros(B * T, 256, dtype=dt, device=gpu_device)
     scale = 32 ** -0.5
     assert _lib.lib().spe_debug_attention(None, code, _p(Q), 256, _p(K), 256, _p(V.transpose(-1, -2).contiguous()),
