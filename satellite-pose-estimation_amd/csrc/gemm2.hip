@@ -65,7 +65,11 @@ constexpr int P8_MIN_K = 1024;
 // workgroup's epilogue and load latency overlap the other's work: short-K linear problems)
 // XA: extended epilogue (SiLU / GELU, residual after the activation) for the RT-DETR encoder.
 // A separate instantiation: the extra live state made the ReLU-only tiles spill (272 B/lane).
-template <int BN, int MODE, bool LN, bool P8K = false, int NST = 2, bool XA = false>
+// PIN: no residual (g.R must be null: the residual prefetch registers are compiled out) and a
+// pinned fragment schedule in the 2-stage loop -- the reads of the next fragment group are
+// issued ahead of the current group's MFMAs and the order is fixed with sched_barrier, where
+// the compiler's schedule waits on lgkmcnt(0) before every 8 MFMAs.
+template <int BN, int MODE, bool LN, bool P8K = false, int NST = 2, bool XA = false, bool PIN = false>
 __global__ __launch_bounds__(NT, NST == 1 ? 4 : 1) void gemm2_kernel(GemmArgs g) {
   constexpr int WM = Cfg<BN>::WM, WN = Cfg<BN>::WN;
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
@@ -176,6 +180,53 @@ __global__ __launch_bounds__(NT, NST == 1 ? 4 : 1) void gemm2_kernel(GemmArgs g)
     }
   };
   auto issue = [&](int ks, const KPos& kp, int buf) { issue_rng(ks, kp, buf, 0, IA, 0, IB); };
+  // PIN: the same loads as buffer_load ... lds (MUBUF: the compiler then counts only the LDS
+  // fragment reads on lgkmcnt -- pending FLAT-encoded global_load_lds make it wait lgkmcnt(0)
+  // before every fragment group).  32-bit byte offsets; out-of-range offsets read zeros.
+  constexpr int BAD = 0x7ffffff0;
+  const long long abytes = !PIN ? 0
+                           : MODE == GEMM_CONV ? (long long)((g.M + g.Ho * g.Wo - 1) / (g.Ho * g.Wo)) * g.H * g.W * g.Cin * 2
+                                               : (long long)g.M * g.lda * 2;
+  const __amdgpu_buffer_rsrc_t rsa =
+      __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, (int)(abytes < BAD ? abytes : BAD), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, (short)0, g.N * g.ldb * 2, 0x00020000);
+  int aoff[PIN ? IA : 1], boff[PIN ? IB : 1];
+  if constexpr (PIN) {
+#pragma unroll
+    for (int i = 0; i < IA; ++i) aoff[i] = (int)(abase[i] - (const char*)g.A);
+#pragma unroll
+    for (int i = 0; i < IB; ++i) boff[i] = bbase[i] ? (int)(bbase[i] - (const char*)g.B) : BAD;
+  }
+  auto issue_pin = [&](int ks, const KPos& kp, int buf) {
+    char* st = smem + buf * STAGE;
+    const int k = ks * BK + chunk * 8;
+    const bool kv = k < g.K;
+#pragma unroll
+    for (int i = 0; i < IA; ++i) {
+      int off;
+      if constexpr (MODE == GEMM_CONV) {
+        int kh, kw, ci;
+        if (kblocked) {
+          kh = kp.kh; kw = kp.kw; ci = kp.cb * 64 + chunk * 8;
+        } else if (taps == 1) {
+          kh = kw = 0; ci = k;
+        } else {
+          conv_k_decode(k, g.Cin, g.KW, taps, kh, kw, ci);
+        }
+        const int ih = aih[i] + kh, iw = aiw[i] + kw;
+        const bool v = kv && arow[i] && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+        off = v ? aoff[i] + ((ih * g.W + iw) * g.Cin + ci) * 2 : BAD;
+      } else {
+        off = (kv && arow[i]) ? aoff[i] + k * 2 : BAD;
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lds_ptr_t)(st + ld_row(i, IA) * 128), 16, off, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {
+      const int off = (boff[i] != BAD && ks * BK < g.K) ? boff[i] + ks * BK * 2 : BAD;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lds_ptr_t)(st + A_BYTES + ld_row(i, IB) * 128), 16, off, 0, 0, 0);
+    }
+  };
   const KPos kp0{0, 0, 0};
 
   f32x4 acc[FM][FN];
@@ -206,7 +257,7 @@ __global__ __launch_bounds__(NT, NST == 1 ? 4 : 1) void gemm2_kernel(GemmArgs g)
       for (int j = 0; j < FN; ++j) {
         dres[i][j] = u32x2{0, 0};
         const int m = m0 + wr * TM + 16 * i + fr, n = n0 + wc * TN + 16 * j + 4 * fg;
-        if (g.R && m < g.M && n + 4 <= g.N) {
+        if (!PIN && g.R && m < g.M && n + 4 <= g.N) {
           const int rm = g.r_period > 0 ? m % g.r_period : m;
           dres[i][j] = ld8((const bf16*)g.R + (size_t)rm * g.ldr + n);
         }
@@ -220,14 +271,14 @@ __global__ __launch_bounds__(NT, NST == 1 ? 4 : 1) void gemm2_kernel(GemmArgs g)
   const bool efull = en + 8 <= g.N;
   // (BN = 256: only the first half here, the rest after the K loop, or the K loop would spill)
   // (P8: none before the loop, its phases hold more fragments live)
-  constexpr int NPRE = (P8 || NST == 1) ? 0 : BN == 256 ? NPASS / 2 : NPASS;
+  constexpr int NPRE = (P8 || NST == 1 || PIN) ? 0 : BN == 256 ? NPASS / 2 : NPASS;
   u32x4 rres[NPASS][RPT];
   auto fetch_res = [&](int pp) {
 #pragma unroll
     for (int q = 0; q < RPT; ++q) {
       rres[pp][q] = u32x4{0, 0, 0, 0};
       const int m = m0 + pp * EPI_ROWS + ert + q * RSTEP;
-      if (!DIRECT && g.R && g.vt_T == 0 && efull && m < g.M) {
+      if (!PIN && !DIRECT && g.R && g.vt_T == 0 && efull && m < g.M) {
         const int rm = g.r_period > 0 ? m % g.r_period : m;
         rres[pp][q] = ld16((const bf16*)g.R + (size_t)rm * g.ldr + en);
       }
@@ -357,6 +408,63 @@ __global__ __launch_bounds__(NT, NST == 1 ? 4 : 1) void gemm2_kernel(GemmArgs g)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       __builtin_amdgcn_s_barrier();             // stage read: the next K-step may refill it
     }
+  } else if constexpr (PIN) {
+    issue_pin(0, kp0, 0);
+    KPos kpn = kadv(kp0);
+    constexpr int NP = FM / 2;                   // A-fragment pairs per kk
+    for (int ks = 0; ks < nk; ++ks) {
+      // unconditional (past the end: zero lines into the free stage) -- a branch here leaves
+      // the compiler unsure of the outstanding LDS counts and every fragment group then waits
+      // on lgkmcnt(0)
+      issue_pin(ks + 1, kpn, (ks + 1) & 1);
+      kpn = kadv(kpn);
+      wait_vmcnt<LOADS>();
+      __builtin_amdgcn_s_barrier();
+      const char* st = smem + (ks & 1) * STAGE;
+      u32x4 bfr[2][FN], af[2][2];                // [kk][j], [pair parity][2 rows]
+      auto rd_b = [&](int kk) {
+#pragma unroll
+        for (int j = 0; j < FN; ++j) bfr[kk][j] = ld16(st + A_BYTES + swz(wc * TN + j * 16 + fr, 4 * kk + fg));
+      };
+      auto rd_a = [&](int kk, int p) {
+#pragma unroll
+        for (int u = 0; u < 2; ++u) af[p & 1][u] = ld16(st + swz(wr * TM + (2 * p + u) * 16 + fr, 4 * kk + fg));
+      };
+      rd_b(0);
+      rd_a(0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int sidx = 0; sidx < 2 * NP; ++sidx) {
+        const int kk = sidx / NP, p = sidx % NP;
+        int nrd = 0;
+        if (sidx + 1 < 2 * NP) {                 // next group's fragments, ahead of this one's MFMAs
+          const int kn = (sidx + 1) / NP, pn = (sidx + 1) % NP;
+          if (kn != kk) { rd_b(kn); nrd += FN; }
+          rd_a(kn, pn);
+          nrd += 2;
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+          for (int j = 0; j < FN; ++j) {
+            const int i = 2 * p + u;
+            acc[i][j] = DIRECT ? __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bfr[kk][j]),
+                                                                        __builtin_bit_cast(bf16x8, af[p & 1][u]), acc[i][j], 0, 0, 0)
+                               : __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, af[p & 1][u]),
+                                                                        __builtin_bit_cast(bf16x8, bfr[kk][j]), acc[i][j], 0, 0, 0);
+          }
+        // the reads first, then the MFMAs (else the scheduler sinks the reads between the MFMAs
+        // that free their registers, and each group waits on lgkmcnt(0))
+        if (nrd == 2) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        else if (nrd == FN + 2) __builtin_amdgcn_sched_group_barrier(0x100, FN + 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2 * FN, 0);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    wait_vmcnt<0>();                             // the zero-line stage, before the epilogue
+    bar_raw();                                   // reuses the LDS
   } else {
   issue(0, kp0, 0);
   KPos kpn = kadv(kp0);                          // K position of step ks+1
@@ -419,7 +527,7 @@ __global__ __launch_bounds__(NT, NST == 1 ? 4 : 1) void gemm2_kernel(GemmArgs g)
           }
         };
         const bool rpost = XA && g.res_post;
-        if (g.R && !rpost) add_res();
+        if (!PIN && g.R && !rpost) add_res();
         if constexpr (XA) {
           if (g.act) {
 #pragma unroll
@@ -429,7 +537,7 @@ __global__ __launch_bounds__(NT, NST == 1 ? 4 : 1) void gemm2_kernel(GemmArgs g)
 #pragma unroll
           for (int r = 0; r < 4; ++r) v[r] = fmaxf(v[r], 0.f);
         }
-        if (g.R && rpost) add_res();
+        if (!PIN && g.R && rpost) add_res();
         if (g.out_f32) {
           float* cp = (float*)g.C + (size_t)m * g.ldc + n;
           if (full) st16(cp, pack16<float>(v));
@@ -507,7 +615,7 @@ __global__ __launch_bounds__(NT, NST == 1 ? 4 : 1) void gemm2_kernel(GemmArgs g)
             }
           };
           const bool rpost = XA && g.res_post;
-          if (g.R && !rpost) add_res();
+          if (!PIN && g.R && !rpost) add_res();
           if constexpr (LN) {
             // fused post-norm LayerNorm (N == BN == 256): a row's 32 column groups are the 32
             // lanes of one half-wave, so the row statistics are five xor-shuffles away
@@ -535,7 +643,7 @@ __global__ __launch_bounds__(NT, NST == 1 ? 4 : 1) void gemm2_kernel(GemmArgs g)
 #pragma unroll
             for (int e = 0; e < 8; ++e) v[e] = fmaxf(v[e], 0.f);
           }
-          if (g.R && rpost) add_res();
+          if (!PIN && g.R && rpost) add_res();
           if (g.out_f32) {
             float* cp = (float*)g.C + (size_t)m * g.ldc + n;
             if (full) {
@@ -571,8 +679,17 @@ int launch_bn(const GemmArgs& g, int mode, hipStream_t s) {
       hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_LINEAR, false, false, 2, true>), grid, block, 0, s, g);
     return (int)hipGetLastError();
   }
+  // SPE_GEMM2_PIN=0: residual-free convs on the compiler-scheduled loop (A/B knob)
+  static const int pin = [] { const char* e = getenv("SPE_GEMM2_PIN"); return e ? atoi(e) : 1; }();
   if (mode == GEMM_CONV) {
-    hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_CONV, false>), grid, block, 0, s, g);
+    // (32-bit buffer offsets: operands below 2 GiB)
+    const long long abytes = (long long)((g.M + g.Ho * g.Wo - 1) / (g.Ho * g.Wo)) * g.H * g.W * g.Cin * 2;
+    // (the stem's tap-major K, Cin = 8, measured slower pinned: 0.33 -> 0.40 ms)
+    const bool kpos_scalar = conv_channel_blocked(g.Cin, g.KH * g.KW) || g.KH * g.KW == 1;
+    if (pin && !g.R && kpos_scalar && abytes < (1ll << 31) - (1 << 20) && (long long)g.N * g.ldb * 2 < (1ll << 31) - (1 << 20))
+      hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_CONV, false, false, 2, false, true>), grid, block, 0, s, g);
+    else
+      hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_CONV, false>), grid, block, 0, s, g);
   } else {
     if constexpr (BN == 256) {
       if (g.ln_g) {
