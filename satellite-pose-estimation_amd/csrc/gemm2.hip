@@ -69,7 +69,8 @@ constexpr int P8_MIN_K = 1024;
 // pinned fragment schedule in the 2-stage loop -- the reads of the next fragment group are
 // issued ahead of the current group's MFMAs and the order is fixed with sched_barrier, where
 // the compiler's schedule waits on lgkmcnt(0) before every 8 MFMAs.
-template <int BN, int MODE, bool LN, bool P8K = false, int NST = 2, bool XA = false, bool PIN = false>
+// BUF: stage through buffer_load ... lds (see PIN) without the pinned schedule.
+template <int BN, int MODE, bool LN, bool P8K = false, int NST = 2, bool XA = false, bool PIN = false, bool BUF = false>
 __global__ __launch_bounds__(NT, NST == 1 ? 4 : 1) void gemm2_kernel(GemmArgs g) {
   constexpr int WM = Cfg<BN>::WM, WN = Cfg<BN>::WN;
   constexpr int TM = BM / WM, TN = BN / WN, FM = TM / 16, FN = TN / 16;
@@ -141,9 +142,62 @@ __global__ __launch_bounds__(NT, NST == 1 ? 4 : 1) void gemm2_kernel(GemmArgs g)
     }
     return p;
   };
+  // PIN: the same loads as buffer_load ... lds (MUBUF: the compiler then counts only the LDS
+  // fragment reads on lgkmcnt -- pending FLAT-encoded global_load_lds make it wait lgkmcnt(0)
+  // before every fragment group).  32-bit byte offsets; out-of-range offsets read zeros.
+  constexpr int BAD = 0x7ffffff0;
+  const long long abytes = !(PIN || BUF) ? 0
+                           : MODE == GEMM_CONV ? (long long)((g.M + g.Ho * g.Wo - 1) / (g.Ho * g.Wo)) * g.H * g.W * g.Cin * 2
+                                               : (long long)g.M * g.lda * 2;
+  const __amdgpu_buffer_rsrc_t rsa =
+      __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, (int)(abytes < BAD ? abytes : BAD), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, (short)0, g.N * g.ldb * 2, 0x00020000);
+  int aoff[(PIN || BUF) ? IA : 1], boff[(PIN || BUF) ? IB : 1];
+  if constexpr (PIN || BUF) {
+#pragma unroll
+    for (int i = 0; i < IA; ++i) aoff[i] = (int)(abase[i] - (const char*)g.A);
+#pragma unroll
+    for (int i = 0; i < IB; ++i) boff[i] = bbase[i] ? (int)(bbase[i] - (const char*)g.B) : BAD;
+  }
+  auto issue_buf = [&](int ks, const KPos& kp, int buf, int ia0, int ia1, int ib0, int ib1) {
+    char* st = smem + buf * STAGE;
+    const int k = ks * BK + chunk * 8;
+    const bool kv = k < g.K;
+#pragma unroll
+    for (int i = 0; i < IA; ++i) {
+      if (i < ia0 || i >= ia1) continue;
+      int off;
+      if constexpr (MODE == GEMM_CONV) {
+        int kh, kw, ci;
+        if (kblocked) {
+          kh = kp.kh; kw = kp.kw; ci = kp.cb * 64 + chunk * 8;
+        } else if (taps == 1) {
+          kh = kw = 0; ci = k;
+        } else {
+          conv_k_decode(k, g.Cin, g.KW, taps, kh, kw, ci);
+        }
+        const int ih = aih[i] + kh, iw = aiw[i] + kw;
+        const bool v = kv && arow[i] && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+        off = v ? aoff[i] + ((ih * g.W + iw) * g.Cin + ci) * 2 : BAD;
+      } else {
+        off = (kv && arow[i]) ? aoff[i] + k * 2 : BAD;
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lds_ptr_t)(st + ld_row(i, IA) * 128), 16, off, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < IB; ++i) {
+      if (i < ib0 || i >= ib1) continue;
+      const int off = (boff[i] != BAD && ks * BK < g.K) ? boff[i] + ks * BK * 2 : BAD;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lds_ptr_t)(st + A_BYTES + ld_row(i, IB) * 128), 16, off, 0, 0, 0);
+    }
+  };
   // issue A instructions [ia0, ia1) and W instructions [ib0, ib1) of K-step ks (K position kp)
   // into stage buf (constant ranges after inlining; K-steps past the end load the zero line)
   auto issue_rng =[&](int ks, const KPos& kp, int buf, int ia0, int ia1, int ib0, int ib1) {
+    if constexpr (PIN || BUF) {
+      issue_buf(ks, kp, buf, ia0, ia1, ib0, ib1);
+      return;
+    }
     char* st = smem + buf * STAGE;
     const int k = ks * BK + chunk * 8;
     const bool kv = k < g.K;
@@ -180,53 +234,6 @@ __global__ __launch_bounds__(NT, NST == 1 ? 4 : 1) void gemm2_kernel(GemmArgs g)
     }
   };
   auto issue = [&](int ks, const KPos& kp, int buf) { issue_rng(ks, kp, buf, 0, IA, 0, IB); };
-  // PIN: the same loads as buffer_load ... lds (MUBUF: the compiler then counts only the LDS
-  // fragment reads on lgkmcnt -- pending FLAT-encoded global_load_lds make it wait lgkmcnt(0)
-  // before every fragment group).  32-bit byte offsets; out-of-range offsets read zeros.
-  constexpr int BAD = 0x7ffffff0;
-  const long long abytes = !PIN ? 0
-                           : MODE == GEMM_CONV ? (long long)((g.M + g.Ho * g.Wo - 1) / (g.Ho * g.Wo)) * g.H * g.W * g.Cin * 2
-                                               : (long long)g.M * g.lda * 2;
-  const __amdgpu_buffer_rsrc_t rsa =
-      __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, (int)(abytes < BAD ? abytes : BAD), 0x00020000);
-  const __amdgpu_buffer_rsrc_t rsb = __builtin_amdgcn_make_buffer_rsrc((void*)g.B, (short)0, g.N * g.ldb * 2, 0x00020000);
-  int aoff[PIN ? IA : 1], boff[PIN ? IB : 1];
-  if constexpr (PIN) {
-#pragma unroll
-    for (int i = 0; i < IA; ++i) aoff[i] = (int)(abase[i] - (const char*)g.A);
-#pragma unroll
-    for (int i = 0; i < IB; ++i) boff[i] = bbase[i] ? (int)(bbase[i] - (const char*)g.B) : BAD;
-  }
-  auto issue_pin = [&](int ks, const KPos& kp, int buf) {
-    char* st = smem + buf * STAGE;
-    const int k = ks * BK + chunk * 8;
-    const bool kv = k < g.K;
-#pragma unroll
-    for (int i = 0; i < IA; ++i) {
-      int off;
-      if constexpr (MODE == GEMM_CONV) {
-        int kh, kw, ci;
-        if (kblocked) {
-          kh = kp.kh; kw = kp.kw; ci = kp.cb * 64 + chunk * 8;
-        } else if (taps == 1) {
-          kh = kw = 0; ci = k;
-        } else {
-          conv_k_decode(k, g.Cin, g.KW, taps, kh, kw, ci);
-        }
-        const int ih = aih[i] + kh, iw = aiw[i] + kw;
-        const bool v = kv && arow[i] && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
-        off = v ? aoff[i] + ((ih * g.W + iw) * g.Cin + ci) * 2 : BAD;
-      } else {
-        off = (kv && arow[i]) ? aoff[i] + k * 2 : BAD;
-      }
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lds_ptr_t)(st + ld_row(i, IA) * 128), 16, off, 0, 0, 0);
-    }
-#pragma unroll
-    for (int i = 0; i < IB; ++i) {
-      const int off = (boff[i] != BAD && ks * BK < g.K) ? boff[i] + ks * BK * 2 : BAD;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lds_ptr_t)(st + A_BYTES + ld_row(i, IB) * 128), 16, off, 0, 0, 0);
-    }
-  };
   const KPos kp0{0, 0, 0};
 
   f32x4 acc[FM][FN];
@@ -409,14 +416,14 @@ __global__ __launch_bounds__(NT, NST == 1 ? 4 : 1) void gemm2_kernel(GemmArgs g)
       __builtin_amdgcn_s_barrier();             // stage read: the next K-step may refill it
     }
   } else if constexpr (PIN) {
-    issue_pin(0, kp0, 0);
+    issue(0, kp0, 0);
     KPos kpn = kadv(kp0);
     constexpr int NP = FM / 2;                   // A-fragment pairs per kk
     for (int ks = 0; ks < nk; ++ks) {
       // unconditional (past the end: zero lines into the free stage) -- a branch here leaves
       // the compiler unsure of the outstanding LDS counts and every fragment group then waits
       // on lgkmcnt(0)
-      issue_pin(ks + 1, kpn, (ks + 1) & 1);
+      issue(ks + 1, kpn, (ks + 1) & 1);
       kpn = kadv(kpn);
       wait_vmcnt<LOADS>();
       __builtin_amdgcn_s_barrier();
@@ -679,21 +686,30 @@ int launch_bn(const GemmArgs& g, int mode, hipStream_t s) {
       hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_LINEAR, false, false, 2, true>), grid, block, 0, s, g);
     return (int)hipGetLastError();
   }
-  // SPE_GEMM2_PIN=0: residual-free convs on the compiler-scheduled loop (A/B knob)
+  // SPE_GEMM2_PIN=0: residual-free convs on the compiler-scheduled loop; SPE_GEMM2_BUF=0: the
+  // other convs and linear problems staged with global_load_lds instead of buffer loads (A/B knobs)
   static const int pin = [] { const char* e = getenv("SPE_GEMM2_PIN"); return e ? atoi(e) : 1; }();
+  // (buffer staging without the pinned schedule measured neutral: 4806 vs 4786 img/s; off)
+  static const int buf = [] { const char* e = getenv("SPE_GEMM2_BUF"); return e ? atoi(e) : 0; }();
+  constexpr long long LIM = (1ll << 31) - (1 << 20);          // 32-bit buffer offsets
+  const bool bfits = (long long)g.N * g.ldb * 2 < LIM;
   if (mode == GEMM_CONV) {
-    // (32-bit buffer offsets: operands below 2 GiB)
     const long long abytes = (long long)((g.M + g.Ho * g.Wo - 1) / (g.Ho * g.Wo)) * g.H * g.W * g.Cin * 2;
     // (the stem's tap-major K, Cin = 8, measured slower pinned: 0.33 -> 0.40 ms)
     const bool kpos_scalar = conv_channel_blocked(g.Cin, g.KH * g.KW) || g.KH * g.KW == 1;
-    if (pin && !g.R && kpos_scalar && abytes < (1ll << 31) - (1 << 20) && (long long)g.N * g.ldb * 2 < (1ll << 31) - (1 << 20))
+    const bool fits = abytes < LIM && bfits;
+    if (pin && !g.R && kpos_scalar && fits)
       hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_CONV, false, false, 2, false, true>), grid, block, 0, s, g);
+    else if (buf && kpos_scalar && fits)
+      hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_CONV, false, false, 2, false, false, true>), grid, block, 0, s, g);
     else
       hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_CONV, false>), grid, block, 0, s, g);
   } else {
+    const bool fits = (long long)g.M * g.lda * 2 < LIM && bfits;
     if constexpr (BN == 256) {
       if (g.ln_g) {
-        hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_LINEAR, true>), grid, block, 0, s, g);
+        if (buf && fits) hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_LINEAR, true, false, 2, false, false, true>), grid, block, 0, s, g);
+        else hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_LINEAR, true>), grid, block, 0, s, g);
         return (int)hipGetLastError();
       }
     }
@@ -703,7 +719,8 @@ int launch_bn(const GemmArgs& g, int mode, hipStream_t s) {
         return (int)hipGetLastError();
       }
     }
-    hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_LINEAR, false>), grid, block, 0, s, g);
+    if (buf && fits) hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_LINEAR, false, false, 2, false, false, true>), grid, block, 0, s, g);
+    else hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_LINEAR, false>), grid, block, 0, s, g);
   }
   return (int)hipGetLastError();
 }
