@@ -27,6 +27,25 @@ __global__ void pack_input_kernel(const float* __restrict__ img, T* __restrict__
   }
 }
 
+// bf16 stem input for the pair-packed stem (forward.cpp): [B][S+6][S+6][4] with the conv's
+// 3-pixel zero border materialised (channel 3 zero), so a 16-byte chunk is two horizontally
+// adjacent pixels and every tap of the 7x7/s2 window is in range.  The border is rewritten on
+// every call (the buffer is shared with later activations).
+__global__ void pack_input_pad4_kernel(const float* __restrict__ img, bf16* __restrict__ out, int B, int S) {
+  const int P = S + 6;
+  const size_t npx = (size_t)B * P * P;
+  for (size_t p = blockIdx.x * (size_t)blockDim.x + threadIdx.x; p < npx; p += (size_t)gridDim.x * blockDim.x) {
+    const size_t b = p / ((size_t)P * P);
+    const int r = (int)(p - b * P * P), y = r / P - 3, x = r % P - 3;
+    u32x2 v{0, 0};
+    if (y >= 0 && y < S && x >= 0 && x < S) {
+      const float* src = img + b * 3 * S * S + (size_t)y * S + x;
+      v = u32x2{pack_bf16x2(src[0], src[(size_t)S * S]), pack_bf16x2(src[2 * (size_t)S * S], 0.f)};
+    }
+    st8(out + p * 4, v);
+  }
+}
+
 template <typename T>
 __global__ void maxpool_kernel(const T* __restrict__ in, T* __restrict__ out, int B, int H, int W, int C, int Ho, int Wo,
                                int ldo) {
@@ -184,6 +203,12 @@ int spe_launch_pack_input(const float* img, void* out, int B, int S, int dtype, 
   const size_t n = (size_t)B * S * S;
   if (dtype == SPE_DTYPE_BF16) hipLaunchKernelGGL(pack_input_kernel<bf16>, grid_for(n, 256), 256, 0, s, img, (bf16*)out, B, S);
   else hipLaunchKernelGGL(pack_input_kernel<float>, grid_for(n, 256), 256, 0, s, img, (float*)out, B, S);
+  return (int)hipGetLastError();
+}
+
+int spe_launch_pack_input_pad4(const float* img, void* out, int B, int S, hipStream_t s) {
+  const size_t n = (size_t)B * (S + 6) * (S + 6);
+  hipLaunchKernelGGL(pack_input_pad4_kernel, grid_for(n, 256), 256, 0, s, img, (bf16*)out, B, S);
   return (int)hipGetLastError();
 }
 

@@ -171,9 +171,15 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   const bool xa = spe_use_xattn(m);
   if (stages & SPE_STAGE_ENCODE) {
   // ---------------- backbone (REV/models/backbone.py:133-149)
-  CK(run_other(m, "eltwise.pack", 0.0, (double)B * S * S * (12 + 8 * m->esz), s, [&] { return spe_launch_pack_input(images, P(w.x0), B, S, dt, s); }));
+  const bool pairs = m->stem.Cin == 4;                 // bf16: pair-packed stem (registry.cpp)
+  if (pairs)
+    CK(run_other(m, "eltwise.pack", 0.0, (double)B * S * S * 12 + (double)B * (S + 6) * (S + 6) * 8, s,
+                 [&] { return spe_launch_pack_input_pad4(images, P(w.x0), B, S, s); }));
+  else
+    CK(run_other(m, "eltwise.pack", 0.0, (double)B * S * S * (12 + 8 * m->esz), s, [&] { return spe_launch_pack_input(images, P(w.x0), B, S, dt, s); }));
   {
-    GemmArgs g = conv_args(m->stem, P(w.x0), B, S, S, P(w.stem), 64);
+    GemmArgs g = pairs ? conv_args(m->stem, P(w.x0), B, S + 6, S + 6, P(w.stem), 64)
+                       : conv_args(m->stem, P(w.x0), B, S, S, P(w.stem), 64);
     g.act = ACT_RELU;
     CK(run_gemm(m, "conv.stem", g, GEMM_CONV, s));
   }

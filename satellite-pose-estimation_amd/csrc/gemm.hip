@@ -318,7 +318,10 @@ int spe_launch_gemm(const GemmArgs& g, int dtype, int mode, hipStream_t s) {
   constexpr int CEb = 8, CEf = 4;
   const int ce = dtype == SPE_DTYPE_BF16 ? CEb : CEf;
   if (g.K % ce) return -2;                                   // K must be whole 16-byte chunks
-  if (mode == GEMM_CONV && (g.Cin % ce)) return -3;
+  // (Cin == 4 pairs: see spe_launch_gemm2 -- a chunk is two adjacent in-range pixels)
+  const bool pairs = mode == GEMM_CONV && ce == 8 && g.Cin == 4 && g.pad == 0 && g.KW % 2 == 0 &&
+                     (g.Wo - 1) * g.stride + g.KW <= g.W && (g.Ho - 1) * g.stride + g.KH <= g.H;
+  if (mode == GEMM_CONV && (g.Cin % ce) && !pairs) return -3;
   if (g.ldb % 64) return -4;                                 // weights padded to 64 elements
   if ((g.lda % ce) || (g.ldc % (g.out_f32 ? 4 : ce)) || (g.R && (g.ldr % ce))) return -5;
   if (g.ln_g && dtype != SPE_DTYPE_BF16) return -5;   // fused LayerNorm: large-tile bf16 kernel only

@@ -892,7 +892,11 @@ bool spe_gemm_ln_fusable(const GemmArgs& g) {
 int spe_launch_gemm2(const GemmArgs& g, int mode, hipStream_t s) {
   if (mode != GEMM_LINEAR && mode != GEMM_CONV) return 1;
   if (g.M <= 0 || g.N <= 0) return 0;
-  if (g.K % 8 || g.ldb % 64 || g.lda % 8 || (mode == GEMM_CONV && g.Cin % 8)) return 1;
+  // conv chunks are 16 bytes of one pixel (Cin % 8 == 0), or two horizontally adjacent pixels
+  // (Cin == 4: the pair-packed stem, pre-padded input, even KW, every tap in range)
+  const bool pairs = mode == GEMM_CONV && g.Cin == 4 && g.pad == 0 && g.KW % 2 == 0 &&
+                     (g.Wo - 1) * g.stride + g.KW <= g.W && (g.Ho - 1) * g.stride + g.KH <= g.H;
+  if (g.K % 8 || g.ldb % 64 || g.lda % 8 || (mode == GEMM_CONV && g.Cin % 8 && !pairs)) return 1;
   if (g.out_f32 ? (g.ldc % 4) : (g.ldc % 8)) return 1;
   if (g.R && g.ldr % 8) return 1;
   {

@@ -6,6 +6,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 
@@ -305,7 +306,30 @@ int build_device(spe_model* m) {
   const auto& c = m->cfg;
   const int d = c.hidden_dim, ff = c.dim_feedforward, Q = c.num_queries;
   const std::string b = "backbone.0.body";
-  m->stem = make_conv(m, b + ".conv1.weight", b + ".bn1", "", 8, 2, 3);
+  static const int stem_pairs = [] { const char* e = getenv("SPE_STEM_PAIRS"); return e ? atoi(e) : 1; }();
+  if (m->esz == 2 && stem_pairs) {
+    // bf16: the pair-packed stem (SPE_STEM_PAIRS=0: the 8-channel tap-major stem, A/B knob).  The 7x7/s2/p3 conv over 3 channels runs as a 7x8/s2 conv
+    // over the zero-bordered 4-channel input (spe_launch_pack_input_pad4): k = (kh*8 + kw)*4 + ci,
+    // kw = 7 and ci = 3 have zero weights, K = 224 (4 K-steps) instead of 7*7*8 = 392 (7 K-steps),
+    // and each 16-byte chunk is the taps kw, kw+1 of one row.
+    std::vector<float> w, bias;
+    fold_conv(m, b + ".conv1.weight", b + ".bn1", "", w, bias);
+    constexpr int KH = 7, KW = 8, CI = 4, K = KH * KW * CI;
+    std::vector<float> rows((size_t)64 * K, 0.f);
+    if (m->dmem)
+      for (int co = 0; co < 64; ++co)
+        for (int ci = 0; ci < 3; ++ci)
+          for (int y = 0; y < 7; ++y)
+            for (int x = 0; x < 7; ++x)
+              rows[(size_t)co * K + (y * KW + x) * CI + ci] = w[(((size_t)co * 3 + ci) * 7 + y) * 7 + x];
+    Conv c;
+    c.N = 64; c.K = K; c.Kpad = pad64(K); c.Cin = CI; c.KH = KH; c.KW = KW; c.stride = 2; c.pad = 0;
+    c.w = upload_rows(m, rows, c.N, c.K, c.Kpad);
+    c.bias = upload_f32(m, bias.data(), bias.size());
+    m->stem = c;
+  } else {
+    m->stem = make_conv(m, b + ".conv1.weight", b + ".bn1", "", 8, 2, 3);
+  }
   m->blocks.clear();
   const int nblk[3] = {3, 4, 6};
   for (int li = 0; li < 3; ++li)

@@ -104,6 +104,8 @@ int spe_ffn_splits(int M, int F);  // split count spe_launch_ffn_ln would use fo
 int spe_launch_preprocess(const uint8_t* frames, int B, int H, int W, int C, const double* bbox, int S,
                           float* images, float* clip_bbox, int32_t* status, hipStream_t s);
 int spe_launch_pack_input(const float* img, void* out, int B, int S, int dtype, hipStream_t s);
+// bf16 [B][S+6][S+6][4], zero border of 3 (the pair-packed stem's input, forward.cpp)
+int spe_launch_pack_input_pad4(const float* img, void* out, int B, int S, hipStream_t s);
 int spe_launch_maxpool3s2(const void* in, void* out, int B, int H, int W, int C, int Ho, int Wo,
                           int dtype, hipStream_t s, int ldo = 0);   // ldo: output row stride (0 = C)
 int spe_launch_upsample2x(const void* in, void* out, int B, int H, int W, int C, int dtype, hipStream_t s);
