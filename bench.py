@@ -26,9 +26,10 @@ PEAK = {"bf16": {"mfma": 2500.0}, "fp32": {"mfma": 157.3}, "hbm": 8000.0}   # TF
 # profiler symbol of each launch class (to match profiles/*kernel_stats.csv rows)
 # (rocprofv3 prints the attention kernels mangled: it does not demangle the __bf16 / _Float16
 # template arguments, DF16b / DF16_)
-KIND_SYMBOL = {"attn.enc": "_ZN12_GLOBAL__N_113attn16_kernelILi0EDF16bEEv8AttnArgs",
-               "attn.dec_self": "_ZN12_GLOBAL__N_113attn16_kernelILi1EDF16bEEv8AttnArgs",
-               "attn.dec_cross": "xattn_kernel", "ffn.enc": "ffn_ln_kernel<3>", "ffn.dec": "ffn_ln_kernel<2>"}
+# (bf16 models' encoder attention: bf16 q/k, fp16 V^T and P -- attn16_kernel<0, bf16, f16>)
+KIND_SYMBOL = {"attn.enc": "_ZN12_GLOBAL__N_113attn16_kernelILi0EDF16bDF16_EEv8AttnArgs",
+               "attn.dec_self": "_ZN12_GLOBAL__N_113attn16_kernelILi1EDF16bDF16bEEv8AttnArgs",
+               "attn.dec_cross": "xattn_kernel", "ffn.enc": "ffn_pipe_kernel<3, true, 6>", "ffn.dec": "ffn_ln_kernel<2, 3>"}
 
 
 # BASELINE.json configs: per-GPU shapes (configs 3-5 are quoted at bs=256 over 8 GPUs = 32/GPU)
@@ -357,7 +358,11 @@ def main():
                                 f"with sigma head, {args.queries} queries, {args.size}x{args.size}, sigma-weighted "
                                 f"EPnP-RANSAC + self-assessment (solver={args.solver}; SURVEY 8f.4, not a BASELINE config)"),
                    "global_batch": B * world, "per_gpu_batch": B, "input_size": args.size,
-                   "num_queries": args.queries, "attention_dtype": args.attn_dtype,
+                   "num_queries": args.queries,
+                   # bf16 models' encoder attention keeps q/k bf16 and runs V^T and P in fp16 (finer
+                   # mantissa than bf16; attention.hip TV)
+                   "attention_dtype": ("bf16 q/k, fp16 V/P" if args.attn_dtype == "bf16" and args.dtype == "bf16"
+                                       and os.environ.get("SPE_ATTN_F16V", "1") != "0" else args.attn_dtype),
                    "parallelism": f"dp{world} (image sharding)"},
         "roofline": {"kernel": dominant, "kernel_symbol": KIND_SYMBOL.get(dominant, dominant).replace(
                          "DF16b", "DF16_" if args.attn_dtype == "fp16" else "DF16b"),
