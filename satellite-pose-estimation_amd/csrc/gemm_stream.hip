@@ -42,7 +42,12 @@ enum { EPI_ROW = 0, EPI_LN = 1, EPI_VT = 2 };
 // drain the prefetched tiles before every multiply.
 __device__ __attribute__((aligned(256))) uint32_t g_sg_sink[64];
 
-template <int K, int BN, int RF, int OCC, int NB, bool HAS_R, int EPI>
+// CP: the pair-packed stem (forward.cpp, registry.cpp) as a streaming GEMM.  Its K order
+// k = (kh*8 + kw)*4 + ci makes fragment kf (32 elements = 64 bytes) the kh = kf row of the
+// 7x8 window: 8 adjacent 4-channel pixels of the zero-bordered input, contiguous.  So A row m
+// (output pixel b, oh, ow) is 8 pieces of 64 B at a stride of one input row; piece 7 (kh = 7,
+// zero weights) stays inside the bordered image.
+template <int K, int BN, int RF, int OCC, int NB, bool HAS_R, int EPI, bool CP = false>
 __global__ __launch_bounds__(256, OCC) void sgemm_kernel(GemmArgs g, int ns_count, int row_tiles) {
   constexpr int KB = K * 2;                          // bytes of one W / A row
   constexpr int KF = K / 32, JF = BN / 16;           // K fragments, 16-column fragments
@@ -102,9 +107,17 @@ __global__ __launch_bounds__(256, OCC) void sgemm_kernel(GemmArgs g, int ns_coun
     for (int rf = 0; rf < RF; ++rf) {
       int m = t * TR + 16 * rf + fr;
       m = m < g.M ? m : g.M - 1;                    // clamp: rows past M are computed, not stored
-      const char* p = (const char*)g.A + (size_t)m * g.lda * 2 + fg * 16;
+      if constexpr (CP) {
+        const int hw = g.Ho * g.Wo, b = m / hw, r = m - b * hw, oh = r / g.Wo, ow = r - oh * g.Wo;
+        const char* p = (const char*)g.A + (((size_t)b * g.H + oh * g.stride) * g.W + ow * g.stride) * 8 + fg * 16;
+        const int rs = g.W * 8;
 #pragma unroll
-      for (int kf = 0; kf < KF; ++kf) a[rf][kf] = ld16(p + kf * 64);
+        for (int kf = 0; kf < KF; ++kf) a[rf][kf] = ld16(p + kf * rs);
+      } else {
+        const char* p = (const char*)g.A + (size_t)m * g.lda * 2 + fg * 16;
+#pragma unroll
+        for (int kf = 0; kf < KF; ++kf) a[rf][kf] = ld16(p + kf * 64);
+      }
     }
   };
   auto load_r = [&](int t, u32x2 (&r)[RF][JF]) {
@@ -292,12 +305,12 @@ bool sgemm_enabled() {
   return on;
 }
 
-template <int K, int BN, int RF, int OCC, int NB, bool HAS_R, int EPI>
+template <int K, int BN, int RF, int OCC, int NB, bool HAS_R, int EPI, bool CP = false>
 int launch_k(const GemmArgs& g, hipStream_t s) {
   const int row_tiles = (g.M + RF * 16 - 1) / (RF * 16), nsc = g.N / BN;
   const int G = (spe_cu_count() * OCC / nsc) * nsc;
   if ((long)row_tiles < 2L * (G / nsc) * 4) return 1;    // fewer than two tiles per wave
-  hipLaunchKernelGGL((sgemm_kernel<K, BN, RF, OCC, NB, HAS_R, EPI>), dim3(G), dim3(256), 0, s, g, nsc, row_tiles);
+  hipLaunchKernelGGL((sgemm_kernel<K, BN, RF, OCC, NB, HAS_R, EPI, CP>), dim3(G), dim3(256), 0, s, g, nsc, row_tiles);
   spe_gemm_last_path = 2;
   return (int)hipGetLastError();
 }
@@ -321,6 +334,15 @@ int launch_kbn(const GemmArgs& g, hipStream_t s) {
 
 // Returns 1 when the problem is not for this kernel (the caller takes gemm2 / gemm).
 int spe_launch_sgemm(const GemmArgs& g, int mode, hipStream_t s) {
+  if (mode == GEMM_CONV && sgemm_enabled()) {
+    // the pair-packed stem (see CP): 7x8 window, 4 channels, pre-bordered input, N = 64
+    static const int on = [] { const char* e = getenv("SPE_SG_STEM"); return e ? atoi(e) : 1; }();
+    if (on && g.Cin == 4 && g.KH == 7 && g.KW == 8 && g.pad == 0 && g.K == 224 && g.ldb == 256 && g.N == 64 &&
+        !g.R && !g.ln_g && g.vt_T == 0 && g.act <= ACT_RELU && !g.res_post && !g.out_f32 && g.ldc % 4 == 0 &&
+        (g.Ho - 1) * g.stride + 8 <= g.H && (g.Wo - 1) * g.stride + 8 <= g.W)
+      return launch_k<256, 64, 1, 2, 4, false, EPI_ROW, true>(g, s);
+    return 1;
+  }
   if (!sgemm_enabled() || mode != GEMM_LINEAR || g.M <= 0) return 1;
   if (g.act > ACT_RELU || g.res_post || g.out_f32) return 1;
   if (g.ldb < g.K || g.ldb % 8 || g.lda % 8 || g.ldc % 4 || (g.R && g.ldr % 4)) return 1;

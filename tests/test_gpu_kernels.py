@@ -6,6 +6,7 @@ pre-rounded to bf16 so only accumulation order and the bf16 output rounding rema
 max|d| <= 1e-2 * scale (scale = max|reference|, at least 1).
 """
 import ctypes
+import os
 
 import numpy as np
 import pytest
@@ -118,6 +119,32 @@ def test_gemm_conv_avgpool_shortcut(gpu_device, dtype, B, H, Cin, Cout):
     _gemm(dtype, 2, x.permute(0, 2, 3, 1).contiguous(), Wp, C.shape[0], Cout, K, 0, K, C, Cout,
           conv=(H, H, Cin, 2, 2, 2, 0))
     _close(C, ref.permute(0, 2, 3, 1).reshape(-1, Cout), tol)
+
+
+@pytest.mark.parametrize("B,S,path", [(2, 416, 2), (1, 416, 1), (1, 64, 0), (3, 130, 0)])
+def test_gemm_conv_pair_packed_stem(gpu_device, B, S, path):
+    """bf16 stem as registry.cpp packs it: the 7x7/s2/p3 conv over 3 channels run as a 7x8/s2
+    conv over the zero-bordered 4-channel input (k = (kh*8 + kw)*4 + ci, kw = 7 and ci = 3 zero),
+    16-byte chunks = two adjacent pixels; against torch conv2d on the same bf16 operands.  The
+    shapes reach the streaming kernel (path 2, sgemm CP), the 256-row tiles (1) and gemm.hip (0)."""
+    dt = torch.bfloat16
+    g = torch.Generator(device="cpu").manual_seed(S + B)
+    x = torch.randn(B, 3, S, S, generator=g).to(gpu_device, dt)
+    w = (torch.randn(64, 3, 7, 7, generator=g) / 12).to(gpu_device, dt)
+    bias = torch.randn(64, generator=g).to(gpu_device)
+    ref = torch.relu(F.conv2d(x.float(), w.float(), bias, stride=2, padding=3))
+    P = S + 6
+    xp = torch.zeros(B, P, P, 4, dtype=dt, device=gpu_device)
+    xp[:, 3:3 + S, 3:3 + S, :3] = x.permute(0, 2, 3, 1)
+    w8 = torch.zeros(64, 7, 8, 4, dtype=dt, device=gpu_device)
+    w8[:, :, :7, :3] = w.permute(0, 2, 3, 1)
+    Wp = _padded_weight(w8.reshape(64, 224), 256, dt)
+    Ho = (P - 7) // 2 + 1
+    C = torch.zeros(B * Ho * Ho, 64, dtype=dt, device=gpu_device)
+    _gemm("bf16", 2, xp, Wp, C.shape[0], 64, 224, 0, 256, C, 64, bias=bias, relu=1, conv=(P, P, 4, 7, 8, 2, 0))
+    if os.environ.get("SPE_SG_STEM", "1") != "0" and os.environ.get("SPE_SGEMM", "1") != "0":
+        assert _lib.lib().spe_debug_gemm_path() == path
+    _close(C, ref.permute(0, 2, 3, 1).reshape(-1, 64), 2e-2)
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "fp32"])
