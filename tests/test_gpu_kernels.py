@@ -265,8 +265,11 @@ def test_gemm_row_periodic_residual(gpu_device, M):
     _close(C, ref, tol)
 
 
+# (residual-free convs with Cin % 64 == 0 or 1x1 take the pinned-schedule kernel (gemm2 PIN),
+#  the others the compiler-scheduled loop; Cout 320 leaves a partial 64-wide column tile)
 @pytest.mark.parametrize("Cin,Cout,k,s,p", [(64, 64, 3, 1, 1), (64, 128, 1, 1, 0), (32, 256, 3, 2, 1), (8, 64, 7, 2, 3),
-                                            (128, 256, 3, 2, 1), (256, 256, 3, 1, 1)])
+                                            (128, 256, 3, 2, 1), (256, 256, 3, 1, 1), (128, 320, 3, 1, 1),
+                                            (64, 128, 1, 2, 0)])
 def test_gemm_large_tile_conv(gpu_device, Cin, Cout, k, s, p):
     _, dt, tol = DT["bf16"]
     B = 2 if Cin == 256 else 4                          # 133 row tiles: the 128..255-tile grids
