@@ -32,7 +32,27 @@ CASES = {
     "s128_q11_l2": (SpeConfig(input_size=128, num_queries=11, enc_layers=2, dec_layers=2), 2, 7, 11),
     "s416_q11_l6": (SpeConfig(input_size=416, num_queries=11, enc_layers=6, dec_layers=6), 2, 0, 1),
     "s224_q30_l4": (SpeConfig(input_size=224, num_queries=30, enc_layers=4, dec_layers=4), 1, 3, 5),
+    # BASELINE config 5: 640x640, 40 queries, 6/6 (REV/train_resnet50s8_query40.sh:23-43 scaled
+    # to BASELINE's input size and depth)
+    "s640_q40_l6": (SpeConfig(input_size=640, num_queries=40, enc_layers=6, dec_layers=6), 1, 13, 17),
+    # BASELINE config 4: the 416/Q11/6-6 DETR with the UNC sigma head on the last decoder output
+    "s416_q11_l6_sigma": (SpeConfig(input_size=416, num_queries=11, enc_layers=6, dec_layers=6, sigma_head=True),
+                          2, 19, 23),
 }
+
+
+def _unc_sigma_mlp(sd):
+    """The reference's own UNC sigma head module: `MLP(hidden, hidden, 1, num_layers=3)`
+    (UNC/src/zoo/rtdetr/rtdetr_decoder.py:24-37, instantiated at :295-297), loaded through the
+    module stubs of oracle/gen_golden_rtdetr.py, with this case's `sigma_embed.*` weights."""
+    import torch
+    from gen_golden_rtdetr import import_reference
+    _, _, dec, _ = import_reference()
+    d = sd["sigma_embed.layers.0.weight"].shape[1]
+    mlp = dec.MLP(d, d, 1, num_layers=3)
+    mlp.load_state_dict({k[len("sigma_embed."):]: torch.from_numpy(v) for k, v in sd.items()
+                         if k.startswith("sigma_embed.")}, strict=True)
+    return mlp.eval()
 
 
 def _import_reference():
@@ -65,10 +85,14 @@ def main():
     torch.set_num_threads(os.cpu_count() or 8)
     build_model, PostProcess = _import_reference()
     out_dir = os.path.join(REPO, "tests", "golden")
+    only = set(sys.argv[1:])
     for tag, (cfg, B, wseed, iseed) in CASES.items():
+        if only and tag not in only:
+            continue
         model, _, _ = build_model(_args(cfg))
         w = random_weights(cfg, wseed)
-        missing, unexpected = model.load_state_dict({k: torch.from_numpy(v) for k, v in w.items()}, strict=True), None
+        rev_w = {k: torch.from_numpy(v) for k, v in w.items() if not k.startswith("sigma_embed.")}
+        model.load_state_dict(rev_w, strict=True)
         model.eval()
         batch = synthetic_batch(cfg, B, iseed)
         stages = {}
@@ -93,6 +117,13 @@ def main():
             "pp_probs": np.stack([r["logits"] for r in pp]), "pp_points": np.stack([r["points"] for r in pp]),
             "clip_bbox": batch["clip_bbox"],
         }
+        if cfg.sigma_head:
+            # UNC semantics: log-sigma = sigma_embed(hs_last).repeat(1, 1, 2)
+            # (rtdetr_decoder.py:367), sigma = exp(log-sigma) (rtdetr_postprocessor.py:53)
+            with torch.no_grad():
+                ls = _unc_sigma_mlp(w)(stages["hs"][-1]).repeat(1, 1, 2)
+            rec["pred_sigmas"] = ls.numpy()
+            rec["pp_sigmas"] = torch.exp(ls).numpy()
         for k in ("xs8", "xs16", "neck", "memory"):
             rec["chk_" + k] = _chk(stages[k].numpy())
         path = os.path.join(out_dir, f"model_{tag}.npz")

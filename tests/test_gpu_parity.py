@@ -42,7 +42,22 @@ def _golden(tag):
     return g, cfg
 
 
-@pytest.mark.parametrize("tag", ["s128_q11_l2", "s224_q30_l4", "s416_q11_l6"])
+# s640_q40_l6 = BASELINE config 5 (640x640, 40 queries, 6/6: T = 6400 tokens);
+# s416_q11_l6_sigma = config 4's model (the UNC sigma head on the DETR's last decoder output)
+GOLDEN_TAGS = ["s128_q11_l2", "s224_q30_l4", "s416_q11_l6", "s640_q40_l6", "s416_q11_l6_sigma"]
+
+
+def _check_sigmas(o, g, log_tol, rel_tol):
+    """sigma head: log-sigma (`pred_sigmas`) against the reference UNC MLP's output on the
+    reference hs, and the fused PostProcess exp (`sigmas`) relative to its golden."""
+    ls = o["pred_sigmas"].cpu().numpy()
+    assert np.abs(ls - g["pred_sigmas"]).max() <= log_tol
+    np.testing.assert_array_equal(ls[..., 0], ls[..., 1])          # .repeat(1, 1, 2)
+    sg = o["sigmas"].cpu().numpy()
+    assert (np.abs(sg - g["pp_sigmas"]) / g["pp_sigmas"]).max() <= rel_tol
+
+
+@pytest.mark.parametrize("tag", GOLDEN_TAGS)
 def test_forward_fp32_matches_reference(gpu_device, tag):
     g, cfg = _golden(tag)
     b = synthetic_batch(cfg, int(g["batch"]), int(g["image_seed"]))
@@ -57,20 +72,24 @@ def test_forward_fp32_matches_reference(gpu_device, tag):
     assert np.abs(lg - g["pred_logits"]).max() <= 2e-3
     assert np.abs(o["points_px"].cpu().numpy() - g["pp_points"]).max() <= 0.05
     assert np.abs(o["probs"].cpu().numpy() - g["pp_probs"]).max() <= 1e-3
+    if cfg.sigma_head:
+        _check_sigmas(o, g, log_tol=2e-3, rel_tol=2e-3)
 
 
 @pytest.mark.parametrize("attn_dtype", [None, "fp16"])
-@pytest.mark.parametrize("tag", ["s128_q11_l2", "s224_q30_l4", "s416_q11_l6"])
+@pytest.mark.parametrize("tag", GOLDEN_TAGS)
 def test_forward_bf16_close_to_reference(gpu_device, tag, attn_dtype):
     """bf16 throughput mode, with bf16 or fp16 (config 5) encoder-attention operands."""
     g, cfg = _golden(tag)
     b = synthetic_batch(cfg, int(g["batch"]), int(g["image_seed"]))
     m = _model(cfg, "bf16", int(g["weight_seed"]), attn_dtype)
-    o = m(torch.from_numpy(b["images"]).to(gpu_device))
+    o = m(torch.from_numpy(b["images"]).to(gpu_device), clip_bbox=torch.from_numpy(b["clip_bbox"]).float().to(gpu_device))
     torch.cuda.synchronize()
     assert np.isfinite(o["pred_points"].cpu().numpy()).all()
     assert np.abs(o["pred_points"].cpu().numpy() - g["pred_points"]).max() <= 2e-2
     assert np.abs(o["pred_logits"].cpu().numpy() - g["pred_logits"]).max() <= 0.25
+    if cfg.sigma_head:
+        _check_sigmas(o, g, log_tol=0.25, rel_tol=0.3)
 
 
 def test_forward_batch_independence(gpu_device):
