@@ -98,6 +98,29 @@ def parse():
     return a
 
 
+def host_cpu():
+    """CPU model name and logical CPU count of this host (BASELINE.md section 3 fields)."""
+    name = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    name = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {"cpu_model": name, "host_logical_cpus": os.cpu_count()}
+
+
+def _baseline_record(n, dt, threads, sample):
+    v = n / dt
+    return {"value": v, "unit": "images/s", "cores": threads, "threads_used": threads,
+            "value_per_core": v / threads, "kind": "port",
+            "kind_note": "the reference's evaluate() cannot run here (cv2 / mathutils / torchvision absent and the "
+                         "reference never ships to the GPU box): oracle/ restatement of the same path timed instead",
+            **host_cpu(), "sample": sample}
+
+
 def cpu_baseline(cfg, seconds, solver="epnp"):
     """Oracle port (torch-fp32 CPU model + C solver) timed on this host's cores on a bounded
     sample of the same workload: single images of the bench's shape, repeated until `seconds`
@@ -127,9 +150,10 @@ def cpu_baseline(cfg, seconds, solver="epnp"):
             if time.perf_counter() - t0 >= seconds:
                 break
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{n} single-image passes ({cfg.input_size}x{cfg.input_size}, Q={cfg.num_queries}, "
-                      f"{cfg.enc_layers}/{cfg.dec_layers}, fp32 torch-CPU model + C {solver} oracle) in {dt:.1f}s"}
+    return _baseline_record(n, dt, threads,
+                            f"{n} single-image passes ({cfg.input_size}x{cfg.input_size}, Q={cfg.num_queries}, "
+                            f"{cfg.enc_layers}/{cfg.dec_layers}{', sigma head' if cfg.sigma_head else ''}, fp32 "
+                            f"torch-CPU model + C {solver} oracle) in {dt:.1f}s")
 
 
 def cpu_baseline_rtdetr(rcfg, seconds):
@@ -158,9 +182,9 @@ def cpu_baseline_rtdetr(rcfg, seconds):
             if time.perf_counter() - t0 >= seconds:
                 break
     dt = time.perf_counter() - t0
-    return {"value": n / dt, "unit": "images/s", "cores": threads, "kind": "port",
-            "sample": f"{n} single-image passes (RT-DETR r{rcfg.depth}vd {rcfg.input_size}x{rcfg.input_size}, "
-                      f"Q={rcfg.num_queries}, fp32 torch-CPU restatement + C epnp_ransac_sigma oracle) in {dt:.1f}s"}
+    return _baseline_record(n, dt, threads,
+                            f"{n} single-image passes (RT-DETR r{rcfg.depth}vd {rcfg.input_size}x{rcfg.input_size}, "
+                            f"Q={rcfg.num_queries}, fp32 torch-CPU restatement + C epnp_ransac_sigma oracle) in {dt:.1f}s")
 
 
 def traffic_for(kind, grid, attn_dtype):
@@ -262,10 +286,8 @@ def main():
         out = pipe.run()
         if world > 1:
             # on the solver's stream: the record exchange waits for this batch's poses only
-            with torch.cuda.stream(out.get("stream") or torch.cuda.current_stream()):
-                rec = sd.pack_records(out["poses"]["quat"], out["poses"]["tvec"], out["s_t"], out["s_q"],
-                                      out["poses"]["status"])
-                sd.all_gather_records(rec)
+            sd.exchange_pose_records(out["poses"], out["s_t"], out["s_q"],
+                                     stream=out.get("stream") or torch.cuda.current_stream())
         return out
 
     for _ in range(max(args.warmup, 1)):

@@ -155,6 +155,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
     return fail(SPE_E_ARG, "bad argument");
   if ((stages & SPE_STAGE_ENCODE) && !images) return fail(SPE_E_ARG, "null images");
   if ((stages & SPE_STAGE_DECODE) && (!out || !out->logits || !out->points)) return fail(SPE_E_ARG, "null outputs");
+  if (m->family != 0) return fail(SPE_E_ARG, "not a DETR model (use spe_rtdetr_forward)");
   if (!m->finalized) return fail(SPE_E_STATE, "model not finalized");
   const Ws w = spe_plan(m, B);
   if ((int64_t)w.total > ws_bytes) return fail(SPE_E_WORKSPACE, "workspace too small");

@@ -100,11 +100,15 @@ __global__ __launch_bounds__(SEL_NT) void query_select_kernel(RtSelectArgs a) {
   for (int t = tid; t < L; t += SEL_NT) {
     const float* lg = a.logits + row_of(t) * a.C;
     float mx = lg[0];
-    for (int c = 1; c < a.C; ++c) mx = fmaxf(mx, lg[c]);
-    sc[t] = mx;
+    bool nan = mx != mx;
+    for (int c = 1; c < a.C; ++c) { mx = fmaxf(mx, lg[c]); nan |= lg[c] != lg[c]; }
+    // torch: max(-1) propagates NaN and topk ranks NaN above every number; NaN is kept
+    // out of sc (it marks taken tokens below), so a NaN score ranks as +inf
+    sc[t] = nan ? INFINITY : mx;
   }
   __syncthreads();
-  // Q rounds of block argmax: descending values, lower token index first among equal values
+  // Q rounds of block argmax: descending values, lower token index first among equal values;
+  // taken tokens hold NaN, which fails every comparison
   for (int k = 0; k < a.Q; ++k) {
     float bv = -INFINITY;
     int bi = 0x7fffffff;
@@ -125,8 +129,9 @@ __global__ __launch_bounds__(SEL_NT) void query_select_kernel(RtSelectArgs a) {
       int idx = ri[0];
       for (int w = 1; w < SEL_NT / 64; ++w)
         if (rv[w] > v || (rv[w] == v && ri[w] < idx)) { v = rv[w]; idx = ri[w]; }
+      if (idx < 0 || idx >= L) idx = 0;         // unreachable while L >= Q (host-checked)
       sel[k] = idx;
-      sc[idx] = -INFINITY;
+      sc[idx] = __builtin_nanf("");
       a.topk[(size_t)b * a.Q + k] = idx;
     }
     __syncthreads();

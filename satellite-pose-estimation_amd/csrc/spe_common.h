@@ -75,11 +75,22 @@ template <> SPE_DEV void unpack16<f16>(u32x4 v, float* f) {
 template <> SPE_DEV u32x4 pack16<f16>(const float* f) {
   return u32x4{pack_f16x2(f[0], f[1]), pack_f16x2(f[2], f[3]), pack_f16x2(f[4], f[5]), pack_f16x2(f[6], f[7])};
 }
-// 16-bit GEMM outputs: bf16 unless the launch asked for fp16 (GemmArgs::out_f16)
-SPE_DEV uint32_t pack_out2(float lo, float hi, bool f16o) { return f16o ? pack_f16x2(lo, hi) : pack_bf16x2(lo, hi); }
-SPE_DEV u32x4 pack_out8(const float* f, bool f16o) { return f16o ? pack16<f16>(f) : pack16<bf16>(f); }
+// 16-bit GEMM outputs: bf16 unless the launch asked for fp16 (GemmArgs::out_f16).  fp16 outputs
+// saturate at +-65504 instead of overflowing to inf (an inf V or q/k entry would turn the
+// attention output into NaN); NaN stays NaN.
+SPE_DEV float sat_f16(float v) { return fabsf(v) > 65504.f ? copysignf(65504.f, v) : v; }
+SPE_DEV uint32_t pack_out2(float lo, float hi, bool f16o) {
+  return f16o ? pack_f16x2(sat_f16(lo), sat_f16(hi)) : pack_bf16x2(lo, hi);
+}
+SPE_DEV u32x4 pack_out8(const float* f, bool f16o) {
+  if (!f16o) return pack16<bf16>(f);
+  float s[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) s[i] = sat_f16(f[i]);
+  return pack16<f16>(s);
+}
 SPE_DEV void store_out1(void* base, size_t i, float v, bool f16o) {
-  if (f16o) reinterpret_cast<f16*>(base)[i] = (f16)v;
+  if (f16o) reinterpret_cast<f16*>(base)[i] = (f16)sat_f16(v);
   else reinterpret_cast<bf16*>(base)[i] = (bf16)v;
 }
 

@@ -57,6 +57,16 @@ def all_gather_records(rec):
     return torch.cat(parts, 0)
 
 
+def exchange_pose_records(poses, s_t, s_q, stream=None):
+    """The bench / pipeline's per-batch exchange: pack this rank's pose records and all-gather
+    them, ordered after the batch's solver work (issued on `stream`, the solver's stream, when
+    given).  Returns [world*B, RECORD_LEN] (this rank's block alone when not distributed)."""
+    if stream is not None:
+        with torch.cuda.stream(stream):
+            return all_gather_records(pack_records(poses["quat"], poses["tvec"], s_t, s_q, poses["status"]))
+    return all_gather_records(pack_records(poses["quat"], poses["tvec"], s_t, s_q, poses["status"]))
+
+
 def all_gather_log(log: dict) -> dict:
     """Merge every rank's SpeedEval.log (host objects, evaluate() path)."""
     if not is_dist() or dist.get_world_size() == 1:

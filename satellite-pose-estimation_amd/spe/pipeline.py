@@ -160,13 +160,16 @@ class PosePipeline:
             self.out = self._body()
             return self.out
         if self.graph is None:
+            # warm-up and capture on the SAME stream: the model workspace and the solver's
+            # scratch are keyed by (device, stream), so the warm-up sizes exactly the buffers the
+            # captured launches use and nothing is allocated during capture
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):
-                self._body()                       # warm-up: allocations happen outside capture
+                self._body()
             torch.cuda.current_stream().wait_stream(s)
             self.graph = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.graph):
+            with torch.cuda.graph(self.graph, stream=s):
                 self.out = self._body()
         self.graph.replay()
         return self.out

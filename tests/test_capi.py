@@ -67,3 +67,22 @@ def test_bad_configs_rejected():
     assert _create(SpeConfig(hidden_dim=128, nheads=4))[0] == -1
     assert _create(SpeConfig(input_size=420))[0] == -1
     assert _create(SpeConfig(num_queries=100))[0] == -1
+
+
+def test_detr_entry_points_reject_rtdetr_handle():
+    """spe_forward / spe_forward_stages on an RT-DETR handle (which shares spe_model) return
+    SPE_E_ARG before touching the device, like spe_rtdetr_forward does for a DETR handle."""
+    from spe.rtdetr_spec import RtdetrConfig
+    L = _lib.lib()
+    r = RtdetrConfig(depth=18, input_size=128)
+    c = _lib.RtdetrConfig(r.depth, r.input_size, r.num_queries, r.dec_layers, r.enc_ff, r.dec_ff, r.csp_hidden,
+                          r.num_classes, _lib.SPE_DTYPE_BF16)
+    h = ctypes.c_void_p()
+    assert L.spe_rtdetr_create(ctypes.byref(c), ctypes.byref(h)) == 0
+    dummy = ctypes.c_void_p(16)          # never dereferenced: the family check comes first
+    out = _lib.ForwardOutputs(dummy, dummy, None, None, None, None, None, None, None, None)
+    for rc in (L.spe_forward(h, None, dummy, 1, dummy, 1 << 40, ctypes.byref(out)),
+               L.spe_forward_stages(h, None, dummy, 1, dummy, 1 << 40, ctypes.byref(out), 3)):
+        assert rc == -1
+        assert b"not a DETR model" in L.spe_last_error()
+    L.spe_model_destroy(h)

@@ -601,3 +601,28 @@ def test_gemm_streaming_short_k(gpu_device, K, N, epi):
             y = y - bias
     assert _lib.lib().spe_debug_gemm_path() == 2, "expected the streaming kernel"
     _close(got, y, tol)
+
+
+@pytest.mark.parametrize("rows", [52 * 2704, 2 * 2704])
+def test_gemm_f16_store_saturates(gpu_device, rows):
+    """fp16 GEMM outputs (the encoder's V^T / config-5 q,k operands) saturate at +-65504 rather
+    than overflowing to inf (an inf V entry would make the attention output NaN); in-range values
+    are unchanged.  Both the streaming kernel (large M) and the tiled kernels (small M)."""
+    T, K, N = 2704, 256, 256
+    g = torch.Generator(device="cpu").manual_seed(91)
+    A = torch.randn(rows, K, generator=g).to(gpu_device, torch.bfloat16)
+    Wt = (torch.randn(N, K, generator=g) / K ** 0.5).to(gpu_device, torch.bfloat16)
+    bias = torch.randn(N, generator=g).to(gpu_device)
+    bias[::7] = 1e6
+    bias[3::7] = -1e6
+    B = rows // T
+    C = torch.zeros(B * N * T, dtype=torch.float16, device=gpu_device)
+    _gemm("bf16", 0, A, _padded_weight(Wt, K, torch.bfloat16), rows, N, K, K, K, C, 8, bias=bias, vt=(T, B), out_f16=1)
+    got = C.view(N // 256, B, 256, T).permute(1, 3, 0, 2).reshape(rows, N).float()
+    assert torch.isfinite(got).all()
+    big = torch.zeros(N, dtype=torch.bool, device=gpu_device)
+    big[::7] = True
+    big[3::7] = True
+    assert (got[:, big].abs() == 65504).all()
+    y = A.float() @ Wt.float().t() + bias
+    _close(got[:, ~big], y[:, ~big], 1e-2)

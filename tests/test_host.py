@@ -118,3 +118,83 @@ def test_gloo_world2_record_exchange():
     assert rec.shape == (8, sd.RECORD_LEN)
     assert (rec[:4, 0] == 0).all() and (rec[4:, 0] == 1).all() and (rec[4:, 9] == 1).all()
     assert keys == ["img0_0", "img0_1", "img1_0", "img1_1"]
+
+
+def _eval_records(n, seed=3):
+    """n images' worth of device-style solver outputs (CPU tensors) + ground truth."""
+    rng = np.random.default_rng(seed)
+    q = rng.normal(size=(n, 4)).astype(np.float32)
+    q /= np.linalg.norm(q, axis=1, keepdims=True)
+    t = rng.normal(size=(n, 3)) + [0, 0, 10]
+    status = rng.integers(0, 4, n).astype(np.int32)
+    q[status == 1] = 0
+    t[status == 1] = 0
+    gt = [{"filename": f"img{i:04d}.jpg", "q_vbs2tango": (q[i] + rng.normal(0, 0.05, 4)).tolist(),
+           "r_Vo2To_vbs_true": (t[i] + rng.normal(0, 0.3, 3)).tolist()} for i in range(n)]
+    return {"gt": gt, "points": rng.uniform(0, 1900, (n, 11, 2)).astype(np.float32),
+            "probs": rng.dirichlet(np.ones(12), (n, 11)).astype(np.float32), "quat": q, "tvec": t, "status": status,
+            "sigmas": rng.uniform(0.5, 9, (n, 11, 2)).astype(np.float32),
+            "mean_sigma": rng.uniform(0.5, 9, n).astype(np.float32), "reliable": rng.integers(0, 2, n).astype(bool)}
+
+
+def _eval_shard(d, lo, hi):
+    ev = SpeedEval(d["gt"], _StubSolver())
+    t = lambda a: torch.from_numpy(np.ascontiguousarray(a[lo:hi]))
+    poses = {"quat": t(d["quat"]), "tvec": t(d["tvec"]), "status": t(d["status"])}
+    ev.update_batch([g["filename"] for g in d["gt"][lo:hi]], t(d["points"]), t(d["probs"]), poses, sigmas=t(d["sigmas"]),
+                    assess={"mean_sigma": t(d["mean_sigma"]), "reliable": t(d["reliable"])})
+    return ev
+
+
+def _eval_worker(rank, world, port, n, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank), WORLD_SIZE=str(world),
+                      LOCAL_RANK=str(rank))
+    r, w, _ = sd.init_distributed_mode(backend="gloo")
+    d = _eval_records(n)
+    lo, hi = sd.shard(n, r, w)
+    ev = _eval_shard(d, lo, hi)
+    # evaluate()'s end of loop (spe/engine.py): merge every rank's log, then summarize
+    ev.log = sd.all_gather_log(ev.log)
+    ev.summarize()
+    # the bench's per-batch record exchange (bench.py step(): pack -> all-gather)
+    from spe.speed_eval import speed_score as host_score
+    # (equal per-rank blocks, as the bench's fixed per-GPU batch gives)
+    hi = lo + n // w
+    st = torch.tensor([host_score(d["quat"][i], d["tvec"][i], d["gt"][i]["q_vbs2tango"], d["gt"][i]["r_Vo2To_vbs_true"])[0]
+                       for i in range(lo, hi)], dtype=torch.float64)
+    rec = sd.exchange_pose_records({"quat": torch.from_numpy(d["quat"][lo:hi]), "tvec": torch.from_numpy(d["tvec"][lo:hi]),
+                                    "status": torch.from_numpy(d["status"][lo:hi])}, st, st * 2)
+    out.put((r, ev.stats, json.dumps(ev.log, sort_keys=False), rec.numpy().tolist()))
+    torch.distributed.destroy_process_group()
+
+
+def test_gloo_world2_speedeval_equals_world1():
+    """with the one log all-gather, the N-rank evaluate() summary equals the 1-rank
+    summary (the reference's summarize() is rank-local, REV/engine.py:122-128), and the bench's
+    record exchange returns every rank's records in rank order."""
+    n = 37                                   # ragged: shards of 19 and 18 images
+    d = _eval_records(n)
+    one = _eval_shard(d, 0, n)
+    one.summarize()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = 30500 + os.getpid() % 1000
+    procs = [ctx.Process(target=_eval_worker, args=(r, 2, port, n, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=180) for _ in range(2)])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for r, stats, log, rec in res:
+        assert stats == one.stats, r
+        assert log == json.dumps(one.log, sort_keys=False)
+    assert "self-assessment" in one.stats
+    for _, _, _, rec in res:
+        rec = np.asarray(rec)
+        assert rec.shape == (2 * 18, sd.RECORD_LEN)
+        idx = np.r_[0:18, 19:37]                     # rank 0's block, then rank 1's
+        np.testing.assert_array_equal(rec[:, :4], d["quat"][idx].astype(np.float64))
+        np.testing.assert_array_equal(rec[:, 4:7], d["tvec"][idx])
+        np.testing.assert_array_equal(rec[:, 9], d["status"][idx])
+        np.testing.assert_allclose(rec[:, 8], 2 * rec[:, 7])

@@ -172,3 +172,27 @@ def test_hip_hs_output_feeds_score_head(gpu_device):
     k = f"decoder.dec_score_head.{cfg.dec_layers - 1}"
     logits = hs @ w[f"{k}.weight"].T.astype(np.float64) + w[f"{k}.bias"]
     assert np.abs(logits - o["pred_logits"].cpu().numpy()).max() <= 1e-4
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["fp32", "bf16"])
+def test_hip_nan_image_selects_valid_queries(gpu_device, dtype):
+    """An all-NaN image makes every encoder score NaN.  torch.topk ranks NaN above every number,
+    so the reference still selects Q distinct tokens; the HIP selection must pick valid, distinct
+    token indices (lowest index first among the tied NaNs) and leave the other images untouched."""
+    g, cfg = _golden("r18_s128")
+    m = _hip_model(cfg, dtype, int(g["weight_seed"]))
+    b = synthetic_batch(SpeConfig(input_size=cfg.input_size), 3, 31)
+    x = torch.from_numpy(b["images"]).to(gpu_device)
+    clean = m(x)
+    x[1] = float("nan")
+    o = m(x)
+    torch.cuda.synchronize()
+    L = sum((cfg.input_size // s) ** 2 for s in (8, 16, 32))
+    tk = o["topk"].cpu().numpy()
+    assert ((tk >= 0) & (tk < L)).all()
+    assert all(len(set(r)) == cfg.num_queries for r in tk)
+    np.testing.assert_array_equal(tk[1], np.arange(cfg.num_queries))
+    for i in (0, 2):
+        np.testing.assert_array_equal(tk[i], clean["topk"][i].cpu().numpy())
+        assert (o["pred_pts"][i] - clean["pred_pts"][i]).abs().max().item() == 0
