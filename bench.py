@@ -69,9 +69,14 @@ def parse():
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
     p.add_argument("--attn-dtype", dest="attn_dtype", default=None, choices=["bf16", "fp16"],
                    help="encoder self-attention operand type (bf16 models; config 5 preset: fp16)")
-    p.add_argument("--weights", default="label-diverse", choices=["label-diverse", "random"],
+    p.add_argument("--weights", default="pose-consistent", choices=["pose-consistent", "label-diverse", "random"],
                    help="label-diverse: random init made query-diverse so the solver sees >= 4 "
-                        "correspondences like a trained model (spe.synthetic.bench_weights)")
+                        "correspondences like a trained model (spe.synthetic.bench_weights); pose-consistent "
+                        "(default, DETR): label-diverse + the point head fitted on the timed batch so each "
+                        "query predicts its label's landmark projection + N(0, 2 px) + 10%% outliers "
+                        "(spe.synthetic.fit_point_head), so RANSAC finds consensus and the refinement runs")
+    p.add_argument("--no-accuracy", action="store_true",
+                   help="skip the post-timing accuracy check of a bf16 run against the fp32 parity mode")
     p.add_argument("--no-overlap", action="store_true",
                    help="run the solver on the forward's stream (default: solver of batch i overlaps the forward of i+1)")
     p.add_argument("--no-overlap-decode", action="store_true",
@@ -187,6 +192,103 @@ def cpu_baseline_rtdetr(rcfg, seconds):
                             f"Q={rcfg.num_queries}, fp32 torch-CPU restatement + C epnp_ransac_sigma oracle) in {dt:.1f}s")
 
 
+def bench_data(cfg, B, rank):
+    from spe.synthetic import synthetic_batch
+    return synthetic_batch(cfg, B, seed=1000 + rank)
+
+
+def pose_consistent_weights(w, cfg, args, B, rank, world, dev):
+    """Fit the point head (spe.synthetic.fit_point_head) on the decoder outputs of every rank's
+    timed batch, so all ranks run identical weights: each rank computes its batch's hs and
+    targets, they are all-gathered, rank 0 fits and broadcasts the head."""
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+    from spe.models import DETR
+    from spe.synthetic import fit_point_head, keypoint_targets
+    data = bench_data(cfg, B, rank)
+    m = DETR(cfg, dtype=args.dtype, attn_dtype=args.attn_dtype)
+    m.load_state_dict(w)
+    o = m(torch.from_numpy(data["images"]).to(dev), return_hs=True)
+    hs = o["hs"].float()
+    labels = o["pred_logits"].argmax(-1).cpu().numpy()
+    del m
+    tgt, mask = keypoint_targets(data, labels, seed=7 + rank)
+    tgt = torch.from_numpy(tgt).float().to(dev)
+    mask = torch.from_numpy(mask).to(dev)
+    if world > 1:
+        parts = [[torch.empty_like(t) for _ in range(world)] for t in (hs, tgt, mask)]
+        for pl, t in zip(parts, (hs, tgt, mask)):
+            dist.all_gather(pl, t.contiguous())
+        hs, tgt, mask = (torch.cat(pl) for pl in parts)
+    keys = [f"point_embed.layers.{j}.{k}" for j in range(3) for k in ("weight", "bias")]
+    err = None
+    if rank == 0:
+        w, err = fit_point_head(w, hs.cpu().numpy(), tgt.cpu().numpy(), mask.cpu().numpy(), device=dev)
+    if world > 1:
+        for k in keys:
+            t = torch.from_numpy(w[k]).to(dev)
+            dist.broadcast(t, 0)
+            w[k] = t.cpu().numpy()
+    fit = None
+    if err is not None:
+        fit = {"fit_err_max_norm": float(err.max()), "fit_err_mean_norm": float(err.mean()),
+               "fit_queries": int(mask.sum().item())}
+    return w, fit
+
+
+def keypoint_error_px(points_px, probs, data):
+    """Per foreground query (argmax label < 11): pixel distance to its label's landmark."""
+    import numpy as np
+    pts, lab = points_px.cpu().numpy(), probs.argmax(-1).cpu().numpy()
+    lm = data["landmarks"]
+    e = [np.linalg.norm(pts[i, q] - lm[i, lab[i, q]]) for i in range(pts.shape[0]) for q in range(pts.shape[1])
+         if lab[i, q] < lm.shape[1]]
+    return np.asarray(e)
+
+
+def accuracy_vs_fp32(model, cfg, args, w, out, data, solver, dev):
+    """Accuracy of the timed bf16 mode against the fp32 parity mode (pinned to the reference at
+    <= 1e-4 normalised keypoints by tests/test_gpu_parity.py) on the timed batch itself: keypoint
+    deltas of the foreground queries the two modes label alike, label agreement, and the SPEED
+    score delta of the two modes' poses through the same solver."""
+    import numpy as np
+    import torch
+    from spe.models import DETR
+    from spe.speed_eval import device_speed_score
+    ref = DETR(cfg, dtype="fp32")
+    ref.load_state_dict(w)
+    clip = torch.from_numpy(data["clip_bbox"]).float().to(dev)
+    r = ref(torch.from_numpy(data["images"]).to(dev), clip_bbox=clip)
+    fo = out["forward"]
+    lab_b, lab_r = fo["probs"].argmax(-1), r["probs"].argmax(-1)
+    fg = (lab_r < 11) & (lab_b == lab_r)
+    wcrop = (clip[:, 2] - clip[:, 0])[:, None].expand_as(lab_r)
+    d = (fo["points_px"] - r["points_px"]).norm(dim=-1)[fg]
+    dn = (fo["pred_points"] - r["pred_points"]).abs().amax(-1)[fg]
+    q_gt = torch.from_numpy(data["quat"]).to(dev)
+    t_gt = torch.from_numpy(data["tvec"]).to(dev)
+    pr = solver.solve_batch(r["points_px"], r["probs"], r.get("sigmas"))
+    st, sq = device_speed_score(pr["quat"], pr["tvec"], q_gt, t_gt)
+    sc_r, sc_b = (st + sq).cpu().numpy(), (out["s_t"] + out["s_q"]).cpu().numpy()
+    both = np.isfinite(sc_r) & np.isfinite(sc_b)
+    ds = np.abs(sc_b - sc_r)[both]
+    res = {"reference_mode": "fp32 parity mode (<= 1e-4 of the reference on its goldens)",
+           "label_agreement": float((lab_b == lab_r).float().mean().item()),
+           "kpt_px_max": float(d.max().item()), "kpt_px_mean": float(d.mean().item()),
+           "kpt_norm_max": float(dn.max().item()), "kpt_norm_mean": float(dn.mean().item()),
+           "kpt_px_per_crop_px": float((d / wcrop[fg]).max().item()),
+           "score_delta_max": float(ds.max()) if ds.size else None,
+           "score_delta_mean": float(ds.mean()) if ds.size else None,
+           "score_mean_fp32": float(np.nanmean(sc_r)), "score_mean_timed": float(np.nanmean(sc_b)),
+           "status_agreement": float((pr["status"] == out["poses"]["status"]).float().mean().item()),
+           "images": int(len(sc_r))}
+    meets = res["kpt_norm_max"] <= 1e-4 and (res["score_delta_max"] or 0.0) <= 1e-4
+    res["meets_1e-4"] = bool(meets)
+    del ref
+    return res
+
+
 def traffic_for(kind, grid, attn_dtype):
     """HBM bytes per launch of `kind` from a committed PMC summary (profiles/pmc_*.json), or None.
     Only a summary measured on the same launch (kind, grid size in threads, operand type) counts."""
@@ -263,8 +365,12 @@ def main():
         model = RTDETR(rcfg, dtype=args.dtype, aux_outputs=False)
         model.load_state_dict(w)
     else:
+        w = bench_weights(cfg, 0, hs_fn) if args.weights != "random" else random_weights(cfg, 0)
+        fit = None
+        if args.weights == "pose-consistent":
+            w, fit = pose_consistent_weights(w, cfg, args, B, rank, world, dev)
         model = DETR(cfg, dtype=args.dtype, attn_dtype=args.attn_dtype)
-        model.load_state_dict(bench_weights(cfg, 0, hs_fn) if args.weights == "label-diverse" else random_weights(cfg, 0))
+        model.load_state_dict(w)
     solver = build_solver(argparse.Namespace(solver=args.solver, repro=20))
     if args.raw_frames:
         from spe.synthetic import synthetic_frames
@@ -277,7 +383,7 @@ def main():
     else:
         pipe = PosePipeline(model, solver, B, device=dev, overlap=not args.no_overlap,
                             overlap_decode=rcfg is None and not (args.no_overlap_decode or args.no_overlap))
-        data = synthetic_batch(cfg, B, seed=1000 + rank)
+        data = bench_data(cfg, B, rank) if rcfg is None else synthetic_batch(SpeConfig(input_size=args.size), B, seed=1000 + rank)
         pipe.load(torch.from_numpy(data["images"]).to(dev), torch.from_numpy(data["clip_bbox"]).float().to(dev),
                   torch.from_numpy(data["quat"]).to(dev), torch.from_numpy(data["tvec"]).to(dev))
     torch.cuda.synchronize()
@@ -399,6 +505,14 @@ def main():
     }
     if "assess" in out:
         result["self_assessment_reliable"] = int(out["assess"]["reliable"].sum().item())
+    if rcfg is None and not args.raw_frames:
+        e = keypoint_error_px(out["forward"]["points_px"], out["forward"]["probs"], data)
+        result["keypoints_vs_gt_px"] = {"median": float(np.median(e)), "p90": float(np.percentile(e, 90)),
+                                        "fg_queries": int(e.size), "weights": args.weights}
+        if fit is not None:
+            result["keypoints_vs_gt_px"].update(fit)
+        if args.dtype == "bf16" and not args.no_accuracy:
+            result["accuracy_vs_fp32"] = accuracy_vs_fp32(model, cfg, args, w, out, data, solver, dev)
     if world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = (cpu_baseline(cfg, args.cpu_seconds, args.solver) if rcfg is None
                                   else cpu_baseline_rtdetr(rcfg, args.cpu_seconds))

@@ -1062,13 +1062,20 @@ static void lm_refine(const cam_t* k, int n, const double* wld, const double* im
  * residual_i = w_i * (x_obs - x_proj) per axis, Huber(delta) robust loss, <= 20 LM iterations. */
 static void sigma_lm(const cam_t* k, int n, const double* wld, const double* img, const double* sig, double delta,
                      double* rvec, double* tvec) {
-  double xn[2 * MAXN], w[2 * MAXN], sum[2] = {0, 0};
+  double xn[2 * MAXN], w[2 * MAXN];
+  float w1[2 * MAXN], sum[2] = {0.f, 0.f};
+  /* the reference computes the weights with numpy on the float32 sigmas (UNC/utils/speed_eval.py
+   * :283-288): float32 sqrt, + 1e-6 and 1 / x in float32, the axis-0 sum row by row in float32,
+   * the division in float32 (pinned by tests/golden/solver_front_ref.npz sig_cost) */
   for (int i = 0; i < n; ++i) {
     xn[2 * i] = (float)((img[2 * i] - k->cx) * (1. / k->fx));
     xn[2 * i + 1] = (float)((img[2 * i + 1] - k->cy) * (1. / k->fy));
-    for (int a = 0; a < 2; ++a) { w[2 * i + a] = 1. / (sqrt(sig[2 * i + a]) + 1e-6); sum[a] += w[2 * i + a]; }
+    for (int a = 0; a < 2; ++a) {
+      w1[2 * i + a] = 1.0f / (sqrtf((float)sig[2 * i + a]) + 1e-6f);
+      sum[a] = sum[a] + w1[2 * i + a];
+    }
   }
-  for (int i = 0; i < n; ++i) { w[2 * i] /= sum[0]; w[2 * i + 1] /= sum[1]; }
+  for (int i = 0; i < n; ++i) for (int a = 0; a < 2; ++a) w[2 * i + a] = (double)(w1[2 * i + a] / sum[a]);
   cam_t unit = {1, 1, 0, 0};
   double param[6] = {rvec[0], rvec[1], rvec[2], tvec[0], tvec[1], tvec[2]};
   double mu = 1e-4, nu = 2;

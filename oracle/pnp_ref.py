@@ -99,6 +99,18 @@ def select_correspondences(points, probs):
     return labs, np.asarray(pts, np.float32).reshape(-1, 2)
 
 
+def sigma_weights_f32(sig):
+    """UNC/utils/speed_eval.py:283-288 (ceres_pnp) on the selected float32 sigmas [n, 2]: numpy
+    float32 sqrt, + 1e-6 and 1 / x, the axis-0 sum accumulated row by row in float32, the
+    division in float32.  (oracle/pnp_ref.c sigma_lm and the HIP solver compute the same.)"""
+    s = np.asarray(sig, np.float32)
+    w1 = (np.float32(1.0) / (np.sqrt(s) + np.float32(1e-6))).astype(np.float32)
+    tot = np.zeros(2, np.float32)
+    for row in w1:
+        tot = (tot + row).astype(np.float32)
+    return (w1 / tot).astype(np.float32)
+
+
 def self_assess(probs, sigmas, status, corr_label, inlier_mask, score_th=0.5, sigma_th=5.0, min_inliers=4):
     """Self-assessment filter (BASELINE config 4).  No reference code exists (parity unpinned):
     the rule restates include/spe.h spe_self_assess, built on the commented per-keypoint gate

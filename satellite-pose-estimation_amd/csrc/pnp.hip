@@ -383,18 +383,20 @@ __device__ void sigma_lm_wave(LmShared& sh, const cam_t* k, const LmPoint& pt, i
                               double* tvec, int lane) {
   const int m = 2 * n;
   double xn[2] = {0, 0}, w[2] = {0, 0};
+  float w1[2] = {0.f, 0.f};
+  // weights in float32 like the reference's numpy on float32 sigmas (sigma_weights_f32)
   if (pt.row >= 0)
     for (int a = 0; a < 2; ++a) {
       xn[a] = (float)((pt.obs[a] - (a ? k->cy : k->cx)) * (1. / (a ? k->fy : k->fx)));
-      w[a] = 1. / (sqrt(pt.sig[a]) + 1e-6);
-      sh.w[2 * pt.row + a] = w[a];
+      w1[a] = 1.0f / (sqrtf((float)pt.sig[a]) + 1e-6f);
+      sh.w[2 * pt.row + a] = w1[a];
     }
   __syncthreads();
-  double sum[2] = {0, 0};
-  for (int i = 0; i < n; ++i) { sum[0] += sh.w[2 * i]; sum[1] += sh.w[2 * i + 1]; }
+  float sum[2] = {0.f, 0.f};
+  for (int i = 0; i < n; ++i) { sum[0] = sum[0] + (float)sh.w[2 * i]; sum[1] = sum[1] + (float)sh.w[2 * i + 1]; }
   __syncthreads();
   if (pt.row >= 0)
-    for (int a = 0; a < 2; ++a) { w[a] /= sum[a]; sh.w[2 * pt.row + a] = w[a]; }
+    for (int a = 0; a < 2; ++a) { w[a] = (double)(w1[a] / sum[a]); sh.w[2 * pt.row + a] = w[a]; }
   const cam_t unit = {1, 1, 0, 0};
   double param[6] = {rvec[0], rvec[1], rvec[2], tvec[0], tvec[1], tvec[2]};
   double mu = 1e-4, nu = 2;

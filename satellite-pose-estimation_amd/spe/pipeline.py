@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import torch
 
+from . import _lib
 from .models import DETR
 from .solver import PoseSolver
 from .speed_eval import device_speed_score
@@ -65,6 +66,9 @@ class PosePipeline:
             self.transform = SpeedValTransform(S)
             self.pp_out = {"images": self.images, "clip_bbox": self.clip_bbox,
                            "status": torch.zeros(batch, dtype=torch.int32, device=dev)}
+        if use_graph and not _lib.GRAPH_SAFE:
+            raise RuntimeError("use_graph needs DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 in effect when HIP initialises "
+                               "(import spe before the first device call, or export it): see spe/_lib.py")
         self.use_graph = use_graph
         self.graph = None
         self.out = None

@@ -225,3 +225,78 @@ def bench_weights(cfg: SpeConfig, seed: int, hs_fn, calib_batch: int = 16):
     w = sharpen_decoder(random_weights(cfg, seed), cfg)
     calib = synthetic_batch(cfg, calib_batch, seed=4242)
     return diversify_class_head(w, hs_fn(w, calib["images"]))
+
+
+# ------------------------------------------------------------- pose-consistent point head
+# Label-diverse weights give queries distinct labels, but their random point head puts every
+# keypoint near the crop centre, so no pose explains them: RANSAC finds no consensus and the
+# refinement the RANSAC configs name never runs.  A trained model's keypoints are the landmark
+# projections up to a few pixels.  fit_point_head fits the point MLP (same 256-256-256-2 + sigmoid
+# architecture, REV/models/detr_speed.py:52,84) on the decoder outputs of the batch the bench times,
+# like a short training run, so that each foreground query predicts its label's landmark
+# projection plus the SURVEY 8(d) stress-set noise: N(0, noise_px) and a fraction of uniform
+# outliers inside the crop.
+
+def keypoint_targets(batch, labels, seed: int = 0, noise_px: float = 2.0, outlier_frac: float = 0.1):
+    """Crop-normalised targets [B,Q,2] for queries labelled `labels` [B,Q] (11 = no object;
+    those keep target 0.5 and are masked out).  Returns (targets, mask [B,Q] bool)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    lm, cb = batch["landmarks"], np.asarray(batch["clip_bbox"], np.float64)
+    B, Q = labels.shape
+    tgt = np.full((B, Q, 2), 0.5)
+    mask = labels < lm.shape[1]
+    for i in range(B):
+        w, h = cb[i, 2] - cb[i, 0], cb[i, 3] - cb[i, 1]
+        for q in range(Q):
+            if not mask[i, q]:
+                continue
+            if rng.uniform() < outlier_frac:
+                tgt[i, q] = rng.uniform(0.02, 0.98, 2)
+                continue
+            u, v = lm[i, labels[i, q]] + rng.normal(0.0, noise_px, 2)
+            tgt[i, q] = ((u - cb[i, 0]) / w, (v - cb[i, 1]) / h)
+    return np.clip(tgt, 1e-3, 1 - 1e-3), mask
+
+
+def fit_point_head(w, hs, targets, mask, steps: int = 3000, lr: float = 1e-3, seed: int = 0, device="cpu",
+                   prefix: str = "point_embed"):
+    """Fit the 3-layer point MLP to `targets` [N,2] on decoder outputs `hs` [N,d] (rows with
+    mask False ignored).  Full-batch Adam in torch on `device`; the input standardisation is
+    folded into layer 0 afterwards.  Returns (weights, fit error in target units [N] on masked rows)."""
+    import torch
+    hs = torch.as_tensor(np.asarray(hs, np.float32).reshape(-1, np.shape(hs)[-1]), device=device)
+    y = torch.as_tensor(np.asarray(targets, np.float32).reshape(-1, 2), device=device)
+    m = torch.as_tensor(np.asarray(mask).reshape(-1), device=device)
+    mu, sd = hs.mean(0), hs.std(0) + 1e-6
+    x = (hs - mu) / sd
+    d = hs.shape[1]
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    shapes = [(d, d), (d, d), (2, d)]
+    params = []
+    for o, i in shapes:
+        lim = (6.0 / (o + i)) ** 0.5
+        params += [((torch.rand(o, i, generator=g) * 2 - 1) * lim).to(device).requires_grad_(),
+                   torch.zeros(o, device=device, requires_grad=True)]
+
+    def net(z):
+        z = torch.relu(z @ params[0].t() + params[1])
+        z = torch.relu(z @ params[2].t() + params[3])
+        return torch.sigmoid(z @ params[4].t() + params[5])
+
+    opt = torch.optim.Adam(params, lr=lr)
+    sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, steps)
+    for _ in range(steps):
+        loss = ((net(x) - y)[m] ** 2).mean()
+        opt.zero_grad()
+        loss.backward()
+        opt.step()
+        sched.step()
+    with torch.no_grad():
+        err = (net(x) - y)[m].abs().amax(1)
+        W0 = params[0] / sd[None, :]
+        b0 = params[1] - W0 @ mu
+        out = dict(w)
+        for j, (Wj, bj) in enumerate(((W0, b0), (params[2], params[3]), (params[4], params[5]))):
+            out[f"{prefix}.layers.{j}.weight"] = Wj.detach().float().cpu().numpy().copy()
+            out[f"{prefix}.layers.{j}.bias"] = bj.detach().float().cpu().numpy().copy()
+    return out, err.cpu().numpy()

@@ -176,23 +176,21 @@ def test_hip_hs_output_feeds_score_head(gpu_device):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dtype", ["fp32", "bf16"])
-def test_hip_nan_image_selects_valid_queries(gpu_device, dtype):
-    """An all-NaN image makes every encoder score NaN.  torch.topk ranks NaN above every number,
-    so the reference still selects Q distinct tokens; the HIP selection must pick valid, distinct
-    token indices (lowest index first among the tied NaNs) and leave the other images untouched."""
+def test_hip_nan_scores_select_valid_queries(gpu_device, dtype):
+    """Every encoder score NaN (a NaN in the encoder score head; a NaN input image does not get
+    there, since the fused ReLU epilogues map NaN to 0).  torch.topk ranks NaN above every number
+    and returns the tied NaNs lowest index first; the HIP selection must pick the same valid,
+    distinct tokens instead of faulting on an unset index."""
+    from spe.rtdetr import RTDETR
     g, cfg = _golden("r18_s128")
-    m = _hip_model(cfg, dtype, int(g["weight_seed"]))
+    w = random_rtdetr_weights(cfg, int(g["weight_seed"]))
+    w["decoder.enc_score_head.bias"] = w["decoder.enc_score_head.bias"].copy()
+    w["decoder.enc_score_head.bias"][3] = np.nan
+    m = RTDETR(cfg, dtype)
+    m.load_state_dict(w)
     b = synthetic_batch(SpeConfig(input_size=cfg.input_size), 3, 31)
-    x = torch.from_numpy(b["images"]).to(gpu_device)
-    clean = m(x)
-    x[1] = float("nan")
-    o = m(x)
+    o = m(torch.from_numpy(b["images"]).to(gpu_device))
     torch.cuda.synchronize()
-    L = sum((cfg.input_size // s) ** 2 for s in (8, 16, 32))
     tk = o["topk"].cpu().numpy()
-    assert ((tk >= 0) & (tk < L)).all()
-    assert all(len(set(r)) == cfg.num_queries for r in tk)
-    np.testing.assert_array_equal(tk[1], np.arange(cfg.num_queries))
-    for i in (0, 2):
-        np.testing.assert_array_equal(tk[i], clean["topk"][i].cpu().numpy())
-        assert (o["pred_pts"][i] - clean["pred_pts"][i]).abs().max().item() == 0
+    for r in tk:
+        np.testing.assert_array_equal(r, np.arange(cfg.num_queries))
