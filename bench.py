@@ -259,7 +259,9 @@ def accuracy_vs_fp32(model, cfg, args, w, out, data, solver, dev):
     ref = DETR(cfg, dtype="fp32")
     ref.load_state_dict(w)
     clip = torch.from_numpy(data["clip_bbox"]).float().to(dev)
-    r = ref(torch.from_numpy(data["images"]).to(dev), clip_bbox=clip)
+    r = ref(torch.from_numpy(data["images"]).to(dev), clip_bbox=clip, return_hs=True)
+    hb = model(torch.from_numpy(data["images"]).to(dev), return_hs=True)["hs"]
+    hs_rel = ((hb - r["hs"]).norm(dim=-1) / r["hs"].norm(dim=-1)).flatten()
     fo = out["forward"]
     lab_b, lab_r = fo["probs"].argmax(-1), r["probs"].argmax(-1)
     fg = (lab_r < 11) & (lab_b == lab_r)
@@ -274,6 +276,7 @@ def accuracy_vs_fp32(model, cfg, args, w, out, data, solver, dev):
     both = np.isfinite(sc_r) & np.isfinite(sc_b)
     ds = np.abs(sc_b - sc_r)[both]
     res = {"reference_mode": "fp32 parity mode (<= 1e-4 of the reference on its goldens)",
+           "hs_rel_err_mean": float(hs_rel.mean().item()), "hs_rel_err_max": float(hs_rel.max().item()),
            "label_agreement": float((lab_b == lab_r).float().mean().item()),
            "kpt_px_max": float(d.max().item()), "kpt_px_mean": float(d.mean().item()),
            "kpt_norm_max": float(dn.max().item()), "kpt_norm_mean": float(dn.mean().item()),

@@ -15,12 +15,9 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 # only with the ROCm runtime's graph packet capture off: with it on, a replay issued after the
 # stream has synchronised reads wrong kernel arguments (measured: the first replay is exact, the
 # later ones are not).  The runtime reads the switch when HIP initialises,
-# so it is set here, before any device call this package makes; GRAPH_SAFE records whether it
-# took effect (it does not if the process initialised HIP before importing spe).
-_PKT = "DEBUG_CLR_GRAPH_PACKET_CAPTURE"
-GRAPH_SAFE = os.environ.get(_PKT) == "0" or not torch.cuda.is_initialized()
-os.environ.setdefault(_PKT, "0")
-GRAPH_SAFE = GRAPH_SAFE and os.environ[_PKT] == "0"
+# so it is set here, which takes effect when no device call preceded this import (the pipeline
+# verifies its captured graph against eager execution either way).
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SPE_LIB_PATH") or os.path.join(_HERE, "libspe.so")   # override: kernel A/B builds

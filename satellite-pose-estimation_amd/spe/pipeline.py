@@ -9,7 +9,6 @@ from __future__ import annotations
 
 import torch
 
-from . import _lib
 from .models import DETR
 from .solver import PoseSolver
 from .speed_eval import device_speed_score
@@ -66,9 +65,6 @@ class PosePipeline:
             self.transform = SpeedValTransform(S)
             self.pp_out = {"images": self.images, "clip_bbox": self.clip_bbox,
                            "status": torch.zeros(batch, dtype=torch.int32, device=dev)}
-        if use_graph and not _lib.GRAPH_SAFE:
-            raise RuntimeError("use_graph needs DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 in effect when HIP initialises "
-                               "(import spe before the first device call, or export it): see spe/_lib.py")
         self.use_graph = use_graph
         self.graph = None
         self.out = None
@@ -170,10 +166,23 @@ class PosePipeline:
             s = torch.cuda.Stream()
             s.wait_stream(torch.cuda.current_stream())
             with torch.cuda.stream(s):
-                self._body()
+                ref = self._body()
             torch.cuda.current_stream().wait_stream(s)
             self.graph = torch.cuda.CUDAGraph()
             with torch.cuda.graph(self.graph, stream=s):
                 self.out = self._body()
+            # self-check: two replays separated by a synchronise must reproduce the eager
+            # warm-up exactly (same kernels, same inputs); see spe/_lib.py on packet capture
+            for _ in range(2):
+                torch.cuda.synchronize()
+                self.graph.replay()
+            torch.cuda.synchronize()
+            pairs = [(ref["forward"][k], self.out["forward"][k]) for k in ref["forward"]]
+            pairs += [(ref["poses"][k], self.out["poses"][k]) for k in ("status", "quat", "tvec")]
+            if not all(torch.equal(a, b) for a, b in pairs):
+                self.graph = None
+                raise RuntimeError("HIP graph replay of the pose pipeline differs from eager execution: run with "
+                                   "DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 set before HIP initialises (spe/_lib.py)")
+            return self.out
         self.graph.replay()
         return self.out

@@ -258,11 +258,15 @@ def keypoint_targets(batch, labels, seed: int = 0, noise_px: float = 2.0, outlie
     return np.clip(tgt, 1e-3, 1 - 1e-3), mask
 
 
-def fit_point_head(w, hs, targets, mask, steps: int = 3000, lr: float = 1e-3, seed: int = 0, device="cpu",
-                   prefix: str = "point_embed"):
+def fit_point_head(w, hs, targets, mask, steps: int = 2000, lr: float = 1e-3, seed: int = 0, device="cpu",
+                   prefix: str = "point_embed", noise_rel: float = 2.0 ** -8):
     """Fit the 3-layer point MLP to `targets` [N,2] on decoder outputs `hs` [N,d] (rows with
     mask False ignored).  Full-batch Adam in torch on `device`; the input standardisation is
-    folded into layer 0 afterwards.  Returns (weights, fit error in target units [N] on masked rows)."""
+    folded into layer 0 afterwards.  Every step perturbs the inputs by Gaussian noise of
+    noise_rel x |hs| (bf16's rounding scale): the hs of different images differ by only a few
+    percent, and an unregularised interpolant of them amplifies any perturbation of hs (such as
+    fp32 vs bf16 rounding) into tens of pixels, unlike a trained model; the noise keeps the fitted
+    head smooth at that scale.  Returns (weights, fit error in target units [N] on masked rows)."""
     import torch
     hs = torch.as_tensor(np.asarray(hs, np.float32).reshape(-1, np.shape(hs)[-1]), device=device)
     y = torch.as_tensor(np.asarray(targets, np.float32).reshape(-1, 2), device=device)
@@ -285,8 +289,11 @@ def fit_point_head(w, hs, targets, mask, steps: int = 3000, lr: float = 1e-3, se
 
     opt = torch.optim.Adam(params, lr=lr)
     sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, steps)
+    gn = torch.Generator(device=device).manual_seed(seed + 1)
+    nstd = noise_rel * hs.abs() / sd
     for _ in range(steps):
-        loss = ((net(x) - y)[m] ** 2).mean()
+        xin = x + nstd * torch.randn(x.shape, generator=gn, device=device) if noise_rel > 0 else x
+        loss = ((net(xin) - y)[m] ** 2).mean()
         opt.zero_grad()
         loss.backward()
         opt.step()

@@ -1,4 +1,9 @@
 import sys, os, time
+if len(sys.argv) > 1 and sys.argv[1] == "pre":
+    os.environ["DEBUG_CLR_GRAPH_PACKET_CAPTURE"] = "0"
+import torch
+if len(sys.argv) > 1 and sys.argv[1] == "post":
+    os.environ["DEBUG_CLR_GRAPH_PACKET_CAPTURE"] = "0"
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), "..", "..", "satellite-pose-estimation_amd"))
 import numpy as np, torch
 from spe.config import SpeConfig

@@ -18,6 +18,9 @@ for c in 3 4 5; do
     || { tail -20 gpurun_out/${TAG}_bench_c$c.log; exit 5; }
   tail -1 gpurun_out/${TAG}_bench_c$c.log | cut -c1-120
 done
+timeout -k 10 600 python bench.py --dtype fp32 --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/${TAG}_bench_fp32.log 2>&1 \
+  || { tail -20 gpurun_out/${TAG}_bench_fp32.log; exit 7; }
+tail -1 gpurun_out/${TAG}_bench_fp32.log | cut -c1-160
 for mdl in rtdetr_r18 rtdetr_r50; do
   timeout -k 10 600 python bench.py --model $mdl --steps 20 --warmup 3 --cpu-seconds 12 > gpurun_out/${TAG}_bench_$mdl.log 2>&1 \
     || { tail -20 gpurun_out/${TAG}_bench_$mdl.log; exit 6; }

@@ -1,6 +1,10 @@
 import os
 import sys
 
+# before anything initialises HIP: graph capture needs the runtime's packet capture off
+# (satellite-pose-estimation_amd/spe/_lib.py)
+os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
