@@ -160,6 +160,22 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int batc
 int spe_preprocess(void* stream, const uint8_t* frames, int batch, int height, int width, int channels,
                    const double* bbox_xxyy, int size, float* images, float* clip_bbox, int32_t* status);
 
+/* Baseline-JPEG decode of grayscale frames on the device: the decode half of
+ * `Image.open(img_path).convert('RGB')` in SpeedTrain.__getitem__ (REV/datasets/speed.py:209-210;
+ * Pillow / libjpeg-turbo, islow IDCT), which the reference runs in DataLoader worker processes
+ * (REV/main.py:252-254).  data: device bytes holding the batch's JPEG files; offsets / sizes:
+ * device int64 [B] (file b = data[offsets[b] .. offsets[b] + sizes[b])); every file must be a
+ * height x width 8-bit single-component sequential Huffman JPEG (SOF0/SOF1, restart intervals
+ * allowed) of at most max_bytes_per_image bytes.  frames: device uint8 [B,height,width], the
+ * 1-channel input spe_preprocess takes.  status (nullable): [B] 0 ok, 1 unsupported coding
+ * (progressive, arithmetic, 12-bit, colour), 2 corrupt stream, 3 frame size != height x width,
+ * 4 stream exceeds the workspace plan; a non-zero image gets a zero frame.  workspace: device
+ * bytes, spe_jpeg_workspace_bytes(batch, height, width, max_bytes_per_image) of them. */
+int64_t spe_jpeg_workspace_bytes(int batch, int height, int width, int64_t max_bytes_per_image);
+int spe_jpeg_decode(void* stream, const uint8_t* data, const int64_t* offsets, const int64_t* sizes, int batch,
+                    int height, int width, int64_t max_bytes_per_image, uint8_t* frames, int32_t* status,
+                    void* workspace, int64_t workspace_bytes);
+
 /* SetCriterion.forward with its HungarianMatcher (REV/models/detr_speed.py:214-261,
  * REV/models/matcher.py:60-88) for `layers` decoder layers (aux first, last layer last), the
  * logging half of evaluate() (REV/engine.py:99-112).  Device pointers: logits [L,B,Q,C] (C = 12),

@@ -6,8 +6,10 @@ image in DataLoader worker processes: Image.open().convert('RGB'), generate_clip
 :295-299), F.to_tensor and Normalize (:25-41).  `SpeedValTransform` does everything after the
 decode for a whole batch of frames already in HBM with one HIP launch (spe_preprocess,
 csrc/preprocess.hip) and returns the model input and the clip boxes PostProcess needs.
-JPEG decode stays on the host (no rocJPEG in this image); the reference's validation-time
-img_trunc(p=0.2) augmentation (:232) is a defect and is not reproduced.
+`JpegDecoder` does the decode before it on the device too (spe_jpeg_decode, csrc/jpeg.hip:
+Huffman, dequantisation and libjpeg's islow IDCT, bit-exact with Pillow), so a batch can start
+from the JPEG files' bytes in HBM.  The reference's validation-time img_trunc(p=0.2)
+augmentation (:232) is a defect and is not reproduced.
 """
 from __future__ import annotations
 
@@ -57,4 +59,50 @@ class SpeedValTransform:
         _lib.check(_lib.lib().spe_preprocess(_lib.stream_ptr(stream), _lib.ptr(frames), B, H, W, C, _lib.ptr(bb), S,
                                              _lib.ptr(out["images"]), _lib.ptr(out["clip_bbox"]),
                                              _lib.ptr(out["status"])), "spe_preprocess")
+        return out
+
+
+class JpegDecoder:
+    """Image.open(path).convert('RGB') of SpeedTrain.__getitem__ (REV/datasets/speed.py:209-210)
+    for a batch of SPEED frames on the device: baseline 8-bit grayscale JPEG files (the dataset's
+    format) -> uint8 [B,H,W] frames, the 1-channel input SpeedValTransform replicates to RGB.
+    Files are packed into one device byte buffer (pack); status [B]: 0 ok, 1 unsupported coding,
+    2 corrupt stream, 3 wrong frame size, 4 file larger than max_bytes (zero frame written)."""
+
+    def __init__(self, height: int = Camera.nv, width: int = Camera.nu, max_bytes: int = 4 << 20):
+        self.height, self.width, self.max_bytes = int(height), int(width), int(max_bytes)
+        self._ws = {}
+
+    @staticmethod
+    def pack(files, device="cuda"):
+        """list of JPEG file contents (bytes) -> (data uint8, offsets int64, sizes int64) on device."""
+        sizes = np.asarray([len(f) for f in files], np.int64)
+        offs = np.zeros(len(files), np.int64)
+        if len(files) > 1:
+            offs[1:] = np.cumsum(sizes)[:-1]
+        buf = np.frombuffer(b"".join(files) + bytes(16), np.uint8)
+        dev = torch.device(device)
+        return torch.from_numpy(buf.copy()).to(dev), torch.from_numpy(offs).to(dev), torch.from_numpy(sizes).to(dev)
+
+    def workspace(self, B, device):
+        key = (torch.device(device).index, B)
+        if key not in self._ws:
+            n = _lib.lib().spe_jpeg_workspace_bytes(B, self.height, self.width, self.max_bytes)
+            self._ws[key] = torch.empty(int(n), dtype=torch.uint8, device=device)
+        return self._ws[key]
+
+    def __call__(self, data: torch.Tensor, offsets: torch.Tensor, sizes: torch.Tensor, out=None, stream=None):
+        if not (data.is_cuda and data.dtype == torch.uint8):
+            raise ValueError("data must be a device uint8 tensor")
+        B = offsets.numel()
+        dev = data.device
+        if out is None:
+            out = {"frames": torch.empty(B, self.height, self.width, dtype=torch.uint8, device=dev),
+                   "status": torch.empty(B, dtype=torch.int32, device=dev)}
+        ws = self.workspace(B, dev)
+        _lib.check(_lib.lib().spe_jpeg_decode(_lib.stream_ptr(stream), _lib.ptr(data),
+                                              _lib.ptr(offsets.to(torch.int64).contiguous()),
+                                              _lib.ptr(sizes.to(torch.int64).contiguous()), B, self.height, self.width,
+                                              self.max_bytes, _lib.ptr(out["frames"]), _lib.ptr(out["status"]),
+                                              _lib.ptr(ws), ws.numel()), "spe_jpeg_decode")
         return out
