@@ -22,7 +22,9 @@ import time
 REPO = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(REPO, "satellite-pose-estimation_amd"))
 
-PEAK = {"bf16": {"mfma": 2500.0}, "fp32": {"mfma": 157.3}, "hbm": 8000.0}   # TFLOP/s, GB/s (MI355X_MICROARCH.md)
+# TFLOP/s, GB/s (MI355X_MICROARCH.md).  fp32x3 runs every product as three bf16 MFMAs (hi.hi +
+# hi.lo + lo.hi), so its ceiling for the model's algorithmic flops is a third of the bf16 peak.
+PEAK = {"bf16": {"mfma": 2500.0}, "fp32": {"mfma": 157.3}, "fp32x3": {"mfma": 2500.0 / 3}, "hbm": 8000.0}
 # profiler symbol of each launch class (to match profiles/*kernel_stats.csv rows)
 # (rocprofv3 prints the attention kernels mangled: it does not demangle the __bf16 / _Float16
 # template arguments, DF16b / DF16_)
@@ -66,7 +68,9 @@ def parse():
     p.add_argument("--layers", type=int, default=None)
     p.add_argument("--solver", default=None, choices=["epnp", "epnp_lm", "ransac_p3p_lm", "epnp_ransac_sigma"])
     p.add_argument("--sigma-head", type=int, default=None, choices=[0, 1])
-    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32"])
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp32x3"],
+                   help="bf16: throughput mode; fp32: exact-f32 MFMA parity mode; fp32x3: fp32 storage with "
+                        "split-bf16 MFMA (the fast parity mode)")
     p.add_argument("--attn-dtype", dest="attn_dtype", default=None, choices=["bf16", "fp16"],
                    help="encoder self-attention operand type (bf16 models; config 5 preset: fp16)")
     p.add_argument("--weights", default="pose-consistent", choices=["pose-consistent", "label-diverse", "random"],
@@ -98,7 +102,7 @@ def parse():
     for k, v in PRESETS[a.config].items():
         if getattr(a, k) is None:
             setattr(a, k, v)
-    if a.attn_dtype is None or a.dtype == "fp32":
+    if a.attn_dtype is None or a.dtype != "bf16":
         a.attn_dtype = a.dtype
     return a
 
@@ -495,8 +499,10 @@ def main():
                    "attention_dtype": ("bf16 q/k, fp16 V/P" if args.attn_dtype == "bf16" and args.dtype == "bf16"
                                        and os.environ.get("SPE_ATTN_F16V", "1") != "0" else args.attn_dtype),
                    "parallelism": f"dp{world} (image sharding)"},
-        "roofline": {"kernel": dominant, "kernel_symbol": KIND_SYMBOL.get(dominant, dominant).replace(
-                         "DF16b", "DF16_" if args.attn_dtype == "fp16" else "DF16b"),
+        "roofline": {"kernel": dominant, "kernel_symbol": (
+                         {"fp32": "attn_f32_kernel", "fp32x3": "attn_x3_kernel"}[args.dtype]
+                         if dominant == "attn.enc" and args.dtype != "bf16" else
+                         KIND_SYMBOL.get(dominant, dominant).replace("DF16b", "DF16_" if args.attn_dtype == "fp16" else "DF16b")),
                      "bound": "mfma" if mfma_bound else "hbm", "achieved": achieved,
                      "peak": peak, "unit": unit, "frac": achieved / peak,
                      "traffic": traffic_for(dominant, launch_grid(dominant, B, cfg), args.attn_dtype), "launches": k_n, "avg_launch_ms": avg_ms,
@@ -514,7 +520,7 @@ def main():
                                         "fg_queries": int(e.size), "weights": args.weights}
         if fit is not None:
             result["keypoints_vs_gt_px"].update(fit)
-        if args.dtype == "bf16" and not args.no_accuracy:
+        if args.dtype != "fp32" and not args.no_accuracy:
             result["accuracy_vs_fp32"] = accuracy_vs_fp32(model, cfg, args, w, out, data, solver, dev)
     if world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = (cpu_baseline(cfg, args.cpu_seconds, args.solver) if rcfg is None

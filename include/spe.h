@@ -29,7 +29,11 @@ enum {
   SPE_E_LAUNCH = -6      /* kernel launch rejected its shapes */
 };
 
-enum { SPE_DTYPE_BF16_ = 0, SPE_DTYPE_F32_ = 1, SPE_DTYPE_F16_ = 2 };
+/* BF16_: bf16 storage, bf16 MFMA with fp32 accumulation (throughput mode); F32_: fp32 storage,
+ * exact-f32 MFMA (parity mode); F16_: fp16 attention operands (attn_dtype only); F32X3_: fp32
+ * storage, split-bf16 MFMA (x = hi + lo, products hi.hi + hi.lo + lo.hi, fp32 accumulation):
+ * the fast parity mode */
+enum { SPE_DTYPE_BF16_ = 0, SPE_DTYPE_F32_ = 1, SPE_DTYPE_F16_ = 2, SPE_DTYPE_F32X3_ = 4 };
 
 /* Solver modes.
  *  SPE_PNP_EPNP              cv2.solvePnPGeneric(EPNP) on all selected points
@@ -63,7 +67,7 @@ typedef struct {
   int nheads;           /* --nheads (8; head_dim must be 32) */
   int dim_feedforward;  /* --dim_feedforward (2048) */
   int sigma_head;       /* 1: UNC-style sigma head (sigma_embed.layers.*) */
-  int dtype;            /* SPE_DTYPE_BF16_ (bf16 storage, fp32 accumulate) or SPE_DTYPE_F32_ */
+  int dtype;            /* SPE_DTYPE_BF16_ (bf16 storage, fp32 accumulate), SPE_DTYPE_F32_ or SPE_DTYPE_F32X3_ */
   int attn_dtype;       /* encoder self-attention operands (q, k, V^T): 0 = as dtype; SPE_DTYPE_F16_ =
                          * fp16 (bf16 models only; BASELINE config 5's "fp16 MFMA attention") */
 } spe_model_config;

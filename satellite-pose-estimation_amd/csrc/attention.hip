@@ -441,11 +441,163 @@ __global__ __launch_bounds__(NT, 2) void attn_f32_kernel(AttnArgs a) {
   }
 }
 
+// ------------------------------------------------------------------ fp32x3 (parity) kernel
+// fp32 q, k, V^T in and fp32 out like attn_f32_kernel, computed with split-bf16 MFMAs: every
+// fp32 operand x = hi + lo (hi = bf16(x), lo = bf16(x - hi)) and each product as hi.hi + hi.lo
+// + lo.hi on v_mfma_f32_32x32x16_bf16 (relative error ~2^-17 per product instead of fp32's
+// 2^-24, at a sixth of the matrix cycles of v_mfma_f32_32x32x2_f32).  K and V^T are split once
+// per tile as they are staged (the bf16 kernel's LDS images, one for hi and one for lo); q is
+// scaled into the exp2 domain in fp32 and split in registers; the probabilities stay fp32 for
+// the running max, the exp2 and the row sums, and are split only as the value-product operand.
+__global__ __launch_bounds__(NT, 2) void attn_x3_kernel(AttnArgs a) {
+  constexpr int KB = KT * KROW, VB = 32 * VROW, SLOT = 2 * (KB + VB);   // [K hi | K lo | V hi | V lo]
+  __shared__ __attribute__((aligned(16))) char smem[2 * SLOT];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int hh = lane >> 5, r32 = lane & 31;
+  const int qblocks = (a.Tq + 127) / 128;
+  const int bid = xcd_remap(blockIdx.x, gridDim.x);
+  const int bh = bid / qblocks, qb = bid - bh * qblocks;
+  const int b = bh / a.H, h = bh - b * a.H;
+  const int q = qb * 128 + wid * 32 + r32;
+  const bool wave_live = qb * 128 + wid * 32 < a.Tq;
+  auto mf = [](u32x4 x, u32x4 y, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, x), __builtin_bit_cast(bf16x8, y), c, 0, 0, 0);
+  };
+  // query fragments: dims 16i + 8hh + (0..7), scaled by softmax_scale * log2(e) in fp32, split
+  u32x4 qh[2], ql[2];
+  {
+    const float sl2 = a.scale * LOG2E;
+    const float* qp = (const float*)a.q + (size_t)(b * a.Tq + (q < a.Tq ? q : 0)) * a.ldq + h * 32;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      float f[8];
+      const u32x4 x0 = q < a.Tq ? ld16(qp + 16 * i + 8 * hh) : u32x4{0, 0, 0, 0};
+      const u32x4 x1 = q < a.Tq ? ld16(qp + 16 * i + 8 * hh + 4) : u32x4{0, 0, 0, 0};
+      unpack16<float>(x0, f);
+      unpack16<float>(x1, f + 4);
+      uint32_t hw[4], lw[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float v0 = f[2 * e] * sl2, v1 = f[2 * e + 1] * sl2;
+        hw[e] = pack_bf16x2(v0, v1);
+        lw[e] = pack_bf16x2(v0 - __uint_as_float(hw[e] << 16), v1 - __uint_as_float(hw[e] & 0xffff0000u));
+      }
+      qh[i] = u32x4{hw[0], hw[1], hw[2], hw[3]};
+      ql[i] = u32x4{lw[0], lw[1], lw[2], lw[3]};
+    }
+  }
+  f32x16 o;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) o[r] = 0.f;
+  float m = NEG_BIG, l = 0.f;
+
+  // staging: fp32 tiles through registers (Stage<float>), split into the hi / lo images
+  Stage<float, KT> st;
+  auto store = [&](char* sl) {
+    constexpr int KCPR = 8, VCPR = KT / 4;
+#pragma unroll
+    for (int i = 0; i < Stage<float, KT>::KCH; ++i) {
+      const int idx = tid + i * NT, key = idx / KCPR, c = idx % KCPR;   // dims 4c..4c+3
+      const f32x4 f = __builtin_bit_cast(f32x4, st.kr[i]);
+      const uint32_t h0 = pack_bf16x2(f[0], f[1]), h1 = pack_bf16x2(f[2], f[3]);
+      const uint32_t l0 = pack_bf16x2(f[0] - __uint_as_float(h0 << 16), f[1] - __uint_as_float(h0 & 0xffff0000u));
+      const uint32_t l1 = pack_bf16x2(f[2] - __uint_as_float(h1 << 16), f[3] - __uint_as_float(h1 & 0xffff0000u));
+      const int off = k_off_bf16(key, c >> 1) + (c & 1) * 8;
+      st8(sl + off, u32x2{h0, h1});
+      st8(sl + KB + off, u32x2{l0, l1});
+    }
+#pragma unroll
+    for (int i = 0; i < Stage<float, KT>::VCH; ++i) {
+      const int idx = tid + i * NT, d = idx / VCPR, c = idx % VCPR;     // keys 4c..4c+3
+      const f32x4 f = __builtin_bit_cast(f32x4, st.vr[i]);
+      const uint32_t h0 = pack_bf16x2(f[0], f[1]), h1 = pack_bf16x2(f[2], f[3]);
+      const uint32_t l0 = pack_bf16x2(f[0] - __uint_as_float(h0 << 16), f[1] - __uint_as_float(h0 & 0xffff0000u));
+      const uint32_t l1 = pack_bf16x2(f[2] - __uint_as_float(h1 << 16), f[3] - __uint_as_float(h1 & 0xffff0000u));
+      st8(sl + 2 * KB + v_quad_off(d, c), u32x2{h0, h1});
+      st8(sl + 2 * KB + VB + v_quad_off(d, c), u32x2{l0, l1});
+    }
+  };
+  const int ntiles = (a.Tk + KT - 1) / KT;
+  st.load(a, b, h, 0, tid);
+  store(smem);
+  __syncthreads();
+  for (int kt = 0; kt < ntiles; ++kt) {
+    const char* kl = smem + (kt & 1) * SLOT;
+    const char* vl = kl + 2 * KB;
+    const bool more = kt + 1 < ntiles;
+    if (more) st.load(a, b, h, kt + 1, tid);
+    if (wave_live) {
+      f32x16 s0, s1;
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        f32x16& s = sub ? s1 : s0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) s[r] = 0.f;
+        const int key = sub * 32 + r32;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+          const u32x4 kh = ld16(kl + k_off_bf16(key, 2 * i + hh)), klo = ld16(kl + KB + k_off_bf16(key, 2 * i + hh));
+          s = mf(klo, qh[i], s);
+          s = mf(kh, ql[i], s);
+          s = mf(kh, qh[i], s);
+        }
+      }
+      const float mx = tile_max(s0, s1, kt * KT, a.Tk, hh);
+      const float mn = __builtin_fmaxf(m, mx);
+      const float alpha = exp2f(m - mn);
+      float sum = 0.f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        s0[r] = exp2f(s0[r] - mn);
+        s1[r] = exp2f(s1[r] - mn);
+        sum += s0[r] + s1[r];
+      }
+      l = l * alpha + sum;
+      m = mn;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) o[r] *= alpha;
+#pragma unroll
+      for (int sub = 0; sub < 2; ++sub) {
+        const f32x16& p = sub ? s1 : s0;
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) {
+          uint32_t hw[4], lw[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float v0 = p[8 * ks + 2 * e], v1 = p[8 * ks + 2 * e + 1];
+            hw[e] = pack_bf16x2(v0, v1);
+            lw[e] = pack_bf16x2(v0 - __uint_as_float(hw[e] << 16), v1 - __uint_as_float(hw[e] & 0xffff0000u));
+          }
+          const int vo = r32 * VROW + (2 * sub + ks) * 32 + hh * 16;
+          const u32x4 vh = ld16(vl + vo), vlo = ld16(vl + VB + vo);
+          const u32x4 ph{hw[0], hw[1], hw[2], hw[3]}, pl{lw[0], lw[1], lw[2], lw[3]};
+          o = mf(vlo, ph, o);
+          o = mf(vh, pl, o);
+          o = mf(vh, ph, o);
+        }
+      }
+    }
+    if (more) store(smem + ((kt + 1) & 1) * SLOT);
+    __syncthreads();
+  }
+
+  if (!wave_live || q >= a.Tq) return;
+  const float lt = l + __shfl_xor(l, 32, 64);
+  const float inv = 1.f / lt;
+  float* op = (float*)a.o + (size_t)(b * a.Tq + q) * a.ldo + h * 32;
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    // O^T accumulator rows: dims 8g + 4hh + (0..3), the bf16 kernel's output order
+    float v[4] = {o[4 * g] * inv, o[4 * g + 1] * inv, o[4 * g + 2] * inv, o[4 * g + 3] * inv};
+    st16(op + 8 * g + 4 * hh, pack16<float>(v));
+  }
+}
+
 }  // namespace
 
 int spe_launch_attention(const AttnArgs& a, int dtype, hipStream_t s) {
   if (a.B <= 0 || a.Tq <= 0 || a.Tk <= 0) return 0;
-  const int ce = dtype == SPE_DTYPE_F32 ? 4 : 8;
+  const int ce = (dtype == SPE_DTYPE_F32 || dtype == SPE_DTYPE_F32X3) ? 4 : 8;
   if ((a.ldq % ce) || (a.ldk % ce) || (a.ldo % 4)) return -5;
   dim3 grid(a.B * a.H * ((a.Tq + 127) / 128)), block(NT);
   if (dtype == SPE_DTYPE_F16)
@@ -463,6 +615,8 @@ int spe_launch_attention(const AttnArgs& a, int dtype, hipStream_t s) {
       hipLaunchKernelGGL((attn16_kernel<0, bf16>), grid, block, 0, s, a);
     else
       hipLaunchKernelGGL((attn16_kernel<1, bf16>), grid, block, 0, s, a);
+  else if (dtype == SPE_DTYPE_F32X3)
+    hipLaunchKernelGGL(attn_x3_kernel, grid, block, 0, s, a);
   else
     hipLaunchKernelGGL(attn_f32_kernel, grid, block, 0, s, a);
   return (int)hipGetLastError();

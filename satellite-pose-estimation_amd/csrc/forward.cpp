@@ -58,13 +58,14 @@ int run_gemm(spe_model* m, const char* kind, const GemmArgs& g, int mode, hipStr
   const double bytes = (a_elems + (double)g.N * g.K + (double)g.M * g.N + r_rows * g.N) * E +
                        (mode == GEMM_LINEAR_ADD ? (double)g.prow * g.K * E : 0.0);
   return run_other(m, kind, 2.0 * g.M * g.N * g.K, bytes, s,
-                   [&] { return spe_launch_gemm(g, m->cfg.dtype, mode, s); });
+                   [&] { return spe_launch_gemm(g, m->x3 ? (int)SPE_DTYPE_F32X3 : m->cfg.dtype, mode, s); });
 }
 
 int run_attn(spe_model* m, const char* kind, const AttnArgs& a, int dtype, hipStream_t s) {
   const double flops = 4.0 * a.B * a.H * (double)a.Tq * a.Tk * 32;
   const double bytes = (double)a.B * a.H * 32 * (2.0 * a.Tq + 2.0 * a.Tk) * m->esz;
-  return run_other(m, kind, flops, bytes, s, [&] { return spe_launch_attention(a, dtype, s); });
+  const int dt = (m->x3 && dtype == SPE_DTYPE_F32) ? (int)SPE_DTYPE_F32X3 : dtype;
+  return run_other(m, kind, flops, bytes, s, [&] { return spe_launch_attention(a, dt, s); });
 }
 
 GemmArgs linear_args(const Conv& c, const void* A, int lda, int M, void* C, int ldc) {

@@ -17,6 +17,12 @@
 // One K-step moves 128 bytes of every row: 64 bf16 (2 x mfma_f32_16x16x32_bf16) or 32 fp32
 // (8 x mfma_f32_16x16x4f32, exact f32).  Global -> register -> LDS staging, double-buffered,
 // XOR-swizzled 16-byte slots (conflict-free ds_read_b128 fragment reads), one barrier per step.
+// X3 (the fp32x3 parity mode, SPE_DTYPE_F32X3): fp32 operands are split while they are staged,
+// x = hi + lo with hi = bf16(x), lo = bf16(x - hi) (x - hi is exact in fp32), the 32-element
+// K-step's hi halves in slots 0-3 and lo halves in slots 4-7 of the same 128-byte LDS row, and
+// each fragment product is hi.hi + hi.lo + lo.hi: three mfma_f32_16x16x32_bf16 with fp32
+// accumulation instead of eight mfma_f32_16x16x4f32 -- a relative error of ~2^-17 per product
+// (the dropped lo.lo term and lo's own rounding) at 5x fewer matrix cycles.
 #include "spe_common.h"
 #include "spe_kernels.h"
 
@@ -104,6 +110,62 @@ SPE_DEV void load_b(const GemmArgs& g, int n0, int kstep, int tid, u32x4* r) {
   }
 }
 
+// split 4 fp32 into bf16 hi (returned) and lo (out) words: RNE both, lo of the exact remainder
+SPE_DEV u32x2 split4(u32x4 x, u32x2& lo) {
+  const f32x4 f = __builtin_bit_cast(f32x4, x);
+  const uint32_t h0 = pack_bf16x2(f[0], f[1]), h1 = pack_bf16x2(f[2], f[3]);
+  const float r0 = f[0] - __uint_as_float(h0 << 16), r1 = f[1] - __uint_as_float(h0 & 0xffff0000u);
+  const float r2 = f[2] - __uint_as_float(h1 << 16), r3 = f[3] - __uint_as_float(h1 & 0xffff0000u);
+  lo = u32x2{pack_bf16x2(r0, r1), pack_bf16x2(r2, r3)};
+  return u32x2{h0, h1};
+}
+
+// X3 stage: the thread's chunk c (fp32 elements 4c..4c+3 of the K-step) -> hi piece at byte
+// 8 * (c & 1) of 16-byte slot c >> 1, lo piece likewise in slot 4 + (c >> 1)
+SPE_DEV void store_stage_x3(char* st, int tid, const u32x4* ra, const u32x4* rb) {
+  const int c = tid & 7, half = (c & 1) * 8;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (tid >> 3) + 32 * i;
+    u32x2 lo;
+    u32x2 hi = split4(ra[i], lo);
+    st8(st + swz(row, c >> 1) + half, hi);
+    st8(st + swz(row, 4 + (c >> 1)) + half, lo);
+    hi = split4(rb[i], lo);
+    st8(st + BM * 128 + swz(row, c >> 1) + half, hi);
+    st8(st + BM * 128 + swz(row, 4 + (c >> 1)) + half, lo);
+  }
+}
+
+SPE_DEV void mma_step_x3(const char* st, int wr, int wc, int lane, f32x4 (&acc)[4][4]) {
+  const int g = lane >> 4, rr = lane & 15;
+  u32x4 ah[4], al[4], bh[4], bl[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = wr * 64 + i * 16 + rr;
+    ah[i] = ld16(st + swz(row, g));
+    al[i] = ld16(st + swz(row, 4 + g));
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = wc * 64 + j * 16 + rr;
+    bh[j] = ld16(st + BM * 128 + swz(row, g));
+    bl[j] = ld16(st + BM * 128 + swz(row, 4 + g));
+  }
+  auto mf = [](u32x4 a, u32x4 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+  };
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      // small terms first, then the large one (each MFMA rounds its sum to fp32)
+      acc[i][j] = mf(al[i], bh[j], acc[i][j]);
+      acc[i][j] = mf(ah[i], bl[j], acc[i][j]);
+      acc[i][j] = mf(ah[i], bh[j], acc[i][j]);
+    }
+}
+
 SPE_DEV void store_stage(char* st, int tid, const u32x4* ra, const u32x4* rb) {
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -149,7 +211,7 @@ SPE_DEV void mma_step(const char* st, int wr, int wc, int lane, f32x4 (&acc)[4][
     }
 }
 
-template <typename T, int MODE>
+template <typename T, int MODE, bool X3 = false>
 __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -178,9 +240,13 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs g) {
   }
 
   u32x4 ra[4], rb[4];
+  auto stage = [&](char* st) {
+    if constexpr (X3) store_stage_x3(st, tid, ra, rb);
+    else store_stage(st, tid, ra, rb);
+  };
   al.load(g, 0, tid, ra);
   load_b<T>(g, n0, 0, tid, rb);
-  store_stage(smem, tid, ra, rb);
+  stage(smem);
   __syncthreads();
   for (int ks = 0; ks < nk; ++ks) {
     const bool more = ks + 1 < nk;
@@ -188,8 +254,9 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs g) {
       al.load(g, ks + 1, tid, ra);
       load_b<T>(g, n0, ks + 1, tid, rb);
     }
-    mma_step<T>(smem + (ks & 1) * STAGE_BYTES, wr, wc, lane, acc);
-    if (more) store_stage(smem + ((ks + 1) & 1) * STAGE_BYTES, tid, ra, rb);
+    if constexpr (X3) mma_step_x3(smem + (ks & 1) * STAGE_BYTES, wr, wc, lane, acc);
+    else mma_step<T>(smem + (ks & 1) * STAGE_BYTES, wr, wc, lane, acc);
+    if (more) stage(smem + ((ks + 1) & 1) * STAGE_BYTES);
     __syncthreads();
   }
 
@@ -296,15 +363,15 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs g) {
   }
 }
 
-template <typename T>
+template <typename T, bool X3 = false>
 int launch_t(const GemmArgs& g, int mode, hipStream_t s) {
   const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
   if (tiles <= 0) return 0;
   dim3 grid(tiles), block(NT);
   switch (mode) {
-    case GEMM_LINEAR: hipLaunchKernelGGL((gemm_kernel<T, GEMM_LINEAR>), grid, block, 0, s, g); break;
-    case GEMM_LINEAR_ADD: hipLaunchKernelGGL((gemm_kernel<T, GEMM_LINEAR_ADD>), grid, block, 0, s, g); break;
-    case GEMM_CONV: hipLaunchKernelGGL((gemm_kernel<T, GEMM_CONV>), grid, block, 0, s, g); break;
+    case GEMM_LINEAR: hipLaunchKernelGGL((gemm_kernel<T, GEMM_LINEAR, X3>), grid, block, 0, s, g); break;
+    case GEMM_LINEAR_ADD: hipLaunchKernelGGL((gemm_kernel<T, GEMM_LINEAR_ADD, X3>), grid, block, 0, s, g); break;
+    case GEMM_CONV: hipLaunchKernelGGL((gemm_kernel<T, GEMM_CONV, X3>), grid, block, 0, s, g); break;
     default: return -1;
   }
   return (int)hipGetLastError();
@@ -331,5 +398,6 @@ int spe_launch_gemm(const GemmArgs& g, int dtype, int mode, hipStream_t s) {
     if (rc != 1) return rc;
   }
   spe_gemm_last_path = 0;
+  if (dtype == SPE_DTYPE_F32X3) return launch_t<float, true>(g, mode, s);
   return dtype == SPE_DTYPE_BF16 ? launch_t<bf16>(g, mode, s) : launch_t<float>(g, mode, s);
 }

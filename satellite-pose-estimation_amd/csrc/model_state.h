@@ -106,6 +106,7 @@ struct RtModel {
 
 struct spe_model {
   int family = 0;            // 0: DETR (REV), 1: RT-DETR (UNC)
+  int x3 = 0;                // fp32 model computed with split-bf16 MFMA (SPE_DTYPE_F32X3_)
   RtModel* rt = nullptr;
   spe_model_config cfg{};
   int esz = 2;

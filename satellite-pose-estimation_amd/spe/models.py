@@ -26,7 +26,9 @@ class DETR(nn.Module):
     """Keypoint-set predictor (REV/models/detr_speed.py:32-100), HIP implementation.
 
     dtype "bf16": bf16 storage / MFMA with fp32 accumulation, softmax, LayerNorm and heads
-    (throughput path).  dtype "fp32": exact-f32 MFMA everywhere (parity path).
+    (throughput path).  dtype "fp32": exact-f32 MFMA everywhere (parity path).  dtype "fp32x3":
+    the fp32 model with split-bf16 MFMA compute (every fp32 operand x = hi + lo in bf16, products
+    hi.hi + hi.lo + lo.hi, fp32 accumulation; fast parity path).
     attn_dtype "fp16" (bf16 models): the encoder self-attention's q/k/V operands are stored
     and multiplied in fp16 (BASELINE config 5, "fp16 MFMA attention")."""
 
@@ -45,7 +47,8 @@ class DETR(nn.Module):
         L = _lib.lib()
         c = _lib.ModelConfig(cfg.input_size, cfg.num_queries, cfg.enc_layers, cfg.dec_layers, cfg.hidden_dim,
                              cfg.nheads, cfg.dim_feedforward, int(cfg.sigma_head),
-                             _lib.SPE_DTYPE_BF16 if dtype == "bf16" else _lib.SPE_DTYPE_F32,
+                             {"bf16": _lib.SPE_DTYPE_BF16, "fp32": _lib.SPE_DTYPE_F32,
+                              "fp32x3": _lib.SPE_DTYPE_F32X3}[dtype],
                              _lib.SPE_DTYPE_F16 if self.attn_dtype == "fp16" else 0)
         h = ctypes.c_void_p()
         _lib.check(L.spe_model_create(ctypes.byref(c), ctypes.byref(h)), "spe_model_create")

@@ -19,6 +19,7 @@ from spe import _lib
 pytestmark = pytest.mark.gpu
 
 DT = {"bf16": (_lib.SPE_DTYPE_BF16, torch.bfloat16, 1e-2), "fp32": (_lib.SPE_DTYPE_F32, torch.float32, 1e-4),
+      "fp32x3": (_lib.SPE_DTYPE_F32X3, torch.float32, 1e-4),
       "fp16": (_lib.SPE_DTYPE_F16, torch.float16, 2e-3)}
 
 
@@ -626,3 +627,73 @@ def test_gemm_f16_store_saturates(gpu_device, rows):
     assert (got[:, big].abs() == 65504).all()
     y = A.float() @ Wt.float().t() + bias
     _close(got[:, ~big], y[:, ~big], 1e-2)
+
+
+# ---------------------------------------------------------------- fp32x3 (split-bf16) parity mode
+@pytest.mark.parametrize("case", ["linear", "linear_add_relu_res", "conv3x3", "conv1x1s2", "vt"])
+def test_gemm_x3_close_to_fp64(gpu_device, case):
+    """fp32 storage, split-bf16 MFMA (hi.hi + hi.lo + lo.hi): within 2e-5 relative of an fp64
+    reference, i.e. far inside the fp32 parity tolerances and ~100x tighter than bf16."""
+    g = torch.Generator(device="cpu").manual_seed(len(case))
+    dev, f = gpu_device, torch.float32
+    if case.startswith("conv"):
+        B, H, Cin, Cout, k, st, pd = (2, 26, 256, 256, 3, 1, 1) if case == "conv3x3" else (2, 52, 512, 256, 1, 2, 0)
+        x = torch.randn(B, Cin, H, H, generator=g, dtype=torch.float64)
+        w = torch.randn(Cout, Cin, k, k, generator=g, dtype=torch.float64) / (Cin * k * k) ** 0.5
+        ref = F.conv2d(x, w, stride=st, padding=pd).permute(0, 2, 3, 1).reshape(-1, Cout)
+        A = x.permute(0, 2, 3, 1).contiguous().to(dev, f)
+        Wp = _pack_conv(w).to(dev, f).contiguous()
+        Ho = (H + 2 * pd - k) // st + 1
+        M, K = B * Ho * Ho, Cin * k * k
+        C = torch.zeros(M, Cout, dtype=f, device=dev)
+        _gemm("fp32x3", 2, A, Wp, M, Cout, K, 0, K, C, Cout, conv=(H, H, Cin, k, k, st, pd))
+        got = C
+    else:
+        M, N, K = (3000, 200, 512) if case != "vt" else (2 * 2704, 256, 256)
+        A = torch.randn(M, K, generator=g, dtype=torch.float64)
+        Wt = torch.randn(N, K, generator=g, dtype=torch.float64) / K ** 0.5
+        bias = torch.randn(N, generator=g, dtype=torch.float64)
+        ref = A @ Wt.t() + bias
+        kw = {}
+        ldc = N + 8
+        if case == "linear_add_relu_res":
+            R = torch.randn(M, ldc, generator=g, dtype=torch.float64)
+            ref = torch.relu(ref + R[:, :N])
+            kw = dict(R=R.to(dev, f), ldr=ldc, relu=1)
+        C = torch.zeros(M, ldc, dtype=f, device=dev)
+        if case == "vt":
+            T, Bv = 2704, 2
+            C = torch.zeros(Bv * N * T, dtype=f, device=dev)
+            _gemm("fp32x3", 0, A.to(dev, f), _padded_weight(Wt.to(dev, f), K, f), M, N, K, K, K, C, 4,
+                  bias=bias.to(dev, f), vt=(T, Bv))
+            got = C.view(N // 256, Bv, 256, T).permute(1, 3, 0, 2).reshape(M, N)
+        else:
+            _gemm("fp32x3", 0, A.to(dev, f), _padded_weight(Wt.to(dev, f), K, f), M, N, K, K, K, C, ldc,
+                  bias=bias.to(dev, f), **kw)
+            got = C[:, :N]
+    err = (got.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
+    assert err <= 2e-5, err
+
+
+@pytest.mark.parametrize("B,H,Tq,Tk", [(1, 8, 300, 333), (2, 8, 2704, 2704), (3, 8, 11, 2704), (2, 8, 11, 11)])
+def test_attention_x3_close_to_fp64(gpu_device, B, H, Tq, Tk):
+    g = torch.Generator(device="cpu").manual_seed(Tq * 3 + Tk)
+    ld = H * 32 + 16
+    Q = torch.randn(B * Tq, ld, generator=g, dtype=torch.float64) * 2
+    K = torch.randn(B * Tk, ld, generator=g, dtype=torch.float64) * 2
+    V = torch.randn(B, H, Tk, 32, generator=g, dtype=torch.float64)
+    dev = gpu_device
+    O = torch.zeros(B * Tq, H * 32, dtype=torch.float32, device=dev)
+    scale = 32 ** -0.5
+    Qd, Kd = Q.to(dev, torch.float32), K.to(dev, torch.float32)     # kept alive across the call
+    VTd = V.transpose(-1, -2).contiguous().to(dev, torch.float32)
+    rc = _lib.lib().spe_debug_attention(None, _lib.SPE_DTYPE_F32X3, _p(Qd), ld, _p(Kd), ld, _p(VTd), _p(O), H * 32, B,
+                                        H, Tq, Tk, scale)
+    assert rc == 0
+    torch.cuda.synchronize()
+    q = Q[:, : H * 32].view(B, Tq, H, 32).transpose(1, 2)
+    k = K[:, : H * 32].view(B, Tk, H, 32).transpose(1, 2)
+    ref = torch.softmax(q @ k.transpose(-1, -2) * scale, -1) @ V
+    ref = ref.transpose(1, 2).reshape(B * Tq, H * 32)
+    err = (O.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
+    assert err <= 5e-5, err

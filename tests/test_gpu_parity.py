@@ -2,8 +2,8 @@
 and the CPU oracles, on seeded inputs.
 
 Tolerances (written here on purpose):
-  fp32 parity mode   pred_points |d| <= 1e-4 (crop-normalised; BASELINE.json keypoint
-                     tolerance), pred_logits |d| <= 2e-3 abs, PostProcess px <= 0.05 px
+  fp32 parity modes  pred_points |d| <= 1e-4 (crop-normalised; BASELINE.json keypoint
+  (fp32, fp32x3)     tolerance), pred_logits |d| <= 2e-3 abs, PostProcess px <= 0.05 px
   bf16 throughput    pred_points |d| <= 2e-2, logits |d| <= 0.25 (bf16 storage, 8-bit mantissa;
                      same bound with fp16 encoder-attention operands)
   solver             status / n_corr / corr_label / inlier masks bit-exact vs oracle/pnp_ref.c,
@@ -57,11 +57,13 @@ def _check_sigmas(o, g, log_tol, rel_tol):
     assert (np.abs(sg - g["pp_sigmas"]) / g["pp_sigmas"]).max() <= rel_tol
 
 
+@pytest.mark.parametrize("dtype", ["fp32", "fp32x3"])
 @pytest.mark.parametrize("tag", GOLDEN_TAGS)
-def test_forward_fp32_matches_reference(gpu_device, tag):
+def test_forward_fp32_matches_reference(gpu_device, tag, dtype):
+    """The parity modes: exact-f32 MFMA, and fp32 storage with split-bf16 MFMA (fp32x3)."""
     g, cfg = _golden(tag)
     b = synthetic_batch(cfg, int(g["batch"]), int(g["image_seed"]))
-    m = _model(cfg, "fp32", int(g["weight_seed"]))
+    m = _model(cfg, dtype, int(g["weight_seed"]))
     img = torch.from_numpy(b["images"]).to(gpu_device)
     clip = torch.from_numpy(b["clip_bbox"]).float().to(gpu_device)
     o = m(img, clip_bbox=clip)
