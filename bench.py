@@ -90,6 +90,9 @@ def parse():
                    help="start every step from 1920x1200 8-bit frames + detector boxes in HBM: the "
                         "validation transform (crop, cv2-cubic resize, normalise; spe.datasets) runs "
                         "on the device inside the timed step")
+    p.add_argument("--jpeg", action="store_true",
+                   help="with --raw-frames: start every step from the frames' baseline-JPEG files (Pillow-encoded, "
+                        "quality 90) in HBM, decoded on the device (spe.datasets.JpegDecoder) inside the timed step")
     p.add_argument("--cpu-seconds", type=float, default=15.0)
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--launch-table", default=None,
@@ -383,10 +386,27 @@ def main():
         from spe.synthetic import synthetic_frames
         data = synthetic_frames(B, seed=1000 + rank)
         H, W = data["frames"].shape[1:3]
+        files, jpeg_bytes = None, 0
+        if args.jpeg:
+            import io
+            from PIL import Image
+            from spe.datasets import JpegDecoder
+
+            def enc(a):
+                bio = io.BytesIO()
+                Image.fromarray(a).save(bio, "JPEG", quality=90)
+                return bio.getvalue()
+            files = [enc(f) for f in data["frames"]]
         pipe = PosePipeline(model, solver, B, device=dev, overlap=not args.no_overlap,
-                            overlap_decode=not (args.no_overlap_decode or args.no_overlap), raw_frames=(H, W, 1))
-        pipe.load_frames(torch.from_numpy(data["frames"]).to(dev), torch.from_numpy(data["bbox_xxyy"]).to(dev),
-                         torch.from_numpy(data["quat"]).to(dev), torch.from_numpy(data["tvec"]).to(dev))
+                            overlap_decode=not (args.no_overlap_decode or args.no_overlap), raw_frames=(H, W, 1),
+                            jpeg_max_bytes=max(len(f) for f in files) if files else 0)
+        if files:
+            jpeg_bytes = sum(len(f) for f in files)
+            pipe.load_jpeg(*JpegDecoder.pack(files, dev), torch.from_numpy(data["bbox_xxyy"]).to(dev),
+                           torch.from_numpy(data["quat"]).to(dev), torch.from_numpy(data["tvec"]).to(dev))
+        else:
+            pipe.load_frames(torch.from_numpy(data["frames"]).to(dev), torch.from_numpy(data["bbox_xxyy"]).to(dev),
+                             torch.from_numpy(data["quat"]).to(dev), torch.from_numpy(data["tvec"]).to(dev))
     else:
         pipe = PosePipeline(model, solver, B, device=dev, overlap=not args.no_overlap,
                             overlap_decode=rcfg is None and not (args.no_overlap_decode or args.no_overlap))
@@ -485,7 +505,7 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": args.dtype,
-        "data": f"synthetic (seeded SPEED-shaped {'1920x1200 8-bit frames + detector boxes, on-device val transform' if args.raw_frames else 'crops'}; "
+        "data": f"synthetic (seeded SPEED-shaped {('1920x1200 grayscale JPEG files (q90) + detector boxes, on-device decode + val transform' if args.jpeg else '1920x1200 8-bit frames + detector boxes, on-device val transform') if args.raw_frames else 'crops'}; "
                 f"{args.weights} random-init weights, no checkpoint exists in the reference)",
         "config": {"workload": (CONFIG_NAME[args.config].format(L=args.layers, Q=args.queries, S=args.size,
                                                                  solver=args.solver, A=args.attn_dtype) if rcfg is None else
@@ -493,6 +513,7 @@ def main():
                                 f"with sigma head, {args.queries} queries, {args.size}x{args.size}, sigma-weighted "
                                 f"EPnP-RANSAC + self-assessment (solver={args.solver}; SURVEY 8f.4, not a BASELINE config)"),
                    "global_batch": B * world, "per_gpu_batch": B, "input_size": args.size,
+                   **({"jpeg_bytes_per_step": jpeg_bytes} if args.raw_frames and args.jpeg else {}),
                    "num_queries": args.queries,
                    # bf16 models' encoder attention keeps q/k bf16 and runs V^T and P in fp16 (finer
                    # mantissa than bf16; attention.hip TV)

@@ -141,9 +141,10 @@ inline bool spe_use_xattn(const spe_model* m) {
   return c.dtype == SPE_DTYPE_BF16_ && c.hidden_dim == 256 && c.nheads == 8 && c.dim_feedforward % 32 == 0 &&
          c.enc_layers > 0;
 }
-// bf16 models evaluate s16_latern(up16sto8s(xs16)) at the low resolution (one per-tap GEMM +
-// upconv_combine); the fp32 parity mode keeps the reference's upsample-then-conv order
+// bf16 and fp32x3 models evaluate s16_latern(up16sto8s(xs16)) at the low resolution (one
+// per-tap GEMM + upconv_combine: exact by linearity, a different rounding order); the exact-f32
+// parity mode keeps the reference's upsample-then-conv order
 inline bool spe_use_upconv(const spe_model* m) {
-  return m->cfg.dtype == SPE_DTYPE_BF16_ && m->cfg.input_size % 16 == 0;
+  return (m->cfg.dtype == SPE_DTYPE_BF16_ || m->x3) && m->cfg.input_size % 16 == 0;
 }
 Ws spe_plan(const spe_model* m, int B);

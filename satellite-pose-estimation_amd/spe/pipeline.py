@@ -1,5 +1,6 @@
 """Whole-batch device pipeline of the evaluate() hot loop (REV/engine.py:91-123 without the
-logging-only criterion): [raw frames -> validation transform (spe.datasets, optional)] ->
+logging-only criterion): [JPEG files -> decode] -> [raw frames -> validation transform
+(spe.datasets, optional)] ->
 images -> backbone/transformer/heads + fused PostProcess -> batched PnP -> SPEED scores, all
 on the device with no host round trip.  Optionally captured
 into a HIP graph (torch.cuda.CUDAGraph drives hipStreamBeginCapture on ROCm): spe_forward,
@@ -16,7 +17,8 @@ from .speed_eval import device_speed_score
 
 class PosePipeline:
     def __init__(self, model: DETR, solver: PoseSolver, batch: int, device="cuda", use_graph: bool = False,
-                 self_assess: bool = True, overlap: bool = False, raw_frames=None, overlap_decode: bool = False):
+                 self_assess: bool = True, overlap: bool = False, raw_frames=None, overlap_decode: bool = False,
+                 jpeg_max_bytes: int = 0):
         self.model, self.solver, self.B = model, solver, batch
         self.self_assess = self_assess
         # overlap: the solver / score / self-assessment of batch i run on a second HIP stream
@@ -65,6 +67,17 @@ class PosePipeline:
             self.transform = SpeedValTransform(S)
             self.pp_out = {"images": self.images, "clip_bbox": self.clip_bbox,
                            "status": torch.zeros(batch, dtype=torch.int32, device=dev)}
+        # jpeg_max_bytes > 0 (with raw_frames = (H, W, 1)): each run() starts from the frames' JPEG
+        # files in HBM (load_jpeg) and decodes them on the device first (spe.datasets.JpegDecoder)
+        self.decoder = None
+        if jpeg_max_bytes > 0:
+            from .datasets import JpegDecoder
+            H, W, C = raw_frames
+            if C != 1:
+                raise ValueError("JPEG input: grayscale frames (raw_frames = (H, W, 1))")
+            self.decoder = JpegDecoder(H, W, jpeg_max_bytes)
+            self.jpeg = None
+            self.dec_out = {"frames": self.frames, "status": torch.zeros(batch, dtype=torch.int32, device=dev)}
         self.use_graph = use_graph
         self.graph = None
         self.out = None
@@ -81,10 +94,15 @@ class PosePipeline:
             out["assess"] = self.solver.self_assess(fo["probs"], sig, poses, stream=stream)   # config-4 filter
         return out
 
+    def _decode(self):
+        if self.decoder is not None:
+            self.decoder(*self.jpeg, out=self.dec_out)
+
     def _body_staged(self):
         main = torch.cuda.current_stream()
         slot = self.calls % 2
         self.calls += 1
+        self._decode()
         if self.transform is not None:
             self.transform(self.frames, self.bbox, out=self.pp_out)
         if self.dec_done[slot] is not None:
@@ -117,6 +135,7 @@ class PosePipeline:
     def _body(self):
         if self.overlap_decode:
             return self._body_staged()
+        self._decode()
         if self.transform is not None:
             self.transform(self.frames, self.bbox, out=self.pp_out)
         fo = self.model(self.images, clip_bbox=self.clip_bbox)
@@ -150,6 +169,15 @@ class PosePipeline:
     def load_frames(self, frames, bbox_xxyy, q_gt=None, t_gt=None):
         """Raw-frame mode: uint8 frames [B,H,W(,3)] + detector boxes [B,4] (fp64)."""
         self.frames.copy_(frames, non_blocking=True)
+        self.bbox.copy_(torch.as_tensor(bbox_xxyy, dtype=torch.float64), non_blocking=True)
+        if q_gt is not None:
+            self.q_gt.copy_(q_gt, non_blocking=True)
+            self.t_gt.copy_(t_gt, non_blocking=True)
+
+    def load_jpeg(self, data, offsets, sizes, bbox_xxyy, q_gt=None, t_gt=None):
+        """JPEG mode: the batch's files packed into one device byte buffer (JpegDecoder.pack; kept
+        by reference, not copied) + detector boxes [B,4]."""
+        self.jpeg = (data, offsets, sizes)
         self.bbox.copy_(torch.as_tensor(bbox_xxyy, dtype=torch.float64), non_blocking=True)
         if q_gt is not None:
             self.q_gt.copy_(q_gt, non_blocking=True)

@@ -221,3 +221,35 @@ def test_pipeline_graph_sigma_matches_eager(gpu_device):
         for key in res[0]:
             assert torch.equal(res[0][key], res[1][key]), (k, key)
     assert graph.graph is not None
+
+
+def test_pipeline_from_jpeg_matches_raw_frames(gpu_device, small_model):
+    """JPEG mode (device decode -> validation transform -> model -> solver) == the raw-frame
+    pipeline fed with Pillow's decode of the same files."""
+    import io
+    from PIL import Image
+    from spe.datasets import JpegDecoder
+    from spe.pipeline import PosePipeline
+    from spe.solver import build_solver
+    from spe.synthetic import synthetic_frames
+    cfg, w, m = small_model
+    B = 4
+    d = synthetic_frames(B, seed=41)
+    files = []
+    for f in d["frames"]:
+        bio = io.BytesIO()
+        Image.fromarray(f).save(bio, "JPEG", quality=90)
+        files.append(bio.getvalue())
+    dec = np.stack([np.asarray(Image.open(io.BytesIO(f))) for f in files])
+    solver = build_solver(argparse.Namespace(solver="ransac_p3p_lm", repro=20))
+    hw = d["frames"].shape[1:3]
+    jp = PosePipeline(m, solver, B, device=gpu_device, raw_frames=hw + (1,), jpeg_max_bytes=max(map(len, files)))
+    jp.load_jpeg(*JpegDecoder.pack(files, gpu_device), torch.from_numpy(d["bbox_xxyy"]).to(gpu_device))
+    a = jp.run()
+    raw = PosePipeline(m, solver, B, device=gpu_device, raw_frames=hw + (1,))
+    raw.load_frames(torch.from_numpy(dec).to(gpu_device), torch.from_numpy(d["bbox_xxyy"]).to(gpu_device))
+    b = raw.run()
+    torch.cuda.synchronize()
+    assert torch.equal(jp.frames, raw.frames)
+    for k in ("status", "quat", "tvec"):
+        assert torch.equal(a["poses"][k], b["poses"][k]), k
