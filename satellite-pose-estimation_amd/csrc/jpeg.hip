@@ -31,6 +31,7 @@
 #include "spe_kernels.h"
 #include "../../include/spe.h"
 
+#include <climits>
 #include <string>
 
 int spe_fail(int code, const std::string& msg);
@@ -66,11 +67,12 @@ struct Sub {                            // one subsequence of one segment
   int ep, ez;                           // entry state (bit, coefficient index)
   int xp, xz;                           // exit state
   int cnt;                              // blocks completed between entry and exit
+  int blkp;                             // exclusive prefix of cnt over the image's subsequences
   int blk;                              // block index (image-wide) at entry
 };
 
 struct JpegWs {                         // device workspace carve-up (byte offsets)
-  size_t imgs, subs, segblk, segstart, stream, coef;
+  size_t imgs, subs, segblk, segstart, segfirst, segbad, stream, coef;
   int max_sub, max_seg, stream_stride;
   size_t total;
 };
@@ -248,11 +250,16 @@ SPE_DEV int block_scan_excl(int v, int* sh, int& total) {   // SCAN/UNSTUFF_NT t
   return base + x - v;
 }
 
+// One workgroup per image sweeps the entropy-coded data in tiles of UNSTUFF_NT x 16 bytes: each
+// thread classifies 16 consecutive bytes (coalesced across the wave), one workgroup scan of
+// (kept, restart) counts places them, and the sweep stops at the tile holding the terminating
+// marker.  Then the segments (restart intervals) are cut into subsequences.
 __global__ __launch_bounds__(UNSTUFF_NT) void jpeg_unstuff_kernel(const uint8_t* __restrict__ data,
                                                                     const int64_t* __restrict__ offs,
                                                                     const int64_t* __restrict__ sizes, JpegImg* imgs,
                                                                     Sub* __restrict__ subs, int* __restrict__ segblk,
-                                                                    int* __restrict__ segstart, uint8_t* __restrict__ streams,
+                                                                    int* __restrict__ segstart, int* __restrict__ segfirst,
+                                                                    int* __restrict__ segbad, uint8_t* __restrict__ streams,
                                                                     JpegWs ws) {
   __shared__ int sh[UNSTUFF_NT / 64];
   __shared__ int s_end;
@@ -261,68 +268,67 @@ __global__ __launch_bounds__(UNSTUFF_NT) void jpeg_unstuff_kernel(const uint8_t*
   if (im.status != ST_OK) return;                   // block-uniform
   const uint8_t* d = data + im.ecs_off;
   const int n = (int)(offs[b] + sizes[b] - im.ecs_off);
-  const int per = (n + UNSTUFF_NT - 1) / UNSTUFF_NT;
-  const int lo = min(n, tid * per), hi = min(n, lo + per);
-  auto at = [&](int i) -> uint8_t { return i < n ? d[i] : (uint8_t)0xD9; };
-  // pass 1: the terminating marker
-  int myend = n;
-  {
-    uint8_t prev = lo > 0 ? d[lo - 1] : 0, cur = lo < n ? d[lo] : 0;
-    for (int i = lo; i < hi; ++i) {
-      const uint8_t next = at(i + 1);
-      if (byte_kind(prev, cur, next, i > 0) == B_END) { myend = i; break; }
-      prev = cur;
-      cur = next;
+  uint8_t* out = streams + (size_t)b * ws.stream_stride;
+  int* sst = segstart + (size_t)b * (ws.max_seg + 1);
+  constexpr int TILE = UNSTUFF_NT * 16;
+  int kept = 0, rsts = 0;                           // totals before the current tile
+  bool overflow = false;
+  for (int t0 = 0; t0 < n; t0 += TILE) {
+    const int i0 = t0 + tid * 16;
+    uint8_t v[18];                                  // bytes i0-1 .. i0+16
+#pragma unroll
+    for (int e = 0; e < 18; ++e) {
+      const int i = i0 - 1 + e;
+      v[e] = i < 0 ? (uint8_t)0 : (i < n ? d[i] : (uint8_t)0xD9);   // past the data: as if EOI
     }
-  }
-  if (tid == 0) s_end = n;
-  __syncthreads();
-  atomicMin(&s_end, myend);
-  __syncthreads();
-  const int end = s_end;
-  // pass 2: kept bytes and restart markers per chunk
-  const int h2 = min(hi, end);
-  int keep = 0, rst = 0;
-  {
-    uint8_t prev = lo > 0 ? d[lo - 1] : 0, cur = lo < n ? d[lo] : 0;
-    for (int i = lo; i < h2; ++i) {
-      const uint8_t next = at(i + 1);
-      const int k = byte_kind(prev, cur, next, i > 0);
-      keep += k == B_KEEP;
-      rst += k == B_RST;
-      prev = cur;
-      cur = next;
+    int kind[16];
+    int myend = INT_MAX;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      kind[e] = byte_kind(v[e], v[e + 1], v[e + 2], i0 + e > 0);
+      if (i0 + e >= n) kind[e] = B_END;
+      if (kind[e] == B_END && myend == INT_MAX) myend = i0 + e;
     }
+    if (tid == 0) s_end = INT_MAX;
+    __syncthreads();
+    if (myend != INT_MAX) atomicMin(&s_end, myend);
+    __syncthreads();
+    const int end = s_end;
+    int k = 0, r = 0;
+#pragma unroll
+    for (int e = 0; e < 16; ++e) {
+      const bool live = i0 + e < end;
+      k += live && kind[e] == B_KEEP;
+      r += live && kind[e] == B_RST;
+    }
+    int tot;
+    const int ex = block_scan_excl(k | (r << 16), sh, tot);
+    const int ktot = tot & 0xffff, rtot = tot >> 16;
+    if (rsts + rtot + 1 > ws.max_seg) overflow = true;   // uniform
+    if (!overflow) {
+      int o = kept + (ex & 0xffff), rr = rsts + (ex >> 16);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const bool live = i0 + e < end;
+        if (live && kind[e] == B_KEEP) out[o++] = v[e + 1];
+        else if (live && kind[e] == B_RST) sst[1 + rr++] = o;
+      }
+    }
+    kept += ktot;
+    rsts += rtot;
+    if (end != INT_MAX || overflow) break;          // uniform
   }
-  int ktot, rtot;
-  const int kbase = block_scan_excl(keep, sh, ktot);
-  const int rbase = block_scan_excl(rst, sh, rtot);
-  const int nseg = rtot + 1;
-  if (nseg > ws.max_seg) {
+  if (overflow) {
     if (tid == 0) im.status = ST_CAPACITY;
     return;
   }
-  // pass 3: write the stream and the segment starts (byte offsets)
-  uint8_t* out = streams + (size_t)b * ws.stream_stride;
-  int* sst = segstart + (size_t)b * (ws.max_seg + 1);
-  {
-    uint8_t prev = lo > 0 ? d[lo - 1] : 0, cur = lo < n ? d[lo] : 0;
-    int o = kbase, r = rbase;
-    for (int i = lo; i < h2; ++i) {
-      const uint8_t next = at(i + 1);
-      const int k = byte_kind(prev, cur, next, i > 0);
-      if (k == B_KEEP) out[o++] = cur;
-      else if (k == B_RST) sst[1 + r++] = o;
-      prev = cur;
-      cur = next;
-    }
-  }
+  const int nseg = rsts + 1;
   // zero padding past the data: the Huffman reader peeks up to 8 bytes ahead
-  for (int i = tid; i < 16; i += UNSTUFF_NT) out[ktot + i] = 0;
+  if (tid < 16) out[kept + tid] = 0;
   if (tid == 0) {
     sst[0] = 0;
-    sst[nseg] = ktot;
-    im.ulen = ktot;
+    sst[nseg] = kept;
+    im.ulen = kept;
     im.nseg = nseg;
   }
   __syncthreads();
@@ -330,6 +336,7 @@ __global__ __launch_bounds__(UNSTUFF_NT) void jpeg_unstuff_kernel(const uint8_t*
   const int R = im.restart > 0 ? im.restart : im.nblocks;
   if (tid == 0 && ((long long)nseg - 1) * R >= im.nblocks) im.status = ST_CORRUPT;   // more intervals than blocks
   int* sb = segblk + (size_t)b * (ws.max_seg + 1);
+  int* sf = segfirst + (size_t)b * (ws.max_seg + 1);
   Sub* sbs = subs + (size_t)b * ws.max_sub;
   int sub_base = 0;
   for (int s0 = 0; s0 < nseg; s0 += UNSTUFF_NT) {
@@ -341,6 +348,8 @@ __global__ __launch_bounds__(UNSTUFF_NT) void jpeg_unstuff_kernel(const uint8_t*
     if (s < nseg) {
       sb[s] = min(s * R, im.nblocks);
       const int first = sub_base + sb0;
+      sf[s] = first;
+      segbad[(size_t)b * (ws.max_seg + 1) + s] = 0;
       const int bit0 = sst[s] * 8, bit1 = sst[s + 1] * 8;
       for (int j = 0; j < ns; ++j) {
         const int k = first + j;
@@ -401,16 +410,16 @@ SPE_DEV int huff_sym(const HuffTab& t, uint32_t pk, int& len) {
 
 SPE_DEV int extend(uint32_t v, int s) { return s == 0 ? 0 : (v < (1u << (s - 1)) ? (int)v - (1 << s) + 1 : (int)v); }
 
-// one decode step (one symbol and its value bits); WRITE stores the coefficient (zig-zag
-// position z) of block `blk` into coef
+// one decode step (one symbol and its value bits); WRITE stores the coefficient at zig-zag
+// position z into blk[natural index] (the thread's LDS block slot)
 template <bool WRITE>
-SPE_DEV void step(const HuffTab& dc, const HuffTab& ac, const BitSrc& bs, Dec& st, int16_t* coef, int blk) {
+SPE_DEV void step(const HuffTab& dc, const HuffTab& ac, const BitSrc& bs, Dec& st, int16_t* blk) {
   const uint32_t pk = bs.peek32(st.p);
   int len;
   if (st.z == 0) {
     const int s = huff_sym(dc, pk, len) & 15;
     const uint32_t v = s ? (uint32_t)(((uint64_t)pk << len) & 0xffffffffu) >> (32 - s) : 0u;
-    if (WRITE) coef[(size_t)blk * 64] = (int16_t)extend(v, s);
+    if (WRITE) blk[0] = (int16_t)extend(v, s);
     st.p += len + s;
     st.z = 1;
   } else {
@@ -420,7 +429,7 @@ SPE_DEV void step(const HuffTab& dc, const HuffTab& ac, const BitSrc& bs, Dec& s
       const int z = st.z + r;
       const uint32_t v = (uint32_t)(((uint64_t)pk << len) & 0xffffffffu) >> (32 - s);
       // (z <= 78: libjpeg's natural-order table maps the overflow entries to 63)
-      if (WRITE) coef[(size_t)blk * 64 + c_zz2nat[z]] = (int16_t)extend(v, s);
+      if (WRITE) blk[c_zz2nat[z]] = (int16_t)extend(v, s);
       st.z = z + 1;
       st.p += len + s;
     } else {
@@ -434,11 +443,9 @@ SPE_DEV void step(const HuffTab& dc, const HuffTab& ac, const BitSrc& bs, Dec& s
   }
 }
 
-// decode from `st` until p >= end (or `maxblk` blocks completed)
-template <bool WRITE>
-SPE_DEV void run_to(const HuffTab& dc, const HuffTab& ac, const BitSrc& bs, Dec& st, int end, int maxblk, int16_t* coef,
-                    int blk0) {
-  while (st.p < end && st.blocks < maxblk) step<WRITE>(dc, ac, bs, st, coef, blk0 + st.blocks);
+// decode from `st` until p >= end
+SPE_DEV void run_to_count(const HuffTab& dc, const HuffTab& ac, const BitSrc& bs, Dec& st, int end) {
+  while (st.p < end) step<false>(dc, ac, bs, st, nullptr);
 }
 
 SPE_DEV const uint8_t* stream_of(const JpegWs& ws, uint8_t* streams, int b) { return streams + (size_t)b * ws.stream_stride; }
@@ -454,7 +461,7 @@ __global__ __launch_bounds__(HUFF_NT) void jpeg_huff_spec_kernel(const JpegImg* 
   Sub& u = subs[(size_t)b * ws.max_sub + k];
   BitSrc bs{stream_of(ws, streams, b)};
   Dec st{u.ep, u.ez, 0};
-  run_to<false>(im.dc, im.ac, bs, st, u.end, 1 << 30, nullptr, 0);
+  run_to_count(im.dc, im.ac, bs, st, u.end);
   u.xp = st.p;
   u.xz = st.z;
   u.cnt = st.blocks;
@@ -476,10 +483,10 @@ __global__ __launch_bounds__(HUFF_NT) void jpeg_huff_sync_kernel(const JpegImg* 
       Dec a{u.ep, u.ez, 0}, c{pv.xp, pv.xz, 0};
       bool synced = false;
       while (c.p < u.end) {
-        if (a.p < c.p && a.p < u.end) step<false>(im.dc, im.ac, bs, a, nullptr, 0);
-        else if (c.p < a.p || a.p >= u.end) step<false>(im.dc, im.ac, bs, c, nullptr, 0);
+        if (a.p < c.p && a.p < u.end) step<false>(im.dc, im.ac, bs, a, nullptr);
+        else if (c.p < a.p || a.p >= u.end) step<false>(im.dc, im.ac, bs, c, nullptr);
         else if (a.z == c.z) { synced = true; break; }
-        else { step<false>(im.dc, im.ac, bs, a, nullptr, 0); step<false>(im.dc, im.ac, bs, c, nullptr, 0); }
+        else { step<false>(im.dc, im.ac, bs, a, nullptr); step<false>(im.dc, im.ac, bs, c, nullptr); }
       }
       if (synced) {
         u.cnt = u.cnt - a.blocks + c.blocks;        // same path from the meeting point on
@@ -493,30 +500,39 @@ __global__ __launch_bounds__(HUFF_NT) void jpeg_huff_sync_kernel(const JpegImg* 
   out[(size_t)b * ws.max_sub + k] = u;
 }
 
-// per segment: verify the entry/exit chain; re-decode the segment sequentially if a
-// subsequence never synchronised
-__global__ void jpeg_huff_fix_kernel(const JpegImg* __restrict__ imgs, Sub* subs, uint8_t* streams, JpegWs ws) {
-  const int b = blockIdx.y;
+// verify every link of the entry/exit chain (one thread per subsequence) and flag the segments
+// with a broken one: a subsequence that never synchronised within the sync rounds
+__global__ __launch_bounds__(HUFF_NT) void jpeg_huff_check_kernel(const JpegImg* __restrict__ imgs,
+                                                                    const Sub* __restrict__ subs, int* segbad, JpegWs ws) {
+  const int b = blockIdx.y, k = blockIdx.x * HUFF_NT + threadIdx.x;
   const JpegImg& im = imgs[b];
-  if (im.status != ST_OK) return;
+  if (im.status != ST_OK || k >= im.nsub) return;
+  const Sub* sb = subs + (size_t)b * ws.max_sub;
+  if (!sb[k].first && (sb[k].ep != sb[k - 1].xp || sb[k].ez != sb[k - 1].xz))
+    segbad[(size_t)b * (ws.max_seg + 1) + sb[k].seg] = 1;
+}
+
+// re-decode a flagged segment sequentially (one thread per segment)
+__global__ __launch_bounds__(HUFF_NT) void jpeg_huff_fix_kernel(const JpegImg* __restrict__ imgs, Sub* subs,
+                                                                  const int* __restrict__ segfirst,
+                                                                  const int* __restrict__ segbad, uint8_t* streams,
+                                                                  JpegWs ws) {
+  const int b = blockIdx.y, sgi = blockIdx.x * HUFF_NT + threadIdx.x;
+  const JpegImg& im = imgs[b];
+  if (im.status != ST_OK || sgi >= im.nseg || !segbad[(size_t)b * (ws.max_seg + 1) + sgi]) return;
   Sub* sb = subs + (size_t)b * ws.max_sub;
-  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < im.nsub; k += gridDim.x * blockDim.x) {
-    if (!sb[k].first) continue;
-    bool ok = true;
-    int j = k + 1;
-    for (; j < im.nsub && !sb[j].first; ++j) ok &= sb[j].ep == sb[j - 1].xp && sb[j].ez == sb[j - 1].xz;
-    if (ok) continue;
-    BitSrc bs{stream_of(ws, streams, b)};
-    Dec st{sb[k].start, 0, 0};
-    for (int i = k; i < j; ++i) {
-      sb[i].ep = st.p;
-      sb[i].ez = st.z;
-      st.blocks = 0;
-      run_to<false>(im.dc, im.ac, bs, st, sb[i].end, 1 << 30, nullptr, 0);
-      sb[i].xp = st.p;
-      sb[i].xz = st.z;
-      sb[i].cnt = st.blocks;
-    }
+  const int k0 = segfirst[(size_t)b * (ws.max_seg + 1) + sgi];
+  const int k1 = sgi + 1 < im.nseg ? segfirst[(size_t)b * (ws.max_seg + 1) + sgi + 1] : im.nsub;
+  BitSrc bs{stream_of(ws, streams, b)};
+  Dec st{sb[k0].start, 0, 0};
+  for (int i = k0; i < k1; ++i) {
+    sb[i].ep = st.p;
+    sb[i].ez = st.z;
+    st.blocks = 0;
+    run_to_count(im.dc, im.ac, bs, st, sb[i].end);
+    sb[i].xp = st.p;
+    sb[i].xz = st.z;
+    sb[i].cnt = st.blocks;
   }
 }
 
@@ -536,39 +552,72 @@ __global__ __launch_bounds__(SCAN_NT) void jpeg_blocks_kernel(const JpegImg* __r
     const int c = k < im.nsub ? sb[k].cnt : 0;
     int tot;
     const int e = block_scan_excl(c, sh, tot);
-    if (k < im.nsub) sb[k].blk = carry + e;
+    if (k < im.nsub) sb[k].blkp = carry + e;
     carry += tot;
   }
 }
 
-__global__ void jpeg_blocks_fix_kernel(const JpegImg* __restrict__ imgs, Sub* subs, const int* __restrict__ segblk,
-                                       JpegWs ws) {
-  const int b = blockIdx.y;
+// block index at each entry = the segment's first block + the counts of the segment's earlier
+// subsequences (one thread per subsequence)
+__global__ __launch_bounds__(HUFF_NT) void jpeg_blocks_fix_kernel(const JpegImg* __restrict__ imgs, Sub* subs,
+                                                                    const int* __restrict__ segblk,
+                                                                    const int* __restrict__ segfirst, JpegWs ws) {
+  const int b = blockIdx.y, k = blockIdx.x * HUFF_NT + threadIdx.x;
   const JpegImg& im = imgs[b];
-  if (im.status != ST_OK) return;
+  if (im.status != ST_OK || k >= im.nsub) return;
   Sub* sb = subs + (size_t)b * ws.max_sub;
-  const int* sgb = segblk + (size_t)b * (ws.max_seg + 1);
-  // one thread per segment: walk its subsequences
-  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < im.nsub; k += gridDim.x * blockDim.x) {
-    if (!sb[k].first) continue;
-    const int p0 = sb[k].blk, s0 = sgb[sb[k].seg];
-    for (int j = k; j < im.nsub && (j == k || !sb[j].first); ++j) sb[j].blk = sb[j].blk - p0 + s0;
-  }
+  const int sg = sb[k].seg;
+  const size_t so = (size_t)b * (ws.max_seg + 1) + sg;
+  sb[k].blk = sb[k].blkp - sb[segfirst[so]].blkp + segblk[so];
 }
 
-// decode again from the true entries, writing DC differences and AC coefficients
+// decode again from the true entries, writing DC differences and AC coefficients (natural
+// order) of every block the subsequence owns: each block is assembled in the thread's LDS slot and
+// stored as 8 16-byte pieces; the block in progress at entry (owned from zig-zag position
+// entry z on) and at exit (owned up to exit z) are stored position by position, zeros included,
+// so every coefficient is written exactly once and the buffer needs no clearing
+constexpr int SLOT_LD = 72;                 // int16 per LDS slot row (16-byte aligned, padded)
 __global__ __launch_bounds__(HUFF_NT) void jpeg_huff_write_kernel(const JpegImg* __restrict__ imgs,
                                                                     const Sub* __restrict__ subs,
                                                                     const int* __restrict__ segblk, uint8_t* streams,
                                                                     int16_t* __restrict__ coef, int64_t coef_stride, JpegWs ws) {
+  __shared__ __attribute__((aligned(16))) int16_t slots[HUFF_NT * SLOT_LD];
   const int b = blockIdx.y, k = blockIdx.x * HUFF_NT + threadIdx.x;
   const JpegImg& im = imgs[b];
   if (im.status != ST_OK || k >= im.nsub) return;
   const Sub& u = subs[(size_t)b * ws.max_sub + k];
   const int seg_end = segblk[(size_t)b * (ws.max_seg + 1) + u.seg + 1];
+  const int maxblk = seg_end - u.blk;
+  int16_t* my = slots + threadIdx.x * SLOT_LD;
+  int16_t* cb = coef + (size_t)b * coef_stride;
+  auto clear = [&]() {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) *reinterpret_cast<u32x4*>(my + 8 * i) = u32x4{0, 0, 0, 0};
+  };
+  auto store_range = [&](int blk, int z0, int z1) {          // zig-zag positions [z0, z1)
+    for (int z = z0; z < z1; ++z) cb[(size_t)blk * 64 + c_zz2nat[z]] = my[c_zz2nat[z]];
+  };
   BitSrc bs{stream_of(ws, streams, b)};
   Dec st{u.ep, u.ez, 0};
-  run_to<true>(im.dc, im.ac, bs, st, u.end, seg_end - u.blk, coef + (size_t)b * coef_stride, u.blk);
+  int zstart = st.z;
+  clear();
+  while (st.p < u.end && st.blocks < maxblk) {
+    const int before = st.blocks;
+    step<true>(im.dc, im.ac, bs, st, my);
+    if (st.blocks != before) {                      // block u.blk + before completed
+      const int blk = u.blk + before;
+      if (zstart == 0) {
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          *reinterpret_cast<u32x4*>(cb + (size_t)blk * 64 + 8 * i) = *reinterpret_cast<const u32x4*>(my + 8 * i);
+      } else {
+        store_range(blk, zstart, 64);
+      }
+      clear();
+      zstart = 0;
+    }
+  }
+  if (st.z != 0 && st.blocks < maxblk) store_range(u.blk + st.blocks, zstart, st.z);
 }
 
 // DC: running sum of the differences, reset at every restart (segment): a segmented inclusive
@@ -631,7 +680,10 @@ ISLOW_FIX(F0899, 7373); ISLOW_FIX(F1175, 9633); ISLOW_FIX(F1501, 12299); ISLOW_F
 ISLOW_FIX(F1961, 16069); ISLOW_FIX(F2053, 16819); ISLOW_FIX(F2562, 20995); ISLOW_FIX(F3072, 25172);
 constexpr int CONST_BITS = 13, PASS1_BITS = 2;
 
-SPE_DEV int descale(long long x, int n) { return (int)((x + (1ll << (n - 1))) >> n); }
+// 32-bit arithmetic: for coefficients an 8-bit encoder produces (dequantised |value| < 2^15)
+// every intermediate fits, as in libjpeg-turbo's SIMD islow (16-bit dequantisation, 32-bit
+// pmaddwd products), so the results equal jidctint.c's 64-bit JLONG ones
+SPE_DEV int descale(int x, int n) { return (x + (1 << (n - 1))) >> n; }
 
 // post-IDCT range limit: libjpeg's table indexed by (value & 1023) with CENTERJSAMPLE added
 SPE_DEV uint8_t range_limit(int v) {
@@ -642,24 +694,23 @@ SPE_DEV uint8_t range_limit(int v) {
   return (uint8_t)(i - 896);
 }
 
-SPE_DEV void idct_1d(long long d0, long long d1, long long d2, long long d3, long long d4, long long d5,
-                     long long d6, long long d7, long long out[8]) {
+SPE_DEV void idct_1d(int d0, int d1, int d2, int d3, int d4, int d5, int d6, int d7, int out[8]) {
   // even part
-  long long z2 = d2, z3 = d6;
-  long long z1 = (z2 + z3) * F0541;
-  const long long tmp2e = z1 + z3 * (-F1847);
-  const long long tmp3e = z1 + z2 * F0765;
+  int z2 = d2, z3 = d6;
+  int z1 = (z2 + z3) * F0541;
+  const int tmp2e = z1 + z3 * (-F1847);
+  const int tmp3e = z1 + z2 * F0765;
   z2 = d0; z3 = d4;
-  const long long tmp0e = (z2 + z3) * (1ll << CONST_BITS);
-  const long long tmp1e = (z2 - z3) * (1ll << CONST_BITS);
-  const long long tmp10 = tmp0e + tmp3e, tmp13 = tmp0e - tmp3e, tmp11 = tmp1e + tmp2e, tmp12 = tmp1e - tmp2e;
+  const int tmp0e = (z2 + z3) * (1 << CONST_BITS);
+  const int tmp1e = (z2 - z3) * (1 << CONST_BITS);
+  const int tmp10 = tmp0e + tmp3e, tmp13 = tmp0e - tmp3e, tmp11 = tmp1e + tmp2e, tmp12 = tmp1e - tmp2e;
   // odd part
-  long long tmp0 = d7, tmp1 = d5, tmp2 = d3, tmp3 = d1;
+  int tmp0 = d7, tmp1 = d5, tmp2 = d3, tmp3 = d1;
   z1 = tmp0 + tmp3;
   z2 = tmp1 + tmp2;
   z3 = tmp0 + tmp2;
-  long long z4 = tmp1 + tmp3;
-  const long long z5 = (z3 + z4) * F1175;
+  int z4 = tmp1 + tmp3;
+  const int z5 = (z3 + z4) * F1175;
   tmp0 = tmp0 * F0298;
   tmp1 = tmp1 * F2053;
   tmp2 = tmp2 * F3072;
@@ -714,7 +765,7 @@ __global__ __launch_bounds__(256) void jpeg_idct_kernel(const JpegImg* __restric
   // pass 1: columns
 #pragma unroll
   for (int c = 0; c < 8; ++c) {
-    long long o[8];
+    int o[8];
     idct_1d(q[c], q[8 + c], q[16 + c], q[24 + c], q[32 + c], q[40 + c], q[48 + c], q[56 + c], o);
 #pragma unroll
     for (int r = 0; r < 8; ++r) ws[8 * r + c] = descale(o[r], CONST_BITS - PASS1_BITS);
@@ -722,7 +773,7 @@ __global__ __launch_bounds__(256) void jpeg_idct_kernel(const JpegImg* __restric
   // pass 2: rows
 #pragma unroll
   for (int r = 0; r < 8; ++r) {
-    long long o[8];
+    int o[8];
     const int* w = ws + 8 * r;
     idct_1d(w[0], w[1], w[2], w[3], w[4], w[5], w[6], w[7], o);
     const int y = by * 8 + r;
@@ -753,6 +804,8 @@ JpegWs plan(int B, int H, int W, int64_t max_bytes) {
   w.subs = take(sizeof(Sub) * (size_t)B * w.max_sub * 2);     // two buffers for the sync rounds
   w.segblk = take(sizeof(int) * (size_t)B * (w.max_seg + 1));
   w.segstart = take(sizeof(int) * (size_t)B * (w.max_seg + 1));
+  w.segfirst = take(sizeof(int) * (size_t)B * (w.max_seg + 1));
+  w.segbad = take(sizeof(int) * (size_t)B * (w.max_seg + 1));
   w.stream = take((size_t)B * w.stream_stride);
   w.coef = take((size_t)B * nblocks * 64 * 2);
   w.total = off;
@@ -790,23 +843,26 @@ int spe_jpeg_decode(void* stream, const uint8_t* data, const int64_t* offsets, c
   const int64_t cstride = (int64_t)nblocks * 64;
   hipLaunchKernelGGL(jpeg_parse_kernel, dim3((batch + 63) / 64), dim3(64), 0, s, data, offsets, sizes, batch, height,
                      width, max_bytes_per_image, imgs);
+  int* segfirst = (int*)(base + w.segfirst);
+  int* segbad = (int*)(base + w.segbad);
   hipLaunchKernelGGL(jpeg_unstuff_kernel, dim3(batch), dim3(UNSTUFF_NT), 0, s, data, offsets, sizes, imgs, subs0, segblk,
-                     segstart, streams, w);
+                     segstart, segfirst, segbad, streams, w);
   const dim3 sg((w.max_sub + HUFF_NT - 1) / HUFF_NT, batch);
+  const dim3 gseg((w.max_seg + HUFF_NT - 1) / HUFF_NT, batch);
   hipLaunchKernelGGL(jpeg_huff_spec_kernel, sg, dim3(HUFF_NT), 0, s, imgs, subs0, streams, w);
-  // two sync rounds (ping-pong), then the per-segment check / sequential repair
+  // two sync rounds (ping-pong), then the chain check and the sequential repair of any segment
+  // that did not synchronise
   hipLaunchKernelGGL(jpeg_huff_sync_kernel, sg, dim3(HUFF_NT), 0, s, imgs, subs0, subs1, streams, w);
   hipLaunchKernelGGL(jpeg_huff_sync_kernel, sg, dim3(HUFF_NT), 0, s, imgs, subs1, subs0, streams, w);
-  hipLaunchKernelGGL(jpeg_huff_fix_kernel, sg, dim3(HUFF_NT), 0, s, imgs, subs0, streams, w);
+  hipLaunchKernelGGL(jpeg_huff_check_kernel, sg, dim3(HUFF_NT), 0, s, imgs, subs0, segbad, w);
+  hipLaunchKernelGGL(jpeg_huff_fix_kernel, gseg, dim3(HUFF_NT), 0, s, imgs, subs0, segfirst, segbad, streams, w);
   hipLaunchKernelGGL(jpeg_blocks_kernel, dim3(batch), dim3(SCAN_NT), 0, s, imgs, subs0, segblk, w);
-  hipLaunchKernelGGL(jpeg_blocks_fix_kernel, sg, dim3(HUFF_NT), 0, s, imgs, subs0, segblk, w);
-  int e = (int)hipMemsetAsync(coef, 0, (size_t)batch * cstride * 2, s);
-  if (e) return spe_fail(e, "jpeg coefficient clear failed");
+  hipLaunchKernelGGL(jpeg_blocks_fix_kernel, sg, dim3(HUFF_NT), 0, s, imgs, subs0, segblk, segfirst, w);
   hipLaunchKernelGGL(jpeg_huff_write_kernel, sg, dim3(HUFF_NT), 0, s, imgs, subs0, segblk, streams, coef, cstride, w);
   hipLaunchKernelGGL(jpeg_dc_kernel, dim3(batch), dim3(SCAN_NT), 0, s, imgs, coef, cstride);
   hipLaunchKernelGGL(jpeg_idct_kernel, dim3((nblocks + 255) / 256, batch), dim3(256), 0, s, imgs, coef, cstride, frames,
                      height, width, status);
-  e = (int)hipGetLastError();
+  const int e = (int)hipGetLastError();
   if (e) return spe_fail(e, "jpeg launch failed");
   return 0;
 }
