@@ -32,6 +32,7 @@
 #include "../../include/spe.h"
 
 #include <climits>
+#include <cstddef>
 #include <string>
 
 int spe_fail(int code, const std::string& msg);
@@ -73,7 +74,8 @@ struct Sub {                            // one subsequence of one segment
 
 struct JpegWs {                         // device workspace carve-up (byte offsets)
   size_t imgs, subs, segblk, segstart, segfirst, segbad, stream, coef;
-  int max_sub, max_seg, stream_stride;
+  int max_sub, max_seg, stream_stride, max_tiles;
+  size_t tiles;
   size_t total;
 };
 
@@ -250,91 +252,162 @@ SPE_DEV int block_scan_excl(int v, int* sh, int& total) {   // SCAN/UNSTUFF_NT t
   return base + x - v;
 }
 
-// One workgroup per image sweeps the entropy-coded data in tiles of UNSTUFF_NT x 16 bytes: each
-// thread classifies 16 consecutive bytes (coalesced across the wave), one workgroup scan of
-// (kept, restart) counts places them, and the sweep stops at the tile holding the terminating
-// marker.  Then the segments (restart intervals) are cut into subsequences.
-__global__ __launch_bounds__(UNSTUFF_NT) void jpeg_unstuff_kernel(const uint8_t* __restrict__ data,
-                                                                    const int64_t* __restrict__ offs,
-                                                                    const int64_t* __restrict__ sizes, JpegImg* imgs,
-                                                                    Sub* __restrict__ subs, int* __restrict__ segblk,
-                                                                    int* __restrict__ segstart, int* __restrict__ segfirst,
-                                                                    int* __restrict__ segbad, uint8_t* __restrict__ streams,
-                                                                    JpegWs ws) {
+// Unstuffing runs over tiles of UNSTUFF_NT x 16 bytes, one workgroup per (tile, image): each
+// thread classifies 16 consecutive bytes (coalesced across the wave).  Pass 1 counts the kept
+// bytes and restart markers of every tile up to the tile's first terminating marker; a per-image
+// scan over the tiles (up to the first tile holding a terminating marker) gives each tile's
+// output offset; pass 2 re-classifies and writes.  Then the segments (restart intervals) are
+// cut into subsequences.
+constexpr int UTILE = UNSTUFF_NT * 16;
+
+struct TileBytes {
+  uint8_t v[18];                                    // bytes i0-1 .. i0+16
+  int kind[16];
+  int end;                                          // first terminating marker of this thread, or INT_MAX
+};
+
+SPE_DEV void classify(const uint8_t* d, int n, int i0, TileBytes& t) {
+#pragma unroll
+  for (int e = 0; e < 18; ++e) {
+    const int i = i0 - 1 + e;
+    t.v[e] = i < 0 ? (uint8_t)0 : (i < n ? d[i] : (uint8_t)0xD9);      // past the data: as if EOI
+  }
+  t.end = INT_MAX;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    t.kind[e] = byte_kind(t.v[e], t.v[e + 1], t.v[e + 2], i0 + e > 0);
+    if (i0 + e >= n) t.kind[e] = B_END;
+    if (t.kind[e] == B_END && t.end == INT_MAX) t.end = i0 + e;
+  }
+}
+
+// pass 1: per tile (kept, restarts) before the tile's first terminating marker, and that marker
+__global__ __launch_bounds__(UNSTUFF_NT) void jpeg_unstuff_count_kernel(const uint8_t* __restrict__ data,
+                                                                          const int64_t* __restrict__ offs,
+                                                                          const int64_t* __restrict__ sizes,
+                                                                          const JpegImg* __restrict__ imgs,
+                                                                          int* __restrict__ tiles, JpegWs ws) {
   __shared__ int sh[UNSTUFF_NT / 64];
   __shared__ int s_end;
+  const int b = blockIdx.y, tile = blockIdx.x, tid = threadIdx.x;
+  const JpegImg& im = imgs[b];
+  if (im.status != ST_OK) return;
+  const int n = (int)(offs[b] + sizes[b] - im.ecs_off);
+  const int t0 = tile * UTILE;
+  int* tl = tiles + ((size_t)b * ws.max_tiles + tile) * 3;
+  if (t0 >= n) {
+    if (tid == 0) { tl[0] = 0; tl[1] = 0; tl[2] = INT_MAX; }
+    return;
+  }
+  TileBytes t;
+  classify(data + im.ecs_off, n, t0 + tid * 16, t);
+  if (tid == 0) s_end = INT_MAX;
+  __syncthreads();
+  if (t.end != INT_MAX) atomicMin(&s_end, t.end);
+  __syncthreads();
+  const int end = s_end, i0 = t0 + tid * 16;
+  int k = 0, r = 0;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const bool live = i0 + e < end;
+    k += live && t.kind[e] == B_KEEP;
+    r += live && t.kind[e] == B_RST;
+  }
+  int tot;
+  block_scan_excl(k | (r << 16), sh, tot);
+  if (tid == 0) { tl[0] = tot & 0xffff; tl[1] = tot >> 16; tl[2] = end; }
+}
+
+// per image: tile offsets (exclusive scans up to the first tile with a terminating marker)
+__global__ __launch_bounds__(64) void jpeg_unstuff_scan_kernel(const int64_t* __restrict__ offs,
+                                                                 const int64_t* __restrict__ sizes, JpegImg* imgs,
+                                                                 int* __restrict__ tiles, JpegWs ws) {
+  const int b = blockIdx.x;
+  JpegImg& im = imgs[b];
+  if (im.status != ST_OK || threadIdx.x) return;
+  const int n = (int)(offs[b] + sizes[b] - im.ecs_off);
+  const int nt = (n + UTILE - 1) / UTILE;
+  int* tl = tiles + (size_t)b * ws.max_tiles * 3;
+  int kept = 0, rst = 0, last = nt - 1;
+  for (int i = 0; i < nt; ++i) {
+    const int k = tl[3 * i], r = tl[3 * i + 1], e = tl[3 * i + 2];
+    tl[3 * i] = kept;
+    tl[3 * i + 1] = rst;
+    kept += k;
+    rst += r;
+    if (e != INT_MAX) { last = i; break; }
+  }
+  for (int i = last + 1; i < nt; ++i) tl[3 * i + 2] = -1;        // past the end: nothing to write
+  im.ulen = kept;
+  im.nseg = rst + 1;
+  if (rst + 1 > ws.max_seg) im.status = ST_CAPACITY;
+}
+
+// pass 2: write the kept bytes and the restart positions (segment starts)
+__global__ __launch_bounds__(UNSTUFF_NT) void jpeg_unstuff_write_kernel(const uint8_t* __restrict__ data,
+                                                                          const int64_t* __restrict__ offs,
+                                                                          const int64_t* __restrict__ sizes,
+                                                                          const JpegImg* __restrict__ imgs,
+                                                                          const int* __restrict__ tiles,
+                                                                          int* __restrict__ segstart,
+                                                                          uint8_t* __restrict__ streams, JpegWs ws) {
+  __shared__ int sh[UNSTUFF_NT / 64];
+  __shared__ int s_end;
+  const int b = blockIdx.y, tile = blockIdx.x, tid = threadIdx.x;
+  const JpegImg& im = imgs[b];
+  if (im.status != ST_OK) return;
+  const int n = (int)(offs[b] + sizes[b] - im.ecs_off);
+  const int t0 = tile * UTILE;
+  const int* tl = tiles + ((size_t)b * ws.max_tiles + tile) * 3;
+  if (t0 >= n || tl[2] == -1) return;
+  TileBytes t;
+  classify(data + im.ecs_off, n, t0 + tid * 16, t);
+  if (tid == 0) s_end = INT_MAX;
+  __syncthreads();
+  if (t.end != INT_MAX) atomicMin(&s_end, t.end);
+  __syncthreads();
+  const int end = s_end, i0 = t0 + tid * 16;
+  int k = 0, r = 0;
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const bool live = i0 + e < end;
+    k += live && t.kind[e] == B_KEEP;
+    r += live && t.kind[e] == B_RST;
+  }
+  int tot;
+  const int ex = block_scan_excl(k | (r << 16), sh, tot);
+  uint8_t* out = streams + (size_t)b * ws.stream_stride;
+  int* sst = segstart + (size_t)b * (ws.max_seg + 1);
+  int o = tl[0] + (ex & 0xffff), rr = tl[1] + (ex >> 16);
+#pragma unroll
+  for (int e = 0; e < 16; ++e) {
+    const bool live = i0 + e < end;
+    if (live && t.kind[e] == B_KEEP) out[o++] = t.v[e + 1];
+    else if (live && t.kind[e] == B_RST) sst[1 + rr++] = o;
+  }
+}
+
+// segments -> blocks and subsequences (one workgroup per image)
+__global__ __launch_bounds__(UNSTUFF_NT) void jpeg_segments_kernel(JpegImg* imgs, Sub* __restrict__ subs,
+                                                                     int* __restrict__ segblk, int* __restrict__ segstart,
+                                                                     int* __restrict__ segfirst, int* __restrict__ segbad,
+                                                                     uint8_t* __restrict__ streams, JpegWs ws) {
+  __shared__ int sh[UNSTUFF_NT / 64];
   const int b = blockIdx.x, tid = threadIdx.x;
   JpegImg& im = imgs[b];
   if (im.status != ST_OK) return;                   // block-uniform
-  const uint8_t* d = data + im.ecs_off;
-  const int n = (int)(offs[b] + sizes[b] - im.ecs_off);
+  const int nseg = im.nseg, kept = im.ulen;
   uint8_t* out = streams + (size_t)b * ws.stream_stride;
   int* sst = segstart + (size_t)b * (ws.max_seg + 1);
-  constexpr int TILE = UNSTUFF_NT * 16;
-  int kept = 0, rsts = 0;                           // totals before the current tile
-  bool overflow = false;
-  for (int t0 = 0; t0 < n; t0 += TILE) {
-    const int i0 = t0 + tid * 16;
-    uint8_t v[18];                                  // bytes i0-1 .. i0+16
-#pragma unroll
-    for (int e = 0; e < 18; ++e) {
-      const int i = i0 - 1 + e;
-      v[e] = i < 0 ? (uint8_t)0 : (i < n ? d[i] : (uint8_t)0xD9);   // past the data: as if EOI
-    }
-    int kind[16];
-    int myend = INT_MAX;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      kind[e] = byte_kind(v[e], v[e + 1], v[e + 2], i0 + e > 0);
-      if (i0 + e >= n) kind[e] = B_END;
-      if (kind[e] == B_END && myend == INT_MAX) myend = i0 + e;
-    }
-    if (tid == 0) s_end = INT_MAX;
-    __syncthreads();
-    if (myend != INT_MAX) atomicMin(&s_end, myend);
-    __syncthreads();
-    const int end = s_end;
-    int k = 0, r = 0;
-#pragma unroll
-    for (int e = 0; e < 16; ++e) {
-      const bool live = i0 + e < end;
-      k += live && kind[e] == B_KEEP;
-      r += live && kind[e] == B_RST;
-    }
-    int tot;
-    const int ex = block_scan_excl(k | (r << 16), sh, tot);
-    const int ktot = tot & 0xffff, rtot = tot >> 16;
-    if (rsts + rtot + 1 > ws.max_seg) overflow = true;   // uniform
-    if (!overflow) {
-      int o = kept + (ex & 0xffff), rr = rsts + (ex >> 16);
-#pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const bool live = i0 + e < end;
-        if (live && kind[e] == B_KEEP) out[o++] = v[e + 1];
-        else if (live && kind[e] == B_RST) sst[1 + rr++] = o;
-      }
-    }
-    kept += ktot;
-    rsts += rtot;
-    if (end != INT_MAX || overflow) break;          // uniform
-  }
-  if (overflow) {
-    if (tid == 0) im.status = ST_CAPACITY;
-    return;
-  }
-  const int nseg = rsts + 1;
   // zero padding past the data: the Huffman reader peeks up to 8 bytes ahead
   if (tid < 16) out[kept + tid] = 0;
   if (tid == 0) {
     sst[0] = 0;
     sst[nseg] = kept;
-    im.ulen = kept;
-    im.nseg = nseg;
   }
   __syncthreads();
-  // segments -> blocks and subsequences
   const int R = im.restart > 0 ? im.restart : im.nblocks;
-  if (tid == 0 && ((long long)nseg - 1) * R >= im.nblocks) im.status = ST_CORRUPT;   // more intervals than blocks
+  const bool corrupt = ((long long)nseg - 1) * R >= im.nblocks;   // more intervals than blocks
   int* sb = segblk + (size_t)b * (ws.max_seg + 1);
   int* sf = segfirst + (size_t)b * (ws.max_seg + 1);
   Sub* sbs = subs + (size_t)b * ws.max_sub;
@@ -365,10 +438,12 @@ __global__ __launch_bounds__(UNSTUFF_NT) void jpeg_unstuff_kernel(const uint8_t*
     }
     sub_base += stot;
   }
+  __syncthreads();
   if (tid == 0) {
     sb[nseg] = im.nblocks;
     im.nsub = sub_base;
     if (sub_base > ws.max_sub) im.status = ST_CAPACITY;
+    if (corrupt) im.status = ST_CORRUPT;
   }
 }
 
@@ -378,14 +453,27 @@ struct Dec {
 };
 
 struct BitSrc {
-  const uint8_t* s;
-  SPE_DEV uint32_t peek32(int p) const {            // bits p .. p+31, MSB first
-    const uint8_t* q = s + (p >> 3);
-    const uint64_t w = ((uint64_t)q[0] << 32) | ((uint64_t)q[1] << 24) | ((uint64_t)q[2] << 16) |
-                       ((uint64_t)q[3] << 8) | (uint64_t)q[4];
-    return (uint32_t)(w >> (8 - (p & 7)));
+  const uint8_t* s;                                 // 256-byte aligned, 16 bytes of zero padding
+  SPE_DEV uint32_t peek32(int p) const {            // bits p .. p+31, MSB first: two aligned words
+    const uint32_t* q = reinterpret_cast<const uint32_t*>(s) + (p >> 5);
+    const uint64_t w = ((uint64_t)__builtin_bswap32(q[0]) << 32) | __builtin_bswap32(q[1]);
+    return (uint32_t)(w >> (32 - (p & 31)));
   }
 };
+
+// the image's two Huffman tables, copied into LDS by the workgroup (every workgroup of the
+// Huffman kernels decodes subsequences of one image)
+struct Tabs {
+  HuffTab dc, ac;
+};
+SPE_DEV const Tabs& load_tabs(const JpegImg& im, Tabs* sh) {
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(&im.dc);
+  uint32_t* dst = reinterpret_cast<uint32_t*>(sh);
+  static_assert(sizeof(Tabs) % 4 == 0 && offsetof(JpegImg, ac) == offsetof(JpegImg, dc) + sizeof(HuffTab), "layout");
+  for (int i = threadIdx.x; i < (int)(sizeof(Tabs) / 4); i += blockDim.x) dst[i] = src[i];
+  __syncthreads();
+  return *sh;
+}
 
 // decode one symbol: returns the symbol, advances p by its code length
 SPE_DEV int huff_sym(const HuffTab& t, uint32_t pk, int& len) {
@@ -455,13 +543,16 @@ constexpr int HUFF_NT = 256;
 // speculative decode of every subsequence from its entry (subsequence start, block start)
 __global__ __launch_bounds__(HUFF_NT) void jpeg_huff_spec_kernel(const JpegImg* __restrict__ imgs, Sub* subs,
                                                                    uint8_t* streams, JpegWs ws) {
+  __shared__ Tabs tabs;
   const int b = blockIdx.y, k = blockIdx.x * HUFF_NT + threadIdx.x;
   const JpegImg& im = imgs[b];
-  if (im.status != ST_OK || k >= im.nsub) return;
+  if (im.status != ST_OK || blockIdx.x * HUFF_NT >= im.nsub) return;     // workgroup-uniform
+  const Tabs& t = load_tabs(im, &tabs);
+  if (k >= im.nsub) return;
   Sub& u = subs[(size_t)b * ws.max_sub + k];
   BitSrc bs{stream_of(ws, streams, b)};
   Dec st{u.ep, u.ez, 0};
-  run_to_count(im.dc, im.ac, bs, st, u.end);
+  run_to_count(t.dc, t.ac, bs, st, u.end);
   u.xp = st.p;
   u.xz = st.z;
   u.cnt = st.blocks;
@@ -471,9 +562,12 @@ __global__ __launch_bounds__(HUFF_NT) void jpeg_huff_spec_kernel(const JpegImg* 
 // lockstep with the decode from its current entry, until they meet
 __global__ __launch_bounds__(HUFF_NT) void jpeg_huff_sync_kernel(const JpegImg* __restrict__ imgs, const Sub* __restrict__ in,
                                                                    Sub* __restrict__ out, uint8_t* streams, JpegWs ws) {
+  __shared__ Tabs tabs;
   const int b = blockIdx.y, k = blockIdx.x * HUFF_NT + threadIdx.x;
   const JpegImg& im = imgs[b];
-  if (im.status != ST_OK || k >= im.nsub) return;
+  if (im.status != ST_OK || blockIdx.x * HUFF_NT >= im.nsub) return;     // workgroup-uniform
+  const Tabs& t = load_tabs(im, &tabs);
+  if (k >= im.nsub) return;
   const Sub* ib = in + (size_t)b * ws.max_sub;
   Sub u = ib[k];
   if (!u.first) {
@@ -483,10 +577,10 @@ __global__ __launch_bounds__(HUFF_NT) void jpeg_huff_sync_kernel(const JpegImg* 
       Dec a{u.ep, u.ez, 0}, c{pv.xp, pv.xz, 0};
       bool synced = false;
       while (c.p < u.end) {
-        if (a.p < c.p && a.p < u.end) step<false>(im.dc, im.ac, bs, a, nullptr);
-        else if (c.p < a.p || a.p >= u.end) step<false>(im.dc, im.ac, bs, c, nullptr);
+        if (a.p < c.p && a.p < u.end) step<false>(t.dc, t.ac, bs, a, nullptr);
+        else if (c.p < a.p || a.p >= u.end) step<false>(t.dc, t.ac, bs, c, nullptr);
         else if (a.z == c.z) { synced = true; break; }
-        else { step<false>(im.dc, im.ac, bs, a, nullptr); step<false>(im.dc, im.ac, bs, c, nullptr); }
+        else { step<false>(t.dc, t.ac, bs, a, nullptr); step<false>(t.dc, t.ac, bs, c, nullptr); }
       }
       if (synced) {
         u.cnt = u.cnt - a.blocks + c.blocks;        // same path from the meeting point on
@@ -582,9 +676,12 @@ __global__ __launch_bounds__(HUFF_NT) void jpeg_huff_write_kernel(const JpegImg*
                                                                     const int* __restrict__ segblk, uint8_t* streams,
                                                                     int16_t* __restrict__ coef, int64_t coef_stride, JpegWs ws) {
   __shared__ __attribute__((aligned(16))) int16_t slots[HUFF_NT * SLOT_LD];
+  __shared__ Tabs tabs;
   const int b = blockIdx.y, k = blockIdx.x * HUFF_NT + threadIdx.x;
   const JpegImg& im = imgs[b];
-  if (im.status != ST_OK || k >= im.nsub) return;
+  if (im.status != ST_OK || blockIdx.x * HUFF_NT >= im.nsub) return;     // workgroup-uniform
+  const Tabs& t = load_tabs(im, &tabs);
+  if (k >= im.nsub) return;
   const Sub& u = subs[(size_t)b * ws.max_sub + k];
   const int seg_end = segblk[(size_t)b * (ws.max_seg + 1) + u.seg + 1];
   const int maxblk = seg_end - u.blk;
@@ -603,7 +700,7 @@ __global__ __launch_bounds__(HUFF_NT) void jpeg_huff_write_kernel(const JpegImg*
   clear();
   while (st.p < u.end && st.blocks < maxblk) {
     const int before = st.blocks;
-    step<true>(im.dc, im.ac, bs, st, my);
+    step<true>(t.dc, t.ac, bs, st, my);
     if (st.blocks != before) {                      // block u.blk + before completed
       const int blk = u.blk + before;
       if (zstart == 0) {
@@ -798,6 +895,7 @@ JpegWs plan(int B, int H, int W, int64_t max_bytes) {
   w.max_seg = nblocks + 1;
   w.max_sub = (int)((max_bytes * 8 + SUBBITS - 1) / SUBBITS) + w.max_seg + 1;
   w.stream_stride = (int)((max_bytes + 64 + 255) / 256 * 256);
+  w.max_tiles = (int)((max_bytes + UTILE - 1) / UTILE);
   size_t off = 0;
   auto take = [&](size_t bytes) { size_t o = off; off += (bytes + 255) / 256 * 256; return o; };
   w.imgs = take(sizeof(JpegImg) * (size_t)B);
@@ -806,6 +904,7 @@ JpegWs plan(int B, int H, int W, int64_t max_bytes) {
   w.segstart = take(sizeof(int) * (size_t)B * (w.max_seg + 1));
   w.segfirst = take(sizeof(int) * (size_t)B * (w.max_seg + 1));
   w.segbad = take(sizeof(int) * (size_t)B * (w.max_seg + 1));
+  w.tiles = take(sizeof(int) * 3 * (size_t)B * w.max_tiles);
   w.stream = take((size_t)B * w.stream_stride);
   w.coef = take((size_t)B * nblocks * 64 * 2);
   w.total = off;
@@ -845,8 +944,14 @@ int spe_jpeg_decode(void* stream, const uint8_t* data, const int64_t* offsets, c
                      width, max_bytes_per_image, imgs);
   int* segfirst = (int*)(base + w.segfirst);
   int* segbad = (int*)(base + w.segbad);
-  hipLaunchKernelGGL(jpeg_unstuff_kernel, dim3(batch), dim3(UNSTUFF_NT), 0, s, data, offsets, sizes, imgs, subs0, segblk,
-                     segstart, segfirst, segbad, streams, w);
+  int* tiles = (int*)(base + w.tiles);
+  const dim3 gt(w.max_tiles, batch);
+  hipLaunchKernelGGL(jpeg_unstuff_count_kernel, gt, dim3(UNSTUFF_NT), 0, s, data, offsets, sizes, imgs, tiles, w);
+  hipLaunchKernelGGL(jpeg_unstuff_scan_kernel, dim3(batch), dim3(64), 0, s, offsets, sizes, imgs, tiles, w);
+  hipLaunchKernelGGL(jpeg_unstuff_write_kernel, gt, dim3(UNSTUFF_NT), 0, s, data, offsets, sizes, imgs, tiles, segstart,
+                     streams, w);
+  hipLaunchKernelGGL(jpeg_segments_kernel, dim3(batch), dim3(UNSTUFF_NT), 0, s, imgs, subs0, segblk, segstart, segfirst,
+                     segbad, streams, w);
   const dim3 sg((w.max_sub + HUFF_NT - 1) / HUFF_NT, batch);
   const dim3 gseg((w.max_seg + HUFF_NT - 1) / HUFF_NT, batch);
   hipLaunchKernelGGL(jpeg_huff_spec_kernel, sg, dim3(HUFF_NT), 0, s, imgs, subs0, streams, w);
