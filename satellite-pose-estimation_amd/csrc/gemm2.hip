@@ -899,6 +899,10 @@ int spe_launch_gemm2(const GemmArgs& g, int mode, hipStream_t s) {
   if (g.K % 8 || g.ldb % 64 || g.lda % 8 || (mode == GEMM_CONV && g.Cin % 8 && !pairs)) return 1;
   if (g.out_f32 ? (g.ldc % 4) : (g.ldc % 8)) return 1;
   if (g.R && g.ldr % 8) return 1;
+  if (mode == GEMM_CONV) {
+    const int rc = spe_launch_pconv(g, s);         // 3x3 stride-1 convs: patch-staged kernel (pconv.hip)
+    if (rc != 1) return rc;
+  }
   {
     const int rc = spe_launch_sgemm(g, mode, s);   // short-K streaming kernel (gemm_stream.hip)
     if (rc != 1) return rc;

@@ -53,8 +53,10 @@ __device__ __forceinline__ void conv_k_decode(int k, int Cin, int KW, int taps, 
 }
 int spe_launch_gemm2(const GemmArgs& g, int mode, hipStream_t s);   // 1 = not applicable
 int spe_launch_sgemm(const GemmArgs& g, int mode, hipStream_t s);   // 1 = not applicable
+int spe_launch_pconv(const GemmArgs& g, hipStream_t s);             // 1 = not applicable (pconv.hip)
 int spe_cu_count();               // CUs of the current device (cached; 256 on MI355X)
-// kernel family of this thread's last spe_launch_gemm: 0 gemm.hip, 1 gemm2.hip, 2 gemm_stream.hip
+// kernel family of this thread's last spe_launch_gemm: 0 gemm.hip, 1 gemm2.hip, 2 gemm_stream.hip,
+// 3 pconv.hip
 extern thread_local int spe_gemm_last_path;
 
 struct AttnArgs {

@@ -14,10 +14,10 @@ import os
 
 def short(name):
     n = name.replace("(anonymous namespace)::", "")
-    for key in ("gemm_kernel", "attn_bf16", "attn_f32", "ffn_ln", "layernorm", "heads", "pnp_kernel",
+    for key in ("sgemm_kernel", "gemm2_kernel", "gemm_kernel", "ffn_pipe_kernel", "attn_bf16", "attn_f32", "ffn_ln", "layernorm", "heads", "pnp_kernel",
                 "maxpool", "upsample", "pack_input", "postprocess", "score"):
         if key in n:
-            return n[n.find(key):][:40]
+            return n[n.find(key):].replace("(GemmArgs", "(").split("(")[0][:64]
     return n[-40:]
 
 

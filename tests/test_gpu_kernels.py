@@ -290,6 +290,32 @@ def test_gemm_large_tile_conv(gpu_device, Cin, Cout, k, s, p):
     _close(C, ref.permute(0, 2, 3, 1).reshape(-1, Cout), tol)
 
 
+# patch-staged 3x3 kernel (pconv.hip): stride 1 / pad 1, Cin % 64 == 0, Cout % 64 == 0 (64: one
+# patch buffer, two workgroups per CU; 128-multiples / 256-multiples: double-buffered patches).
+# Shapes: the bench's layer 1-3 convs and neck at small B, odd image sizes (partial blocks in both
+# directions), several column tiles, and the one-buffer patch refetch across channel blocks.
+@pytest.mark.parametrize("B,H,W,Cin,Cout,relu", [(3, 104, 104, 64, 64, 1), (2, 52, 52, 128, 128, 1),
+                                                 (2, 26, 26, 256, 256, 1), (1, 52, 52, 1024, 256, 0),
+                                                 (2, 13, 17, 128, 64, 1), (2, 9, 40, 64, 512, 0),
+                                                 (5, 7, 7, 256, 128, 1), (1, 30, 61, 192, 384, 1)])
+def test_patch_conv3x3(gpu_device, B, H, W, Cin, Cout, relu):
+    _, dt, tol = DT["bf16"]
+    g = torch.Generator(device="cpu").manual_seed(B * H * W + Cin + Cout)
+    x = torch.randn(B, Cin, H, W, generator=g).to(gpu_device, dt)
+    w = (torch.randn(Cout, Cin, 3, 3, generator=g) / (Cin * 9) ** 0.5).to(gpu_device, dt)
+    bias = torch.randn(Cout, generator=g).to(gpu_device)
+    ref = F.conv2d(x.float(), w.float(), bias, stride=1, padding=1)
+    if relu:
+        ref = torch.relu(ref)
+    K = 9 * Cin
+    Wp = _padded_weight(_pack_conv(w), K, dt)
+    C = torch.full((B * H * W, Cout), float("nan"), dtype=dt, device=gpu_device)
+    _gemm("bf16", 2, x.permute(0, 2, 3, 1).contiguous(), Wp, B * H * W, Cout, K, 0, K, C, Cout, bias=bias, relu=relu,
+          conv=(H, W, Cin, 3, 3, 1, 1))
+    assert _lib.lib().spe_debug_gemm_path() == 3, "expected the patch-staged conv kernel"
+    _close(C, ref.permute(0, 2, 3, 1).reshape(-1, Cout), tol)
+
+
 def test_gemm_large_tile_head_transposed(gpu_device):
     _, dt, tol = DT["bf16"]
     B, T, K, N = 25, 2704, 256, 512
