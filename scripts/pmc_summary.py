@@ -57,7 +57,10 @@ def main():
                 if c in d:
                     line += f" {c[3:]}={d[c] / wc:.2f}"
         if "SQ_VALU_MFMA_BUSY_CYCLES" in d and "GRBM_GUI_ACTIVE" in d:
-            line += f" mfma_busy={d['SQ_VALU_MFMA_BUSY_CYCLES'] / (d['GRBM_GUI_ACTIVE'] * 1024):.2f}"
+            # MFMA-busy cycles per SIMD over the dispatch: GRBM_GUI_ACTIVE sums the 8 XCDs' clocks,
+            # the chip has 1024 SIMDs (MI355X_MICROARCH.md PMC notes)
+            line += f" mfma_busy={d['SQ_VALU_MFMA_BUSY_CYCLES'] / (d['GRBM_GUI_ACTIVE'] / 8 * 1024):.2f}"
+            line += f" clk={d['GRBM_GUI_ACTIVE'] / 8 / d['us'] / 1e3:.2f}GHz"
         if "SQ_LDS_BANK_CONFLICT" in d and "SQ_LDS_IDX_ACTIVE" in d:
             line += f" lds_conf={d['SQ_LDS_BANK_CONFLICT'] / max(d['SQ_LDS_IDX_ACTIVE'], 1):.2f}"
         print(line)
