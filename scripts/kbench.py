@@ -100,6 +100,7 @@ def main():
                  ("cross_k +posW", 0, B * T, 1536, 256, T, None),
                  ("enc.o +res", 0, B * T, 256, 256, -1, None),
                  ("neck s16 3x3", 2, B * T, 256, 9 * 1024, 0, (52, 52, 1024, 3, 3, 1, 1)),
+                 ("neck out 3x3", 2, B * T, 512, 9 * 512, 0, (52, 52, 512, 3, 3, 1, 1)),
                  ("l1 3x3", 2, B * 104 * 104, 64, 9 * 64, 0, (104, 104, 64, 3, 3, 1, 1)),
                  ("l2 3x3", 2, B * T, 128, 9 * 128, 0, (52, 52, 128, 3, 3, 1, 1)),
                  ("l3 3x3", 2, B * 676, 256, 9 * 256, 0, (26, 26, 256, 3, 3, 1, 1)),
