@@ -265,6 +265,10 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
     CK(run_gemm(m, "conv.neck", g, GEMM_CONV, s));
   }
   }
+  if (spe_use_neckfold(m)) {  // input_proj . output_conv as one 3x3 conv 512->256 -> src [B*T, 256]
+    GemmArgs g = conv_args(m->neckip, P(w.cat), B, F, F, P(w.src), d);
+    CK(run_gemm(m, "conv.neck", g, GEMM_CONV, s));
+  } else {
   {  // output_conv 3x3 512->512 + bias
     GemmArgs g = conv_args(m->outc, P(w.cat), B, F, F, P(w.neck), 512);
     CK(run_gemm(m, "conv.neck", g, GEMM_CONV, s));
@@ -272,6 +276,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   {  // input_proj 1x1 512->256 + bias -> src [B*T, 256] (token order h*W+w)
     GemmArgs g = linear_args(m->inproj, P(w.neck), 512, B * T, P(w.src), d);
     CK(run_gemm(m, "gemm.input_proj", g, GEMM_LINEAR, s));
+  }
   }
 
   // ---------------- encoder (REV/models/transformer.py:154-167)

@@ -118,6 +118,7 @@ struct spe_model {
   int upload_err = 0;
   Conv stem, s8, s16, outc, inproj, crossK, crossV;
   Conv s16taps;            // bf16 models: s16_latern as 9 per-tap [256][1024] blocks (spe_use_upconv)
+  Conv neckip;             // input_proj . output_conv as one 3x3 conv 512 -> hidden (spe_use_neckfold)
   std::vector<Block> blocks;
   std::vector<Enc> enc;
   std::vector<Dec> dec;
@@ -147,4 +148,11 @@ inline bool spe_use_xattn(const spe_model* m) {
 inline bool spe_use_upconv(const spe_model* m) {
   return (m->cfg.dtype == SPE_DTYPE_BF16_ || m->x3) && m->cfg.input_size % 16 == 0;
 }
+// bf16 and fp32x3 models fold input_proj (1x1 + bias) into output_conv (3x3 + bias): nothing
+// nonlinear sits between them (REV/models/backbone.py:141, detr_speed.py:81), so
+// input_proj(output_conv(x)) is one 3x3 conv 512 -> hidden_dim with per-tap weights
+// W_ip . W_oc[:, :, kh, kw] and bias W_ip . b_oc + b_ip (folded in double at finalize): half the
+// output_conv multiply-adds, no 512-channel neck output round trip, no input_proj launch.  The
+// exact-f32 parity mode keeps the reference's two convolutions.  SPE_NECK_FOLD=0 disables it.
+bool spe_use_neckfold(const spe_model* m);
 Ws spe_plan(const spe_model* m, int B);

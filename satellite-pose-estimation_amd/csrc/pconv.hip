@@ -24,9 +24,12 @@
 //   each wrap repeated two keys: 14-38 % of LDS cycles were bank conflicts).
 // * Staging: buffer_load ... lds (16 B per lane, 8 rows per wave-instruction); out-of-image taps
 //   and rows past N use an out-of-range offset, which the buffer descriptor returns as zeros.
-// * One barrier per K-step: wait for this wave's loads of step s, barrier (every wave's loads
-//   landed and every wave finished reading step s-1's buffers), then issue step s+1's weights
-//   into the freed stage and multiply step s.
+// * One barrier per K-step, software-pipelined across it: a step's fragments are read from LDS
+//   during the previous step's MFMAs, and the weight DMA of step s+2 is issued at step s's
+//   barrier, so neither an LDS read nor a DMA is waited on right behind a barrier (the form with
+//   the reads after the barrier and half a step of DMA lead ran the MFMA pipe ~35-40 % busy).
+// * Fragment addresses: the A swizzle key does not depend on the fragment, so each (tap, kk)
+//   costs one per-lane offset and one add per fragment.
 // NPB = 1 (Cin = 64, the layer-1 conv2: one channel block, nothing to prefetch) sizes LDS and
 // registers for two workgroups per CU, so one workgroup's patch fetch overlaps the other's work.
 #include "spe_common.h"
@@ -46,18 +49,22 @@ struct PcGeom {
   int TH, TW, nbh, nbw;                     // output block and block counts per image
   int tilesN;                               // N / BN
   int PW, PR;                               // patch row pitch (TW+2) and rows (TH+2)*(TW+2)
-  int abl;                                  // ablation bits (SPE_PCONV_ABL, timing only; 0 in the product)
 };
 
+// s_waitcnt through the builtin (not inline asm), so the compiler's own wait insertion sees it:
+// a pending-unknown counter (e.g. a kernel-argument s_load it issued before an asm wait) makes
+// it fall back to lgkmcnt(0) at the next LDS use.  gfx9 encoding: vmcnt [3:0] + [15:14],
+// expcnt [6:4], lgkmcnt [11:8].
+constexpr int waitcnt_enc(int vm, int lgkm) { return (vm & 15) | ((vm >> 4) << 14) | (7 << 4) | ((lgkm & 15) << 8); }
 template <int N>
-SPE_DEV void wait_vm() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory"); }
+SPE_DEV void wait_vm() { __builtin_amdgcn_s_waitcnt(waitcnt_enc(N, 15)); }
+SPE_DEV void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(waitcnt_enc(63, 0)); }
 
 template <int BM, int BN, int NPB>
 __global__ __launch_bounds__(PNT, NPB == 1 ? 2 : 1) void pconv_kernel(GemmArgs g, PcGeom p) {
   constexpr int WN = BN == 64 ? 1 : BN == 128 ? 2 : 4;
   constexpr int WM = 8 / WN;
   constexpr int TMw = BM / WM, TNw = BN / WN, FM = TMw / 16, FN = TNw / 16;
-  constexpr bool PF = FM <= 6;              // next-tap A prefetch (registers: the 8-fragment tile would spill)
   static_assert(TMw % 16 == 0 && TNw % 16 == 0, "wave tile");
   constexpr int PBYTES = PCAP * 128, WBYTES = BN * 128;
   constexpr int PPW = (PCAP / 8 + 7) / 8;   // patch pieces per wave (upper bound)
@@ -116,16 +123,18 @@ __global__ __launch_bounds__(PNT, NPB == 1 ? 2 : 1) void pconv_kernel(GemmArgs g
     }
   };
 
-  // ---- fragment read addresses.  A fragment i row fr = tile pixel m -> patch row of tap (0, 0).
+  // ---- fragment read addresses.  A fragment i row fr = tile pixel m -> patch row of tap (0, 0),
+  // as a byte offset.  The swizzle key of pixel m at tap (kh, kw) is (m + kh*TW + kw) & 7 and
+  // m = wr*TMw + 16i + fr with TMw % 16 == 0, so the key is (fr + kh*TW + kw) & 7 for every
+  // fragment of the lane: one per-lane offset per (tap, kk) serves all FM fragments.
+  static_assert(TMw % 16 == 0, "key independent of the fragment");
   const int fg = lane >> 4, fr = lane & 15;
-  int pbase[FM], pswz[FM];
+  int pb[FM];
 #pragma unroll
   for (int i = 0; i < FM; ++i) {
     const int m = wr * TMw + 16 * i + fr;
     const int th = m / p.TW, tw = m - th * p.TW;
-    const bool in = th < p.TH;                            // rows past the block read row 0 (discarded)
-    pbase[i] = in ? th * p.PW + tw : 0;
-    pswz[i] = in ? m : 0;
+    pb[i] = th < p.TH ? (th * p.PW + tw) * 128 : 0;       // rows past the block read row 0 (discarded)
   }
   // Weight fragment j, lane row t = fr reads channel 16 * (t >> 2) + 4j + (t & 3) of the wave's
   // 64: the C^T fragment's lane (fg, fr) then holds channels 16 fg + 4j + r, i.e. over its four
@@ -148,14 +157,17 @@ __global__ __launch_bounds__(PNT, NPB == 1 ? 2 : 1) void pconv_kernel(GemmArgs g
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  auto read_a = [&](u32x4* dst, const char* pst, int tap, int kk) {
+  // fragments of step (cb, tap), half kk: A from the patch of cb at the tap's row shift, B from
+  // weight stage ws
+  auto read_step = [&](u32x4* a, u32x4* bw, int cb, int tap, int ws, int kk) {
     const int kh = tap / 3, kw = tap - 3 * (tap / 3);
-    const int toff = kh * p.PW + kw, tswz = kh * p.TW + kw;
+    const int sbase = (NPB == 2 ? (cb & 1) * PBYTES : 0) + (kh * p.PW + kw) * 128;
+    const int t = (((fg ^ ((fr + kh * p.TW + kw) & 7)) << 4) + sbase) ^ (kk << 6);
+    const char* wcur = wst + ws * WBYTES;
 #pragma unroll
-    for (int i = 0; i < FM; ++i) {
-      const int q = pbase[i] + toff;
-      dst[i] = ld16(pst + ((q * 128 + ((fg ^ ((pswz[i] + tswz) & 7)) << 4)) ^ (kk << 6)));
-    }
+    for (int j = 0; j < FN; ++j) bw[j] = ld16(wcur + (brd[j] ^ (kk << 6)));
+#pragma unroll
+    for (int i = 0; i < FM; ++i) a[i] = ld16(smem + pb[i] + t);
   };
   auto mma = [&](const u32x4* af, const u32x4* bf) {
 #pragma unroll
@@ -165,58 +177,58 @@ __global__ __launch_bounds__(PNT, NPB == 1 ? 2 : 1) void pconv_kernel(GemmArgs g
         acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, bf[j]),
                                                             __builtin_bit_cast(bf16x8, af[i]), acc[i][j], 0, 0, 0);
   };
+  auto sync = [&]() {
+    wait_vm<0>();
+    wait_lgkm0();
+    __builtin_amdgcn_s_barrier();
+  };
 
+  // Pipeline.  Step s's fragments are read during iteration s-1, so no MFMA waits on an LDS
+  // read issued behind a barrier; iteration s multiplies kk = 0 of step s, then at the barrier
+  // (every wave's DMA of step s+1 landed, every wave done reading step s's weight stage) issues
+  // step s+2's weights into that stage -- a whole iteration ahead of their use -- reads step
+  // s+1's kk = 0 fragments into the registers the kk = 0 MFMAs just consumed, multiplies kk = 1,
+  // and reads step s+1's kk = 1 fragments.  Two weight stages suffice.
   const int cbs = Cin >> 6, steps = 9 * cbs;
 #pragma unroll
   for (int j = 0; j < PPW; ++j) issue_patch(0, 0, j);
   issue_w(0, 0);
+  issue_w(1, 1);                                          // (steps >= 9)
+  wait_vm<WPW>();                                         // patch 0 + step 0's weights
+  wait_lgkm0();
+  __builtin_amdgcn_s_barrier();
+  u32x4 a0[FM], a1[FM], b0[FN], b1[FN];
+  read_step(a0, b0, 0, 0, 0, 0);
+  read_step(a1, b1, 0, 0, 0, 1);
   int cb = 0, tap = 0;
-  u32x4 a0[FM], a1[FM], an[PF ? FM : 1], b0[FN], b1[FN];
-  bool pre = false;                                       // an holds this step's kk = 0 A fragments
-  for (int s = 0; s < steps; ++s) {
-    wait_vm<0>();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (!(p.abl & 1)) __builtin_amdgcn_s_barrier();
-    const char* pst = smem + (NPB == 2 ? (cb & 1) * PBYTES : 0);
-    const char* wcur = wst + (s & 1) * WBYTES;
-#pragma unroll
-    for (int j = 0; j < FN; ++j) b0[j] = ld16(wcur + brd[j]);
-    if (PF && pre) {
-#pragma unroll
-      for (int i = 0; i < FM; ++i) a0[i] = an[i];
-    } else {
-      read_a(a0, pst, tap, 0);
-    }
-#pragma unroll
-    for (int j = 0; j < FN; ++j) b1[j] = ld16(wcur + (brd[j] ^ 64));
-    read_a(a1, pst, tap, 1);
+  // (the last step is peeled: every back edge then carries the same 10 pending fragment reads,
+  // and the compiler's wait at the top counts only those of the next kk = 0 half)
+  for (int s = 0; s + 1 < steps; ++s) {
     mma(a0, b0);
     __builtin_amdgcn_sched_barrier(0);
-    // the next step's weights into the stage every wave finished reading before the barrier,
-    // issued once this step's first MFMA group is queued
-    if (s + 1 < steps && !(p.abl & 2)) issue_w(s + 1, (s + 1) & 1);
+    int tapn = tap + 1, cbn = cb;
+    if (tapn == 9) { tapn = 0; ++cbn; }
+    sync();
+    if (s + 2 < steps) issue_w(s + 2, s & 1);
     if constexpr (NPB == 2) {
-      if (cb + 1 < cbs) {                                 // next channel block's patch, a piece per tap
+      if (cb + 1 < cbs && tap < PPW) issue_patch(cb + 1, (cb + 1) & 1, tap);   // a piece per tap
+    } else {
+      if (cbn != cb) {                                    // one buffer: refill it once every wave is done
 #pragma unroll
-        for (int j = 0; j < PPW; ++j)
-          if (j == tap) issue_patch(cb + 1, (cb + 1) & 1, j);
+        for (int j = 0; j < PPW; ++j) issue_patch(cbn, 0, j);
+        sync();
       }
     }
-    // the next tap of the same channel block reads the same (complete) patch: its first A
-    // fragments need no barrier
-    pre = PF && tap < 8;
-    if (PF && pre) read_a(an, pst, tap + 1, 0);
+    read_step(a0, b0, cbn, tapn, (s + 1) & 1, 0);
+    __builtin_amdgcn_sched_barrier(0);
     mma(a1, b1);
-    if constexpr (NPB == 1) {
-      if (tap == 8 && cb + 1 < cbs) {
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();                      // every wave done with this patch
-#pragma unroll
-        for (int j = 0; j < PPW; ++j) issue_patch(cb + 1, 0, j);
-      }
-    }
-    if (++tap == 9) { tap = 0; ++cb; }
+    __builtin_amdgcn_sched_barrier(0);
+    read_step(a1, b1, cbn, tapn, (s + 1) & 1, 1);
+    tap = tapn;
+    cb = cbn;
   }
+  mma(a0, b0);
+  mma(a1, b1);
 
   // ---- epilogue: lane owns C[pixel m = 16i + fr][channels nb .. nb + 15] of its wave tile
   const int nb = n0 + wc * TNw + 16 * fg;
@@ -268,7 +280,7 @@ bool choose_block(const GemmArgs& g, int BM, int BN, int slots, PcChoice& best) 
     const int rounds = (int)((tiles + slots - 1) / slots);
     const double halo = (double)(TH + 2) * (TW + 2) / ((double)g.Ho * g.Wo / (nbh * nbw));
     if (!found || rounds < best.rounds || (rounds == best.rounds && halo < best.halo)) {
-      best.geo = PcGeom{TH, TW, nbh, nbw, g.N / BN, TW + 2, (TH + 2) * (TW + 2), 0};
+      best.geo = PcGeom{TH, TW, nbh, nbw, g.N / BN, TW + 2, (TH + 2) * (TW + 2)};
       best.rounds = rounds;
       best.halo = halo;
       found = true;
@@ -278,12 +290,10 @@ bool choose_block(const GemmArgs& g, int BM, int BN, int slots, PcChoice& best) 
 }
 
 template <int BM, int BN, int NPB>
-int launch_pc(const GemmArgs& g, const PcGeom& geo, int abl, hipStream_t s) {
+int launch_pc(const GemmArgs& g, const PcGeom& geo, hipStream_t s) {
   const int B = g.M / (g.Ho * g.Wo);
   const long long tiles = (long long)B * geo.nbh * geo.nbw * geo.tilesN;
-  PcGeom gp = geo;
-  gp.abl = abl;
-  hipLaunchKernelGGL((pconv_kernel<BM, BN, NPB>), dim3((unsigned)tiles), dim3(PNT), 0, s, g, gp);
+  hipLaunchKernelGGL((pconv_kernel<BM, BN, NPB>), dim3((unsigned)tiles), dim3(PNT), 0, s, g, geo);
   spe_gemm_last_path = 3;
   return (int)hipGetLastError();
 }
@@ -293,7 +303,6 @@ int launch_pc(const GemmArgs& g, const PcGeom& geo, int abl, hipStream_t s) {
 // 1 = not a problem for this kernel (the caller takes gemm2 / gemm)
 int spe_launch_pconv(const GemmArgs& g, hipStream_t s) {
   static const int en = [] { const char* e = getenv("SPE_PCONV"); return e ? atoi(e) : 1; }();
-  static const int abl = [] { const char* e = getenv("SPE_PCONV_ABL"); return e ? atoi(e) : 0; }();
   if (!en) return 1;
   if (g.KH != 3 || g.KW != 3 || g.stride != 1 || g.pad != 1 || g.Ho != g.H || g.Wo != g.W) return 1;
   if (g.Cin % 64 || g.N % 64 || g.R || g.act > ACT_RELU || g.res_post || g.out_f32 || g.vt_T > 0 || g.ln_g) return 1;
@@ -305,19 +314,19 @@ int spe_launch_pconv(const GemmArgs& g, hipStream_t s) {
   PcChoice c{};
   if (g.N == 64) {
     if (!choose_block(g, 256, 64, 2 * cus, c)) return 1;
-    return launch_pc<256, 64, 1>(g, c.geo, abl, s);
+    return launch_pc<256, 64, 1>(g, c.geo, s);
   }
   if (g.N % 256 == 0) {
     PcChoice c2{};
     const bool a = choose_block(g, 192, 256, cus, c), bq = choose_block(g, 256, 256, cus, c2);
     if (!a && !bq) return 1;
     // per-tile time ~ BM: compare rounds x BM
-    if (bq && (!a || (long long)c2.rounds * 256 <= (long long)c.rounds * 192)) return launch_pc<256, 256, 2>(g, c2.geo, abl, s);
-    return launch_pc<192, 256, 2>(g, c.geo, abl, s);
+    if (bq && (!a || (long long)c2.rounds * 256 <= (long long)c.rounds * 192)) return launch_pc<256, 256, 2>(g, c2.geo, s);
+    return launch_pc<192, 256, 2>(g, c.geo, s);
   }
   if (g.N % 128 == 0) {
     if (!choose_block(g, 256, 128, cus, c)) return 1;
-    return launch_pc<256, 128, 2>(g, c.geo, abl, s);
+    return launch_pc<256, 128, 2>(g, c.geo, s);
   }
   return 1;
 }

@@ -232,6 +232,11 @@ float* upload_transposed(spe_model* m, const std::string& k, int out, int in) {
   return upload_f32(m, t.data(), t.size());
 }
 
+bool spe_use_neckfold(const spe_model* m) {
+  static const int on = [] { const char* e = getenv("SPE_NECK_FOLD"); return e ? atoi(e) : 1; }();
+  return on && (m->cfg.dtype == SPE_DTYPE_BF16_ || m->x3);
+}
+
 namespace {
 
 // sine position table for an all-valid mask (REV/models/position_encoding.py:30-53),
@@ -390,6 +395,33 @@ int build_device(spe_model* m) {
   }
   m->outc = make_conv(m, "backbone.0.output_conv.weight", "", "backbone.0.output_conv.bias", 0, 1, 1);
   m->inproj = make_conv(m, "input_proj.weight", "", "input_proj.bias", 0, 1, 0);
+  m->neckip = Conv{};
+  if (spe_use_neckfold(m)) {
+    const auto so = param_shape(m, "backbone.0.output_conv.weight");   // [512][512][3][3]
+    const auto sp = param_shape(m, "input_proj.weight");                // [hidden][512][1][1]
+    const int cm = (int)so[0], ci_n = (int)so[1], co_n = (int)sp[0], taps = (int)(so[2] * so[3]);
+    std::vector<float> w((size_t)co_n * ci_n * taps, 0.f), bias(co_n, 0.f);
+    if (m->dmem) {
+      const auto& wo = m->host["backbone.0.output_conv.weight"];
+      const auto& bo = m->host["backbone.0.output_conv.bias"];
+      const auto& wp = m->host["input_proj.weight"];
+      const auto& bp = m->host["input_proj.bias"];
+      std::vector<double> acc((size_t)ci_n * taps);
+      for (int co = 0; co < co_n; ++co) {
+        std::fill(acc.begin(), acc.end(), 0.0);
+        double b = bp[co];
+        for (int j = 0; j < cm; ++j) {
+          const double a = wp[(size_t)co * cm + j];
+          const float* src = &wo[(size_t)j * ci_n * taps];
+          for (size_t k = 0; k < acc.size(); ++k) acc[k] += a * src[k];
+          b += a * bo[j];
+        }
+        for (size_t k = 0; k < acc.size(); ++k) w[(size_t)co * ci_n * taps + k] = (float)acc[k];
+        bias[co] = (float)b;
+      }
+    }
+    m->neckip = pack_conv(m, w, bias, co_n, ci_n, (int)so[2], (int)so[3], 0, 1, 1);
+  }
 
   m->enc.clear();
   for (int i = 0; i < c.enc_layers; ++i) {
