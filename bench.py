@@ -83,6 +83,8 @@ def parse():
                    help="skip the post-timing accuracy check of a bf16 run against the fp32 parity mode")
     p.add_argument("--no-overlap", action="store_true",
                    help="run the solver on the forward's stream (default: solver of batch i overlaps the forward of i+1)")
+    p.add_argument("--overlap-backbone", action="store_true",
+                   help="also run batch i's encoder layers on their own stream beside batch i+1's backbone (A/B)")
     p.add_argument("--no-overlap-decode", action="store_true",
                    help="keep each batch's decoder + heads on the forward's stream (default: batch i's "
                         "decoder runs on its own stream beside batch i+1's backbone/encoder, two workspaces)")
@@ -409,7 +411,8 @@ def main():
                              torch.from_numpy(data["quat"]).to(dev), torch.from_numpy(data["tvec"]).to(dev))
     else:
         pipe = PosePipeline(model, solver, B, device=dev, overlap=not args.no_overlap,
-                            overlap_decode=rcfg is None and not (args.no_overlap_decode or args.no_overlap))
+                            overlap_decode=rcfg is None and not (args.no_overlap_decode or args.no_overlap),
+                            overlap_backbone=rcfg is None and args.overlap_backbone and not args.no_overlap)
         data = bench_data(cfg, B, rank) if rcfg is None else synthetic_batch(SpeConfig(input_size=args.size), B, seed=1000 + rank)
         pipe.load(torch.from_numpy(data["images"]).to(dev), torch.from_numpy(data["clip_bbox"]).float().to(dev),
                   torch.from_numpy(data["quat"]).to(dev), torch.from_numpy(data["tvec"]).to(dev))

@@ -150,7 +150,11 @@ int spe_forward(spe_model* m, void* stream, const float* images, int batch, void
  * PostProcess (memory in `workspace` -> out).  spe_forward == both stages in order.  A caller
  * that overlaps batch i's DECODE with batch i+1's ENCODE gives each in-flight batch its own
  * workspace. */
-enum { SPE_STAGE_ENCODE = 1, SPE_STAGE_DECODE = 2 };
+/* ENCODE itself splits in two: BACKBONE = backbone + neck + input_proj (images -> src in the
+ * workspace) and TRANSFORMER = the encoder layers (src -> memory); ENCODE == BACKBONE followed by
+ * TRANSFORMER.  A caller may run batch i's TRANSFORMER beside batch i+1's BACKBONE (the HBM-bound
+ * convolutions beside the VALU-bound attention), each batch with its own workspace. */
+enum { SPE_STAGE_ENCODE = 1, SPE_STAGE_DECODE = 2, SPE_STAGE_BACKBONE = 4, SPE_STAGE_TRANSFORMER = 8 };
 int spe_forward_stages(spe_model* m, void* stream, const float* images, int batch, void* workspace,
                        int64_t workspace_bytes, const spe_forward_outputs* out, int stages);
 

@@ -152,9 +152,11 @@ int spe_forward(spe_model* m, void* stream, const float* images, int B, void* wo
 
 int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, void* workspace, int64_t ws_bytes,
                        const spe_forward_outputs* out, int stages) {
-  if (!m || !workspace || B <= 0 || (stages & ~(SPE_STAGE_ENCODE | SPE_STAGE_DECODE)) || !stages)
+  if (!m || !workspace || B <= 0 ||
+      (stages & ~(SPE_STAGE_ENCODE | SPE_STAGE_DECODE | SPE_STAGE_BACKBONE | SPE_STAGE_TRANSFORMER)) || !stages)
     return fail(SPE_E_ARG, "bad argument");
-  if ((stages & SPE_STAGE_ENCODE) && !images) return fail(SPE_E_ARG, "null images");
+  if (stages & SPE_STAGE_ENCODE) stages |= SPE_STAGE_BACKBONE | SPE_STAGE_TRANSFORMER;
+  if ((stages & SPE_STAGE_BACKBONE) && !images) return fail(SPE_E_ARG, "null images");
   if ((stages & SPE_STAGE_DECODE) && (!out || !out->logits || !out->points)) return fail(SPE_E_ARG, "null outputs");
   if (m->family != 0) return fail(SPE_E_ARG, "not a DETR model (use spe_rtdetr_forward)");
   if (!m->finalized) return fail(SPE_E_STATE, "model not finalized");
@@ -171,7 +173,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   const float scale = 1.0f / std::sqrt(32.0f);
   const int Mt = B * T;
   const bool xa = spe_use_xattn(m);
-  if (stages & SPE_STAGE_ENCODE) {
+  if (stages & SPE_STAGE_BACKBONE) {
   // ---------------- backbone (REV/models/backbone.py:133-149)
   const bool pairs = m->stem.Cin == 4;                 // bf16: pair-packed stem (registry.cpp)
   if (pairs)
@@ -278,6 +280,8 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
     CK(run_gemm(m, "gemm.input_proj", g, GEMM_LINEAR, s));
   }
   }
+  }  // SPE_STAGE_BACKBONE
+  if (stages & SPE_STAGE_TRANSFORMER) {
 
   // ---------------- encoder (REV/models/transformer.py:154-167)
   // fp16 encoder attention operands (bf16 models, attn_dtype = SPE_DTYPE_F16_): the q/k and V^T
@@ -360,7 +364,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   }
   }
 
-  }  // SPE_STAGE_ENCODE
+  }  // SPE_STAGE_TRANSFORMER
   if (!(stages & SPE_STAGE_DECODE)) return 0;
 
   // ---------------- decoder (REV/models/transformer.py:100-129,218-239)

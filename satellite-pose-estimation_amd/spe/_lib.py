@@ -29,7 +29,7 @@ F = ctypes.c_float
 D = ctypes.c_double
 
 SPE_DTYPE_BF16, SPE_DTYPE_F32, SPE_DTYPE_F16, SPE_DTYPE_F32X3 = 0, 1, 2, 4
-SPE_STAGE_ENCODE, SPE_STAGE_DECODE = 1, 2
+SPE_STAGE_ENCODE, SPE_STAGE_DECODE, SPE_STAGE_BACKBONE, SPE_STAGE_TRANSFORMER = 1, 2, 4, 8
 SPE_PNP_EPNP, SPE_PNP_RANSAC_P3P_LM, SPE_PNP_EPNP_RANSAC_SIGMA, SPE_PNP_EPNP_LM = 0, 1, 2, 3
 SPE_PNP_OK, SPE_PNP_NO_FG, SPE_PNP_CV_ERROR, SPE_PNP_RANSAC_FALLBACK, SPE_PNP_UNPINNED = 0, 1, 2, 3, 4
 

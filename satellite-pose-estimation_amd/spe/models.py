@@ -127,11 +127,15 @@ class DETR(nn.Module):
                                 _lib.ptr(out.get("hs")), _lib.ptr(aux_l), _lib.ptr(aux_p))
         return out, o
 
-    def encode(self, images, ws, stream=None):
-        """Encode stage (backbone, neck, input_proj, encoder): images -> memory kept in `ws`."""
-        B = images.shape[0]
+    def encode(self, images, ws, stream=None, part=None, B=None):
+        """Encode stage (backbone, neck, input_proj, encoder): images -> memory kept in `ws`.
+        part="backbone": up to input_proj (images -> src in `ws`); part="transformer": the
+        encoder layers over the src a backbone part left in `ws` (images may be None, B given)."""
+        stage = {None: _lib.SPE_STAGE_ENCODE, "backbone": _lib.SPE_STAGE_BACKBONE,
+                 "transformer": _lib.SPE_STAGE_TRANSFORMER}[part]
+        B = images.shape[0] if images is not None else int(B)
         _lib.check(_lib.lib().spe_forward_stages(self._h, _lib.stream_ptr(stream), _lib.ptr(images), B, _lib.ptr(ws),
-                                                 ws.numel(), None, _lib.SPE_STAGE_ENCODE), "spe_forward_stages")
+                                                 ws.numel(), None, stage), "spe_forward_stages")
 
     def decode(self, B, ws, clip_bbox=None, stream=None, return_hs=False):
         """Decode stage (decoder, heads, fused PostProcess) of the memory an encode() left in `ws`."""

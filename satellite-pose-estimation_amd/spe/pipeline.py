@@ -18,7 +18,7 @@ from .speed_eval import device_speed_score
 class PosePipeline:
     def __init__(self, model: DETR, solver: PoseSolver, batch: int, device="cuda", use_graph: bool = False,
                  self_assess: bool = True, overlap: bool = False, raw_frames=None, overlap_decode: bool = False,
-                 jpeg_max_bytes: int = 0):
+                 jpeg_max_bytes: int = 0, overlap_backbone: bool = False):
         self.model, self.solver, self.B = model, solver, batch
         self.self_assess = self_assess
         # overlap: the solver / score / self-assessment of batch i run on a second HIP stream
@@ -29,7 +29,12 @@ class PosePipeline:
         # (spe_forward_stages) and batch i's decoder + heads run on a third stream beside batch
         # i+1's backbone/encoder; two workspaces alternate between in-flight batches.  The
         # decoder is ~55 launches of few-row kernels that leave most CUs idle on their own.
-        self.overlap_decode = overlap_decode and not use_graph
+        # overlap_backbone (implies overlap_decode): the encode stage splits once more at the
+        # encoder input (SPE_STAGE_BACKBONE / SPE_STAGE_TRANSFORMER): batch i's encoder layers run
+        # on a fourth stream beside batch i+1's backbone -- the VALU-bound attention beside the
+        # HBM-bound convolutions -- with three workspaces rotating between in-flight batches.
+        self.overlap_decode = (overlap_decode or overlap_backbone) and not use_graph
+        self.overlap_backbone = overlap_backbone and self.overlap_decode
         self.overlap = (overlap or self.overlap_decode) and not use_graph
         self.solve_stream = torch.cuda.Stream(device=device) if self.overlap else None
         self.device = torch.device(device)
@@ -45,16 +50,18 @@ class PosePipeline:
             model.workspace(batch, dev)           # sized outside any graph capture
         if self.overlap_decode:
             self.dec_stream = torch.cuda.Stream(device=device)
+            self.enc_stream = torch.cuda.Stream(device=device) if self.overlap_backbone else None
+            self.nslot = 3 if self.overlap_backbone else 2
             # the staged slots own their workspaces: a direct model(...) call or another
             # pipeline on the same model never writes into a slot's encoder memory
-            self.ws2 = [model.new_workspace(batch, dev), model.new_workspace(batch, dev)]
+            self.ws2 = [model.new_workspace(batch, dev) for _ in range(self.nslot)]
             # per-slot snapshots of what the later stages read (a load() for the next batch may
             # overwrite the staging buffers while this batch's decoder / solver still run)
-            self.slot_clip = [torch.zeros(batch, 4, device=dev) for _ in range(2)]
-            self.slot_q = [torch.zeros(batch, 4, dtype=torch.float64, device=dev) for _ in range(2)]
-            self.slot_t = [torch.zeros(batch, 3, dtype=torch.float64, device=dev) for _ in range(2)]
-            self.dec_done = [None, None]
-            self.solve_done = [None, None]
+            self.slot_clip = [torch.zeros(batch, 4, device=dev) for _ in range(self.nslot)]
+            self.slot_q = [torch.zeros(batch, 4, dtype=torch.float64, device=dev) for _ in range(self.nslot)]
+            self.slot_t = [torch.zeros(batch, 3, dtype=torch.float64, device=dev) for _ in range(self.nslot)]
+            self.dec_done = [None] * self.nslot
+            self.solve_done = [None] * self.nslot
             self.calls = 0
         # raw_frames = (H, W, C): each run() starts from uint8 frames + detector boxes resident in
         # HBM (load_frames) and runs the validation transform on the device first
@@ -100,21 +107,29 @@ class PosePipeline:
 
     def _body_staged(self):
         main = torch.cuda.current_stream()
-        slot = self.calls % 2
+        slot = self.calls % self.nslot
         self.calls += 1
         self._decode()
         if self.transform is not None:
             self.transform(self.frames, self.bbox, out=self.pp_out)
         if self.dec_done[slot] is not None:
-            main.wait_event(self.dec_done[slot])      # batch i-2's decoder is done with this workspace
+            main.wait_event(self.dec_done[slot])      # batch i-nslot's decoder is done with this workspace
         if self.solve_done[slot] is not None:
             main.wait_event(self.solve_done[slot])    # ... and its solver / score with the slot's snapshots
         self.slot_clip[slot].copy_(self.clip_bbox)
         self.slot_q[slot].copy_(self.q_gt)
         self.slot_t[slot].copy_(self.t_gt)
-        self.model.encode(self.images, self.ws2[slot], stream=main)
+        if self.overlap_backbone:
+            self.model.encode(self.images, self.ws2[slot], stream=main, part="backbone")
+            e = self.enc_stream
+            e.wait_stream(main)
+            with torch.cuda.stream(e):
+                self.model.encode(None, self.ws2[slot], stream=e, part="transformer", B=self.B)
+        else:
+            self.model.encode(self.images, self.ws2[slot], stream=main)
+            e = main
         d = self.dec_stream
-        d.wait_stream(main)
+        d.wait_stream(e)
         with torch.cuda.stream(d):
             fo = self.model.decode(self.B, self.ws2[slot], clip_bbox=self.slot_clip[slot], stream=d)
             ev = torch.cuda.Event()

@@ -152,18 +152,20 @@ def test_pipeline_from_raw_frames(gpu_device, small_model):
         assert torch.equal(a["poses"][k], b["poses"][k]), k
 
 
-def test_pipeline_overlap_decode_matches_serial(gpu_device, small_model):
+@pytest.mark.parametrize("backbone", [False, True])
+def test_pipeline_overlap_decode_matches_serial(gpu_device, small_model, backbone):
     """Decoder of batch i on its own stream beside the encoder of batch i+1 (two workspaces,
-    per-slot snapshots of clip boxes / ground truth): every batch's poses and scores equal the
-    serial pipeline's, over consecutive batches that reuse both workspace slots."""
+    per-slot snapshots of clip boxes / ground truth) -- and with `backbone`, batch i's encoder
+    layers on a fourth stream beside batch i+1's backbone (three workspaces): every batch's poses
+    and scores equal the serial pipeline's, over consecutive batches that reuse every slot."""
     from spe.pipeline import PosePipeline
     from spe.solver import build_solver
     cfg, w, m = small_model
     B = 8
     solver = build_solver(argparse.Namespace(solver="ransac_p3p_lm", repro=20))
     serial = PosePipeline(m, solver, B, device=gpu_device)
-    staged = PosePipeline(m, solver, B, device=gpu_device, overlap_decode=True)
-    batches = [synthetic_batch(cfg, B, 500 + k) for k in range(4)]
+    staged = PosePipeline(m, solver, B, device=gpu_device, overlap_decode=True, overlap_backbone=backbone)
+    batches = [synthetic_batch(cfg, B, 500 + k) for k in range(7 if backbone else 4)]
     dev = gpu_device
 
     def load(p, b):
