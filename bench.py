@@ -310,6 +310,8 @@ def traffic_for(kind, grid, attn_dtype):
             d = json.load(open(f))
         except Exception:
             continue
+        if not isinstance(d, dict):            # per-kernel counter tables (scripts/pmc_summary.py --json)
+            continue
         if (d.get("kind") == kind and "hbm_bytes_per_launch" in d and grid is not None and d.get("grid") == grid
                 and d.get("attn_dtype", "bf16") == attn_dtype):
             best = d["hbm_bytes_per_launch"]
