@@ -83,8 +83,9 @@ def parse():
                    help="skip the post-timing accuracy check of a bf16 run against the fp32 parity mode")
     p.add_argument("--no-overlap", action="store_true",
                    help="run the solver on the forward's stream (default: solver of batch i overlaps the forward of i+1)")
-    p.add_argument("--overlap-backbone", action="store_true",
-                   help="also run batch i's encoder layers on their own stream beside batch i+1's backbone (A/B)")
+    p.add_argument("--no-overlap-backbone", action="store_true",
+                   help="run batch i's encoder layers on the backbone's stream (default: on their own stream beside "
+                        "batch i+1's backbone, three workspaces)")
     p.add_argument("--no-overlap-decode", action="store_true",
                    help="keep each batch's decoder + heads on the forward's stream (default: batch i's "
                         "decoder runs on its own stream beside batch i+1's backbone/encoder, two workspaces)")
@@ -403,6 +404,7 @@ def main():
             files = [enc(f) for f in data["frames"]]
         pipe = PosePipeline(model, solver, B, device=dev, overlap=not args.no_overlap,
                             overlap_decode=not (args.no_overlap_decode or args.no_overlap), raw_frames=(H, W, 1),
+                            overlap_backbone=not (args.no_overlap_backbone or args.no_overlap_decode or args.no_overlap),
                             jpeg_max_bytes=max(len(f) for f in files) if files else 0)
         if files:
             jpeg_bytes = sum(len(f) for f in files)
@@ -414,7 +416,7 @@ def main():
     else:
         pipe = PosePipeline(model, solver, B, device=dev, overlap=not args.no_overlap,
                             overlap_decode=rcfg is None and not (args.no_overlap_decode or args.no_overlap),
-                            overlap_backbone=rcfg is None and args.overlap_backbone and not args.no_overlap)
+                            overlap_backbone=rcfg is None and not (args.no_overlap_backbone or args.no_overlap_decode or args.no_overlap))
         data = bench_data(cfg, B, rank) if rcfg is None else synthetic_batch(SpeConfig(input_size=args.size), B, seed=1000 + rank)
         pipe.load(torch.from_numpy(data["images"]).to(dev), torch.from_numpy(data["clip_bbox"]).float().to(dev),
                   torch.from_numpy(data["quat"]).to(dev), torch.from_numpy(data["tvec"]).to(dev))
