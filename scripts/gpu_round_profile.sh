@@ -21,8 +21,14 @@ done
 timeout -k 10 600 python bench.py --dtype fp32 --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/${TAG}_bench_fp32.log 2>&1 \
   || { tail -20 gpurun_out/${TAG}_bench_fp32.log; exit 7; }
 tail -1 gpurun_out/${TAG}_bench_fp32.log | cut -c1-160
+timeout -k 10 600 python bench.py --dtype fp32x3 --steps 10 --warmup 2 --no-cpu-baseline > gpurun_out/${TAG}_bench_fp32x3.log 2>&1 \
+  || { tail -20 gpurun_out/${TAG}_bench_fp32x3.log; exit 8; }
+tail -1 gpurun_out/${TAG}_bench_fp32x3.log | cut -c1-160
 for mdl in rtdetr_r18 rtdetr_r50; do
   timeout -k 10 600 python bench.py --model $mdl --steps 20 --warmup 3 --cpu-seconds 12 > gpurun_out/${TAG}_bench_$mdl.log 2>&1 \
     || { tail -20 gpurun_out/${TAG}_bench_$mdl.log; exit 6; }
   tail -1 gpurun_out/${TAG}_bench_$mdl.log | cut -c1-120
 done
+KB="gemm --only 3x3" PROF_TAG=${TAG}_pconv bash scripts/gpu_pmc_sets.sh > gpurun_out/${TAG}_pmc_pconv.txt 2>&1 || { tail -20 gpurun_out/${TAG}_pmc_pconv.txt; exit 9; }
+python3 scripts/pmc_summary.py gpurun_out/pmc_${TAG}_pconv --min-us 20 --json gpurun_out/${TAG}_counters_pconv.json > /dev/null
+tail -6 gpurun_out/${TAG}_pmc_pconv.txt | cut -c1-200
