@@ -534,6 +534,13 @@ def main():
                      "bound": "mfma" if mfma_bound else "hbm", "achieved": achieved,
                      "peak": peak, "unit": unit, "frac": achieved / peak,
                      "traffic": traffic_for(dominant, launch_grid(dominant, B, cfg), args.attn_dtype), "launches": k_n, "avg_launch_ms": avg_ms,
+                     # the timed-region launches share the CUs with the next batch's backbone
+                     # (stream overlap); the per-launch profiled step times each launch between
+                     # events on its stream, the kernel's own rate
+                     "avg_launch_ms_profiled_step": tot[dominant][0] / max(tot[dominant][1], 1),
+                     "frac_profiled_step": ((k_fl if mfma_bound else k_by) / max(k_n, 1)) /
+                                           (tot[dominant][0] / max(tot[dominant][1], 1) * 1e-3) /
+                                           (1e12 if mfma_bound else 1e9) / peak,
                      "algorithmic_flops_per_launch": k_fl / max(k_n, 1),
                      "algorithmic_bytes_per_launch": k_by / max(k_n, 1)},
         "kernel_time_ms_per_step": {k: v[0] for k, v in sorted(tot.items(), key=lambda kv: -kv[1][0])},
