@@ -86,3 +86,21 @@ def test_detr_entry_points_reject_rtdetr_handle():
         assert rc == -1
         assert b"not a DETR model" in L.spe_last_error()
     L.spe_model_destroy(h)
+
+
+def test_forward_stage_flags_validated():
+    """spe_forward_stages accepts ENCODE / DECODE / BACKBONE / TRANSFORMER bits and rejects any
+    other bit, a zero mask, and a BACKBONE stage without images, all before touching the device."""
+    from spe.rtdetr_spec import RtdetrConfig
+    L = _lib.lib()
+    assert (_lib.SPE_STAGE_ENCODE, _lib.SPE_STAGE_DECODE, _lib.SPE_STAGE_BACKBONE, _lib.SPE_STAGE_TRANSFORMER) == (1, 2, 4, 8)
+    r = RtdetrConfig(depth=18, input_size=128)
+    c = _lib.RtdetrConfig(r.depth, r.input_size, r.num_queries, r.dec_layers, r.enc_ff, r.dec_ff, r.csp_hidden,
+                          r.num_classes, _lib.SPE_DTYPE_BF16)
+    h = ctypes.c_void_p()
+    assert L.spe_rtdetr_create(ctypes.byref(c), ctypes.byref(h)) == 0
+    dummy = ctypes.c_void_p(16)
+    for stages, images in ((16, dummy), (0, dummy), (_lib.SPE_STAGE_BACKBONE, None), (_lib.SPE_STAGE_ENCODE, None)):
+        assert L.spe_forward_stages(h, None, images, 1, dummy, 1 << 40, None, stages) == -1
+        assert b"not a DETR model" not in L.spe_last_error()
+    L.spe_model_destroy(h)

@@ -152,6 +152,24 @@ def test_pipeline_from_raw_frames(gpu_device, small_model):
         assert torch.equal(a["poses"][k], b["poses"][k]), k
 
 
+def test_encode_parts_match_forward(gpu_device, small_model):
+    """BACKBONE then TRANSFORMER (spe_forward_stages bits 4, 8) then DECODE in one workspace
+    equals the one-call forward bit for bit."""
+    cfg, w, m = small_model
+    B = 4
+    b = synthetic_batch(cfg, B, 77)
+    x = torch.from_numpy(b["images"]).to(gpu_device)
+    clip = torch.from_numpy(b["clip_bbox"]).float().to(gpu_device)
+    ref = m(x, clip_bbox=clip)
+    ws = m.new_workspace(B, gpu_device)
+    m.encode(x, ws, part="backbone")
+    m.encode(None, ws, part="transformer", B=B)
+    out = m.decode(B, ws, clip_bbox=clip)
+    torch.cuda.synchronize()
+    for k in ("pred_logits", "pred_points", "probs", "points_px"):
+        assert torch.equal(out[k], ref[k]), k
+
+
 @pytest.mark.parametrize("backbone", [False, True])
 def test_pipeline_overlap_decode_matches_serial(gpu_device, small_model, backbone):
     """Decoder of batch i on its own stream beside the encoder of batch i+1 (two workspaces,
