@@ -287,6 +287,14 @@ int spe_debug_xattn(void* stream, const void* q, int ldq, const void* k, int ldk
  * align_corners bilinear x2 upsample, i.e. sum over in-grid taps of the bilinear interpolation
  * of z's tap block.  C % 8 == 0 (bf16) / C % 4 == 0 (fp32). */
 int spe_debug_upconv(void* stream, int dtype, const void* z, void* out, int ldo, int B, int H, int W, int C);
+/* btail (bf16, the layer-1 bottleneck tail fused with the next block's conv1, btail.hip):
+ * y [M][256] = relu(a [M][k1] . w3^T + b3 (+ r [M][256])), z [M][n2] = relu(y . w1p^T + b1) where
+ * w1p [n2][256] holds conv1's columns in spe_debug_btail_perm order; (k1, n2, r) in
+ * {(64, 64, r), (64, 128, r), (128, 64, null)}. */
+int spe_debug_btail(void* stream, const void* a, int lda, int k1, const void* r, const void* w3, int ld3,
+                    const float* b3, void* y, const void* w1p, int ld1, const float* b1, void* z, int n2, int M);
+/* the K-column order btail's second product expects: stored column k holds channel perm(k) */
+int spe_debug_btail_perm(int k);
 
 #ifdef __cplusplus
 }

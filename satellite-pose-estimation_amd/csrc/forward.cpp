@@ -200,26 +200,49 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   H = Hp;
   size_t cur = pool_at;                                 // (w.pool aliases bufA)
   int cin = 64, cur_ld = uld;
+  bool t1_ready = false;                                // this block's conv1 ran in the previous tail
+  // conv3 (+ residual) + relu of block bi and the next block's conv1 as one launch (btail.hip)
+  // when the next block carries permuted conv1 weights (layer-1 outputs, registry.cpp c1p)
+  auto tail = [&](const Block& nb, const void* A, int lda, int k1, const void* R, const Conv& c3, size_t out, int M) {
+    BtailArgs t{};
+    t.A = A; t.lda = lda; t.k1 = k1; t.R = R; t.ldr = 256;
+    t.w3 = c3.w; t.ld3 = c3.Kpad; t.b3 = c3.bias; t.y = P(out); t.ldy = c3.N; t.n1 = c3.N;
+    t.w1 = nb.c1p.w; t.ld1 = nb.c1p.Kpad; t.b1 = nb.c1p.bias; t.z = P(w.t1); t.ldz = nb.c1.N; t.n2 = nb.c1.N;
+    t.M = M;
+    const double flops = 2.0 * M * ((double)c3.N * k1 + (double)nb.c1.N * c3.N);
+    const double bytes = ((double)M * (k1 + c3.N + nb.c1.N) + (R ? (double)M * c3.N : 0.0)) * m->esz;
+    return run_other(m, "conv.1x1", flops, bytes, s, [&] { return spe_launch_btail(t, s); });
+  };
   for (size_t bi = 0; bi < m->blocks.size(); ++bi) {
     const Block& blk = m->blocks[bi];
     const bool fused = bi == 0 && fuse0;
+    const Block* nb = bi + 1 < m->blocks.size() && m->blocks[bi + 1].c1p.w ? &m->blocks[bi + 1] : nullptr;
     // layer1: blocks 0-2, layer2: 3-6 (its output xs8 is kept for the neck), layer3: 7-12
     const size_t outbuf = (bi == 6) ? w.xs8 : (cur == w.bufA ? w.bufB : w.bufA);
     const int Ho = (H + 2 - 3) / blk.stride + 1;
-    {  // conv1 1x1 + bn1 + relu
+    if (!t1_ready) {  // conv1 1x1 + bn1 + relu
       GemmArgs g = linear_args(blk.c1, P(cur), cur_ld, B * H * H, P(w.t1), blk.c1.N);
       g.act = ACT_RELU;
       CK(run_gemm(m, "conv.1x1", g, GEMM_LINEAR, s));
     }
+    t1_ready = false;
     {  // conv2 3x3 (stride on the 3x3, ResNet v1.5) + bn2 + relu
       GemmArgs g = conv_args(blk.c2, P(w.t1), B, H, H, fused ? P(w.ds) : P(w.t2), fused ? uld : blk.c2.N);
       g.act = ACT_RELU;
       CK(run_gemm(m, "conv.3x3", g, GEMM_CONV, s));
     }
     if (fused) {  // relu(W3 t2 + Wds x + b3 + bds) over the concatenation
-      GemmArgs g = linear_args(blk.c3ds, P(w.ds), uld, B * Ho * Ho, P(outbuf), blk.c3ds.N);
-      g.act = ACT_RELU;
-      CK(run_gemm(m, "conv.1x1", g, GEMM_LINEAR, s));
+      int rc = 1;
+      if (nb && blk.c3ds.N == 256) {
+        rc = tail(*nb, P(w.ds), uld, blk.c3ds.K, nullptr, blk.c3ds, outbuf, B * Ho * Ho);
+        if (rc < 0) CK(rc);
+      }
+      if (rc == 1) {
+        GemmArgs g = linear_args(blk.c3ds, P(w.ds), uld, B * Ho * Ho, P(outbuf), blk.c3ds.N);
+        g.act = ACT_RELU;
+        CK(run_gemm(m, "conv.1x1", g, GEMM_LINEAR, s));
+      }
+      t1_ready = rc == 0;
       cin = cur_ld = blk.c3.N;
       H = Ho;
       cur = outbuf;
@@ -236,10 +259,18 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       }
       res = w.ds;
     }
-    {  // conv3 1x1 + bn3 + residual + relu
-      GemmArgs g = linear_args(blk.c3, P(w.t2), blk.c2.N, B * Ho * Ho, P(outbuf), blk.c3.N);
-      g.R = P(res); g.ldr = blk.c3.N; g.act = ACT_RELU;
-      CK(run_gemm(m, "conv.1x1", g, GEMM_LINEAR, s));
+    {  // conv3 1x1 + bn3 + residual + relu (+ the next block's conv1, btail.hip)
+      int rc = 1;
+      if (nb && blk.c3.N == 256) {
+        rc = tail(*nb, P(w.t2), blk.c2.N, blk.c3.K, P(res), blk.c3, outbuf, B * Ho * Ho);
+        if (rc < 0) CK(rc);
+      }
+      if (rc == 1) {
+        GemmArgs g = linear_args(blk.c3, P(w.t2), blk.c2.N, B * Ho * Ho, P(outbuf), blk.c3.N);
+        g.R = P(res); g.ldr = blk.c3.N; g.act = ACT_RELU;
+        CK(run_gemm(m, "conv.1x1", g, GEMM_LINEAR, s));
+      }
+      t1_ready = rc == 0;
     }
     cin = cur_ld = blk.c3.N;
     H = Ho;

@@ -19,6 +19,8 @@ struct Conv {              // conv / linear packed as [N][Kpad] in T, bias fp32
 struct Block {
   Conv c1, c2, c3, ds;
   Conv c3ds;               // bf16, stride-1 first block: [W3 | Wds] over [t2 | x] (K = w + cin), or empty
+  Conv c1p;                // bf16, input = a layer-1 block output: conv1 with K columns in spe_btail_perm
+                           // order, fused into the previous block's tail (btail.hip), or empty
   bool has_ds = false;
   int stride = 1;
 };

@@ -370,6 +370,23 @@ int build_device(spe_model* m) {
           f.bias = upload_f32(m, bias.data(), bias.size());
         }
       }
+      // conv1 of the blocks whose input is a layer-1 block output (blocks 1-3: layer 1 blocks 1
+      // and 2, layer 2 block 0) as the second product of the previous block's fused tail:
+      // columns permuted into spe_btail_perm order (btail.hip)
+      const int gi = li == 0 ? k : (li == 1 && k == 0 ? 3 : -1);
+      if (m->esz == 2 && spe_btail_enabled() && gi >= 1 && blk.c1.K == 256) {
+        std::vector<float> w1, b1;
+        fold_conv(m, p + ".conv1.weight", p + ".bn1", "", w1, b1);
+        const int n = blk.c1.N, K = blk.c1.K;
+        std::vector<float> rows((size_t)n * K, 0.f);
+        if (m->dmem)
+          for (int r = 0; r < n; ++r)
+            for (int c = 0; c < K; ++c) rows[(size_t)r * K + c] = w1[(size_t)r * K + spe_btail_perm(c)];
+        Conv& f = blk.c1p;
+        f.N = n; f.K = K; f.Kpad = pad64(K); f.Cin = K;
+        f.w = upload_rows(m, rows, f.N, f.K, f.Kpad);
+        f.bias = upload_f32(m, b1.data(), b1.size());
+      }
       m->blocks.push_back(blk);
     }
   m->s8 = make_conv(m, "backbone.0.s8_latern.weight", "", "", 0, 1, 0);

@@ -316,6 +316,37 @@ def test_patch_conv3x3(gpu_device, B, H, W, Cin, Cout, relu):
     _close(C, ref.permute(0, 2, 3, 1).reshape(-1, Cout), tol)
 
 
+# fused bottleneck tail (btail.hip): the layer-1 conv3 (+ identity) + relu with the next block's
+# conv1 + relu, against torch fp32 of the two convs with y rounded to bf16 in between (the
+# separate launches' intermediate); row counts off the 16-row tile and off the wave grid.
+@pytest.mark.parametrize("M,k1,n2,res", [(173056, 64, 64, True), (1000, 64, 64, True), (40000, 64, 128, True),
+                                         (16, 128, 64, False), (69217, 128, 64, False)])
+def test_btail(gpu_device, M, k1, n2, res):
+    L = _lib.lib()
+    dt = torch.bfloat16
+    g = torch.Generator(device="cpu").manual_seed(M + k1 + n2)
+    A = torch.randn(M, k1, generator=g).to(gpu_device, dt)
+    R = torch.randn(M, 256, generator=g).to(gpu_device, dt) if res else None
+    W3 = (torch.randn(256, k1, generator=g) / k1 ** 0.5).to(gpu_device, dt)
+    b3 = (0.1 * torch.randn(256, generator=g)).to(gpu_device)
+    W1 = (torch.randn(n2, 256, generator=g) / 16).to(gpu_device, dt)
+    b1 = (0.1 * torch.randn(n2, generator=g)).to(gpu_device)
+    perm = torch.tensor([L.spe_debug_btail_perm(k) for k in range(256)], device=gpu_device)
+    assert sorted(perm.tolist()) == list(range(256))
+    W1p = W1[:, perm].contiguous()
+    Y = torch.full((M, 256), float("nan"), dtype=dt, device=gpu_device)
+    Z = torch.full((M, n2), float("nan"), dtype=dt, device=gpu_device)
+    rc = L.spe_debug_btail(None, _p(A), k1, k1, _p(R), _p(_padded_weight(W3, 64 * ((k1 + 63) // 64), dt)),
+                           64 * ((k1 + 63) // 64), _p(b3), _p(Y), _p(W1p), 256, _p(b1), _p(Z), n2, M)
+    assert rc == 0, L.spe_last_error()
+    torch.cuda.synchronize()
+    yref = A.float() @ W3.float().t() + b3 + (R.float() if res else 0)
+    yref = torch.relu(yref)
+    _close(Y, yref, DT["bf16"][2])
+    zref = torch.relu(Y.float() @ W1.float().t() + b1)
+    _close(Z, zref, DT["bf16"][2])
+
+
 def test_gemm_large_tile_head_transposed(gpu_device):
     _, dt, tol = DT["bf16"]
     B, T, K, N = 25, 2704, 256, 512
