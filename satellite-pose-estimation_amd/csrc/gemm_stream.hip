@@ -356,6 +356,9 @@ int spe_launch_sgemm(const GemmArgs& g, int mode, hipStream_t s) {
     case 128:
       if (g.N == 64) return launch_kbn<128, 64, 1, 2, 4, 1, 2, 4>(g, s);
       if (g.N == 128) return launch_kbn<128, 128, 1, 2, 4, 1, 2, 2>(g, s);
+      // the layer-2 conv3 + identity (N = 512): 0.126 -> 0.115 ms per launch at B = 64 against
+      // gemm2's 256-row tiles (kbench); without a residual gemm2 stays faster
+      if (g.N % 256 == 0 && g.R) return launch_kbn<128, 256, 1, 2, 2, 1, 2, 2>(g, s);
       return 1;
     case 256:
       if (g.N == 64) return launch_kbn<256, 64, 1, 2, 4, 1, 2, 4>(g, s);
