@@ -253,7 +253,10 @@ int spe_model_profile_get(const spe_model* m, int i, char* kind, int kind_len, d
  * vt_T > 0 stores head-transposed C[((n/256)*vt_B + m/vt_T)*256 + n%256][m%vt_T]; r_period > 0
  * reads the residual row-periodically, R[(m % r_period)*ldr + n].  bf16 problems that fill the chip
  * with 256-row tiles run the direct-to-LDS kernel (gemm2.hip), the rest the 128x128 kernel.
- * attention: per (b,h) softmax(scale Q K^T) V with Q/K rows b*T+i at column h*32, V^T [B][H][32][Tk]. */
+ * attention: per (b,h) softmax(scale Q K^T) V with Q/K rows b*T+i at column h*32, V^T [B][H][32][Tk].
+ * Bit 9 of the gemm act_code and bit 8 of the attention dtype select the swizzled V^T layout the
+ * encoder uses with 16-bit operands (token t of every 16-token group stored at position t with
+ * bits 2 and 3 swapped; Tk % 16 == 0): the v projection writes it, the LDS-DMA attention reads it. */
 int spe_debug_gemm(void* stream, int dtype, int mode, const void* A, int lda, const void* P, int ldp, int prow, int H,
                    int W, int Cin, int KH, int KW, int stride, int pad, const void* Bw, int ldb, int M, int N, int K,
                    const float* bias, const void* R, int ldr, int act_code, void* C, int ldc, int out_f32, int vt_T,

@@ -134,6 +134,11 @@ struct Stage {
   }
 };
 
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+// s_waitcnt immediate (gfx9: vmcnt [3:0] + [15:14], expcnt [6:4], lgkmcnt [11:8]) for a vmcnt-only
+// wait, issued through the builtin so the compiler's own wait insertion accounts for it
+constexpr int attn_waitcnt_vm(int vm) { return (vm & 15) | ((vm >> 4) << 14) | (7 << 4) | (15 << 8); }
+
 // mask keys past Tk (last tile only) and return the lane-pair max of the 32 scores
 SPE_DEV float tile_max(f32x16& s0, f32x16& s1, int key_base, int Tk, int hh) {
   if (key_base + KT > Tk) {
@@ -181,7 +186,12 @@ template <> struct AT<f16> {
 // pairs, and the row sums are packed-fp16 adds of those same words (15 v_pk_add_f16 + one
 // v_dot2_f32_f16 per 64-key tile instead of 32 f32 adds; the tile's partial sum <= 32 * 2^8
 // fits fp16, and it is the rounded P the value product uses).
-template <int ROLE, typename TI, typename TV = TI>
+// DMA: K and V^T tiles go global -> LDS by buffer_load ... lds (V^T stored in vt_pos order by the
+// v projection, so each 16-byte chunk lands verbatim), through a three-slot ring with two tiles
+// in flight: no staging registers, no ds_write, no per-tile vmcnt(0) before a store.  Each
+// wave issues exactly three 1 KB pieces per tile (10 pieces: K 5, V^T 5; two duplicates), so
+// one immediate vmcnt retires a tile.  Needs Tk % 16 == 0 (the quad swap stays inside a row).
+template <int ROLE, typename TI, typename TV = TI, bool DMA = false>
 __global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn16_kernel(AttnArgs a) {
   typedef AT<TI> A;
   typedef AT<TV> AV;
@@ -189,7 +199,9 @@ __global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn16_kernel(AttnArgs a) {
   typedef typename AV::v8 vv8;
   constexpr bool HSUM = sizeof(TV) == 2 && !std::is_same<TV, bf16>::value;   // fp16 P: packed sums
   constexpr int KBYTES = KT * KROW, VBYTES = 32 * VROW;
-  __shared__ __attribute__((aligned(16))) char smem[2 * (KBYTES + VBYTES)];
+  constexpr int DSLOT = 10240;                     // DMA slot: K 5 KB + V^T 4.5 KB (+ 0.5 KB spill room)
+  static_assert(KBYTES == 5120 && VBYTES <= DSLOT - KBYTES, "DMA slot");
+  __shared__ __attribute__((aligned(1024))) char smem[DMA ? 3 * DSLOT : 2 * (KBYTES + VBYTES)];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int hh = lane >> 5, r32 = lane & 31;
   const int qblocks = (a.Tq + 127) / 128;
@@ -213,6 +225,10 @@ __global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn16_kernel(AttnArgs a) {
       qf[i] = __builtin_bit_cast(v8, pack16<TI>(f));
     }
   }
+  // the query fragments are formed here, before the DMA stream starts: left to the compiler it
+  // re-forms them inside the key loop, and its wait for the q loads (vmcnt is in-order) then
+  // drains the next tile's DMA every iteration
+  if constexpr (DMA) asm volatile("" ::"v"(qf[0]), "v"(qf[1]));
   // o: O^T accumulator; ls: this lane's running sum of p over its half of the keys.
   f32x16 o;
   float ls = 0.f;
@@ -230,18 +246,74 @@ __global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn16_kernel(AttnArgs a) {
   const int ntiles = (a.Tk + KT - 1) / KT;
   constexpr int SLOT = KBYTES + VBYTES;
   Stage<TI, KT> st;
-  st.load(a, b, h, 0, tid);
-  st.store(smem, smem + KBYTES, tid);
-  __syncthreads();
+  // DMA pieces of this wave: slots wid, wid + 4, wid + 8 of {K 0-4, V^T 0-4, K 0-1 again}.  Per
+  // lane a fixed voffset; the tile moves the scalar soffset.  Rows past Tk read as zero through
+  // the descriptors' ranges (this image's K rows, this (image, head)'s V^T block).
+  // (b, h and the wave index are wave-uniform; readfirstlane lets the compiler keep the
+  // descriptors and the piece selection scalar instead of waterfalling over lanes)
+  const int bu = __builtin_amdgcn_readfirstlane(b), hu = __builtin_amdgcn_readfirstlane(h);
+  const int wu = __builtin_amdgcn_readfirstlane(wid);
+  const __amdgpu_buffer_rsrc_t rk = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)((const TI*)a.k + (size_t)bu * a.Tk * a.ldk + hu * 32), (short)0, a.Tk * a.ldk * 2, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rv = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)((const TV*)a.vt + (size_t)(bu * a.H + hu) * 32 * a.Tk), (short)0, 32 * a.Tk * 2, 0x00020000);
+  int dvo[3] = {0, 0, 0}, dlo[3] = {0, 0, 0};
+  bool dv[3] = {false, false, false};
+  if constexpr (DMA) {
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      const int slot = wu + 4 * j;
+      const int piece = slot < 10 ? slot : slot - 10;
+      const int isv = piece >= 5, pc = isv ? piece - 5 : piece;
+      const int o = pc * 1024 + lane * 16;
+      if (!isv) {
+        const int key = o / KROW, c = (o - key * KROW) >> 4;
+        dvo[j] = key * a.ldk * 2 + (c < 4 ? c : 0) * 16;
+        dlo[j] = pc * 1024;
+      } else {
+        const int d = o / VROW, c = (o - d * VROW) >> 4;
+        dvo[j] = (d < 32 && c < 8) ? (d * a.Tk + c * 8) * 2 : 0;
+        dlo[j] = KBYTES + pc * 1024;
+      }
+      dv[j] = isv;
+    }
+  }
+  auto issue = [&](int kt, int slot) {
+    char* base = smem + slot * DSLOT;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) {
+      // (the LDS address is per wave-instruction: lane 0's; lanes follow at 16-byte steps)
+      lds_ptr_t dst = (lds_ptr_t)(base + dlo[j]);
+      if (dv[j]) __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, dst, 16, dvo[j], kt * KT * 2, 0, 0);
+      else __builtin_amdgcn_raw_ptr_buffer_load_lds(rk, dst, 16, dvo[j], kt * KT * a.ldk * 2, 0, 0);
+    }
+  };
+  if constexpr (DMA) {
+    issue(0, 0);
+    if (ntiles > 1) issue(1, 1);
+  } else {
+    st.load(a, b, h, 0, tid);
+    st.store(smem, smem + KBYTES, tid);
+    __syncthreads();
+  }
   for (int kt = 0; kt < ntiles; ++kt) {
-    const char* kl = smem + (kt & 1) * SLOT;
+    const char* kl = smem + (DMA ? (kt % 3) * DSLOT : (kt & 1) * SLOT);
     const char* vl = kl + KBYTES;
     const bool more = kt + 1 < ntiles;
+    if constexpr (DMA) {
+      // tile kt landed (tile kt+1 may stay in flight), then the barrier: tile kt visible to all,
+      // every wave done with tile kt-1, whose slot takes tile kt+2
+      if (more) __builtin_amdgcn_s_waitcnt(attn_waitcnt_vm(3));
+      else __builtin_amdgcn_s_waitcnt(attn_waitcnt_vm(0));
+      __builtin_amdgcn_s_barrier();
+      if (kt + 2 < ntiles) issue(kt + 2, (kt + 2) % 3);
+    } else {
 #ifdef SPE_X_NOSTAGE
-    if (more && kt == 0) st.load(a, b, h, kt + 1, tid);
+      if (more && kt == 0) st.load(a, b, h, kt + 1, tid);
 #else
-    if (more) st.load(a, b, h, kt + 1, tid);
+      if (more) st.load(a, b, h, kt + 1, tid);
 #endif
+    }
     if (wave_live) {
       // every fragment read of this step is issued up front; V lands during QK^T + softmax
       u32x4 kf[2][2], vf[2][2];
@@ -327,14 +399,16 @@ __global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn16_kernel(AttnArgs a) {
         for (int ks = 0; ks < 2; ++ks)
           o = AV::mfma(__builtin_bit_cast(vv8, vf[sub][ks]), __builtin_bit_cast(vv8, pw[sub][ks]), o);
     }
+    if constexpr (!DMA) {
 #ifdef SPE_X_NOSTAGE
-    if (more && kt == 0) st.store(smem + ((kt + 1) & 1) * SLOT, smem + ((kt + 1) & 1) * SLOT + KBYTES, tid);
+      if (more && kt == 0) st.store(smem + ((kt + 1) & 1) * SLOT, smem + ((kt + 1) & 1) * SLOT + KBYTES, tid);
 #else
-    if (more) st.store(smem + ((kt + 1) & 1) * SLOT, smem + ((kt + 1) & 1) * SLOT + KBYTES, tid);
+      if (more) st.store(smem + ((kt + 1) & 1) * SLOT, smem + ((kt + 1) & 1) * SLOT + KBYTES, tid);
 #endif
 #ifndef SPE_X_NOBAR
-    __syncthreads();
+      __syncthreads();
 #endif
+    }
   }
 
   if (!wave_live || q >= a.Tq) return;
@@ -600,6 +674,21 @@ int spe_launch_attention(const AttnArgs& a, int dtype, hipStream_t s) {
   const int ce = (dtype == SPE_DTYPE_F32 || dtype == SPE_DTYPE_F32X3) ? 4 : 8;
   if ((a.ldq % ce) || (a.ldk % ce) || (a.ldo % 4)) return -5;
   dim3 grid(a.B * a.H * ((a.Tq + 127) / 128)), block(NT);
+  if (a.vt_swz && (a.Tk % 16 || (dtype != SPE_DTYPE_F16 && dtype != SPE_DTYPE_BF16 && dtype != SPE_DTYPE_BF16_F16V)))
+    return -5;                                     // (swizzled V^T: 16-bit operands, whole quads per row)
+  if (a.vt_swz) {                                  // LDS-DMA staging (the only reader of that layout)
+    if (dtype == SPE_DTYPE_F16) {
+      if (a.Tq >= 128) hipLaunchKernelGGL((attn16_kernel<0, f16, f16, true>), grid, block, 0, s, a);
+      else hipLaunchKernelGGL((attn16_kernel<1, f16, f16, true>), grid, block, 0, s, a);
+    } else if (dtype == SPE_DTYPE_BF16_F16V) {
+      if (a.Tq >= 128) hipLaunchKernelGGL((attn16_kernel<0, bf16, f16, true>), grid, block, 0, s, a);
+      else hipLaunchKernelGGL((attn16_kernel<1, bf16, f16, true>), grid, block, 0, s, a);
+    } else {
+      if (a.Tq >= 128) hipLaunchKernelGGL((attn16_kernel<0, bf16, bf16, true>), grid, block, 0, s, a);
+      else hipLaunchKernelGGL((attn16_kernel<1, bf16, bf16, true>), grid, block, 0, s, a);
+    }
+    return (int)hipGetLastError();
+  }
   if (dtype == SPE_DTYPE_F16)
     if (a.Tq >= 128)
       hipLaunchKernelGGL((attn16_kernel<0, f16>), grid, block, 0, s, a);

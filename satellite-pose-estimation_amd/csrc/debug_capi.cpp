@@ -20,6 +20,7 @@ int spe_debug_gemm(void* stream, int dtype, int mode, const void* A, int lda, co
   g.Wo = mode == GEMM_CONV ? (W + 2 * pad - KW) / stride + 1 : 0;
   g.B = Bw; g.ldb = ldb; g.M = M; g.N = N; g.K = K;
   g.bias = bias; g.R = R; g.ldr = ldr; g.act = act_code & 255; g.res_post = (act_code >> 8) & 1; g.C = C; g.ldc = ldc; g.out_f32 = out_f32;
+  g.vt_swz = (act_code >> 9) & 1;
   g.vt_T = vt_T; g.vt_B = vt_B;
   g.r_period = r_period;
   g.ln_g = ln_g; g.ln_b = ln_b;
@@ -35,7 +36,8 @@ int spe_debug_attention(void* stream, int dtype, const void* q, int ldq, const v
   AttnArgs a{};
   a.q = q; a.ldq = ldq; a.k = k; a.ldk = ldk; a.vt = vt; a.o = o; a.ldo = ldo;
   a.B = B; a.H = H; a.Tq = Tq; a.Tk = Tk; a.scale = scale;
-  int rc = spe_launch_attention(a, dtype, (hipStream_t)stream);
+  a.vt_swz = (dtype >> 8) & 1;
+  int rc = spe_launch_attention(a, dtype & 255, (hipStream_t)stream);
   return rc < 0 ? spe_fail(SPE_E_LAUNCH, "attention launch rejected its arguments") : rc;
 }
 

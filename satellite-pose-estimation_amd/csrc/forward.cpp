@@ -324,6 +324,10 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   static const int f16v_env = [] { const char* e = getenv("SPE_ATTN_F16V"); return e ? atoi(e) : 1; }();
   const int f16v = !f16attn && dt == SPE_DTYPE_BF16 && f16v_env;
   const int attn_dt = f16attn ? SPE_DTYPE_F16 : f16v ? SPE_DTYPE_BF16_F16V : dt;
+  // 16-bit encoder attention stages K / V^T by LDS DMA, which needs V^T rows in its key order
+  // (vt_pos: the v projection's epilogue writes them so); SPE_ATTN_DMA=0 keeps register staging
+  static const int dma_env = [] { const char* e = getenv("SPE_ATTN_DMA"); return e ? atoi(e) : 1; }();
+  const int vt_swz = dma_env && dt == SPE_DTYPE_BF16 && T % 16 == 0;
   for (const Enc& e : m->enc) {
     {
       GemmArgs g = linear_args(e.qk, P(w.src), d, Mt, P(w.qkv), 3 * d);
@@ -333,7 +337,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
     }
     {
       GemmArgs g = linear_args(e.v, P(w.src), d, Mt, P(w.vt), 8);
-      g.vt_T = T; g.vt_B = B;
+      g.vt_T = T; g.vt_B = B; g.vt_swz = vt_swz;
       g.out_f16 = f16attn || f16v;
       CK(run_gemm(m, "gemm.enc.v", g, GEMM_LINEAR, s));
     }
@@ -341,7 +345,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       AttnArgs a{};
       a.q = P(w.qkv); a.ldq = 3 * d;
       a.k = (char*)P(w.qkv) + d * m->esz; a.ldk = 3 * d;
-      a.vt = P(w.vt);
+      a.vt = P(w.vt); a.vt_swz = vt_swz;
       a.o = P(w.ao); a.ldo = d;
       a.B = B; a.H = c.nheads; a.Tq = T; a.Tk = T; a.scale = scale;
       CK(run_attn(m, "attn.enc", a, attn_dt, s));

@@ -291,7 +291,13 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs g) {
       if ((g.vt_T & 7) == 0 && m + 8 <= g.M) {
         char* cp = (char*)g.C + (rowbase + tok) * sizeof(T);
         if constexpr (sizeof(T) == 2) {
-          st16(cp, pack_out8(v, g.out_f16));
+          const u32x4 pk = pack_out8(v, g.out_f16);
+          if (g.vt_swz) {                        // the two quads land apart (vt_pos)
+            st8((char*)g.C + (rowbase + vt_pos(tok)) * 2, u32x2{pk.x, pk.y});
+            st8((char*)g.C + (rowbase + vt_pos(tok + 4)) * 2, u32x2{pk.z, pk.w});
+          } else {
+            st16(cp, pk);
+          }
         } else {
           st16(cp, pack16<T>(v));
           st16(cp + 16, pack16<T>(v + 4));
@@ -299,7 +305,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs g) {
       } else {
         for (int e = 0; e < 8 && m + e < g.M; ++e) {
           const int me = m + e, be = me / g.vt_T, te = me - be * g.vt_T;
-          const size_t idx = ((size_t)(grp * g.vt_B + be) * 256 + hd) * g.vt_T + te;
+          const size_t idx = ((size_t)(grp * g.vt_B + be) * 256 + hd) * g.vt_T + (g.vt_swz ? vt_pos(te) : te);
           if constexpr (sizeof(T) == 2) store_out1(g.C, idx, v[e], g.out_f16);
           else ((T*)g.C)[idx] = from_f32<T>(v[e]);
         }

@@ -590,11 +590,19 @@ __global__ __launch_bounds__(NT, NST == 1 ? 4 : 1) void gemm2_kernel(GemmArgs g)
         const int grp = n >> 8, hd = n & 255;
         const int b = m / g.vt_T, tok = m - b * g.vt_T;
         if ((g.vt_T & 7) == 0 && m + 8 <= g.M) {
-          st16((bf16*)g.C + ((size_t)(grp * g.vt_B + b) * 256 + hd) * g.vt_T + tok, pack_out8(v, g.out_f16));
+          bf16* row = (bf16*)g.C + ((size_t)(grp * g.vt_B + b) * 256 + hd) * g.vt_T;
+          const u32x4 pk = pack_out8(v, g.out_f16);
+          if (g.vt_swz) {                        // the two quads land apart (vt_pos)
+            st8(row + vt_pos(tok), u32x2{pk.x, pk.y});
+            st8(row + vt_pos(tok + 4), u32x2{pk.z, pk.w});
+          } else {
+            st16(row + tok, pk);
+          }
         } else {
           for (int e = 0; e < 8 && m + e < g.M; ++e) {
             const int me = m + e, be = me / g.vt_T, te = me - be * g.vt_T;
-            store_out1(g.C, ((size_t)(grp * g.vt_B + be) * 256 + hd) * g.vt_T + te, v[e], g.out_f16);
+            store_out1(g.C, ((size_t)(grp * g.vt_B + be) * 256 + hd) * g.vt_T + (g.vt_swz ? vt_pos(te) : te), v[e],
+                       g.out_f16);
           }
         }
       }
@@ -842,7 +850,8 @@ __global__ __launch_bounds__(SM_NT) void gemm_small_kernel(GemmArgs g) {
         const int grp = n >> 8, hd = n & 255;
         for (int r = 0; r < 4 && m + r < g.M; ++r) {
           const int me = m + r, be = me / g.vt_T, te = me - be * g.vt_T;
-          store_out1(g.C, ((size_t)(grp * g.vt_B + be) * 256 + hd) * g.vt_T + te, acc[i][j][r] + bv, g.out_f16);
+          store_out1(g.C, ((size_t)(grp * g.vt_B + be) * 256 + hd) * g.vt_T + (g.vt_swz ? vt_pos(te) : te),
+                     acc[i][j][r] + bv, g.out_f16);
         }
       } else {
         // C^T fragment: 4 consecutive columns n = .. + 4fg + r of row m

@@ -187,7 +187,8 @@ __global__ __launch_bounds__(256, OCC) void sgemm_kernel(GemmArgs g, int ns_coun
             const float bv = sb[16 * j + fr];
             const uint32_t lo = pack_out2(acc[rf][j][0] + bv, acc[rf][j][1] + bv, F16);
             const uint32_t hi = pack_out2(acc[rf][j][2] + bv, acc[rf][j][3] + bv, F16);
-            char* cp = (char*)g.C + (((size_t)((n >> 8) * g.vt_B + b) * 256 + (n & 255)) * g.vt_T + tok) * 2;
+            const int pos = g.vt_swz ? vt_pos(tok) : tok;   // (a 4-token quad moves as a whole)
+            char* cp = (char*)g.C + (((size_t)((n >> 8) * g.vt_B + b) * 256 + (n & 255)) * g.vt_T + pos) * 2;
             st8(ok ? cp : (char*)g_sg_sink, u32x2{lo, hi});
           }
         }
@@ -347,7 +348,7 @@ int spe_launch_sgemm(const GemmArgs& g, int mode, hipStream_t s) {
   if (g.act > ACT_RELU || g.res_post || g.out_f32) return 1;
   if (g.ldb < g.K || g.ldb % 8 || g.lda % 8 || g.ldc % 4 || (g.R && g.ldr % 4)) return 1;
   if (g.ln_g && (g.N != 256 || g.act)) return 1;
-  if (g.vt_T > 0 && (g.vt_T % 4 || g.M % 4 || g.N % 256 || g.act)) return 1;
+  if (g.vt_T > 0 && (g.vt_T % 4 || g.M % 4 || g.N % 256 || g.act || (g.vt_swz && g.vt_T % 16))) return 1;
   switch (g.K) {
     case 64:
       if (g.N == 64) return launch_kbn<64, 64, 2, 2, 4, 2, 2, 4>(g, s);

@@ -26,6 +26,8 @@ struct GemmArgs {
   int out_f32;                     // store fp32 instead of T
   int out_f16;                     // bf16 models: store fp16 instead of bf16 (fp16 attention operands)
   int vt_T, vt_B;                  // >0: head-transposed store (see gemm.hip)
+  int vt_swz;                      // head-transposed 16-bit store with the attention's key order: within
+                                   // each 16-token group the middle quads swap (vt_pos; vt_T % 16 == 0)
   int r_period;                    // >0: residual row = m % r_period (row-periodic add, e.g. pos . W^T)
   const float* ln_g; const float* ln_b;   // optional fused post-norm LayerNorm over N == 256 (bf16, large M)
 };
@@ -73,10 +75,16 @@ int spe_cu_count();               // CUs of the current device (cached; 256 on M
 // 3 pconv.hip
 extern thread_local int spe_gemm_last_path;
 
+// Stored position of token t in a vt_swz V^T row: bits 2 and 3 swap (quads 0, 2, 1, 3 of every
+// 16 tokens), the key order the attention's P^T operand has straight out of its S^T accumulator.
+__host__ __device__ inline int vt_pos(int t) { return (t & ~12) | ((t & 4) << 1) | ((t & 8) >> 1); }
+
 struct AttnArgs {
   const void* q; int ldq;          // query row b*Tq+i, head h at columns [h*32, h*32+32)
   const void* k; int ldk;          // key row b*Tk+j
   const void* vt;                  // V^T [B][H][32][Tk]
+  int vt_swz;                      // V^T rows in vt_pos order (16-bit operands, Tk % 16 == 0): the
+                                   // encoder kernel then stages K / V^T by LDS DMA
   void* o; int ldo;                // output row b*Tq+i
   int B, H, Tq, Tk;
   float scale;                     // softmax scale (1/sqrt(head_dim))

@@ -461,6 +461,64 @@ def test_attention(gpu_device, dtype, B, H, Tq, Tk):
     _close(O, ref, {"bf16": 2e-2, "fp16": 1e-2, "fp32": 1e-5, "bf16_f16v": 2e-2}[dtype])
 
 
+def _vt_swizzle(VT):
+    """[..., Tk] rows in the encoder's LDS-DMA key order: token t stored at position t with
+    bits 2 and 3 swapped (spe_kernels.h vt_pos)."""
+    Tk = VT.shape[-1]
+    t = torch.arange(Tk)
+    pos = (t & ~12) | ((t & 4) << 1) | ((t & 8) >> 1)
+    out = torch.empty_like(VT)
+    out[..., pos.to(VT.device)] = VT
+    return out
+
+
+# the encoder's LDS-DMA staging (swizzled V^T, Tk % 16 == 0): keys past a whole tile, one-tile
+# and two-tile sweeps, Tq below the 128-query block, and the bench's T = 2704
+@pytest.mark.parametrize("dtype", ["bf16", "fp16", "bf16_f16v"])
+@pytest.mark.parametrize("B,H,Tq,Tk", [(2, 8, 200, 208), (1, 8, 64, 64), (1, 2, 300, 128), (3, 8, 256, 96),
+                                       (1, 8, 2704, 2704)])
+def test_attention_dma(gpu_device, dtype, B, H, Tq, Tk):
+    if dtype == "bf16_f16v":
+        code, dt, vdt = SPE_DTYPE_BF16_F16V, torch.bfloat16, torch.float16
+    else:
+        code, dt, _ = DT[dtype]
+        vdt = dt
+    g = torch.Generator(device="cpu").manual_seed(Tq + Tk + 7)
+    ld = H * 32 + 16
+    Q = (torch.randn(B * Tq, ld, generator=g) * 2).to(gpu_device, dt)
+    K = (torch.randn(B * Tk, ld, generator=g) * 2).to(gpu_device, dt)
+    V = torch.randn(B, H, Tk, 32, generator=g).to(gpu_device, vdt)
+    VTs = _vt_swizzle(V.transpose(-1, -2).contiguous())
+    O = torch.zeros(B * Tq, H * 32, dtype=torch.bfloat16, device=gpu_device)
+    scale = 32 ** -0.5
+    rc = _lib.lib().spe_debug_attention(None, code | 0x100, _p(Q), ld, _p(K), ld, _p(VTs), _p(O), H * 32, B, H, Tq,
+                                        Tk, scale)
+    assert rc == 0, _lib.lib().spe_last_error()
+    torch.cuda.synchronize()
+    q = Q[:, : H * 32].view(B, Tq, H, 32).transpose(1, 2)
+    k = K[:, : H * 32].view(B, Tk, H, 32).transpose(1, 2)
+    q = (q.float() * scale * 1.4426950408889634).to(dt).float() / (scale * 1.4426950408889634)
+    ref = _attn_ref(q, k, V, scale).transpose(1, 2).reshape(B * Tq, H * 32)
+    _close(O, ref, {"bf16": 2e-2, "fp16": 1e-2, "bf16_f16v": 2e-2}[dtype])
+
+
+def test_gemm_vt_swizzle(gpu_device):
+    """Head-transposed GEMM stores in the swizzled key order (act_code bit 9) on the streaming,
+    large-tile and small kernels: the swizzled output un-permutes to the plain one."""
+    dt = torch.bfloat16
+    for B, T in ((64, 2704), (3, 256), (1, 64)):
+        M, K, N = B * T, 256, 256
+        g = torch.Generator(device="cpu").manual_seed(B + T)
+        A = torch.randn(M, K, generator=g).to(gpu_device, dt)
+        W = (torch.randn(N, K, generator=g) / 16).to(gpu_device, dt)
+        bias = torch.randn(N, generator=g).to(gpu_device)
+        plain = torch.zeros(B * N * T, dtype=dt, device=gpu_device)
+        swz = torch.zeros_like(plain)
+        _gemm("bf16", 0, A, W, M, N, K, K, K, plain, 8, bias=bias, vt=(T, B))
+        _gemm("bf16", 0, A, W, M, N, K, K, K, swz, 8, bias=bias, vt=(T, B), relu=1 << 9)
+        assert torch.equal(_vt_swizzle(plain.view(B, N, T)), swz.view(B, N, T)), (B, T)
+
+
 @pytest.mark.parametrize("mode", ["bf16", "bf16_f16v"])
 def test_attention_large_score_range(gpu_device, mode):
     """Scores spanning > 100 in log space force rescales of the running max late in the sweep."""
