@@ -29,7 +29,7 @@ PEAK = {"bf16": {"mfma": 2500.0}, "fp32": {"mfma": 157.3}, "fp32x3": {"mfma": 25
 # (rocprofv3 prints the attention kernels mangled: it does not demangle the __bf16 / _Float16
 # template arguments, DF16b / DF16_)
 # (bf16 models' encoder attention: bf16 q/k, fp16 V^T and P -- attn16_kernel<0, bf16, f16>)
-KIND_SYMBOL = {"attn.enc": "_ZN12_GLOBAL__N_113attn16_kernelILi0EDF16bDF16_EEv8AttnArgs",
+KIND_SYMBOL = {"attn.enc": "_ZN12_GLOBAL__N_113attn16_kernelILi0EDF16bDF16_Lb1EEEv8AttnArgs",
                "attn.dec_self": "_ZN12_GLOBAL__N_113attn16_kernelILi1EDF16bDF16bEEv8AttnArgs",
                "attn.dec_cross": "xattn_kernel", "ffn.enc": "ffn_pipe_kernel<3, true, 6>", "ffn.dec": "ffn_ln_kernel<2, 3>"}
 
