@@ -264,7 +264,8 @@ int spe_debug_gemm(void* stream, int dtype, int mode, const void* A, int lda, co
 /* (out_f16: bf16 launches store fp16 instead of bf16.  ln_g/ln_b non-null: post-norm LayerNorm over each output row fused into the epilogue; bf16,
  * N == 256 and enough rows for the large-tile kernel, else SPE_E_LAUNCH) */
 /* kernel family that served this thread's last gemm launch: 0 the 128x128 kernel, 1 the large-tile
- * kernels (gemm2.hip), 2 the persistent streaming kernel for short-K problems (gemm_stream.hip) */
+ * kernels (gemm2.hip), 2 the persistent streaming kernel for short-K problems (gemm_stream.hip),
+ * 3 the patch-staged 3x3 conv (pconv.hip), 4 the projection + residual + LayerNorm (lnproj.hip) */
 int spe_debug_gemm_path(void);
 int spe_debug_attention(void* stream, int dtype, const void* q, int ldq, const void* k, int ldk, const void* vt,
                         void* o, int ldo, int B, int H, int Tq, int Tk, float scale);

@@ -356,7 +356,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       g.R = P(w.src); g.ldr = d;
       GemmArgs gf = g;
       gf.C = P(w.src); gf.ln_g = e.n1g; gf.ln_b = e.n1b;
-      if (m->esz == 2 && spe_gemm_ln_fusable(gf)) {
+      if (m->esz == 2 && spe_ln_fusable(gf)) {
         CK(run_gemm(m, "gemm.enc.o", gf, GEMM_LINEAR, s));
       } else {
         CK(run_gemm(m, "gemm.enc.o", g, GEMM_LINEAR, s));

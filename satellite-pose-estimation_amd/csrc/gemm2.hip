@@ -912,6 +912,10 @@ int spe_launch_gemm2(const GemmArgs& g, int mode, hipStream_t s) {
     const int rc = spe_launch_pconv(g, s);         // 3x3 stride-1 convs: patch-staged kernel (pconv.hip)
     if (rc != 1) return rc;
   }
+  if (mode == GEMM_LINEAR && g.ln_g) {
+    const int rc = spe_launch_lnproj(g, s);       // out-projection + residual + LayerNorm (lnproj.hip)
+    if (rc != 1) return rc;
+  }
   {
     const int rc = spe_launch_sgemm(g, mode, s);   // short-K streaming kernel (gemm_stream.hip)
     if (rc != 1) return rc;

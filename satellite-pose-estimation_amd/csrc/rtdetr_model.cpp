@@ -604,7 +604,7 @@ int spe_rtdetr_forward(spe_model* m, void* stream, const float* images, int B, v
     GemmArgs g = linear_args(r.enc_out, P(w.mem), d, ML, P(w.omem), d);
     GemmArgs gf = g;
     gf.ln_g = r.eo_g; gf.ln_b = r.eo_b;
-    if (E == 2 && spe_gemm_ln_fusable(gf)) {
+    if (E == 2 && spe_ln_fusable(gf)) {
       CK(run_gemm(m, "rt.dec.enc_out", gf, GEMM_LINEAR, s));
     } else {
       CK(run_gemm(m, "rt.dec.enc_out", g, GEMM_LINEAR, s));

@@ -69,6 +69,10 @@ int spe_btail_perm(int k);
 bool spe_btail_enabled();
 int spe_launch_gemm2(const GemmArgs& g, int mode, hipStream_t s);   // 1 = not applicable
 int spe_launch_sgemm(const GemmArgs& g, int mode, hipStream_t s);   // 1 = not applicable
+int spe_launch_lnproj(const GemmArgs& g, hipStream_t s);             // 1 = not applicable (lnproj.hip)
+bool spe_lnproj_applies(const GemmArgs& g);
+// bf16 GEMM + residual + LayerNorm in one launch: lnproj.hip at any row count, else the large-tile kernel
+inline bool spe_ln_fusable(const GemmArgs& g) { return spe_lnproj_applies(g) || spe_gemm_ln_fusable(g); }
 int spe_launch_pconv(const GemmArgs& g, hipStream_t s);             // 1 = not applicable (pconv.hip)
 int spe_cu_count();               // CUs of the current device (cached; 256 on MI355X)
 // kernel family of this thread's last spe_launch_gemm: 0 gemm.hip, 1 gemm2.hip, 2 gemm_stream.hip,

@@ -225,10 +225,12 @@ def test_gemm_large_tile_linear(gpu_device, N, K):
 
 
 @pytest.mark.parametrize("inplace", [True, False])
-def test_gemm_fused_layernorm(gpu_device, inplace):
-    """out-proj + residual + LayerNorm in one launch (encoder norm1), optionally in place over R."""
+@pytest.mark.parametrize("M", [256 * 256 + 77, 1000, 16])
+def test_gemm_fused_layernorm(gpu_device, inplace, M):
+    """out-proj + residual + LayerNorm in one launch (encoder norm1, lnproj.hip), optionally in
+    place over R; rows off the 16-row tile and fewer tiles than waves."""
     _, dt, tol = DT["bf16"]
-    M, N, K = 256 * 256 + 77, 256, 256
+    N, K = 256, 256
     g = torch.Generator(device="cpu").manual_seed(11)
     A = torch.randn(M, K, generator=g).to(gpu_device, dt)
     Wt = (torch.randn(N, K, generator=g) / 16).to(gpu_device, dt)
@@ -240,6 +242,7 @@ def test_gemm_fused_layernorm(gpu_device, inplace):
     ref = F.layer_norm(pre, (N,), gam, bet, 1e-5)
     C = R if inplace else torch.zeros(M, N, dtype=dt, device=gpu_device)
     _gemm("bf16", 0, A, _padded_weight(Wt, 256, dt), M, N, K, K, 256, C, N, bias=bias, R=R, ldr=N, ln=(gam, bet))
+    assert _lib.lib().spe_debug_gemm_path() == 4, "expected the LayerNorm projection kernel"
     _close(C, ref, 3e-2)
     # not fusable (too few rows for the large-tile kernel): the hook must refuse, not ignore
     L = _lib.lib()
