@@ -36,6 +36,10 @@ constexpr int KT = 64;                 // keys per softmax step (and per staged 
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float NEG_BIG = -1.0e30f;    // finite "minus infinity" (exp2 of it underflows to 0)
 constexpr float RESCALE_SLACK = 8.0f;  // log2 units (bf16 path)
+constexpr float LAZY_LIMIT = 4096.0f;  // fp16-P tiles: a lane's 32-key sum that forces the max path
+#ifndef SPE_ATTN_LAZY
+#define SPE_ATTN_LAZY 1
+#endif
 #ifndef SPE_ATTN_OCC
 #define SPE_ATTN_OCC 4
 #endif
@@ -139,8 +143,8 @@ typedef __attribute__((address_space(3))) void* lds_ptr_t;
 // wait, issued through the builtin so the compiler's own wait insertion accounts for it
 constexpr int attn_waitcnt_vm(int vm) { return (vm & 15) | ((vm >> 4) << 14) | (7 << 4) | (15 << 8); }
 
-// mask keys past Tk (last tile only) and return the lane-pair max of the 32 scores
-SPE_DEV float tile_max(f32x16& s0, f32x16& s1, int key_base, int Tk, int hh) {
+// mask keys past Tk (last tile only)
+SPE_DEV void tile_mask(f32x16& s0, f32x16& s1, int key_base, int Tk, int hh) {
   if (key_base + KT > Tk) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
@@ -149,6 +153,28 @@ SPE_DEV float tile_max(f32x16& s0, f32x16& s1, int key_base, int Tk, int hh) {
       if (key_base + 32 + kr >= Tk) s1[r] = NEG_BIG;
     }
   }
+}
+
+// Tk % 16 == 0 (the DMA kernel): the lane's scores r = 0-7 of s0 are keys 0-15 of the tile, r =
+// 8-15 keys 16-31, and s1 the next 32 -- each register group is one whole 16-key group, so the
+// mask is four wave-uniform tests
+SPE_DEV void tile_mask16(f32x16& s0, f32x16& s1, int key_base, int Tk) {
+  if (key_base + KT > Tk) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      if (key_base + 16 * g >= Tk) {
+        f32x16& s = g < 2 ? s0 : s1;
+#pragma unroll
+        for (int r = 0; r < 8; ++r) s[8 * (g & 1) + r] = NEG_BIG;
+      }
+  }
+}
+
+// mask keys past Tk (last tile only; MASK = false: done by the caller) and return the lane-pair
+// max of the 32 scores
+template <bool MASK = true>
+SPE_DEV float tile_max(f32x16& s0, f32x16& s1, int key_base, int Tk, int hh) {
+  if constexpr (MASK) tile_mask(s0, s1, key_base, Tk, hh);
   // two independent v_max3 chains (the file is built with -fno-honor-nans, so no canonicalizes)
   float ma = __builtin_fmaxf(s0[0], s1[0]), mb = __builtin_fmaxf(s0[1], s1[1]);
 #pragma unroll
@@ -198,6 +224,7 @@ __global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn16_kernel(AttnArgs a) {
   typedef typename A::v8 v8;
   typedef typename AV::v8 vv8;
   constexpr bool HSUM = sizeof(TV) == 2 && !std::is_same<TV, bf16>::value;   // fp16 P: packed sums
+  constexpr bool LAZY = HSUM && DMA && SPE_ATTN_LAZY;   // no per-tile max (below)
   constexpr int KBYTES = KT * KROW, VBYTES = 32 * VROW;
   constexpr int DSLOT = 10240;                     // DMA slot: K 5 KB + V^T 4.5 KB (+ 0.5 KB spill room)
   static_assert(KBYTES == 5120 && VBYTES <= DSLOT - KBYTES, "DMA slot");
@@ -334,65 +361,72 @@ __global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn16_kernel(AttnArgs a) {
         s = A::mfma(__builtin_bit_cast(v8, kf[sub][0]), qf[0], negm);
         s = A::mfma(__builtin_bit_cast(v8, kf[sub][1]), qf[1], s);
       }
-#ifdef SPE_X_NOMAX
-      const float mx = kt == 0 ? s0[0] : 0.f;
-#else
-      const float mx = tile_max(s0, s1, kt * KT, a.Tk, hh);   // relative to m
-#endif
-      // Lazy rescale (wave-uniform): keep the stale max until some lane's max grew by more than
-      // RESCALE_SLACK (p <= 2^8 then, harmless in fp32 accumulators and bf16 P).  With an exact
-      // "grew at all" test, 32 queries per wave re-fire the rescale on about half the tiles.
-      // The first tile always sets m to its own max (o and l are still zero then).
-      if (kt == 0 || __any(mx > RESCALE_SLACK)) {
-        const float d = kt == 0 ? mx : __builtin_fmaxf(mx, 0.f);
-        if (kt != 0) {
-          const float alpha = __builtin_amdgcn_exp2f(-d);
-#pragma unroll
-          for (int r = 0; r < 16; ++r) o[r] *= alpha;
-          ls *= alpha;
-        }
-        m += d;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) { s0[r] -= d; s1[r] -= d; negm[r] = -m; }
-      }
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-#ifdef SPE_X_NOEXP
-        s0[r] = s0[r] * 0.001f;
-        s1[r] = s1[r] * 0.001f;
-#else
-        s0[r] = __builtin_amdgcn_exp2f(s0[r]);
-        s1[r] = __builtin_amdgcn_exp2f(s1[r]);
-#endif
-      }
-#ifndef SPE_X_NOLS
-      if constexpr (!HSUM) {
-        float t0 = 0.f, t1 = 0.f, t2 = 0.f, t3 = 0.f;
-#pragma unroll
-        for (int r = 0; r < 16; r += 2) { t0 += s0[r]; t1 += s0[r + 1]; t2 += s1[r]; t3 += s1[r + 1]; }
-        ls += (t0 + t1) + (t2 + t3);
-      }
-#endif
+      // LAZY (fp16 P): no per-tile max at all.  The tile is exponentiated against the stale
+      // running max and its packed-fp16 row sum, formed anyway, is the overflow test: only if
+      // some lane's 32-key sum passes LAZY_LIMIT (any p > 2^12, or an fp16 overflow) are the
+      // scores recomputed from the K tile still in LDS and taken through the max/rescale path.
+      bool full = !LAZY || kt == 0;
       u32x4 pw[2][2];
+      float tsum = 0.f;
+      for (;;) {
+        if constexpr (DMA) tile_mask16(s0, s1, kt * KT, a.Tk);
+        if (full) {
+          const float mx = tile_max<!DMA>(s0, s1, kt * KT, a.Tk, hh);   // relative to m
+          // Lazy rescale (wave-uniform): keep the stale max until some lane's max grew by more
+          // than RESCALE_SLACK (p <= 2^8 then, harmless in fp32 accumulators and 16-bit P).  With
+          // an exact "grew at all" test, 32 queries per wave re-fire the rescale on about half the
+          // tiles.  The first tile always sets m to its own max (o and l are still zero then).
+          if (kt == 0 || __any(mx > RESCALE_SLACK)) {
+            const float d = kt == 0 ? mx : __builtin_fmaxf(mx, 0.f);
+            if (kt != 0) {
+              const float alpha = __builtin_amdgcn_exp2f(-d);
 #pragma unroll
-      for (int sub = 0; sub < 2; ++sub) {
-        const f32x16& p = sub ? s1 : s0;
+              for (int r = 0; r < 16; ++r) o[r] *= alpha;
+              ls *= alpha;
+            }
+            m += d;
 #pragma unroll
-        for (int ks = 0; ks < 2; ++ks)
-          pw[sub][ks] = u32x4{AV::pk(p[8 * ks + 0], p[8 * ks + 1]), AV::pk(p[8 * ks + 2], p[8 * ks + 3]),
-                              AV::pk(p[8 * ks + 4], p[8 * ks + 5]), AV::pk(p[8 * ks + 6], p[8 * ks + 7])};
+            for (int r = 0; r < 16; ++r) { s0[r] -= d; s1[r] -= d; negm[r] = -m; }
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          s0[r] = __builtin_amdgcn_exp2f(s0[r]);
+          s1[r] = __builtin_amdgcn_exp2f(s1[r]);
+        }
+        if constexpr (!HSUM) {
+          float t0 = 0.f, t1 = 0.f, t2 = 0.f, t3 = 0.f;
+#pragma unroll
+          for (int r = 0; r < 16; r += 2) { t0 += s0[r]; t1 += s0[r + 1]; t2 += s1[r]; t3 += s1[r + 1]; }
+          tsum = (t0 + t1) + (t2 + t3);
+        }
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub) {
+          const f32x16& p = sub ? s1 : s0;
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks)
+            pw[sub][ks] = u32x4{AV::pk(p[8 * ks + 0], p[8 * ks + 1]), AV::pk(p[8 * ks + 2], p[8 * ks + 3]),
+                                AV::pk(p[8 * ks + 4], p[8 * ks + 5]), AV::pk(p[8 * ks + 6], p[8 * ks + 7])};
+        }
+        if constexpr (HSUM) {
+          typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+          auto H2 = [](uint32_t w) { return __builtin_bit_cast(h2, w); };
+          h2 u[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            u[e] = (H2(pw[0][0][e]) + H2(pw[0][1][e])) + (H2(pw[1][0][e]) + H2(pw[1][1][e]));
+          tsum = __builtin_amdgcn_fdot2((u[0] + u[1]) + (u[2] + u[3]), h2{(_Float16)1.f, (_Float16)1.f}, 0.f, false);
+        }
+        if (full || !__any(tsum > LAZY_LIMIT)) break;
+        full = true;
+#pragma unroll
+        for (int sub = 0; sub < 2; ++sub) {
+          f32x16& s = sub ? s1 : s0;
+          s = A::mfma(__builtin_bit_cast(v8, ld16(kl + k_off_bf16(sub * 32 + r32, hh))), qf[0], negm);
+          s = A::mfma(__builtin_bit_cast(v8, ld16(kl + k_off_bf16(sub * 32 + r32, 2 + hh))), qf[1], s);
+        }
       }
-#ifndef SPE_X_NOLS
-      if constexpr (HSUM) {
-        typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-        auto H2 = [](uint32_t w) { return __builtin_bit_cast(h2, w); };
-        h2 u[4];
-#pragma unroll
-        for (int e = 0; e < 4; ++e)
-          u[e] = (H2(pw[0][0][e]) + H2(pw[0][1][e])) + (H2(pw[1][0][e]) + H2(pw[1][1][e]));
-        ls = __builtin_amdgcn_fdot2((u[0] + u[1]) + (u[2] + u[3]), h2{(_Float16)1.f, (_Float16)1.f}, ls, false);
-      }
-#endif
+      ls += tsum;
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub)
 #pragma unroll

@@ -522,24 +522,31 @@ def test_gemm_vt_swizzle(gpu_device):
         assert torch.equal(_vt_swizzle(plain.view(B, N, T)), swz.view(B, N, T)), (B, T)
 
 
-@pytest.mark.parametrize("mode", ["bf16", "bf16_f16v"])
-def test_attention_large_score_range(gpu_device, mode):
-    """Scores spanning > 100 in log space force rescales of the running max late in the sweep."""
+@pytest.mark.parametrize("mode,gain", [("bf16", 12.0), ("bf16_f16v", 12.0), ("bf16_f16v_dma", 12.0),
+                                       ("bf16_f16v_dma", 3.0), ("bf16_f16v_dma", 40.0)])
+def test_attention_large_score_range(gpu_device, mode, gain):
+    """Scores spanning > 100 in log space force rescales of the running max late in the sweep.
+    DMA kernel: its tiles skip the max unless the fp16 row sum overflows the lazy limit, so a
+    late jump (gain 12), a mild one (3, rescales within the slack) and one past f32 exp2's range
+    (40: p = inf against the stale max) must all come out through the recompute path."""
     code, dt, _ = DT["bf16"]
     vdt = dt
-    if mode == "bf16_f16v":
+    if mode.startswith("bf16_f16v"):
         code, vdt = SPE_DTYPE_BF16_F16V, torch.float16
     B, H, T = 1, 8, 256
     g = torch.Generator(device="cpu").manual_seed(0)
     Q = torch.randn(B * T, 256, generator=g).to(gpu_device, dt)
     K = torch.randn(B * T, 256, generator=g)
-    K[200:] *= 12.0                                    # late keys dominate
+    K[200:] *= gain                                    # late keys dominate
     K = K.to(gpu_device, dt)
     V = torch.randn(B, H, T, 32, generator=g).to(gpu_device, vdt)
     O = torch.zeros(B * T, 256, dtype=dt, device=gpu_device)
     scale = 32 ** -0.5
-    assert _lib.lib().spe_debug_attention(None, code, _p(Q), 256, _p(K), 256, _p(V.transpose(-1, -2).contiguous()),
-                                          _p(O), 256, B, H, T, T, scale) == 0
+    VT = V.transpose(-1, -2).contiguous()
+    if mode.endswith("_dma"):
+        code, VT = code | 0x100, _vt_swizzle(VT)
+    assert _lib.lib().spe_debug_attention(None, code, _p(Q), 256, _p(K), 256, _p(VT), _p(O), 256, B, H, T, T,
+                                          scale) == 0
     torch.cuda.synchronize()
     q = Q.view(B, T, H, 32).transpose(1, 2)
     q = (q.float() * scale * 1.4426950408889634).to(dt).float() / (scale * 1.4426950408889634)
