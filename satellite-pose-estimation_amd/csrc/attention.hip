@@ -37,6 +37,9 @@ constexpr float LOG2E = 1.4426950408889634f;
 constexpr float NEG_BIG = -1.0e30f;    // finite "minus infinity" (exp2 of it underflows to 0)
 constexpr float RESCALE_SLACK = 8.0f;  // log2 units (bf16 path)
 constexpr float LAZY_LIMIT = 4096.0f;  // fp16-P tiles: a lane's 32-key sum that forces the max path
+#ifndef SPE_ATTN_PACK
+#define SPE_ATTN_PACK 1
+#endif
 #ifndef SPE_ATTN_LAZY
 #define SPE_ATTN_LAZY 1
 #endif
@@ -215,8 +218,9 @@ template <> struct AT<f16> {
 // DMA: K and V^T tiles go global -> LDS by buffer_load ... lds (V^T stored in vt_pos order by the
 // v projection, so each 16-byte chunk lands verbatim), through a three-slot ring with two tiles
 // in flight: no staging registers, no ds_write, no per-tile vmcnt(0) before a store.  Each
-// wave issues exactly three 1 KB pieces per tile (10 pieces: K 5, V^T 5; two duplicates), so
-// one immediate vmcnt retires a tile.  Needs Tk % 16 == 0 (the quad swap stays inside a row).
+// wave issues exactly two 1 KB pieces per tile (unpadded XOR-swizzled images: K 4, V^T 4; the
+// padded images took 10 pieces, 3 per wave with two duplicates), so one immediate vmcnt retires
+// a tile.  Needs Tk % 16 == 0 (the quad swap stays inside a row).
 template <int ROLE, typename TI, typename TV = TI, bool DMA = false>
 __global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn16_kernel(AttnArgs a) {
   typedef AT<TI> A;
@@ -225,9 +229,12 @@ __global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn16_kernel(AttnArgs a) {
   typedef typename AV::v8 vv8;
   constexpr bool HSUM = sizeof(TV) == 2 && !std::is_same<TV, bf16>::value;   // fp16 P: packed sums
   constexpr bool LAZY = HSUM && DMA && SPE_ATTN_LAZY;   // no per-tile max (below)
-  constexpr int KBYTES = KT * KROW, VBYTES = 32 * VROW;
-  constexpr int DSLOT = 10240;                     // DMA slot: K 5 KB + V^T 4.5 KB (+ 0.5 KB spill room)
-  static_assert(KBYTES == 5120 && VBYTES <= DSLOT - KBYTES, "DMA slot");
+  // PACK (DMA): unpadded tiles, XOR-swizzled instead -- K 4 KB + V^T 4 KB = 8 pieces, two per wave
+  constexpr bool PACK = DMA && SPE_ATTN_PACK;
+  constexpr int KBYTES = PACK ? KT * 64 : KT * KROW, VBYTES = PACK ? 32 * KT * 2 : 32 * VROW;
+  constexpr int DSLOT = PACK ? 8192 : 10240;       // DMA slot (padded: K 5 KB + V^T 4.5 KB + 0.5 KB spill room)
+  constexpr int NPC = PACK ? 2 : 3;                // DMA pieces per wave per tile
+  static_assert(KBYTES + VBYTES <= DSLOT, "DMA slot");
   __shared__ __attribute__((aligned(1024))) char smem[DMA ? 3 * DSLOT : 2 * (KBYTES + VBYTES)];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int hh = lane >> 5, r32 = lane & 31;
@@ -273,8 +280,11 @@ __global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn16_kernel(AttnArgs a) {
   const int ntiles = (a.Tk + KT - 1) / KT;
   constexpr int SLOT = KBYTES + VBYTES;
   Stage<TI, KT> st;
-  // DMA pieces of this wave: slots wid, wid + 4, wid + 8 of {K 0-4, V^T 0-4, K 0-1 again}.  Per
-  // lane a fixed voffset; the tile moves the scalar soffset.  Rows past Tk read as zero through
+  // DMA pieces of this wave: slots wid, wid + 4 (PACK: of {K 0-3, V^T 0-3}), or wid, wid + 4,
+  // wid + 8 (padded: of {K 0-4, V^T 0-4, K 0-1 again}).  Per lane a fixed voffset; the tile moves
+  // the scalar soffset.  PACK images (conflict-free for ds_read_b128's 16-lane groups): key row
+  // of 64 B with 16-byte chunk c at slot c ^ ((key >> 2) & 3); V^T row of 128 B with chunk c at
+  // slot c ^ ((d >> 1) & 7) -- a lane-linear DMA piece gets the swizzle on its source addresses.  Rows past Tk read as zero through
   // the descriptors' ranges (this image's K rows, this (image, head)'s V^T block).
   // (b, h and the wave index are wave-uniform; readfirstlane lets the compiler keep the
   // descriptors and the piece selection scalar instead of waterfalling over lanes)
@@ -288,8 +298,22 @@ __global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn16_kernel(AttnArgs a) {
   bool dv[3] = {false, false, false};
   if constexpr (DMA) {
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
+    for (int j = 0; j < NPC; ++j) {
       const int slot = wu + 4 * j;
+      if constexpr (PACK) {
+        const int isv = slot >= 4, pc = slot & 3;
+        if (!isv) {
+          const int key = pc * 16 + (lane >> 2), c = (lane & 3) ^ ((key >> 2) & 3);
+          dvo[j] = key * a.ldk * 2 + c * 16;
+          dlo[j] = pc * 1024;
+        } else {
+          const int d = pc * 8 + (lane >> 3), c = (lane & 7) ^ ((d >> 1) & 7);
+          dvo[j] = (d * a.Tk + c * 8) * 2;
+          dlo[j] = KBYTES + pc * 1024;
+        }
+        dv[j] = isv;
+        continue;
+      }
       const int piece = slot < 10 ? slot : slot - 10;
       const int isv = piece >= 5, pc = isv ? piece - 5 : piece;
       const int o = pc * 1024 + lane * 16;
@@ -308,7 +332,7 @@ __global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn16_kernel(AttnArgs a) {
   auto issue = [&](int kt, int slot) {
     char* base = smem + slot * DSLOT;
 #pragma unroll
-    for (int j = 0; j < 3; ++j) {
+    for (int j = 0; j < NPC; ++j) {
       // (the LDS address is per wave-instruction: lane 0's; lanes follow at 16-byte steps)
       lds_ptr_t dst = (lds_ptr_t)(base + dlo[j]);
       if (dv[j]) __builtin_amdgcn_raw_ptr_buffer_load_lds(rv, dst, 16, dvo[j], kt * KT * 2, 0, 0);
@@ -323,6 +347,15 @@ __global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn16_kernel(AttnArgs a) {
     st.store(smem, smem + KBYTES, tid);
     __syncthreads();
   }
+  // fragment offsets in a staged tile: K (key sub * 32 + r32, 16-byte chunk c), V^T (row r32, the
+  // chunk of keys sub * 32 + 16 ks + 8 hh)
+  auto koff = [&](int sub, int c) {
+    return PACK ? (sub * 32 + r32) * 64 + ((c ^ ((r32 >> 2) & 3)) << 4) : k_off_bf16(sub * 32 + r32, c);
+  };
+  auto voff = [&](int sub, int ks) {
+    const int ch = (2 * sub + ks) * 2 + hh;
+    return PACK ? r32 * 128 + ((ch ^ ((r32 >> 1) & 7)) << 4) : r32 * VROW + ch * 16;
+  };
   for (int kt = 0; kt < ntiles; ++kt) {
     const char* kl = smem + (DMA ? (kt % 3) * DSLOT : (kt & 1) * SLOT);
     const char* vl = kl + KBYTES;
@@ -330,7 +363,7 @@ __global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn16_kernel(AttnArgs a) {
     if constexpr (DMA) {
       // tile kt landed (tile kt+1 may stay in flight), then the barrier: tile kt visible to all,
       // every wave done with tile kt-1, whose slot takes tile kt+2
-      if (more) __builtin_amdgcn_s_waitcnt(attn_waitcnt_vm(3));
+      if (more) __builtin_amdgcn_s_waitcnt(attn_waitcnt_vm(NPC));
       else __builtin_amdgcn_s_waitcnt(attn_waitcnt_vm(0));
       __builtin_amdgcn_s_barrier();
       if (kt + 2 < ntiles) issue(kt + 2, (kt + 2) % 3);
@@ -346,14 +379,14 @@ __global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn16_kernel(AttnArgs a) {
       u32x4 kf[2][2], vf[2][2];
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub) {
-        kf[sub][0] = ld16(kl + k_off_bf16(sub * 32 + r32, hh));
-        kf[sub][1] = ld16(kl + k_off_bf16(sub * 32 + r32, 2 + hh));
+        kf[sub][0] = ld16(kl + koff(sub, hh));
+        kf[sub][1] = ld16(kl + koff(sub, 2 + hh));
       }
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub)
 #pragma unroll
         for (int ks = 0; ks < 2; ++ks)      // keys sub*32 + 16ks + {4hh..+3, 8+4hh..+3}
-          vf[sub][ks] = ld16(vl + r32 * VROW + (2 * sub + ks) * 32 + hh * 16);
+          vf[sub][ks] = ld16(vl + voff(sub, ks));
       f32x16 s0, s1;                    // s - m
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub) {
@@ -422,8 +455,8 @@ __global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn16_kernel(AttnArgs a) {
 #pragma unroll
         for (int sub = 0; sub < 2; ++sub) {
           f32x16& s = sub ? s1 : s0;
-          s = A::mfma(__builtin_bit_cast(v8, ld16(kl + k_off_bf16(sub * 32 + r32, hh))), qf[0], negm);
-          s = A::mfma(__builtin_bit_cast(v8, ld16(kl + k_off_bf16(sub * 32 + r32, 2 + hh))), qf[1], s);
+          s = A::mfma(__builtin_bit_cast(v8, ld16(kl + koff(sub, hh))), qf[0], negm);
+          s = A::mfma(__builtin_bit_cast(v8, ld16(kl + koff(sub, 2 + hh))), qf[1], s);
         }
       }
       ls += tsum;
