@@ -299,6 +299,11 @@ int spe_debug_btail(void* stream, const void* a, int lda, int k1, const void* r,
                     const float* b3, void* y, const void* w1p, int ld1, const float* b1, void* z, int n2, int M);
 /* the K-column order btail's second product expects: stored column k holds channel perm(k) */
 int spe_debug_btail_perm(int k);
+/* stempool (bf16, stempool.hip): out [B][Po][Po] rows of stride ldo (Po = S/4 for S % 4 == 0) =
+ * maxpool3x3/s2/p1(relu(conv7x7/s2/p3(image) + bias)) from x = the zero-bordered pair-packed
+ * input [B][S+6][S+6][4] and w [64][ldw] with k = (kh*8 + kw)*4 + ci (registry.cpp's stem). */
+int spe_debug_stempool(void* stream, const void* x, const void* w, int ldw, const float* bias, void* out, int ldo,
+                       int B, int S);
 
 #ifdef __cplusplus
 }

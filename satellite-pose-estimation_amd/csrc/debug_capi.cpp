@@ -91,4 +91,11 @@ int spe_debug_btail(void* stream, const void* a, int lda, int k1, const void* r,
 
 int spe_debug_btail_perm(int k) { return spe_btail_perm(k); }
 
+int spe_debug_stempool(void* stream, const void* x, const void* w, int ldw, const float* bias, void* out, int ldo,
+                       int B, int S) {
+  if (!x || !w || !bias || !out || B < 0) return spe_fail(SPE_E_ARG, "bad argument");
+  const int rc = spe_launch_stempool(x, w, ldw, bias, out, ldo, B, S, (hipStream_t)stream);
+  return rc != 0 ? spe_fail(SPE_E_LAUNCH, "stempool launch rejected its arguments") : 0;
+}
+
 }  // extern "C"

@@ -181,12 +181,6 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
                  [&] { return spe_launch_pack_input_pad4(images, P(w.x0), B, S, s); }));
   else
     CK(run_other(m, "eltwise.pack", 0.0, (double)B * S * S * (12 + 8 * m->esz), s, [&] { return spe_launch_pack_input(images, P(w.x0), B, S, dt, s); }));
-  {
-    GemmArgs g = pairs ? conv_args(m->stem, P(w.x0), B, S + 6, S + 6, P(w.stem), 64)
-                       : conv_args(m->stem, P(w.x0), B, S, S, P(w.stem), 64);
-    g.act = ACT_RELU;
-    CK(run_gemm(m, "conv.stem", g, GEMM_CONV, s));
-  }
   int H = S / 2;
   const int Hp = (H + 2 - 3) / 2 + 1;
   // bf16: layer1 block 0's conv3 + downsample run as one GEMM over [conv2 output | pool output]
@@ -196,7 +190,22 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   const bool fuse0 = b0.c3ds.w != nullptr;
   const int uld = fuse0 ? b0.c3ds.K : 64;
   const size_t pool_at = fuse0 ? w.ds + (size_t)b0.c2.N * m->esz : w.pool;
-  CK(run_other(m, "eltwise.maxpool", 0.0, (double)B * 64 * (H * H + Hp * Hp) * m->esz, s, [&] { return spe_launch_maxpool3s2(P(w.stem), P(pool_at), B, H, H, 64, Hp, Hp, dt, s, uld); }));
+  if (pairs && spe_stempool_enabled() && spe_stempool_fits(S)) {
+    // stem + bias + ReLU + max-pool in one pass (stempool.hip): the stem output stays in registers
+    const double flops = 2.0 * B * H * H * 64 * 7 * 8 * 4;
+    const double bytes = (double)B * (S + 6) * (S + 6) * 8 + (double)B * Hp * Hp * 64 * m->esz;
+    CK(run_other(m, "conv.stem", flops, bytes, s, [&] {
+      return spe_launch_stempool(P(w.x0), m->stem.w, m->stem.Kpad, m->stem.bias, P(pool_at), uld, B, S, s);
+    }));
+  } else {
+    {
+      GemmArgs g = pairs ? conv_args(m->stem, P(w.x0), B, S + 6, S + 6, P(w.stem), 64)
+                         : conv_args(m->stem, P(w.x0), B, S, S, P(w.stem), 64);
+      g.act = ACT_RELU;
+      CK(run_gemm(m, "conv.stem", g, GEMM_CONV, s));
+    }
+    CK(run_other(m, "eltwise.maxpool", 0.0, (double)B * 64 * (H * H + Hp * Hp) * m->esz, s, [&] { return spe_launch_maxpool3s2(P(w.stem), P(pool_at), B, H, H, 64, Hp, Hp, dt, s, uld); }));
+  }
   H = Hp;
   size_t cur = pool_at;                                 // (w.pool aliases bufA)
   int cin = 64, cur_ld = uld;

@@ -135,6 +135,13 @@ int spe_launch_preprocess(const uint8_t* frames, int B, int H, int W, int C, con
 int spe_launch_pack_input(const float* img, void* out, int B, int S, int dtype, hipStream_t s);
 // bf16 [B][S+6][S+6][4], zero border of 3 (the pair-packed stem's input, forward.cpp)
 int spe_launch_pack_input_pad4(const float* img, void* out, int B, int S, hipStream_t s);
+// bf16 pair-packed stem (x: spe_launch_pack_input_pad4 layout, w: [64][ldw] k = (kh*8 + kw)*4 + ci)
+// + bias + ReLU + 3x3/s2/p1 max-pool in one pass (stempool.hip); out [B][Po][Po] rows of stride
+// ldo.  Returns 1 when the shape does not fit the kernel.
+bool spe_stempool_enabled();
+bool spe_stempool_fits(int S);
+int spe_launch_stempool(const void* x, const void* w, int ldw, const float* bias, void* out, int ldo, int B, int S,
+                        hipStream_t s);
 int spe_launch_maxpool3s2(const void* in, void* out, int B, int H, int W, int C, int Ho, int Wo,
                           int dtype, hipStream_t s, int ldo = 0);   // ldo: output row stride (0 = C)
 int spe_launch_upsample2x(const void* in, void* out, int B, int H, int W, int C, int dtype, hipStream_t s);

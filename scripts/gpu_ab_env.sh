@@ -9,5 +9,5 @@ if [ -n "$TESTK" ]; then
 fi
 for v in $A $B $A $B; do
   env $VAR=$v timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-accuracy $BENCH_ARGS > gpurun_out/ab_e_$v.log 2>&1 || { tail -20 gpurun_out/ab_e_$v.log; exit 3; }
-  echo "$VAR=$v $(tail -1 gpurun_out/ab_e_$v.log | grep -o '"value": [0-9.]*') $(tail -1 gpurun_out/ab_e_$v.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); k=d['kernel_time_ms_per_step']; print({x: round(k[x],3) for x in ('attn.enc','ffn.enc','conv.1x1','gemm.enc.qk','gemm.enc.o','conv.neck') if x in k})")"
+  echo "$VAR=$v $(tail -1 gpurun_out/ab_e_$v.log | grep -o '"value": [0-9.]*') $(tail -1 gpurun_out/ab_e_$v.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); k=d['kernel_time_ms_per_step']; print({x: round(k[x],3) for x in ${KEYS:-('attn.enc','ffn.enc','conv.1x1','gemm.enc.qk','gemm.enc.o','conv.neck')} if x in k})")"
 done

@@ -350,6 +350,36 @@ def test_btail(gpu_device, M, k1, n2, res):
     _close(Z, zref, DT["bf16"][2])
 
 
+# the fused stem + bias + ReLU + max-pool (stempool.hip): the bench's 416^2 (one column group,
+# 15 waves), a small image, 640^2 (config 5: two column groups, an idle wave) and a strided
+# output row (the pool writes the right half of layer 1 block 0's [conv2 | pool] concatenation)
+@pytest.mark.parametrize("B,S,ldo", [(2, 416, 64), (3, 64, 64), (1, 640, 64), (2, 416, 128)])
+def test_stempool(gpu_device, B, S, ldo):
+    L = _lib.lib()
+    dt = torch.bfloat16
+    g = torch.Generator(device="cpu").manual_seed(B * S + ldo)
+    img = torch.randn(B, 3, S, S, generator=g)
+    X = torch.zeros(B, S + 6, S + 6, 4)
+    X[:, 3:S + 3, 3:S + 3, :3] = img.permute(0, 2, 3, 1)
+    X = X.to(gpu_device, dt)
+    W7 = torch.randn(64, 3, 7, 7, generator=g) / 8
+    Wp = torch.zeros(64, 7, 8, 4)
+    Wp[:, :, :7, :3] = W7.permute(0, 2, 3, 1)
+    Wp = torch.cat([Wp.reshape(64, 224), torch.zeros(64, 32)], 1).to(gpu_device, dt)
+    bias = (0.2 * torch.randn(64, generator=g)).to(gpu_device)
+    Po = S // 4
+    out = torch.full((B, Po, Po, ldo), float("nan"), dtype=dt, device=gpu_device)
+    rc = L.spe_debug_stempool(None, _p(X), _p(Wp), 256, _p(bias), _p(out), ldo, B, S)
+    assert rc == 0, L.spe_last_error()
+    torch.cuda.synchronize()
+    xr = X[:, 3:S + 3, 3:S + 3, :3].float().permute(0, 3, 1, 2)
+    wr = Wp[:, :224].float().view(64, 7, 8, 4)[:, :, :7, :3].permute(0, 3, 1, 2)
+    ref = F.max_pool2d(torch.relu(F.conv2d(xr, wr, bias, stride=2, padding=3)), 3, 2, 1).permute(0, 2, 3, 1)
+    _close(out[..., :64], ref, DT["bf16"][2])
+    if ldo > 64:
+        assert torch.isnan(out[..., 64:].float()).all()       # nothing written past the 64 channels
+
+
 def test_gemm_large_tile_head_transposed(gpu_device):
     _, dt, tol = DT["bf16"]
     B, T, K, N = 25, 2704, 256, 512
