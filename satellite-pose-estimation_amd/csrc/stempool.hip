@@ -31,11 +31,22 @@
 namespace {
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
-constexpr int PR = 6;                      // pool rows per band
+// PR pool rows per band, at most MAXW waves (fragments) per workgroup, OCC workgroups per CU
+#ifndef SPE_SP_PR
+#define SPE_SP_PR 4
+#endif
+#ifndef SPE_SP_MAXW
+#define SPE_SP_MAXW 8
+#endif
+#ifndef SPE_SP_OCC
+#define SPE_SP_OCC 2
+#endif
+constexpr int PR = SPE_SP_PR, MAXW = SPE_SP_MAXW, OCC = SPE_SP_OCC;
 constexpr int PROWS = 4 * PR + 7;          // input rows a band reads
 constexpr int WPITCH = 464;                // LDS W row: 448 B of K = 224 + 16 B (29 chunks, odd: conflict-free)
 constexpr int KCH = 28;                    // 16-byte chunks of a W row
-constexpr int LDS_PATCH = 108 * 1024;      // patch capacity
+constexpr int LDS_PATCH = (PROWS * (28 * MAXW + 10) * 8 + 1023) / 1024 * 1024;   // patch capacity
+static_assert(OCC * (LDS_PATCH + 64 * WPITCH) <= 160 * 1024, "LDS");
 constexpr int PBAD = 0x7ffffff0;           // out-of-range buffer offset -> reads zeros
 
 struct SpGeom {
@@ -45,7 +56,7 @@ struct SpGeom {
   int pwid, pitch;                         // patch width (pixels) and row pitch (bytes)
 };
 
-__global__ __launch_bounds__(1024, 1) void stempool_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, int ldw,
+__global__ __launch_bounds__(64 * MAXW, OCC) void stempool_kernel(const bf16* __restrict__ x, const bf16* __restrict__ w, int ldw,
                                                            const float* __restrict__ bias, bf16* __restrict__ out, int ldo,
                                                            SpGeom p) {
   __shared__ __attribute__((aligned(1024))) char lds[LDS_PATCH + 64 * WPITCH];
@@ -171,7 +182,7 @@ bool geom(int S, SpGeom& p) {
   p.So = (S + 6 - 7) / 2 + 1;               // 7x7 / stride 2 over the bordered input (= S / 2 for even S)
   p.Po = (p.So + 2 - 3) / 2 + 1;
   p.nfrag = (p.Po + 6) / 7;
-  p.groups = (p.nfrag + 15) / 16;
+  p.groups = (p.nfrag + MAXW - 1) / MAXW;
   p.fpg = (p.nfrag + p.groups - 1) / p.groups;
   p.bands = (p.Po + PR - 1) / PR;
   p.pwid = 28 * p.fpg + 10;
