@@ -43,6 +43,13 @@ constexpr float LAZY_LIMIT = 4096.0f;  // fp16-P tiles: a lane's 32-key sum that
 #ifndef SPE_ATTN_LAZY
 #define SPE_ATTN_LAZY 1
 #endif
+// DMA kernel: waves per workgroup (4: 128 queries, two DMA pieces per wave per tile; 8: 256
+// queries, one piece per wave -- the piece's issue cost halves -- and two workgroups per CU)
+#ifndef SPE_ATTN_DMA_WAVES
+#define SPE_ATTN_DMA_WAVES 8
+#endif
+constexpr int DMA_WAVES = SPE_ATTN_DMA_WAVES;
+static_assert(DMA_WAVES == 4 || DMA_WAVES == 8, "DMA waves");
 #ifndef SPE_ATTN_OCC
 #define SPE_ATTN_OCC 4
 #endif
@@ -222,28 +229,30 @@ template <> struct AT<f16> {
 // padded images took 10 pieces, 3 per wave with two duplicates), so one immediate vmcnt retires
 // a tile.  Needs Tk % 16 == 0 (the quad swap stays inside a row).
 template <int ROLE, typename TI, typename TV = TI, bool DMA = false>
-__global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn16_kernel(AttnArgs a) {
+__global__ __launch_bounds__(DMA ? 64 * DMA_WAVES : NT, DMA ? 16 / DMA_WAVES : SPE_ATTN_OCC) void attn16_kernel(AttnArgs a) {
   typedef AT<TI> A;
   typedef AT<TV> AV;
   typedef typename A::v8 v8;
   typedef typename AV::v8 vv8;
   constexpr bool HSUM = sizeof(TV) == 2 && !std::is_same<TV, bf16>::value;   // fp16 P: packed sums
   constexpr bool LAZY = HSUM && DMA && SPE_ATTN_LAZY;   // no per-tile max (below)
-  // PACK (DMA): unpadded tiles, XOR-swizzled instead -- K 4 KB + V^T 4 KB = 8 pieces, two per wave
+  // PACK (DMA): unpadded tiles, XOR-swizzled instead -- K 4 KB + V^T 4 KB = 8 pieces, 8 / DMA_WAVES per wave
   constexpr bool PACK = DMA && SPE_ATTN_PACK;
   constexpr int KBYTES = PACK ? KT * 64 : KT * KROW, VBYTES = PACK ? 32 * KT * 2 : 32 * VROW;
   constexpr int DSLOT = PACK ? 8192 : 10240;       // DMA slot (padded: K 5 KB + V^T 4.5 KB + 0.5 KB spill room)
-  constexpr int NPC = PACK ? 2 : 3;                // DMA pieces per wave per tile
+  constexpr int NPC = PACK ? 8 / DMA_WAVES : 3;    // DMA pieces per wave per tile
   static_assert(KBYTES + VBYTES <= DSLOT, "DMA slot");
+  static_assert(!DMA || PACK || DMA_WAVES == 4, "padded DMA images: 4 waves");
   __shared__ __attribute__((aligned(1024))) char smem[DMA ? 3 * DSLOT : 2 * (KBYTES + VBYTES)];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int hh = lane >> 5, r32 = lane & 31;
-  const int qblocks = (a.Tq + 127) / 128;
+  constexpr int QB = 32 * (DMA ? DMA_WAVES : 4);   // queries per workgroup
+  const int qblocks = (a.Tq + QB - 1) / QB;
   const int bid = xcd_remap(blockIdx.x, gridDim.x);
   const int bh = bid / qblocks, qb = bid - bh * qblocks;
   const int b = bh / a.H, h = bh - b * a.H;
-  const int q = qb * 128 + wid * 32 + r32;
-  const bool wave_live = qb * 128 + wid * 32 < a.Tq;
+  const int q = qb * QB + wid * 32 + r32;
+  const bool wave_live = qb * QB + wid * 32 < a.Tq;
 
   // query fragment (B operand of S^T = K . Q^T), pre-scaled into the exp2 domain
   v8 qf[2];
@@ -299,7 +308,7 @@ __global__ __launch_bounds__(NT, SPE_ATTN_OCC) void attn16_kernel(AttnArgs a) {
   if constexpr (DMA) {
 #pragma unroll
     for (int j = 0; j < NPC; ++j) {
-      const int slot = wu + 4 * j;
+      const int slot = wu + DMA_WAVES * j;
       if constexpr (PACK) {
         const int isv = slot >= 4, pc = slot & 3;
         if (!isv) {
@@ -744,6 +753,8 @@ int spe_launch_attention(const AttnArgs& a, int dtype, hipStream_t s) {
   if (a.vt_swz && (a.Tk % 16 || (dtype != SPE_DTYPE_F16 && dtype != SPE_DTYPE_BF16 && dtype != SPE_DTYPE_BF16_F16V)))
     return -5;                                     // (swizzled V^T: 16-bit operands, whole quads per row)
   if (a.vt_swz) {                                  // LDS-DMA staging (the only reader of that layout)
+    grid = dim3(a.B * a.H * ((a.Tq + 32 * DMA_WAVES - 1) / (32 * DMA_WAVES)));
+    block = dim3(64 * DMA_WAVES);
     if (dtype == SPE_DTYPE_F16) {
       if (a.Tq >= 128) hipLaunchKernelGGL((attn16_kernel<0, f16, f16, true>), grid, block, 0, s, a);
       else hipLaunchKernelGGL((attn16_kernel<1, f16, f16, true>), grid, block, 0, s, a);
