@@ -365,8 +365,12 @@ __global__ __launch_bounds__(DMA ? 64 * DMA_WAVES : NT, DMA ? 16 / DMA_WAVES : S
     const int ch = (2 * sub + ks) * 2 + hh;
     return PACK ? r32 * 128 + ((ch ^ ((r32 >> 1) & 7)) << 4) : r32 * VROW + ch * 16;
   };
-  for (int kt = 0; kt < ntiles; ++kt) {
-    const char* kl = smem + (DMA ? (kt % 3) * DSLOT : (kt & 1) * SLOT);
+  // one 64-key step; SC = the DMA ring slot as a compile-time constant (the DMA loop below is
+  // unrolled by the ring's three slots, so every fragment read is a lane base + immediate
+  // offset: no per-step address VALU), -1 for the register-staged kernel
+  auto step = [&](int kt, auto SC) {
+    constexpr int S = decltype(SC)::value;
+    const char* kl = smem + (DMA ? S * DSLOT : (kt & 1) * SLOT);
     const char* vl = kl + KBYTES;
     const bool more = kt + 1 < ntiles;
     if constexpr (DMA) {
@@ -375,7 +379,7 @@ __global__ __launch_bounds__(DMA ? 64 * DMA_WAVES : NT, DMA ? 16 / DMA_WAVES : S
       if (more) __builtin_amdgcn_s_waitcnt(attn_waitcnt_vm(NPC));
       else __builtin_amdgcn_s_waitcnt(attn_waitcnt_vm(0));
       __builtin_amdgcn_s_barrier();
-      if (kt + 2 < ntiles) issue(kt + 2, (kt + 2) % 3);
+      if (kt + 2 < ntiles) issue(kt + 2, (S + 2) % 3);
     } else {
 #ifdef SPE_X_NOSTAGE
       if (more && kt == 0) st.load(a, b, h, kt + 1, tid);
@@ -485,6 +489,15 @@ __global__ __launch_bounds__(DMA ? 64 * DMA_WAVES : NT, DMA ? 16 / DMA_WAVES : S
       __syncthreads();
 #endif
     }
+  };
+  if constexpr (DMA) {
+    for (int kt = 0; kt < ntiles; kt += 3) {
+      step(kt, std::integral_constant<int, 0>{});
+      if (kt + 1 < ntiles) step(kt + 1, std::integral_constant<int, 1>{});
+      if (kt + 2 < ntiles) step(kt + 2, std::integral_constant<int, 2>{});
+    }
+  } else {
+    for (int kt = 0; kt < ntiles; ++kt) step(kt, std::integral_constant<int, -1>{});
   }
 
   if (!wave_live || q >= a.Tq) return;

@@ -39,6 +39,7 @@ def main():
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--only", default="")
     ap.add_argument("--attn-dtype", type=int, default=0, help="0 bf16, 2 fp16, 3 bf16 q/k + fp16 V^T/P")
+    ap.add_argument("--dma", action="store_true", help="the encoder's LDS-DMA attention kernel (V^T key order as stored)")
     a = ap.parse_args()
     L = _lib.lib()
     dev = torch.device("cuda", 0)
@@ -52,8 +53,8 @@ def main():
         vt = torch.randn(B, H, 32, T, generator=g).to(dev, vdt)
         o = torch.empty(B * T, D, dtype=torch.bfloat16, device=dev)
         kp = ctypes.c_void_p(qk.data_ptr() + 256 * 2)
-        fn = lambda: L.spe_debug_attention(None, a.attn_dtype, p(qk), 512, kp, 512, p(vt), p(o), D, B, H, T, T,
-                                           32 ** -0.5)
+        code = a.attn_dtype | (0x100 if a.dma else 0)
+        fn = lambda: L.spe_debug_attention(None, code, p(qk), 512, kp, 512, p(vt), p(o), D, B, H, T, T, 32 ** -0.5)
         ms = timeit(fn, a.iters)
         fl = 4.0 * B * H * T * T * 32
         print(f"attn.enc  {ms:.3f} ms  {fl / ms / 1e9:.1f} TF/s")
