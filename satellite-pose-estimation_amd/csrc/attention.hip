@@ -379,7 +379,9 @@ __global__ __launch_bounds__(DMA ? 64 * DMA_WAVES : NT, DMA ? 16 / DMA_WAVES : S
       if (more) __builtin_amdgcn_s_waitcnt(attn_waitcnt_vm(NPC));
       else __builtin_amdgcn_s_waitcnt(attn_waitcnt_vm(0));
       __builtin_amdgcn_s_barrier();
-      if (kt + 2 < ntiles) issue(kt + 2, (S + 2) % 3);
+      // (live waves issue tile kt+2 after their score MFMAs: a DMA issued ahead of the fragment
+      // reads made the compiler wait for every read, V included, before the first MFMA)
+      if (!wave_live && kt + 2 < ntiles) issue(kt + 2, (S + 2) % 3);
     } else {
 #ifdef SPE_X_NOSTAGE
       if (more && kt == 0) st.load(a, b, h, kt + 1, tid);
@@ -406,6 +408,9 @@ __global__ __launch_bounds__(DMA ? 64 * DMA_WAVES : NT, DMA ? 16 / DMA_WAVES : S
         f32x16& s = sub ? s1 : s0;
         s = A::mfma(__builtin_bit_cast(v8, kf[sub][0]), qf[0], negm);
         s = A::mfma(__builtin_bit_cast(v8, kf[sub][1]), qf[1], s);
+      }
+      if constexpr (DMA) {
+        if (kt + 2 < ntiles) issue(kt + 2, (S + 2) % 3);
       }
       // LAZY (fp16 P): no per-tile max at all.  The tile is exponentiated against the stale
       // running max and its packed-fp16 row sum, formed anyway, is the overflow test: only if
