@@ -22,6 +22,7 @@
 #include "spe_kernels.h"
 
 #include <cstdlib>
+#include <type_traits>
 
 namespace {
 
@@ -407,6 +408,79 @@ __global__ __launch_bounds__(NT, 1) void ffn_pipe_kernel(FfnArgs a) {
   for (int i = 0; i < 16 * MB; ++i) p1(i);
   pack_h(hb);
 
+  // SCHED: the chunk loop unrolled by the ring's four slots (the slot a compile-time constant, so
+  // every fragment read is a lane base + an immediate offset: no per-read address VALU)
+  auto sched_step = [&](int c, auto SC) {
+    constexpr int S = decltype(SC)::value;
+#ifndef SPE_X_FFN_NODMA
+    if (c + 2 < nch) wait_vmcnt<LOADS>();        // chunk c+1 landed, c+2 may stay in flight
+    else wait_vmcnt<0>();
+#endif
+#ifndef SPE_X_FFN_NOBAR
+    sync();
+#endif
+    const char* st = lds + S * STAGE;
+    const char* st1 = lds + ((S + 1) % NST) * STAGE;
+    // read r in consumption order: r < 24 -> block k = r / 3: W1(c+1) ks = k jb 0, W2(c) nb = k,
+    // W1(c+1) ks = k jb 1 (block k feeds interleaved steps MB*k .. MB*k + MB-1);
+    // r >= 24 -> W2(c) nb = r - 16 (the tail)
+    auto rd = [&](int r) {
+#ifdef SPE_X_FFN_NOLDS
+      if (c > 0) return;
+#endif
+      if (r < 24) {
+        const int k = r / 3, q = r % 3;
+        if (q == 1) wb[k] = ld16(st + W1_BYTES + w2_off(16 * k + c16, g));
+        else wa[k][q >> 1] = ld16(st1 + w1_off(16 * (q >> 1) + c16, 4 * k + g));
+      } else {
+        wb[r - 16] = ld16(st + W1_BYTES + w2_off(16 * (r - 16) + c16, g));
+      }
+    };
+    // chunk c+3's pieces are issued unconditionally (a branch would split the MFMA block and
+    // the accumulators get copied across it): past the last chunk the buffer resource's range
+    // check makes them zero-fill the free slot (c+3) % 4, which nothing reads any more
+    char* dst = lds + ((S + 3) % NST) * STAGE;
+    init_h(c + 1);
+#pragma unroll
+    for (int r = 0; r < PRE; ++r) rd(r);
+    __builtin_amdgcn_sched_barrier(0);
+    // interleaved steps t: p1(2t), p1(2t+1), p2(t); 3 reads per MB steps, one DMA piece per MB
+    int issued = PRE;
+#pragma unroll
+    for (int t = 0; t < 8 * MB; ++t) {
+      const int upto = PRE + (3 * (t + 1) + MB - 1) / MB < 32 ? PRE + (3 * (t + 1) + MB - 1) / MB : 32;
+      for (; issued < upto; ++issued) rd(issued);
+#ifndef SPE_X_FFN_NODMA
+      if (t % MB == 1 % MB) dma.piece(a, c + 3, dst, wid, t / MB);
+#endif
+      p1(2 * t);
+      p1(2 * t + 1);
+      p2(t);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    bf16x8 hb_next[MB];
+    // tail: p2(8MB..16MB) in groups of MB (one W2 block each), the remaining reads and
+    // H(c+1)'s pack between them
+#pragma unroll
+    for (int t = 8 * MB; t < 16 * MB; t += MB) {
+      if (issued < 32) rd(issued++);
+#pragma unroll
+      for (int u = 0; u < MB; ++u) p2(t + u);
+      if (t == 9 * MB) pack_h(hb_next);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) hb[mb] = hb_next[mb];
+  };
+  if constexpr (SCHED) {
+    static_assert(NST == 4, "unrolled by the ring's slots");
+    for (int c = 0; c + 1 < nch; c += NST) {
+      sched_step(c, std::integral_constant<int, 0>{});
+      if (c + 2 < nch) sched_step(c + 1, std::integral_constant<int, 1>{});
+      if (c + 3 < nch) sched_step(c + 2, std::integral_constant<int, 2>{});
+      if (c + 4 < nch) sched_step(c + 3, std::integral_constant<int, 3>{});
+    }
+  } else
   for (int c = 0; c + 1 < nch; ++c) {
 #ifndef SPE_X_FFN_NODMA
     if (c + 2 < nch) wait_vmcnt<LOADS>();        // chunk c+1 landed, c+2 may stay in flight
@@ -417,59 +491,6 @@ __global__ __launch_bounds__(NT, 1) void ffn_pipe_kernel(FfnArgs a) {
 #endif
     const char* st = lds + (c % NST) * STAGE;
     const char* st1 = lds + ((c + 1) % NST) * STAGE;
-    if constexpr (SCHED) {
-      // read r in consumption order: r < 24 -> block k = r / 3: W1(c+1) ks = k jb 0, W2(c) nb = k,
-      // W1(c+1) ks = k jb 1 (block k feeds interleaved steps MB*k .. MB*k + MB-1);
-      // r >= 24 -> W2(c) nb = r - 16 (the tail)
-      auto rd = [&](int r) {
-#ifdef SPE_X_FFN_NOLDS
-        if (c > 0) return;
-#endif
-        if (r < 24) {
-          const int k = r / 3, q = r % 3;
-          if (q == 1) wb[k] = ld16(st + W1_BYTES + w2_off(16 * k + c16, g));
-          else wa[k][q >> 1] = ld16(st1 + w1_off(16 * (q >> 1) + c16, 4 * k + g));
-        } else {
-          wb[r - 16] = ld16(st + W1_BYTES + w2_off(16 * (r - 16) + c16, g));
-        }
-      };
-      // chunk c+3's pieces are issued unconditionally (a branch would split the MFMA block and
-      // the accumulators get copied across it): past the last chunk the buffer resource's range
-      // check makes them zero-fill the free slot (c+3) % 4, which nothing reads any more
-      char* dst = lds + ((c + 3) % NST) * STAGE;
-      init_h(c + 1);
-#pragma unroll
-      for (int r = 0; r < PRE; ++r) rd(r);
-      __builtin_amdgcn_sched_barrier(0);
-      // interleaved steps t: p1(2t), p1(2t+1), p2(t); 3 reads per MB steps, one DMA piece per MB
-      int issued = PRE;
-#pragma unroll
-      for (int t = 0; t < 8 * MB; ++t) {
-        const int upto = PRE + (3 * (t + 1) + MB - 1) / MB < 32 ? PRE + (3 * (t + 1) + MB - 1) / MB : 32;
-        for (; issued < upto; ++issued) rd(issued);
-#ifndef SPE_X_FFN_NODMA
-        if (t % MB == 1 % MB) dma.piece(a, c + 3, dst, wid, t / MB);
-#endif
-        p1(2 * t);
-        p1(2 * t + 1);
-        p2(t);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      bf16x8 hb_next[MB];
-      // tail: p2(8MB..16MB) in groups of MB (one W2 block each), the remaining reads and
-      // H(c+1)'s pack between them
-#pragma unroll
-      for (int t = 8 * MB; t < 16 * MB; t += MB) {
-        if (issued < 32) rd(issued++);
-#pragma unroll
-        for (int u = 0; u < MB; ++u) p2(t + u);
-        if (t == 9 * MB) pack_h(hb_next);
-        __builtin_amdgcn_sched_barrier(0);
-      }
-#pragma unroll
-      for (int mb = 0; mb < MB; ++mb) hb[mb] = hb_next[mb];
-      continue;
-    }
 #ifdef SPE_X_FFN_NOLDS
     if (c == 0) {
 #endif
