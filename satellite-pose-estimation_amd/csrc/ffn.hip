@@ -318,7 +318,9 @@ __global__ __launch_bounds__(NT, 1) void ffn_pipe_kernel(FfnArgs a) {
   constexpr int NST = 4;
   __shared__ __attribute__((aligned(1024))) char lds[NST * STAGE + FMAX * 4];
   float* sb1 = reinterpret_cast<float*>(lds + NST * STAGE);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  // (wid wave-uniform in a scalar register: the DMA pieces' LDS addresses (m0) then need no
+  // v_readfirstlane per piece)
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, c16 = lane & 15;
   const int m0 = a.row0 + blockIdx.x * 64 * MB + wid * 16 * MB;
   const int nch = a.F / HC;
