@@ -182,7 +182,7 @@ __global__ __launch_bounds__(NT, 1) void ffn_ln_kernel(FfnArgs a) {
   // compiler drain vmcnt before LDS reads): [NSTAGE weight stages][b1]
   __shared__ __attribute__((aligned(1024))) char lds[NSTAGE * STAGE + FMAX * 4];
   float* sb1 = reinterpret_cast<float*>(lds + NSTAGE * STAGE);
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, c16 = lane & 15;
   // split-F mode (few rows, e.g. the decoder's B*Q): block = (row tile, hidden-unit range);
   // the partial out^T of each range goes to a.partial and ffn_reduce_ln_kernel finishes

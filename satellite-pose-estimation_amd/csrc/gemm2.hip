@@ -81,7 +81,7 @@ __global__ __launch_bounds__(NT, NST == 1 ? 4 : 1) void gemm2_kernel(GemmArgs g)
   constexpr int SMEM = (NST * STAGE > EPI_ROWS * EPI_LD * 4) ? NST * STAGE : EPI_ROWS * EPI_LD * 4;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wid / WN, wc = wid % WN;
   const int tilesN = (g.N + BN - 1) / BN;
   const int t = xcd_remap(blockIdx.x, gridDim.x);
@@ -770,7 +770,7 @@ template <bool VT>
 __global__ __launch_bounds__(SM_NT) void gemm_small_kernel(GemmArgs g) {
   constexpr int ROWB = SM_KMAX * 2;                  // 512 B LDS row (K = 256 bf16)
   __shared__ __attribute__((aligned(1024))) char lds[2 * SM_T * ROWB];   // A tile | W tile
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int tilesN = (g.N + SM_T - 1) / SM_T;
   const int m0 = (blockIdx.x / tilesN) * SM_T, n0 = (blockIdx.x % tilesN) * SM_T;
   const char* zero = reinterpret_cast<const char*>(g_zero_line);

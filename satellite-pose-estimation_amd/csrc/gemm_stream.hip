@@ -64,7 +64,7 @@ __global__ __launch_bounds__(256, OCC) void sgemm_kernel(GemmArgs g, int ns_coun
   // in registers for the kernel's life
   __shared__ __attribute__((aligned(16))) float sb[BN], slg[EPI == EPI_LN ? BN : 1], slb[EPI == EPI_LN ? BN : 1];
 
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int fg = lane >> 4, fr = lane & 15;
   const int G = gridDim.x;
   const int gid = xcd_remap(blockIdx.x, G);

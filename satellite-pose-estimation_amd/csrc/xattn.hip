@@ -72,7 +72,7 @@ SPE_DEV u32x2 ds_read_tr(uint32_t addr) {
 
 __global__ __launch_bounds__(NT, 1) void xattn_kernel(XattnArgs a) {
   __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hh = lane >> 5, r32 = lane & 31, l16 = lane & 15, dg = 16 * ((lane >> 4) & 1);
   const int R = 8 * a.Q, ngroups = (R + RG - 1) / RG;
   int bid = blockIdx.x;
