@@ -55,28 +55,38 @@ __global__ __launch_bounds__(NT, 1) void lnproj_kernel(GemmArgs g, int row_tiles
     for (int j = 0; j < JF; ++j) r[j] = ld8(pr + j * 32);
   };
 
+  // W fragment bases: row 16j+fr, chunk 4kf+fg lives at wb[kf&1][j>>3] + (j&7)*8192 + (kf>>1)*128 (all
+  // immediates); the bases are opaque to the compiler so it cannot re-derive one address register per (j, kf).
+  int wb[2][2];
+#pragma unroll
+  for (int p = 0; p < 2; ++p)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      wb[p][h] = w_addr(fr + 128 * h, 4 * p + fg);
+      asm volatile("" : "+v"(wb[p][h]));
+    }
   auto tile = [&](int t, const u32x4 (&x)[KF], const u32x2 (&r)[JF]) {
     asm volatile("" ::: "memory");              // (W fragments: loop-invariant LDS reads, not hoisted)
+    // accumulators start at the bias (no bias adds in the epilogue)
     f32x4 acc[JF];
 #pragma unroll
-    for (int j = 0; j < JF; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < JF; ++j) acc[j] = *reinterpret_cast<const f32x4*>(sb + 16 * j + 4 * fg);
 #pragma unroll
     for (int kf = 0; kf < KF; ++kf) {
       const bf16x8 av = __builtin_bit_cast(bf16x8, x[kf]);
 #pragma unroll
       for (int j = 0; j < JF; ++j)
-        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, ld16(wl + w_addr(16 * j + fr, 4 * kf + fg))),
-                                                         av, acc[j], 0, 0, 0);
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            __builtin_bit_cast(bf16x8, ld16(wl + wb[kf & 1][j >> 3] + (j & 7) * 8192 + (kf >> 1) * 128)), av, acc[j], 0, 0, 0);
     }
     // lane: row m = fr, columns 16j + 4fg + e
     float s = 0.f;
 #pragma unroll
     for (int j = 0; j < JF; ++j) {
-      const f32x4 bv = *reinterpret_cast<const f32x4*>(sb + 16 * j + 4 * fg);
-      acc[j][0] += bv[0] + __uint_as_float(r[j].x << 16);
-      acc[j][1] += bv[1] + __uint_as_float(r[j].x & 0xffff0000u);
-      acc[j][2] += bv[2] + __uint_as_float(r[j].y << 16);
-      acc[j][3] += bv[3] + __uint_as_float(r[j].y & 0xffff0000u);
+      acc[j][0] += __uint_as_float(r[j].x << 16);
+      acc[j][1] += __uint_as_float(r[j].x & 0xffff0000u);
+      acc[j][2] += __uint_as_float(r[j].y << 16);
+      acc[j][3] += __uint_as_float(r[j].y & 0xffff0000u);
       s += (acc[j][0] + acc[j][1]) + (acc[j][2] + acc[j][3]);
     }
     s += __shfl_xor(s, 16, 64);
