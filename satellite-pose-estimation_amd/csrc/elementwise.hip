@@ -114,50 +114,114 @@ __global__ void upsample_kernel(const T* __restrict__ in, T* __restrict__ out, i
 //   out[Y][X][c] = sum_t [U = Y+dy, V = X+dx inside the 2h x 2w grid] bilerp(Z[.][t*C + c], U, V)
 // with bilerp the upsample kernel's weights above.  (REV/models/backbone.py:141
 // s16_latern(up16sto8s(xs16)): 4x fewer MFMA flops and no 2h x 2w x Cin intermediate.)
-// One thread per 8 output channels of one output pixel; fp32 sums, one rounding at the store.
+// A thread owns one 16-byte channel chunk of one output row Y and walks a segment of UC_SEG
+// output columns.  Per tap (dy, dx) and source row (y0, y1) it keeps the two corner chunks x0, x1
+// in registers; stepping X -> X+1 moves every tap's source column V = X+dx-1 by one output
+// pixel, i.e. by sx < 1/2 low-resolution columns, so x0 advances by 0 or 1 -- uniformly over the
+// workgroup (it depends on V only): an advance shifts x1 into x0 and loads the new x1.  About 9
+// instead of 36 16-byte reads per output chunk (the reads were the kernel's cost: each Z element
+// was fetched 16 times through L2).  fp32 sums in the order of the one-pixel form, one rounding
+// at the store.
+#ifndef SPE_UC_SEG
+#define SPE_UC_SEG 8
+#endif
+constexpr int UC_SEG = SPE_UC_SEG;
 template <typename T>
-__global__ void upconv_combine_kernel(const T* __restrict__ z, T* __restrict__ out, int ldo, int B, int H, int W, int C) {
+__global__ __launch_bounds__(256) void upconv_combine_kernel(const T* __restrict__ z, T* __restrict__ out, int ldo, int B, int H,
+                                                             int W, int C) {
   constexpr int CE = Chunk<T>::CE;
   const int Ho = 2 * H, Wo = 2 * W, cch = C / CE;
-  const size_t ldz = (size_t)9 * C;
-  const float sy = Ho > 1 ? (float)(H - 1) / (float)(Ho - 1) : 0.f;
-  const float sx = Wo > 1 ? (float)(W - 1) / (float)(Wo - 1) : 0.f;
-  const size_t n = (size_t)B * Ho * Wo * cch;
-  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
-    const int c = (int)(i % cch);
-    size_t r = i / cch;
-    const int ox = (int)(r % Wo); r /= Wo;
-    const int oy = (int)(r % Ho);
-    const int b = (int)(r / Ho);
-    const T* zb = z + (size_t)b * H * W * ldz + c * CE;
+  const int ldz = 9 * C;
+  const float sy = (float)(H - 1) / (float)(Ho - 1);
+  const float sx = (float)(W - 1) / (float)(Wo - 1);
+  const int j = blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= B * Ho * cch) return;
+  const int c = j % cch, r = j / cch, Y = r % Ho, b = r / Ho;
+  const int X0 = blockIdx.y * UC_SEG, X1 = min(X0 + UC_SEG, Wo);
+  const T* zb = z + (size_t)b * H * W * ldz + c * CE;
+  // per dy: the two source rows (clamped in range; a row outside the 2H grid contributes nothing)
+  const T* zr[3][2];
+  float wy[3][2];
+#pragma unroll
+  for (int dy = 0; dy < 3; ++dy) {
+    const int U = Y + dy - 1;
+    const bool in = U >= 0 && U < Ho;
+    const float fy = (in ? U : 0) * sy;
+    const int y0 = (int)fy, y1 = y0 + (y0 < H - 1);
+    const float ly = fy - y0;
+    wy[dy][0] = in ? 1.f - ly : 0.f;
+    wy[dy][1] = ly;
+    zr[dy][0] = zb + (size_t)y0 * W * ldz + dy * 3 * C;
+    zr[dy][1] = zb + (size_t)y1 * W * ldz + dy * 3 * C;
+  }
+  auto col = [&](int V, int& x0, int& x1, float& lx) {
+    const float fx = (V < 0 ? 0 : V) * sx;
+    x0 = min((int)fx, W - 1);
+    x1 = x0 + (x0 < W - 1);
+    lx = fx - x0;
+  };
+  u32x4 q0[3][3][2], q1[3][3][2];                 // [dy][dx][row]: corners x0, x1
+  int xs[3];
+#pragma unroll
+  for (int dx = 0; dx < 3; ++dx) {
+    int x0, x1;
+    float lx;
+    col(X0 + dx - 1, x0, x1, lx);
+    xs[dx] = x0;
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        q0[dy][dx][h] = ld16(zr[dy][h] + (size_t)x0 * ldz + dx * C);
+        q1[dy][dx][h] = ld16(zr[dy][h] + (size_t)x1 * ldz + dx * C);
+      }
+  }
+  for (int X = X0; X < X1; ++X) {
+    // the corner state stays packed across iterations (unpacked per use, not carried as floats)
+#pragma unroll
+    for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 3; ++dx)
+#pragma unroll
+        for (int h = 0; h < 2; ++h) asm volatile("" : "+v"(q0[dy][dx][h]), "+v"(q1[dy][dx][h]));
     float acc[CE];
 #pragma unroll
     for (int e = 0; e < CE; ++e) acc[e] = 0.f;
 #pragma unroll
-    for (int dy = -1; dy <= 1; ++dy) {
-      const int U = oy + dy;
-      if (U < 0 || U >= Ho) continue;
-      const float fy = U * sy;
-      const int y0 = (int)fy, y1 = y0 + (y0 < H - 1);
-      const float ly = fy - y0, hy = 1.f - ly;
+    for (int dy = 0; dy < 3; ++dy) {
+      const float hy = wy[dy][0], ly = wy[dy][1];
 #pragma unroll
-      for (int dx = -1; dx <= 1; ++dx) {
-        const int V = ox + dx;
+      for (int dx = 0; dx < 3; ++dx) {
+        const int V = X + dx - 1;
         if (V < 0 || V >= Wo) continue;
-        const float fx = V * sx;
-        const int x0 = (int)fx, x1 = x0 + (x0 < W - 1);
-        const float lx = fx - x0, hx = 1.f - lx;
-        const T* zt = zb + (size_t)((dy + 1) * 3 + dx + 1) * C;
+        const float lx = V * sx - xs[dx], hx = 1.f - lx;
         float a[CE], bb[CE], cc[CE], d[CE];
-        unpack16<T>(ld16(zt + ((size_t)y0 * W + x0) * ldz), a);
-        unpack16<T>(ld16(zt + ((size_t)y0 * W + x1) * ldz), bb);
-        unpack16<T>(ld16(zt + ((size_t)y1 * W + x0) * ldz), cc);
-        unpack16<T>(ld16(zt + ((size_t)y1 * W + x1) * ldz), d);
+        unpack16<T>(q0[dy][dx][0], a);
+        unpack16<T>(q1[dy][dx][0], bb);
+        unpack16<T>(q0[dy][dx][1], cc);
+        unpack16<T>(q1[dy][dx][1], d);
 #pragma unroll
         for (int e = 0; e < CE; ++e) acc[e] += hy * (hx * a[e] + lx * bb[e]) + ly * (hx * cc[e] + lx * d[e]);
       }
     }
-    st16(out + (((size_t)b * Ho + oy) * Wo + ox) * ldo + c * CE, pack16<T>(acc));
+    st16(out + (((size_t)b * Ho + Y) * Wo + X) * ldo + c * CE, pack16<T>(acc));
+    if (X + 1 >= X1) break;
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) {
+      int x0, x1;
+      float lx;
+      col(X + dx, x0, x1, lx);
+      if (x0 != xs[dx]) {                        // uniform: x0 advanced by one
+        xs[dx] = x0;
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            q0[dy][dx][h] = q1[dy][dx][h];
+            q1[dy][dx][h] = ld16(zr[dy][h] + (size_t)x1 * ldz + dx * C);
+          }
+      }
+    }
   }
 }
 
@@ -239,11 +303,13 @@ int spe_launch_upsample2x(const void* in, void* out, int B, int H, int W, int C,
 int spe_launch_upconv_combine(const void* z, void* out, int ldo, int B, int H, int W, int C, int dtype, hipStream_t s) {
   const int ce = dtype == SPE_DTYPE_BF16 ? 8 : 4;
   if (C % ce || ldo % ce || ldo < C) return -5;
-  const size_t n = (size_t)B * 4 * H * W * (C / ce);
+  if (H < 1 || W < 1 || (size_t)B * 2 * H * (C / ce) >= (1u << 31) || (size_t)B * H * W * 9 * C >= (1ull << 40)) return -5;
+  const int rows = B * 2 * H * (C / ce);
+  dim3 grid((rows + 255) / 256, (2 * W + UC_SEG - 1) / UC_SEG);
   if (dtype == SPE_DTYPE_BF16)
-    hipLaunchKernelGGL(upconv_combine_kernel<bf16>, grid_for(n, 256), 256, 0, s, (const bf16*)z, (bf16*)out, ldo, B, H, W, C);
+    hipLaunchKernelGGL(upconv_combine_kernel<bf16>, grid, 256, 0, s, (const bf16*)z, (bf16*)out, ldo, B, H, W, C);
   else
-    hipLaunchKernelGGL(upconv_combine_kernel<float>, grid_for(n, 256), 256, 0, s, (const float*)z, (float*)out, ldo, B, H, W, C);
+    hipLaunchKernelGGL(upconv_combine_kernel<float>, grid, 256, 0, s, (const float*)z, (float*)out, ldo, B, H, W, C);
   return (int)hipGetLastError();
 }
 
