@@ -114,23 +114,39 @@ __global__ void upsample_kernel(const T* __restrict__ in, T* __restrict__ out, i
 //   out[Y][X][c] = sum_t [U = Y+dy, V = X+dx inside the 2h x 2w grid] bilerp(Z[.][t*C + c], U, V)
 // with bilerp the upsample kernel's weights above.  (REV/models/backbone.py:141
 // s16_latern(up16sto8s(xs16)): 4x fewer MFMA flops and no 2h x 2w x Cin intermediate.)
-// A thread owns one 16-byte channel chunk of one output row Y and walks a segment of UC_SEG
-// output columns.  Per tap (dy, dx) and source row (y0, y1) it keeps the two corner chunks x0, x1
-// in registers; stepping X -> X+1 moves every tap's source column V = X+dx-1 by one output
-// pixel, i.e. by sx < 1/2 low-resolution columns, so x0 advances by 0 or 1 -- uniformly over the
-// workgroup (it depends on V only): an advance shifts x1 into x0 and loads the new x1.  About 9
-// instead of 36 16-byte reads per output chunk (the reads were the kernel's cost: each Z element
-// was fetched 16 times through L2).  fp32 sums in the order of the one-pixel form, one rounding
-// at the store.
+// A thread owns four channels of one output row Y and walks a segment of UC_SEG output
+// columns.  Per tap (dy, dx) it keeps the two corner columns x0, x1 in registers, already
+// interpolated along y (fp32, hy * Z[y0] + ly * Z[y1]); stepping X -> X+1 moves every tap's source
+// column V = X+dx-1 by one output pixel, i.e. by sx < 1/2 low-resolution columns, so x0 advances
+// by 0 or 1 -- uniformly over the workgroup (it depends on V only): an advance shifts x1 into x0
+// and brings in the new x1, whose loads are issued before the current column is computed.  About
+// 9 instead of 36 reads per output (each Z element was fetched 16 times through L2).
 #ifndef SPE_UC_SEG
 #define SPE_UC_SEG 8
 #endif
 constexpr int UC_SEG = SPE_UC_SEG;
+template <typename T> struct Q4;                 // four channels of T in registers
+template <> struct Q4<bf16> {
+  typedef u32x2 V;
+  static SPE_DEV V ld(const bf16* p) { return ld8(p); }
+  static SPE_DEV void unpack(V v, float* f) {
+    f[0] = __uint_as_float(v.x << 16); f[1] = __uint_as_float(v.x & 0xffff0000u);
+    f[2] = __uint_as_float(v.y << 16); f[3] = __uint_as_float(v.y & 0xffff0000u);
+  }
+  static SPE_DEV void st(bf16* p, const float* f) { st8(p, u32x2{pack_bf16x2(f[0], f[1]), pack_bf16x2(f[2], f[3])}); }
+};
+template <> struct Q4<float> {
+  typedef u32x4 V;
+  static SPE_DEV V ld(const float* p) { return ld16(p); }
+  static SPE_DEV void unpack(V v, float* f) { unpack16<float>(v, f); }
+  static SPE_DEV void st(float* p, const float* f) { st16(p, pack16<float>(f)); }
+};
 template <typename T>
 __global__ __launch_bounds__(256) void upconv_combine_kernel(const T* __restrict__ z, T* __restrict__ out, int ldo, int B, int H,
                                                              int W, int C) {
-  constexpr int CE = Chunk<T>::CE;
-  const int Ho = 2 * H, Wo = 2 * W, cch = C / CE;
+  typedef Q4<T> Q;
+  typedef typename Q::V V;
+  const int Ho = 2 * H, Wo = 2 * W, cch = C / 4;
   const int ldz = 9 * C;
   const float sy = (float)(H - 1) / (float)(Ho - 1);
   const float sx = (float)(W - 1) / (float)(Wo - 1);
@@ -138,9 +154,9 @@ __global__ __launch_bounds__(256) void upconv_combine_kernel(const T* __restrict
   if (j >= B * Ho * cch) return;
   const int c = j % cch, r = j / cch, Y = r % Ho, b = r / Ho;
   const int X0 = blockIdx.y * UC_SEG, X1 = min(X0 + UC_SEG, Wo);
-  const T* zb = z + (size_t)b * H * W * ldz + c * CE;
-  // per dy: the two source rows (clamped in range; a row outside the 2H grid contributes nothing)
-  const T* zr[3][2];
+  const T* zb = z + (size_t)b * H * W * ldz + c * 4;
+  // per dy: the two source rows (a row outside the 2H grid gets zero weights)
+  int zr[3][2];                                   // element offsets from zb (32-bit: one image's Z)
   float wy[3][2];
 #pragma unroll
   for (int dy = 0; dy < 3; ++dy) {
@@ -150,78 +166,72 @@ __global__ __launch_bounds__(256) void upconv_combine_kernel(const T* __restrict
     const int y0 = (int)fy, y1 = y0 + (y0 < H - 1);
     const float ly = fy - y0;
     wy[dy][0] = in ? 1.f - ly : 0.f;
-    wy[dy][1] = ly;
-    zr[dy][0] = zb + (size_t)y0 * W * ldz + dy * 3 * C;
-    zr[dy][1] = zb + (size_t)y1 * W * ldz + dy * 3 * C;
+    wy[dy][1] = in ? ly : 0.f;
+    zr[dy][0] = y0 * W * ldz + dy * 3 * C;
+    zr[dy][1] = y1 * W * ldz + dy * 3 * C;
   }
-  auto col = [&](int V, int& x0, int& x1, float& lx) {
-    const float fx = (V < 0 ? 0 : V) * sx;
-    x0 = min((int)fx, W - 1);
-    x1 = x0 + (x0 < W - 1);
-    lx = fx - x0;
+  auto col0 = [&](int V) { return min((int)((V < 0 ? 0 : V) * sx), W - 1); };
+  auto ymix = [&](int dy, V top, V bot, f32x4& o) {
+    float t[4], u[4];
+    Q::unpack(top, t);
+    Q::unpack(bot, u);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = wy[dy][0] * t[e] + wy[dy][1] * u[e];
   };
-  u32x4 q0[3][3][2], q1[3][3][2];                 // [dy][dx][row]: corners x0, x1
+  f32x4 c0[3][3], c1[3][3];                       // [dy][dx]: y-interpolated corners x0, x1
   int xs[3];
 #pragma unroll
   for (int dx = 0; dx < 3; ++dx) {
-    int x0, x1;
-    float lx;
-    col(X0 + dx - 1, x0, x1, lx);
+    const int x0 = col0(X0 + dx - 1), x1 = x0 + (x0 < W - 1);
     xs[dx] = x0;
 #pragma unroll
-    for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        q0[dy][dx][h] = ld16(zr[dy][h] + (size_t)x0 * ldz + dx * C);
-        q1[dy][dx][h] = ld16(zr[dy][h] + (size_t)x1 * ldz + dx * C);
-      }
+    for (int dy = 0; dy < 3; ++dy) {
+      const T* p = zb + zr[dy][0] + dx * C;
+      const T* q = zb + zr[dy][1] + dx * C;
+      ymix(dy, Q::ld(p + x0 * ldz), Q::ld(q + x0 * ldz), c0[dy][dx]);
+      ymix(dy, Q::ld(p + x1 * ldz), Q::ld(q + x1 * ldz), c1[dy][dx]);
+    }
   }
   for (int X = X0; X < X1; ++X) {
-    // the corner state stays packed across iterations (unpacked per use, not carried as floats)
-#pragma unroll
-    for (int dy = 0; dy < 3; ++dy)
-#pragma unroll
-      for (int dx = 0; dx < 3; ++dx)
-#pragma unroll
-        for (int h = 0; h < 2; ++h) asm volatile("" : "+v"(q0[dy][dx][h]), "+v"(q1[dy][dx][h]));
-    float acc[CE];
-#pragma unroll
-    for (int e = 0; e < CE; ++e) acc[e] = 0.f;
-#pragma unroll
-    for (int dy = 0; dy < 3; ++dy) {
-      const float hy = wy[dy][0], ly = wy[dy][1];
-#pragma unroll
-      for (int dx = 0; dx < 3; ++dx) {
-        const int V = X + dx - 1;
-        if (V < 0 || V >= Wo) continue;
-        const float lx = V * sx - xs[dx], hx = 1.f - lx;
-        float a[CE], bb[CE], cc[CE], d[CE];
-        unpack16<T>(q0[dy][dx][0], a);
-        unpack16<T>(q1[dy][dx][0], bb);
-        unpack16<T>(q0[dy][dx][1], cc);
-        unpack16<T>(q1[dy][dx][1], d);
-#pragma unroll
-        for (int e = 0; e < CE; ++e) acc[e] += hy * (hx * a[e] + lx * bb[e]) + ly * (hx * cc[e] + lx * d[e]);
-      }
-    }
-    st16(out + (((size_t)b * Ho + Y) * Wo + X) * ldo + c * CE, pack16<T>(acc));
-    if (X + 1 >= X1) break;
+    // next column's new corners in flight while this one is combined
+    const bool more = X + 1 < X1;
+    bool adv[3];
+    V nt[3][3][2];
 #pragma unroll
     for (int dx = 0; dx < 3; ++dx) {
-      int x0, x1;
-      float lx;
-      col(X + dx, x0, x1, lx);
-      if (x0 != xs[dx]) {                        // uniform: x0 advanced by one
+      const int x0 = col0(X + dx);
+      adv[dx] = more && x0 != xs[dx];               // uniform
+      if (adv[dx]) {
         xs[dx] = x0;
+        const int x1 = x0 + (x0 < W - 1);
 #pragma unroll
         for (int dy = 0; dy < 3; ++dy)
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            q0[dy][dx][h] = q1[dy][dx][h];
-            q1[dy][dx][h] = ld16(zr[dy][h] + (size_t)x1 * ldz + dx * C);
-          }
+          for (int h = 0; h < 2; ++h) nt[dy][dx][h] = Q::ld(zb + (zr[dy][h] + dx * C + x1 * ldz));
       }
     }
+    float acc[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx) {
+      const int V = X + dx - 1;
+      if (V < 0 || V >= Wo) continue;
+      const float fx = V * sx;
+      const float lx = fx - min((int)fx, W - 1), hx = 1.f - lx;
+#pragma unroll
+      for (int dy = 0; dy < 3; ++dy)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[e] += hx * c0[dy][dx][e] + lx * c1[dy][dx][e];
+    }
+    Q::st(out + (((size_t)b * Ho + Y) * Wo + X) * ldo + c * 4, acc);
+#pragma unroll
+    for (int dx = 0; dx < 3; ++dx)
+      if (adv[dx]) {
+#pragma unroll
+        for (int dy = 0; dy < 3; ++dy) {
+          c0[dy][dx] = c1[dy][dx];
+          ymix(dy, nt[dy][dx][0], nt[dy][dx][1], c1[dy][dx]);
+        }
+      }
   }
 }
 
@@ -301,10 +311,9 @@ int spe_launch_upsample2x(const void* in, void* out, int B, int H, int W, int C,
 }
 
 int spe_launch_upconv_combine(const void* z, void* out, int ldo, int B, int H, int W, int C, int dtype, hipStream_t s) {
-  const int ce = dtype == SPE_DTYPE_BF16 ? 8 : 4;
-  if (C % ce || ldo % ce || ldo < C) return -5;
-  if (H < 1 || W < 1 || (size_t)B * 2 * H * (C / ce) >= (1u << 31) || (size_t)B * H * W * 9 * C >= (1ull << 40)) return -5;
-  const int rows = B * 2 * H * (C / ce);
+  if (C % 4 || ldo % 4 || ldo < C) return -5;
+  if (H < 1 || W < 1 || (size_t)B * 2 * H * (C / 4) >= (1u << 31) || (size_t)H * W * 9 * C >= (1u << 31)) return -5;
+  const int rows = B * 2 * H * (C / 4);
   dim3 grid((rows + 255) / 256, (2 * W + UC_SEG - 1) / UC_SEG);
   if (dtype == SPE_DTYPE_BF16)
     hipLaunchKernelGGL(upconv_combine_kernel<bf16>, grid, 256, 0, s, (const bf16*)z, (bf16*)out, ldo, B, H, W, C);
