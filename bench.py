@@ -367,6 +367,8 @@ def main():
                             num_queries=args.queries, dec_layers=args.layers)
         from spe.synthetic import diversify_class_head
         w = random_rtdetr_weights(rcfg, 0)
+        if args.weights == "pose-consistent":
+            args.weights = "label-diverse"        # no point-head fit for the RT-DETR heads
         if args.weights == "label-diverse":
             # RT-DETR's queries are distinct encoder tokens already; only the last score head is
             # drawn in the principal subspace of its input (spe.synthetic.diversify_class_head)
@@ -376,6 +378,11 @@ def main():
             x = torch.from_numpy(np.concatenate([calib] * ((B + 15) // 16))[:B]).to(dev)
             hs = m(x, return_hs=True)["hs"].cpu().numpy()[:16]
             del m
+            # the selected queries of one image sit close together (top-k encoder tokens of a
+            # random-init encoder): take the head's directions from the within-image spread, or
+            # every query of an image gets the same one to three labels and the solver stops at
+            # its fewer-than-4-correspondences check
+            hs = hs - hs.mean(axis=1, keepdims=True) + hs.mean(axis=(0, 1), keepdims=True)
             w = diversify_class_head(w, hs, head=f"decoder.dec_score_head.{rcfg.dec_layers - 1}")
         model = RTDETR(rcfg, dtype=args.dtype, aux_outputs=False)
         model.load_state_dict(w)
