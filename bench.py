@@ -24,7 +24,17 @@ sys.path.insert(0, os.path.join(REPO, "satellite-pose-estimation_amd"))
 
 # TFLOP/s, GB/s (MI355X_MICROARCH.md).  fp32x3 runs every product as three bf16 MFMAs (hi.hi +
 # hi.lo + lo.hi), so its ceiling for the model's algorithmic flops is a third of the bf16 peak.
-PEAK = {"bf16": {"mfma": 2500.0}, "fp32": {"mfma": 157.3}, "fp32x3": {"mfma": 2500.0 / 3}, "hbm": 8000.0}
+# fp32x6 (the accuracy-contract mode) runs its GEMMs / convolutions on six bf16 MFMAs per product and
+# its attention as fp32x3: the ceiling for a launch depends on its class (peak_for).
+PEAK = {"bf16": {"mfma": 2500.0}, "fp32": {"mfma": 157.3}, "fp32x3": {"mfma": 2500.0 / 3},
+        "fp32x6": {"mfma": 2500.0 / 6}, "hbm": 8000.0}
+
+
+def peak_for(dtype, kind):
+    """MFMA ceiling (TFLOP/s of model flops) of launch class `kind` in mode `dtype`."""
+    if dtype == "fp32x6" and kind.startswith("attn."):
+        return PEAK["fp32x3"]["mfma"]
+    return PEAK[dtype]["mfma"]
 # profiler symbol of each launch class (to match profiles/*kernel_stats.csv rows)
 # (rocprofv3 prints the attention kernels mangled: it does not demangle the __bf16 / _Float16
 # template arguments, DF16b / DF16_)
@@ -68,7 +78,7 @@ def parse():
     p.add_argument("--layers", type=int, default=None)
     p.add_argument("--solver", default=None, choices=["epnp", "epnp_lm", "ransac_p3p_lm", "epnp_ransac_sigma"])
     p.add_argument("--sigma-head", type=int, default=None, choices=[0, 1])
-    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp32x3"],
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp32x3", "fp32x6"],
                    help="bf16: throughput mode; fp32: exact-f32 MFMA parity mode; fp32x3: fp32 storage with "
                         "split-bf16 MFMA (the fast parity mode)")
     p.add_argument("--attn-dtype", dest="attn_dtype", default=None, choices=["bf16", "fp16"],
@@ -79,6 +89,10 @@ def parse():
                         "(default, DETR): label-diverse + the point head fitted on the timed batch so each "
                         "query predicts its label's landmark projection + N(0, 2 px) + 10%% outliers "
                         "(spe.synthetic.fit_point_head), so RANSAC finds consensus and the refinement runs")
+    p.add_argument("--parity-dtype", default="fp32x6", choices=["fp32x6", "fp32x3", "fp32"],
+                   help="the parity mode timed after the main line in the same process (parity_mode object: its "
+                        "own ms_per_step, value, roofline and accuracy against the exact-f32 mode)")
+    p.add_argument("--no-parity", action="store_true", help="skip the parity_mode timing")
     p.add_argument("--no-accuracy", action="store_true",
                    help="skip the post-timing accuracy check of a bf16 run against the fp32 parity mode")
     p.add_argument("--no-overlap", action="store_true",
@@ -113,24 +127,53 @@ def parse():
     return a
 
 
+def usable_cpus():
+    """CPUs this process may run on: the affinity mask, capped by a cgroup CPU quota when one is
+    set (a GPU box's share of a large host is enforced that way; os.cpu_count() shows the host)."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    return n
+
+
 def host_cpu():
-    """CPU model name and logical CPU count of this host (BASELINE.md section 3 fields)."""
-    name = "unknown"
+    """CPU model, logical CPUs, physical cores of this host and the CPUs usable by this process
+    (BASELINE.md section 3 fields)."""
+    name, cores = "unknown", set()
+    phys = core = None
     try:
         with open("/proc/cpuinfo") as f:
             for line in f:
-                if line.startswith("model name"):
-                    name = line.split(":", 1)[1].strip()
-                    break
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "model name" and name == "unknown":
+                    name = v
+                elif k == "physical id":
+                    phys = v
+                elif k == "core id":
+                    core = v
+                elif not k and phys is not None and core is not None:
+                    cores.add((phys, core))
+                    phys = core = None
+        if phys is not None and core is not None:
+            cores.add((phys, core))
     except OSError:
         pass
-    return {"cpu_model": name, "host_logical_cpus": os.cpu_count()}
+    return {"cpu_model": name, "host_logical_cpus": os.cpu_count(), "host_physical_cores": len(cores) or None,
+            "usable_cpus": usable_cpus(), "omp_num_threads_env": os.environ.get("OMP_NUM_THREADS")}
 
 
 def _baseline_record(n, dt, threads, sample):
     v = n / dt
     return {"value": v, "unit": "images/s", "cores": threads, "threads_used": threads,
             "value_per_core": v / threads, "kind": "port",
+            "threads_note": "torch.set_num_threads(all CPUs usable by this process: affinity mask capped by the "
+                            "cgroup quota); one thread per usable CPU",
             "kind_note": "the reference's evaluate() cannot run here (cv2 / mathutils / torchvision absent and the "
                          "reference never ships to the GPU box): oracle/ restatement of the same path timed instead",
             **host_cpu(), "sample": sample}
@@ -148,7 +191,7 @@ def cpu_baseline(cfg, seconds, solver="epnp"):
     from spe.synthetic import random_weights, synthetic_batch
     mode = {"epnp": pnp_ref.MODE_EPNP, "epnp_lm": pnp_ref.MODE_EPNP_LM, "ransac_p3p_lm": pnp_ref.MODE_RANSAC_P3P_LM,
             "epnp_ransac_sigma": pnp_ref.MODE_EPNP_RANSAC_SIGMA}[solver]
-    threads = min(16, os.cpu_count() or 1)
+    threads = usable_cpus()
     torch.set_num_threads(threads)
     w = random_weights(cfg, 0)
     b = synthetic_batch(cfg, 1, 99)
@@ -181,7 +224,7 @@ def cpu_baseline_rtdetr(rcfg, seconds):
     from spe.config import Camera, SpeConfig, world_points
     from spe.rtdetr_spec import random_rtdetr_weights
     from spe.synthetic import synthetic_batch
-    threads = min(16, os.cpu_count() or 1)
+    threads = usable_cpus()
     torch.set_num_threads(threads)
     w = random_rtdetr_weights(rcfg, 0)
     b = synthetic_batch(SpeConfig(input_size=rcfg.input_size), 1, 99)
@@ -257,32 +300,44 @@ def keypoint_error_px(points_px, probs, data):
     return np.asarray(e)
 
 
-def accuracy_vs_fp32(model, cfg, args, w, out, data, solver, dev):
-    """Accuracy of the timed bf16 mode against the fp32 parity mode (pinned to the reference at
-    <= 1e-4 normalised keypoints by tests/test_gpu_parity.py) on the timed batch itself: keypoint
-    deltas of the foreground queries the two modes label alike, label agreement, and the SPEED
-    score delta of the two modes' poses through the same solver."""
+class Fp32Reference:
+    """The exact-f32 parity mode's outputs on the timed batch (that mode is pinned to the reference
+    at <= 1e-4 by tests/test_gpu_parity.py on every golden case), computed once and compared with
+    every timed mode: forward outputs, hs, and its poses / SPEED scores through the same solver."""
+
+    def __init__(self, cfg, w, data, solver, dev):
+        import torch
+        from spe.models import DETR
+        from spe.speed_eval import device_speed_score
+        ref = DETR(cfg, dtype="fp32")
+        ref.load_state_dict(w)
+        self.images = torch.from_numpy(data["images"]).to(dev)
+        self.clip = torch.from_numpy(data["clip_bbox"]).float().to(dev)
+        self.r = ref(self.images, clip_bbox=self.clip, return_hs=True)
+        self.pr = solver.solve_batch(self.r["points_px"], self.r["probs"], self.r.get("sigmas"))
+        q_gt = torch.from_numpy(data["quat"]).to(dev)
+        t_gt = torch.from_numpy(data["tvec"]).to(dev)
+        st, sq = device_speed_score(self.pr["quat"], self.pr["tvec"], q_gt, t_gt)
+        self.score = (st + sq).cpu().numpy()
+        torch.cuda.synchronize()
+        del ref
+
+
+def accuracy_vs_fp32(model, ref, out):
+    """Accuracy of a timed mode against the fp32 parity mode on the timed batch itself: keypoint
+    deltas of the foreground queries both label alike, label agreement, hs relative error, and the
+    SPEED-score delta of the two modes' poses through the same solver."""
     import numpy as np
-    import torch
-    from spe.models import DETR
-    from spe.speed_eval import device_speed_score
-    ref = DETR(cfg, dtype="fp32")
-    ref.load_state_dict(w)
-    clip = torch.from_numpy(data["clip_bbox"]).float().to(dev)
-    r = ref(torch.from_numpy(data["images"]).to(dev), clip_bbox=clip, return_hs=True)
-    hb = model(torch.from_numpy(data["images"]).to(dev), return_hs=True)["hs"]
+    r = ref.r
+    hb = model(ref.images, return_hs=True)["hs"]
     hs_rel = ((hb - r["hs"]).norm(dim=-1) / r["hs"].norm(dim=-1)).flatten()
     fo = out["forward"]
     lab_b, lab_r = fo["probs"].argmax(-1), r["probs"].argmax(-1)
     fg = (lab_r < 11) & (lab_b == lab_r)
-    wcrop = (clip[:, 2] - clip[:, 0])[:, None].expand_as(lab_r)
+    wcrop = (ref.clip[:, 2] - ref.clip[:, 0])[:, None].expand_as(lab_r)
     d = (fo["points_px"] - r["points_px"]).norm(dim=-1)[fg]
     dn = (fo["pred_points"] - r["pred_points"]).abs().amax(-1)[fg]
-    q_gt = torch.from_numpy(data["quat"]).to(dev)
-    t_gt = torch.from_numpy(data["tvec"]).to(dev)
-    pr = solver.solve_batch(r["points_px"], r["probs"], r.get("sigmas"))
-    st, sq = device_speed_score(pr["quat"], pr["tvec"], q_gt, t_gt)
-    sc_r, sc_b = (st + sq).cpu().numpy(), (out["s_t"] + out["s_q"]).cpu().numpy()
+    sc_r, sc_b = ref.score, (out["s_t"] + out["s_q"]).cpu().numpy()
     both = np.isfinite(sc_r) & np.isfinite(sc_b)
     ds = np.abs(sc_b - sc_r)[both]
     res = {"reference_mode": "fp32 parity mode (<= 1e-4 of the reference on its goldens)",
@@ -290,15 +345,17 @@ def accuracy_vs_fp32(model, cfg, args, w, out, data, solver, dev):
            "label_agreement": float((lab_b == lab_r).float().mean().item()),
            "kpt_px_max": float(d.max().item()), "kpt_px_mean": float(d.mean().item()),
            "kpt_norm_max": float(dn.max().item()), "kpt_norm_mean": float(dn.mean().item()),
+           "frac_kpt_norm_le_1e-4": float((dn <= 1e-4).float().mean().item()),
            "kpt_px_per_crop_px": float((d / wcrop[fg]).max().item()),
            "score_delta_max": float(ds.max()) if ds.size else None,
            "score_delta_mean": float(ds.mean()) if ds.size else None,
+           "frac_score_delta_le_1e-4": float((ds <= 1e-4).mean()) if ds.size else None,
            "score_mean_fp32": float(np.nanmean(sc_r)), "score_mean_timed": float(np.nanmean(sc_b)),
-           "status_agreement": float((pr["status"] == out["poses"]["status"]).float().mean().item()),
+           "status_agreement": float((ref.pr["status"] == out["poses"]["status"]).float().mean().item()),
            "images": int(len(sc_r))}
-    meets = res["kpt_norm_max"] <= 1e-4 and (res["score_delta_max"] or 0.0) <= 1e-4
-    res["meets_1e-4"] = bool(meets)
-    del ref
+    res["meets_1e-4_kpt"] = bool(res["kpt_norm_max"] <= 1e-4)
+    res["meets_1e-4_score"] = bool((res["score_delta_max"] or 0.0) <= 1e-4)
+    res["meets_1e-4"] = res["meets_1e-4_kpt"] and res["meets_1e-4_score"]
     return res
 
 
@@ -326,8 +383,182 @@ def launch_grid(kind, B, cfg):
     return None
 
 
+def launch_ranks(args):
+    """`bench.py --gpus N` outside a torchrun environment: start N ranks (one process per GPU,
+    python -m torch.distributed.run, rendezvous on 127.0.0.1) BEFORE this process touches the GPU,
+    and return the launcher's exit status.  Rank 0 prints the JSON line.  Mirrors the reference's
+    one-process-per-GPU launch (REV/main.py:213-217, REV/utils/misc.py:415-440)."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.call(cmd, env=env)
+
+
+def result_header(args, world, elapsed, B, dtype):
+    """The contract fields of the JSON line (whole-job img/s over all ranks, max-over-ranks time)."""
+    return {
+        "metric": f"images/sec end-to-end (backbone->kpts->PnP) at {args.size}x{args.size}; SPEED pose score",
+        "value": B * world * args.steps / elapsed,
+        "unit": "images/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": 1e3 * elapsed / args.steps,
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": dtype,
+    }
+
+
+def stub_worker(args):
+    """SPE_BENCH_STUB=1 (CPU tests of the launcher, tests/test_host.py): the rank bookkeeping of a
+    real run -- env:// rendezvous over gloo, world == --gpus check, barrier-bracketed timing, max
+    over ranks, one pose-record all-gather -- with no GPU work; rank 0 prints the line."""
+    import torch
+    import torch.distributed as dist
+    from spe import dist as sd
+    rank, world, _ = sd.init_distributed_mode(backend="gloo")
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but world size {world}", file=sys.stderr)
+        return 2
+    B = args.batch
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        rec = sd.all_gather_records(sd.pack_records(torch.zeros(B, 4), torch.zeros(B, 3), torch.zeros(B, dtype=torch.float64),
+                                                    torch.zeros(B, dtype=torch.float64), torch.zeros(B, dtype=torch.int32)))
+    if world > 1:
+        dist.barrier()
+    el = torch.tensor([time.perf_counter() - t0], dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(el, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        r = result_header(args, world, float(el.item()), B, args.dtype)
+        r["config"] = {"workload": "launcher stub (no GPU work)", "global_batch": B * world, "per_gpu_batch": B,
+                       "parallelism": f"dp{world} (image sharding)"}
+        r["records_gathered_per_step"] = int(rec.shape[0])
+        print(json.dumps(r))
+    if dist.is_initialized():
+        dist.destroy_process_group()
+    return 0
+
+
+def time_mode(pipe, model, args, world, dev, dtype, attn_dtype, cfg, B, launch_table=None):
+    """Warm-up, one per-launch-profiled step (dominant kernel class), then EXACTLY args.steps timed
+    steps between barriers + synchronize, the dominant class's launches bracketed by HIP events on
+    their stream; elapsed = max over ranks.  Returns the timing, the roofline object and the last
+    step's outputs."""
+    import ctypes
+    import torch
+    import torch.distributed as dist
+    from spe import _lib
+    from spe import dist as sd
+
+    def step():
+        out = pipe.run()
+        if world > 1:
+            # on the solver's stream: the record exchange waits for this batch's poses only
+            sd.exchange_pose_records(out["poses"], out["s_t"], out["s_q"],
+                                     stream=out.get("stream") or torch.cuda.current_stream())
+        return out
+
+    for _ in range(max(args.warmup, 1)):
+        step()
+    torch.cuda.synchronize()
+
+    # dominant kernel class: one fully profiled step after warm-up
+    L = _lib.lib()
+    L.spe_model_profile_begin(model._h, b"")
+    step()
+    n = L.spe_model_profile_end(model._h)
+    tot = {}
+    kb = ctypes.create_string_buffer(64)
+    ms, fl, by = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
+    table = []
+    for i in range(n):
+        L.spe_model_profile_get(model._h, i, kb, 64, ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(by))
+        k = kb.value.decode()
+        t = tot.setdefault(k, [0.0, 0])
+        t[0] += ms.value
+        t[1] += 1
+        floor_ms = 1e3 * max(fl.value / (peak_for(dtype, k) * 1e12), by.value / (PEAK["hbm"] * 1e9))
+        table.append({"i": i, "kind": k, "ms": ms.value, "flops": fl.value, "bytes": by.value,
+                      "floor_ms": floor_ms, "frac": floor_ms / max(ms.value, 1e-9)})
+    dominant = max(tot, key=lambda k: tot[k][0])
+    if launch_table and int(os.environ.get("RANK", "0")) == 0:
+        with open(launch_table, "w") as f:
+            json.dump(table, f, indent=0)
+
+    # ---- timed region: K steps, dominant kernel bracketed with HIP events on its stream
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    L.spe_model_profile_begin(model._h, dominant.encode())
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    if world > 1:
+        dist.barrier()
+    n = L.spe_model_profile_end(model._h)
+    k_ms, k_fl, k_by, k_n = 0.0, 0.0, 0.0, 0
+    for i in range(n):
+        L.spe_model_profile_get(model._h, i, kb, 64, ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(by))
+        if kb.value.decode() == dominant:
+            k_ms += ms.value; k_fl += fl.value; k_by += by.value; k_n += 1
+    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
+    elapsed = float(elapsed.item())
+
+    avg_ms = k_ms / max(k_n, 1)
+    # bound by the class's own arithmetic intensity against the ridge point (2500 TF/s / 8 TB/s
+    # = 312 flop/B): the K <= 256 1x1 convs are HBM-bound, attention / FFN / 3x3 convs MFMA-bound
+    mfma_bound = k_fl * PEAK["hbm"] * 1e9 > k_by * peak_for(dtype, dominant) * 1e12
+    if mfma_bound:
+        achieved = (k_fl / max(k_n, 1)) / (avg_ms * 1e-3) / 1e12
+        peak, unit = peak_for(dtype, dominant), "TFLOP/s"
+    else:
+        achieved = (k_by / max(k_n, 1)) / (avg_ms * 1e-3) / 1e9
+        peak, unit = PEAK["hbm"], "GB/s"
+    prof_ms = tot[dominant][0] / max(tot[dominant][1], 1)
+    symbol = ({"fp32": "attn_f32_kernel", "fp32x3": "attn_x3_kernel", "fp32x6": "attn_x3_kernel"}[dtype]
+              if dominant == "attn.enc" and dtype != "bf16" else
+              KIND_SYMBOL.get(dominant, dominant).replace("DF16b", "DF16_" if attn_dtype == "fp16" else "DF16b"))
+    roofline = {"kernel": dominant, "kernel_symbol": symbol,
+                "bound": "mfma" if mfma_bound else "hbm", "achieved": achieved,
+                "peak": peak, "unit": unit, "frac": achieved / peak,
+                "traffic": traffic_for(dominant, launch_grid(dominant, B, cfg), attn_dtype) if dtype == "bf16" else None,
+                "launches": k_n, "avg_launch_ms": avg_ms,
+                # the timed-region launches share the CUs with the next batch's backbone (stream
+                # overlap); the per-launch profiled step times each launch between events on its
+                # stream, the kernel's own rate
+                "avg_launch_ms_profiled_step": prof_ms,
+                "frac_profiled_step": ((k_fl if mfma_bound else k_by) / max(k_n, 1)) / (prof_ms * 1e-3) /
+                                      (1e12 if mfma_bound else 1e9) / peak,
+                "algorithmic_flops_per_launch": k_fl / max(k_n, 1),
+                "algorithmic_bytes_per_launch": k_by / max(k_n, 1)}
+    return {"elapsed": elapsed, "out": out, "roofline": roofline,
+            "kernel_time_ms_per_step": {k: v[0] for k, v in sorted(tot.items(), key=lambda kv: -kv[1][0])}}
+
+
 def main():
     args = parse()
+    if os.environ.get("SPE_BENCH_STUB"):
+        if args.gpus > 1 and "RANK" not in os.environ:
+            return launch_ranks(args)
+        return stub_worker(args)
+    if args.gpus > 1 and "RANK" not in os.environ:
+        return launch_ranks(args)
     import torch
     import torch.distributed as dist
     from spe import dist as sd
@@ -337,9 +568,11 @@ def main():
     from spe.solver import build_solver
     import numpy as np
     from spe.synthetic import bench_weights, random_weights, synthetic_batch
-    from spe import _lib
 
     rank, world, local = sd.init_distributed_mode()
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but the launch has world size {world}", file=sys.stderr)
+        return 2
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     cfg = SpeConfig(input_size=args.size, num_queries=args.queries, enc_layers=args.layers, dec_layers=args.layers,
@@ -360,6 +593,7 @@ def main():
         return hs
 
     rcfg = None
+    fit = None
     if args.model != "detr":
         from spe.rtdetr import RTDETR
         from spe.rtdetr_spec import RtdetrConfig, random_rtdetr_weights
@@ -388,17 +622,20 @@ def main():
         model.load_state_dict(w)
     else:
         w = bench_weights(cfg, 0, hs_fn) if args.weights != "random" else random_weights(cfg, 0)
-        fit = None
         if args.weights == "pose-consistent":
             w, fit = pose_consistent_weights(w, cfg, args, B, rank, world, dev)
         model = DETR(cfg, dtype=args.dtype, attn_dtype=args.attn_dtype)
         model.load_state_dict(w)
     solver = build_solver(argparse.Namespace(solver=args.solver, repro=20))
+    overlap = dict(overlap=not args.no_overlap,
+                   overlap_decode=rcfg is None and not (args.no_overlap_decode or args.no_overlap),
+                   overlap_backbone=rcfg is None and not (args.no_overlap_backbone or args.no_overlap_decode or args.no_overlap))
+    jpeg_bytes = 0
     if args.raw_frames:
         from spe.synthetic import synthetic_frames
         data = synthetic_frames(B, seed=1000 + rank)
         H, W = data["frames"].shape[1:3]
-        files, jpeg_bytes = None, 0
+        files = None
         if args.jpeg:
             import io
             from PIL import Image
@@ -421,104 +658,53 @@ def main():
             pipe.load_frames(torch.from_numpy(data["frames"]).to(dev), torch.from_numpy(data["bbox_xxyy"]).to(dev),
                              torch.from_numpy(data["quat"]).to(dev), torch.from_numpy(data["tvec"]).to(dev))
     else:
-        pipe = PosePipeline(model, solver, B, device=dev, overlap=not args.no_overlap,
-                            overlap_decode=rcfg is None and not (args.no_overlap_decode or args.no_overlap),
-                            overlap_backbone=rcfg is None and not (args.no_overlap_backbone or args.no_overlap_decode or args.no_overlap))
+        pipe = PosePipeline(model, solver, B, device=dev, **overlap)
         data = bench_data(cfg, B, rank) if rcfg is None else synthetic_batch(SpeConfig(input_size=args.size), B, seed=1000 + rank)
         pipe.load(torch.from_numpy(data["images"]).to(dev), torch.from_numpy(data["clip_bbox"]).float().to(dev),
                   torch.from_numpy(data["quat"]).to(dev), torch.from_numpy(data["tvec"]).to(dev))
     torch.cuda.synchronize()
 
-    def step():
-        out = pipe.run()
-        if world > 1:
-            # on the solver's stream: the record exchange waits for this batch's poses only
-            sd.exchange_pose_records(out["poses"], out["s_t"], out["s_q"],
-                                     stream=out.get("stream") or torch.cuda.current_stream())
-        return out
-
-    for _ in range(max(args.warmup, 1)):
-        step()
-    torch.cuda.synchronize()
-
-    # dominant kernel class: one fully profiled step after warm-up
-    L = _lib.lib()
-    L.spe_model_profile_begin(model._h, b"")
-    step()
-    n = L.spe_model_profile_end(model._h)
-    import ctypes
-    tot = {}
-    kb = ctypes.create_string_buffer(64)
-    ms, fl, by = ctypes.c_double(), ctypes.c_double(), ctypes.c_double()
-    table = []
-    for i in range(n):
-        L.spe_model_profile_get(model._h, i, kb, 64, ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(by))
-        k = kb.value.decode()
-        t = tot.setdefault(k, [0.0, 0])
-        t[0] += ms.value
-        t[1] += 1
-        floor_ms = 1e3 * max(fl.value / (PEAK[args.dtype]["mfma"] * 1e12), by.value / (PEAK["hbm"] * 1e9))
-        table.append({"i": i, "kind": k, "ms": ms.value, "flops": fl.value, "bytes": by.value,
-                      "floor_ms": floor_ms, "frac": floor_ms / max(ms.value, 1e-9)})
-    dominant = max(tot, key=lambda k: tot[k][0])
-    if args.launch_table and rank == 0:
-        with open(args.launch_table, "w") as f:
-            json.dump(table, f, indent=0)
-
-    # ---- timed region: K steps, dominant kernel bracketed with HIP events on its stream
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    L.spe_model_profile_begin(model._h, dominant.encode())
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        out = step()
-    torch.cuda.synchronize()
-    t1 = time.perf_counter()
-    if world > 1:
-        dist.barrier()
-    n = L.spe_model_profile_end(model._h)
-    k_ms, k_fl, k_by, k_n = 0.0, 0.0, 0.0, 0
-    for i in range(n):
-        L.spe_model_profile_get(model._h, i, kb, 64, ctypes.byref(ms), ctypes.byref(fl), ctypes.byref(by))
-        if kb.value.decode() == dominant:
-            k_ms += ms.value; k_fl += fl.value; k_by += by.value; k_n += 1
-    elapsed = torch.tensor([t1 - t0], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(elapsed, op=dist.ReduceOp.MAX)
-    elapsed = float(elapsed.item())
-
+    tm = time_mode(pipe, model, args, world, dev, args.dtype, args.attn_dtype, cfg, B, args.launch_table)
+    out = tm["out"]
     score = float((out["s_t"] + out["s_q"]).mean().item())
     status = out["poses"]["status"].cpu()
+
+    # ---- parity mode: the same weights, batch and pipeline in the fast parity dtype, timed the
+    # same way (its own steps between barriers), with its accuracy against the exact-f32 mode
+    parity = None
+    want_parity = (rcfg is None and not args.raw_frames and not args.no_parity and args.parity_dtype != args.dtype)
+    ref = None
+    if rcfg is None and not args.raw_frames and not args.no_accuracy and (args.dtype != "fp32" or want_parity):
+        ref = Fp32Reference(cfg, w, data, solver, dev)
+    acc = accuracy_vs_fp32(model, ref, out) if (ref is not None and args.dtype != "fp32") else None
+    if want_parity:
+        del pipe
+        pm = DETR(cfg, dtype=args.parity_dtype)
+        pm.load_state_dict(w)
+        ppipe = PosePipeline(pm, solver, B, device=dev, **overlap)
+        ppipe.load(torch.from_numpy(data["images"]).to(dev), torch.from_numpy(data["clip_bbox"]).float().to(dev),
+                   torch.from_numpy(data["quat"]).to(dev), torch.from_numpy(data["tvec"]).to(dev))
+        torch.cuda.synchronize()
+        pt = time_mode(ppipe, pm, args, world, dev, args.parity_dtype, args.parity_dtype, cfg, B)
+        parity = {k: v for k, v in result_header(args, world, pt["elapsed"], B, args.parity_dtype).items()
+                  if k in ("value", "unit", "ms_per_step", "dtype")}
+        parity["value_per_gpu"] = parity["value"] / world
+        parity["mode"] = {"fp32x6": "fp32 storage; GEMMs / convolutions at near-fp32 precision (three-way split, "
+                                    "six bf16 products), attention as fp32x3 (DESIGN.md section 4)",
+                          "fp32x3": "fp32 storage, split-bf16 MFMA (hi.hi + hi.lo + lo.hi)",
+                          "fp32": "fp32 storage, exact-f32 MFMA"}.get(args.parity_dtype, args.parity_dtype)
+        parity["roofline"] = pt["roofline"]
+        parity["kernel_time_ms_per_step"] = pt["kernel_time_ms_per_step"]
+        if ref is not None:
+            parity["accuracy_vs_fp32"] = accuracy_vs_fp32(pm, ref, pt["out"])
+        del ppipe, pm
+
     if rank != 0:
         if dist.is_initialized():
             dist.destroy_process_group()
-        return
-    total_images = B * world * args.steps
-    avg_ms = k_ms / max(k_n, 1)
-    # bound by the class's own arithmetic intensity against the ridge point (2500 TF/s / 8 TB/s
-    # = 312 flop/B): the K <= 256 1x1 convs are HBM-bound, attention / FFN / 3x3 convs MFMA-bound
-    mfma_bound = k_fl * PEAK["hbm"] * 1e9 > k_by * PEAK[args.dtype]["mfma"] * 1e12
-    if mfma_bound:
-        achieved = (k_fl / max(k_n, 1)) / (avg_ms * 1e-3) / 1e12
-        peak = PEAK[args.dtype]["mfma"]
-        unit = "TFLOP/s"
-    else:
-        achieved = (k_by / max(k_n, 1)) / (avg_ms * 1e-3) / 1e9
-        peak = PEAK["hbm"]
-        unit = "GB/s"
-    result = {
-        "metric": f"images/sec end-to-end (backbone->kpts->PnP) at {args.size}x{args.size}; SPEED pose score",
-        "value": total_images / elapsed,
-        "unit": "images/s",
-        "n_gpus": world,
-        "steps": args.steps,
-        "warmup": args.warmup,
-        "ms_per_step": 1e3 * elapsed / args.steps,
-        "higher_is_better": True,
-        "scaling": "weak",
-        "vs_baseline": None,
-        "dtype": args.dtype,
+        return 0
+    result = result_header(args, world, tm["elapsed"], B, args.dtype)
+    result.update({
         "data": f"synthetic (seeded SPEED-shaped {('1920x1200 grayscale JPEG files (q90) + detector boxes, on-device decode + val transform' if args.jpeg else '1920x1200 8-bit frames + detector boxes, on-device val transform') if args.raw_frames else 'crops'}; "
                 f"{args.weights} random-init weights, no checkpoint exists in the reference)",
         "config": {"workload": (CONFIG_NAME[args.config].format(L=args.layers, Q=args.queries, S=args.size,
@@ -534,26 +720,11 @@ def main():
                    "attention_dtype": ("bf16 q/k, fp16 V/P" if args.attn_dtype == "bf16" and args.dtype == "bf16"
                                        and os.environ.get("SPE_ATTN_F16V", "1") != "0" else args.attn_dtype),
                    "parallelism": f"dp{world} (image sharding)"},
-        "roofline": {"kernel": dominant, "kernel_symbol": (
-                         {"fp32": "attn_f32_kernel", "fp32x3": "attn_x3_kernel"}[args.dtype]
-                         if dominant == "attn.enc" and args.dtype != "bf16" else
-                         KIND_SYMBOL.get(dominant, dominant).replace("DF16b", "DF16_" if args.attn_dtype == "fp16" else "DF16b")),
-                     "bound": "mfma" if mfma_bound else "hbm", "achieved": achieved,
-                     "peak": peak, "unit": unit, "frac": achieved / peak,
-                     "traffic": traffic_for(dominant, launch_grid(dominant, B, cfg), args.attn_dtype), "launches": k_n, "avg_launch_ms": avg_ms,
-                     # the timed-region launches share the CUs with the next batch's backbone
-                     # (stream overlap); the per-launch profiled step times each launch between
-                     # events on its stream, the kernel's own rate
-                     "avg_launch_ms_profiled_step": tot[dominant][0] / max(tot[dominant][1], 1),
-                     "frac_profiled_step": ((k_fl if mfma_bound else k_by) / max(k_n, 1)) /
-                                           (tot[dominant][0] / max(tot[dominant][1], 1) * 1e-3) /
-                                           (1e12 if mfma_bound else 1e9) / peak,
-                     "algorithmic_flops_per_launch": k_fl / max(k_n, 1),
-                     "algorithmic_bytes_per_launch": k_by / max(k_n, 1)},
-        "kernel_time_ms_per_step": {k: v[0] for k, v in sorted(tot.items(), key=lambda kv: -kv[1][0])},
+        "roofline": tm["roofline"],
+        "kernel_time_ms_per_step": tm["kernel_time_ms_per_step"],
         "speed_score_mean_random_weights": score,
         "solver_status_counts": {str(s): int((status == s).sum()) for s in range(5)},
-    }
+    })
     if "assess" in out:
         result["self_assessment_reliable"] = int(out["assess"]["reliable"].sum().item())
     if rcfg is None and not args.raw_frames:
@@ -561,16 +732,21 @@ def main():
         result["keypoints_vs_gt_px"] = {"median": float(np.median(e)), "p90": float(np.percentile(e, 90)),
                                         "fg_queries": int(e.size), "weights": args.weights}
         if fit is not None:
-            result["keypoints_vs_gt_px"].update(fit)
-        if args.dtype != "fp32" and not args.no_accuracy:
-            result["accuracy_vs_fp32"] = accuracy_vs_fp32(model, cfg, args, w, out, data, solver, dev)
+            # the point head is fitted on the timed batch itself (spe.synthetic.fit_point_head), so
+            # these are fit-set (training-set) errors, not held-out accuracy
+            result["keypoints_vs_gt_px"].update(fit, fit_set="the timed batch (training-set error)")
+        if acc is not None:
+            result["accuracy_vs_fp32"] = acc
+    if parity is not None:
+        result["parity_mode"] = parity
     if world == 1 and not args.no_cpu_baseline:
         result["cpu_baseline"] = (cpu_baseline(cfg, args.cpu_seconds, args.solver) if rcfg is None
                                   else cpu_baseline_rtdetr(rcfg, args.cpu_seconds))
     print(json.dumps(result))
     if dist.is_initialized():
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

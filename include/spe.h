@@ -18,7 +18,7 @@
 extern "C" {
 #endif
 
-#define SPE_ABI_VERSION 4
+#define SPE_ABI_VERSION 5
 
 enum {
   SPE_E_ARG = -1,        /* bad argument / size */
@@ -32,8 +32,11 @@ enum {
 /* BF16_: bf16 storage, bf16 MFMA with fp32 accumulation (throughput mode); F32_: fp32 storage,
  * exact-f32 MFMA (parity mode); F16_: fp16 attention operands (attn_dtype only); F32X3_: fp32
  * storage, split-bf16 MFMA (x = hi + lo, products hi.hi + hi.lo + lo.hi, fp32 accumulation):
- * the fast parity mode */
-enum { SPE_DTYPE_BF16_ = 0, SPE_DTYPE_F32_ = 1, SPE_DTYPE_F16_ = 2, SPE_DTYPE_F32X3_ = 4 };
+ * the fast parity mode on the reference goldens; F32X6_: the accuracy-contract mode (<= 1e-4 of the exact-f32
+ * mode on the bench's amplifying weights too): fp32 storage, every GEMM / convolution with
+ * near-fp32 precision (x = hi + mid + lo in bf16, the six products of relative order >= 2^-16), the
+ * attention contractions as F32X3_ */
+enum { SPE_DTYPE_BF16_ = 0, SPE_DTYPE_F32_ = 1, SPE_DTYPE_F16_ = 2, SPE_DTYPE_F32X3_ = 4, SPE_DTYPE_F32X6_ = 5 };
 
 /* Solver modes.
  *  SPE_PNP_EPNP              cv2.solvePnPGeneric(EPNP) on all selected points
@@ -42,8 +45,15 @@ enum { SPE_DTYPE_BF16_ = 0, SPE_DTYPE_F32_ = 1, SPE_DTYPE_F16_ = 2, SPE_DTYPE_F3
  *                            (REV/utils/speed_eval.py:209-230) — BASELINE config 3
  *  SPE_PNP_EPNP_RANSAC_SIGMA cv2.solvePnPRansac(EPNP) + sigma-weighted Huber LM
  *                            (UNC/utils/speed_eval.py:332-420) — BASELINE config 4
- *  SPE_PNP_EPNP_LM           EPnP + solvePnPGeneric(ITERATIVE) on all points */
-enum { SPE_PNP_EPNP = 0, SPE_PNP_RANSAC_P3P_LM = 1, SPE_PNP_EPNP_RANSAC_SIGMA = 2, SPE_PNP_EPNP_LM = 3 };
+ *  SPE_PNP_EPNP_LM           EPnP + solvePnPGeneric(ITERATIVE) on all points
+ *  SPE_PNP_EPNP_CERES        UNC EPnPCeresSolver (UNC/utils/speed_eval_ceres.py:43-243): EPnP on all points,
+ *                            inliers = reprojection error < the image's threshold (get_repro_th, :53-58),
+ *                            sigma-weighted Huber(0.001) LM on the inliers (weights normalised over them),
+ *                            the EPnP pose kept when the refined error sum over all points is larger
+ *                            (:142-146); exactly one inlier raises IndexError there -> status NO_FG
+ * SPE_PNP_EPNP's inlier_mask is epnp_init's set, reprojection error < repro (:163-166). */
+enum { SPE_PNP_EPNP = 0, SPE_PNP_RANSAC_P3P_LM = 1, SPE_PNP_EPNP_RANSAC_SIGMA = 2, SPE_PNP_EPNP_LM = 3,
+       SPE_PNP_EPNP_CERES = 4 };
 
 /* Per-image solver status (reference exception mapping, REV/datasets/speed.py:355-363).
  *  OK              pose solved
@@ -67,7 +77,7 @@ typedef struct {
   int nheads;           /* --nheads (8; head_dim must be 32) */
   int dim_feedforward;  /* --dim_feedforward (2048) */
   int sigma_head;       /* 1: UNC-style sigma head (sigma_embed.layers.*) */
-  int dtype;            /* SPE_DTYPE_BF16_ (bf16 storage, fp32 accumulate), SPE_DTYPE_F32_ or SPE_DTYPE_F32X3_ */
+  int dtype;            /* SPE_DTYPE_BF16_ (bf16 storage, fp32 accumulate), SPE_DTYPE_F32_, _F32X3_ or _F32X6_ */
   int attn_dtype;       /* encoder self-attention operands (q, k, V^T): 0 = as dtype; SPE_DTYPE_F16_ =
                          * fp16 (bf16 models only; BASELINE config 5's "fp16 MFMA attention") */
 } spe_model_config;
@@ -212,12 +222,13 @@ int spe_postprocess(void* stream, const float* logits, const float* points, cons
  * K: 3x3 row-major fp64; world: [C-1][3] fp64 landmarks (REV/all_result.json).
  * quat: [B,4] (float32 values, Blender order w,x,y,z); tvec/rvec: [B,3] fp64;
  * corr_label: [B,16] label of each correspondence in first-seen order (-1 padded);
- * inlier_mask: [B] bit i = correspondence i is a RANSAC inlier.  Nullable: sigmas, rvec,
- * status, n_corr, corr_label, inlier_mask. */
+ * inlier_mask: [B] bit i = correspondence i is an inlier.  repro_per_image: [B] fp32 thresholds that
+ * replace `repro` image by image (EPnPCeresSolver.get_repro_th of each image's box area).  Nullable:
+ * sigmas, rvec, status, n_corr, corr_label, inlier_mask, repro_per_image. */
 int spe_pnp_batch(void* stream, const float* points_px, const float* probs, const float* sigmas, int batch,
                   int num_queries, int num_classes, const double* K, const double* world, int mode, float repro,
                   int ransac_iters, double confidence, float* quat, double* tvec, double* rvec, int32_t* status,
-                  int32_t* n_corr, int32_t* corr_label, uint32_t* inlier_mask);
+                  int32_t* n_corr, int32_t* corr_label, uint32_t* inlier_mask, const float* repro_per_image);
 
 /* Self-assessment filter over the sigma solver's output (BASELINE config 4).  No reference code
  * exists: the UNC README (ROOT/README.md:15-20) names the mechanism and the commented gate

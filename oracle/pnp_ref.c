@@ -30,7 +30,7 @@
 
 #define MAXN 16
 
-enum { MODE_EPNP = 0, MODE_RANSAC_P3P_LM = 1, MODE_EPNP_RANSAC_SIGMA = 2, MODE_EPNP_LM = 3 };
+enum { MODE_EPNP = 0, MODE_RANSAC_P3P_LM = 1, MODE_EPNP_RANSAC_SIGMA = 2, MODE_EPNP_LM = 3, MODE_EPNP_CERES = 4 };
 enum { ST_OK = 0, ST_NO_FG = 1, ST_CV_ERROR = 2, ST_RANSAC_FALLBACK = 3, ST_UNPINNED = 4 };
 
 typedef struct { double fx, fy, cx, cy; } cam_t;
@@ -1060,6 +1060,9 @@ static void lm_refine(const cam_t* k, int n, const double* wld, const double* im
 
 /* sigma-weighted Huber LM in normalised coordinates (UNC ceres_pnp restatement, UNPINNED):
  * residual_i = w_i * (x_obs - x_proj) per axis, Huber(delta) robust loss, <= 20 LM iterations. */
+static void sigma_lm_core(int n, const double* wld, const double* xn, const double* w, double delta, double* rvec,
+                          double* tvec);
+
 static void sigma_lm(const cam_t* k, int n, const double* wld, const double* img, const double* sig, double delta,
                      double* rvec, double* tvec) {
   double xn[2 * MAXN], w[2 * MAXN];
@@ -1076,6 +1079,13 @@ static void sigma_lm(const cam_t* k, int n, const double* wld, const double* img
     }
   }
   for (int i = 0; i < n; ++i) for (int a = 0; a < 2; ++a) w[2 * i + a] = (double)(w1[2 * i + a] / sum[a]);
+  sigma_lm_core(n, wld, xn, w, delta, rvec, tvec);
+}
+
+/* the LM itself over normalised observations xn [2n] and per-row weights w [2n] (the values the
+ * reference hands PyCeres.CreatePnPCostFunction) */
+static void sigma_lm_core(int n, const double* wld, const double* xn, const double* w, double delta, double* rvec,
+                          double* tvec) {
   cam_t unit = {1, 1, 0, 0};
   double param[6] = {rvec[0], rvec[1], rvec[2], tvec[0], tvec[1], tvec[2]};
   double mu = 1e-4, nu = 2;
@@ -1257,6 +1267,104 @@ static void blender_quat(const double* Rd, float* q) {
   else { q[1] = 1.0f; q[0] = q[2] = q[3] = 0.0f; }
 }
 
+/* ------------------------------------------------------------------ EPnPCeresSolver pieces */
+/* np.sum of a contiguous float32 vector (numpy's pairwise summation: sequential below 8
+ * elements, 8 accumulators combined pairwise above, float32 throughout) */
+static float np_sum_f32(const float* a, int n) {
+  if (n < 8) {
+    float r = 0.f;
+    for (int i = 0; i < n; ++i) r += a[i];
+    return r;
+  }
+  float r[8];
+  for (int j = 0; j < 8; ++j) r[j] = a[j];
+  int i = 8;
+  for (; i < n - (n % 8); i += 8)
+    for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+  float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; ++i) res += a[i];
+  return res;
+}
+
+/* np.linalg.norm(cv2.projectPoints(wld_f32, r, t, K, 0) - obj_f32, axis=-1) per point: OpenCV
+ * projects in double and stores float32 (project_f), numpy subtracts, squares, adds and takes
+ * the root in float32 (UNC/utils/speed_eval_ceres.py:142-143,163-165) */
+static void repro_errors(const cam_t* k, int n, const float* wld_f, const float* img_f, const double* rvec,
+                         const double* t, float* err) {
+  double R[9];
+  rodrigues_r2R(rvec, R);
+  for (int i = 0; i < n; ++i) {
+    float uv[2];
+    project_f(k, R, t, wld_f + 3 * i, uv);
+    const float dx = uv[0] - img_f[2 * i], dy = uv[1] - img_f[2 * i + 1];
+    const float dx2 = dx * dx, dy2 = dy * dy;
+    err[i] = sqrtf(dx2 + dy2);
+  }
+}
+
+/* EPnPCeresSolver.__call__ after the selection (UNC/utils/speed_eval_ceres.py:121-151):
+ * epnp_init (:153-169) -> inliers err < th -> ceres_pnp on the inliers with the sigma weights
+ * normalised over them (:172-243, HuberLoss(0.001), <= 20 iterations) -> keep the EPnP pose when
+ * the refined reprojection sum over ALL points is larger (:142-146).  One inlier: the
+ * reference's np.squeeze leaves a 1-D array and obj_pts[idx, 0] raises IndexError (status NO_FG,
+ * a zero pose, as SpeedEval maps it); no inliers: an empty Ceres problem leaves the camera as it
+ * is (parity unpinned: OpenCV's undistortPoints on zero points is outside the reference's runs). */
+static int epnp_ceres(const cam_t* k, int nl, const float* wld_f, const float* img_f, const double* wld_d,
+                      const double* img_d, const double* sig_d, float th, double* rvec, double* t, uint32_t* inl) {
+  epnp_solve(k, nl, wld_d, img_d, 1, rvec, t);
+  float err[MAXN];
+  repro_errors(k, nl, wld_f, img_f, rvec, t, err);
+  const float before = np_sum_f32(err, nl);
+  int m = 0;
+  double wi[3 * MAXN], ii[2 * MAXN], si[2 * MAXN];
+  for (int i = 0; i < nl; ++i)
+    if ((double)err[i] < (double)th) {
+      *inl |= 1u << i;
+      for (int c = 0; c < 3; ++c) wi[3 * m + c] = wld_d[3 * i + c];
+      for (int c = 0; c < 2; ++c) { ii[2 * m + c] = img_d[2 * i + c]; si[2 * m + c] = sig_d ? sig_d[2 * i + c] : 1.0; }
+      m++;
+    }
+  if (m == 1) return ST_NO_FG;
+  if (m == 0) return ST_OK;
+  double r2[3] = {rvec[0], rvec[1], rvec[2]}, t2[3] = {t[0], t[1], t[2]};
+  sigma_lm(k, m, wi, ii, si, 0.001, r2, t2);
+  repro_errors(k, nl, wld_f, img_f, r2, t2, err);
+  const float after = np_sum_f32(err, nl);
+  if (!(after > before)) {
+    for (int c = 0; c < 3; ++c) { rvec[c] = r2[c]; t[c] = t2[c]; }
+  }
+  return ST_OK;
+}
+
+/* UNC get_repro_th (speed_eval_ceres.py:53-58): int(area / input_size * 10) clamped to [1.5, 20] */
+float oracle_repro_th(double area, int input_size) {
+  double r = (double)(long long)(area / input_size * 10);
+  r = r > 1.5 ? r : 1.5;
+  return (float)(r < 20 ? r : 20);
+}
+
+/* primitives for the golden generator's OpenCV / PyCeres / mathutils stand-ins */
+void oracle_epnp(int n, const float* wld_f, const float* img_f, const double* Kmat, double* rvec, double* tvec) {
+  cam_t k = {Kmat[0], Kmat[4], Kmat[2], Kmat[5]};
+  double wd[3 * MAXN], id[2 * MAXN];
+  for (int i = 0; i < 3 * n; ++i) wd[i] = wld_f[i];
+  for (int i = 0; i < 2 * n; ++i) id[i] = img_f[i];
+  epnp_solve(&k, n, wd, id, 1, rvec, tvec);
+}
+void oracle_project(int n, const float* wld_f, const double* rvec, const double* tvec, const double* Kmat, float* uv) {
+  cam_t k = {Kmat[0], Kmat[4], Kmat[2], Kmat[5]};
+  double R[9];
+  rodrigues_r2R(rvec, R);
+  for (int i = 0; i < n; ++i) project_f(&k, R, tvec, wld_f + 3 * i, uv + 2 * i);
+}
+void oracle_sigma_lm_core(int n, const double* wld, const double* xn, const double* w, double delta, double* rvec,
+                          double* tvec) {
+  sigma_lm_core(n, wld, xn, w, delta, rvec, tvec);
+}
+void oracle_rodrigues(const double* r, double* R) { rodrigues_r2R(r, R); }
+void oracle_blender_quat(const double* R, float* q) { blender_quat(R, q); }
+float oracle_np_sum_f32(const float* a, int n) { return np_sum_f32(a, n); }
+
 /* ------------------------------------------------------------------ public oracle entry */
 /* One image.  pts [Q*2] px (float32), probs [Q*C], sigmas [Q*2] or NULL, world [(C-1)*3].
  * Outputs: quat[4] (float32-valued), tvec[3], n_corr, corr_label[MAXN], inlier bitmask over
@@ -1300,8 +1408,18 @@ int oracle_pnp_one(const float* pts, const float* probs, const float* sigmas, in
   int status = ST_OK;
   if (mode == MODE_EPNP || mode == MODE_EPNP_LM) {
     epnp_solve(&k, nl, wld_d, img_d, 1, rvec, t);
-    *inlier_mask = (nl >= 32) ? 0xffffffffu : ((1u << nl) - 1);
-    if (mode == MODE_EPNP_LM) lm_refine(&k, nl, wld_d, img_d, rvec, t);
+    if (mode == MODE_EPNP) {
+      /* epnp_init's inlier set (UNC/utils/speed_eval_ceres.py:163-166): reprojection error < repro */
+      float err[MAXN];
+      repro_errors(&k, nl, wld_f, img_f, rvec, t, err);
+      for (int i = 0; i < nl; ++i) if ((double)err[i] < (double)repro) *inlier_mask |= 1u << i;
+    } else {
+      *inlier_mask = (nl >= 32) ? 0xffffffffu : ((1u << nl) - 1);
+      lm_refine(&k, nl, wld_d, img_d, rvec, t);
+    }
+  } else if (mode == MODE_EPNP_CERES) {
+    status = epnp_ceres(&k, nl, wld_f, img_f, wld_d, img_d, sigmas ? sig_d : NULL, repro, rvec, t, inlier_mask);
+    if (status == ST_NO_FG) return status;
   } else {
     /* solvePnPRansac switches to the P3P kernel for exactly 4 points (solvepnp.cpp) */
     const int kernel = (mode == MODE_RANSAC_P3P_LM || nl == 4) ? 0 : 1;
@@ -1345,11 +1463,11 @@ int oracle_pnp_one(const float* pts, const float* probs, const float* sigmas, in
 /* batch wrapper */
 int oracle_pnp_batch(const float* pts, const float* probs, const float* sigmas, int B, int Q, int C, const double* Kmat,
                      const double* world, int mode, float repro, int iters, double conf, double* quat, double* tvec,
-                     int* status, int* n_corr, int* corr_label, uint32_t* inlier_mask) {
+                     int* status, int* n_corr, int* corr_label, uint32_t* inlier_mask, const float* repro_img) {
   for (int b = 0; b < B; ++b)
     status[b] = oracle_pnp_one(pts + (size_t)b * Q * 2, probs + (size_t)b * Q * C, sigmas ? sigmas + (size_t)b * Q * 2 : NULL, Q,
-                               C, Kmat, world, mode, repro, iters, conf, quat + 4 * b, tvec + 3 * b, n_corr + b,
-                               corr_label + MAXN * b, inlier_mask + b);
+                               C, Kmat, world, mode, repro_img ? repro_img[b] : repro, iters, conf, quat + 4 * b,
+                               tvec + 3 * b, n_corr + b, corr_label + MAXN * b, inlier_mask + b);
   return 0;
 }
 

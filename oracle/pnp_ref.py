@@ -19,7 +19,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB = os.path.join(HERE, "build", "liboracle_pnp.so")
 MAXN = 16
 
-MODE_EPNP, MODE_RANSAC_P3P_LM, MODE_EPNP_RANSAC_SIGMA, MODE_EPNP_LM = 0, 1, 2, 3
+MODE_EPNP, MODE_RANSAC_P3P_LM, MODE_EPNP_RANSAC_SIGMA, MODE_EPNP_LM, MODE_EPNP_CERES = 0, 1, 2, 3, 4
 ST_OK, ST_NO_FG, ST_CV_ERROR, ST_RANSAC_FALLBACK, ST_UNPINNED = 0, 1, 2, 3, 4
 
 _lib = None
@@ -37,7 +37,16 @@ def lib():
         _lib = ctypes.CDLL(LIB)
         P = ctypes.c_void_p
         _lib.oracle_pnp_batch.argtypes = [P, P, P, ctypes.c_int, ctypes.c_int, ctypes.c_int, P, P, ctypes.c_int,
-                                          ctypes.c_float, ctypes.c_int, ctypes.c_double, P, P, P, P, P, P]
+                                          ctypes.c_float, ctypes.c_int, ctypes.c_double, P, P, P, P, P, P, P]
+        _lib.oracle_repro_th.argtypes = [ctypes.c_double, ctypes.c_int]
+        _lib.oracle_repro_th.restype = ctypes.c_float
+        _lib.oracle_epnp.argtypes = [ctypes.c_int, P, P, P, P, P]
+        _lib.oracle_project.argtypes = [ctypes.c_int, P, P, P, P, P]
+        _lib.oracle_sigma_lm_core.argtypes = [ctypes.c_int, P, P, P, ctypes.c_double, P, P]
+        _lib.oracle_rodrigues.argtypes = [P, P]
+        _lib.oracle_blender_quat.argtypes = [P, P]
+        _lib.oracle_np_sum_f32.argtypes = [P, ctypes.c_int]
+        _lib.oracle_np_sum_f32.restype = ctypes.c_float
         _lib.oracle_speed_score.argtypes = [P, P, P, P, P, P]
     return _lib
 
@@ -46,9 +55,11 @@ def _p(a):
     return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
 
 
-def pnp_batch(points, probs, K, world, mode=MODE_RANSAC_P3P_LM, repro=20.0, sigmas=None, iters=100, conf=0.99):
+def pnp_batch(points, probs, K, world, mode=MODE_RANSAC_P3P_LM, repro=20.0, sigmas=None, iters=100, conf=0.99,
+              repro_per_image=None):
     """points [B,Q,2] px, probs [B,Q,C] -> dict(quat [B,4], tvec [B,3], status [B], n_corr [B],
-    corr_label [B,16], inlier_mask [B])."""
+    corr_label [B,16], inlier_mask [B]).  repro_per_image [B] (optional) replaces `repro` per image
+    (the EPnPCeresSolver's area threshold, repro_th)."""
     points = np.ascontiguousarray(points, np.float32)
     probs = np.ascontiguousarray(probs, np.float32)
     B, Q, C = probs.shape
@@ -60,8 +71,60 @@ def pnp_batch(points, probs, K, world, mode=MODE_RANSAC_P3P_LM, repro=20.0, sigm
                inlier_mask=np.zeros(B, np.uint32))
     lib().oracle_pnp_batch(_p(points), _p(probs), _p(sig), B, Q, C, _p(K), _p(world), mode, repro, iters, conf,
                            _p(out["quat"]), _p(out["tvec"]), _p(out["status"]), _p(out["n_corr"]),
-                           _p(out["corr_label"]), _p(out["inlier_mask"]))
+                           _p(out["corr_label"]), _p(out["inlier_mask"]),
+                           _p(None if repro_per_image is None else np.ascontiguousarray(repro_per_image, np.float32)))
     return out
+
+
+def repro_th(area, input_size=256):
+    """EPnPCeresSolver.get_repro_th (UNC/utils/speed_eval_ceres.py:53-58)."""
+    return float(lib().oracle_repro_th(float(area), int(input_size)))
+
+
+def speedeval_area(bbox_xxyy):
+    """UNC SpeedEval's area field as written (src/data/speed/speed_dataset.py, ground_truth
+    'area'): np.sqrt((x2 - x1) * y2 - y1) -- the reference's precedence, kept."""
+    x1, y1, x2, y2 = [float(v) for v in bbox_xxyy]
+    return float(np.sqrt((x2 - x1) * y2 - y1))
+
+
+def epnp(wld, img, K):
+    wld = np.ascontiguousarray(wld, np.float32).reshape(-1, 3)
+    img = np.ascontiguousarray(img, np.float32).reshape(-1, 2)
+    r, t = np.zeros(3), np.zeros(3)
+    lib().oracle_epnp(len(wld), _p(wld), _p(img), _p(np.ascontiguousarray(K, np.float64)), _p(r), _p(t))
+    return r, t
+
+
+def project(wld, rvec, tvec, K):
+    wld = np.ascontiguousarray(wld, np.float32).reshape(-1, 3)
+    uv = np.zeros((len(wld), 2), np.float32)
+    lib().oracle_project(len(wld), _p(wld), _p(np.ascontiguousarray(rvec, np.float64).reshape(3)),
+                         _p(np.ascontiguousarray(tvec, np.float64).reshape(3)), _p(np.ascontiguousarray(K, np.float64)),
+                         _p(uv))
+    return uv
+
+
+def sigma_lm_core(wld, xn, w, delta, rvec, tvec):
+    """The sigma-weighted Huber LM on normalised observations xn [n,2] with row weights w [n,2]."""
+    wld = np.ascontiguousarray(wld, np.float64).reshape(-1, 3)
+    r = np.array(rvec, np.float64).reshape(3).copy()
+    t = np.array(tvec, np.float64).reshape(3).copy()
+    lib().oracle_sigma_lm_core(len(wld), _p(wld), _p(np.ascontiguousarray(xn, np.float64).reshape(-1)),
+                               _p(np.ascontiguousarray(w, np.float64).reshape(-1)), float(delta), _p(r), _p(t))
+    return r, t
+
+
+def rodrigues(rvec):
+    R = np.zeros(9)
+    lib().oracle_rodrigues(_p(np.ascontiguousarray(rvec, np.float64).reshape(3)), _p(R))
+    return R.reshape(3, 3)
+
+
+def blender_quat(R):
+    q = np.zeros(4, np.float32)
+    lib().oracle_blender_quat(_p(np.ascontiguousarray(R, np.float64).reshape(9)), _p(q))
+    return q
 
 
 def speed_score(q_pr, t_pr, q_gt, t_gt):

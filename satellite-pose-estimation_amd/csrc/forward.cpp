@@ -51,20 +51,28 @@ int run_other(spe_model* m, const char* kind, double flops, double bytes, hipStr
   return rc;
 }
 
+// fp32x3 models: split-bf16 MFMA unless the launch kind is listed in x3_exact
+static bool x3_for(const spe_model* m, const char* kind) {
+  if (!m->x3) return false;
+  for (const auto& p : m->x3_exact)
+    if (std::strncmp(kind, p.c_str(), p.size()) == 0) return false;
+  return true;
+}
+
 int run_gemm(spe_model* m, const char* kind, const GemmArgs& g, int mode, hipStream_t s) {
   const double E = m->esz;
   const double a_elems = mode == GEMM_CONV ? (double)(g.M / (g.Ho * g.Wo)) * g.H * g.W * g.Cin : (double)g.M * g.K;
   const double r_rows = g.R ? (g.r_period > 0 ? (double)g.r_period : (double)g.M) : 0.0;
   const double bytes = (a_elems + (double)g.N * g.K + (double)g.M * g.N + r_rows * g.N) * E +
                        (mode == GEMM_LINEAR_ADD ? (double)g.prow * g.K * E : 0.0);
-  return run_other(m, kind, 2.0 * g.M * g.N * g.K, bytes, s,
-                   [&] { return spe_launch_gemm(g, m->x3 ? (int)SPE_DTYPE_F32X3 : m->cfg.dtype, mode, s); });
+  const int dt = !x3_for(m, kind) ? m->cfg.dtype : m->x6 ? (int)SPE_DTYPE_F32X6 : (int)SPE_DTYPE_F32X3;
+  return run_other(m, kind, 2.0 * g.M * g.N * g.K, bytes, s, [&] { return spe_launch_gemm(g, dt, mode, s); });
 }
 
 int run_attn(spe_model* m, const char* kind, const AttnArgs& a, int dtype, hipStream_t s) {
   const double flops = 4.0 * a.B * a.H * (double)a.Tq * a.Tk * 32;
   const double bytes = (double)a.B * a.H * 32 * (2.0 * a.Tq + 2.0 * a.Tk) * m->esz;
-  const int dt = (m->x3 && dtype == SPE_DTYPE_F32) ? (int)SPE_DTYPE_F32X3 : dtype;
+  const int dt = (x3_for(m, kind) && dtype == SPE_DTYPE_F32) ? (int)SPE_DTYPE_F32X3 : dtype;
   return run_other(m, kind, flops, bytes, s, [&] { return spe_launch_attention(a, dt, s); });
 }
 
@@ -244,7 +252,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       int rc = 1;
       if (nb && blk.c3ds.N == 256) {
         rc = tail(*nb, P(w.ds), uld, blk.c3ds.K, nullptr, blk.c3ds, outbuf, B * Ho * Ho);
-        if (rc < 0) CK(rc);
+        if (rc != 0 && rc != 1) CK(rc);   // 1 = shapes not served: the GEMM pair below
       }
       if (rc == 1) {
         GemmArgs g = linear_args(blk.c3ds, P(w.ds), uld, B * Ho * Ho, P(outbuf), blk.c3ds.N);
@@ -272,7 +280,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       int rc = 1;
       if (nb && blk.c3.N == 256) {
         rc = tail(*nb, P(w.t2), blk.c2.N, blk.c3.K, P(res), blk.c3, outbuf, B * Ho * Ho);
-        if (rc < 0) CK(rc);
+        if (rc != 0 && rc != 1) CK(rc);   // 1 = shapes not served: the GEMM pair below
       }
       if (rc == 1) {
         GemmArgs g = linear_args(blk.c3, P(w.t2), blk.c2.N, B * Ho * Ho, P(outbuf), blk.c3.N);
@@ -604,15 +612,16 @@ int spe_postprocess(void* stream, const float* logits, const float* points, cons
 int spe_pnp_batch(void* stream, const float* points_px, const float* probs, const float* sigmas, int B, int Q, int C,
                   const double* K, const double* world, int mode, float repro, int ransac_iters, double confidence,
                   float* quat, double* tvec, double* rvec, int32_t* status, int32_t* n_corr, int32_t* corr_label,
-                  uint32_t* inlier_mask) {
+                  uint32_t* inlier_mask, const float* repro_per_image) {
   if (!points_px || !probs || !K || !world || !quat || !tvec || B < 0 || Q <= 0 || Q > 64 || C < 2 || C > 17)
     return fail(SPE_E_ARG, "bad argument");
-  if (mode < SPE_PNP_EPNP || mode > SPE_PNP_EPNP_LM) return fail(SPE_E_ARG, "bad solver mode");
+  if (mode < SPE_PNP_EPNP || mode > SPE_PNP_EPNP_CERES) return fail(SPE_E_ARG, "bad solver mode");
   if (ransac_iters < 1 || ransac_iters > 255 || !(confidence > 0 && confidence < 1))
     return fail(SPE_E_ARG, "ransac_iters must be in [1,255], confidence in (0,1)");
   PnpArgs a{};
   a.points = points_px; a.probs = probs; a.sigmas = sigmas;
   a.B = B; a.Q = Q; a.C = C; a.K = K; a.world = world; a.mode = mode; a.repro = repro;
+  a.repro_img = repro_per_image;
   a.ransac_iters = ransac_iters; a.confidence = confidence;
   a.quat = quat; a.tvec = tvec; a.rvec = rvec; a.status = status; a.n_corr = n_corr;
   a.corr_label = corr_label; a.inlier_mask = inlier_mask;

@@ -35,10 +35,10 @@ constexpr int SMEM_BYTES = (2 * STAGE_BYTES > BM * EPI_LD * 4) ? 2 * STAGE_BYTES
 
 SPE_DEV int swz(int row, int chunk) { return row * 128 + ((chunk ^ (row & 7)) << 4); }
 
-template <typename T, int MODE>
+template <typename T, int MODE, int RS = 32>
 struct ALoader {
   static constexpr int CE = Chunk<T>::CE;
-  // per-thread: 4 rows, one chunk column
+  // per-thread: 4 rows RS apart, one chunk column
   const char* base[4];
   int ih0[4], iw0[4];
   bool rv[4];
@@ -46,7 +46,7 @@ struct ALoader {
   SPE_DEV void init(const GemmArgs& g, int m0, int tid) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      int m = m0 + (tid >> 3) + 32 * i;
+      int m = m0 + (tid >> 3) + RS * i;
       rv[i] = m < g.M;
       int mm = rv[i] ? m : 0;
       if (MODE == GEMM_CONV) {
@@ -99,13 +99,13 @@ struct ALoader {
   }
 };
 
-template <typename T>
+template <typename T, int NR = 4, int RS = 32>
 SPE_DEV void load_b(const GemmArgs& g, int n0, int kstep, int tid, u32x4* r) {
   constexpr int BKE = 128 / sizeof(T);
   const int k = kstep * BKE + (tid & 7) * Chunk<T>::CE;
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    int n = n0 + (tid >> 3) + 32 * i;
+  for (int i = 0; i < NR; ++i) {
+    int n = n0 + (tid >> 3) + RS * i;
     r[i] = (n < g.N) ? ld16((const char*)g.B + ((size_t)n * g.ldb + k) * sizeof(T)) : u32x4{0, 0, 0, 0};
   }
 }
@@ -211,6 +211,105 @@ SPE_DEV void mma_step(const char* st, int wr, int wc, int lane, f32x4 (&acc)[4][
     }
 }
 
+// bias / residual / activation / head-transposed or row stores of a BM_ x BN tile whose fp32
+// accumulators are in LDS (ct, row stride EPI_LD), NT_ threads; bv = the thread's 8 bias values
+template <typename T, int BM_, int NT_>
+SPE_DEV void store_tile(const GemmArgs& g, const float* ct, int m0, int n0, int tid, const float* bv) {
+  if (g.vt_T > 0) {
+    // head-transposed store: column n = grp*256 + hd -> C[((grp*vt_B + b)*256 + hd)*T + tok]
+    const int col = tid & 127, n = n0 + col;
+    if (n >= g.N) return;
+    const float bn = g.bias ? g.bias[n] : 0.f;
+    const int grp = n >> 8, hd = n & 255;
+    for (int rg = (tid >> 7) * 8; rg < BM_; rg += NT_ / 16) {
+      const int m = m0 + rg;
+      if (m >= g.M) break;
+      float v[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = ct[(rg + e) * EPI_LD + col] + bn;
+      const int b = m / g.vt_T, tok = m - b * g.vt_T;
+      const size_t rowbase = ((size_t)(grp * g.vt_B + b) * 256 + hd) * g.vt_T;
+      if ((g.vt_T & 7) == 0 && m + 8 <= g.M) {
+        char* cp = (char*)g.C + (rowbase + tok) * sizeof(T);
+        if constexpr (sizeof(T) == 2) {
+          const u32x4 pk = pack_out8(v, g.out_f16);
+          if (g.vt_swz) {                        // the two quads land apart (vt_pos)
+            st8((char*)g.C + (rowbase + vt_pos(tok)) * 2, u32x2{pk.x, pk.y});
+            st8((char*)g.C + (rowbase + vt_pos(tok + 4)) * 2, u32x2{pk.z, pk.w});
+          } else {
+            st16(cp, pk);
+          }
+        } else {
+          st16(cp, pack16<T>(v));
+          st16(cp + 16, pack16<T>(v + 4));
+        }
+      } else {
+        for (int e = 0; e < 8 && m + e < g.M; ++e) {
+          const int me = m + e, be = me / g.vt_T, te = me - be * g.vt_T;
+          const size_t idx = ((size_t)(grp * g.vt_B + be) * 256 + hd) * g.vt_T + (g.vt_swz ? vt_pos(te) : te);
+          if constexpr (sizeof(T) == 2) store_out1(g.C, idx, v[e], g.out_f16);
+          else ((T*)g.C)[idx] = from_f32<T>(v[e]);
+        }
+      }
+    }
+    return;
+  }
+
+  const int cg = (tid & 15) * 8;
+  const int n = n0 + cg;
+  if (n >= g.N) return;
+  const bool full = n + 8 <= g.N;
+  for (int rr = tid >> 4; rr < BM_; rr += NT_ / 16) {
+    const int m = m0 + rr;
+    if (m >= g.M) break;
+    float v[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = ct[rr * EPI_LD + cg + e] + bv[e];
+    auto add_res = [&]() {                         // residual, or row-periodic add (pos . W^T)
+      const T* rp = (const T*)g.R + (size_t)(g.r_period > 0 ? m % g.r_period : m) * g.ldr + n;
+      if (full) {
+        float f[8];
+        unpack16<T>(ld16(rp), f);
+        if constexpr (sizeof(T) == 4) unpack16<T>(ld16(rp + 4), f + 4);
+#pragma unroll
+        for (int e = 0; e < 8; ++e) v[e] += f[e];
+      } else {
+        for (int e = 0; e < 8 && n + e < g.N; ++e) v[e] += to_f32(rp[e]);
+      }
+    };
+    if (g.R && !g.res_post) add_res();
+    if (g.act) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], g.act);
+    }
+    if (g.R && g.res_post) add_res();
+    if (g.out_f32) {
+      float* cp = (float*)g.C + (size_t)m * g.ldc + n;
+      if (full) {
+        st16(cp, pack16<float>(v));
+        st16(cp + 4, pack16<float>(v + 4));
+      } else {
+        for (int e = 0; e < 8 && n + e < g.N; ++e) cp[e] = v[e];
+      }
+    } else {
+      T* cp = (T*)g.C + (size_t)m * g.ldc + n;
+      if (full) {
+        if constexpr (sizeof(T) == 2) {
+          st16(cp, pack_out8(v, g.out_f16));
+        } else {
+          st16(cp, pack16<T>(v));
+          st16(cp + 4, pack16<T>(v + 4));
+        }
+      } else {
+        for (int e = 0; e < 8 && n + e < g.N; ++e) {
+          if constexpr (sizeof(T) == 2) store_out1(cp, e, v[e], g.out_f16);
+          else cp[e] = from_f32<T>(v[e]);
+        }
+      }
+    }
+  }
+}
+
 template <typename T, int MODE, bool X3 = false>
 __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) char smem[SMEM_BYTES];
@@ -274,99 +373,160 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs g) {
   }
   __syncthreads();
 
-  if (g.vt_T > 0) {
-    // head-transposed store: column n = grp*256 + hd -> C[((grp*vt_B + b)*256 + hd)*T + tok]
-    const int col = tid & 127, n = n0 + col;
-    if (n >= g.N) return;
-    const float bv = g.bias ? g.bias[n] : 0.f;
-    const int grp = n >> 8, hd = n & 255;
-    for (int rg = (tid >> 7) * 8; rg < BM; rg += 16) {
-      const int m = m0 + rg;
-      if (m >= g.M) break;
-      float v[8];
+  store_tile<T, BM, NT>(g, ct, m0, n0, tid, bv);
+}
+
+// ------------------------------------------------------------------ fp32x6 (near-fp32) kernel
+// fp32 operands split while staged into three bf16 planes, x = h + m + l (h = bf16(x),
+// m = bf16(x - h), l = bf16(x - h - m); both remainders exact in fp32, x - h - m - l within 2^-24
+// of |x|), every fragment product as the six terms of relative order >= 2^-16 --
+// l.h + h.l + m.m + m.h + h.m + h.h, small terms first -- on mfma_f32_16x16x32_bf16 with fp32
+// accumulation: the product error is that of an fp32 FMA chain (~2^-24) at six bf16 MFMAs, i.e.
+// 2.65x the fp32 MFMA ceiling (417 vs 157 TFLOP/s).  256 x 128 tiles, 8 waves of 64 x 64, one
+// 32-element K-step per stage: planes [3][rows][64 B] with the 16-byte chunk XOR-swizzled by
+// row bits 2-3 (conflict-free ds_read_b128 for the 16 rows of a fragment), two stages (144 KiB)
+// so the next step's global loads and split overlap this step's MFMAs; one workgroup per CU.
+constexpr int BM6 = 256, BN6 = 128, NT6 = 512;
+constexpr int PLANE_A6 = BM6 * 64, PLANE_B6 = BN6 * 64;
+constexpr int STAGE6 = 3 * (PLANE_A6 + PLANE_B6);     // 72 KiB
+constexpr int SMEM6 = (2 * STAGE6 > BM6 * EPI_LD * 4) ? 2 * STAGE6 : BM6 * EPI_LD * 4;
+
+SPE_DEV int swz6(int row, int chunk) { return row * 64 + ((chunk ^ ((row >> 2) & 3)) << 4); }
+
+// 4 fp32 -> bf16 planes h, m, l (4 values each, RNE; remainders exact)
+SPE_DEV void split3(u32x4 x, u32x2& h, u32x2& m, u32x2& l) {
+  const f32x4 f = __builtin_bit_cast(f32x4, x);
+  const uint32_t h0 = pack_bf16x2(f[0], f[1]), h1 = pack_bf16x2(f[2], f[3]);
+  const float r0 = f[0] - __uint_as_float(h0 << 16), r1 = f[1] - __uint_as_float(h0 & 0xffff0000u);
+  const float r2 = f[2] - __uint_as_float(h1 << 16), r3 = f[3] - __uint_as_float(h1 & 0xffff0000u);
+  const uint32_t m0 = pack_bf16x2(r0, r1), m1 = pack_bf16x2(r2, r3);
+  const float s0 = r0 - __uint_as_float(m0 << 16), s1 = r1 - __uint_as_float(m0 & 0xffff0000u);
+  const float s2 = r2 - __uint_as_float(m1 << 16), s3 = r3 - __uint_as_float(m1 & 0xffff0000u);
+  h = u32x2{h0, h1};
+  m = u32x2{m0, m1};
+  l = u32x2{pack_bf16x2(s0, s1), pack_bf16x2(s2, s3)};
+}
+
+// the thread's fp32 chunk c4 (elements 4 c4 .. 4 c4 + 3 of the K-step) of `rows` rows RS apart
+// -> 8-byte pieces of bf16 chunk c4 >> 1 in each plane
+template <int NR, int RS, int PLANE>
+SPE_DEV void store_split6(char* st, int tid, const u32x4* r) {
+  const int c4 = tid & 7, half = (c4 & 1) * 8;
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = ct[(rg + e) * EPI_LD + col] + bv;
-      const int b = m / g.vt_T, tok = m - b * g.vt_T;
-      const size_t rowbase = ((size_t)(grp * g.vt_B + b) * 256 + hd) * g.vt_T;
-      if ((g.vt_T & 7) == 0 && m + 8 <= g.M) {
-        char* cp = (char*)g.C + (rowbase + tok) * sizeof(T);
-        if constexpr (sizeof(T) == 2) {
-          const u32x4 pk = pack_out8(v, g.out_f16);
-          if (g.vt_swz) {                        // the two quads land apart (vt_pos)
-            st8((char*)g.C + (rowbase + vt_pos(tok)) * 2, u32x2{pk.x, pk.y});
-            st8((char*)g.C + (rowbase + vt_pos(tok + 4)) * 2, u32x2{pk.z, pk.w});
-          } else {
-            st16(cp, pk);
-          }
-        } else {
-          st16(cp, pack16<T>(v));
-          st16(cp + 16, pack16<T>(v + 4));
-        }
-      } else {
-        for (int e = 0; e < 8 && m + e < g.M; ++e) {
-          const int me = m + e, be = me / g.vt_T, te = me - be * g.vt_T;
-          const size_t idx = ((size_t)(grp * g.vt_B + be) * 256 + hd) * g.vt_T + (g.vt_swz ? vt_pos(te) : te);
-          if constexpr (sizeof(T) == 2) store_out1(g.C, idx, v[e], g.out_f16);
-          else ((T*)g.C)[idx] = from_f32<T>(v[e]);
-        }
-      }
+  for (int i = 0; i < NR; ++i) {
+    const int row = (tid >> 3) + RS * i;
+    u32x2 h, m, l;
+    split3(r[i], h, m, l);
+    const int o = swz6(row, c4 >> 1) + half;
+    st8(st + o, h);
+    st8(st + PLANE + o, m);
+    st8(st + 2 * PLANE + o, l);
+  }
+}
+
+SPE_DEV void mma_step_x6(const char* st, int wr, int wc, int lane, f32x4 (&acc)[4][4]) {
+  const int g = lane >> 4, rr = lane & 15;
+  const char* sa = st;
+  const char* sb = st + 3 * PLANE_A6;
+  u32x4 a[3][4], b[3][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int o = swz6(wr * 64 + i * 16 + rr, g);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) a[p][i] = ld16(sa + p * PLANE_A6 + o);
+  }
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int o = swz6(wc * 64 + j * 16 + rr, g);
+#pragma unroll
+    for (int p = 0; p < 3; ++p) b[p][j] = ld16(sb + p * PLANE_B6 + o);
+  }
+  auto mf = [](u32x4 x, u32x4 y, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, x), __builtin_bit_cast(bf16x8, y), c, 0, 0, 0);
+  };
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      f32x4 c = acc[i][j];
+      c = mf(a[2][i], b[0][j], c);      // l.h
+      c = mf(a[0][i], b[2][j], c);      // h.l
+      c = mf(a[1][i], b[1][j], c);      // m.m
+      c = mf(a[1][i], b[0][j], c);      // m.h
+      c = mf(a[0][i], b[1][j], c);      // h.m
+      acc[i][j] = mf(a[0][i], b[0][j], c);   // h.h
     }
-    return;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(NT6, 1) void gemm_x6_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) char smem[SMEM6];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 1, wc = wid & 1;
+  const int tilesN = (g.N + BN6 - 1) / BN6;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (t / tilesN) * BM6, n0 = (t % tilesN) * BN6;
+  const int nk = (g.K + 31) / 32;
+
+  ALoader<float, MODE, 64> al;
+  al.init(g, m0, tid);
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float bv[8];
+  {
+    const int n = n0 + (tid & 15) * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bv[e] = (g.bias && n + e < g.N) ? g.bias[n + e] : 0.f;
+  }
+  u32x4 ra[4], rb[2];
+  auto stage = [&](char* st) {
+    store_split6<4, 64, PLANE_A6>(st, tid, ra);
+    store_split6<2, 64, PLANE_B6>(st + 3 * PLANE_A6, tid, rb);
+  };
+  al.load(g, 0, tid, ra);
+  load_b<float, 2, 64>(g, n0, 0, tid, rb);
+  stage(smem);
+  __syncthreads();
+  for (int ks = 0; ks < nk; ++ks) {
+    const bool more = ks + 1 < nk;
+    if (more) {
+      al.load(g, ks + 1, tid, ra);
+      load_b<float, 2, 64>(g, n0, ks + 1, tid, rb);
+    }
+    mma_step_x6(smem + (ks & 1) * STAGE6, wr, wc, lane, acc);
+    if (more) stage(smem + ((ks + 1) & 1) * STAGE6);
+    __syncthreads();
   }
 
-  const int cg = (tid & 15) * 8;
-  const int n = n0 + cg;
-  if (n >= g.N) return;
-  const bool full = n + 8 <= g.N;
-  for (int rr = tid >> 4; rr < BM; rr += 16) {
-    const int m = m0 + rr;
-    if (m >= g.M) break;
-    float v[8];
+  float* ct = reinterpret_cast<float*>(smem);
+  {
+    const int q = lane >> 4, c = lane & 15;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = ct[rr * EPI_LD + cg + e] + bv[e];
-    auto add_res = [&]() {                         // residual, or row-periodic add (pos . W^T)
-      const T* rp = (const T*)g.R + (size_t)(g.r_period > 0 ? m % g.r_period : m) * g.ldr + n;
-      if (full) {
-        float f[8];
-        unpack16<T>(ld16(rp), f);
-        if constexpr (sizeof(T) == 4) unpack16<T>(ld16(rp + 4), f + 4);
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int e = 0; e < 8; ++e) v[e] += f[e];
-      } else {
-        for (int e = 0; e < 8 && n + e < g.N; ++e) v[e] += to_f32(rp[e]);
-      }
-    };
-    if (g.R && !g.res_post) add_res();
-    if (g.act) {
+      for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], g.act);
-    }
-    if (g.R && g.res_post) add_res();
-    if (g.out_f32) {
-      float* cp = (float*)g.C + (size_t)m * g.ldc + n;
-      if (full) {
-        st16(cp, pack16<float>(v));
-        st16(cp + 4, pack16<float>(v + 4));
-      } else {
-        for (int e = 0; e < 8 && n + e < g.N; ++e) cp[e] = v[e];
-      }
-    } else {
-      T* cp = (T*)g.C + (size_t)m * g.ldc + n;
-      if (full) {
-        if constexpr (sizeof(T) == 2) {
-          st16(cp, pack_out8(v, g.out_f16));
-        } else {
-          st16(cp, pack16<T>(v));
-          st16(cp + 4, pack16<T>(v + 4));
-        }
-      } else {
-        for (int e = 0; e < 8 && n + e < g.N; ++e) {
-          if constexpr (sizeof(T) == 2) store_out1(cp, e, v[e], g.out_f16);
-          else cp[e] = from_f32<T>(v[e]);
-        }
-      }
-    }
+        for (int r = 0; r < 4; ++r)
+          ct[(wr * 64 + i * 16 + q * 4 + r) * EPI_LD + wc * 64 + j * 16 + c] = acc[i][j][r];
   }
+  __syncthreads();
+  store_tile<float, BM6, NT6>(g, ct, m0, n0, tid, bv);
+}
+
+int launch_x6(const GemmArgs& g, int mode, hipStream_t s) {
+  const int tiles = ((g.M + BM6 - 1) / BM6) * ((g.N + BN6 - 1) / BN6);
+  if (tiles <= 0) return 0;
+  dim3 grid(tiles), block(NT6);
+  switch (mode) {
+    case GEMM_LINEAR: hipLaunchKernelGGL((gemm_x6_kernel<GEMM_LINEAR>), grid, block, 0, s, g); break;
+    case GEMM_LINEAR_ADD: hipLaunchKernelGGL((gemm_x6_kernel<GEMM_LINEAR_ADD>), grid, block, 0, s, g); break;
+    case GEMM_CONV: hipLaunchKernelGGL((gemm_x6_kernel<GEMM_CONV>), grid, block, 0, s, g); break;
+    default: return -1;
+  }
+  return (int)hipGetLastError();
 }
 
 template <typename T, bool X3 = false>
@@ -405,5 +565,6 @@ int spe_launch_gemm(const GemmArgs& g, int dtype, int mode, hipStream_t s) {
   }
   spe_gemm_last_path = 0;
   if (dtype == SPE_DTYPE_F32X3) return launch_t<float, true>(g, mode, s);
+  if (dtype == SPE_DTYPE_F32X6) return launch_x6(g, mode, s);
   return dtype == SPE_DTYPE_BF16 ? launch_t<bf16>(g, mode, s) : launch_t<float>(g, mode, s);
 }

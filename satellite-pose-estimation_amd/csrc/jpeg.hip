@@ -652,17 +652,25 @@ __global__ __launch_bounds__(SCAN_NT) void jpeg_blocks_kernel(const JpegImg* __r
 }
 
 // block index at each entry = the segment's first block + the counts of the segment's earlier
-// subsequences (one thread per subsequence)
-__global__ __launch_bounds__(HUFF_NT) void jpeg_blocks_fix_kernel(const JpegImg* __restrict__ imgs, Sub* subs,
+// subsequences (one thread per subsequence).  The last subsequence of every segment also checks
+// that the segment's data completed all of its blocks: a truncated entropy-coded segment (short
+// file, short restart interval) would otherwise leave blocks unwritten -- the coefficient buffer
+// is never cleared -- so the image is marked corrupt (Pillow raises "image file is truncated")
+__global__ __launch_bounds__(HUFF_NT) void jpeg_blocks_fix_kernel(JpegImg* __restrict__ imgs, Sub* subs,
                                                                     const int* __restrict__ segblk,
                                                                     const int* __restrict__ segfirst, JpegWs ws) {
   const int b = blockIdx.y, k = blockIdx.x * HUFF_NT + threadIdx.x;
-  const JpegImg& im = imgs[b];
+  JpegImg& im = imgs[b];
   if (im.status != ST_OK || k >= im.nsub) return;
   Sub* sb = subs + (size_t)b * ws.max_sub;
   const int sg = sb[k].seg;
   const size_t so = (size_t)b * (ws.max_seg + 1) + sg;
-  sb[k].blk = sb[k].blkp - sb[segfirst[so]].blkp + segblk[so];
+  const int p0 = sb[segfirst[so]].blkp;
+  sb[k].blk = sb[k].blkp - p0 + segblk[so];
+  if (k + 1 == im.nsub || sb[k + 1].seg != sg) {
+    const int decoded = sb[k].blkp + sb[k].cnt - p0;
+    if (decoded < segblk[so + 1] - segblk[so]) im.status = ST_CORRUPT;
+  }
 }
 
 // decode again from the true entries, writing DC differences and AC coefficients (natural

@@ -378,6 +378,22 @@ __device__ void bcast_pose(LmShared& sh, double* rvec, double* tvec, int lane) {
   __syncthreads();
 }
 
+// float32 reprojection error of correspondence `lane` under (rvec, t) into err[lane]; returns the
+// np.sum of err[0 .. nl) on every lane (pose uniform across lanes)
+__device__ float repro_errors_wave(float* err, const cam_t* k, const float* img_f, const float* wld_f, int nl,
+                                   const double* rvec, const double* t, int lane) {
+  __syncthreads();
+  if (lane < nl) {
+    double R[9];
+    rodrigues_r2R(rvec, R);
+    float uv[2];
+    project_f(k, R, t, wld_f + 3 * lane, uv);
+    err[lane] = repro_err_f(img_f + 2 * lane, uv);
+  }
+  __syncthreads();
+  return np_sum_f32(err, nl);
+}
+
 // sigma_lm (pnp_math.h) over the selected correspondences, all lanes; result uniform
 __device__ void sigma_lm_wave(LmShared& sh, const cam_t* k, const LmPoint& pt, int n, double delta, double* rvec,
                               double* tvec, int lane) {
@@ -566,6 +582,7 @@ __global__ __launch_bounds__(WAVE) void pnp_kernel(PnpArgs a) {
   __shared__ double s_rt[MAXIT][6];
   __shared__ EpnpShared s_ep;
   __shared__ LmShared s_lm;
+  __shared__ float s_err[MAXN];
 
   const cam_t k = {a.K[0], a.K[4], a.K[2], a.K[5]};
 
@@ -582,14 +599,32 @@ __global__ __launch_bounds__(WAVE) void pnp_kernel(PnpArgs a) {
     status = SPE_PNP_NO_FG;
   } else if (nl < 4) {
     status = SPE_PNP_CV_ERROR;
-  } else if (a.mode == SPE_PNP_EPNP || a.mode == SPE_PNP_EPNP_LM) {
+  } else if (a.mode == SPE_PNP_EPNP || a.mode == SPE_PNP_EPNP_LM || a.mode == SPE_PNP_EPNP_CERES) {
     epnp_solve_wave(s_ep, &k, s_img, s_wld, nl, all, 1, rvec, t, lane);
+    bcast_pose(s_lm, rvec, t, lane);
     if (a.mode == SPE_PNP_EPNP_LM) {
-      bcast_pose(s_lm, rvec, t, lane);
       lm_refine_wave(s_lm, &k, lm_point(s_img, s_wld, nullptr, nl, all, lane), nl, rvec, t, lane);
+      inl = all;
+    } else {
+      // epnp_init (UNC/utils/speed_eval_ceres.py:153-169): float32 reprojection errors of every
+      // correspondence, inliers err < th, and their np.sum
+      const float th = a.repro_img ? a.repro_img[b] : a.repro;
+      const float before = repro_errors_wave(s_err, &k, s_img, s_wld, nl, rvec, t, lane);
+      inl = (uint32_t)__ballot(lane < nl && (double)s_err[lane] < (double)th);
+      const int m = __popc(inl);
+      if (a.mode == SPE_PNP_EPNP_CERES && m == 1) {
+        status = SPE_PNP_NO_FG;                    // obj_pts[idx, 0] on a squeezed 1-D array: IndexError
+      } else if (a.mode == SPE_PNP_EPNP_CERES && m >= 2) {
+        // ceres_pnp (:172-243) on the inliers, weights normalised over them, HuberLoss(0.001);
+        // keep the EPnP pose if the refined error sum over all points is larger (:142-146)
+        double r2[3] = {rvec[0], rvec[1], rvec[2]}, t2[3] = {t[0], t[1], t[2]};
+        sigma_lm_wave(s_lm, &k, lm_point(s_img, s_wld, s_sig, nl, inl, lane), m, 0.001, r2, t2, lane);
+        const float after = repro_errors_wave(s_err, &k, s_img, s_wld, nl, r2, t2, lane);
+        if (!(after > before))
+          for (int c = 0; c < 3; ++c) { rvec[c] = r2[c]; t[c] = t2[c]; }
+      }
     }
-    inl = all;
-    have_pose = true;
+    have_pose = status == SPE_PNP_OK;
   } else {
     const int kernel = (a.mode == SPE_PNP_RANSAC_P3P_LM || nl == 4) ? 0 : 1;
     const int mp = kernel == 0 ? 4 : 5;

@@ -416,6 +416,32 @@ PNP_FN float sq_err_f(const float* obs, const float* proj) {
   return dx * dx + dy * dy;
 }
 
+/* np.linalg.norm(projected - observed, axis=-1) of one float32 point (UNC/utils/speed_eval_ceres.py
+ * :143,164): float32 difference, squares, sum and root */
+PNP_FN float repro_err_f(const float* obs, const float* proj) {
+  const float dx = proj[0] - obs[0], dy = proj[1] - obs[1];
+  const float dx2 = dx * dx, dy2 = dy * dy;
+  return sqrtf(dx2 + dy2);
+}
+
+/* np.sum of a contiguous float32 vector: numpy's pairwise summation (sequential below 8
+ * elements, 8 accumulators combined pairwise above), float32 throughout */
+PNP_FN float np_sum_f32(const float* a, int n) {
+  if (n < 8) {
+    float r = 0.f;
+    for (int i = 0; i < n; ++i) r += a[i];
+    return r;
+  }
+  float r[8];
+  for (int j = 0; j < 8; ++j) r[j] = a[j];
+  int i = 8;
+  for (; i < n - (n % 8); i += 8)
+    for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+  float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
+  for (; i < n; ++i) res += a[i];
+  return res;
+}
+
 /* ------------------------------------------------------------------ polynomial roots */
 PNP_FN int solve_deg2(double a, double b, double c, double* x1, double* x2) {
   double delta = b * b - 4 * a * c;

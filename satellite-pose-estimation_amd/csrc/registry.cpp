@@ -587,16 +587,29 @@ int spe_model_create(const spe_model_config* cfg, spe_model** out) {
   if (cfg->input_size % 16 || cfg->input_size < 32) return fail(SPE_E_ARG, "input_size must be a multiple of 16");
   if (cfg->num_queries < 1 || cfg->num_queries > 64) return fail(SPE_E_ARG, "num_queries must be in [1, 64]");
   if (cfg->dim_feedforward % 64) return fail(SPE_E_ARG, "dim_feedforward must be a multiple of 64");
-  if (cfg->dtype != SPE_DTYPE_BF16_ && cfg->dtype != SPE_DTYPE_F32_ && cfg->dtype != SPE_DTYPE_F32X3_)
+  if (cfg->dtype != SPE_DTYPE_BF16_ && cfg->dtype != SPE_DTYPE_F32_ && cfg->dtype != SPE_DTYPE_F32X3_ &&
+      cfg->dtype != SPE_DTYPE_F32X6_)
     return fail(SPE_E_ARG, "bad dtype");
   if (cfg->attn_dtype != 0 && cfg->attn_dtype != cfg->dtype &&
       !(cfg->attn_dtype == SPE_DTYPE_F16_ && cfg->dtype == SPE_DTYPE_BF16_))
     return fail(SPE_E_ARG, "attn_dtype: 0, the model dtype, or SPE_DTYPE_F16_ for bf16 models");
   spe_model* m = new spe_model();
   m->cfg = *cfg;
-  // fp32x3: the fp32 model (storage, layouts, kernels' fp32 paths) with split-bf16 MFMA compute
-  m->x3 = cfg->dtype == SPE_DTYPE_F32X3_;
+  // fp32x3: the fp32 model (storage, layouts, kernels' fp32 paths) with split-bf16 MFMA compute;
+  // fp32x6: the same with the GEMMs / convolutions on the three-way split (x6) path
+  m->x6 = cfg->dtype == SPE_DTYPE_F32X6_;
+  m->x3 = cfg->dtype == SPE_DTYPE_F32X3_ || m->x6;
   if (m->x3) { m->cfg.dtype = SPE_DTYPE_F32_; if (m->cfg.attn_dtype) m->cfg.attn_dtype = SPE_DTYPE_F32_; }
+  if (m->x3)
+    if (const char* e = getenv("SPE_X3_EXACT")) {
+      std::string s(e);
+      for (size_t p = 0; p <= s.size();) {
+        size_t q = s.find(',', p);
+        if (q == std::string::npos) q = s.size();
+        if (q > p) m->x3_exact.push_back(s.substr(p, q - p));
+        p = q + 1;
+      }
+    }
   m->esz = cfg->dtype == SPE_DTYPE_BF16_ ? 2 : 4;
   m->spec = build_spec(*cfg);
   *out = m;

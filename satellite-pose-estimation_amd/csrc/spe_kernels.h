@@ -6,7 +6,8 @@
 
 enum { SPE_DTYPE_BF16 = 0, SPE_DTYPE_F32 = 1, SPE_DTYPE_F16 = 2,    // F16: attention operands only
        SPE_DTYPE_BF16_F16V = 3,     // attention only: bf16 q/k, fp16 V^T and P (bf16 models' encoder)
-       SPE_DTYPE_F32X3 = 4 };       // fp32 storage, split-bf16 (hi.hi + hi.lo + lo.hi) MFMA compute
+       SPE_DTYPE_F32X3 = 4,         // fp32 storage, split-bf16 (hi.hi + hi.lo + lo.hi) MFMA compute
+       SPE_DTYPE_F32X6 = 5 };       // fp32 storage, three-way split-bf16 (6 products, ~fp32) MFMA compute (GEMMs)
 enum { GEMM_LINEAR = 0, GEMM_LINEAR_ADD = 1, GEMM_CONV = 2 };
 // GEMM epilogue activations: ReLU (ResNet, DETR FFN), SiLU (UNC hybrid encoder ConvNormLayer,
 // hybrid_encoder.py:17-37), exact-erf GELU (UNC AIFI FFN, torch nn.GELU default)

@@ -19,7 +19,8 @@ struct PnpArgs {
   const double* K;         // 3x3 row-major (device)
   const double* world;     // [C-1][3] landmarks (device)
   int mode;                // SPE_PNP_*
-  float repro;             // RANSAC reprojection threshold (px)
+  float repro;             // RANSAC / inlier reprojection threshold (px)
+  const float* repro_img;  // [B] per-image threshold replacing repro (EPnPCeresSolver's area rule) or null
   int ransac_iters;        // cv2 default 100
   double confidence;       // cv2 default 0.99
   float* quat;             // [B][4] (float32 values, mathutils)

@@ -76,15 +76,17 @@ __global__ __launch_bounds__(64 * MAXW, OCC) void stempool_kernel(const bf16* __
   const int row0 = 4 * p0 - 2, col0 = 28 * f0 - 2;  // first padded-input row / column of the patch
 
   // ---- patch: PROWS rows x pwid pixels (8 bytes each), lane-linear 1 KB pieces
+  // one descriptor per image (64-bit base), so the 32-bit offsets never grow with the batch
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)x, (short)0, (int)std::min<long long>((long long)(b + 1) * p.SP * p.SP * 8, PBAD), 0x00020000);
+      (void*)((const char*)x + (size_t)b * p.SP * p.SP * 8), (short)0,
+      (int)std::min<long long>((long long)p.SP * p.SP * 8, PBAD), 0x00020000);
   const int pieces = (PROWS * p.pitch + 1023) >> 10;
   for (int q = wid; q < pieces; q += nw) {
     const int o = q * 1024 + lane * 16;
     const int pr = o / p.pitch, pc = (o - pr * p.pitch) >> 3;
     const int ir = row0 + pr, ic = col0 + pc;
     const bool v = pr < PROWS && ir >= 0 && ir < p.SP && ic >= 0 && ic < p.SP;
-    const int off = v ? (((b * p.SP + ir) * p.SP + ic) << 3) : PBAD;
+    const int off = v ? ((ir * p.SP + ic) << 3) : PBAD;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_ptr_t)(patch + q * 1024), 16, off, 0, 0, 0);
   }
   // ---- weights: 64 rows x 28 chunks, padded pitch

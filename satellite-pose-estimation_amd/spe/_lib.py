@@ -14,10 +14,13 @@ import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 # HIP graph capture of this library's launches (PosePipeline(use_graph=True)) replays correctly
 # only with the ROCm runtime's graph packet capture off: with it on, a replay issued after the
 # stream has synchronised reads wrong kernel arguments (measured: the first replay is exact, the
-# later ones are not).  The runtime reads the switch when HIP initialises,
-# so it is set here, which takes effect when no device call preceded this import (the pipeline
-# verifies its captured graph against eager execution either way).
-os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
+# later ones are not).  The runtime reads the switch when HIP initialises and
+# it applies to every graph of the process, so importing spe does not set it: a caller that wants
+# graph capture sets DEBUG_CLR_GRAPH_PACKET_CAPTURE=0 before its first device call (tests/conftest.py
+# does), or opts in with SPE_GRAPH_CAPTURE=1 before importing spe.  The pipeline verifies its
+# captured graph against eager execution either way and raises if they differ.
+if os.environ.get("SPE_GRAPH_CAPTURE") == "1":
+    os.environ.setdefault("DEBUG_CLR_GRAPH_PACKET_CAPTURE", "0")
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SPE_LIB_PATH") or os.path.join(_HERE, "libspe.so")   # override: kernel A/B builds
@@ -28,9 +31,9 @@ I64 = ctypes.c_int64
 F = ctypes.c_float
 D = ctypes.c_double
 
-SPE_DTYPE_BF16, SPE_DTYPE_F32, SPE_DTYPE_F16, SPE_DTYPE_F32X3 = 0, 1, 2, 4
+SPE_DTYPE_BF16, SPE_DTYPE_F32, SPE_DTYPE_F16, SPE_DTYPE_F32X3, SPE_DTYPE_F32X6 = 0, 1, 2, 4, 5
 SPE_STAGE_ENCODE, SPE_STAGE_DECODE, SPE_STAGE_BACKBONE, SPE_STAGE_TRANSFORMER = 1, 2, 4, 8
-SPE_PNP_EPNP, SPE_PNP_RANSAC_P3P_LM, SPE_PNP_EPNP_RANSAC_SIGMA, SPE_PNP_EPNP_LM = 0, 1, 2, 3
+SPE_PNP_EPNP, SPE_PNP_RANSAC_P3P_LM, SPE_PNP_EPNP_RANSAC_SIGMA, SPE_PNP_EPNP_LM, SPE_PNP_EPNP_CERES = 0, 1, 2, 3, 4
 SPE_PNP_OK, SPE_PNP_NO_FG, SPE_PNP_CV_ERROR, SPE_PNP_RANSAC_FALLBACK, SPE_PNP_UNPINNED = 0, 1, 2, 3, 4
 
 # every symbol include/spe.h declares (checked by tests/test_capi.py)
@@ -96,7 +99,7 @@ def lib():
     L.spe_preprocess.argtypes = [P, P, I, I, I, I, P, I, P, P, P]
     L.spe_ensemble_fuse.argtypes = [P, P, P, I, I, I, I, P, P]
     L.spe_criterion.argtypes = [P, P, P, P, P, I, I, I, I, I, F, F, F, D, P, P]
-    L.spe_pnp_batch.argtypes = [P, P, P, P, I, I, I, P, P, I, F, I, D, P, P, P, P, P, P, P]
+    L.spe_pnp_batch.argtypes = [P, P, P, P, I, I, I, P, P, I, F, I, D, P, P, P, P, P, P, P, P]
     L.spe_speed_score.argtypes = [P, P, P, P, P, I, P, P]
     L.spe_self_assess.argtypes = [P, P, P, P, P, P, I, I, I, F, F, I, P, P, P]
     L.spe_model_profile_begin.argtypes = [P, ctypes.c_char_p]
@@ -120,7 +123,7 @@ def lib():
     L.spe_jpeg_workspace_bytes.argtypes = [I, I, I, I64]
     L.spe_jpeg_workspace_bytes.restype = I64
     L.spe_jpeg_decode.argtypes = [P, P, P, P, I, I, I, I64, P, P, P, I64]
-    if L.spe_abi_version() != 4:
+    if L.spe_abi_version() != 5:
         raise ImportError("libspe.so ABI version mismatch")
     _lib = L
     return L

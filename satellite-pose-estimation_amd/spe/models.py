@@ -28,7 +28,9 @@ class DETR(nn.Module):
     dtype "bf16": bf16 storage / MFMA with fp32 accumulation, softmax, LayerNorm and heads
     (throughput path).  dtype "fp32": exact-f32 MFMA everywhere (parity path).  dtype "fp32x3":
     the fp32 model with split-bf16 MFMA compute (every fp32 operand x = hi + lo in bf16, products
-    hi.hi + hi.lo + lo.hi, fp32 accumulation; fast parity path).
+    hi.hi + hi.lo + lo.hi, fp32 accumulation; fast parity path).  dtype "fp32x6": the accuracy-contract
+    mode -- fp32x3's attention, every GEMM / convolution at near-fp32 precision (three-way split,
+    six products).
     attn_dtype "fp16" (bf16 models): the encoder self-attention's q/k/V operands are stored
     and multiplied in fp16 (BASELINE config 5, "fp16 MFMA attention")."""
 
@@ -48,7 +50,7 @@ class DETR(nn.Module):
         c = _lib.ModelConfig(cfg.input_size, cfg.num_queries, cfg.enc_layers, cfg.dec_layers, cfg.hidden_dim,
                              cfg.nheads, cfg.dim_feedforward, int(cfg.sigma_head),
                              {"bf16": _lib.SPE_DTYPE_BF16, "fp32": _lib.SPE_DTYPE_F32,
-                              "fp32x3": _lib.SPE_DTYPE_F32X3}[dtype],
+                              "fp32x3": _lib.SPE_DTYPE_F32X3, "fp32x6": _lib.SPE_DTYPE_F32X6}[dtype],
                              _lib.SPE_DTYPE_F16 if self.attn_dtype == "fp16" else 0)
         h = ctypes.c_void_p()
         _lib.check(L.spe_model_create(ctypes.byref(c), ctypes.byref(h)), "spe_model_create")

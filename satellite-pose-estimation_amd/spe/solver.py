@@ -19,7 +19,8 @@ from . import _lib
 from .config import Camera, world_points
 
 MODES = {"epnp": _lib.SPE_PNP_EPNP, "ransac_p3p_lm": _lib.SPE_PNP_RANSAC_P3P_LM,
-         "epnp_ransac_sigma": _lib.SPE_PNP_EPNP_RANSAC_SIGMA, "epnp_lm": _lib.SPE_PNP_EPNP_LM}
+         "epnp_ransac_sigma": _lib.SPE_PNP_EPNP_RANSAC_SIGMA, "epnp_lm": _lib.SPE_PNP_EPNP_LM,
+         "epnp_ceres": _lib.SPE_PNP_EPNP_CERES}
 
 
 class SolverError(RuntimeError):
@@ -45,10 +46,11 @@ class PoseSolver:
                               torch.as_tensor(self.W_Pt, dtype=torch.float64, device=device).contiguous())
         return self._dev[key]
 
-    def solve_batch(self, points_px, probs, sigmas=None, stream=None, out=None):
+    def solve_batch(self, points_px, probs, sigmas=None, stream=None, out=None, repro_per_image=None):
         """points_px [B,Q,2], probs [B,Q,C] (+ sigmas [B,Q,2]) device fp32 -> dict of device
         tensors quat [B,4] f32, tvec [B,3] f64, rvec, status, n_corr, corr_label [B,16],
-        inlier_mask [B]."""
+        inlier_mask [B].  repro_per_image: device fp32 [B] thresholds replacing
+        reprojectionError image by image (EPnPCeresSolver)."""
         B, Q, C = probs.shape
         dev = probs.device
         Kd, Wd = self._consts(dev)
@@ -64,7 +66,8 @@ class PoseSolver:
             _lib.ptr(sigmas.contiguous() if sigmas is not None else None), B, Q, C, _lib.ptr(Kd), _lib.ptr(Wd),
             self.mode, self.reprojectionError, self.ransac_iters, self.confidence, _lib.ptr(out["quat"]),
             _lib.ptr(out["tvec"]), _lib.ptr(out["rvec"]), _lib.ptr(out["status"]), _lib.ptr(out["n_corr"]),
-            _lib.ptr(out["corr_label"]), _lib.ptr(out["inlier_mask"])), "spe_pnp_batch")
+            _lib.ptr(out["corr_label"]), _lib.ptr(out["inlier_mask"]),
+            _lib.ptr(repro_per_image.float().contiguous() if repro_per_image is not None else None)), "spe_pnp_batch")
         return out
 
     def self_assess(self, probs, sigmas, poses, score_th=0.5, sigma_th=5.0, min_inliers=4, stream=None):
@@ -121,11 +124,42 @@ class SimplePoseSolverSigma(PoseSolver):
 
 
 class EPnPSolver(PoseSolver):
-    """solvePnPGeneric(EPNP) on all selected points (UNC/utils/speed_eval_ceres.py:153-169);
-    BASELINE config 2 ("EPnP only, no RANSAC")."""
+    """solvePnPGeneric(EPNP) on all selected points (UNC/utils/speed_eval_ceres.py:153-169, epnp_init);
+    BASELINE config 2 ("EPnP only, no RANSAC").  inlier_mask: epnp_init's set, reprojection error
+    < reprojectionError."""
 
     def __init__(self, args=None, refine=False):
         super().__init__(_lib.SPE_PNP_EPNP_LM if refine else _lib.SPE_PNP_EPNP, 20.0)
+
+
+class EPnPCeresSolver(PoseSolver):
+    """UNC EPnPCeresSolver (UNC/utils/speed_eval_ceres.py:43-243): EPnP on every selected point,
+    inliers = reprojection error < the threshold of the image's box area (get_repro_th), the
+    sigma-weighted Huber(0.001) LM on the inliers, and the EPnP pose kept when the refined error
+    sum over all points is larger.  A batch carries one threshold per image."""
+
+    def __init__(self, input_size=256):
+        super().__init__(_lib.SPE_PNP_EPNP_CERES, 20.0)
+        self.input_size = input_size
+
+    def get_repro_th(self, area):
+        """UNC/utils/speed_eval_ceres.py:53-58 (int() truncation, then [1.5, 20])."""
+        repro = int(area / self.input_size * 10)
+        repro = min(max(repro, 1.5), 20)
+        self.reprojectionError = float(repro)
+        return self.reprojectionError
+
+    def solve_batch(self, points_px, probs, sigmas=None, stream=None, out=None, repro_per_image=None, area=None):
+        """As PoseSolver.solve_batch; `area` (sequence of B box areas) sets the per-image thresholds."""
+        if repro_per_image is None and area is not None:
+            th = [self.get_repro_th(float(a)) for a in area]
+            repro_per_image = torch.tensor(th, dtype=torch.float32, device=probs.device)
+        return super().solve_batch(points_px, probs, sigmas, stream=stream, out=out, repro_per_image=repro_per_image)
+
+    def __call__(self, points, logits, area, sigma, device=None):
+        """One image, the reference's signature (:70): numpy in / numpy out."""
+        self.get_repro_th(area)
+        return PoseSolver.__call__(self, points, logits, sigma, device=device)
 
 
 class Multi_Mean_PoseSolver(PoseSolver):
@@ -171,4 +205,6 @@ def build_solver(args=None):
         return SimplePoseSolverSigma(args)
     if name in ("epnp", "epnp_lm"):
         return EPnPSolver(args, refine=name == "epnp_lm")
+    if name == "epnp_ceres":
+        return EPnPCeresSolver(getattr(args, "input_size", 256) if args is not None else 256)
     raise ValueError(f"unknown solver {name}")

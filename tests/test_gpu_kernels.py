@@ -20,6 +20,7 @@ pytestmark = pytest.mark.gpu
 
 DT = {"bf16": (_lib.SPE_DTYPE_BF16, torch.bfloat16, 1e-2), "fp32": (_lib.SPE_DTYPE_F32, torch.float32, 1e-4),
       "fp32x3": (_lib.SPE_DTYPE_F32X3, torch.float32, 1e-4),
+      "fp32x6": (_lib.SPE_DTYPE_F32X6, torch.float32, 1e-4),
       "fp16": (_lib.SPE_DTYPE_F16, torch.float16, 2e-3)}
 
 
@@ -787,10 +788,12 @@ def test_gemm_f16_store_saturates(gpu_device, rows):
 
 
 # ---------------------------------------------------------------- fp32x3 (split-bf16) parity mode
+@pytest.mark.parametrize("dtype,tol", [("fp32x3", 2e-5), ("fp32x6", 1e-6)])
 @pytest.mark.parametrize("case", ["linear", "linear_add_relu_res", "conv3x3", "conv1x1s2", "vt"])
-def test_gemm_x3_close_to_fp64(gpu_device, case):
-    """fp32 storage, split-bf16 MFMA (hi.hi + hi.lo + lo.hi): within 2e-5 relative of an fp64
-    reference, i.e. far inside the fp32 parity tolerances and ~100x tighter than bf16."""
+def test_gemm_x3_close_to_fp64(gpu_device, case, dtype, tol):
+    """fp32 storage, split-bf16 MFMA: fp32x3 (hi.hi + hi.lo + lo.hi) within 2e-5 relative of an
+    fp64 reference, i.e. far inside the fp32 parity tolerances and ~100x tighter than bf16;
+    fp32x6 (three-way split, six products) within 1e-6, i.e. fp32-level."""
     g = torch.Generator(device="cpu").manual_seed(len(case))
     dev, f = gpu_device, torch.float32
     if case.startswith("conv"):
@@ -803,7 +806,7 @@ def test_gemm_x3_close_to_fp64(gpu_device, case):
         Ho = (H + 2 * pd - k) // st + 1
         M, K = B * Ho * Ho, Cin * k * k
         C = torch.zeros(M, Cout, dtype=f, device=dev)
-        _gemm("fp32x3", 2, A, Wp, M, Cout, K, 0, K, C, Cout, conv=(H, H, Cin, k, k, st, pd))
+        _gemm(dtype, 2, A, Wp, M, Cout, K, 0, K, C, Cout, conv=(H, H, Cin, k, k, st, pd))
         got = C
     else:
         M, N, K = (3000, 200, 512) if case != "vt" else (2 * 2704, 256, 256)
@@ -821,15 +824,15 @@ def test_gemm_x3_close_to_fp64(gpu_device, case):
         if case == "vt":
             T, Bv = 2704, 2
             C = torch.zeros(Bv * N * T, dtype=f, device=dev)
-            _gemm("fp32x3", 0, A.to(dev, f), _padded_weight(Wt.to(dev, f), K, f), M, N, K, K, K, C, 4,
+            _gemm(dtype, 0, A.to(dev, f), _padded_weight(Wt.to(dev, f), K, f), M, N, K, K, K, C, 4,
                   bias=bias.to(dev, f), vt=(T, Bv))
             got = C.view(N // 256, Bv, 256, T).permute(1, 3, 0, 2).reshape(M, N)
         else:
-            _gemm("fp32x3", 0, A.to(dev, f), _padded_weight(Wt.to(dev, f), K, f), M, N, K, K, K, C, ldc,
+            _gemm(dtype, 0, A.to(dev, f), _padded_weight(Wt.to(dev, f), K, f), M, N, K, K, K, C, ldc,
                   bias=bias.to(dev, f), **kw)
             got = C[:, :N]
     err = (got.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
-    assert err <= 2e-5, err
+    assert err <= tol, err
 
 
 @pytest.mark.parametrize("B,H,Tq,Tk", [(1, 8, 300, 333), (2, 8, 2704, 2704), (3, 8, 11, 2704), (2, 8, 11, 11)])

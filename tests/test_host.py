@@ -198,3 +198,40 @@ def test_gloo_world2_speedeval_equals_world1():
         np.testing.assert_array_equal(rec[:, 4:7], d["tvec"][idx])
         np.testing.assert_array_equal(rec[:, 9], d["status"][idx])
         np.testing.assert_allclose(rec[:, 8], 2 * rec[:, 7])
+
+
+def _bench_line(stdout):
+    lines = [l for l in stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, stdout
+    return json.loads(lines[0])
+
+
+def test_bench_launcher_spawns_ranks():
+    """`python bench.py --gpus 2` (the driver's command form, no torchrun env) starts two ranks
+    through the launcher; rank 0's single line reports the whole job.  The
+    SPE_BENCH_STUB worker runs the rank bookkeeping over gloo with no GPU work."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, SPE_BENCH_STUB="1", OMP_NUM_THREADS="1")
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--batch", "4", "--steps", "3",
+                        "--warmup", "1"], env=env, capture_output=True, text=True, timeout=180)
+    assert r.returncode == 0, r.stderr[-2000:]
+    d = _bench_line(r.stdout)
+    assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 8 and d["config"]["per_gpu_batch"] == 4
+    assert d["records_gathered_per_step"] == 8
+    assert d["value"] > 0 and d["steps"] == 3
+
+
+def test_bench_rejects_world_mismatch():
+    """A rank whose world size differs from --gpus exits non-zero instead of reporting n_gpus 1."""
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, SPE_BENCH_STUB="1", RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1",
+               MASTER_PORT=str(29400 + os.getpid() % 500))
+    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--batch", "4", "--steps", "1"],
+                       env=env, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2 and "world size" in r.stderr

@@ -98,6 +98,47 @@ def test_jpeg_batch_mixed_and_unsupported(gpu_device):
         assert (got[i] == 0).all()
 
 
+def _truncated_files(fr):
+    """A file cut at 60 % (no EOI: Pillow raises "image file is truncated"), the same cut with an EOI
+    appended, and a file whose third restart interval lost two thirds of its bytes."""
+    f = _encode(fr[0], quality=75)
+    cut = f[:int(len(f) * 0.6)]
+    g = _encode(fr[1], quality=75, restart_marker_blocks=4)
+    rst = [i for i in range(len(g) - 1) if g[i] == 0xFF and 0xD0 <= g[i + 1] <= 0xD7]
+    p2, p3 = rst[2], rst[3]
+    short = g[:p2 + 2] + g[p2 + 2:p2 + 2 + (p3 - p2 - 2) // 3] + g[p3:]
+    return [cut, cut + b"\xff\xd9", short]
+
+
+@pytest.mark.gpu
+def test_jpeg_truncated_streams_are_corrupt(gpu_device):
+    """Entropy-coded data that ends before the frame's blocks are complete is status 2 (corrupt) with
+    a zero frame -- never a frame holding an earlier image's coefficients (the coefficient buffer is
+    reused uncleared).  The neighbours in the batch decode exactly.  Pillow raises on the cut file
+    without EOI (checked here); with an EOI, or with a short restart interval, libjpeg instead warns
+    and paints the rest of the segment gray -- that recovery is not reproduced (status 2)."""
+    from spe.datasets import JpegDecoder
+    h, w = 96, 128
+    fr = _frames(4, h, w, seed=11)
+    bad = _truncated_files(fr)
+    with pytest.raises(OSError):
+        Image.open(io.BytesIO(bad[0])).load()
+    good = [_encode(fr[2], quality=80), _encode(fr[3], quality=60, restart_marker_blocks=4)]
+    dec = JpegDecoder(h, w, max_bytes=max(len(f) for f in good + bad))
+    # decode the good files first so the workspace holds coefficients of real images
+    dec(*JpegDecoder.pack(good + good[:1], gpu_device))
+    files = [good[0], bad[0], bad[1], good[1], bad[2]]
+    o = dec(*JpegDecoder.pack(files, gpu_device))
+    torch.cuda.synchronize()
+    st = o["status"].cpu().numpy()
+    got = o["frames"].cpu().numpy()
+    np.testing.assert_array_equal(st, [0, 2, 2, 0, 2])
+    np.testing.assert_array_equal(got[0], _pillow(good[0]))
+    np.testing.assert_array_equal(got[3], _pillow(good[1]))
+    for i in (1, 2, 4):
+        assert (got[i] == 0).all()
+
+
 @pytest.mark.gpu
 def test_jpeg_to_model_input_matches_pillow_path(gpu_device):
     """Decode -> spe_preprocess on the device equals Pillow's decode -> the same preprocess on

@@ -253,3 +253,73 @@ def test_hip_score_matches_reference(gpu_device):
             assert abs(s_t[i] - a) <= 1e-12
         if not np.isnan(b):
             assert abs(s_q[i] - b) <= 1e-9
+
+
+# ------------------------------------------------------------------ EPnPCeresSolver (a18, UNC)
+def _ceres_inputs():
+    th = np.array([pnp_ref.repro_th(a) for a in G["ceres_area"]], np.float32)
+    return G["ceres_points"], G["ceres_probs"], G["ceres_sigmas"], th
+
+
+def test_oracle_epnp_ceres_matches_reference():
+    """UNC EPnPCeresSolver.__call__ run by oracle/gen_golden_solver_front.py through to its return
+    value (the reference's own control flow: area threshold, selection, inliers err < th, sigma
+    weights over the inliers, Huber 0.001, revert-if-worse; OpenCV / PyCeres / mathutils as the
+    oracle's primitives) against oracle/pnp_ref.c's mode 4: thresholds, statuses, inlier sets and
+    poses identical."""
+    pts, probs, sig, th = _ceres_inputs()
+    ok = G["ceres_status"] == 0
+    np.testing.assert_array_equal(th[np.isfinite(G["ceres_th"])], G["ceres_th"][np.isfinite(G["ceres_th"])])
+    assert set(np.unique(th)) >= {1.5, 20.0} and ok.sum() > 60 and G["ceres_reverted"].sum() > 5
+    K, W = pnp_ref_K()
+    o = pnp_ref.pnp_batch(pts, probs, K, W, mode=pnp_ref.MODE_EPNP_CERES, sigmas=sig, repro_per_image=th)
+    np.testing.assert_array_equal(o["status"], G["ceres_status"])
+    has = G["ceres_n"] > 0
+    np.testing.assert_array_equal(o["n_corr"][has], G["ceres_n"][has])
+    for b in np.nonzero(has)[0]:
+        np.testing.assert_array_equal(o["corr_label"][b, :G["ceres_n"][b]], G["ceres_labels"][b, :G["ceres_n"][b]])
+    lm = ok & (G["ceres_lm_ran"] == 1)
+    np.testing.assert_array_equal(o["inlier_mask"][lm], G["ceres_inliers"][lm])
+    np.testing.assert_array_equal(o["tvec"][ok], G["ceres_tvec"][ok])
+    np.testing.assert_array_equal(o["quat"][ok], G["ceres_quat"][ok])
+
+
+def pnp_ref_K():
+    from spe.config import Camera, world_points
+    return Camera.K, world_points()
+
+
+def test_host_repro_th_matches_reference():
+    """spe.solver.EPnPCeresSolver.get_repro_th == the thresholds the reference computed."""
+    from spe.solver import EPnPCeresSolver
+    s = EPnPCeresSolver()
+    fin = np.isfinite(G["ceres_th"])
+    got = np.array([s.get_repro_th(a) for a in G["ceres_area"]])
+    np.testing.assert_array_equal(got[fin], G["ceres_th"][fin])
+
+
+@pytest.mark.gpu
+def test_hip_epnp_ceres_matches_reference(gpu_device):
+    """The HIP solver's mode 4 (EPnPCeresSolver) on raw queries + sigmas + per-image area
+    thresholds against the reference's recorded run: statuses (IndexError / cv2.error mapping),
+    selection, inlier sets exact; poses |dq| <= 1e-5, |dt|/|t| <= 1e-6 (the fp64 LM of the device
+    and of the oracle primitives the recording used)."""
+    import torch
+    from spe.solver import EPnPCeresSolver
+    pts, probs, sig, th = _ceres_inputs()
+    d = gpu_device
+    o = EPnPCeresSolver().solve_batch(torch.from_numpy(pts).to(d), torch.from_numpy(probs).to(d),
+                                      torch.from_numpy(sig).to(d), area=G["ceres_area"])
+    torch.cuda.synchronize()
+    o = {k: v.cpu().numpy() for k, v in o.items()}
+    np.testing.assert_array_equal(o["status"], G["ceres_status"])
+    has = G["ceres_n"] > 0
+    np.testing.assert_array_equal(o["n_corr"][has], G["ceres_n"][has])
+    for b in np.nonzero(has)[0]:
+        np.testing.assert_array_equal(o["corr_label"][b, :G["ceres_n"][b]], G["ceres_labels"][b, :G["ceres_n"][b]])
+    ok = G["ceres_status"] == 0
+    lm = ok & (G["ceres_lm_ran"] == 1)
+    np.testing.assert_array_equal(o["inlier_mask"][lm].astype(np.uint32), G["ceres_inliers"][lm])
+    dq = np.abs(o["quat"][ok].astype(np.float64) - G["ceres_quat"][ok]).max()
+    dt = (np.linalg.norm(o["tvec"][ok] - G["ceres_tvec"][ok], axis=1) / np.linalg.norm(G["ceres_tvec"][ok], axis=1)).max()
+    assert dq <= 1e-5 and dt <= 1e-6, (dq, dt)
