@@ -276,7 +276,8 @@ int spe_debug_gemm(void* stream, int dtype, int mode, const void* A, int lda, co
  * N == 256 and enough rows for the large-tile kernel, else SPE_E_LAUNCH) */
 /* kernel family that served this thread's last gemm launch: 0 the 128x128 kernel, 1 the large-tile
  * kernels (gemm2.hip), 2 the persistent streaming kernel for short-K problems (gemm_stream.hip),
- * 3 the patch-staged 3x3 conv (pconv.hip), 4 the projection + residual + LayerNorm (lnproj.hip) */
+ * 3 the patch-staged 3x3 conv (pconv.hip), 4 the projection + residual + LayerNorm (lnproj.hip),
+ * 5 the fp32x6 three-way split kernel (gemm.hip) */
 int spe_debug_gemm_path(void);
 int spe_debug_attention(void* stream, int dtype, const void* q, int ldq, const void* k, int ldk, const void* vt,
                         void* o, int ldo, int B, int H, int Tq, int Tk, float scale);

@@ -107,13 +107,14 @@ def _mlp3(x, sd, p):
 def forward(images, sd, cfg, return_stages=False):
     """images [B,3,S,S] fp32 -> dict(pred_logits [B,Q,12], pred_points [B,Q,2], hs [L,B,Q,d],
     optional pred_sigmas [B,Q,2])."""
-    sd = {k: torch.as_tensor(v, dtype=torch.float32) for k, v in sd.items()}
     images = torch.as_tensor(images, dtype=torch.float32)
+    dev = images.device                                 # CPU, or a GPU for the precision-floor test
+    sd = {k: torch.as_tensor(v, dtype=torch.float32).to(dev) for k, v in sd.items()}
     xs8, xs16, neck = backbone_s8(images, sd)
     B, _, h, w = neck.shape
     nh = cfg.nheads
     src = F.conv2d(neck, sd["input_proj.weight"], sd["input_proj.bias"])
-    pos = sine_pos(h, w, cfg.hidden_dim)[None].expand(B, -1, -1, -1)
+    pos = sine_pos(h, w, cfg.hidden_dim).to(dev)[None].expand(B, -1, -1, -1)
     src = src.flatten(2).transpose(1, 2)               # [B, HW, d] (row-major h*W + w)
     pos = pos.flatten(2).transpose(1, 2)
     for i in range(cfg.enc_layers):

@@ -444,21 +444,27 @@ SPE_DEV void mma_step_x6(const char* st, int wr, int wc, int lane, f32x4 (&acc)[
   auto mf = [](u32x4 x, u32x4 y, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, x), __builtin_bit_cast(bf16x8, y), c, 0, 0, 0);
   };
+  // the step's six products go to a fresh accumulator, which is then added to the running sum
+  // with an IEEE fp32 add: accumulated in the MFMA across the whole K extent, the sum of small
+  // terms onto a large running value measured 3x the error of the exact-f32 kernel on the bench
+  // weights (the MFMA's internal alignment of the addends is not a correctly rounded fp32 add)
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      f32x4 c = acc[i][j];
-      c = mf(a[2][i], b[0][j], c);      // l.h
+      f32x4 c = mf(a[2][i], b[0][j], f32x4{0.f, 0.f, 0.f, 0.f});   // l.h
       c = mf(a[0][i], b[2][j], c);      // h.l
       c = mf(a[1][i], b[1][j], c);      // m.m
       c = mf(a[1][i], b[0][j], c);      // m.h
       c = mf(a[0][i], b[1][j], c);      // h.m
-      acc[i][j] = mf(a[0][i], b[0][j], c);   // h.h
+      c = mf(a[0][i], b[0][j], c);      // h.h
+      acc[i][j] += c;
     }
 }
 
-template <int MODE>
+// BP: the weights arrive pre-split (GemmArgs::B6, bf16 planes [3][N][ldb] written at finalize):
+// one 16-byte chunk per plane and thread per K-step, no split work for the B tile
+template <int MODE, bool BP>
 __global__ __launch_bounds__(NT6, 1) void gemm_x6_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) char smem[SMEM6];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -481,20 +487,40 @@ __global__ __launch_bounds__(NT6, 1) void gemm_x6_kernel(GemmArgs g) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) bv[e] = (g.bias && n + e < g.N) ? g.bias[n + e] : 0.f;
   }
-  u32x4 ra[4], rb[2];
+  u32x4 ra[4], rb[3];
+  // BP: row tid >> 2 of the tile, 16-byte chunk tid & 3 of the step's 64 bytes, in each plane
+  const int brow = tid >> 2, bch = tid & 3;
+  const size_t pstride = (size_t)g.b6_rows * g.ldb;
+  const bool bvalid = n0 + brow < g.N;
+  const char* bsrc = (const char*)g.B6 + ((size_t)(bvalid ? n0 + brow : 0) * g.ldb + bch * 8) * 2;
+  auto load_bp = [&](int kstep) {
+#pragma unroll
+    for (int p = 0; p < 3; ++p)
+      rb[p] = bvalid ? ld16(bsrc + (p * pstride + (size_t)kstep * 32) * 2) : u32x4{0, 0, 0, 0};
+  };
   auto stage = [&](char* st) {
     store_split6<4, 64, PLANE_A6>(st, tid, ra);
-    store_split6<2, 64, PLANE_B6>(st + 3 * PLANE_A6, tid, rb);
+    if constexpr (BP) {
+      char* sb = st + 3 * PLANE_A6 + swz6(brow, bch);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) st16(sb + p * PLANE_B6, rb[p]);
+    } else {
+      store_split6<2, 64, PLANE_B6>(st + 3 * PLANE_A6, tid, rb);
+    }
+  };
+  auto load_bt = [&](int kstep) {
+    if constexpr (BP) load_bp(kstep);
+    else load_b<float, 2, 64>(g, n0, kstep, tid, rb);
   };
   al.load(g, 0, tid, ra);
-  load_b<float, 2, 64>(g, n0, 0, tid, rb);
+  load_bt(0);
   stage(smem);
   __syncthreads();
   for (int ks = 0; ks < nk; ++ks) {
     const bool more = ks + 1 < nk;
     if (more) {
       al.load(g, ks + 1, tid, ra);
-      load_b<float, 2, 64>(g, n0, ks + 1, tid, rb);
+      load_bt(ks + 1);
     }
     mma_step_x6(smem + (ks & 1) * STAGE6, wr, wc, lane, acc);
     if (more) stage(smem + ((ks + 1) & 1) * STAGE6);
@@ -520,10 +546,14 @@ int launch_x6(const GemmArgs& g, int mode, hipStream_t s) {
   const int tiles = ((g.M + BM6 - 1) / BM6) * ((g.N + BN6 - 1) / BN6);
   if (tiles <= 0) return 0;
   dim3 grid(tiles), block(NT6);
-  switch (mode) {
-    case GEMM_LINEAR: hipLaunchKernelGGL((gemm_x6_kernel<GEMM_LINEAR>), grid, block, 0, s, g); break;
-    case GEMM_LINEAR_ADD: hipLaunchKernelGGL((gemm_x6_kernel<GEMM_LINEAR_ADD>), grid, block, 0, s, g); break;
-    case GEMM_CONV: hipLaunchKernelGGL((gemm_x6_kernel<GEMM_CONV>), grid, block, 0, s, g); break;
+  const bool bp = g.B6 != nullptr;
+  switch (mode * 2 + bp) {
+    case GEMM_LINEAR * 2: hipLaunchKernelGGL((gemm_x6_kernel<GEMM_LINEAR, false>), grid, block, 0, s, g); break;
+    case GEMM_LINEAR * 2 + 1: hipLaunchKernelGGL((gemm_x6_kernel<GEMM_LINEAR, true>), grid, block, 0, s, g); break;
+    case GEMM_LINEAR_ADD * 2: hipLaunchKernelGGL((gemm_x6_kernel<GEMM_LINEAR_ADD, false>), grid, block, 0, s, g); break;
+    case GEMM_LINEAR_ADD * 2 + 1: hipLaunchKernelGGL((gemm_x6_kernel<GEMM_LINEAR_ADD, true>), grid, block, 0, s, g); break;
+    case GEMM_CONV * 2: hipLaunchKernelGGL((gemm_x6_kernel<GEMM_CONV, false>), grid, block, 0, s, g); break;
+    case GEMM_CONV * 2 + 1: hipLaunchKernelGGL((gemm_x6_kernel<GEMM_CONV, true>), grid, block, 0, s, g); break;
     default: return -1;
   }
   return (int)hipGetLastError();
@@ -565,6 +595,12 @@ int spe_launch_gemm(const GemmArgs& g, int dtype, int mode, hipStream_t s) {
   }
   spe_gemm_last_path = 0;
   if (dtype == SPE_DTYPE_F32X3) return launch_t<float, true>(g, mode, s);
-  if (dtype == SPE_DTYPE_F32X6) return launch_x6(g, mode, s);
+  if (dtype == SPE_DTYPE_F32X6) {
+    // few-row problems (the decoder's B*Q rows) would leave most CUs idle on 256 x 128 tiles:
+    // they take the 128 x 128 exact-f32 kernel, which is at least as precise
+    const int tiles6 = ((g.M + BM6 - 1) / BM6) * ((g.N + BN6 - 1) / BN6);
+    spe_gemm_last_path = tiles6 >= 128 ? 5 : 0;
+    return tiles6 >= 128 ? launch_x6(g, mode, s) : launch_t<float>(g, mode, s);
+  }
   return dtype == SPE_DTYPE_BF16 ? launch_t<bf16>(g, mode, s) : launch_t<float>(g, mode, s);
 }

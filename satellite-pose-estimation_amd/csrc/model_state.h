@@ -114,6 +114,9 @@ struct spe_model {
   // kernels instead of the split-bf16 ones -- the per-stage precision study of DESIGN.md §4
   // (SPE_X3_EXACT="kind,kind,..." read at spe_model_create)
   std::vector<std::string> x3_exact;
+  // fp32x6 models: fp32 weight block -> (its bf16 planes [3][rows][Kpad] h, m, l, rows), written
+  // at finalize next to each packed weight (upload_rows) so the x6 GEMM never splits weights
+  std::map<const void*, std::pair<const void*, int>> w6;
   RtModel* rt = nullptr;
   spe_model_config cfg{};
   int esz = 2;

@@ -101,19 +101,44 @@ void* dalloc(spe_model* m, size_t bytes) {
   return m->dmem ? (void*)(m->dmem + off) : nullptr;
 }
 
-// pack host fp32 [N][K] rows (already in K order) into device T [N][Kpad]
+// bf16 bits -> the float they represent
+static float bf2f(uint16_t b) {
+  const uint32_t u = (uint32_t)b << 16;
+  float f;
+  std::memcpy(&f, &u, 4);
+  return f;
+}
+
+// pack host fp32 [N][K] rows (already in K order) into device T [N][Kpad]; fp32x6 models also
+// get the rows' three-way bf16 split x = hi + mid + lo (RNE each, remainders exact in fp32) as
+// planes [3][N][Kpad] right after them, registered in m->w6 for the x6 GEMM
 void* upload_rows(spe_model* m, const std::vector<float>& rows, int N, int K, int Kpad) {
-  void* dst = dalloc(m, (size_t)N * Kpad * m->esz);
+  const size_t n = (size_t)N * Kpad;
+  void* dst = dalloc(m, n * m->esz);
+  void* pl = (m->x6 && m->esz == 4) ? dalloc(m, 3 * n * 2) : nullptr;   // sized in both passes
   if (!m->dmem) return nullptr;
   if (m->esz == 2) {
-    std::vector<uint16_t> h((size_t)N * Kpad, 0);
-    for (int n = 0; n < N; ++n)
-      for (int k = 0; k < K; ++k) h[(size_t)n * Kpad + k] = f2bf(rows[(size_t)n * K + k]);
+    std::vector<uint16_t> h(n, 0);
+    for (int r = 0; r < N; ++r)
+      for (int k = 0; k < K; ++k) h[(size_t)r * Kpad + k] = f2bf(rows[(size_t)r * K + k]);
     m->upload_err |= (int)hipMemcpy(dst, h.data(), h.size() * 2, hipMemcpyHostToDevice);
   } else {
-    std::vector<float> h((size_t)N * Kpad, 0.f);
-    for (int n = 0; n < N; ++n) std::memcpy(&h[(size_t)n * Kpad], &rows[(size_t)n * K], (size_t)K * 4);
+    std::vector<float> h(n, 0.f);
+    for (int r = 0; r < N; ++r) std::memcpy(&h[(size_t)r * Kpad], &rows[(size_t)r * K], (size_t)K * 4);
     m->upload_err |= (int)hipMemcpy(dst, h.data(), h.size() * 4, hipMemcpyHostToDevice);
+    if (pl) {
+      std::vector<uint16_t> b(3 * n);
+      for (size_t i = 0; i < n; ++i) {
+        const uint16_t hi = f2bf(h[i]);
+        const float r = h[i] - bf2f(hi);
+        const uint16_t mid = f2bf(r);
+        b[i] = hi;
+        b[n + i] = mid;
+        b[2 * n + i] = f2bf(r - bf2f(mid));
+      }
+      m->upload_err |= (int)hipMemcpy(pl, b.data(), b.size() * 2, hipMemcpyHostToDevice);
+      m->w6[dst] = {pl, N};
+    }
   }
   return dst;
 }

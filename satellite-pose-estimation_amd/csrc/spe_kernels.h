@@ -31,6 +31,7 @@ struct GemmArgs {
                                    // each 16-token group the middle quads swap (vt_pos; vt_T % 16 == 0)
   int r_period;                    // >0: residual row = m % r_period (row-periodic add, e.g. pos . W^T)
   const float* ln_g; const float* ln_b;   // optional fused post-norm LayerNorm over N == 256 (bf16, large M)
+  const void* B6; int b6_rows;     // fp32x6: the weights pre-split into bf16 planes [3][b6_rows][ldb] (h, m, l), or null
 };
 bool spe_gemm_ln_fusable(const GemmArgs& g);   // the large-tile kernel can fuse ln_g/ln_b for g
 int spe_launch_gemm(const GemmArgs& g, int dtype, int mode, hipStream_t s);

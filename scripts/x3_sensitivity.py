@@ -65,7 +65,7 @@ def main():
     print(f"weights ready in {time.time() - t0:.1f}s fit={fit}", flush=True)
 
     def run(dtype, exact=None):
-        if exact is None:
+        if not exact:
             os.environ.pop("SPE_X3_EXACT", None)
         else:
             os.environ["SPE_X3_EXACT"] = exact
@@ -112,8 +112,13 @@ def main():
     res = {"config": "config 2, B=%d, bench pose-consistent weights" % B, "fp32_ms": ref["ms"], "fit": fit, "rows": []}
     if a.variants == "all" or "fp32x6" in a.variants.split(";"):
         variants.insert(0, ("fp32x6", "__x6__"))
+    if a.variants == "x6":            # the fp32x6 mode with one group at a time on the exact-f32 kernels
+        variants = [("fp32x6", "__x6__")] + [(f"x6, {g} exact", "__x6__" + v) for g, v in GROUPS.items()]
     for name, exact in variants:
-        r = cmp(run("fp32x6", None) if exact == "__x6__" else run("fp32x3", exact))
+        if exact is not None and exact.startswith("__x6__"):
+            r = cmp(run("fp32x6", exact[6:] or None))
+        else:
+            r = cmp(run("fp32x3", exact))
         r["variant"], r["exact_kinds"] = name, exact
         res["rows"].append(r)
         print(json.dumps(r), flush=True)

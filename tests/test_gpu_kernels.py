@@ -788,12 +788,8 @@ def test_gemm_f16_store_saturates(gpu_device, rows):
 
 
 # ---------------------------------------------------------------- fp32x3 (split-bf16) parity mode
-@pytest.mark.parametrize("dtype,tol", [("fp32x3", 2e-5), ("fp32x6", 1e-6)])
-@pytest.mark.parametrize("case", ["linear", "linear_add_relu_res", "conv3x3", "conv1x1s2", "vt"])
-def test_gemm_x3_close_to_fp64(gpu_device, case, dtype, tol):
-    """fp32 storage, split-bf16 MFMA: fp32x3 (hi.hi + hi.lo + lo.hi) within 2e-5 relative of an
-    fp64 reference, i.e. far inside the fp32 parity tolerances and ~100x tighter than bf16;
-    fp32x6 (three-way split, six products) within 1e-6, i.e. fp32-level."""
+def _split_gemm_err(gpu_device, case, dtype):
+    """max |C - C_fp64| / max |C_fp64| of one launch of `dtype` on `case`."""
     g = torch.Generator(device="cpu").manual_seed(len(case))
     dev, f = gpu_device, torch.float32
     if case.startswith("conv"):
@@ -831,8 +827,22 @@ def test_gemm_x3_close_to_fp64(gpu_device, case, dtype, tol):
             _gemm(dtype, 0, A.to(dev, f), _padded_weight(Wt.to(dev, f), K, f), M, N, K, K, K, C, ldc,
                   bias=bias.to(dev, f), **kw)
             got = C[:, :N]
-    err = (got.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
-    assert err <= tol, err
+    return (got.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
+
+
+@pytest.mark.parametrize("dtype", ["fp32x3", "fp32x6"])
+@pytest.mark.parametrize("case", ["linear", "linear_add_relu_res", "conv3x3", "conv1x1s2", "vt"])
+def test_gemm_x3_close_to_fp64(gpu_device, case, dtype):
+    """fp32 storage, split-bf16 MFMA: fp32x3 (hi.hi + hi.lo + lo.hi) within 2e-5 relative of an
+    fp64 reference, i.e. far inside the fp32 parity tolerances and ~100x tighter than bf16;
+    fp32x6 (three-way split, six products) at the exact-f32 MFMA kernel's own error on the same
+    problem (fp32 accumulation over K = 256 .. 2304): <= max(1e-6, 2x that error)."""
+    err = _split_gemm_err(gpu_device, case, dtype)
+    if dtype == "fp32x3":
+        assert err <= 2e-5, err
+    else:
+        e32 = _split_gemm_err(gpu_device, case, "fp32")
+        assert err <= max(1e-6, 2 * e32), (err, e32)
 
 
 @pytest.mark.parametrize("B,H,Tq,Tk", [(1, 8, 300, 333), (2, 8, 2704, 2704), (3, 8, 11, 2704), (2, 8, 11, 11)])
