@@ -35,7 +35,8 @@ enum {
  * the fast parity mode on the reference goldens; F32X6_: the accuracy-contract mode (<= 1e-4 of the exact-f32
  * mode on the bench's amplifying weights too): fp32 storage, every GEMM / convolution with
  * near-fp32 precision (x = hi + mid + lo in bf16, the six products of relative order >= 2^-16), the
- * attention contractions as F32X3_ */
+ * encoder attention contractions as F32X3_, the decoder attention (whose 64x-sharpened cross-attention
+ * amplifies operand error most) in exact f32 */
 enum { SPE_DTYPE_BF16_ = 0, SPE_DTYPE_F32_ = 1, SPE_DTYPE_F16_ = 2, SPE_DTYPE_F32X3_ = 4, SPE_DTYPE_F32X6_ = 5 };
 
 /* Solver modes.
@@ -279,6 +280,12 @@ int spe_debug_gemm(void* stream, int dtype, int mode, const void* A, int lda, co
  * 3 the patch-staged 3x3 conv (pconv.hip), 4 the projection + residual + LayerNorm (lnproj.hip),
  * 5 the fp32x6 three-way split kernel (gemm.hip) */
 int spe_debug_gemm_path(void);
+/* the same launch with the weights also given pre-split (dtype SPE_DTYPE_F32X6_): planes = bf16
+ * [3][plane_rows][ldb] holding hi, mid, lo of Bw (what spe_model_finalize writes for fp32x6 models) */
+int spe_debug_gemm_planes(void* stream, int dtype, int mode, const void* A, int lda, const void* P, int ldp, int prow,
+                          int H, int W, int Cin, int KH, int KW, int stride, int pad, const void* Bw, int ldb, int M,
+                          int N, int K, const float* bias, const void* R, int ldr, int act_code, void* C, int ldc,
+                          const void* planes, int plane_rows);
 int spe_debug_attention(void* stream, int dtype, const void* q, int ldq, const void* k, int ldk, const void* vt,
                         void* o, int ldo, int B, int H, int Tq, int Tk, float scale);
 int spe_debug_layernorm(void* stream, int dtype, const void* x, const float* gamma, const float* beta, void* out,

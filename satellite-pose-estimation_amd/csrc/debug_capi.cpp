@@ -7,6 +7,11 @@
 #include "../../include/spe.h"
 #include "model_state.h"
 
+namespace {
+thread_local const void* g_planes = nullptr;   // spe_debug_gemm_planes -> spe_debug_gemm
+thread_local int g_plane_rows = 0;
+}  // namespace
+
 extern "C" {
 
 int spe_debug_gemm(void* stream, int dtype, int mode, const void* A, int lda, const void* P, int ldp, int prow,
@@ -25,8 +30,23 @@ int spe_debug_gemm(void* stream, int dtype, int mode, const void* A, int lda, co
   g.r_period = r_period;
   g.ln_g = ln_g; g.ln_b = ln_b;
   g.out_f16 = out_f16;
+  g.B6 = g_planes;
+  g.b6_rows = g_plane_rows;
   int rc = spe_launch_gemm(g, dtype, mode, (hipStream_t)stream);
   return rc < 0 ? spe_fail(SPE_E_LAUNCH, "gemm launch rejected its arguments") : rc;
+}
+
+int spe_debug_gemm_planes(void* stream, int dtype, int mode, const void* A, int lda, const void* P, int ldp, int prow,
+                          int H, int W, int Cin, int KH, int KW, int stride, int pad, const void* Bw, int ldb, int M,
+                          int N, int K, const float* bias, const void* R, int ldr, int act_code, void* C, int ldc,
+                          const void* planes, int plane_rows) {
+  g_planes = planes;
+  g_plane_rows = plane_rows;
+  const int rc = spe_debug_gemm(stream, dtype, mode, A, lda, P, ldp, prow, H, W, Cin, KH, KW, stride, pad, Bw, ldb, M, N,
+                                K, bias, R, ldr, act_code, C, ldc, 0, 0, 0, 0, nullptr, nullptr, 0);
+  g_planes = nullptr;
+  g_plane_rows = 0;
+  return rc;
 }
 
 int spe_debug_gemm_path(void) { return spe_gemm_last_path; }

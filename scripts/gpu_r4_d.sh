@@ -1,0 +1,12 @@
+#!/bin/bash
+# x6 iteration: kernel + parity tests, GEMM microbenchmark (default tile), precision gate, bench line
+set -o pipefail
+mkdir -p gpurun_out
+T="timeout -k 10"
+$T 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_kernels.py tests/test_gpu_parity.py \
+   tests/test_gpu_precision.py -k "x3_close or forward_fp32 or precision" > gpurun_out/d_tests.log 2>&1; rc=$?; tail -2 gpurun_out/d_tests.log; cat gpurun_out/precision_floor.json | grep x6; [ $rc = 0 ] || exit $rc
+$T 300 python -u scripts/x6_bench.py > gpurun_out/d_x6bench.log 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/d_x6bench.log; [ $rc = 0 ] || exit $rc
+$T 600 python -u bench.py --steps 20 --warmup 5 > gpurun_out/d_bench.json 2> gpurun_out/d_bench.err; rc=$?; python -c "
+import json; d=json.loads(open('gpurun_out/d_bench.json').read().strip().splitlines()[-1]); p=d['parity_mode']
+print('bf16', round(d['value']), 'parity', round(p['value']), p['ms_per_step'], {k: p['accuracy_vs_fp32'][k] for k in ('kpt_norm_max','frac_kpt_norm_le_1e-4','frac_score_delta_le_1e-4','meets_1e-4_kpt')})
+print({k: round(v,2) for k,v in p['kernel_time_ms_per_step'].items()})"; exit $rc

@@ -15,7 +15,8 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(REPO, "satellite-pose-estimation_amd"))
 from spe import _lib  # noqa: E402
 
-DT = {"fp32": _lib.SPE_DTYPE_F32, "fp32x3": _lib.SPE_DTYPE_F32X3, "fp32x6": _lib.SPE_DTYPE_F32X6}
+DT = {"fp32": _lib.SPE_DTYPE_F32, "fp32x3": _lib.SPE_DTYPE_F32X3, "fp32x6": _lib.SPE_DTYPE_F32X6,
+      "fp32x6bp": _lib.SPE_DTYPE_F32X6}       # bp: weights pre-split into bf16 planes, as the model has them
 # name: (M, N, K) linear, or (B, H, Cin, Cout, k, stride, pad) conv
 SHAPES = {
     "enc.ffn1": (64 * 2704, 2048, 256), "enc.ffn2": (64 * 2704, 256, 2048), "enc.qk": (64 * 2704, 512, 256),
@@ -52,10 +53,18 @@ def main():
         W = torch.randn(N, ldb, device=dev) / K ** 0.5
         bias = torch.randn(N, device=dev)
         C = torch.empty(M, N, device=dev)
+        h = W.to(torch.bfloat16)
+        r = W - h.float()
+        m_ = r.to(torch.bfloat16)
+        planes = torch.stack([h, m_, (r - m_.float()).to(torch.bfloat16)]).contiguous()
         row = [name]
         for dn, dt in DT.items():
-            fn = lambda: L.spe_debug_gemm(None, dt, mode, p(A), K if mode == 0 else 0, None, 0, 1, *conv, p(W), ldb, M, N,
-                                          K, p(bias), None, 0, 1, p(C), N, 0, 0, 0, 0, None, None, 0)
+            if dn == "fp32x6bp":
+                fn = lambda: L.spe_debug_gemm_planes(None, dt, mode, p(A), K if mode == 0 else 0, None, 0, 1, *conv, p(W),
+                                                     ldb, M, N, K, p(bias), None, 0, 1, p(C), N, p(planes), N)
+            else:
+                fn = lambda: L.spe_debug_gemm(None, dt, mode, p(A), K if mode == 0 else 0, None, 0, 1, *conv, p(W), ldb,
+                                              M, N, K, p(bias), None, 0, 1, p(C), N, 0, 0, 0, 0, None, None, 0)
             assert fn() == 0, L.spe_last_error()
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
