@@ -76,7 +76,7 @@ def parse():
     p.add_argument("--size", type=int, default=None)
     p.add_argument("--queries", type=int, default=None)
     p.add_argument("--layers", type=int, default=None)
-    p.add_argument("--solver", default=None, choices=["epnp", "epnp_lm", "ransac_p3p_lm", "epnp_ransac_sigma"])
+    p.add_argument("--solver", default=None, choices=["epnp", "epnp_lm", "ransac_p3p_lm", "epnp_ransac_sigma", "epnp_ceres"])
     p.add_argument("--sigma-head", type=int, default=None, choices=[0, 1])
     p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp32x3", "fp32x6"],
                    help="bf16: throughput mode; fp32: exact-f32 MFMA parity mode; fp32x3: fp32 storage with "

@@ -570,12 +570,12 @@ __global__ __launch_bounds__(NT, 2) void attn_f32_kernel(AttnArgs a) {
       for (int r = 0; r < 16; ++r) { s0[r] *= sl2; s1[r] *= sl2; }
       const float mx = tile_max(s0, s1, kt * KT, a.Tk, hh);
       const float mn = __builtin_fmaxf(m, mx);
-      const float alpha = exp2f(m - mn);
+      const float alpha = __builtin_amdgcn_exp2f(m - mn);   // (bare v_exp_f32: exp2f's denormal scaling buys nothing here)
       float sum = 0.f;
 #pragma unroll
       for (int r = 0; r < 16; ++r) {
-        s0[r] = exp2f(s0[r] - mn);
-        s1[r] = exp2f(s1[r] - mn);
+        s0[r] = __builtin_amdgcn_exp2f(s0[r] - mn);
+        s1[r] = __builtin_amdgcn_exp2f(s1[r] - mn);
         sum += s0[r] + s1[r];
       }
       l = l * alpha + sum;
@@ -654,10 +654,12 @@ __global__ __launch_bounds__(NT, 2) void attn_x3_kernel(AttnArgs a) {
       ql[i] = u32x4{lw[0], lw[1], lw[2], lw[3]};
     }
   }
-  f32x16 o;
+  // negm: -m in every element, the accumulator the score MFMAs start from (scores come out
+  // shifted by the running max), as in the bf16 kernel; m is set by the first tile
+  f32x16 o, negm;
 #pragma unroll
-  for (int r = 0; r < 16; ++r) o[r] = 0.f;
-  float m = NEG_BIG, l = 0.f;
+  for (int r = 0; r < 16; ++r) { o[r] = 0.f; negm[r] = 0.f; }
+  float m = 0.f, l = 0.f;
 
   // staging: fp32 tiles through registers (Stage<float>), split into the hi / lo images
   Stage<float, KT> st;
@@ -695,35 +697,52 @@ __global__ __launch_bounds__(NT, 2) void attn_x3_kernel(AttnArgs a) {
     const bool more = kt + 1 < ntiles;
     if (more) st.load(a, b, h, kt + 1, tid);
     if (wave_live) {
+      // (fragments read at their use: reading all 16 up front measured 1.85 vs 1.76 ms per
+      // B = 64 launch -- 172 instead of 164 VGPRs, a wave per SIMD less)
       f32x16 s0, s1;
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub) {
         f32x16& s = sub ? s1 : s0;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) s[r] = 0.f;
-        const int key = sub * 32 + r32;
+        s = negm;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
-          const u32x4 kh = ld16(kl + k_off_bf16(key, 2 * i + hh)), klo = ld16(kl + KB + k_off_bf16(key, 2 * i + hh));
+          const int ko = k_off_bf16(sub * 32 + r32, 2 * i + hh);
+          const u32x4 kh = ld16(kl + ko), klo = ld16(kl + KB + ko);
           s = mf(klo, qh[i], s);
           s = mf(kh, ql[i], s);
           s = mf(kh, qh[i], s);
         }
       }
+      // lazy rescale (the bf16 kernel's rule): the running max moves only when some lane's tile
+      // max passed it by more than RESCALE_SLACK, so p <= 2^8 -- exact-range fp32 for p, l, o and
+      // the hi / lo split; the first tile sets m.  p = exp2 by the bare v_exp_f32 (exp2f's
+      // denormal-range scaling costs 4 VALU per score; p < 2^-126 is below any sum's ulp).
       const float mx = tile_max(s0, s1, kt * KT, a.Tk, hh);
-      const float mn = __builtin_fmaxf(m, mx);
-      const float alpha = exp2f(m - mn);
-      float sum = 0.f;
+      if (kt == 0 || __any(mx > RESCALE_SLACK)) {
+        const float d = kt == 0 ? mx : __builtin_fmaxf(mx, 0.f);
+        if (kt != 0) {
+          const float alpha = __builtin_amdgcn_exp2f(-d);
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        s0[r] = exp2f(s0[r] - mn);
-        s1[r] = exp2f(s1[r] - mn);
-        sum += s0[r] + s1[r];
+          for (int r = 0; r < 16; ++r) o[r] *= alpha;
+          l *= alpha;
+        }
+        m += d;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { s0[r] -= d; s1[r] -= d; negm[r] = -m; }
       }
-      l = l * alpha + sum;
-      m = mn;
+      float t0 = 0.f, t1 = 0.f, t2 = 0.f, t3 = 0.f;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) o[r] *= alpha;
+      for (int r = 0; r < 16; r += 2) {
+        s0[r] = __builtin_amdgcn_exp2f(s0[r]);
+        s0[r + 1] = __builtin_amdgcn_exp2f(s0[r + 1]);
+        s1[r] = __builtin_amdgcn_exp2f(s1[r]);
+        s1[r + 1] = __builtin_amdgcn_exp2f(s1[r + 1]);
+        t0 += s0[r];
+        t1 += s0[r + 1];
+        t2 += s1[r];
+        t3 += s1[r + 1];
+      }
+      l += (t0 + t1) + (t2 + t3);
 #pragma unroll
       for (int sub = 0; sub < 2; ++sub) {
         const f32x16& p = sub ? s1 : s0;
@@ -736,9 +755,9 @@ __global__ __launch_bounds__(NT, 2) void attn_x3_kernel(AttnArgs a) {
             hw[e] = pack_bf16x2(v0, v1);
             lw[e] = pack_bf16x2(v0 - __uint_as_float(hw[e] << 16), v1 - __uint_as_float(hw[e] & 0xffff0000u));
           }
+          const u32x4 ph{hw[0], hw[1], hw[2], hw[3]}, pl{lw[0], lw[1], lw[2], lw[3]};
           const int vo = r32 * VROW + (2 * sub + ks) * 32 + hh * 16;
           const u32x4 vh = ld16(vl + vo), vlo = ld16(vl + VB + vo);
-          const u32x4 ph{hw[0], hw[1], hw[2], hw[3]}, pl{lw[0], lw[1], lw[2], lw[3]};
           o = mf(vlo, ph, o);
           o = mf(vh, pl, o);
           o = mf(vh, ph, o);

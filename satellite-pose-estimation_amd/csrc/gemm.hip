@@ -609,6 +609,195 @@ int launch_x6(const GemmArgs& g, int mode, hipStream_t s) {
   return tile == 128 ? launch_x6_geo<128>(g, mode, s) : launch_x6_geo<256>(g, mode, s);
 }
 
+// ---------------------------------------------------------------- fp32x6, LDS-DMA staged
+// The same six-product split as gemm_x6_kernel, restaged: both operands go global -> LDS by
+// buffer_load ... lds (no staging registers, no ds_write, no per-step wait on loads issued in
+// that step) -- A as raw fp32, split into its h / m / l planes by the waves that read the
+// fragments; B from the pre-split weight planes (GemmArgs::B6).  One barrier per K-step (32
+// elements); the DMA of step ks+1 is issued right behind step ks's barrier into the other stage
+// and has all of step ks's MFMAs to land.  v_mfma_f32_32x32x16_bf16 fragments (2 x 2 per wave of
+// 64 x 64): per step and wave 48 MFMAs, 8 A reads (2 x 16 B per 8-element fragment row) + 12 B
+// plane reads, 32 fp32 split.
+//   LDS stage (40 KiB): A [128 rows][128 B] fp32, chunk c of row r at slot c ^ ((r >> 1) & 7);
+//   B planes [3][128 rows][64 B] bf16, chunk c at slot c ^ ((r >> 2) & 3) -- both keyed for
+//   gfx950's ds_read_b128 lane groups under the 32x32 fragment's lane -> row map (lane & 31),
+//   applied on the DMA source address.  Two stages (80 KiB) = two workgroups per CU.
+// Used for GEMM_LINEAR and GEMM_CONV with K % 32 == 0 (Cin % 32 == 0), pre-split weights and
+// 32-bit buffer offsets; everything else takes gemm_x6_kernel.
+constexpr int D6_BM = 128, D6_BN = 128, D6_NT = 256;
+constexpr int D6_A = D6_BM * 128, D6_PB = D6_BN * 64, D6_STAGE = D6_A + 3 * D6_PB;
+constexpr int D6_SMEM = 2 * D6_STAGE;
+static_assert(D6_SMEM >= D6_BM * EPI_LD * 4, "epilogue tile fits the stages");
+constexpr int D6_BAD = 0x7ffffff0;          // out-of-range buffer offset -> zeros
+typedef __attribute__((address_space(3))) void* lds_ptr6_t;
+constexpr int d6_waitcnt_vm0() { return (7 << 4) | (15 << 8); }   // vmcnt(0), expcnt/lgkmcnt untouched
+
+SPE_DEV u32x4 cat2(u32x2 a, u32x2 b) { return u32x4{a.x, a.y, b.x, b.y}; }
+
+template <int MODE>
+__global__ __launch_bounds__(D6_NT, 2) void gemm_x6d_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(1024))) char smem[D6_SMEM];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wr = wid >> 1, wc = wid & 1;
+  const int tilesN = (g.N + D6_BN - 1) / D6_BN;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (t / tilesN) * D6_BM, n0 = (t % tilesN) * D6_BN;
+  const int nk = g.K >> 5;
+  const long long abytes = MODE == GEMM_CONV ? (long long)(g.M / (g.Ho * g.Wo)) * g.H * g.W * g.Cin * 4
+                                             : (long long)g.M * g.lda * 4;
+  const size_t pstride = (size_t)g.b6_rows * g.ldb;
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, (int)abytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)g.B6, (short)0, (int)(3 * pstride * 2), 0x00020000);
+
+  // ---- DMA pieces of this wave: A pieces wid + 4q (rows 8p .. 8p+7, lane -> row 8p + lane/8,
+  // slot lane & 7), B pieces wid + 4q (plane p / 8, rows 16 (p % 8) + lane/4, slot lane & 3)
+  int avo[4], ih0[4], iw0[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int row = (wid + 4 * q) * 8 + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7), m = m0 + row;
+    if constexpr (MODE == GEMM_CONV) {
+      const int hw = g.Ho * g.Wo, mm = m < g.M ? m : 0;
+      const int b = mm / hw, r = mm - b * hw, oh = r / g.Wo, ow = r - oh * g.Wo;
+      ih0[q] = m < g.M ? oh * g.stride - g.pad : -(1 << 28);
+      iw0[q] = ow * g.stride - g.pad;
+      avo[q] = b * g.H * g.W * g.Cin + c * 4;            // elements: image base + the lane's chunk
+    } else {
+      avo[q] = m < g.M ? m * g.lda * 4 + c * 16 : D6_BAD;
+      ih0[q] = iw0[q] = 0;
+    }
+  }
+  int bvo[6];
+#pragma unroll
+  for (int q = 0; q < 6; ++q) {
+    const int p = wid + 4 * q, plane = p >> 3, row = (p & 7) * 16 + (lane >> 2);
+    const int c = (lane & 3) ^ ((row >> 2) & 3), n = n0 + row;
+    bvo[q] = n < g.N ? (int)((plane * pstride + (size_t)n * g.ldb) * 2) + c * 16 : D6_BAD;
+  }
+  auto issue = [&](int ks, int stg) {
+    char* base = smem + stg * D6_STAGE;
+    int kh = 0, kw = 0, ci = 0;
+    if constexpr (MODE == GEMM_CONV) conv_k_decode(ks * 32, g.Cin, g.KW, g.KH * g.KW, kh, kw, ci);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      int off;
+      if constexpr (MODE == GEMM_CONV) {
+        const int ih = ih0[q] + kh, iw = iw0[q] + kw;
+        const bool v = ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+        off = v ? (avo[q] + (ih * g.W + iw) * g.Cin + ci) * 4 : D6_BAD;
+      } else {
+        off = avo[q];
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lds_ptr6_t)(base + (wid + 4 * q) * 1024), 16, off,
+                                               MODE == GEMM_CONV ? 0 : ks * 128, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lds_ptr6_t)(base + D6_A + (wid + 4 * q) * 1024), 16, bvo[q],
+                                               ks * 64, 0, 0);
+  };
+
+  // ---- fragment offsets: A row wr*64 + 32i + (lane & 31), 16-byte chunks 4kk + 2(lane >> 5) + h;
+  // B row wc*64 + 32j + (lane & 31), chunk 2kk + (lane >> 5)
+  const int l31 = lane & 31, hi = lane >> 5;
+  int aoff[2][2], boff[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      aoff[kk][h] = (wr * 64 + l31) * 128 + (((4 * kk + 2 * hi + h) ^ ((l31 >> 1) & 7)) << 4);
+    boff[kk] = D6_A + (wc * 64 + l31) * 64 + (((2 * kk + hi) ^ ((l31 >> 2) & 3)) << 4);
+  }
+  auto mf = [](u32x4 x, u32x4 y, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, x), __builtin_bit_cast(bf16x8, y), c, 0, 0, 0);
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  issue(0, 0);
+  for (int ks = 0; ks < nk; ++ks) {
+    __builtin_amdgcn_s_waitcnt(d6_waitcnt_vm0());          // this wave's pieces of step ks landed
+    __syncthreads();                                         // everyone's; step ks-1's stage is free
+    if (ks + 1 < nk) issue(ks + 1, (ks + 1) & 1);
+    const char* st = smem + (ks & 1) * D6_STAGE;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      u32x4 b[3][2], ah[2], am[2], al[2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int p = 0; p < 3; ++p) b[p][j] = ld16(st + boff[kk] + p * D6_PB + j * 2048);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const u32x4 x0 = ld16(st + aoff[kk][0] + i * 4096), x1 = ld16(st + aoff[kk][1] + i * 4096);
+        u32x2 h0, m0_, l0, h1, m1, l1;
+        split3(x0, h0, m0_, l0);
+        split3(x1, h1, m1, l1);
+        ah[i] = cat2(h0, h1);
+        am[i] = cat2(m0_, m1);
+        al[i] = cat2(l0, l1);
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          f32x16 c = acc[i][j];
+          c = mf(al[i], b[0][j], c);
+          c = mf(ah[i], b[2][j], c);
+          c = mf(am[i], b[1][j], c);
+          c = mf(am[i], b[0][j], c);
+          c = mf(ah[i], b[1][j], c);
+          acc[i][j] = mf(ah[i], b[0][j], c);
+        }
+    }
+  }
+  __syncthreads();                                           // stages -> epilogue tile
+
+  float bv[8];
+  {
+    const int n = n0 + (tid & 15) * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bv[e] = (g.bias && n + e < g.N) ? g.bias[n + e] : 0.f;
+  }
+  float* ct = reinterpret_cast<float*>(smem);
+  // 32x32 accumulator: lane holds rows 8 (r >> 2) + 4 (lane >> 5) + (r & 3), column lane & 31
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r)
+        ct[(wr * 64 + 32 * i + 8 * (r >> 2) + 4 * hi + (r & 3)) * EPI_LD + wc * 64 + 32 * j + l31] = acc[i][j][r];
+  __syncthreads();
+  store_tile<float, D6_BM, D6_NT>(g, ct, m0, n0, tid, bv);
+}
+
+// 1 = not a problem for the DMA kernel
+int launch_x6d(const GemmArgs& g, int mode, hipStream_t s) {
+  static const int en = [] { const char* e = getenv("SPE_X6_DMA"); return e ? atoi(e) : 1; }();
+  if (!en || !g.B6 || (mode != GEMM_LINEAR && mode != GEMM_CONV) || (g.K & 31) || (g.lda & 3)) return 1;
+  if ((reinterpret_cast<uintptr_t>(g.A) & 15) || (reinterpret_cast<uintptr_t>(g.B6) & 15) || (g.ldb & 7)) return 1;
+  constexpr long long LIM = (1LL << 31) - (1LL << 24);
+  if ((long long)3 * g.b6_rows * g.ldb * 2 >= LIM || g.b6_rows < g.N) return 1;
+  if (mode == GEMM_CONV) {
+    if (g.Cin & 31) return 1;
+    if ((long long)(g.M / (g.Ho * g.Wo)) * g.H * g.W * g.Cin * 4 >= LIM) return 1;
+  } else if ((long long)(g.M + D6_BM) * g.lda * 4 + (long long)g.K * 4 >= LIM) {
+    return 1;
+  }
+  const int tiles = ((g.M + D6_BM - 1) / D6_BM) * ((g.N + D6_BN - 1) / D6_BN);
+  if (tiles <= 0) return 0;
+  if (mode == GEMM_CONV) hipLaunchKernelGGL(gemm_x6d_kernel<GEMM_CONV>, dim3(tiles), dim3(D6_NT), 0, s, g);
+  else hipLaunchKernelGGL(gemm_x6d_kernel<GEMM_LINEAR>, dim3(tiles), dim3(D6_NT), 0, s, g);
+  return (int)hipGetLastError();
+}
+
 template <typename T, bool X3 = false>
 int launch_t(const GemmArgs& g, int mode, hipStream_t s) {
   const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
@@ -649,6 +838,9 @@ int spe_launch_gemm(const GemmArgs& g, int dtype, int mode, hipStream_t s) {
     // few-row problems (the decoder's B*Q rows) would leave most CUs idle on 256 x 128 tiles:
     // they take the 128 x 128 geometry (at 2.7x the exact-f32 kernel's matrix rate per tile)
     const int tiles6 = ((g.M + BM6 - 1) / BM6) * ((g.N + BN6 - 1) / BN6);
+    spe_gemm_last_path = 6;
+    const int rc = launch_x6d(g, mode, s);
+    if (rc != 1) return rc;
     spe_gemm_last_path = 5;
     return tiles6 >= 128 ? launch_x6(g, mode, s) : launch_x6_geo<128>(g, mode, s);
   }

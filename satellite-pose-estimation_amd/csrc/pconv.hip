@@ -211,7 +211,13 @@ __global__ __launch_bounds__(PNT, NPB == 1 ? 2 : 1) void pconv_kernel(GemmArgs g
     sync();
     if (s + 2 < steps) issue_w(s + 2, s & 1);
     if constexpr (NPB == 2) {
-      if (cb + 1 < cbs && tap < PPW) issue_patch(cb + 1, (cb + 1) & 1, tap);   // a piece per tap
+      // the next channel block's whole patch at its first tap (compile-time piece indices: a
+      // piece per tap, poff[tap], made the compiler version the loop on "this tap issues a
+      // piece" with ~130 v_mov of the fragment registers on 5 of 9 taps -- 1.8 VALU per MFMA)
+      if (tap == 0 && cb + 1 < cbs) {
+#pragma unroll
+        for (int j = 0; j < PPW; ++j) issue_patch(cb + 1, (cb + 1) & 1, j);
+      }
     } else {
       if (cbn != cb) {                                    // one buffer: refill it once every wave is done
 #pragma unroll

@@ -13,5 +13,5 @@ fi
 for v in old main old main; do
   if [ "$v" = main ]; then unset SPE_LIB_PATH; else export SPE_LIB_PATH=ablate/$v/libspe.so; fi
   timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-accuracy $BENCH_ARGS > gpurun_out/ab_b_$v.log 2>&1 || { tail -20 gpurun_out/ab_b_$v.log; exit 3; }
-  echo "$v $(tail -1 gpurun_out/ab_b_$v.log | grep -o '"value": [0-9.]*') $(tail -1 gpurun_out/ab_b_$v.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); k=d['kernel_time_ms_per_step']; print({x: round(k[x],3) for x in ('attn.enc','ffn.enc','conv.1x1','gemm.enc.qk','gemm.enc.o','gemm.enc.v','conv.neck') if x in k})")"
+  echo "$v $(tail -1 gpurun_out/ab_b_$v.log | grep -o '"value": [0-9.]*') $(tail -1 gpurun_out/ab_b_$v.log | python -c "import json,sys; d=json.loads(sys.stdin.read()); k=d['kernel_time_ms_per_step']; print({x: round(k[x],3) for x in ('attn.enc','ffn.enc','conv.1x1','conv.3x3','gemm.enc.qk','gemm.enc.o','gemm.enc.v','conv.neck') if x in k})")"
 done

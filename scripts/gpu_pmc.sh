@@ -12,7 +12,7 @@ IFS=';' read -ra ARR <<< "$SETS"
 for C in "${ARR[@]}"; do
   i=$((i+1))
   timeout -k 10 600 rocprofv3 --kernel-trace --pmc $C --output-format csv -d gpurun_out/pmc_$TAG/set$i -o bench -- \
-    python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-accuracy --weights label-diverse > gpurun_out/pmc_$TAG/set$i.log 2>&1 \
+    python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-accuracy --no-parity --weights label-diverse > gpurun_out/pmc_$TAG/set$i.log 2>&1 \
     || { echo "pmc set $i ($C) failed"; tail -20 gpurun_out/pmc_$TAG/set$i.log; exit 6; }
   echo "$C" > gpurun_out/pmc_$TAG/set$i/counters.txt
   find gpurun_out/pmc_$TAG/set$i -name "*kernel_trace*" -delete

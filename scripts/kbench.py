@@ -38,7 +38,7 @@ def main():
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--batch", type=int, default=64)
     ap.add_argument("--only", default="")
-    ap.add_argument("--attn-dtype", type=int, default=0, help="0 bf16, 2 fp16, 3 bf16 q/k + fp16 V^T/P")
+    ap.add_argument("--attn-dtype", type=int, default=0, help="0 bf16, 1 fp32, 2 fp16, 3 bf16 q/k + fp16 V^T/P, 4 fp32x3")
     ap.add_argument("--dma", action="store_true", help="the encoder's LDS-DMA attention kernel (V^T key order as stored)")
     a = ap.parse_args()
     L = _lib.lib()
@@ -46,13 +46,14 @@ def main():
     B, H, T, D, F = a.batch, 8, 2704, 256, 2048
     g = torch.Generator(device="cpu").manual_seed(0)
     if a.which in ("attn", "all"):
-        qk = torch.randn(B * T, 512, generator=g).to(dev, torch.bfloat16)
-        vdt = torch.float16 if a.attn_dtype in (2, 3) else torch.bfloat16
+        f32 = a.attn_dtype in (1, 4)               # exact fp32 / fp32x3 parity kernels: fp32 operands
+        qk = torch.randn(B * T, 512, generator=g).to(dev, torch.float32 if f32 else torch.bfloat16)
+        vdt = torch.float16 if a.attn_dtype in (2, 3) else torch.float32 if f32 else torch.bfloat16
         if a.attn_dtype == 2:
             qk = qk.to(torch.float16)
         vt = torch.randn(B, H, 32, T, generator=g).to(dev, vdt)
-        o = torch.empty(B * T, D, dtype=torch.bfloat16, device=dev)
-        kp = ctypes.c_void_p(qk.data_ptr() + 256 * 2)
+        o = torch.empty(B * T, D, dtype=torch.float32 if f32 else torch.bfloat16, device=dev)
+        kp = ctypes.c_void_p(qk.data_ptr() + 256 * qk.element_size())
         code = a.attn_dtype | (0x100 if a.dma else 0)
         fn = lambda: L.spe_debug_attention(None, code, p(qk), 512, kp, 512, p(vt), p(o), D, B, H, T, T, 32 ** -0.5)
         ms = timeit(fn, a.iters)

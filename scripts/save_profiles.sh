@@ -5,6 +5,7 @@ set -e
 T=$1
 cd "$(dirname "$0")/.."
 cp gpurun_out/prof_$T/bench_kernel_stats.csv profiles/${T}_kernel_stats.csv
+cp gpurun_out/prof_$T/bench_kernel_stats_model.csv profiles/${T}_kernel_stats_model.csv
 grep '^{"metric"' gpurun_out/prof_$T/bench_under_rocprof.log > profiles/${T}_bench_under_rocprof.json
 tail -1 gpurun_out/${T}_bench.log > profiles/${T}_bench.json
 cp gpurun_out/${T}_launch_table.json profiles/

@@ -788,8 +788,29 @@ def test_gemm_f16_store_saturates(gpu_device, rows):
 
 
 # ---------------------------------------------------------------- fp32x3 (split-bf16) parity mode
-def _split_gemm_err(gpu_device, case, dtype):
-    """max |C - C_fp64| / max |C_fp64| of one launch of `dtype` on `case`."""
+def _weight_planes(Wp):
+    """fp32 [N][ldb] -> bf16 [3][N][ldb] h, m, l (RNE each; what spe_model_finalize writes)."""
+    h = Wp.to(torch.bfloat16)
+    r = Wp - h.float()
+    m = r.to(torch.bfloat16)
+    return torch.stack([h, m, (r - m.float()).to(torch.bfloat16)]).contiguous()
+
+
+def _gemm_planes(mode, A, Wp, M, N, K, lda, C, ldc, bias=None, R=None, ldr=0, relu=0, conv=(0, 0, 0, 1, 1, 1, 0)):
+    L = _lib.lib()
+    H, Wd, Cin, KH, KW, stride, pad = conv
+    planes = _weight_planes(Wp)
+    rc = L.spe_debug_gemm_planes(None, _lib.SPE_DTYPE_F32X6, mode, _p(A), lda, None, 0, 1, H, Wd, Cin, KH, KW, stride,
+                                 pad, _p(Wp), Wp.shape[1], M, N, K, _p(bias), _p(R), ldr, relu, _p(C), ldc, _p(planes),
+                                 Wp.shape[0])
+    assert rc == 0, L.spe_last_error()
+    torch.cuda.synchronize()
+    return L.spe_debug_gemm_path()
+
+
+def _split_gemm_err(gpu_device, case, dtype, planes=False, want_path=None):
+    """max |C - C_fp64| / max |C_fp64| of one launch of `dtype` on `case` (planes: fp32x6 with the
+    weights pre-split, as the models launch it; want_path: the kernel that must have run)."""
     g = torch.Generator(device="cpu").manual_seed(len(case))
     dev, f = gpu_device, torch.float32
     if case.startswith("conv"):
@@ -802,7 +823,11 @@ def _split_gemm_err(gpu_device, case, dtype):
         Ho = (H + 2 * pd - k) // st + 1
         M, K = B * Ho * Ho, Cin * k * k
         C = torch.zeros(M, Cout, dtype=f, device=dev)
-        _gemm(dtype, 2, A, Wp, M, Cout, K, 0, K, C, Cout, conv=(H, H, Cin, k, k, st, pd))
+        if planes:
+            path = _gemm_planes(2, A, Wp, M, Cout, K, 0, C, Cout, conv=(H, H, Cin, k, k, st, pd))
+            assert want_path is None or path == want_path, path
+        else:
+            _gemm(dtype, 2, A, Wp, M, Cout, K, 0, K, C, Cout, conv=(H, H, Cin, k, k, st, pd))
         got = C
     else:
         M, N, K = (3000, 200, 512) if case != "vt" else (2 * 2704, 256, 256)
@@ -823,6 +848,11 @@ def _split_gemm_err(gpu_device, case, dtype):
             _gemm(dtype, 0, A.to(dev, f), _padded_weight(Wt.to(dev, f), K, f), M, N, K, K, K, C, 4,
                   bias=bias.to(dev, f), vt=(T, Bv))
             got = C.view(N // 256, Bv, 256, T).permute(1, 3, 0, 2).reshape(M, N)
+        elif planes:
+            path = _gemm_planes(0, A.to(dev, f), _padded_weight(Wt.to(dev, f), K, f), M, N, K, K, C, ldc,
+                                bias=bias.to(dev, f), **kw)
+            assert want_path is None or path == want_path, path
+            got = C[:, :N]
         else:
             _gemm(dtype, 0, A.to(dev, f), _padded_weight(Wt.to(dev, f), K, f), M, N, K, K, K, C, ldc,
                   bias=bias.to(dev, f), **kw)
@@ -843,6 +873,16 @@ def test_gemm_x3_close_to_fp64(gpu_device, case, dtype):
     else:
         e32 = _split_gemm_err(gpu_device, case, "fp32")
         assert err <= max(1e-6, 2 * e32), (err, e32)
+
+
+@pytest.mark.parametrize("case", ["linear", "linear_add_relu_res", "conv3x3", "conv1x1s2"])
+def test_gemm_x6_dma_close_to_fp64(gpu_device, case):
+    """fp32x6 with the weights pre-split (the models' launch): the LDS-DMA kernel (gemm path 6)
+    runs -- ragged M and N tiles, residual + ReLU epilogue, padded 3x3 and strided 1x1 implicit
+    GEMMs -- at the exact-f32 kernel's own error, like the register-staged x6 kernel."""
+    err = _split_gemm_err(gpu_device, case, "fp32x6", planes=True, want_path=6)
+    e32 = _split_gemm_err(gpu_device, case, "fp32")
+    assert err <= max(1e-6, 2 * e32), (err, e32)
 
 
 @pytest.mark.parametrize("B,H,Tq,Tk", [(1, 8, 300, 333), (2, 8, 2704, 2704), (3, 8, 11, 2704), (2, 8, 11, 11)])
@@ -867,3 +907,35 @@ def test_attention_x3_close_to_fp64(gpu_device, B, H, Tq, Tk):
     ref = ref.transpose(1, 2).reshape(B * Tq, H * 32)
     err = (O.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
     assert err <= 5e-5, err
+
+
+@pytest.mark.parametrize("dtype,gain", [("fp32x3", 3.0), ("fp32x3", 12.0), ("fp32x3", 40.0), ("fp32", 12.0),
+                                        ("fp32", 40.0)])
+def test_attention_fp32_modes_large_score_range(gpu_device, dtype, gain):
+    """fp32 / fp32x3 attention when late keys dominate (scores spanning > 100 in log2 space): the
+    x3 kernel keeps a stale running max until a tile passes it by more than the rescale slack,
+    so late jumps must go through its rescale path; both against an fp64 softmax."""
+    B, H, T = 2, 8, 333
+    g = torch.Generator(device="cpu").manual_seed(int(gain))
+    Q = torch.randn(B * T, 256, generator=g, dtype=torch.float64)
+    K = torch.randn(B * T, 256, generator=g, dtype=torch.float64)
+    K[T - 90:T] *= gain                              # late keys of image 0 dominate
+    K[2 * T - 20:] *= gain / 2                       # image 1: a milder jump in its last tile
+    V = torch.randn(B, H, T, 32, generator=g, dtype=torch.float64)
+    dev = gpu_device
+    Qd, Kd = Q.to(dev, torch.float32), K.to(dev, torch.float32)
+    VTd = V.transpose(-1, -2).contiguous().to(dev, torch.float32)
+    O = torch.zeros(B * T, 256, dtype=torch.float32, device=dev)
+    scale = 32 ** -0.5
+    rc = _lib.lib().spe_debug_attention(None, DT[dtype][0], _p(Qd), 256, _p(Kd), 256, _p(VTd), _p(O), 256, B, H, T,
+                                        T, scale)
+    assert rc == 0
+    torch.cuda.synchronize()
+    q = Qd.double().cpu().view(B, T, H, 32).transpose(1, 2)
+    k = Kd.double().cpu().view(B, T, H, 32).transpose(1, 2)
+    ref = torch.softmax(q @ k.transpose(-1, -2) * scale, -1) @ V
+    ref = ref.transpose(1, 2).reshape(B * T, 256)
+    err = (O.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
+    # x3: each score carries ~2^-17 of sum |q_i k_i| (the split's product error), so the bound
+    # grows with the score magnitude (gain 40: scores of ~200 log2 units, error ~1e-3 of a p)
+    assert err <= (5e-5 * max(1.0, gain / 8) if dtype == "fp32x3" else 1e-5), err
