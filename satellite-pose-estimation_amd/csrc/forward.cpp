@@ -119,10 +119,10 @@ bool use_fused_ffn(const spe_model* m) {
   return m->cfg.dtype == SPE_DTYPE_BF16 && m->cfg.hidden_dim == 256 && m->cfg.dim_feedforward % 32 == 0;
 }
 
-// `(x + pos) . W^T`: fp32 models add pos to the A operand as the reference does; bf16 models
-// add the precomputed pos . W^T as a row-periodic residual (see gemm2.hip).
+// `(x + pos) . W^T`: fp32 / fp32x3 models add pos to the A operand as the reference does; bf16
+// and fp32x6 models add the precomputed pos . W^T as a row-periodic residual (see gemm2.hip).
 int add_pos(const spe_model* m, GemmArgs& g, const void* pos, int ldp, int period, const void* posw, int ldw) {
-  if (m->esz == 2 && posw) {
+  if ((m->esz == 2 || m->x6) && posw) {
     g.R = posw; g.ldr = ldw; g.r_period = period;
     return GEMM_LINEAR;
   }

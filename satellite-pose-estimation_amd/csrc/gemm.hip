@@ -630,7 +630,8 @@ constexpr int D6_SMEM = 2 * D6_STAGE;
 static_assert(D6_SMEM >= D6_BM * EPI_LD * 4, "epilogue tile fits the stages");
 constexpr int D6_BAD = 0x7ffffff0;          // out-of-range buffer offset -> zeros
 typedef __attribute__((address_space(3))) void* lds_ptr6_t;
-constexpr int d6_waitcnt_vm0() { return (7 << 4) | (15 << 8); }   // vmcnt(0), expcnt/lgkmcnt untouched
+constexpr int d6_waitcnt_vm(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }  // vmcnt(n) only
+constexpr int d6_waitcnt_vm0() { return d6_waitcnt_vm(0); }
 
 SPE_DEV u32x4 cat2(u32x2 a, u32x2 b) { return u32x4{a.x, a.y, b.x, b.y}; }
 
@@ -720,43 +721,93 @@ __global__ __launch_bounds__(D6_NT, 2) void gemm_x6d_kernel(GemmArgs g) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
+  // One 16-element half kk of a stage = one fragment set: the B planes b[p][j], and per A
+  // fragment row i the two 16-byte fp32 reads (halves h) split into 8-byte plane pieces.
+  struct Frag {
+    u32x4 b[3][2];
+    u32x4 raw[2][2];
+    u32x2 ph[2][2], pm[2][2], pl[2][2];
+  };
+  auto read_b = [&](const char* st, int kk, Frag& f) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int p = 0; p < 3; ++p) f.b[p][j] = ld16(st + boff[kk] + p * D6_PB + j * 2048);
+  };
+  auto read_a = [&](const char* st, int kk, Frag& f) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) f.raw[i][h] = ld16(st + aoff[kk][h] + i * 4096);
+  };
+  auto split_a = [&](Frag& f, int i, int h) { split3(f.raw[i][h], f.ph[i][h], f.pm[i][h], f.pl[i][h]); };
+  // MFMA number q (0..23) of a set: accumulator q / 6, product q % 6 (l.h, h.l, m.m, m.h, h.m, h.h)
+  auto mma1 = [&](const Frag& f, int q) {
+    const int a = q / 6, i = a >> 1, j = a & 1, t = q % 6;
+    const u32x4 ah = cat2(f.ph[i][0], f.ph[i][1]), am = cat2(f.pm[i][0], f.pm[i][1]), al = cat2(f.pl[i][0], f.pl[i][1]);
+    const u32x4 xa = t == 0 ? al : (t == 1 || t == 4 || t == 5) ? ah : am;
+    const u32x4 xb = (t == 0 || t == 3 || t == 5) ? f.b[0][j] : t == 1 ? f.b[2][j] : f.b[1][j];
+    acc[i][j] = mf(xa, xb, acc[i][j]);
+  };
+#define D6_MMA(F, LO, HI)                                \
+  _Pragma("unroll") for (int q = LO; q < HI; ++q) mma1(F, q); \
+  __builtin_amdgcn_sched_barrier(0);
+
+  // Software pipeline over K-step halves: X = the kk = 0 fragments, Y = kk = 1.  Phase A of step
+  // ks multiplies X while Y is read and split from the same stage; then every wave's reads of
+  // that stage are done and step ks+1's DMA has landed (issued a whole step earlier), so one
+  // barrier frees the stage for step ks+2's DMA; phase B multiplies Y while step ks+1's X is read
+  // and split from the other stage.  The loop body has no branches (past the last step the DMA
+  // and reads fetch in-bounds or zeroed bytes nobody uses) and is pinned in chunks
+  // (sched_barrier): the DS reads and DMA issues beside the first MFMAs, one split3 (4 values,
+  // ~18 VALU) per 3 MFMAs -- the 24 free issue cycles of each 32-cycle MFMA.
   issue(0, 0);
+  issue(1, 1);
+  __builtin_amdgcn_s_waitcnt(d6_waitcnt_vm(10));             // step 0's pieces (step 1's in flight)
+  __syncthreads();
+  Frag X, Y;
+  read_b(smem, 0, X);
+  read_a(smem, 0, X);
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) split_a(X, i, h);
   for (int ks = 0; ks < nk; ++ks) {
-    __builtin_amdgcn_s_waitcnt(d6_waitcnt_vm0());          // this wave's pieces of step ks landed
-    __syncthreads();                                         // everyone's; step ks-1's stage is free
-    if (ks + 1 < nk) issue(ks + 1, (ks + 1) & 1);
     const char* st = smem + (ks & 1) * D6_STAGE;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      u32x4 b[3][2], ah[2], am[2], al[2];
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int p = 0; p < 3; ++p) b[p][j] = ld16(st + boff[kk] + p * D6_PB + j * 2048);
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const u32x4 x0 = ld16(st + aoff[kk][0] + i * 4096), x1 = ld16(st + aoff[kk][1] + i * 4096);
-        u32x2 h0, m0_, l0, h1, m1, l1;
-        split3(x0, h0, m0_, l0);
-        split3(x1, h1, m1, l1);
-        ah[i] = cat2(h0, h1);
-        am[i] = cat2(m0_, m1);
-        al[i] = cat2(l0, l1);
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < 2; ++j) {
-          f32x16 c = acc[i][j];
-          c = mf(al[i], b[0][j], c);
-          c = mf(ah[i], b[2][j], c);
-          c = mf(am[i], b[1][j], c);
-          c = mf(am[i], b[0][j], c);
-          c = mf(ah[i], b[1][j], c);
-          acc[i][j] = mf(ah[i], b[0][j], c);
-        }
-    }
+    const char* sn = smem + ((ks + 1) & 1) * D6_STAGE;
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- phase A: X's MFMAs, Y read + split
+    read_b(st, 1, Y);
+    read_a(st, 1, Y);
+    D6_MMA(X, 0, 6)
+    split_a(Y, 0, 0);
+    D6_MMA(X, 6, 9)
+    split_a(Y, 0, 1);
+    D6_MMA(X, 9, 12)
+    split_a(Y, 1, 0);
+    D6_MMA(X, 12, 15)
+    split_a(Y, 1, 1);
+    D6_MMA(X, 15, 24)
+    __builtin_amdgcn_s_waitcnt(d6_waitcnt_vm0() & ~(15 << 8));  // vmcnt(0) lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- phase B: Y's MFMAs, step ks+2's DMA, step ks+1's X read + split
+    issue(ks + 2, ks & 1);
+    D6_MMA(Y, 0, 3)
+    read_b(sn, 0, X);
+    read_a(sn, 0, X);
+    D6_MMA(Y, 3, 9)
+    split_a(X, 0, 0);
+    D6_MMA(Y, 9, 12)
+    split_a(X, 0, 1);
+    D6_MMA(Y, 12, 15)
+    split_a(X, 1, 0);
+    D6_MMA(Y, 15, 18)
+    split_a(X, 1, 1);
+    D6_MMA(Y, 18, 24)
   }
+#undef D6_MMA
+  __builtin_amdgcn_s_waitcnt(d6_waitcnt_vm0());              // the past-the-end DMA, before the stages are reused
   __syncthreads();                                           // stages -> epilogue tile
 
   float bv[8];

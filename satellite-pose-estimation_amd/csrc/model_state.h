@@ -28,13 +28,13 @@ struct Block {
 struct Enc {
   Conv qk, v, o, l1, l2;
   float *n1g, *n1b, *n2g, *n2b;
-  void* pos_qk = nullptr;   // bf16 models: pos . W_qk^T [tokens][512] (row-periodic residual)
+  void* pos_qk = nullptr;   // bf16 / fp32x6 models: pos . W_qk^T [tokens][512] (row-periodic residual)
 };
 
 struct Dec {
   Conv sqk, sv, so, cq, co, l1, l2;
   float *n1g, *n1b, *n2g, *n2b, *n3g, *n3b;
-  void* qpos_sqk = nullptr; // bf16 models: query_pos . W_sqk^T [Q][512]
+  void* qpos_sqk = nullptr; // bf16 / fp32x6 models: query_pos . W_sqk^T [Q][512]
   void* qpos_cq = nullptr;  // bf16 models: query_pos . W_cq^T [Q][256]
   // cross-attention against the memory (spe_use_xattn, xattn.hip): q' = tgt . Wqk^T + xq_r
   // with Wq/Wk folded per head at finalize; xv = the value projection rows of in_proj
@@ -134,7 +134,7 @@ struct spe_model {
   std::vector<Dec> dec;
   void* pos = nullptr;     // [tokens][256] T
   void* qpos = nullptr;    // [Q][256] T
-  void* pos_crossK = nullptr;  // bf16 models: pos . W_crossK^T [tokens][L*256]
+  void* pos_crossK = nullptr;  // bf16 / fp32x6 models: pos . W_crossK^T [tokens][L*256]
   float *dng = nullptr, *dnb = nullptr;
   HeadArgs head{};
   Profiler prof;

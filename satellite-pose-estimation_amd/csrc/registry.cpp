@@ -516,16 +516,17 @@ int build_device(spe_model* m) {
   const int fs = c.input_size / 8;
   m->pos = upload_T(m, sine_pos(fs, fs, d));
   m->qpos = upload_T(m, m->host["query_embed.weight"]);
-  if (m->esz == 2) {
-    // bf16 throughput path: the `+ pos` of the q/k projections is applied as (pos . W^T), a
-    // row-periodic residual filled by spe_model_finalize (gemm2.hip header); fp32 keeps the
-    // reference's (x + pos) . W^T order for exact parity.
-    const size_t T = (size_t)fs * fs, Q = c.num_queries;
-    for (auto& e : m->enc) e.pos_qk = dalloc(m, T * 2 * d * 2);
-    m->pos_crossK = spe_use_xattn(m) ? nullptr : dalloc(m, T * c.dec_layers * d * 2);
+  if (m->esz == 2 || m->x6) {
+    // bf16 throughput path and fp32x6: the `+ pos` of the q/k projections is applied as
+    // (pos . W^T), a row-periodic residual filled by spe_model_finalize (gemm2.hip header) -- for
+    // fp32x6 in fp32, computed by the exact-f32 kernel, so the projection is a plain GEMM that the
+    // LDS-DMA x6 kernel takes; fp32 / fp32x3 keep the reference's (x + pos) . W^T order.
+    const size_t T = (size_t)fs * fs, Q = c.num_queries, es = m->esz;
+    for (auto& e : m->enc) e.pos_qk = dalloc(m, T * 2 * d * es);
+    m->pos_crossK = spe_use_xattn(m) ? nullptr : dalloc(m, T * c.dec_layers * d * es);
     for (auto& e : m->dec) {
-      e.qpos_sqk = dalloc(m, Q * 2 * d * 2);
-      e.qpos_cq = spe_use_xattn(m) ? nullptr : dalloc(m, Q * d * 2);
+      e.qpos_sqk = dalloc(m, Q * 2 * d * es);
+      e.qpos_cq = spe_use_xattn(m) ? nullptr : dalloc(m, Q * d * es);
     }
   }
   m->dng = upload_key(m, "transformer.decoder.norm.weight");
@@ -688,13 +689,13 @@ int spe_model_finalize(spe_model* m) {
   if (rc0) return rc0;
   e = hipDeviceSynchronize();
   if (e != hipSuccess || m->upload_err) return fail(e != hipSuccess ? (int)e : m->upload_err, "weight upload failed");
-  if (m->esz == 2 && m->family == 0) {
+  if ((m->esz == 2 || m->x6) && m->family == 0) {
     const int d = m->cfg.hidden_dim, fs = m->cfg.input_size / 8, T = fs * fs, Q = m->cfg.num_queries;
     auto proj = [&](const void* A, int rows, const Conv& w, void* out) {
       GemmArgs g{};
       g.A = A; g.lda = d; g.B = w.w; g.ldb = w.Kpad;
       g.M = rows; g.N = w.N; g.K = w.K; g.C = out; g.ldc = w.N;
-      return spe_launch_gemm(g, SPE_DTYPE_BF16, GEMM_LINEAR, nullptr);
+      return spe_launch_gemm(g, m->esz == 2 ? SPE_DTYPE_BF16 : SPE_DTYPE_F32, GEMM_LINEAR, nullptr);
     };
     int rc = 0;
     for (auto& l : m->enc) rc |= proj(m->pos, T, l.qk, l.pos_qk);

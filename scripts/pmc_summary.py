@@ -14,7 +14,7 @@ import os
 
 def short(name):
     n = name.replace("(anonymous namespace)::", "")
-    for key in ("gemm_x6_kernel", "attn_x3_kernel", "sgemm_kernel", "gemm2_kernel", "gemm_kernel", "ffn_pipe_kernel", "attn_bf16", "attn_f32", "ffn_ln", "layernorm", "heads", "pnp_kernel",
+    for key in ("gemm_x6d_kernel", "gemm_x6_kernel", "attn_x3_kernel", "sgemm_kernel", "gemm2_kernel", "gemm_kernel", "ffn_pipe_kernel", "attn_bf16", "attn_f32", "ffn_ln", "layernorm", "heads", "pnp_kernel",
                 "maxpool", "upsample", "pack_input", "postprocess", "score"):
         if key in n:
             return n[n.find(key):].replace("(GemmArgs", "(").split("(")[0][:64]
@@ -61,6 +61,10 @@ def main():
             # the chip has 1024 SIMDs (MI355X_MICROARCH.md PMC notes)
             line += f" mfma_busy={d['SQ_VALU_MFMA_BUSY_CYCLES'] / (d['GRBM_GUI_ACTIVE'] / 8 * 1024):.2f}"
             line += f" clk={d['GRBM_GUI_ACTIVE'] / 8 / d['us'] / 1e3:.2f}GHz"
+        if "SQ_INSTS_MFMA" in d and d["SQ_INSTS_MFMA"]:
+            line += f" valu/mfma={d.get('SQ_INSTS_VALU', 0) / d['SQ_INSTS_MFMA']:.2f}"
+            if "SQ_VALU_MFMA_COEXEC_CYCLES" in d and "SQ_VALU_MFMA_BUSY_CYCLES" in d:
+                line += f" coexec={d['SQ_VALU_MFMA_COEXEC_CYCLES'] / max(d['SQ_VALU_MFMA_BUSY_CYCLES'], 1):.2f}"
         if "SQ_LDS_BANK_CONFLICT" in d and "SQ_LDS_IDX_ACTIVE" in d:
             line += f" lds_conf={d['SQ_LDS_BANK_CONFLICT'] / max(d['SQ_LDS_IDX_ACTIVE'], 1):.2f}"
         print(line)
