@@ -250,34 +250,51 @@ def bench_data(cfg, B, rank):
     return synthetic_batch(cfg, B, seed=1000 + rank)
 
 
-def pose_consistent_weights(w, cfg, args, B, rank, world, dev):
+def pose_consistent_weights(w, cfg, args, B, rank, world, dev, rcfg=None):
     """Fit the point head (spe.synthetic.fit_point_head) on the decoder outputs of every rank's
     timed batch, so all ranks run identical weights: each rank computes its batch's hs and
-    targets, they are all-gathered, rank 0 fits and broadcasts the head."""
+    targets, they are all-gathered, rank 0 fits and broadcasts the head.  RT-DETR (rcfg): the
+    last decoder layer's dec_bbox_head, whose points are sigmoid(head(hs) + inverse_sigmoid(the
+    previous layer's points)) (UNC src/zoo/rtdetr/rtdetr_decoder.py:336-337) -- the fit gets those
+    logits as its offset."""
     import numpy as np
     import torch
     import torch.distributed as dist
-    from spe.models import DETR
     from spe.synthetic import fit_point_head, keypoint_targets
     data = bench_data(cfg, B, rank)
-    m = DETR(cfg, dtype=args.dtype, attn_dtype=args.attn_dtype)
-    m.load_state_dict(w)
-    o = m(torch.from_numpy(data["images"]).to(dev), return_hs=True)
+    x = torch.from_numpy(data["images"]).to(dev)
+    if rcfg is None:
+        from spe.models import DETR
+        m = DETR(cfg, dtype=args.dtype, attn_dtype=args.attn_dtype)
+        m.load_state_dict(w)
+        o = m(x, return_hs=True)
+        off = torch.zeros(o["hs"].shape[:2] + (2,), device=dev)
+        prefix = "point_embed"
+    else:
+        from spe.rtdetr import RTDETR
+        m = RTDETR(rcfg, dtype=args.dtype, aux_outputs=True)
+        m.load_state_dict(w)
+        o = m(x, return_hs=True)
+        ref = o["aux_outputs"][rcfg.dec_layers - 2]["pred_pts"].clamp(0.0, 1.0)
+        off = torch.log(ref.clamp(min=1e-5) / (1 - ref).clamp(min=1e-5))     # inverse_sigmoid, utils.py
+        prefix = f"decoder.dec_bbox_head.{rcfg.dec_layers - 1}"
     hs = o["hs"].float()
     labels = o["pred_logits"].argmax(-1).cpu().numpy()
     del m
     tgt, mask = keypoint_targets(data, labels, seed=7 + rank)
     tgt = torch.from_numpy(tgt).float().to(dev)
     mask = torch.from_numpy(mask).to(dev)
+    off = off.float().contiguous()
     if world > 1:
-        parts = [[torch.empty_like(t) for _ in range(world)] for t in (hs, tgt, mask)]
-        for pl, t in zip(parts, (hs, tgt, mask)):
+        parts = [[torch.empty_like(t) for _ in range(world)] for t in (hs, tgt, mask, off)]
+        for pl, t in zip(parts, (hs, tgt, mask, off)):
             dist.all_gather(pl, t.contiguous())
-        hs, tgt, mask = (torch.cat(pl) for pl in parts)
-    keys = [f"point_embed.layers.{j}.{k}" for j in range(3) for k in ("weight", "bias")]
+        hs, tgt, mask, off = (torch.cat(pl) for pl in parts)
+    keys = [f"{prefix}.layers.{j}.{k}" for j in range(3) for k in ("weight", "bias")]
     err = None
     if rank == 0:
-        w, err = fit_point_head(w, hs.cpu().numpy(), tgt.cpu().numpy(), mask.cpu().numpy(), device=dev)
+        w, err = fit_point_head(w, hs.cpu().numpy(), tgt.cpu().numpy(), mask.cpu().numpy(), device=dev,
+                                prefix=prefix, offset=None if rcfg is None else off.cpu().numpy())
     if world > 1:
         for k in keys:
             t = torch.from_numpy(w[k]).to(dev)
@@ -601,23 +618,24 @@ def main():
                             num_queries=args.queries, dec_layers=args.layers)
         from spe.synthetic import diversify_class_head
         w = random_rtdetr_weights(rcfg, 0)
-        if args.weights == "pose-consistent":
-            args.weights = "label-diverse"        # no point-head fit for the RT-DETR heads
-        if args.weights == "label-diverse":
+        if args.weights in ("label-diverse", "pose-consistent"):
             # RT-DETR's queries are distinct encoder tokens already; only the last score head is
             # drawn in the principal subspace of its input (spe.synthetic.diversify_class_head)
             m = RTDETR(rcfg, dtype=args.dtype, aux_outputs=False)
             m.load_state_dict(w)
-            calib = synthetic_batch(SpeConfig(input_size=args.size), 16, seed=4242)["images"]
-            x = torch.from_numpy(np.concatenate([calib] * ((B + 15) // 16))[:B]).to(dev)
-            hs = m(x, return_hs=True)["hs"].cpu().numpy()[:16]
+            # calibrated on rank 0's timed batch (every rank can draw it: identical weights on
+            # all ranks without a collective)
+            x = torch.from_numpy(bench_data(cfg, B, 0)["images"]).to(dev)
+            hs = m(x, return_hs=True)["hs"].cpu().numpy()
             del m
             # the selected queries of one image sit close together (top-k encoder tokens of a
-            # random-init encoder): take the head's directions from the within-image spread, or
-            # every query of an image gets the same one to three labels and the solver stops at
-            # its fewer-than-4-correspondences check
-            hs = hs - hs.mean(axis=1, keepdims=True) + hs.mean(axis=(0, 1), keepdims=True)
-            w = diversify_class_head(w, hs, head=f"decoder.dec_score_head.{rcfg.dec_layers - 1}")
+            # random-init encoder): the head's directions come from the within-image spread, off
+            # the span of the image means, or every query of an image gets the same one to three
+            # labels and the solver stops at its fewer-than-4-correspondences check
+            w = diversify_class_head(w, hs, head=f"decoder.dec_score_head.{rcfg.dec_layers - 1}", within_image=True)
+        if args.weights == "pose-consistent":
+            # then the last layer's point head fitted to the timed batch's keypoints, like the DETR line
+            w, fit = pose_consistent_weights(w, cfg, args, B, rank, world, dev, rcfg=rcfg)
         model = RTDETR(rcfg, dtype=args.dtype, aux_outputs=False)
         model.load_state_dict(w)
     else:
@@ -727,7 +745,7 @@ def main():
     })
     if "assess" in out:
         result["self_assessment_reliable"] = int(out["assess"]["reliable"].sum().item())
-    if rcfg is None and not args.raw_frames:
+    if not args.raw_frames and "points_px" in out["forward"] and "probs" in out["forward"]:
         e = keypoint_error_px(out["forward"]["points_px"], out["forward"]["probs"], data)
         result["keypoints_vs_gt_px"] = {"median": float(np.median(e)), "p90": float(np.percentile(e, 90)),
                                         "fg_queries": int(e.size), "weights": args.weights}

@@ -213,15 +213,15 @@ SPE_DEV void mma_step(const char* st, int wr, int wc, int lane, f32x4 (&acc)[4][
 
 // bias / residual / activation / head-transposed or row stores of a BM_ x BN tile whose fp32
 // accumulators are in LDS (ct, row stride EPI_LD), NT_ threads; bv = the thread's 8 bias values
-template <typename T, int BM_, int NT_>
+template <typename T, int BM_, int NT_, int BN_ = BN>
 SPE_DEV void store_tile(const GemmArgs& g, const float* ct, int m0, int n0, int tid, const float* bv) {
   if (g.vt_T > 0) {
     // head-transposed store: column n = grp*256 + hd -> C[((grp*vt_B + b)*256 + hd)*T + tok]
-    const int col = tid & 127, n = n0 + col;
+    const int col = tid % BN_, n = n0 + col;
     if (n >= g.N) return;
     const float bn = g.bias ? g.bias[n] : 0.f;
     const int grp = n >> 8, hd = n & 255;
-    for (int rg = (tid >> 7) * 8; rg < BM_; rg += NT_ / 16) {
+    for (int rg = (tid / BN_) * 8; rg < BM_; rg += (NT_ / BN_) * 8) {
       const int m = m0 + rg;
       if (m >= g.M) break;
       float v[8];
@@ -255,11 +255,12 @@ SPE_DEV void store_tile(const GemmArgs& g, const float* ct, int m0, int n0, int 
     return;
   }
 
-  const int cg = (tid & 15) * 8;
+  constexpr int CG = BN_ / 8;                       // 8-column groups per row
+  const int cg = (tid % CG) * 8;
   const int n = n0 + cg;
   if (n >= g.N) return;
   const bool full = n + 8 <= g.N;
-  for (int rr = tid >> 4; rr < BM_; rr += NT_ / 16) {
+  for (int rr = tid / CG; rr < BM_; rr += NT_ / CG) {
     const int m = m0 + rr;
     if (m >= g.M) break;
     float v[8];
@@ -615,19 +616,25 @@ int launch_x6(const GemmArgs& g, int mode, hipStream_t s) {
 // that step) -- A as raw fp32, split into its h / m / l planes by the waves that read the
 // fragments; B from the pre-split weight planes (GemmArgs::B6).  One barrier per K-step (32
 // elements); the DMA of step ks+1 is issued right behind step ks's barrier into the other stage
-// and has all of step ks's MFMAs to land.  v_mfma_f32_32x32x16_bf16 fragments (2 x 2 per wave of
-// 64 x 64): per step and wave 48 MFMAs, 8 A reads (2 x 16 B per 8-element fragment row) + 12 B
-// plane reads, 32 fp32 split.
-//   LDS stage (40 KiB): A [128 rows][128 B] fp32, chunk c of row r at slot c ^ ((r >> 1) & 7);
-//   B planes [3][128 rows][64 B] bf16, chunk c at slot c ^ ((r >> 2) & 3) -- both keyed for
+// and has all of step ks's MFMAs to land.  v_mfma_f32_32x32x16_bf16 fragments, FI x 2 per wave
+// of (32 FI) x 64: tile 128 x 128 (FI = 2, 2 x 2 waves) or 128 x 64 (FI = 1, 4 x 1 waves, for the
+// N = 64 convs of layer 1 that a 128-wide tile would compute half empty).  Per step and wave
+// 24 FI MFMAs, 4 FI A reads (2 x 16 B per 8-element fragment row) + 12 B plane reads, 16 FI fp32
+// split.
+//   LDS stage: A [128 rows][128 B] fp32, chunk c of row r at slot c ^ ((r >> 1) & 7);
+//   B planes [3][BN rows][64 B] bf16, chunk c at slot c ^ ((r >> 2) & 3) -- both keyed for
 //   gfx950's ds_read_b128 lane groups under the 32x32 fragment's lane -> row map (lane & 31),
-//   applied on the DMA source address.  Two stages (80 KiB) = two workgroups per CU.
+//   applied on the DMA source address.  Two stages (80 / 56 KiB) = two workgroups per CU.
 // Used for GEMM_LINEAR and GEMM_CONV with K % 32 == 0 (Cin % 32 == 0), pre-split weights and
 // 32-bit buffer offsets; everything else takes gemm_x6_kernel.
-constexpr int D6_BM = 128, D6_BN = 128, D6_NT = 256;
-constexpr int D6_A = D6_BM * 128, D6_PB = D6_BN * 64, D6_STAGE = D6_A + 3 * D6_PB;
-constexpr int D6_SMEM = 2 * D6_STAGE;
-static_assert(D6_SMEM >= D6_BM * EPI_LD * 4, "epilogue tile fits the stages");
+constexpr int D6_BM = 128, D6_NT = 256, D6_A = D6_BM * 128;
+template <int FI> struct D6Geo {
+  static constexpr int WN = FI, WM = 4 / WN, BN = 64 * WN;
+  static constexpr int PB = BN * 64, STAGE = D6_A + 3 * PB;
+  static constexpr int NBQ = 3 * BN / 64;              // B DMA pieces per wave per step
+  static constexpr int SMEM = 2 * STAGE > D6_BM * EPI_LD * 4 ? 2 * STAGE : D6_BM * EPI_LD * 4;
+  static constexpr int NQ = 12 * FI;                   // MFMAs per fragment set
+};
 constexpr int D6_BAD = 0x7ffffff0;          // out-of-range buffer offset -> zeros
 typedef __attribute__((address_space(3))) void* lds_ptr6_t;
 constexpr int d6_waitcnt_vm(int n) { return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8); }  // vmcnt(n) only
@@ -635,12 +642,24 @@ constexpr int d6_waitcnt_vm0() { return d6_waitcnt_vm(0); }
 
 SPE_DEV u32x4 cat2(u32x2 a, u32x2 b) { return u32x4{a.x, a.y, b.x, b.y}; }
 
-template <int MODE>
-__global__ __launch_bounds__(D6_NT, 2) void gemm_x6d_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(1024))) char smem[D6_SMEM];
+// One 16-element half kk of a stage = one fragment set: the B planes b[p][j], and per A
+// fragment row i the two 16-byte fp32 reads (halves h) split into 8-byte plane pieces.
+// (namespace scope: a kernel-local class depending on the template parameter lost the
+// kernel's host stub)
+template <int FI> struct D6Frag {
+  u32x4 b[3][2];
+  u32x4 raw[FI][2];
+  u32x2 ph[FI][2], pm[FI][2], pl[FI][2];
+};
+
+template <int MODE, int FI>
+__device__ __forceinline__ void gemm_x6d_body(const GemmArgs& g) {
+  using G = D6Geo<FI>;
+  constexpr int D6_BN = G::BN, D6_PB = G::PB, D6_STAGE = G::STAGE, NBQ = G::NBQ, NQ = G::NQ;
+  __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wr = wid >> 1, wc = wid & 1;
+  const int wr = wid / G::WN, wc = wid % G::WN;
   const int tilesN = (g.N + D6_BN - 1) / D6_BN;
   const int t = xcd_remap(blockIdx.x, gridDim.x);
   const int m0 = (t / tilesN) * D6_BM, n0 = (t % tilesN) * D6_BN;
@@ -669,10 +688,10 @@ __global__ __launch_bounds__(D6_NT, 2) void gemm_x6d_kernel(GemmArgs g) {
       ih0[q] = iw0[q] = 0;
     }
   }
-  int bvo[6];
+  int bvo[NBQ];
 #pragma unroll
-  for (int q = 0; q < 6; ++q) {
-    const int p = wid + 4 * q, plane = p >> 3, row = (p & 7) * 16 + (lane >> 2);
+  for (int q = 0; q < NBQ; ++q) {
+    const int p = wid + 4 * q, plane = p / (D6_BN / 16), row = (p % (D6_BN / 16)) * 16 + (lane >> 2);
     const int c = (lane & 3) ^ ((row >> 2) & 3), n = n0 + row;
     bvo[q] = n < g.N ? (int)((plane * pstride + (size_t)n * g.ldb) * 2) + c * 16 : D6_BAD;
   }
@@ -694,12 +713,12 @@ __global__ __launch_bounds__(D6_NT, 2) void gemm_x6d_kernel(GemmArgs g) {
                                                MODE == GEMM_CONV ? 0 : ks * 128, 0, 0);
     }
 #pragma unroll
-    for (int q = 0; q < 6; ++q)
+    for (int q = 0; q < NBQ; ++q)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lds_ptr6_t)(base + D6_A + (wid + 4 * q) * 1024), 16, bvo[q],
                                                ks * 64, 0, 0);
   };
 
-  // ---- fragment offsets: A row wr*64 + 32i + (lane & 31), 16-byte chunks 4kk + 2(lane >> 5) + h;
+  // ---- fragment offsets: A row wr*32FI + 32i + (lane & 31), 16-byte chunks 4kk + 2(lane >> 5) + h;
   // B row wc*64 + 32j + (lane & 31), chunk 2kk + (lane >> 5)
   const int l31 = lane & 31, hi = lane >> 5;
   int aoff[2][2], boff[2];
@@ -707,27 +726,21 @@ __global__ __launch_bounds__(D6_NT, 2) void gemm_x6d_kernel(GemmArgs g) {
   for (int kk = 0; kk < 2; ++kk) {
 #pragma unroll
     for (int h = 0; h < 2; ++h)
-      aoff[kk][h] = (wr * 64 + l31) * 128 + (((4 * kk + 2 * hi + h) ^ ((l31 >> 1) & 7)) << 4);
+      aoff[kk][h] = (wr * 32 * FI + l31) * 128 + (((4 * kk + 2 * hi + h) ^ ((l31 >> 1) & 7)) << 4);
     boff[kk] = D6_A + (wc * 64 + l31) * 64 + (((2 * kk + hi) ^ ((l31 >> 2) & 3)) << 4);
   }
   auto mf = [](u32x4 x, u32x4 y, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, x), __builtin_bit_cast(bf16x8, y), c, 0, 0, 0);
   };
-  f32x16 acc[2][2];
+  f32x16 acc[FI][2];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FI; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  // One 16-element half kk of a stage = one fragment set: the B planes b[p][j], and per A
-  // fragment row i the two 16-byte fp32 reads (halves h) split into 8-byte plane pieces.
-  struct Frag {
-    u32x4 b[3][2];
-    u32x4 raw[2][2];
-    u32x2 ph[2][2], pm[2][2], pl[2][2];
-  };
+  using Frag = D6Frag<FI>;
   auto read_b = [&](const char* st, int kk, Frag& f) {
 #pragma unroll
     for (int j = 0; j < 2; ++j)
@@ -736,12 +749,12 @@ __global__ __launch_bounds__(D6_NT, 2) void gemm_x6d_kernel(GemmArgs g) {
   };
   auto read_a = [&](const char* st, int kk, Frag& f) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
+    for (int i = 0; i < FI; ++i)
 #pragma unroll
       for (int h = 0; h < 2; ++h) f.raw[i][h] = ld16(st + aoff[kk][h] + i * 4096);
   };
   auto split_a = [&](Frag& f, int i, int h) { split3(f.raw[i][h], f.ph[i][h], f.pm[i][h], f.pl[i][h]); };
-  // MFMA number q (0..23) of a set: accumulator q / 6, product q % 6 (l.h, h.l, m.m, m.h, h.m, h.h)
+  // MFMA number q (0 .. NQ-1) of a set: accumulator q / 6, product q % 6 (l.h, h.l, m.m, m.h, h.m, h.h)
   auto mma1 = [&](const Frag& f, int q) {
     const int a = q / 6, i = a >> 1, j = a & 1, t = q % 6;
     const u32x4 ah = cat2(f.ph[i][0], f.ph[i][1]), am = cat2(f.pm[i][0], f.pm[i][1]), al = cat2(f.pl[i][0], f.pl[i][1]);
@@ -763,15 +776,16 @@ __global__ __launch_bounds__(D6_NT, 2) void gemm_x6d_kernel(GemmArgs g) {
   // ~18 VALU) per 3 MFMAs -- the 24 free issue cycles of each 32-cycle MFMA.
   issue(0, 0);
   issue(1, 1);
-  __builtin_amdgcn_s_waitcnt(d6_waitcnt_vm(10));             // step 0's pieces (step 1's in flight)
+  __builtin_amdgcn_s_waitcnt(d6_waitcnt_vm(4 + NBQ));        // step 0's pieces (step 1's in flight)
   __syncthreads();
   Frag X, Y;
   read_b(smem, 0, X);
   read_a(smem, 0, X);
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FI; ++i)
 #pragma unroll
     for (int h = 0; h < 2; ++h) split_a(X, i, h);
+  constexpr int QA = NQ / 4, QB = 3 + NQ / 4;          // MFMAs before the first split of each phase
   for (int ks = 0; ks < nk; ++ks) {
     const char* st = smem + (ks & 1) * D6_STAGE;
     const char* sn = smem + ((ks + 1) & 1) * D6_STAGE;
@@ -779,15 +793,13 @@ __global__ __launch_bounds__(D6_NT, 2) void gemm_x6d_kernel(GemmArgs g) {
     // ---- phase A: X's MFMAs, Y read + split
     read_b(st, 1, Y);
     read_a(st, 1, Y);
-    D6_MMA(X, 0, 6)
-    split_a(Y, 0, 0);
-    D6_MMA(X, 6, 9)
-    split_a(Y, 0, 1);
-    D6_MMA(X, 9, 12)
-    split_a(Y, 1, 0);
-    D6_MMA(X, 12, 15)
-    split_a(Y, 1, 1);
-    D6_MMA(X, 15, 24)
+    D6_MMA(X, 0, QA)
+#pragma unroll
+    for (int sp = 0; sp < 2 * FI; ++sp) {
+      split_a(Y, sp >> 1, sp & 1);
+      D6_MMA(X, QA + 3 * sp, QA + 3 * sp + 3)
+    }
+    D6_MMA(X, QA + 6 * FI, NQ)
     __builtin_amdgcn_s_waitcnt(d6_waitcnt_vm0() & ~(15 << 8));  // vmcnt(0) lgkmcnt(0)
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
@@ -796,15 +808,13 @@ __global__ __launch_bounds__(D6_NT, 2) void gemm_x6d_kernel(GemmArgs g) {
     D6_MMA(Y, 0, 3)
     read_b(sn, 0, X);
     read_a(sn, 0, X);
-    D6_MMA(Y, 3, 9)
-    split_a(X, 0, 0);
-    D6_MMA(Y, 9, 12)
-    split_a(X, 0, 1);
-    D6_MMA(Y, 12, 15)
-    split_a(X, 1, 0);
-    D6_MMA(Y, 15, 18)
-    split_a(X, 1, 1);
-    D6_MMA(Y, 18, 24)
+    D6_MMA(Y, 3, QB)
+#pragma unroll
+    for (int sp = 0; sp < 2 * FI; ++sp) {
+      split_a(X, sp >> 1, sp & 1);
+      D6_MMA(Y, QB + 3 * sp, QB + 3 * sp + 3)
+    }
+    D6_MMA(Y, QB + 6 * FI, NQ)
   }
 #undef D6_MMA
   __builtin_amdgcn_s_waitcnt(d6_waitcnt_vm0());              // the past-the-end DMA, before the stages are reused
@@ -812,22 +822,28 @@ __global__ __launch_bounds__(D6_NT, 2) void gemm_x6d_kernel(GemmArgs g) {
 
   float bv[8];
   {
-    const int n = n0 + (tid & 15) * 8;
+    const int n = n0 + (tid % (D6_BN / 8)) * 8;
 #pragma unroll
     for (int e = 0; e < 8; ++e) bv[e] = (g.bias && n + e < g.N) ? g.bias[n + e] : 0.f;
   }
   float* ct = reinterpret_cast<float*>(smem);
   // 32x32 accumulator: lane holds rows 8 (r >> 2) + 4 (lane >> 5) + (r & 3), column lane & 31
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < FI; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r = 0; r < 16; ++r)
-        ct[(wr * 64 + 32 * i + 8 * (r >> 2) + 4 * hi + (r & 3)) * EPI_LD + wc * 64 + 32 * j + l31] = acc[i][j][r];
+        ct[(wr * 32 * FI + 32 * i + 8 * (r >> 2) + 4 * hi + (r & 3)) * EPI_LD + wc * 64 + 32 * j + l31] = acc[i][j][r];
   __syncthreads();
-  store_tile<float, D6_BM, D6_NT>(g, ct, m0, n0, tid, bv);
+  store_tile<float, D6_BM, D6_NT, D6_BN>(g, ct, m0, n0, tid, bv);
 }
+
+// (non-template entry points: the host stubs of a template of this body were not emitted)
+__global__ __launch_bounds__(D6_NT, 2) void gemm_x6d_linear(GemmArgs g) { gemm_x6d_body<GEMM_LINEAR, 2>(g); }
+__global__ __launch_bounds__(D6_NT, 2) void gemm_x6d_linear_n64(GemmArgs g) { gemm_x6d_body<GEMM_LINEAR, 1>(g); }
+__global__ __launch_bounds__(D6_NT, 2) void gemm_x6d_conv(GemmArgs g) { gemm_x6d_body<GEMM_CONV, 2>(g); }
+__global__ __launch_bounds__(D6_NT, 2) void gemm_x6d_conv_n64(GemmArgs g) { gemm_x6d_body<GEMM_CONV, 1>(g); }
 
 // 1 = not a problem for the DMA kernel
 int launch_x6d(const GemmArgs& g, int mode, hipStream_t s) {
@@ -842,10 +858,20 @@ int launch_x6d(const GemmArgs& g, int mode, hipStream_t s) {
   } else if ((long long)(g.M + D6_BM) * g.lda * 4 + (long long)g.K * 4 >= LIM) {
     return 1;
   }
-  const int tiles = ((g.M + D6_BM - 1) / D6_BM) * ((g.N + D6_BN - 1) / D6_BN);
+  // N <= 64: the 128 x 64 tile (SPE_X6_N64=0 keeps 128 x 128)
+  static const int n64 = [] { const char* e = getenv("SPE_X6_N64"); return e ? atoi(e) : 1; }();
+  const bool narrow = n64 && g.N <= 64;
+  const int bn = narrow ? 64 : 128;
+  const int tiles = ((g.M + D6_BM - 1) / D6_BM) * ((g.N + bn - 1) / bn);
   if (tiles <= 0) return 0;
-  if (mode == GEMM_CONV) hipLaunchKernelGGL(gemm_x6d_kernel<GEMM_CONV>, dim3(tiles), dim3(D6_NT), 0, s, g);
-  else hipLaunchKernelGGL(gemm_x6d_kernel<GEMM_LINEAR>, dim3(tiles), dim3(D6_NT), 0, s, g);
+  const dim3 grid(tiles), block(D6_NT);
+  if (mode == GEMM_CONV) {
+    if (narrow) hipLaunchKernelGGL(gemm_x6d_conv_n64, grid, block, 0, s, g);
+    else hipLaunchKernelGGL(gemm_x6d_conv, grid, block, 0, s, g);
+  } else {
+    if (narrow) hipLaunchKernelGGL(gemm_x6d_linear_n64, grid, block, 0, s, g);
+    else hipLaunchKernelGGL(gemm_x6d_linear, grid, block, 0, s, g);
+  }
   return (int)hipGetLastError();
 }
 

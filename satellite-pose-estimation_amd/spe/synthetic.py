@@ -205,9 +205,23 @@ def sharpen_decoder(w, cfg: SpeConfig, factor: float = 64.0):
     return w
 
 
-def diversify_class_head(w, hs, seed: int = 1, k: int = 12, logit_scale: float = 6.0, head: str = "cls_embed"):
+def diversify_class_head(w, hs, seed: int = 1, k: int = 12, logit_scale: float = 6.0, head: str = "cls_embed",
+                         within_image: bool = False):
     """hs: [N, d] decoder outputs (after decoder_norm) of a calibration batch; head: the class
-    head's state_dict prefix (RT-DETR: decoder.dec_score_head.<last layer>)."""
+    head's state_dict prefix (RT-DETR: decoder.dec_score_head.<last layer>).  within_image (hs
+    [B, Q, d]): the head's directions come from the spread of each image's queries about their
+    image mean, projected off the span of the image means' differences -- so the head ignores
+    which image a query belongs to and labels by the within-image differences alone (RT-DETR's
+    selected queries of one image sit close together: a head that also sees the image means gives
+    all of an image's queries the same few labels)."""
+    if within_image:
+        h3 = np.asarray(hs, np.float64)
+        means = h3.mean(axis=1)
+        U, sv, _ = np.linalg.svd((means - means.mean(0)).T, full_matrices=False)
+        U = U[:, sv > 1e-9 * max(sv.max(), 1e-30)]
+        dev = (h3 - means[:, None, :]).reshape(-1, h3.shape[-1])
+        dev = dev - (dev @ U) @ U.T
+        hs = dev + means.mean(0)
     hs = np.asarray(hs, np.float64).reshape(-1, hs.shape[-1])
     mu = hs.mean(0)
     _, S, Vt = np.linalg.svd(hs - mu, full_matrices=False)
@@ -259,18 +273,21 @@ def keypoint_targets(batch, labels, seed: int = 0, noise_px: float = 2.0, outlie
 
 
 def fit_point_head(w, hs, targets, mask, steps: int = 2000, lr: float = 1e-3, seed: int = 0, device="cpu",
-                   prefix: str = "point_embed", noise_rel: float = 2.0 ** -8):
+                   prefix: str = "point_embed", noise_rel: float = 2.0 ** -8, offset=None):
     """Fit the 3-layer point MLP to `targets` [N,2] on decoder outputs `hs` [N,d] (rows with
     mask False ignored).  Full-batch Adam in torch on `device`; the input standardisation is
     folded into layer 0 afterwards.  Every step perturbs the inputs by Gaussian noise of
     noise_rel x |hs| (bf16's rounding scale): the hs of different images differ by only a few
     percent, and an unregularised interpolant of them amplifies any perturbation of hs (such as
     fp32 vs bf16 rounding) into tens of pixels, unlike a trained model; the noise keeps the fitted
-    head smooth at that scale.  Returns (weights, fit error in target units [N] on masked rows)."""
+    head smooth at that scale.  offset [N,2] (logits): the head's output is sigmoid(MLP(hs) +
+    offset) -- RT-DETR's refined points, sigmoid(dec_bbox_head(hs) + inverse_sigmoid(reference))
+    (UNC src/zoo/rtdetr/rtdetr_decoder.py:336-337).  Returns (weights, fit error in target units [N] on masked rows)."""
     import torch
     hs = torch.as_tensor(np.asarray(hs, np.float32).reshape(-1, np.shape(hs)[-1]), device=device)
     y = torch.as_tensor(np.asarray(targets, np.float32).reshape(-1, 2), device=device)
     m = torch.as_tensor(np.asarray(mask).reshape(-1), device=device)
+    off = 0.0 if offset is None else torch.as_tensor(np.asarray(offset, np.float32).reshape(-1, 2), device=device)
     mu, sd = hs.mean(0), hs.std(0) + 1e-6
     x = (hs - mu) / sd
     d = hs.shape[1]
@@ -285,7 +302,7 @@ def fit_point_head(w, hs, targets, mask, steps: int = 2000, lr: float = 1e-3, se
     def net(z):
         z = torch.relu(z @ params[0].t() + params[1])
         z = torch.relu(z @ params[2].t() + params[3])
-        return torch.sigmoid(z @ params[4].t() + params[5])
+        return torch.sigmoid(z @ params[4].t() + params[5] + off)
 
     opt = torch.optim.Adam(params, lr=lr)
     sched = torch.optim.lr_scheduler.CosineAnnealingLR(opt, steps)

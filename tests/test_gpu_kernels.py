@@ -814,7 +814,8 @@ def _split_gemm_err(gpu_device, case, dtype, planes=False, want_path=None):
     g = torch.Generator(device="cpu").manual_seed(len(case))
     dev, f = gpu_device, torch.float32
     if case.startswith("conv"):
-        B, H, Cin, Cout, k, st, pd = (2, 26, 256, 256, 3, 1, 1) if case == "conv3x3" else (2, 52, 512, 256, 1, 2, 0)
+        B, H, Cin, Cout, k, st, pd = {"conv3x3": (2, 26, 256, 256, 3, 1, 1), "conv3x3_n64": (2, 26, 64, 64, 3, 1, 1),
+                                      "conv1x1s2": (2, 52, 512, 256, 1, 2, 0)}[case]
         x = torch.randn(B, Cin, H, H, generator=g, dtype=torch.float64)
         w = torch.randn(Cout, Cin, k, k, generator=g, dtype=torch.float64) / (Cin * k * k) ** 0.5
         ref = F.conv2d(x, w, stride=st, padding=pd).permute(0, 2, 3, 1).reshape(-1, Cout)
@@ -830,7 +831,8 @@ def _split_gemm_err(gpu_device, case, dtype, planes=False, want_path=None):
             _gemm(dtype, 2, A, Wp, M, Cout, K, 0, K, C, Cout, conv=(H, H, Cin, k, k, st, pd))
         got = C
     else:
-        M, N, K = (3000, 200, 512) if case != "vt" else (2 * 2704, 256, 256)
+        M, N, K = {"vt": (2 * 2704, 256, 256), "linear_n64": (3000, 64, 256), "linear_n40": (3000, 40, 256)}.get(
+            case, (3000, 200, 512))
         A = torch.randn(M, K, generator=g, dtype=torch.float64)
         Wt = torch.randn(N, K, generator=g, dtype=torch.float64) / K ** 0.5
         bias = torch.randn(N, generator=g, dtype=torch.float64)
@@ -875,11 +877,13 @@ def test_gemm_x3_close_to_fp64(gpu_device, case, dtype):
         assert err <= max(1e-6, 2 * e32), (err, e32)
 
 
-@pytest.mark.parametrize("case", ["linear", "linear_add_relu_res", "conv3x3", "conv1x1s2"])
+@pytest.mark.parametrize("case", ["linear", "linear_add_relu_res", "conv3x3", "conv1x1s2", "linear_n64", "linear_n40",
+                                  "conv3x3_n64"])
 def test_gemm_x6_dma_close_to_fp64(gpu_device, case):
     """fp32x6 with the weights pre-split (the models' launch): the LDS-DMA kernel (gemm path 6)
     runs -- ragged M and N tiles, residual + ReLU epilogue, padded 3x3 and strided 1x1 implicit
-    GEMMs -- at the exact-f32 kernel's own error, like the register-staged x6 kernel."""
+    GEMMs, the 128 x 64 tile of N <= 64 -- at the exact-f32 kernel's own error, like the
+    register-staged x6 kernel."""
     err = _split_gemm_err(gpu_device, case, "fp32x6", planes=True, want_path=6)
     e32 = _split_gemm_err(gpu_device, case, "fp32")
     assert err <= max(1e-6, 2 * e32), (err, e32)

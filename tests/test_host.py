@@ -235,3 +235,39 @@ def test_bench_rejects_world_mismatch():
     r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--batch", "4", "--steps", "1"],
                        env=env, capture_output=True, text=True, timeout=120)
     assert r.returncode == 2 and "world size" in r.stderr
+
+
+def test_diversify_within_image_labels_ignore_the_image():
+    """RT-DETR bench weights (spe.synthetic.diversify_class_head, within_image): when the image
+    means dominate the query features, the head still gives each image's queries several labels
+    and does not see the image-mean differences."""
+    from spe.synthetic import diversify_class_head
+    rng = np.random.Generator(np.random.PCG64(3))
+    B, Q, d = 16, 30, 64
+    means = rng.normal(0, 10.0, (B, d))
+    hs = means[:, None, :] + rng.normal(0, 0.05, (B, Q, d))
+    w = {"h.weight": np.zeros((12, d), np.float32), "h.bias": np.zeros(12, np.float32)}
+    w = diversify_class_head(w, hs, head="h", within_image=True)
+    lab = (hs @ w["h.weight"].T + w["h.bias"]).argmax(-1)
+    assert min(len(set(lab[i].tolist()) - {11}) for i in range(B)) >= 4
+    # the head's rows are orthogonal to the image-mean differences (to float32 storage precision)
+    W = w["h.weight"].astype(np.float64)
+    diff = means[3] - means[5]
+    assert np.abs(W @ diff).max() <= 1e-3 * np.linalg.norm(W, axis=1).max() * np.linalg.norm(diff)
+
+
+def test_fit_point_head_with_logit_offset():
+    """RT-DETR's refined points are sigmoid(head(hs) + inverse_sigmoid(reference)): the fit with
+    that offset reproduces its targets through the same formula."""
+    from spe.synthetic import fit_point_head
+    rng = np.random.Generator(np.random.PCG64(5))
+    N, d = 200, 32
+    hs = rng.normal(0, 1.0, (N, d)).astype(np.float32)
+    tgt = rng.uniform(0.1, 0.9, (N, 2)).astype(np.float32)
+    off = rng.normal(0, 1.0, (N, 2)).astype(np.float32)
+    mask = np.ones(N, bool)
+    w, err = fit_point_head({}, hs, tgt, mask, steps=1500, lr=3e-3, prefix="p", noise_rel=0.0, offset=off)
+    z = np.maximum(hs @ w["p.layers.0.weight"].T + w["p.layers.0.bias"], 0)
+    z = np.maximum(z @ w["p.layers.1.weight"].T + w["p.layers.1.bias"], 0)
+    pts = 1 / (1 + np.exp(-(z @ w["p.layers.2.weight"].T + w["p.layers.2.bias"] + off)))
+    assert np.abs(pts - tgt).max() < 0.05 and err.max() < 0.05, (np.abs(pts - tgt).max(), err.max())
