@@ -652,7 +652,10 @@ template <int FI> struct D6Frag {
   u32x2 ph[FI][2], pm[FI][2], pl[FI][2];
 };
 
-template <int MODE, int FI>
+// PL (GEMM_CONV, Cin % 32 != 0, e.g. the stem's 4- or 8-channel input): a 32-element K-step
+// spans several taps, so each lane decodes its own chunk's (kh, kw, ci) per step, and chunks past
+// K read zeros (K need not be a multiple of 32)
+template <int MODE, int FI, bool PL = false>
 __device__ __forceinline__ void gemm_x6d_body(const GemmArgs& g) {
   using G = D6Geo<FI>;
   constexpr int D6_BN = G::BN, D6_PB = G::PB, D6_STAGE = G::STAGE, NBQ = G::NBQ, NQ = G::NQ;
@@ -663,7 +666,7 @@ __device__ __forceinline__ void gemm_x6d_body(const GemmArgs& g) {
   const int tilesN = (g.N + D6_BN - 1) / D6_BN;
   const int t = xcd_remap(blockIdx.x, gridDim.x);
   const int m0 = (t / tilesN) * D6_BM, n0 = (t % tilesN) * D6_BN;
-  const int nk = g.K >> 5;
+  const int nk = (g.K + 31) >> 5;
   const long long abytes = MODE == GEMM_CONV ? (long long)(g.M / (g.Ho * g.Wo)) * g.H * g.W * g.Cin * 4
                                              : (long long)g.M * g.lda * 4;
   const size_t pstride = (size_t)g.b6_rows * g.ldb;
@@ -682,7 +685,7 @@ __device__ __forceinline__ void gemm_x6d_body(const GemmArgs& g) {
       const int b = mm / hw, r = mm - b * hw, oh = r / g.Wo, ow = r - oh * g.Wo;
       ih0[q] = m < g.M ? oh * g.stride - g.pad : -(1 << 28);
       iw0[q] = ow * g.stride - g.pad;
-      avo[q] = b * g.H * g.W * g.Cin + c * 4;            // elements: image base + the lane's chunk
+      avo[q] = b * g.H * g.W * g.Cin + (PL ? 0 : c * 4);   // elements: image base (+ the lane's chunk)
     } else {
       avo[q] = m < g.M ? m * g.lda * 4 + c * 16 : D6_BAD;
       ih0[q] = iw0[q] = 0;
@@ -695,16 +698,29 @@ __device__ __forceinline__ void gemm_x6d_body(const GemmArgs& g) {
     const int c = (lane & 3) ^ ((row >> 2) & 3), n = n0 + row;
     bvo[q] = n < g.N ? (int)((plane * pstride + (size_t)n * g.ldb) * 2) + c * 16 : D6_BAD;
   }
+  // the lane's A chunk column: (lane & 7) ^ ((row >> 1) & 7) is the same for all four pieces
+  const int ck = (lane & 7) ^ ((wid * 4 + (lane >> 4)) & 7);
   auto issue = [&](int ks, int stg) {
     char* base = smem + stg * D6_STAGE;
     int kh = 0, kw = 0, ci = 0;
-    if constexpr (MODE == GEMM_CONV) conv_k_decode(ks * 32, g.Cin, g.KW, g.KH * g.KW, kh, kw, ci);
+    bool kv = true;
+    if constexpr (MODE == GEMM_CONV) {
+      if constexpr (PL) {
+        const int k = ks * 32 + ck * 4, tap = k / g.Cin;
+        ci = k - tap * g.Cin;
+        kh = tap / g.KW;
+        kw = tap - kh * g.KW;
+        kv = k < g.K;
+      } else {
+        conv_k_decode(ks * 32, g.Cin, g.KW, g.KH * g.KW, kh, kw, ci);
+      }
+    }
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       int off;
       if constexpr (MODE == GEMM_CONV) {
         const int ih = ih0[q] + kh, iw = iw0[q] + kw;
-        const bool v = ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+        const bool v = kv && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
         off = v ? (avo[q] + (ih * g.W + iw) * g.Cin + ci) * 4 : D6_BAD;
       } else {
         off = avo[q];
@@ -844,16 +860,19 @@ __global__ __launch_bounds__(D6_NT, 2) void gemm_x6d_linear(GemmArgs g) { gemm_x
 __global__ __launch_bounds__(D6_NT, 2) void gemm_x6d_linear_n64(GemmArgs g) { gemm_x6d_body<GEMM_LINEAR, 1>(g); }
 __global__ __launch_bounds__(D6_NT, 2) void gemm_x6d_conv(GemmArgs g) { gemm_x6d_body<GEMM_CONV, 2>(g); }
 __global__ __launch_bounds__(D6_NT, 2) void gemm_x6d_conv_n64(GemmArgs g) { gemm_x6d_body<GEMM_CONV, 1>(g); }
+__global__ __launch_bounds__(D6_NT, 2) void gemm_x6d_conv_pl(GemmArgs g) { gemm_x6d_body<GEMM_CONV, 2, true>(g); }
+__global__ __launch_bounds__(D6_NT, 2) void gemm_x6d_conv_pl_n64(GemmArgs g) { gemm_x6d_body<GEMM_CONV, 1, true>(g); }
 
 // 1 = not a problem for the DMA kernel
 int launch_x6d(const GemmArgs& g, int mode, hipStream_t s) {
   static const int en = [] { const char* e = getenv("SPE_X6_DMA"); return e ? atoi(e) : 1; }();
-  if (!en || !g.B6 || (mode != GEMM_LINEAR && mode != GEMM_CONV) || (g.K & 31) || (g.lda & 3)) return 1;
+  if (!en || !g.B6 || (mode != GEMM_LINEAR && mode != GEMM_CONV) || (g.lda & 3)) return 1;
+  const bool pl = mode == GEMM_CONV && (g.Cin & 31);      // per-lane tap decode (stem)
+  if (pl ? ((g.Cin & 3) || (g.K & 3) || g.K != g.Cin * g.KH * g.KW) : (g.K & 31)) return 1;
   if ((reinterpret_cast<uintptr_t>(g.A) & 15) || (reinterpret_cast<uintptr_t>(g.B6) & 15) || (g.ldb & 7)) return 1;
   constexpr long long LIM = (1LL << 31) - (1LL << 24);
   if ((long long)3 * g.b6_rows * g.ldb * 2 >= LIM || g.b6_rows < g.N) return 1;
   if (mode == GEMM_CONV) {
-    if (g.Cin & 31) return 1;
     if ((long long)(g.M / (g.Ho * g.Wo)) * g.H * g.W * g.Cin * 4 >= LIM) return 1;
   } else if ((long long)(g.M + D6_BM) * g.lda * 4 + (long long)g.K * 4 >= LIM) {
     return 1;
@@ -865,7 +884,10 @@ int launch_x6d(const GemmArgs& g, int mode, hipStream_t s) {
   const int tiles = ((g.M + D6_BM - 1) / D6_BM) * ((g.N + bn - 1) / bn);
   if (tiles <= 0) return 0;
   const dim3 grid(tiles), block(D6_NT);
-  if (mode == GEMM_CONV) {
+  if (mode == GEMM_CONV && pl) {
+    if (narrow) hipLaunchKernelGGL(gemm_x6d_conv_pl_n64, grid, block, 0, s, g);
+    else hipLaunchKernelGGL(gemm_x6d_conv_pl, grid, block, 0, s, g);
+  } else if (mode == GEMM_CONV) {
     if (narrow) hipLaunchKernelGGL(gemm_x6d_conv_n64, grid, block, 0, s, g);
     else hipLaunchKernelGGL(gemm_x6d_conv, grid, block, 0, s, g);
   } else {

@@ -815,7 +815,8 @@ def _split_gemm_err(gpu_device, case, dtype, planes=False, want_path=None):
     dev, f = gpu_device, torch.float32
     if case.startswith("conv"):
         B, H, Cin, Cout, k, st, pd = {"conv3x3": (2, 26, 256, 256, 3, 1, 1), "conv3x3_n64": (2, 26, 64, 64, 3, 1, 1),
-                                      "conv1x1s2": (2, 52, 512, 256, 1, 2, 0)}[case]
+                                      "conv1x1s2": (2, 52, 512, 256, 1, 2, 0),
+                                      "conv7x7s2_c8": (2, 40, 8, 64, 7, 2, 3)}[case]
         x = torch.randn(B, Cin, H, H, generator=g, dtype=torch.float64)
         w = torch.randn(Cout, Cin, k, k, generator=g, dtype=torch.float64) / (Cin * k * k) ** 0.5
         ref = F.conv2d(x, w, stride=st, padding=pd).permute(0, 2, 3, 1).reshape(-1, Cout)
@@ -823,12 +824,14 @@ def _split_gemm_err(gpu_device, case, dtype, planes=False, want_path=None):
         Wp = _pack_conv(w).to(dev, f).contiguous()
         Ho = (H + 2 * pd - k) // st + 1
         M, K = B * Ho * Ho, Cin * k * k
+        if K % 64:                                     # weight rows padded to 64 elements
+            Wp = torch.nn.functional.pad(Wp, (0, 64 - K % 64))
         C = torch.zeros(M, Cout, dtype=f, device=dev)
         if planes:
             path = _gemm_planes(2, A, Wp, M, Cout, K, 0, C, Cout, conv=(H, H, Cin, k, k, st, pd))
             assert want_path is None or path == want_path, path
         else:
-            _gemm(dtype, 2, A, Wp, M, Cout, K, 0, K, C, Cout, conv=(H, H, Cin, k, k, st, pd))
+            _gemm(dtype, 2, A, Wp, M, Cout, K, 0, Wp.shape[1], C, Cout, conv=(H, H, Cin, k, k, st, pd))
         got = C
     else:
         M, N, K = {"vt": (2 * 2704, 256, 256), "linear_n64": (3000, 64, 256), "linear_n40": (3000, 40, 256)}.get(
@@ -878,12 +881,13 @@ def test_gemm_x3_close_to_fp64(gpu_device, case, dtype):
 
 
 @pytest.mark.parametrize("case", ["linear", "linear_add_relu_res", "conv3x3", "conv1x1s2", "linear_n64", "linear_n40",
-                                  "conv3x3_n64"])
+                                  "conv3x3_n64", "conv7x7s2_c8"])
 def test_gemm_x6_dma_close_to_fp64(gpu_device, case):
     """fp32x6 with the weights pre-split (the models' launch): the LDS-DMA kernel (gemm path 6)
     runs -- ragged M and N tiles, residual + ReLU epilogue, padded 3x3 and strided 1x1 implicit
-    GEMMs, the 128 x 64 tile of N <= 64 -- at the exact-f32 kernel's own error, like the
-    register-staged x6 kernel."""
+    GEMMs, the 128 x 64 tile of N <= 64, the stem's 8-channel 7x7 with per-lane tap decode and a
+    partial last K-step -- at the exact-f32 kernel's own error, like the register-staged x6
+    kernel."""
     err = _split_gemm_err(gpu_device, case, "fp32x6", planes=True, want_path=6)
     e32 = _split_gemm_err(gpu_device, case, "fp32")
     assert err <= max(1e-6, 2 * e32), (err, e32)
