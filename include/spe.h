@@ -316,6 +316,14 @@ int spe_debug_upconv(void* stream, int dtype, const void* z, void* out, int ldo,
  * {(64, 64, r), (64, 128, r), (128, 64, null)}. */
 int spe_debug_btail(void* stream, const void* a, int lda, int k1, const void* r, const void* w3, int ld3,
                     const float* b3, void* y, const void* w1p, int ld1, const float* b1, void* z, int n2, int M);
+/* the same with the block-output width n1 (round 4): n1 = 512 / 1024 runs the split-N form of the
+ * layer-2 / layer-3 boundaries (y produced in column chunks, weights streamed through LDS);
+ * (k1, n1, n2) in {(128, 512, 128), (128, 512, 256), (256, 1024, 256)} with r [M][n1] non-null,
+ * or n1 = 256 as spe_debug_btail.  Replaces the conv3 + conv1 launch pair of
+ * REV/models/backbone.py:114-125 (torchvision Bottleneck) at those boundaries. */
+int spe_debug_btail_n1(void* stream, const void* a, int lda, int k1, const void* r, const void* w3, int ld3,
+                       const float* b3, void* y, const void* w1p, int ld1, const float* b1, void* z, int n1, int n2,
+                       int M);
 /* the K-column order btail's second product expects: stored column k holds channel perm(k) */
 int spe_debug_btail_perm(int k);
 /* stempool (bf16, stempool.hip): out [B][Po][Po] rows of stride ldo (Po = S/4 for S % 4 == 0) =

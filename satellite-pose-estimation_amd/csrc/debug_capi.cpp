@@ -109,6 +109,18 @@ int spe_debug_btail(void* stream, const void* a, int lda, int k1, const void* r,
   return rc != 0 ? spe_fail(SPE_E_LAUNCH, "btail launch rejected its arguments") : 0;
 }
 
+int spe_debug_btail_n1(void* stream, const void* a, int lda, int k1, const void* r, const void* w3, int ld3,
+                       const float* b3, void* y, const void* w1p, int ld1, const float* b1, void* z, int n1, int n2,
+                       int M) {
+  if (!a || !w3 || !b3 || !y || !w1p || !b1 || !z || M < 0 || n1 <= 0) return spe_fail(SPE_E_ARG, "bad argument");
+  BtailArgs t{};
+  t.A = a; t.lda = lda; t.k1 = k1; t.R = r; t.ldr = n1;
+  t.w3 = w3; t.ld3 = ld3; t.b3 = b3; t.y = y; t.ldy = n1; t.n1 = n1;
+  t.w1 = w1p; t.ld1 = ld1; t.b1 = b1; t.z = z; t.ldz = n2; t.n2 = n2; t.M = M;
+  const int rc = spe_launch_btail(t, (hipStream_t)stream);
+  return rc != 0 ? spe_fail(SPE_E_LAUNCH, "btail launch rejected its arguments") : 0;
+}
+
 int spe_debug_btail_perm(int k) { return spe_btail_perm(k); }
 
 int spe_debug_stempool(void* stream, const void* x, const void* w, int ldw, const float* bias, void* out, int ldo,

@@ -231,7 +231,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   // when the next block carries permuted conv1 weights (layer-1 outputs, registry.cpp c1p)
   auto tail = [&](const Block& nb, const void* A, int lda, int k1, const void* R, const Conv& c3, size_t out, int M) {
     BtailArgs t{};
-    t.A = A; t.lda = lda; t.k1 = k1; t.R = R; t.ldr = 256;
+    t.A = A; t.lda = lda; t.k1 = k1; t.R = R; t.ldr = c3.N;
     t.w3 = c3.w; t.ld3 = c3.Kpad; t.b3 = c3.bias; t.y = P(out); t.ldy = c3.N; t.n1 = c3.N;
     t.w1 = nb.c1p.w; t.ld1 = nb.c1p.Kpad; t.b1 = nb.c1p.bias; t.z = P(w.t1); t.ldz = nb.c1.N; t.n2 = nb.c1.N;
     t.M = M;
@@ -287,7 +287,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
     }
     {  // conv3 1x1 + bn3 + residual + relu (+ the next block's conv1, btail.hip)
       int rc = 1;
-      if (nb && blk.c3.N == 256) {
+      if (nb) {
         rc = tail(*nb, P(w.t2), blk.c2.N, blk.c3.K, P(res), blk.c3, outbuf, B * Ho * Ho);
         if (rc != 0 && rc != 1) CK(rc);   // 1 = shapes not served: the GEMM pair below
       }

@@ -398,8 +398,11 @@ int build_device(spe_model* m) {
       // conv1 of the blocks whose input is a layer-1 block output (blocks 1-3: layer 1 blocks 1
       // and 2, layer 2 block 0) as the second product of the previous block's fused tail:
       // columns permuted into spe_btail_perm order (btail.hip)
+      // (layers 2 / 3: the split-N tail, btail.hip, for every block whose input is the previous
+      // block's output -- layer 2 blocks 1-3, layer 3 blocks 0-5)
       const int gi = li == 0 ? k : (li == 1 && k == 0 ? 3 : -1);
-      if (m->esz == 2 && spe_btail_enabled() && gi >= 1 && blk.c1.K == 256) {
+      const bool split = li >= 1 && !(li == 1 && k == 0) && spe_btail_split_enabled();
+      if (m->esz == 2 && spe_btail_enabled() && ((gi >= 1 && blk.c1.K == 256) || split)) {
         std::vector<float> w1, b1;
         fold_conv(m, p + ".conv1.weight", p + ".bn1", "", w1, b1);
         const int n = blk.c1.N, K = blk.c1.K;

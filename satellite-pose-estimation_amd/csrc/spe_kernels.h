@@ -56,10 +56,11 @@ __device__ __forceinline__ void conv_k_decode(int k, int Cin, int KW, int taps, 
   kw = tap - kh * KW;
 }
 // Bottleneck tail + next conv1 (btail.hip): y = relu(A . W3^T + b3 (+ R)), z = relu(y . W1p^T + b1)
-// with W1p's columns in spe_btail_perm order.  bf16, N1 = n1 = 256.
+// with W1p's columns in spe_btail_perm order.  bf16; N1 = n1 = 256 (layer 1), or the split-N
+// form for 512 / 1024 (layers 2 / 3, residual row stride ldr = n1).
 struct BtailArgs {
   const void* A; int lda; int k1;        // conv3 input [M][k1] (row stride lda)
-  const void* R; int ldr;                // residual [M][256] or null
+  const void* R; int ldr;                // residual [M][n1] or null
   const void* w3; int ld3; const float* b3;   // [256][ld3]
   void* y; int ldy; int n1;              // block output [M][256]
   const void* w1; int ld1; const float* b1;   // next conv1, permuted columns [n2][ld1]
@@ -69,6 +70,7 @@ struct BtailArgs {
 int spe_launch_btail(const BtailArgs& a, hipStream_t s);   // 1 = not applicable
 int spe_btail_perm(int k);
 bool spe_btail_enabled();
+bool spe_btail_split_enabled();
 int spe_launch_gemm2(const GemmArgs& g, int mode, hipStream_t s);   // 1 = not applicable
 int spe_launch_sgemm(const GemmArgs& g, int mode, hipStream_t s);   // 1 = not applicable
 int spe_launch_lnproj(const GemmArgs& g, hipStream_t s);             // 1 = not applicable (lnproj.hip)

@@ -351,6 +351,35 @@ def test_btail(gpu_device, M, k1, n2, res):
     _close(Z, zref, DT["bf16"][2])
 
 
+# split-N bottleneck tail (btail.hip, layers 2 and 3): y produced in column chunks with the
+# weights streamed through LDS; row counts off the 128-row block and the bench's sizes
+@pytest.mark.parametrize("M,k1,n1,n2", [(173056, 128, 512, 128), (1000, 128, 512, 128), (3001, 128, 512, 256),
+                                        (43264, 256, 1024, 256), (77, 256, 1024, 256)])
+def test_btail_split(gpu_device, M, k1, n1, n2):
+    L = _lib.lib()
+    dt = torch.bfloat16
+    g = torch.Generator(device="cpu").manual_seed(M + k1 + n1 + n2)
+    A = torch.randn(M, k1, generator=g).to(gpu_device, dt)
+    R = torch.randn(M, n1, generator=g).to(gpu_device, dt)
+    W3 = (torch.randn(n1, k1, generator=g) / k1 ** 0.5).to(gpu_device, dt)
+    b3 = (0.1 * torch.randn(n1, generator=g)).to(gpu_device)
+    W1 = (torch.randn(n2, n1, generator=g) / n1 ** 0.5).to(gpu_device, dt)
+    b1 = (0.1 * torch.randn(n2, generator=g)).to(gpu_device)
+    perm = torch.tensor([L.spe_debug_btail_perm(k) for k in range(n1)], device=gpu_device)
+    assert sorted(perm.tolist()) == list(range(n1))
+    W1p = W1[:, perm].contiguous()
+    Y = torch.full((M, n1), float("nan"), dtype=dt, device=gpu_device)
+    Z = torch.full((M, n2), float("nan"), dtype=dt, device=gpu_device)
+    rc = L.spe_debug_btail_n1(None, _p(A), k1, k1, _p(R), _p(W3), k1, _p(b3), _p(Y), _p(W1p), n1, _p(b1), _p(Z), n1,
+                              n2, M)
+    assert rc == 0, L.spe_last_error()
+    torch.cuda.synchronize()
+    yref = torch.relu(A.float() @ W3.float().t() + b3 + R.float())
+    _close(Y, yref, DT["bf16"][2])
+    zref = torch.relu(Y.float() @ W1.float().t() + b1)
+    _close(Z, zref, DT["bf16"][2])
+
+
 # the fused stem + bias + ReLU + max-pool (stempool.hip): the bench's 416^2 (one column group,
 # 15 waves), a small image, 640^2 (config 5: two column groups, an idle wave) and a strided
 # output row (the pool writes the right half of layer 1 block 0's [conv2 | pool] concatenation)
