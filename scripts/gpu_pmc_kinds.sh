@@ -7,7 +7,8 @@ export TMPDIR=/tmp
 D=gpurun_out/pmc_kinds
 mkdir -p $D
 for C in FETCH_SIZE WRITE_SIZE; do
-  timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $C --output-format csv -d $D/$C -o run -- \
+  timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $C --kernel-exclude-regex "Cijk|at::|rocprim|hipcub|rocclr" \
+    --output-format csv -d $D/$C -o run -- \
     python3 bench.py --steps 1 --warmup 1 --no-overlap --no-cpu-baseline --no-accuracy --no-parity \
     --launch-table $D/lt.json > $D/$C.log 2>&1 || { echo "pmc pass $C failed"; tail -5 $D/$C.log; exit 6; }
   find $D/$C -name "*kernel_trace*" -delete

@@ -19,7 +19,7 @@ import json
 import os
 from collections import defaultdict
 
-SKIP = ("pnp_", "score_kernel", "self_assess", "at::", "void at", "rocprim", "hipcub")
+SKIP = ("pnp_", "score_kernel", "self_assess", "at::", "void at", "rocprim", "hipcub", "__amd_rocclr", "Cijk")
 FAMILY = {"attn.enc": ("attn16",), "attn.dec_self": ("attn16",), "attn.dec_cross": ("xattn",),
           "ffn.enc": ("ffn_",), "ffn.dec": ("ffn_",)}
 
@@ -82,7 +82,7 @@ def main():
             r = res[rec["kind"]]
             r[key] += sum(v for _, _, v in grp) * scale
             for _, n, _ in grp:
-                r["kernels"].add(n.split("(")[0][:80])
+                r["kernels"].add(n.replace("void ", "").replace("(anonymous namespace)::", "").split("(")[0][:80])
     for rec in table:
         r = res[rec["kind"]]
         r["launches"] += 1
