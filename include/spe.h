@@ -278,7 +278,7 @@ int spe_debug_gemm(void* stream, int dtype, int mode, const void* A, int lda, co
 /* kernel family that served this thread's last gemm launch: 0 the 128x128 kernel, 1 the large-tile
  * kernels (gemm2.hip), 2 the persistent streaming kernel for short-K problems (gemm_stream.hip),
  * 3 the patch-staged 3x3 conv (pconv.hip), 4 the projection + residual + LayerNorm (lnproj.hip),
- * 5 the fp32x6 three-way split kernel (gemm.hip) */
+ * 5 the fp32x6 three-way split kernel (gemm.hip), 6 its LDS-DMA form (gemm.hip gemm_x6d) */
 int spe_debug_gemm_path(void);
 /* the same launch with the weights also given pre-split (dtype SPE_DTYPE_F32X6_): planes = bf16
  * [3][plane_rows][ldb] holding hi, mid, lo of Bw (what spe_model_finalize writes for fp32x6 models) */
@@ -286,6 +286,9 @@ int spe_debug_gemm_planes(void* stream, int dtype, int mode, const void* A, int 
                           int H, int W, int Cin, int KH, int KW, int stride, int pad, const void* Bw, int ldb, int M,
                           int N, int K, const float* bias, const void* R, int ldr, int act_code, void* C, int ldc,
                           const void* planes, int plane_rows);
+/* attention: dtype | 0x100 = V^T in the 16-bit DMA kernel's key order; dtype SPE_DTYPE_F32X3_ | 0x200 =
+ * k and vt given as bf16 hi planes ([B*Tk][ldk] and [B][H][32][Tk]), each followed by its lo plane
+ * (what the fp32x3 / fp32x6 models' projection epilogues write; Tk % 8 == 0) */
 int spe_debug_attention(void* stream, int dtype, const void* q, int ldq, const void* k, int ldk, const void* vt,
                         void* o, int ldo, int B, int H, int Tq, int Tk, float scale);
 int spe_debug_layernorm(void* stream, int dtype, const void* x, const float* gamma, const float* beta, void* out,

@@ -617,6 +617,10 @@ __global__ __launch_bounds__(NT, 2) void attn_f32_kernel(AttnArgs a) {
 // per tile as they are staged (the bf16 kernel's LDS images, one for hi and one for lo); q is
 // scaled into the exp2 domain in fp32 and split in registers; the probabilities stay fp32 for
 // the running max, the exp2 and the row sums, and are split only as the value-product operand.
+// PS (AttnArgs::presplit): K and V^T arrive as bf16 hi / lo planes written by the projection
+// epilogues (GemmArgs::S) -- the same RNE split, done once per element instead of once per
+// (element, query block) -- and are staged as plain 16-byte copies.
+template <bool PS>
 __global__ __launch_bounds__(NT, 2) void attn_x3_kernel(AttnArgs a) {
   constexpr int KB = KT * KROW, VB = 32 * VROW, SLOT = 2 * (KB + VB);   // [K hi | K lo | V hi | V lo]
   __shared__ __attribute__((aligned(16))) char smem[2 * SLOT];
@@ -661,8 +665,31 @@ __global__ __launch_bounds__(NT, 2) void attn_x3_kernel(AttnArgs a) {
   for (int r = 0; r < 16; ++r) { o[r] = 0.f; negm[r] = 0.f; }
   float m = 0.f, l = 0.f;
 
-  // staging: fp32 tiles through registers (Stage<float>), split into the hi / lo images
+  // staging: fp32 tiles through registers (Stage<float>), split into the hi / lo images; PS:
+  // one 16-byte K chunk (8 dims of a key) and one V^T chunk (8 keys of a d row) per plane
   Stage<float, KT> st;
+  u32x4 pk[2], pv[2];
+  const size_t klo = (size_t)a.B * a.Tk * a.ldk, vlo = (size_t)a.B * a.H * 32 * a.Tk;
+  auto load_ps = [&](int kt) {
+    const int key = kt * KT + (tid >> 2), c = tid & 3;
+    const bf16* kp = (const bf16*)a.k + (size_t)(b * a.Tk + (key < a.Tk ? key : 0)) * a.ldk + h * 32 + c * 8;
+    pk[0] = key < a.Tk ? ld16(kp) : u32x4{0, 0, 0, 0};
+    pk[1] = key < a.Tk ? ld16(kp + klo) : u32x4{0, 0, 0, 0};
+    const int d = tid >> 3, k0 = kt * KT + (tid & 7) * 8;
+    const bf16* vp = (const bf16*)a.vt + ((size_t)(b * a.H + h) * 32 + d) * a.Tk + (k0 < a.Tk ? k0 : 0);
+    pv[0] = k0 < a.Tk ? ld16(vp) : u32x4{0, 0, 0, 0};
+    pv[1] = k0 < a.Tk ? ld16(vp + vlo) : u32x4{0, 0, 0, 0};
+  };
+  auto store_ps = [&](char* sl) {
+    const int key = tid >> 2, c = tid & 3, d = tid >> 3, cv = tid & 7;
+    st16(sl + k_off_bf16(key, c), pk[0]);
+    st16(sl + KB + k_off_bf16(key, c), pk[1]);
+#pragma unroll
+    for (int p = 0; p < 2; ++p) {
+      st8(sl + 2 * KB + p * VB + v_quad_off(d, 2 * cv), u32x2{pv[p].x, pv[p].y});
+      st8(sl + 2 * KB + p * VB + v_quad_off(d, 2 * cv + 1), u32x2{pv[p].z, pv[p].w});
+    }
+  };
   auto store = [&](char* sl) {
     constexpr int KCPR = 8, VCPR = KT / 4;
 #pragma unroll
@@ -688,14 +715,22 @@ __global__ __launch_bounds__(NT, 2) void attn_x3_kernel(AttnArgs a) {
     }
   };
   const int ntiles = (a.Tk + KT - 1) / KT;
-  st.load(a, b, h, 0, tid);
-  store(smem);
+  if constexpr (PS) {
+    load_ps(0);
+    store_ps(smem);
+  } else {
+    st.load(a, b, h, 0, tid);
+    store(smem);
+  }
   __syncthreads();
   for (int kt = 0; kt < ntiles; ++kt) {
     const char* kl = smem + (kt & 1) * SLOT;
     const char* vl = kl + 2 * KB;
     const bool more = kt + 1 < ntiles;
-    if (more) st.load(a, b, h, kt + 1, tid);
+    if (more) {
+      if constexpr (PS) load_ps(kt + 1);
+      else st.load(a, b, h, kt + 1, tid);
+    }
     if (wave_live) {
       // (fragments read at their use: reading all 16 up front measured 1.85 vs 1.76 ms per
       // B = 64 launch -- 172 instead of 164 VGPRs, a wave per SIMD less)
@@ -764,7 +799,10 @@ __global__ __launch_bounds__(NT, 2) void attn_x3_kernel(AttnArgs a) {
         }
       }
     }
-    if (more) store(smem + ((kt + 1) & 1) * SLOT);
+    if (more) {
+      if constexpr (PS) store_ps(smem + ((kt + 1) & 1) * SLOT);
+      else store(smem + ((kt + 1) & 1) * SLOT);
+    }
     __syncthreads();
   }
 
@@ -786,6 +824,7 @@ int spe_launch_attention(const AttnArgs& a, int dtype, hipStream_t s) {
   if (a.B <= 0 || a.Tq <= 0 || a.Tk <= 0) return 0;
   const int ce = (dtype == SPE_DTYPE_F32 || dtype == SPE_DTYPE_F32X3) ? 4 : 8;
   if ((a.ldq % ce) || (a.ldk % ce) || (a.ldo % 4)) return -5;
+  if (a.presplit && (dtype != SPE_DTYPE_F32X3 || a.Tk % 8 || a.ldk % 8 || a.vt_swz)) return -5;
   dim3 grid(a.B * a.H * ((a.Tq + 127) / 128)), block(NT);
   if (a.vt_swz && (a.Tk % 16 || (dtype != SPE_DTYPE_F16 && dtype != SPE_DTYPE_BF16 && dtype != SPE_DTYPE_BF16_F16V)))
     return -5;                                     // (swizzled V^T: 16-bit operands, whole quads per row)
@@ -819,8 +858,10 @@ int spe_launch_attention(const AttnArgs& a, int dtype, hipStream_t s) {
       hipLaunchKernelGGL((attn16_kernel<0, bf16>), grid, block, 0, s, a);
     else
       hipLaunchKernelGGL((attn16_kernel<1, bf16>), grid, block, 0, s, a);
+  else if (dtype == SPE_DTYPE_F32X3 && a.presplit)
+    hipLaunchKernelGGL(attn_x3_kernel<true>, grid, block, 0, s, a);
   else if (dtype == SPE_DTYPE_F32X3)
-    hipLaunchKernelGGL(attn_x3_kernel, grid, block, 0, s, a);
+    hipLaunchKernelGGL(attn_x3_kernel<false>, grid, block, 0, s, a);
   else
     hipLaunchKernelGGL(attn_f32_kernel, grid, block, 0, s, a);
   return (int)hipGetLastError();

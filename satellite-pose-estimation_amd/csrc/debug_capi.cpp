@@ -57,6 +57,7 @@ int spe_debug_attention(void* stream, int dtype, const void* q, int ldq, const v
   a.q = q; a.ldq = ldq; a.k = k; a.ldk = ldk; a.vt = vt; a.o = o; a.ldo = ldo;
   a.B = B; a.H = H; a.Tq = Tq; a.Tk = Tk; a.scale = scale;
   a.vt_swz = (dtype >> 8) & 1;
+  a.presplit = (dtype >> 9) & 1;
   int rc = spe_launch_attention(a, dtype & 255, (hipStream_t)stream);
   return rc < 0 ? spe_fail(SPE_E_LAUNCH, "attention launch rejected its arguments") : rc;
 }

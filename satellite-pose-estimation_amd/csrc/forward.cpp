@@ -354,10 +354,16 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   // (vt_pos: the v projection's epilogue writes them so); SPE_ATTN_DMA=0 keeps register staging
   static const int dma_env = [] { const char* e = getenv("SPE_ATTN_DMA"); return e ? atoi(e) : 1; }();
   const int vt_swz = dma_env && dt == SPE_DTYPE_BF16 && T % 16 == 0;
+  // fp32x3 / fp32x6 encoder attention: the q/k and v projection epilogues write K and V^T as bf16
+  // hi / lo planes (GemmArgs::S) that the attention stages as plain copies (SPE_ATTN_PRESPLIT=0:
+  // fp32 K / V^T, split per tile inside the attention)
+  static const int ps_env = [] { const char* e = getenv("SPE_ATTN_PRESPLIT"); return e ? atoi(e) : 1; }();
+  const bool presplit = ps_env && w.kpl && x3_for(m, "attn.enc") && T % 8 == 0;
   for (const Enc& e : m->enc) {
     {
       GemmArgs g = linear_args(e.qk, P(w.src), d, Mt, P(w.qkv), 3 * d);
       g.out_f16 = f16attn;
+      if (presplit) { g.S = P(w.kpl); g.s_col0 = d; }
       const int mode = add_pos(m, g, m->pos, d, T, e.pos_qk, 2 * d);
       CK(run_gemm(m, "gemm.enc.qk", g, mode, s));
     }
@@ -365,12 +371,14 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       GemmArgs g = linear_args(e.v, P(w.src), d, Mt, P(w.vt), 8);
       g.vt_T = T; g.vt_B = B; g.vt_swz = vt_swz;
       g.out_f16 = f16attn || f16v;
+      if (presplit) g.S = P(w.vt);               // hi plane then lo plane, in the fp32 V^T's bytes
       CK(run_gemm(m, "gemm.enc.v", g, GEMM_LINEAR, s));
     }
     {
       AttnArgs a{};
       a.q = P(w.qkv); a.ldq = 3 * d;
-      a.k = (char*)P(w.qkv) + d * m->esz; a.ldk = 3 * d;
+      a.k = presplit ? P(w.kpl) : (char*)P(w.qkv) + d * m->esz; a.ldk = presplit ? d : 3 * d;
+      a.presplit = presplit;
       a.vt = P(w.vt); a.vt_swz = vt_swz;
       a.o = P(w.ao); a.ldo = d;
       a.B = B; a.H = c.nheads; a.Tq = T; a.Tk = T; a.scale = scale;

@@ -229,6 +229,30 @@ SPE_DEV void store_tile(const GemmArgs& g, const float* ct, int m0, int n0, int 
       for (int e = 0; e < 8; ++e) v[e] = ct[(rg + e) * EPI_LD + col] + bn;
       const int b = m / g.vt_T, tok = m - b * g.vt_T;
       const size_t rowbase = ((size_t)(grp * g.vt_B + b) * 256 + hd) * g.vt_T;
+      if constexpr (sizeof(T) == 4) {
+        if (g.S) {                               // bf16 hi / lo planes (fp32x3 attention operands)
+          const size_t lo = (size_t)g.vt_B * g.N * g.vt_T;
+          if ((g.vt_T & 7) == 0 && m + 8 <= g.M) {   // 8 consecutive tokens of one row: 16-byte stores
+            float hv[8], lv[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              hv[e] = to_f32(from_f32<bf16>(v[e]));
+              lv[e] = v[e] - hv[e];
+            }
+            st16((bf16*)g.S + rowbase + tok, pack16<bf16>(hv));
+            st16((bf16*)g.S + lo + rowbase + tok, pack16<bf16>(lv));
+            continue;
+          }
+          for (int e = 0; e < 8 && m + e < g.M; ++e) {
+            const int me = m + e, be = me / g.vt_T, te = me - be * g.vt_T;
+            const size_t idx = ((size_t)(grp * g.vt_B + be) * 256 + hd) * g.vt_T + te;
+            const bf16 h = from_f32<bf16>(v[e]);
+            ((bf16*)g.S)[idx] = h;
+            ((bf16*)g.S)[lo + idx] = from_f32<bf16>(v[e] - to_f32(h));
+          }
+          continue;
+        }
+      }
       if ((g.vt_T & 7) == 0 && m + 8 <= g.M) {
         char* cp = (char*)g.C + (rowbase + tok) * sizeof(T);
         if constexpr (sizeof(T) == 2) {
@@ -284,6 +308,29 @@ SPE_DEV void store_tile(const GemmArgs& g, const float* ct, int m0, int n0, int 
       for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], g.act);
     }
     if (g.R && g.res_post) add_res();
+    if constexpr (sizeof(T) == 4) {
+      if (g.S && n >= g.s_col0) {                // bf16 hi / lo planes (fp32x3 attention operands)
+        const int ns = g.N - g.s_col0;
+        bf16* hp = (bf16*)g.S + (size_t)m * ns + (n - g.s_col0);
+        bf16* lp = hp + (size_t)g.M * ns;
+        float hv[8], lv[8];
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          hv[e] = to_f32(from_f32<bf16>(v[e]));
+          lv[e] = v[e] - hv[e];
+        }
+        if (full) {
+          st16(hp, pack16<bf16>(hv));
+          st16(lp, pack16<bf16>(lv));
+        } else {
+          for (int e = 0; e < 8 && n + e < g.N; ++e) {
+            hp[e] = from_f32<bf16>(hv[e]);
+            lp[e] = from_f32<bf16>(lv[e]);
+          }
+        }
+        continue;
+      }
+    }
     if (g.out_f32) {
       float* cp = (float*)g.C + (size_t)m * g.ldc + n;
       if (full) {

@@ -45,6 +45,7 @@ struct Dec {
 struct Ws {                // workspace layout (byte offsets)
   size_t x0, stem, pool, bufA, bufB, t1, t2, ds, xs8, up, cat, neck;
   size_t src, srcpos, qkv, vt, ao, tmp, ffn, ck, cvt;
+  size_t kpl;                // fp32x3 / fp32x6: the encoder K as bf16 hi / lo planes (0 = none)
   size_t tgt, dtmp, dqkv, dvt, dao, dqc, dffn, dffnpart, hs;
   size_t xq, xu, xpm, xpl, xpu;           // cross-attention against the memory (xattn.hip)
   size_t total;

@@ -579,6 +579,7 @@ Ws spe_plan(const spe_model* m, int B) {
   w.srcpos = take((size_t)B * T * d * E);   // memory + pos (bf16 fused path: cross-attention K input)
   w.qkv = take((size_t)B * T * 3 * d * E);
   w.vt = take((size_t)B * T * d * E);
+  w.kpl = m->x3 ? take((size_t)B * T * d * 4) : 0;     // (offset 0 is bufA: nonzero = planes present)
   w.ao = take((size_t)B * T * d * E);
   w.tmp = take((size_t)B * T * d * E);
   w.ffn = take((size_t)B * T * ff * E);

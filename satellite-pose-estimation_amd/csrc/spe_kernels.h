@@ -32,6 +32,9 @@ struct GemmArgs {
   int r_period;                    // >0: residual row = m % r_period (row-periodic add, e.g. pos . W^T)
   const float* ln_g; const float* ln_b;   // optional fused post-norm LayerNorm over N == 256 (bf16, large M)
   const void* B6; int b6_rows;     // fp32x6: the weights pre-split into bf16 planes [3][b6_rows][ldb] (h, m, l), or null
+  void* S; int s_col0;             // fp32 models: columns n >= s_col0 stored instead as bf16 hi / lo planes for the
+                                   // fp32x3 attention: rows -> hi [M][N - s_col0] then lo; head-transposed
+                                   // (vt_T) -> hi in C's layout [vt_B][N][vt_T] then lo (s_col0 = 0)
 };
 bool spe_gemm_ln_fusable(const GemmArgs& g);   // the large-tile kernel can fuse ln_g/ln_b for g
 int spe_launch_gemm(const GemmArgs& g, int dtype, int mode, hipStream_t s);
@@ -96,6 +99,8 @@ struct AttnArgs {
   void* o; int ldo;                // output row b*Tq+i
   int B, H, Tq, Tk;
   float scale;                     // softmax scale (1/sqrt(head_dim))
+  int presplit;                    // fp32x3: k and vt are bf16 hi planes (k [B*Tk][ldk], vt [B][H][32][Tk]),
+                                   // each followed by its lo plane (GemmArgs::S); Tk % 8 == 0
 };
 int spe_launch_attention(const AttnArgs& a, int dtype, hipStream_t s);
 

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 T="timeout -k 10"
 $T 400 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_kernels.py tests/test_gpu_parity.py \
-   tests/test_gpu_precision.py -k "x3_close or x6_dma or forward_fp32 or precision or linear_epilogue or vt" > gpurun_out/f_tests.log 2>&1; rc=$?
+   tests/test_gpu_precision.py -k "x3_close or x6_dma or forward_fp32 or precision or linear_epilogue or vt or attention" > gpurun_out/f_tests.log 2>&1; rc=$?
 tail -2 gpurun_out/f_tests.log; [ $rc = 0 ] || { grep -E "^E |FAILED" gpurun_out/f_tests.log | head -20; exit $rc; }
 grep x6 gpurun_out/precision_floor.json
 $T 300 python -u scripts/x6_bench.py > gpurun_out/f_x6bench.log 2>&1; rc=$?; grep -v amdgpu.ids gpurun_out/f_x6bench.log; [ $rc = 0 ] || exit $rc

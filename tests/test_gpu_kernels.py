@@ -922,6 +922,34 @@ def test_gemm_x6_dma_close_to_fp64(gpu_device, case):
     assert err <= max(1e-6, 2 * e32), (err, e32)
 
 
+def _bf16_planes(x):
+    """fp32 tensor -> bf16 hi plane followed by its lo plane (RNE both), flattened."""
+    h = x.to(torch.bfloat16)
+    return torch.cat([h.reshape(-1), (x - h.float()).to(torch.bfloat16).reshape(-1)])
+
+
+@pytest.mark.parametrize("B,H,Tq,Tk", [(1, 8, 304, 336), (2, 8, 2704, 2704), (3, 8, 11, 2704)])
+def test_attention_x3_presplit_equals_in_kernel_split(gpu_device, B, H, Tq, Tk):
+    """K and V^T handed over as the bf16 hi / lo planes the projection epilogues write
+    (GemmArgs::S, AttnArgs::presplit): the same RNE split the kernel does per tile, so the
+    output is bit-identical to the fp32-operand launch."""
+    g = torch.Generator(device="cpu").manual_seed(Tq + Tk)
+    ld = H * 32
+    Q = (torch.randn(B * Tq, ld, generator=g) * 2).to(gpu_device)
+    K = (torch.randn(B * Tk, ld, generator=g) * 2).to(gpu_device)
+    VT = torch.randn(B, H, 32, Tk, generator=g).to(gpu_device)
+    Kp, VTp = _bf16_planes(K), _bf16_planes(VT)
+    O = torch.zeros(B * Tq, ld, device=gpu_device)
+    Op = torch.zeros_like(O)
+    L = _lib.lib()
+    assert L.spe_debug_attention(None, _lib.SPE_DTYPE_F32X3, _p(Q), ld, _p(K), ld, _p(VT), _p(O), ld, B, H, Tq, Tk,
+                                 32 ** -0.5) == 0
+    assert L.spe_debug_attention(None, _lib.SPE_DTYPE_F32X3 | 0x200, _p(Q), ld, _p(Kp), ld, _p(VTp), _p(Op), ld, B,
+                                 H, Tq, Tk, 32 ** -0.5) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(O, Op), (O - Op).abs().max().item()
+
+
 @pytest.mark.parametrize("B,H,Tq,Tk", [(1, 8, 300, 333), (2, 8, 2704, 2704), (3, 8, 11, 2704), (2, 8, 11, 11)])
 def test_attention_x3_close_to_fp64(gpu_device, B, H, Tq, Tk):
     g = torch.Generator(device="cpu").manual_seed(Tq * 3 + Tk)
