@@ -590,6 +590,9 @@ def main():
     if world != args.gpus:
         print(f"bench.py: --gpus {args.gpus} but the launch has world size {world}", file=sys.stderr)
         return 2
+    if os.environ.get("SPE_BENCH_SHARE_GPU") == "1":
+        # rehearsal of the N-rank path on fewer GPUs (with SPE_DIST_BACKEND=gloo): ranks share devices
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     cfg = SpeConfig(input_size=args.size, num_queries=args.queries, enc_layers=args.layers, dec_layers=args.layers,
@@ -647,7 +650,9 @@ def main():
     solver = build_solver(argparse.Namespace(solver=args.solver, repro=20))
     overlap = dict(overlap=not args.no_overlap,
                    overlap_decode=rcfg is None and not (args.no_overlap_decode or args.no_overlap),
-                   overlap_backbone=rcfg is None and not (args.no_overlap_backbone or args.no_overlap_decode or args.no_overlap))
+                   overlap_backbone=rcfg is None and not (args.no_overlap_backbone or args.no_overlap_decode or args.no_overlap),
+                   # SPE_CU_SPLIT = k: backbone / encoder streams on k/8 and (8-k)/8 of the CUs (PosePipeline)
+                   cu_split=int(os.environ.get("SPE_CU_SPLIT", "0")))
     jpeg_bytes = 0
     if args.raw_frames:
         from spe.synthetic import synthetic_frames

@@ -258,6 +258,13 @@ int spe_model_profile_end(spe_model* m);
 int spe_model_profile_get(const spe_model* m, int i, char* kind, int kind_len, double* ms, double* flops,
                           double* bytes);
 
+/* A HIP stream whose kernels may only use the CUs set in mask (words 32-bit words, bit i = CU i
+ * in the runtime's CU order; hipExtStreamCreateWithCUMask): PosePipeline's CU partition between
+ * the HBM-bound backbone and the MFMA/VALU-bound encoder (no reference counterpart).  destroy
+ * releases it. */
+int spe_stream_create_cu_mask(const uint32_t* mask, int words, void** stream);
+int spe_stream_destroy(void* stream);
+
 /* Kernel test hooks: launch one kernel family on caller buffers (tests/test_gpu_kernels.py).
  * gemm: C[M,N] = act(A . W^T + bias + R) with act = act_code & 255 (0 none, 1 ReLU, 2 SiLU, 3
  * exact GELU); bit 8 of act_code adds R after the activation instead; mode 0 linear (A[m*lda+k]), 1 linear + P[(m%prow)

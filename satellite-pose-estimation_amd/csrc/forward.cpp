@@ -5,6 +5,7 @@
 // may capture them into a hipGraph.  Every launch goes through run_gemm / run_attn / run_other,
 // which bracket it with HIP events when the per-launch profiler is on (bench roofline).
 #include <hip/hip_runtime.h>
+#include <hip/hip_ext.h>
 
 #include <cmath>
 #include <cstdio>
@@ -668,6 +669,21 @@ int spe_speed_score(void* stream, const float* quat, const double* tvec, const d
   if (!quat || !tvec || !q_gt || !t_gt || !s_t || !s_q || B < 0) return fail(SPE_E_ARG, "bad argument");
   CK(spe_launch_score(quat, tvec, q_gt, t_gt, B, s_t, s_q, (hipStream_t)stream));
   return 0;
+}
+
+int spe_stream_create_cu_mask(const uint32_t* mask, int words, void** stream) {
+  if (!mask || words <= 0 || !stream) return fail(SPE_E_ARG, "bad argument");
+  hipStream_t s = nullptr;
+  const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask);
+  if (e != hipSuccess) return fail((int)e, "hipExtStreamCreateWithCUMask failed");
+  *stream = s;
+  return 0;
+}
+
+int spe_stream_destroy(void* stream) {
+  if (!stream) return fail(SPE_E_ARG, "null stream");
+  const hipError_t e = hipStreamDestroy((hipStream_t)stream);
+  return e == hipSuccess ? 0 : fail((int)e, "hipStreamDestroy failed");
 }
 
 int spe_model_profile_begin(spe_model* m, const char* kind_prefix) {

@@ -25,7 +25,9 @@ def init_distributed_mode(backend=None):
     local = int(os.environ.get("LOCAL_RANK", 0))
     if not dist.is_initialized():
         if backend is None:
-            backend = "nccl" if torch.cuda.is_available() else "gloo"
+            # SPE_DIST_BACKEND=gloo: the rehearsal of the multi-rank path with every rank on one
+            # GPU (RCCL needs one device per rank)
+            backend = os.environ.get("SPE_DIST_BACKEND") or ("nccl" if torch.cuda.is_available() else "gloo")
         if backend == "nccl":
             torch.cuda.set_device(local)
         dist.init_process_group(backend=backend, init_method="env://", world_size=world, rank=rank)

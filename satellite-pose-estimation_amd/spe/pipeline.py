@@ -15,10 +15,21 @@ from .solver import PoseSolver
 from .speed_eval import device_speed_score
 
 
+def cu_partition(ncu: int, k: int):
+    """(backbone, encoder) CU masks as lists of 32-bit words: CU i goes to the backbone when
+    (i % 8 + i // 8) % 8 < k, i.e. k/8 of every run of 8 CUs and of every 8-strided set."""
+    words = (ncu + 31) // 32
+    bb, en = [0] * words, [0] * words
+    for i in range(ncu):
+        tgt = bb if (i % 8 + i // 8) % 8 < k else en
+        tgt[i // 32] |= 1 << (i % 32)
+    return bb, en
+
+
 class PosePipeline:
     def __init__(self, model: DETR, solver: PoseSolver, batch: int, device="cuda", use_graph: bool = False,
                  self_assess: bool = True, overlap: bool = False, raw_frames=None, overlap_decode: bool = False,
-                 jpeg_max_bytes: int = 0, overlap_backbone: bool = False):
+                 jpeg_max_bytes: int = 0, overlap_backbone: bool = False, cu_split: int = 0):
         self.model, self.solver, self.B = model, solver, batch
         self.self_assess = self_assess
         # overlap: the solver / score / self-assessment of batch i run on a second HIP stream
@@ -51,6 +62,28 @@ class PosePipeline:
         if self.overlap_decode:
             self.dec_stream = torch.cuda.Stream(device=device)
             self.enc_stream = torch.cuda.Stream(device=device) if self.overlap_backbone else None
+        # cu_split = k (1..7, with overlap_backbone): the backbone runs on its own stream limited to
+        # k/8 of the CUs and the encoder on a stream limited to the rest (spe_stream_create_cu_mask),
+        # so the HBM-bound convolutions and the MFMA/VALU-bound encoder layers hold fixed CU shares
+        # instead of alternating workgroup by workgroup.  CU i goes to the backbone when
+        # (i % 8 + i // 8) % 8 < k: k/8 of every run of 8 and of every 8-strided set, whichever way
+        # the runtime's CU order interleaves the XCDs.
+        self.bb_stream = None
+        if cu_split and self.overlap_backbone:
+            from . import _lib
+            import ctypes
+            ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
+            words = (ncu + 31) // 32
+
+            def masked(words_list):
+                m = (ctypes.c_uint32 * words)(*words_list)
+                h = ctypes.c_void_p()
+                _lib.check(_lib.lib().spe_stream_create_cu_mask(ctypes.cast(m, ctypes.c_void_p), words, ctypes.byref(h)),
+                           "spe_stream_create_cu_mask")
+                return torch.cuda.ExternalStream(h.value, device=self.device)
+            bbm, encm = cu_partition(ncu, cu_split)
+            self.bb_stream = masked(bbm)
+            self.enc_stream = masked(encm)
             self.nslot = 3 if self.overlap_backbone else 2
             # the staged slots own their workspaces: a direct model(...) call or another
             # pipeline on the same model never writes into a slot's encoder memory
@@ -120,9 +153,15 @@ class PosePipeline:
         self.slot_q[slot].copy_(self.q_gt)
         self.slot_t[slot].copy_(self.t_gt)
         if self.overlap_backbone:
-            self.model.encode(self.images, self.ws2[slot], stream=main, part="backbone")
+            bb = main
+            if self.bb_stream is not None:
+                bb = self.bb_stream
+                bb.wait_stream(main)
+            self.model.encode(self.images, self.ws2[slot], stream=bb, part="backbone")
+            if bb is not main:
+                main.wait_stream(bb)                  # the next load() overwrites what the backbone read
             e = self.enc_stream
-            e.wait_stream(main)
+            e.wait_stream(bb)
             with torch.cuda.stream(e):
                 self.model.encode(None, self.ws2[slot], stream=e, part="transformer", B=self.B)
         else:

@@ -271,3 +271,18 @@ def test_fit_point_head_with_logit_offset():
     z = np.maximum(z @ w["p.layers.1.weight"].T + w["p.layers.1.bias"], 0)
     pts = 1 / (1 + np.exp(-(z @ w["p.layers.2.weight"].T + w["p.layers.2.bias"] + off)))
     assert np.abs(pts - tgt).max() < 0.05 and err.max() < 0.05, (np.abs(pts - tgt).max(), err.max())
+
+
+def test_cu_partition_balanced_both_ways():
+    """PosePipeline(cu_split=k): the backbone mask holds k/8 of every run of 8 CUs and of every
+    8-strided set (either XCD interleave of the runtime's CU order), the encoder the rest."""
+    from spe.pipeline import cu_partition
+    ncu = 256
+    for k in (1, 2, 3, 4):
+        bb, en = cu_partition(ncu, k)
+        bits = lambda m: [i for i in range(ncu) if (m[i // 32] >> (i % 32)) & 1]
+        b, e = set(bits(bb)), set(bits(en))
+        assert not (b & e) and len(b | e) == ncu and len(b) == ncu * k // 8
+        for x in range(8):
+            assert sum(1 for i in b if i % 8 == x) == 32 * k // 8      # striped XCD order
+            assert sum(1 for i in b if i // 32 == x) == 32 * k // 8    # blocked XCD order
