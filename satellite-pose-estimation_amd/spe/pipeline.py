@@ -62,6 +62,18 @@ class PosePipeline:
         if self.overlap_decode:
             self.dec_stream = torch.cuda.Stream(device=device)
             self.enc_stream = torch.cuda.Stream(device=device) if self.overlap_backbone else None
+            self.nslot = 3 if self.overlap_backbone else 2
+            # the staged slots own their workspaces: a direct model(...) call or another
+            # pipeline on the same model never writes into a slot's encoder memory
+            self.ws2 = [model.new_workspace(batch, dev) for _ in range(self.nslot)]
+            # per-slot snapshots of what the later stages read (a load() for the next batch may
+            # overwrite the staging buffers while this batch's decoder / solver still run)
+            self.slot_clip = [torch.zeros(batch, 4, device=dev) for _ in range(self.nslot)]
+            self.slot_q = [torch.zeros(batch, 4, dtype=torch.float64, device=dev) for _ in range(self.nslot)]
+            self.slot_t = [torch.zeros(batch, 3, dtype=torch.float64, device=dev) for _ in range(self.nslot)]
+            self.dec_done = [None] * self.nslot
+            self.solve_done = [None] * self.nslot
+            self.calls = 0
         # cu_split = k (1..7, with overlap_backbone): the backbone runs on its own stream limited to
         # k/8 of the CUs and the encoder on a stream limited to the rest (spe_stream_create_cu_mask),
         # so the HBM-bound convolutions and the MFMA/VALU-bound encoder layers hold fixed CU shares
@@ -84,18 +96,6 @@ class PosePipeline:
             bbm, encm = cu_partition(ncu, cu_split)
             self.bb_stream = masked(bbm)
             self.enc_stream = masked(encm)
-            self.nslot = 3 if self.overlap_backbone else 2
-            # the staged slots own their workspaces: a direct model(...) call or another
-            # pipeline on the same model never writes into a slot's encoder memory
-            self.ws2 = [model.new_workspace(batch, dev) for _ in range(self.nslot)]
-            # per-slot snapshots of what the later stages read (a load() for the next batch may
-            # overwrite the staging buffers while this batch's decoder / solver still run)
-            self.slot_clip = [torch.zeros(batch, 4, device=dev) for _ in range(self.nslot)]
-            self.slot_q = [torch.zeros(batch, 4, dtype=torch.float64, device=dev) for _ in range(self.nslot)]
-            self.slot_t = [torch.zeros(batch, 3, dtype=torch.float64, device=dev) for _ in range(self.nslot)]
-            self.dec_done = [None] * self.nslot
-            self.solve_done = [None] * self.nslot
-            self.calls = 0
         # raw_frames = (H, W, C): each run() starts from uint8 frames + detector boxes resident in
         # HBM (load_frames) and runs the validation transform on the device first
         self.frames = self.bbox = self.transform = None
