@@ -41,7 +41,7 @@ __global__ __launch_bounds__(NT, 1) void btail_kernel(BtailArgs a, int row_tiles
 
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int fg = lane >> 4, fr = lane & 15;
-  // ---- weights -> LDS.  Row n, 16-byte chunk c at n*KB + (c/8)*128 + ((c%8)^(n%8))*16; one
+  // ---- weights -> LDS.  Row n, 16-byte chunk c at n*KB + (c ^ (n & wkey_mask(KB)))*16; one
   // direct-to-LDS wave instruction fills 1 KB linearly, the swizzle applied on the source.
   {
     constexpr int INS3 = N1 * KB1 / 1024, INS1 = N2 * KB2 / 1024;
@@ -50,7 +50,7 @@ __global__ __launch_bounds__(NT, 1) void btail_kernel(BtailArgs a, int row_tiles
       const int qq = first ? q : q - INS3, KB = first ? KB1 : KB2;
       const int o = qq * 1024 + lane * 16;
       const int n = o / KB, within = o - n * KB;
-      const int chunk = (within >> 7) * 8 + (((within >> 4) & 7) ^ (n & 7));
+      const int chunk = (within >> 4) ^ (n & wkey_mask(KB));
       const char* src = first ? (const char*)a.w3 + (size_t)n * a.ld3 * 2 + chunk * 16
                               : (const char*)a.w1 + (size_t)n * a.ld1 * 2 + chunk * 16;
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)((first ? w3s : w1s) + qq * 1024), 16, 0, 0);
@@ -60,7 +60,7 @@ __global__ __launch_bounds__(NT, 1) void btail_kernel(BtailArgs a, int row_tiles
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-  auto w_addr = [](int n, int chunk, int KB) { return n * KB + ((chunk >> 3) << 7) + (((chunk & 7) ^ (n & 7)) << 4); };
+  auto w_addr = [](int n, int chunk, int KB) { return wkey_addr(n, chunk, KB); };
 
   auto load_a = [&](int t, u32x4 (&x)[KF1]) {
     t = t < row_tiles ? t : row_tiles - 1;
@@ -202,7 +202,7 @@ __global__ __launch_bounds__(NT, 1) void btail_split_kernel(BtailArgs a, int row
   const int fg = lane >> 4, fr = lane & 15;
   for (int i = tid; i < N1; i += NT) sb3[i] = a.b3[i];
   for (int i = tid; i < N2; i += NT) sb1[i] = a.b1[i];
-  auto w_addr = [](int n, int chunk, int KB) { return n * KB + ((chunk >> 3) << 7) + (((chunk & 7) ^ (n & 7)) << 4); };
+  auto w_addr = [](int n, int chunk, int KB) { return wkey_addr(n, chunk, KB); };
   // chunk c of both weights -> stage st: 64 pieces of 1 KiB, 8 per wave (W3c then W1c, each a
   // linear LDS image per wave-instruction with the swizzle applied on the source)
   auto issue = [&](int c, int st) {
@@ -212,11 +212,11 @@ __global__ __launch_bounds__(NT, 1) void btail_split_kernel(BtailArgs a, int row
       const char* src;
       if (o < W3C) {
         const int n = o / KB1, within = o - n * KB1;
-        const int ch = (within >> 7) * 8 + (((within >> 4) & 7) ^ (n & 7));
+        const int ch = (within >> 4) ^ (n & wkey_mask(KB1));
         src = (const char*)a.w3 + (size_t)(c * NC + n) * a.ld3 * 2 + ch * 16;
       } else {
         const int o2 = o - W3C, n = o2 / KBC, within = o2 - n * KBC;
-        const int ch = (within >> 7) * 8 + (((within >> 4) & 7) ^ (n & 7));
+        const int ch = (within >> 4) ^ (n & wkey_mask(KBC));
         src = (const char*)a.w1 + (size_t)n * a.ld1 * 2 + (size_t)c * NC * 2 + ch * 16;
       }
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(wst + st * STG + q * 1024), 16, 0, 0);

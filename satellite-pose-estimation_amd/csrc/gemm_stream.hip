@@ -73,14 +73,14 @@ __global__ __launch_bounds__(256, OCC) void sgemm_kernel(GemmArgs g, int ns_coun
   const int wstride = (G / ns_count) * NW;           // row tiles advanced per step of one wave
   int rt = (gid / ns_count) * NW + wid;               // this wave's first row tile
 
-  // ---- W slice -> LDS.  Row n, 16-byte chunk c (of K/8) at n*KB + (c/8)*128 + ((c%8)^(n%8))*16.
+  // ---- W slice -> LDS.  Row n, 16-byte chunk c (of K/8) at n*KB + (c ^ (n & wkey_mask(KB)))*16.
   // One direct-to-LDS wave instruction fills 1 KB linearly; the swizzle is applied on the source.
   {
     constexpr int INS = BN * KB / 1024;
     for (int q = wid; q < INS; q += NW) {
       const int o = q * 1024 + lane * 16;
       const int n = o / KB, within = o - n * KB;
-      const int chunk = (within >> 7) * 8 + (((within >> 4) & 7) ^ (n & 7));
+      const int chunk = (within >> 4) ^ (n & wkey_mask(KB));
       const int nn = n0 + n < g.N ? n0 + n : g.N - 1;     // (N % BN == 0 on every launch)
       const char* src = (const char*)g.B + (size_t)nn * g.ldb * 2 + chunk * 16;
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(wl + q * 1024), 16, 0, 0);
@@ -95,7 +95,7 @@ __global__ __launch_bounds__(256, OCC) void sgemm_kernel(GemmArgs g, int ns_coun
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-  auto w_addr = [&](int n, int chunk) { return n * KB + ((chunk >> 3) << 7) + (((chunk & 7) ^ (n & 7)) << 4); };
+  auto w_addr = [&](int n, int chunk) { return wkey_addr(n, chunk, KB); };
 
   // A fragments of one row tile: lane (fg, fr) holds row fr of fragment rf, K chunk 4kf + fg
   auto load_a = [&](int t, u32x4 (&a)[RF][KF]) {

@@ -24,12 +24,12 @@ __global__ __launch_bounds__(NT, 1) void lnproj_kernel(GemmArgs g, int row_tiles
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int fg = lane >> 4, fr = lane & 15;
   {
-    // W -> LDS: row n, 16-byte chunk c at n*KB + (c/8)*128 + ((c%8)^(n%8))*16 (swizzle on the source)
+    // W -> LDS: row n, 16-byte chunk c at n*KB + (c ^ (n & wkey_mask(KB)))*16 (swizzle on the source)
     constexpr int INS = D * KB / 1024;
     for (int q = wid; q < INS; q += NW) {
       const int o = q * 1024 + lane * 16;
       const int n = o / KB, within = o - n * KB;
-      const int chunk = (within >> 7) * 8 + (((within >> 4) & 7) ^ (n & 7));
+      const int chunk = (within >> 4) ^ (n & wkey_mask(KB));
       __builtin_amdgcn_global_load_lds((const void*)((const char*)g.B + (size_t)n * g.ldb * 2 + chunk * 16),
                                        (lds_ptr_t)(wl + q * 1024), 16, 0, 0);
     }
@@ -41,7 +41,7 @@ __global__ __launch_bounds__(NT, 1) void lnproj_kernel(GemmArgs g, int row_tiles
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
   }
-  auto w_addr = [](int n, int chunk) { return n * KB + ((chunk >> 3) << 7) + (((chunk & 7) ^ (n & 7)) << 4); };
+  auto w_addr = [](int n, int chunk) { return wkey_addr(n, chunk, KB); };
 
   auto load = [&](int t, u32x4 (&x)[KF], u32x2 (&r)[JF]) {
     t = t < row_tiles ? t : row_tiles - 1;
@@ -55,11 +55,12 @@ __global__ __launch_bounds__(NT, 1) void lnproj_kernel(GemmArgs g, int row_tiles
     for (int j = 0; j < JF; ++j) r[j] = ld8(pr + j * 32);
   };
 
-  // W fragment bases: row 16j+fr, chunk 4kf+fg lives at wb[kf&1][j>>3] + (j&7)*8192 + (kf>>1)*128 (all
-  // immediates); the bases are opaque to the compiler so it cannot re-derive one address register per (j, kf).
-  int wb[2][2];
+  // W fragment bases: row 16j+fr, chunk 4kf+fg lives at wb[kf&3][j>>3] + (j&7)*8192 + (kf>>2)*256 (the
+  // key n & 15 = fr touches the chunk's low 4 bits only; the rest are immediates); the bases are
+  // opaque to the compiler so it cannot re-derive one address register per (j, kf).
+  int wb[4][2];
 #pragma unroll
-  for (int p = 0; p < 2; ++p)
+  for (int p = 0; p < 4; ++p)
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       wb[p][h] = w_addr(fr + 128 * h, 4 * p + fg);
@@ -77,7 +78,7 @@ __global__ __launch_bounds__(NT, 1) void lnproj_kernel(GemmArgs g, int row_tiles
 #pragma unroll
       for (int j = 0; j < JF; ++j)
         acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-            __builtin_bit_cast(bf16x8, ld16(wl + wb[kf & 1][j >> 3] + (j & 7) * 8192 + (kf >> 1) * 128)), av, acc[j], 0, 0, 0);
+            __builtin_bit_cast(bf16x8, ld16(wl + wb[kf & 3][j >> 3] + (j & 7) * 8192 + (kf >> 2) * 256)), av, acc[j], 0, 0, 0);
     }
     // lane: row m = fr, columns 16j + 4fg + e
     float s = 0.f;

@@ -121,3 +121,12 @@ SPE_DEV float apply_act(float v, int act) {
   if (act == 3) return 0.5f * v * (1.f + erff(v * 0.7071067811865476f));
   return v;
 }
+
+// LDS weight images of KB-byte rows read as 16x16x32 bf16 fragments (lane -> row 16j + (lane & 15),
+// 16-byte chunk 4kf + (lane >> 4)): chunk c of row n sits at slot c ^ (n & wkey_mask(KB)).  With
+// the mask min(KB/16, 16) - 1 the 16 lanes of every gfx950 ds_read_b128 lane group hit 16
+// distinct 16-byte bank groups for any KB >= 128; the older 128-byte-group form (chunk & 7) ^
+// (n & 7) left half of the banks unused for KB >= 256 (2-way conflicts: 28-45 % of the LDS
+// cycles of the bottleneck-tail kernels).
+SPE_DEV constexpr int wkey_mask(int KB) { return (KB / 16 < 16 ? KB / 16 : 16) - 1; }
+SPE_DEV constexpr int wkey_addr(int n, int chunk, int KB) { return n * KB + ((chunk ^ (n & wkey_mask(KB))) << 4); }

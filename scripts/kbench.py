@@ -134,6 +134,23 @@ def main():
             abytes = (B * H * W * Cin if conv else M * K) * 2
             byts = abytes + N * ldb * 2 + M * N * 2 + (0 if R is None else R.numel() * 2)
             print(f"{name:16s} {ms:.3f} ms  {2.0 * M * N * K / ms / 1e9:7.1f} TF/s  {byts / ms / 1e9:6.2f} TB/s")
+    if a.which in ("btail", "all"):
+        # the fused layer-1 bottleneck tail (btail.hip): conv3 (+ identity) + relu and the next
+        # conv1, the bench's three layer-1 shapes
+        M = B * 104 * 104
+        for k1, n2, res in ((64, 64, True), (64, 128, True), (128, 64, False)):
+            A = torch.randn(M, k1, generator=g).to(dev, torch.bfloat16)
+            R = torch.randn(M, 256, generator=g).to(dev, torch.bfloat16) if res else None
+            W3 = (torch.randn(256, 64 * ((k1 + 63) // 64), generator=g) / k1 ** 0.5).to(dev, torch.bfloat16)
+            W1 = (torch.randn(n2, 256, generator=g) / 16).to(dev, torch.bfloat16)
+            b3, b1 = torch.zeros(256, device=dev), torch.zeros(n2, device=dev)
+            Y = torch.empty(M, 256, dtype=torch.bfloat16, device=dev)
+            Z = torch.empty(M, n2, dtype=torch.bfloat16, device=dev)
+            fn = lambda: L.spe_debug_btail(None, p(A), k1, k1, p(R) if R is not None else None, p(W3), W3.shape[1], p(b3), p(Y), p(W1), 256, p(b1),
+                                           p(Z), n2, M)
+            ms = timeit(fn, a.iters)
+            byts = M * (k1 + 256 + n2 + (256 if res else 0)) * 2
+            print(f"btail k1={k1} n2={n2} res={int(res)}  {ms:.3f} ms  {byts / ms / 1e9:6.2f} TB/s")
 
 
 if __name__ == "__main__":
