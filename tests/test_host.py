@@ -286,3 +286,34 @@ def test_cu_partition_balanced_both_ways():
         for x in range(8):
             assert sum(1 for i in b if i % 8 == x) == 32 * k // 8      # striped XCD order
             assert sum(1 for i in b if i // 32 == x) == 32 * k // 8    # blocked XCD order
+
+
+@pytest.mark.parametrize("decode,backbone", [(False, False), (True, False), (True, True)])
+def test_pipeline_staged_state_without_gpu(monkeypatch, decode, backbone):
+    """PosePipeline's constructor on the CPU (HIP streams stubbed): the staged forms own their
+    slot workspaces, snapshots and counters (a regression once left them under an unrelated
+    branch, and only the GPU pipeline tests noticed)."""
+    from types import SimpleNamespace
+    import spe.pipeline as pp
+
+    class _Stream:
+        def __init__(self, device=None):
+            self.device = device
+    monkeypatch.setattr(pp.torch.cuda, "Stream", _Stream)
+
+    class _Model:
+        cfg = SimpleNamespace(input_size=32, num_queries=11)
+
+        def workspace(self, B, dev):
+            pass
+
+        def new_workspace(self, B, dev):
+            return torch.zeros(1)
+    p = pp.PosePipeline(_Model(), None, 2, device="cpu", overlap_decode=decode, overlap_backbone=backbone)
+    assert p.bb_stream is None
+    if decode:
+        n = 3 if backbone else 2
+        assert p.nslot == n and p.calls == 0 and len(p.ws2) == n and len(p.slot_clip) == n
+        assert (p.enc_stream is not None) == backbone and p.dec_stream is not None
+    else:
+        assert not hasattr(p, "ws2")
