@@ -548,7 +548,10 @@ def time_mode(pipe, model, args, world, dev, dtype, attn_dtype, cfg, B, launch_t
         achieved = (k_by / max(k_n, 1)) / (avg_ms * 1e-3) / 1e9
         peak, unit = PEAK["hbm"], "GB/s"
     prof_ms = tot[dominant][0] / max(tot[dominant][1], 1)
-    symbol = ({"fp32": "attn_f32_kernel", "fp32x3": "attn_x3_kernel", "fp32x6": "attn_x3_kernel"}[dtype]
+    # (fp32x3 / fp32x6: attn_x3_kernel<true>, K / V^T pre-split by the projections, unless
+    # SPE_ATTN_PRESPLIT=0)
+    ps = "<true>" if os.environ.get("SPE_ATTN_PRESPLIT", "1") != "0" else "<false>"
+    symbol = ({"fp32": "attn_f32_kernel", "fp32x3": "attn_x3_kernel" + ps, "fp32x6": "attn_x3_kernel" + ps}[dtype]
               if dominant == "attn.enc" and dtype != "bf16" else
               KIND_SYMBOL.get(dominant, dominant).replace("DF16b", "DF16_" if attn_dtype == "fp16" else "DF16b"))
     roofline = {"kernel": dominant, "kernel_symbol": symbol,
