@@ -18,7 +18,7 @@
 extern "C" {
 #endif
 
-#define SPE_ABI_VERSION 5
+#define SPE_ABI_VERSION 6
 
 enum {
   SPE_E_ARG = -1,        /* bad argument / size */
@@ -307,13 +307,15 @@ int spe_debug_ffn(void* stream, const void* x, int ldx, const void* w1, int ld1,
                   int ld2, const float* b2, const float* gamma, const float* beta, void* y, int ldy, int M, int D,
                   int F, float* partial, int splits);
 /* xattn (bf16 only, the decoder cross-attention against the memory): for image b, query q and
- * head h, u[b*Q+q][h*256 .. +256] = softmax_t(q'[b*Q+q][h*256 ..] . k[b*T+t]) . v[b*T+t] with the
- * scores already in the exp2 domain.  k, v: rows b*T+t of 256.  wv non-null ([256][256] bf16,
- * bv fp32): o[b*Q+q][h*32 + j] = wv[h*32 + j] . u_h + bv[h*32 + j] is written instead of u.
- * splits <= 0 picks the launch's own key split; partial_scratch: fp32, splits * B * 8Q * 258. */
+ * head h, u[b*Q+q][h*256 .. +256] = softmax_t(q'[b*Q+q][h*256 ..] . K_t) . v[b*T+t] with the
+ * scores already in the exp2 domain; K_t = k[b*T+t] (k_shared 0) or v[b*T+t] + k[t] (k_shared 1:
+ * k is the positional table [T] shared by all images, the model's mode).  k, v rows of 256.  wv
+ * non-null ([256][256] bf16, bv fp32): o[b*Q+q][h*32 + j] = wv[h*32 + j] . u_h + bv[h*32 + j] is
+ * written instead of u.  splits <= 0 picks the launch's own key split; partial_scratch: fp32,
+ * splits * B * 8Q * 258.  (ABI 6: k_shared added.) */
 int spe_debug_xattn(void* stream, const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* u,
                     int ldu, const void* wv, const float* bv, void* o, int ldo, int B, int Q, int T, int splits,
-                    float* partial_scratch);
+                    float* partial_scratch, int k_shared);
 /* upconv (bf16 models' neck, replaces the upsample + conv pair of REV/models/backbone.py:141
  * s16_latern(up16sto8s(xs16))): z [B*H*W][9*C] holds the per-tap products W_t . x at the low
  * resolution (t = kh*3 + kw); out [B][2H][2W] rows of stride ldo receive conv3x3(pad 1) of the
@@ -334,6 +336,13 @@ int spe_debug_btail(void* stream, const void* a, int lda, int k1, const void* r,
 int spe_debug_btail_n1(void* stream, const void* a, int lda, int k1, const void* r, const void* w3, int ld3,
                        const float* b3, void* y, const void* w1p, int ld1, const float* b1, void* z, int n1, int n2,
                        int M);
+/* decsa (bf16 only, the decoder self-attention block, decsa.hip): in place over tgt [B*Q][ldt],
+ * per image b: tgt = LayerNorm(tgt + MHA(q = k = tgt + query_pos, v = tgt) . wo^T + bo) with
+ * 8 heads of 32 (d = 256), q|k = tgt . wqk^T + bqk + qpos ([Q][512] bf16, query_pos . wqk^T),
+ * v = tgt . wv^T + bv, LayerNorm gamma g / beta b (eps 1e-5).  Q <= 64; weights bf16 rows. */
+int spe_debug_decsa(void* stream, void* tgt, int ldt, int B, int Q, const void* wqk, int ldqk, const float* bqk,
+                    const void* wv, int ldv, const float* bv, const void* qpos, const void* wo, int ldo,
+                    const float* bo, const float* g, const float* b, float scale);
 /* the K-column order btail's second product expects: stored column k holds channel perm(k) */
 int spe_debug_btail_perm(int k);
 /* stempool (bf16, stempool.hip): out [B][Po][Po] rows of stride ldo (Po = S/4 for S % 4 == 0) =

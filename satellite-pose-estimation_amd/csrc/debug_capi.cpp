@@ -87,8 +87,9 @@ int spe_debug_upconv(void* stream, int dtype, const void* z, void* out, int ldo,
 
 int spe_debug_xattn(void* stream, const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* u,
                     int ldu, const void* wv, const float* bv, void* o, int ldo, int B, int Q, int T, int splits,
-                    float* partial_scratch) {
+                    float* partial_scratch, int k_shared) {
   XattnArgs a{};
+  a.k_shared = k_shared ? 1 : 0;
   a.q = q; a.ldq = ldq; a.k = k; a.ldk = ldk; a.v = v; a.ldv = ldv; a.u = u; a.ldu = ldu;
   a.wv = wv; a.bv = bv; a.o = o; a.ldo = ldo;
   a.B = B; a.Q = Q; a.T = T; a.splits = splits > 0 ? splits : spe_xattn_splits(B, Q, T);
@@ -108,6 +109,17 @@ int spe_debug_btail(void* stream, const void* a, int lda, int k1, const void* r,
   t.w1 = w1p; t.ld1 = ld1; t.b1 = b1; t.z = z; t.ldz = n2; t.n2 = n2; t.M = M;
   const int rc = spe_launch_btail(t, (hipStream_t)stream);
   return rc != 0 ? spe_fail(SPE_E_LAUNCH, "btail launch rejected its arguments") : 0;
+}
+
+int spe_debug_decsa(void* stream, void* tgt, int ldt, int B, int Q, const void* wqk, int ldqk, const float* bqk,
+                    const void* wv, int ldv, const float* bv, const void* qpos, const void* wo, int ldo,
+                    const float* bo, const float* g, const float* b, float scale) {
+  DecSaArgs a{};
+  a.tgt = tgt; a.ldt = ldt; a.B = B; a.Q = Q;
+  a.wqk = wqk; a.ldqk = ldqk; a.bqk = bqk; a.wv = wv; a.ldv = ldv; a.bv = bv; a.qpos = qpos;
+  a.wo = wo; a.ldo = ldo; a.bo = bo; a.g = g; a.b = b; a.scale = scale;
+  const int rc = spe_launch_decsa(a, (hipStream_t)stream);
+  return rc != 0 ? spe_fail(SPE_E_LAUNCH, "decsa launch rejected its arguments") : 0;
 }
 
 int spe_debug_btail_n1(void* stream, const void* a, int lda, int k1, const void* r, const void* w3, int ld3,

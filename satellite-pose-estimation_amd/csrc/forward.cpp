@@ -191,6 +191,9 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   const float scale = 1.0f / std::sqrt(32.0f);
   const int Mt = B * T;
   const bool xa = spe_use_xattn(m);
+  // xattn reads pos (shared by all images, L2-resident) instead of a materialised memory + pos;
+  // SPE_XATTN_SHARED=0 restores the latter for A/B runs
+  static const bool xshared = [] { const char* e = getenv("SPE_XATTN_SHARED"); return e ? atoi(e) != 0 : true; }();
   if (stages & SPE_STAGE_BACKBONE) {
   // ---------------- backbone (REV/models/backbone.py:133-149)
   const bool pairs = m->stem.Cin == 4;                 // bf16: pair-packed stem (registry.cpp)
@@ -399,7 +402,8 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       }
     }
     if (use_fused_ffn(m)) {
-      const bool last = &e == &m->enc.back();     // last layer also emits memory + pos
+      // the last layer also emits memory + pos for the cross-K projection (xattn adds pos itself)
+      const bool last = &e == &m->enc.back() && !(xa && xshared);
       CK(run_ffn(m, "ffn.enc", e.l1, e.l2, e.n2g, e.n2b, P(w.src), Mt, s, last ? m->pos : nullptr,
                  last ? P(w.srcpos) : nullptr, T));
     } else {
@@ -443,8 +447,39 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   // batch i+1's backbone with two workspaces)
   const int Mq = B * Q;
   CK((int)hipMemsetAsync(P(w.tgt), 0, (size_t)Mq * d * m->esz, s));
+  // tgt = LayerNorm(tgt + dao . W^T + b) (REV/models/transformer.py:227-228, 233-234): bf16 models
+  // run it as one lnproj launch in place over tgt, the others as GEMM + LayerNorm
+  auto dec_proj_ln = [&](const Conv& wo, const float* lg, const float* lb) -> int {
+    GemmArgs g = linear_args(wo, P(w.dao), d, Mq, P(w.dtmp), d);
+    g.R = P(w.tgt); g.ldr = d;
+    GemmArgs gf = g;
+    gf.C = P(w.tgt); gf.ln_g = lg; gf.ln_b = lb;
+    if (m->esz == 2 && spe_lnproj_applies(gf)) {
+      CK(run_gemm(m, "gemm.dec.o", gf, GEMM_LINEAR, s));
+      return 0;
+    }
+    CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR, s));
+    CK(run_other(m, "ln.dec", 0.0, (double)Mq * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.dtmp), lg, lb, P(w.tgt), nullptr, Mq, d, dt, s); }));
+    return 0;
+  };
+  // bf16: the self-attention block (projections, attention, out-projection, norm1) as one
+  // launch per layer (decsa.hip); SPE_DECSA=0 runs the separate launches for A/B runs
+  static const bool decsa_on = [] { const char* e = getenv("SPE_DECSA"); return e ? atoi(e) != 0 : true; }();
   for (int l = 0; l < L; ++l) {
     const Dec& e = m->dec[l];
+    const bool sa_fused = decsa_on && m->esz == 2 && d == 256 && c.nheads == 8 && Q <= 64 && e.qpos_sqk;
+    if (sa_fused) {
+      DecSaArgs sa{};
+      sa.tgt = P(w.tgt); sa.ldt = d; sa.B = B; sa.Q = Q;
+      sa.wqk = e.sqk.w; sa.ldqk = e.sqk.Kpad; sa.bqk = e.sqk.bias;
+      sa.wv = e.sv.w; sa.ldv = e.sv.Kpad; sa.bv = e.sv.bias;
+      sa.qpos = e.qpos_sqk;
+      sa.wo = e.so.w; sa.ldo = e.so.Kpad; sa.bo = e.so.bias;
+      sa.g = e.n1g; sa.b = e.n1b; sa.scale = scale;
+      const double fl = 2.0 * Mq * d * (4.0 * d) + 4.0 * B * 8.0 * Q * Q * 32;
+      const double by = 2.0 * Mq * d * m->esz + 4.0 * d * d * m->esz;
+      CK(run_other(m, "dec.self", fl, by, s, [&] { return spe_launch_decsa(sa, s); }));
+    } else {
     {
       GemmArgs g = linear_args(e.sqk, P(w.tgt), d, Mq, P(w.dqkv), 3 * d);
       const int mode = add_pos(m, g, m->qpos, d, Q, e.qpos_sqk, 2 * d);
@@ -464,12 +499,8 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       a.B = B; a.H = c.nheads; a.Tq = Q; a.Tk = Q; a.scale = scale;
       CK(run_attn(m, "attn.dec_self", a, dt, s));
     }
-    {
-      GemmArgs g = linear_args(e.so, P(w.dao), d, Mq, P(w.dtmp), d);
-      g.R = P(w.tgt); g.ldr = d;
-      CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR, s));
+    CK(dec_proj_ln(e.so, e.n1g, e.n1b));
     }
-    CK(run_other(m, "ln.dec", 0.0, (double)Mq * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.dtmp), e.n1g, e.n1b, P(w.tgt), nullptr, Mq, d, dt, s); }));
     if (xa) {
       // q' = (tgt + query_pos) . Wqk^T + bqk: the query-side fold of Wq and Wk (xattn.hip)
       GemmArgs g = linear_args(e.xq, P(w.tgt), d, Mq, P(w.xq), 8 * d);
@@ -477,7 +508,8 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR, s));
       XattnArgs x{};
       x.q = P(w.xq); x.ldq = 8 * d;
-      x.k = P(w.srcpos); x.ldk = d;
+      if (xshared) { x.k = m->pos; x.ldk = d; x.k_shared = 1; }   // K = memory + pos: pos from L2, not HBM
+      else { x.k = P(w.srcpos); x.ldk = d; }
       x.v = P(w.src); x.ldv = d;
       x.wv = e.xv.w; x.bv = e.xv.bias;
       x.o = P(w.dao); x.ldo = d;
@@ -502,12 +534,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       CK(run_attn(m, "attn.dec_cross", a, dt, s));
     }
     }
-    {
-      GemmArgs g = linear_args(e.co, P(w.dao), d, Mq, P(w.dtmp), d);
-      g.R = P(w.tgt); g.ldr = d;
-      CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR, s));
-    }
-    CK(run_other(m, "ln.dec", 0.0, (double)Mq * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.dtmp), e.n2g, e.n2b, P(w.tgt), nullptr, Mq, d, dt, s); }));
+    CK(dec_proj_ln(e.co, e.n2g, e.n2b));
     if (use_fused_ffn(m)) {
       CK(run_ffn(m, "ffn.dec", e.l1, e.l2, e.n3g, e.n3b, P(w.tgt), Mq, s, nullptr, nullptr, 0,
                  (float*)P(w.dffnpart)));

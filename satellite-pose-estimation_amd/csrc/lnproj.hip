@@ -11,6 +11,7 @@
 #include "spe_common.h"
 #include "spe_kernels.h"
 
+#include <algorithm>
 #include <cstdlib>
 
 namespace {
@@ -149,7 +150,10 @@ bool spe_lnproj_applies(const GemmArgs& g) {
 int spe_launch_lnproj(const GemmArgs& g, hipStream_t s) {
   if (!spe_lnproj_applies(g)) return 1;
   const int row_tiles = (g.M + 15) / 16;
-  hipLaunchKernelGGL(lnproj_kernel, dim3(spe_cu_count()), dim3(NT), 0, s, g, row_tiles);
+  // one workgroup per CU, but no more than the tiles need (each workgroup stages all of W first:
+  // the decoder's 704-row launches take 6 workgroups, not 256 that would load W and exit)
+  const int grid = std::min(spe_cu_count(), (row_tiles + NW - 1) / NW);
+  hipLaunchKernelGGL(lnproj_kernel, dim3(grid), dim3(NT), 0, s, g, row_tiles);
   spe_gemm_last_path = 4;
   return (int)hipGetLastError();
 }

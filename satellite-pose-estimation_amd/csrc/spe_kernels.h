@@ -109,16 +109,31 @@ int spe_launch_attention(const AttnArgs& a, int dtype, hipStream_t s);
 // pos [T][256], V = memory [T][256], q' pre-scaled into the exp2 domain.
 struct XattnArgs {
   const void* q; int ldq;          // q' rows b*Q + q, head h at columns [h*256, h*256 + 256)
-  const void* k; int ldk;          // memory + pos, rows b*T + t
+  const void* k; int ldk;          // memory + pos, rows b*T + t; k_shared: pos, rows t (K = v + k)
   const void* v; int ldv;          // memory, rows b*T + t
   void* u; int ldu;                // output rows b*Q + q, head h at columns [h*256, h*256 + 256)
   const void* wv; const float* bv; // optional: o_h = Wv_h u_h + bv_h written instead of u
   void* o; int ldo;                //   o rows b*Q + q, head h at columns [h*32, h*32 + 32)
   int B, Q, T, splits, tiles_per_split;
   float *pm, *pl, *pu;             // key-split partials [B][splits][8Q] (pu: x 256), required
+  int k_shared;                    // 1: k holds pos [T][256], the same for every image
 };
 int spe_xattn_splits(int B, int Q, int T);
 int spe_launch_xattn(const XattnArgs& a, hipStream_t s);
+
+// Decoder self-attention block (bf16 only, decsa.hip), one workgroup per image, in place over tgt:
+// tgt = LN(tgt + SelfAttn(q = k = tgt + qpos, v = tgt) . Wo^T + bo), 8 heads of 32, d = 256.
+struct DecSaArgs {
+  void* tgt; int ldt;              // [B*Q][ldt] bf16
+  int B, Q;                        // Q <= 64
+  const void* wqk; int ldqk; const float* bqk;   // in_proj rows 0..511 [512][ldqk] bf16, bias fp32
+  const void* wv; int ldv; const float* bv;      // in_proj rows 512..767
+  const void* qpos;                // [Q][512] bf16: query_pos . Wqk^T
+  const void* wo; int ldo; const float* bo;      // out_proj [256][ldo]
+  const float* g; const float* b;  // norm1
+  float scale;                     // 1/sqrt(head_dim)
+};
+int spe_launch_decsa(const DecSaArgs& a, hipStream_t s);   // 1 = not applicable
 
 // Fused FFN + residual + LayerNorm (bf16 only): y = LN(x + W2 relu(W1 x + b1) + b2).
 // x / y may alias (each block reads and writes only its own rows).

@@ -26,6 +26,12 @@
 //   accumulator's) and V^T read transposed out of the row-major V tile by ds_read_b64_tr_b16
 //   in that same key order.
 // Each key split writes fp32 partials (m, l, unnormalised U) that a merge kernel combines.
+//
+// KS (k_shared, the model's mode): the key operand is memory + pos with pos [T][256] the same for
+// every image, so the kernel streams only the memory from HBM (the V tile, used twice) and the
+// shared pos rows (L2-resident across the batch's images), and forms the scores as
+// q' . mem + q' . pos in one fp32 MFMA chain -- half the HBM bytes of reading a materialised
+// memory + pos, and no bf16 rounding of that sum.
 #include "spe_common.h"
 #include "spe_kernels.h"
 
@@ -50,16 +56,24 @@ SPE_DEV void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memor
 
 // K tile: chunk c of key row k at slot c ^ (k & 15) (the 16 keys of a ds_read_b128 lane group
 // hit distinct bank groups).  V tile: chunk c at slot c ^ ((k & 3) << 2), so the four key rows
-// of every ds_read_b64_tr_b16 block fall in four different 64-byte bank segments.
-SPE_DEV int k_off(int key, int c) { return key * 512 + ((c ^ (key & 15)) << 4); }
-SPE_DEV int v_off(int key, int c) { return key * 512 + ((c ^ ((key & 3) << 2)) << 4); }
+// of every ds_read_b64_tr_b16 block fall in four different 64-byte bank segments.  KS: both
+// tiles at c ^ f(k), f(k) = (k & 3) << 2 | (k >> 2) & 3 -- a bijection on 16 consecutive keys
+// (ds_read_b128: distinct bank groups) that also puts the four key rows of every
+// ds_read_b64_tr_b16 block (k0 % 4 == 0, chunk pair c0, c0 + 1 with c0 even) on four different
+// 32-byte pairs of one 128-byte window, so the memory tile serves the score reads and the
+// transposed value reads alike.
+template <bool KS> SPE_DEV int kkey(int key) { return KS ? ((key & 3) << 2) | ((key >> 2) & 3) : key & 15; }
+template <bool KS> SPE_DEV int vkey(int key) { return KS ? ((key & 3) << 2) | ((key >> 2) & 3) : (key & 3) << 2; }
+template <bool KS> SPE_DEV int k_off(int key, int c) { return key * 512 + ((c ^ kkey<KS>(key)) << 4); }
+template <bool KS> SPE_DEV int v_off(int key, int c) { return key * 512 + ((c ^ vkey<KS>(key)) << 4); }
 
 // 4 keys x 16 dims of the V tile, delivered transposed: lane i of each 16-lane group gets dim
 // d0 + i of keys k0 .. k0+3 (cdna_hip_programming.md T10); lane 4q+p addresses key k0+q, dims
 // d0 + 4p .. +3 (d0 % 16 == 0).  LDS byte address of this lane's block row:
+template <bool KS>
 SPE_DEV uint32_t v_tr_addr(uint32_t vbase, int k0, int d0, int lane16) {
   const int q = lane16 >> 2, p = lane16 & 3;
-  return vbase + v_off(k0 + q, (d0 >> 3) + (p >> 1)) + 8 * (p & 1);
+  return vbase + v_off<KS>(k0 + q, (d0 >> 3) + (p >> 1)) + 8 * (p & 1);
 }
 // Issued as inline asm: the compiler treats the ds_read_b64_tr_b16 builtin as aliasing the
 // tiles still in flight by LDS-DMA and drains them (vmcnt(0)) before it; the waits for these
@@ -70,6 +84,7 @@ SPE_DEV u32x2 ds_read_tr(uint32_t addr) {
   return r;
 }
 
+template <bool KS>
 __global__ __launch_bounds__(NT, 1) void xattn_kernel(XattnArgs a) {
   __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -101,8 +116,8 @@ __global__ __launch_bounds__(NT, 1) void xattn_kernel(XattnArgs a) {
       qf[ks] = __builtin_bit_cast(bf16x8, live ? ld16(qp + 16 * ks + 8 * hh) : u32x4{0, 0, 0, 0});
   }
 
-  // ---- staging (loader waves): wave 6 the K tile, wave 7 the V tile, 16 x 1 KB each (2 key
-  // rows per instruction)
+  // ---- staging (loader waves): wave 6 the K tile (KS: the shared pos rows), wave 7 the V tile,
+  // 16 x 1 KB each (2 key rows per instruction)
   const char* zero = reinterpret_cast<const char*>(g_xzero);
   const bool isv = wid == 7;
   const char* src0 = isv ? (const char*)a.v : (const char*)a.k;
@@ -113,8 +128,9 @@ __global__ __launch_bounds__(NT, 1) void xattn_kernel(XattnArgs a) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int key = 2 * i + (lane >> 5), s = lane & 31;
-      const int c = isv ? s ^ ((key & 3) << 2) : s ^ (key & 15);
-      const char* src = key0 + key < a.T ? src0 + ((size_t)(b * a.T + key0 + key) * ldsrc + c * 8) * 2 : zero;
+      const int c = s ^ (isv ? vkey<KS>(key) : kkey<KS>(key));
+      const int row = (KS && !isv ? 0 : b * a.T) + key0 + key;
+      const char* src = key0 + key < a.T ? src0 + ((size_t)row * ldsrc + c * 8) * 2 : zero;
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(st + i * 1024), 16, 0, 0);
     }
   };
@@ -160,16 +176,24 @@ __global__ __launch_bounds__(NT, 1) void xattn_kernel(XattnArgs a) {
     const char* vl = kl + KTILE;
 
     // S^T - m: lane (row r32, hh) register r <-> key (r & 3) + 8 (r >> 2) + 4 hh
+    // (KS: the V tile's memory rows, then the pos rows, into the same two chains)
     f32x16 sa, sb;
 #pragma unroll
     for (int ks = 0; ks < 16; ks += 2) {
-      const bf16x8 k0 = __builtin_bit_cast(bf16x8, ld16(kl + k_off(r32, 2 * ks + hh)));
-      const bf16x8 k1 = __builtin_bit_cast(bf16x8, ld16(kl + k_off(r32, 2 * ks + 2 + hh)));
+      const char* t0 = KS ? vl : kl;
+      const bf16x8 k0 = __builtin_bit_cast(bf16x8, ld16(t0 + k_off<KS>(r32, 2 * ks + hh)));
+      const bf16x8 k1 = __builtin_bit_cast(bf16x8, ld16(t0 + k_off<KS>(r32, 2 * ks + 2 + hh)));
       sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf[ks], ks == 0 ? negm : sa, 0, 0, 0);
       if (ks == 0) {
         sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[ks + 1], f32x16{}, 0, 0, 0);
       } else {
         sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[ks + 1], sb, 0, 0, 0);
+      }
+      if constexpr (KS) {
+        const bf16x8 p0 = __builtin_bit_cast(bf16x8, ld16(kl + k_off<KS>(r32, 2 * ks + hh)));
+        const bf16x8 p1 = __builtin_bit_cast(bf16x8, ld16(kl + k_off<KS>(r32, 2 * ks + 2 + hh)));
+        sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p0, qf[ks], sa, 0, 0, 0);
+        sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p1, qf[ks + 1], sb, 0, 0, 0);
       }
     }
     f32x16 s = sa + sb;
@@ -224,8 +248,8 @@ __global__ __launch_bounds__(NT, 1) void xattn_kernel(XattnArgs a) {
     auto read_v = [&](u32x2 (&r)[4], int db) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        r[2 * ks] = ds_read_tr(v_tr_addr(vbase, 16 * ks + 4 * hh, 128 * dh + 32 * db + dg, l16));
-        r[2 * ks + 1] = ds_read_tr(v_tr_addr(vbase, 16 * ks + 8 + 4 * hh, 128 * dh + 32 * db + dg, l16));
+        r[2 * ks] = ds_read_tr(v_tr_addr<KS>(vbase, 16 * ks + 4 * hh, 128 * dh + 32 * db + dg, l16));
+        r[2 * ks + 1] = ds_read_tr(v_tr_addr<KS>(vbase, 16 * ks + 8 + 4 * hh, 128 * dh + 32 * db + dg, l16));
       }
     };
     read_v(vr[0], 0);
@@ -377,7 +401,8 @@ int spe_launch_xattn(const XattnArgs& a0, hipStream_t s) {
   a.splits = (ntiles + a.tiles_per_split - 1) / a.tiles_per_split;   // no empty split (<= requested)
   if (!a.pm || !a.pl || !a.pu || (a.wv ? !a.o || !a.bv || a.ldo % 2 : !a.u)) return -5;
   const int groups = (8 * a.Q + RG - 1) / RG;
-  hipLaunchKernelGGL(xattn_kernel, dim3(a.B * a.splits * groups), dim3(NT), 0, s, a);
+  if (a.k_shared) hipLaunchKernelGGL(xattn_kernel<true>, dim3(a.B * a.splits * groups), dim3(NT), 0, s, a);
+  else hipLaunchKernelGGL(xattn_kernel<false>, dim3(a.B * a.splits * groups), dim3(NT), 0, s, a);
   if (a.wv)
     hipLaunchKernelGGL(xattn_merge_wv_kernel, dim3((a.B * a.Q + MR - 1) / MR, 8), dim3(256), 0, s, a);
   else

@@ -41,7 +41,7 @@ EXPORTS = ["spe_abi_version", "spe_last_error", "spe_model_create", "spe_model_d
            "spe_model_num_params", "spe_model_param_name", "spe_model_finalize", "spe_model_workspace_bytes",
            "spe_forward", "spe_forward_stages", "spe_preprocess", "spe_criterion", "spe_ensemble_fuse", "spe_postprocess", "spe_pnp_batch", "spe_self_assess", "spe_speed_score", "spe_model_profile_begin",
            "spe_model_profile_end", "spe_model_profile_get", "spe_stream_create_cu_mask", "spe_stream_destroy", "spe_debug_gemm", "spe_debug_gemm_path", "spe_debug_gemm_planes", "spe_debug_attention",
-           "spe_debug_layernorm", "spe_debug_ffn", "spe_debug_xattn", "spe_debug_upconv", "spe_debug_btail", "spe_debug_btail_n1", "spe_debug_btail_perm", "spe_debug_stempool", "spe_rtdetr_create", "spe_rtdetr_forward",
+           "spe_debug_layernorm", "spe_debug_ffn", "spe_debug_xattn", "spe_debug_upconv", "spe_debug_btail", "spe_debug_btail_n1", "spe_debug_decsa", "spe_debug_btail_perm", "spe_debug_stempool", "spe_rtdetr_create", "spe_rtdetr_forward",
            "spe_jpeg_workspace_bytes", "spe_jpeg_decode"]
 
 
@@ -114,11 +114,12 @@ def lib():
     L.spe_debug_attention.argtypes = [P, I, P, I, P, I, P, P, I, I, I, I, I, F]
     L.spe_debug_layernorm.argtypes = [P, I, P, P, P, P, P, I, I]
     L.spe_debug_ffn.argtypes = [P, P, I, P, I, P, P, I, P, P, P, P, I, I, I, I, P, I]
-    L.spe_debug_xattn.argtypes = [P, P, I, P, I, P, I, P, I, P, P, P, I, I, I, I, I, P]
+    L.spe_debug_xattn.argtypes = [P, P, I, P, I, P, I, P, I, P, P, P, I, I, I, I, I, P, I]
     L.spe_debug_upconv.argtypes = [P, I, P, P, I, I, I, I, I]
     if hasattr(L, "spe_debug_btail"):          # (absent from older kernel A/B builds, SPE_LIB_PATH)
         L.spe_debug_btail.argtypes = [P, P, I, I, P, P, I, P, P, P, I, P, P, I, I]
         L.spe_debug_btail_perm.argtypes = [I]
+    L.spe_debug_decsa.argtypes = [P, P, I, I, I, P, I, P, P, I, P, P, P, I, P, P, P, ctypes.c_float]
     if hasattr(L, "spe_debug_btail_n1"):
         L.spe_debug_btail_n1.argtypes = [P, P, I, I, P, P, I, P, P, P, I, P, P, I, I, I]
     if hasattr(L, "spe_debug_stempool"):
@@ -128,7 +129,7 @@ def lib():
     L.spe_jpeg_workspace_bytes.argtypes = [I, I, I, I64]
     L.spe_jpeg_workspace_bytes.restype = I64
     L.spe_jpeg_decode.argtypes = [P, P, P, P, I, I, I, I64, P, P, P, I64]
-    if L.spe_abi_version() != 5:
+    if L.spe_abi_version() != 6:
         raise ImportError("libspe.so ABI version mismatch")
     _lib = L
     return L

@@ -73,6 +73,25 @@ def main():
         ms = timeit(fn, a.iters)
         fl = 4.0 * B * T * D * F
         print(f"ffn.enc   {ms:.3f} ms  {fl / ms / 1e9:.1f} TF/s")
+    if a.which in ("ffndec", "all"):
+        # the decoder's few-row FFN (M = B * 11): split-F partials over `splits` workgroups per
+        # 128-row tile, then the reduce + LayerNorm kernel
+        M = B * 11
+        x = torch.randn(M, D, generator=g).to(dev, torch.bfloat16)
+        w1 = (torch.randn(F, D, generator=g) / 16).to(dev, torch.bfloat16)
+        w2 = (torch.randn(D, F, generator=g) / 45).to(dev, torch.bfloat16)
+        b1, b2 = torch.zeros(F, device=dev), torch.zeros(D, device=dev)
+        gm, bt = torch.ones(D, device=dev), torch.zeros(D, device=dev)
+        y = torch.empty_like(x)
+        part = torch.empty(64 * M * D, device=dev)
+        for sp in (1, 2, 4, 8, 16, 32, 64):
+            fn = lambda: L.spe_debug_ffn(None, p(x), D, p(w1), D, p(b1), p(w2), F, p(b2), p(gm), p(bt), p(y), D,
+                                         M, D, F, p(part) if sp > 1 else None, sp)
+            if fn() != 0:
+                print(f"ffn.dec splits={sp}: rejected")
+                continue
+            ms = timeit(fn, a.iters)
+            print(f"ffn.dec M={M} splits={sp}: {ms * 1e3:.1f} us")
     if a.which in ("xattn", "all"):
         Q = 11
         q = (torch.randn(B * Q, 8 * D, generator=g) / 16).to(dev, torch.bfloat16)
@@ -85,13 +104,18 @@ def main():
         part = torch.empty(256 * B * 8 * Q * 258, device=dev)
         for sp in (0, 2, 8):
             fn = lambda: L.spe_debug_xattn(None, p(q), 8 * D, p(k), D, p(v), D, None, 0, p(wv), p(bv), p(o), D,
-                                           B, Q, T, sp, p(part))
+                                           B, Q, T, sp, p(part), 0)
             ms = timeit(fn, a.iters)
             fn_u = lambda: L.spe_debug_xattn(None, p(q), 8 * D, p(k), D, p(v), D, p(u), 8 * D, None, None, None,
-                                             0, B, Q, T, sp, p(part))
+                                             0, B, Q, T, sp, p(part), 0)
             ms_u = timeit(fn_u, a.iters)
             byts = 2 * B * T * D * 2                      # K and V reads
             print(f"xattn splits={sp}: {ms:.3f} ms with Wv, {ms_u:.3f} ms u only ({byts / ms_u / 1e9:.2f} TB/s)")
+            # the model's mode: K = V + pos, pos [T] shared (HBM: V only)
+            fn_s = lambda: L.spe_debug_xattn(None, p(q), 8 * D, p(k), D, p(v), D, None, 0, p(wv), p(bv), p(o), D,
+                                             B, Q, T, sp, p(part), 1)
+            ms_s = timeit(fn_s, a.iters)
+            print(f"xattn k_shared splits={sp}: {ms_s:.3f} ms with Wv ({B * T * D * 2 / ms_s / 1e9:.2f} TB/s of V)")
     if a.which in ("gemm", "all"):
         # name, mode, M, N, K, residual rows (0 none, -1 full, >0 period), conv geometry
         cases = [("l1.c3 1x1+res", 0, B * 104 * 104, 256, 64, -1, None),

@@ -646,19 +646,25 @@ def test_fused_ffn(gpu_device, M, F, inplace, splits):
         assert (y[:, D:] == 7.0).all()                 # nothing written past D
 
 
+@pytest.mark.parametrize("shared", [0, 1], ids=["k_rows", "k_shared_pos"])
 @pytest.mark.parametrize("B,Q,T,splits,amp", [(3, 11, 200, 1, 1.0), (2, 11, 203, 3, 1.0), (1, 17, 136, 2, 1.0),
                                               (2, 11, 2704, 0, 1.0), (2, 5, 640, 4, 12.0), (64, 11, 2704, 0, 1.0)])
-def test_cross_attention_memory(gpu_device, B, Q, T, splits, amp):
+def test_cross_attention_memory(gpu_device, B, Q, T, splits, amp, shared):
     """decoder cross-attention against the memory (xattn.hip): u = softmax_2(q' . K^T) . V per
     (image, query, head) row, against torch fp32 on the same bf16 operands.  amp = 12 spreads the
     scores over ~100 log2 units (many lazy-rescale branches taken, split partials merged far apart).
+    shared = 1 is the model's mode: K_t = V_t + pos_t with one pos table [T] for every image (the
+    reference's key = memory + pos, REV/models/transformer.py:230-233), summed in fp32 here.
     Tolerance: P is rounded to bf16 (2^-9 relative) before the value product; 1e-2 * scale."""
     dt, D = torch.bfloat16, 256
     g = torch.Generator(device="cpu").manual_seed(B * T + Q)
     ldq, ldv = 8 * D + 8, D + 8
     q = (torch.randn(B * Q, ldq, generator=g) * amp / 16).to(gpu_device, dt)
-    k = torch.randn(B * T, D, generator=g).to(gpu_device, dt)
+    k = torch.randn((T if shared else B * T), D, generator=g).to(gpu_device, dt)
     v = torch.randn(B * T, ldv, generator=g).to(gpu_device, dt)          # strided rows
+    if shared:
+        k *= 0.5
+        v[:, :D] *= 0.5
     if amp > 1:
         k[5] *= 4                                           # one key far above the rest
     wv = (torch.randn(D, D, generator=g) / 16).to(gpu_device, dt)
@@ -669,14 +675,15 @@ def test_cross_attention_memory(gpu_device, B, Q, T, splits, amp):
     part = torch.empty(S * B * 8 * Q * 258, device=gpu_device)
     L = _lib.lib()
     rc = L.spe_debug_xattn(None, _p(q), ldq, _p(k), D, _p(v), ldv, _p(u), ldq, None, None, None, 0, B, Q, T,
-                           splits, _p(part))
+                           splits, _p(part), shared)
     assert rc == 0, L.spe_last_error()
     rc = L.spe_debug_xattn(None, _p(q), ldq, _p(k), D, _p(v), ldv, None, 0, _p(wv), _p(bv), _p(o), D + 8, B, Q,
-                           T, splits, _p(part))
+                           T, splits, _p(part), shared)
     assert rc == 0, L.spe_last_error()
     torch.cuda.synchronize()
     qh = q[:, :8 * D].float().view(B, Q * 8, D)
-    s = torch.einsum("brd,btd->brt", qh, k.float().view(B, T, D))
+    kk = v[:, :D].float().view(B, T, D) + k.float().view(1, T, D) if shared else k.float().view(B, T, D)
+    s = torch.einsum("brd,btd->brt", qh, kk)
     p = torch.softmax(s * 0.6931471805599453, dim=-1)
     ref = torch.einsum("brt,btd->brd", p, v[:, :D].float().view(B, T, D))   # [B][Q*8][D], rows q*8 + h
     _close(u[:, :8 * D], ref.reshape(B * Q, 8 * D), 1e-2)
@@ -685,6 +692,45 @@ def test_cross_attention_memory(gpu_device, B, Q, T, splits, amp):
     ref_o = torch.einsum("bqhn,hjn->bqhj", ref.view(B, Q, 8, D), wv.float().view(8, 32, D)) + bv.view(8, 32)
     _close(o[:, :D], ref_o.reshape(B * Q, D), 1e-2)
     assert (o[:, D:] == 7.0).all()
+
+
+@pytest.mark.parametrize("B,Q", [(3, 11), (2, 40), (1, 64), (4, 1), (0, 11)])
+def test_decoder_self_attention_block(gpu_device, B, Q):
+    """decsa.hip: tgt = LN(tgt + MHA(q = k = tgt + query_pos, v = tgt) . Wo^T + bo) in place, one
+    workgroup per image (REV/models/transformer.py:218-228, forward_post), against torch fp32 on
+    the same bf16 operands with the separate path's roundings (q/k/v and the attention output
+    stored as bf16).  Tolerance 2e-2 * scale (bf16 output, unit-variance rows after the norm)."""
+    dt, D, H = torch.bfloat16, 256, 8
+    g = torch.Generator(device="cpu").manual_seed(31 * B + Q)
+    ldt = D + 8
+    x = torch.randn(max(B, 1) * Q, ldt, generator=g)
+    wqk = (torch.randn(2 * D, D, generator=g) / 16).to(dt)
+    wv = (torch.randn(D, D, generator=g) / 16).to(dt)
+    wo = (torch.randn(D, D, generator=g) / 16).to(dt)
+    bqk, bv, bo = (torch.randn(n, generator=g) * 0.1 for n in (2 * D, D, D))
+    qpos = (torch.randn(Q, 2 * D, generator=g) * 0.5).to(dt)
+    gam, bet = 1 + 0.1 * torch.randn(D, generator=g), 0.1 * torch.randn(D, generator=g)
+    t = x.to(dt).to(gpu_device)
+    dev = lambda a: a.to(gpu_device).contiguous()          # noqa: E731
+    args = [dev(wqk), dev(bqk), dev(wv), dev(bv), dev(qpos), dev(wo), dev(bo), dev(gam), dev(bet)]
+    L = _lib.lib()
+    rc = L.spe_debug_decsa(None, _p(t), ldt, B, Q, _p(args[0]), D, _p(args[1]), _p(args[2]), D, _p(args[3]),
+                           _p(args[4]), _p(args[5]), D, _p(args[6]), _p(args[7]), _p(args[8]), 32 ** -0.5)
+    assert rc == 0, L.spe_last_error()
+    torch.cuda.synchronize()
+    if B == 0:
+        assert torch.equal(t.cpu(), x.to(dt))
+        return
+    r = lambda a: a.to(dt).float()                         # noqa: E731  (bf16 rounding)
+    xb = x[:, :D].to(dt).float()
+    qk = r(xb @ wqk.float().T + bqk + qpos.float().repeat(B, 1))
+    v = r(xb @ wv.float().T + bv)
+    q, k = qk[:, :D].view(B, Q, H, 32), qk[:, D:].view(B, Q, H, 32)
+    s = torch.einsum("bihc,bjhc->bhij", q * 32 ** -0.5, k)
+    o = r(torch.einsum("bhij,bjhc->bihc", torch.softmax(s, -1), v.view(B, Q, H, 32)).reshape(B * Q, D))
+    y = torch.nn.functional.layer_norm(o @ wo.float().T + bo + xb, (D,), gam, bet, 1e-5)
+    _close(t[:, :D].cpu(), y, 2e-2)
+    assert torch.equal(t[:, D:].cpu(), x[:, D:].to(dt))   # nothing written past D
 
 
 @pytest.mark.parametrize("dtype", ["bf16", "fp32"])
