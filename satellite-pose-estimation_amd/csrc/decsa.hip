@@ -12,28 +12,34 @@
 //      16x16x32 bf16 MFMAs in the C^T form D[n][m] = W[n] . x[m] (W fragments from L2/global,
 //      the x rows from LDS), stored to LDS as bf16 -- the rounding the separate path's GEMM
 //      output had.
-//   2. attention per (query, head) on the VALU in fp32: scores scaled by 1/sqrt(32), softmax
-//      (max pass, then exp-weighted sums of v), written over the query's own q slot as bf16.
+//   2. attention per (query, head) on the VALU in fp32, four lanes of 8 dims each: scores scaled
+//      by 1/sqrt(32), softmax (max pass, then exp-weighted sums of v), written over the query's
+//      own q slot as bf16 (the out-projection's W fragments are in flight meanwhile).
 //   3. out-projection the same way as 1., + bo + tgt (the residual as stored), fp32 rows to LDS,
 //      then the LayerNorm (one wave per row, 4 columns a lane) and the bf16 store of tgt.
 #include "spe_common.h"
 #include "spe_kernels.h"
 
+#include <cstdlib>
+
 namespace {
 
-constexpr int D = 256, NT = 256, QMAX = 64;
+constexpr int D = 256, NT = 512, NW = NT / 64, QMAX = 64;
 constexpr int XLD = D + 8;                 // x rows in LDS (bf16 elements): 528 B, conflict-free b128 reads
 constexpr int QKVLD = 3 * D + 8;           // q | k | v rows (bf16): 1552 B
 constexpr int YLD = D + 4;                 // fp32 rows before the LayerNorm
 
-// D^T tile (16 output columns n0.. x 16 rows m0..) += W[n0..][K] . x[m0..][K]^T over K = 256:
-// lane l: A = W row n0 + (l & 15), k 8 (l >> 4) .. +8 of each 32-wide step; B = x row m0 + (l & 15)
-SPE_DEV f32x4 tile_wx(const bf16* w, int ldw, int n0, const bf16* xs, int xld, int m0, int lane) {
+// W fragments of one 16-column tile (A operand of the C^T form): lane l holds row n0 + (l & 15),
+// k 8 (l >> 4) .. +8 of each of the 8 32-wide K steps.  All of a wave's tiles are fetched before
+// the first MFMA (the few rows give each tile only RT x 8 MFMAs: the L2 round trip is the cost).
+SPE_DEV void w_frags(u32x4 (&wf)[8], const bf16* w, int ldw, int n0, int lane) {
   const bf16* wp = w + (size_t)(n0 + (lane & 15)) * ldw + 8 * (lane >> 4);
-  const bf16* xp = xs + (m0 + (lane & 15)) * xld + 8 * (lane >> 4);
-  u32x4 wf[8];
 #pragma unroll
   for (int ks = 0; ks < 8; ++ks) wf[ks] = ld16(wp + 32 * ks);
+}
+// D^T tile (16 output columns x 16 rows m0..) = W . x[m0..]^T over K = 256; B = x row m0 + (l & 15)
+SPE_DEV f32x4 tile_wx(const u32x4 (&wf)[8], const bf16* xs, int xld, int m0, int lane) {
+  const bf16* xp = xs + (m0 + (lane & 15)) * xld + 8 * (lane >> 4);
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < 8; ++ks)
@@ -50,24 +56,43 @@ __global__ __launch_bounds__(NT) void decsa_kernel(DecSaArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int b = blockIdx.x, Q = a.Q, RT = (Q + 15) / 16;
   bf16* tg = (bf16*)a.tgt + (size_t)b * Q * a.ldt;
+  if (a.stop == 5) return;
 
+  // ---- 1. q | k | v: 48 column tiles of 16, 6 per wave (tile wid + 8 j); the W fragments are
+  // requested first, so their round trip overlaps the tgt rows' (which stage through LDS)
+  constexpr int CT1 = 3 * D / 16 / NW;
+  u32x4 wf1[CT1][8];
+  auto tile1 = [&](int j) { return wid + NW * j; };
+#pragma unroll
+  for (int j = 0; j < CT1; ++j) {
+    const int n0 = tile1(j) * 16;
+    const bool isv = n0 >= 2 * D;
+    w_frags(wf1[j], isv ? (const bf16*)a.wv : (const bf16*)a.wqk, isv ? a.ldv : a.ldqk, isv ? n0 - 2 * D : n0, lane);
+  }
   // tgt rows -> LDS (rows past Q zero)
   for (int i = tid; i < RT * 16 * (D / 8); i += NT) {
     const int r = i / (D / 8), c = i % (D / 8);
     st16(xs + r * XLD + 8 * c, r < Q ? ld16(tg + (size_t)r * a.ldt + 8 * c) : u32x4{0, 0, 0, 0});
   }
   __syncthreads();
-
-  // ---- 1. q | k | v: 48 column tiles of 16, 12 per wave
-  for (int ct = wid; ct < 3 * D / 16; ct += NT / 64) {
-    const int n0 = ct * 16;
+  if (a.stop == 4) {                            // (timing: the loads only; keep them live)
+    u32x4 x = {0, 0, 0, 0};
+#pragma unroll
+    for (int j = 0; j < CT1; ++j)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) x ^= wf1[j][k];
+    if (x.x == 0x12345678u) st16(xs, x);
+    return;
+  }
+#pragma unroll
+  for (int j = 0; j < CT1; ++j) {
+    const int n0 = tile1(j) * 16;
     const bool isv = n0 >= 2 * D;
-    const bf16* w = isv ? (const bf16*)a.wv : (const bf16*)a.wqk;
-    const int ldw = isv ? a.ldv : a.ldqk, nw = isv ? n0 - 2 * D : n0;
+    const int nw = isv ? n0 - 2 * D : n0;
     const int ncol = n0 + 4 * (lane >> 4);
     const f32x4 bias = *reinterpret_cast<const f32x4*>((isv ? a.bv : a.bqk) + nw + 4 * (lane >> 4));
     for (int rt = 0; rt < RT; ++rt) {
-      f32x4 acc = tile_wx(w, ldw, nw, xs, XLD, rt * 16, lane);
+      f32x4 acc = tile_wx(wf1[j], xs, XLD, rt * 16, lane);
       const int m = rt * 16 + (lane & 15);
       float o[4];
 #pragma unroll
@@ -80,63 +105,64 @@ __global__ __launch_bounds__(NT) void decsa_kernel(DecSaArgs a) {
       st8(qkv + m * QKVLD + ncol, u32x2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])});
     }
   }
+  if (a.stop == 1) return;
+  // the out-projection's W fragments travel during the attention
+  constexpr int CT3 = D / 16 / NW;
+  u32x4 wf3[CT3][8];
+#pragma unroll
+  for (int j = 0; j < CT3; ++j) w_frags(wf3[j], (const bf16*)a.wo, a.ldo, (wid * CT3 + j) * 16, lane);
   __syncthreads();
 
-  // ---- 2. attention, one thread per (query i, head h); o_ih overwrites q_ih (only this thread reads it)
-  for (int idx = tid; idx < 8 * Q; idx += NT) {
-    const int i = idx >> 3, h = idx & 7;
-    float q[32];
+  // ---- 2. attention: four lanes per (query i, head h), 8 of the head's 32 dims each (the score's
+  // partial dot products summed over the four lanes); o_ih overwrites the lane's own q dims
+  for (int idx = tid; idx < 32 * Q; idx += NT) {
+    const int c = idx & 3, h = (idx >> 2) & 7, i = idx >> 5;
+    const int col = h * 32 + 8 * c;
+    float q[8];
+    unpack16<bf16>(ld16(qkv + i * QKVLD + col), q);
 #pragma unroll
-    for (int c = 0; c < 4; ++c) unpack16<bf16>(ld16(qkv + i * QKVLD + h * 32 + 8 * c), q + 8 * c);
-#pragma unroll
-    for (int e = 0; e < 32; ++e) q[e] *= a.scale;
+    for (int e = 0; e < 8; ++e) q[e] *= a.scale;
     auto score = [&](int j) {
-      const bf16* kp = qkv + j * QKVLD + D + h * 32;
+      float k[8];
+      unpack16<bf16>(ld16(qkv + j * QKVLD + D + col), k);
       float s = 0.f;
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        float k[8];
-        unpack16<bf16>(ld16(kp + 8 * c), k);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) s = fmaf(q[8 * c + e], k[e], s);
-      }
-      return s;
+      for (int e = 0; e < 8; ++e) s = fmaf(q[e], k[e], s);
+      // sum over the lane quad: DPP quad_perm [1,0,3,2] then [2,3,0,1] (no LDS round trip)
+      s += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0xB1, 0xF, 0xF, false));
+      return s + __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(s), 0x4E, 0xF, 0xF, false));
     };
     float mx = -INFINITY;
     for (int j = 0; j < Q; ++j) mx = fmaxf(mx, score(j));
-    float o[32], l = 0.f;
+    float o[8], l = 0.f;
 #pragma unroll
-    for (int e = 0; e < 32; ++e) o[e] = 0.f;
+    for (int e = 0; e < 8; ++e) o[e] = 0.f;
     for (int j = 0; j < Q; ++j) {
       const float p = expf(score(j) - mx);
       l += p;
-      const bf16* vp = qkv + j * QKVLD + 2 * D + h * 32;
+      float v[8];
+      unpack16<bf16>(ld16(qkv + j * QKVLD + 2 * D + col), v);
 #pragma unroll
-      for (int c = 0; c < 4; ++c) {
-        float v[8];
-        unpack16<bf16>(ld16(vp + 8 * c), v);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[8 * c + e] = fmaf(p, v[e], o[8 * c + e]);
-      }
+      for (int e = 0; e < 8; ++e) o[e] = fmaf(p, v[e], o[e]);
     }
     const float inv = 1.f / l;
 #pragma unroll
-    for (int e = 0; e < 32; ++e) o[e] *= inv;
-#pragma unroll
-    for (int c = 0; c < 4; ++c) st16(qkv + i * QKVLD + h * 32 + 8 * c, pack16<bf16>(o + 8 * c));
+    for (int e = 0; e < 8; ++e) o[e] *= inv;
+    st16(qkv + i * QKVLD + col, pack16<bf16>(o));
   }
   __syncthreads();
 
+  if (a.stop == 2) return;
   // ---- 3. out-projection + bo + residual (registers), then the fp32 rows over q|k|v
-  f32x4 yo[4][QMAX / 16];
+  f32x4 yo[CT3][QMAX / 16];
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int n0 = (wid * 4 + j) * 16;
+  for (int j = 0; j < CT3; ++j) {
+    const int n0 = (wid * CT3 + j) * 16;
     const f32x4 bias = *reinterpret_cast<const f32x4*>(a.bo + n0 + 4 * (lane >> 4));
 #pragma unroll
     for (int rt = 0; rt < QMAX / 16; ++rt) {
       if (rt >= RT) break;
-      f32x4 acc = tile_wx((const bf16*)a.wo, a.ldo, n0, qkv, QKVLD, rt * 16, lane);
+      f32x4 acc = tile_wx(wf3[j], qkv, QKVLD, rt * 16, lane);
       const int m = rt * 16 + (lane & 15);
       const u32x2 r = ld8(xs + m * XLD + n0 + 4 * (lane >> 4));
       acc[0] += bias[0] + __uint_as_float(r.x << 16);
@@ -147,9 +173,10 @@ __global__ __launch_bounds__(NT) void decsa_kernel(DecSaArgs a) {
     }
   }
   __syncthreads();                              // every wave done reading the attention output
+  if (a.stop == 3) return;
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int n0 = (wid * 4 + j) * 16;
+  for (int j = 0; j < CT3; ++j) {
+    const int n0 = (wid * CT3 + j) * 16;
 #pragma unroll
     for (int rt = 0; rt < QMAX / 16; ++rt) {
       if (rt >= RT) break;
@@ -162,7 +189,7 @@ __global__ __launch_bounds__(NT) void decsa_kernel(DecSaArgs a) {
   // LayerNorm, one wave per row, columns 4 lane .. +4
   const f32x4 gm = *reinterpret_cast<const f32x4*>(a.g + 4 * lane);
   const f32x4 bt = *reinterpret_cast<const f32x4*>(a.b + 4 * lane);
-  for (int m = wid; m < Q; m += NT / 64) {
+  for (int m = wid; m < Q; m += NW) {
     const f32x4 y = *reinterpret_cast<const f32x4*>(ys + m * YLD + 4 * lane);
     const float mean = wave_sum((y[0] + y[1]) + (y[2] + y[3])) * (1.f / D);
     float q = 0.f;
@@ -184,6 +211,12 @@ int spe_launch_decsa(const DecSaArgs& a, hipStream_t s) {
   if (a.Q < 1 || a.Q > QMAX || a.ldt % 8 || a.ldqk % 8 || a.ldv % 8 || a.ldo % 8 || !a.tgt || !a.wqk || !a.wv ||
       !a.wo || !a.bqk || !a.bv || !a.bo || !a.qpos || !a.g || !a.b)
     return 1;
-  hipLaunchKernelGGL(decsa_kernel, dim3(a.B), dim3(NT), 0, s, a);
+  DecSaArgs b = a;
+  // SPE_DECSA_STOP (kbench phase timing only): 5 = return at entry, 4 = after the loads, 1/2/3 =
+  // after the projections / attention / out-projection (kbench decsa, B = 64, Q = 11: 5.1 / 12.4 /
+  // 14.8 / ~20 / ~20.5 us of 22)
+  static const int stop = [] { const char* e = getenv("SPE_DECSA_STOP"); return e ? atoi(e) : 0; }();
+  b.stop = stop;
+  hipLaunchKernelGGL(decsa_kernel, dim3(b.B), dim3(NT), 0, s, b);
   return (int)hipGetLastError();
 }

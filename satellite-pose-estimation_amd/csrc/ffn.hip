@@ -566,8 +566,10 @@ constexpr int SPLIT_ROWS = 128 * 64;
 
 int spe_ffn_splits(int M, int F) {
   if (M >= SPLIT_ROWS) return 1;
+  // up to ~64 workgroups: more splits spread the weights thinner but the fp32 partials the
+  // reduce kernel reads grow with them (kbench ffndec, M = 704: 8 splits 23 us, 16: 25, 32: 34)
   int s = 1;
-  while (s < 32 && (F / HC) % (2 * s) == 0 && ((M + BM - 1) / BM) * s < 256) s *= 2;
+  while (s < 32 && (F / HC) % (2 * s) == 0 && ((M + BM - 1) / BM) * 2 * s <= 64) s *= 2;
   return s;
 }
 

@@ -191,9 +191,10 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   const float scale = 1.0f / std::sqrt(32.0f);
   const int Mt = B * T;
   const bool xa = spe_use_xattn(m);
-  // xattn reads pos (shared by all images, L2-resident) instead of a materialised memory + pos;
-  // SPE_XATTN_SHARED=0 restores the latter for A/B runs
-  static const bool xshared = [] { const char* e = getenv("SPE_XATTN_SHARED"); return e ? atoi(e) != 0 : true; }();
+  // SPE_XATTN_SHARED=1: xattn reads pos (shared by all images, L2-resident) instead of a
+  // materialised memory + pos -- half the HBM bytes, but the doubled score MFMAs (each wave pair
+  // computes its rows' scores twice) made it slower: 0.078 vs 0.059 ms per layer (kbench, B = 64)
+  static const bool xshared = [] { const char* e = getenv("SPE_XATTN_SHARED"); return e ? atoi(e) != 0 : false; }();
   if (stages & SPE_STAGE_BACKBONE) {
   // ---------------- backbone (REV/models/backbone.py:133-149)
   const bool pairs = m->stem.Cin == 4;                 // bf16: pair-packed stem (registry.cpp)
@@ -447,17 +448,12 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   // batch i+1's backbone with two workspaces)
   const int Mq = B * Q;
   CK((int)hipMemsetAsync(P(w.tgt), 0, (size_t)Mq * d * m->esz, s));
-  // tgt = LayerNorm(tgt + dao . W^T + b) (REV/models/transformer.py:227-228, 233-234): bf16 models
-  // run it as one lnproj launch in place over tgt, the others as GEMM + LayerNorm
+  // tgt = LayerNorm(tgt + dao . W^T + b) (REV/models/transformer.py:227-228, 233-234) as GEMM +
+  // LayerNorm: at these few rows (B.Q) lnproj's one-workgroup-per-8-tiles form measured slower
+  // (24 vs 18 us a layer: 6 workgroups each staging all of W)
   auto dec_proj_ln = [&](const Conv& wo, const float* lg, const float* lb) -> int {
     GemmArgs g = linear_args(wo, P(w.dao), d, Mq, P(w.dtmp), d);
     g.R = P(w.tgt); g.ldr = d;
-    GemmArgs gf = g;
-    gf.C = P(w.tgt); gf.ln_g = lg; gf.ln_b = lb;
-    if (m->esz == 2 && spe_lnproj_applies(gf)) {
-      CK(run_gemm(m, "gemm.dec.o", gf, GEMM_LINEAR, s));
-      return 0;
-    }
     CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR, s));
     CK(run_other(m, "ln.dec", 0.0, (double)Mq * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.dtmp), lg, lb, P(w.tgt), nullptr, Mq, d, dt, s); }));
     return 0;

@@ -132,6 +132,7 @@ struct DecSaArgs {
   const void* wo; int ldo; const float* bo;      // out_proj [256][ldo]
   const float* g; const float* b;  // norm1
   float scale;                     // 1/sqrt(head_dim)
+  int stop;                        // (timing experiments only: set by the launcher from SPE_DECSA_STOP)
 };
 int spe_launch_decsa(const DecSaArgs& a, hipStream_t s);   // 1 = not applicable
 

@@ -41,8 +41,12 @@ constexpr int NT = 512, KT = 32, RG = 96, D = 256;   // RG: rows per workgroup (
 constexpr int KTILE = KT * D * 2;               // 16 KB: K rows [key][256] (512 B rows)
 constexpr int VTILE = KT * D * 2;               // 16 KB: V rows [key][256] (512 B rows)
 constexpr int STAGE = KTILE + VTILE;
-constexpr int NSTAGE = 4;                       // ring: tile t in use, t+1 .. t+3 in flight
+#ifndef SPE_XATTN_STAGES
+#define SPE_XATTN_STAGES 4
+#endif
+constexpr int NSTAGE = SPE_XATTN_STAGES;        // ring: tile t in use, t+1 .. t+NSTAGE-1 in flight
 constexpr int LDS_BYTES = NSTAGE * STAGE;
+static_assert(NSTAGE >= 3 && NSTAGE <= 5, "ring: 3..5 slots (160 KB of LDS)");
 constexpr int LOADS = STAGE / 1024 / 2;         // glds per loader wave per tile
 constexpr int DB = 4;                           // 32-dim blocks of U per wave
 constexpr float NEG_BIG = -1.0e30f;
@@ -149,18 +153,21 @@ __global__ __launch_bounds__(NT, 1) void xattn_kernel(XattnArgs a) {
   // the q' loads must retire before the DMA stream starts (vmcnt is in-order; see ffn.hip)
 #pragma unroll
   for (int ks = 0; ks < 16; ++ks) asm volatile("" ::"v"(qf[ks]));
-  // Four-stage ring: tiles t+1..t+3 stay in flight while tile t is consumed; stage (t+3) % 4
-  // is refilled once every wave has passed tile t's barrier (it held tile t-1).
+  // NSTAGE-slot ring: tiles t+1..t+NSTAGE-1 stay in flight while tile t is consumed; the slot of
+  // tile t+NSTAGE-1 is refilled once every wave has passed tile t's barrier (it held tile t-1).
   if (loader) {
-    issue(tb, 0);
-    if (tb + 1 < te) issue(tb + 1, 1);
-    if (tb + 2 < te) issue(tb + 2, 2);
+#pragma unroll
+    for (int i = 0; i < NSTAGE - 1; ++i)
+      if (tb + i < te) issue(tb + i, i);
   }
   for (int t = tb; t < te; ++t) {
-    const int buf = (t - tb) & 3;
+    const int buf = (t - tb) % NSTAGE;
     if (loader) {
-      if (t + 2 < te) wait_vmcnt<2 * LOADS>();
-      else if (t + 1 < te) wait_vmcnt<LOADS>();
+      // tile t landed; the (up to NSTAGE - 2) newer tiles may stay in flight
+      const int newer = min(NSTAGE - 2, te - 1 - t);
+      if (newer >= 3) wait_vmcnt<3 * LOADS>();
+      else if (newer == 2) wait_vmcnt<2 * LOADS>();
+      else if (newer == 1) wait_vmcnt<LOADS>();
       else wait_vmcnt<0>();
     }
     // raw barrier (__syncthreads' fence would drain the tiles in flight): tile t visible to
@@ -168,7 +175,7 @@ __global__ __launch_bounds__(NT, 1) void xattn_kernel(XattnArgs a) {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (loader) {
-      if (t + 3 < te) issue(t + 3, (buf + 3) & 3);
+      if (t + NSTAGE - 1 < te) issue(t + NSTAGE - 1, (buf + NSTAGE - 1) % NSTAGE);
       continue;
     }
     if (!live_wave) continue;

@@ -92,6 +92,20 @@ def main():
                 continue
             ms = timeit(fn, a.iters)
             print(f"ffn.dec M={M} splits={sp}: {ms * 1e3:.1f} us")
+    if a.which in ("decsa", "all"):
+        # the decoder's fused self-attention block (decsa.hip), B images of Q = 11 rows
+        Q = 11
+        t = torch.randn(B * Q, D, generator=g).to(dev, torch.bfloat16)
+        wqk = (torch.randn(2 * D, D, generator=g) / 16).to(dev, torch.bfloat16)
+        wv = (torch.randn(D, D, generator=g) / 16).to(dev, torch.bfloat16)
+        wo = (torch.randn(D, D, generator=g) / 16).to(dev, torch.bfloat16)
+        qpos = torch.zeros(Q, 2 * D, device=dev, dtype=torch.bfloat16)
+        bqk, bv, bo, bt = (torch.zeros(n, device=dev) for n in (2 * D, D, D, D))
+        gm = torch.ones(D, device=dev)
+        fn = lambda: L.spe_debug_decsa(None, p(t), D, B, Q, p(wqk), D, p(bqk), p(wv), D, p(bv), p(qpos), p(wo), D,
+                                       p(bo), p(gm), p(bt), 32 ** -0.5)
+        ms = timeit(fn, a.iters)
+        print(f"decsa B={B} Q={Q}: {ms * 1e3:.1f} us")
     if a.which in ("xattn", "all"):
         Q = 11
         q = (torch.randn(B * Q, 8 * D, generator=g) / 16).to(dev, torch.bfloat16)
