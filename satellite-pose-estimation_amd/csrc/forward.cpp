@@ -192,8 +192,9 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   const int Mt = B * T;
   const bool xa = spe_use_xattn(m);
   // SPE_XATTN_SHARED=1: xattn reads pos (shared by all images, L2-resident) instead of a
-  // materialised memory + pos -- half the HBM bytes, but the doubled score MFMAs (each wave pair
-  // computes its rows' scores twice) made it slower: 0.078 vs 0.059 ms per layer (kbench, B = 64)
+  // materialised memory + pos -- half the HBM bytes, the score reduction split over each wave
+  // pair and exchanged through LDS, but measured slower: 0.070-0.074 vs 0.058 ms per layer
+  // (kbench, B = 64; the kernel is not HBM-bound at this size)
   static const bool xshared = [] { const char* e = getenv("SPE_XATTN_SHARED"); return e ? atoi(e) != 0 : false; }();
   if (stages & SPE_STAGE_BACKBONE) {
   // ---------------- backbone (REV/models/backbone.py:133-149)

@@ -35,6 +35,8 @@
 #include "spe_common.h"
 #include "spe_kernels.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr int NT = 512, KT = 32, RG = 96, D = 256;   // RG: rows per workgroup (3 wave pairs)
@@ -88,9 +90,11 @@ SPE_DEV u32x2 ds_read_tr(uint32_t addr) {
   return r;
 }
 
+constexpr int XCH = 6 * 16 * 64 * 4;           // KS: the compute waves' partial-score exchange (24 KB)
+
 template <bool KS>
 __global__ __launch_bounds__(NT, 1) void xattn_kernel(XattnArgs a) {
-  __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];
+  __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES + (KS ? XCH : 0)];
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hh = lane >> 5, r32 = lane & 31, l16 = lane & 15, dg = 16 * ((lane >> 4) & 1);
   const int R = 8 * a.Q, ngroups = (R + RG - 1) / RG;
@@ -153,18 +157,23 @@ __global__ __launch_bounds__(NT, 1) void xattn_kernel(XattnArgs a) {
   // the q' loads must retire before the DMA stream starts (vmcnt is in-order; see ffn.hip)
 #pragma unroll
   for (int ks = 0; ks < 16; ++ks) asm volatile("" ::"v"(qf[ks]));
+  // KS: each image walks its split's tiles from its own starting offset, so the 64 workgroups
+  // of a split do not all read the same shared pos rows at once (one L2 channel per line); the
+  // online softmax does not depend on the tile order.  (The memory rows differ per image anyway.)
+  const int nt = te - tb, rot = KS ? (b * 7) % nt : 0;
+  auto tile_at = [&](int i) { const int j = i + rot; return tb + (j >= nt ? j - nt : j); };
   // NSTAGE-slot ring: tiles t+1..t+NSTAGE-1 stay in flight while tile t is consumed; the slot of
   // tile t+NSTAGE-1 is refilled once every wave has passed tile t's barrier (it held tile t-1).
   if (loader) {
 #pragma unroll
     for (int i = 0; i < NSTAGE - 1; ++i)
-      if (tb + i < te) issue(tb + i, i);
+      if (tb + i < te) issue(tile_at(i), i);
   }
-  for (int t = tb; t < te; ++t) {
-    const int buf = (t - tb) % NSTAGE;
+  for (int it = 0; it < nt; ++it) {
+    const int t = tile_at(it), buf = it % NSTAGE;
     if (loader) {
       // tile t landed; the (up to NSTAGE - 2) newer tiles may stay in flight
-      const int newer = min(NSTAGE - 2, te - 1 - t);
+      const int newer = min(NSTAGE - 2, nt - 1 - it);
       if (newer >= 3) wait_vmcnt<3 * LOADS>();
       else if (newer == 2) wait_vmcnt<2 * LOADS>();
       else if (newer == 1) wait_vmcnt<LOADS>();
@@ -175,35 +184,53 @@ __global__ __launch_bounds__(NT, 1) void xattn_kernel(XattnArgs a) {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (loader) {
-      if (t + NSTAGE - 1 < te) issue(t + NSTAGE - 1, (buf + NSTAGE - 1) % NSTAGE);
+      if (it + NSTAGE - 1 < nt) issue(tile_at(it + NSTAGE - 1), (buf + NSTAGE - 1) % NSTAGE);
+      if constexpr (KS) __builtin_amdgcn_s_barrier();   // (the compute waves' exchange barrier)
       continue;
     }
-    if (!live_wave) continue;
+    if (!live_wave) {
+      if constexpr (KS) __builtin_amdgcn_s_barrier();
+      continue;
+    }
     const char* kl = lds + buf * STAGE;
     const char* vl = kl + KTILE;
 
-    // S^T - m: lane (row r32, hh) register r <-> key (r & 3) + 8 (r >> 2) + 4 hh
-    // (KS: the V tile's memory rows, then the pos rows, into the same two chains)
-    f32x16 sa, sb;
+    // S^T - m: lane (row r32, hh) register r <-> key (r & 3) + 8 (r >> 2) + 4 hh.  KS: the wave
+    // pair splits the K = 512 reduction -- dh 0 the memory rows (from -m), dh 1 the pos rows --
+    // and swaps the partial scores through LDS; both waves then form memory part + pos part in
+    // the same order, so their softmax state stays bit-identical.
+    f32x16 s;
+    auto chain = [&](const char* t0, auto NEG) {
+      f32x16 sa, sb;
 #pragma unroll
-    for (int ks = 0; ks < 16; ks += 2) {
-      const char* t0 = KS ? vl : kl;
-      const bf16x8 k0 = __builtin_bit_cast(bf16x8, ld16(t0 + k_off<KS>(r32, 2 * ks + hh)));
-      const bf16x8 k1 = __builtin_bit_cast(bf16x8, ld16(t0 + k_off<KS>(r32, 2 * ks + 2 + hh)));
-      sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf[ks], ks == 0 ? negm : sa, 0, 0, 0);
-      if (ks == 0) {
-        sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[ks + 1], f32x16{}, 0, 0, 0);
-      } else {
-        sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[ks + 1], sb, 0, 0, 0);
+      for (int ks = 0; ks < 16; ks += 2) {
+        const bf16x8 k0 = __builtin_bit_cast(bf16x8, ld16(t0 + k_off<KS>(r32, 2 * ks + hh)));
+        const bf16x8 k1 = __builtin_bit_cast(bf16x8, ld16(t0 + k_off<KS>(r32, 2 * ks + 2 + hh)));
+        if (ks == 0) {
+          sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf[ks], decltype(NEG)::value ? negm : f32x16{}, 0, 0, 0);
+          sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[ks + 1], f32x16{}, 0, 0, 0);
+        } else {
+          sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf[ks], sa, 0, 0, 0);
+          sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[ks + 1], sb, 0, 0, 0);
+        }
       }
-      if constexpr (KS) {
-        const bf16x8 p0 = __builtin_bit_cast(bf16x8, ld16(kl + k_off<KS>(r32, 2 * ks + hh)));
-        const bf16x8 p1 = __builtin_bit_cast(bf16x8, ld16(kl + k_off<KS>(r32, 2 * ks + 2 + hh)));
-        sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p0, qf[ks], sa, 0, 0, 0);
-        sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(p1, qf[ks + 1], sb, 0, 0, 0);
+      s = sa + sb;
+    };
+    if (!KS) chain(kl, std::true_type{});
+    else chain(dh ? kl : vl, std::false_type{});   // (KS: -m after the exchange, no negm registers)
+    if constexpr (KS) {
+      float* xch = reinterpret_cast<float*>(lds + LDS_BYTES);
+#pragma unroll
+      for (int r = 0; r < 16; ++r) xch[(wid * 16 + r) * 64 + lane] = s[r];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float o = xch[((wid ^ 1) * 16 + r) * 64 + lane];
+        s[r] = (dh ? o + s[r] : s[r] + o) - m;   // memory part + pos part, shifted by the running max
       }
     }
-    f32x16 s = sa + sb;
     const int key_base = t * KT;
     if (key_base + KT > a.T) {
 #pragma unroll
@@ -219,9 +246,9 @@ __global__ __launch_bounds__(NT, 1) void xattn_kernel(XattnArgs a) {
       const auto sw = __builtin_amdgcn_permlane32_swap(__float_as_uint(mx), __float_as_uint(mx), false, false);
       mx = __builtin_fmaxf(__uint_as_float(sw[0]), __uint_as_float(sw[1]));
     }
-    if (t == tb || __any(mx > SLACK)) {
-      const float d = t == tb ? mx : __builtin_fmaxf(mx, 0.f);
-      if (t != tb) {
+    if (it == 0 || __any(mx > SLACK)) {
+      const float d = it == 0 ? mx : __builtin_fmaxf(mx, 0.f);
+      if (it != 0) {
         const float alpha = __builtin_amdgcn_exp2f(-d);
         l *= alpha;
 #pragma unroll
