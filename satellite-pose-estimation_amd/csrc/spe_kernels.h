@@ -35,6 +35,7 @@ struct GemmArgs {
   void* S; int s_col0;             // fp32 models: columns n >= s_col0 stored instead as bf16 hi / lo planes for the
                                    // fp32x3 attention: rows -> hi [M][N - s_col0] then lo; head-transposed
                                    // (vt_T) -> hi in C's layout [vt_B][N][vt_T] then lo (s_col0 = 0)
+  int ns_rmap;                     // (set by gemm_stream.hip's launcher) image-interleaved tile order
 };
 bool spe_gemm_ln_fusable(const GemmArgs& g);   // the large-tile kernel can fuse ln_g/ln_b for g
 int spe_launch_gemm(const GemmArgs& g, int dtype, int mode, hipStream_t s);

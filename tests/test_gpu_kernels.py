@@ -253,10 +253,11 @@ def test_gemm_fused_layernorm(gpu_device, inplace, M):
     assert rc != 0
 
 
-@pytest.mark.parametrize("M", [256 * 256 + 77, 300])
+@pytest.mark.parametrize("M", [256 * 256 + 77, 300, 24 * 2704])
 def test_gemm_row_periodic_residual(gpu_device, M):
     """C = A W^T + b + R[m % period]: the (x + pos) W^T = x W^T + pos W^T rewrite of the
-    attention q/k projections (both kernels: M = 300 stays on the 128x128 one)."""
+    attention q/k projections (both kernels: M = 300 stays on the 128x128 one; M = 24 images x
+    2704 tokens, the model's shape, with SPE_SG_RMAP=1 takes the image-interleaved tile order)."""
     _, dt, tol = DT["bf16"]
     N, K, period = 512, 256, 2704 if M > 1000 else 11
     g = torch.Generator(device="cpu").manual_seed(M)
