@@ -343,6 +343,11 @@ int spe_debug_btail_n1(void* stream, const void* a, int lda, int k1, const void*
 int spe_debug_decsa(void* stream, void* tgt, int ldt, int B, int Q, const void* wqk, int ldqk, const float* bqk,
                     const void* wv, int ldv, const float* bv, const void* qpos, const void* wo, int ldo,
                     const float* bo, const float* g, const float* b, float scale);
+/* decproj (bf16 only, decsa.hip): in place over tgt [B*Q][ldt], tgt = LayerNorm(tgt + x . wo^T + bo)
+ * per row (the decoder cross-attention's out-projection + norm2), x [B*Q][ldx] bf16, d = 256,
+ * Q <= 64 (one workgroup per image). */
+int spe_debug_decproj(void* stream, void* tgt, int ldt, const void* x, int ldx, int B, int Q, const void* wo, int ldo,
+                      const float* bo, const float* g, const float* b);
 /* the K-column order btail's second product expects: stored column k holds channel perm(k) */
 int spe_debug_btail_perm(int k);
 /* stempool (bf16, stempool.hip): out [B][Po][Po] rows of stride ldo (Po = S/4 for S % 4 == 0) =

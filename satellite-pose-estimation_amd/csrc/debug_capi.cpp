@@ -122,6 +122,14 @@ int spe_debug_decsa(void* stream, void* tgt, int ldt, int B, int Q, const void* 
   return rc != 0 ? spe_fail(SPE_E_LAUNCH, "decsa launch rejected its arguments") : 0;
 }
 
+int spe_debug_decproj(void* stream, void* tgt, int ldt, const void* x, int ldx, int B, int Q, const void* wo, int ldo,
+                      const float* bo, const float* g, const float* b) {
+  DecProjArgs a{};
+  a.tgt = tgt; a.ldt = ldt; a.x = x; a.ldx = ldx; a.B = B; a.Q = Q; a.wo = wo; a.ldo = ldo; a.bo = bo; a.g = g; a.b = b;
+  const int rc = spe_launch_decproj(a, (hipStream_t)stream);
+  return rc != 0 ? spe_fail(SPE_E_LAUNCH, "decproj launch rejected its arguments") : 0;
+}
+
 int spe_debug_btail_n1(void* stream, const void* a, int lda, int k1, const void* r, const void* w3, int ld3,
                        const float* b3, void* y, const void* w1p, int ld1, const float* b1, void* z, int n1, int n2,
                        int M) {

@@ -75,15 +75,6 @@ __global__ __launch_bounds__(NT) void decsa_kernel(DecSaArgs a) {
     st16(xs + r * XLD + 8 * c, r < Q ? ld16(tg + (size_t)r * a.ldt + 8 * c) : u32x4{0, 0, 0, 0});
   }
   __syncthreads();
-  if (a.stop == 4) {                            // (timing: the loads only; keep them live)
-    u32x4 x = {0, 0, 0, 0};
-#pragma unroll
-    for (int j = 0; j < CT1; ++j)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) x ^= wf1[j][k];
-    if (x.x == 0x12345678u) st16(xs, x);
-    return;
-  }
 #pragma unroll
   for (int j = 0; j < CT1; ++j) {
     const int n0 = tile1(j) * 16;
@@ -203,7 +194,70 @@ __global__ __launch_bounds__(NT) void decsa_kernel(DecSaArgs a) {
   }
 }
 
+// tgt = LayerNorm(tgt + x . Wo^T + bo) per image: the cross-attention's out-projection + norm2
+// (REV/models/transformer.py:233-234), decsa's phase 3 on its own -- one launch instead of a
+// few-row GEMM and a LayerNorm, the rows never leaving LDS between them.
+__global__ __launch_bounds__(NT) void decproj_kernel(DecProjArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16 rs[QMAX * XLD];   // tgt rows (the residual)
+  __shared__ __attribute__((aligned(16))) bf16 xs[QMAX * XLD];   // input rows
+  __shared__ __attribute__((aligned(16))) float ys[QMAX * YLD];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int b = blockIdx.x, Q = a.Q, RT = (Q + 15) / 16;
+  bf16* tg = (bf16*)a.tgt + (size_t)b * Q * a.ldt;
+  const bf16* xg = (const bf16*)a.x + (size_t)b * Q * a.ldx;
+  constexpr int CT3 = D / 16 / NW;
+  u32x4 wf[CT3][8];
+#pragma unroll
+  for (int j = 0; j < CT3; ++j) w_frags(wf[j], (const bf16*)a.wo, a.ldo, (wid * CT3 + j) * 16, lane);
+  for (int i = tid; i < RT * 16 * (D / 8); i += NT) {
+    const int r = i / (D / 8), c = i % (D / 8);
+    st16(xs + r * XLD + 8 * c, r < Q ? ld16(xg + (size_t)r * a.ldx + 8 * c) : u32x4{0, 0, 0, 0});
+    st16(rs + r * XLD + 8 * c, r < Q ? ld16(tg + (size_t)r * a.ldt + 8 * c) : u32x4{0, 0, 0, 0});
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < CT3; ++j) {
+    const int n0 = (wid * CT3 + j) * 16;
+    const f32x4 bias = *reinterpret_cast<const f32x4*>(a.bo + n0 + 4 * (lane >> 4));
+#pragma unroll
+    for (int rt = 0; rt < QMAX / 16; ++rt) {
+      if (rt >= RT) break;
+      f32x4 acc = tile_wx(wf[j], xs, XLD, rt * 16, lane);
+      const int m = rt * 16 + (lane & 15);
+      const u32x2 r = ld8(rs + m * XLD + n0 + 4 * (lane >> 4));
+      acc[0] += bias[0] + __uint_as_float(r.x << 16);
+      acc[1] += bias[1] + __uint_as_float(r.x & 0xffff0000u);
+      acc[2] += bias[2] + __uint_as_float(r.y << 16);
+      acc[3] += bias[3] + __uint_as_float(r.y & 0xffff0000u);
+      *reinterpret_cast<f32x4*>(ys + m * YLD + n0 + 4 * (lane >> 4)) = acc;
+    }
+  }
+  __syncthreads();
+  const f32x4 gm = *reinterpret_cast<const f32x4*>(a.g + 4 * lane);
+  const f32x4 bt = *reinterpret_cast<const f32x4*>(a.b + 4 * lane);
+  for (int m = wid; m < Q; m += NW) {
+    const f32x4 y = *reinterpret_cast<const f32x4*>(ys + m * YLD + 4 * lane);
+    const float mean = wave_sum((y[0] + y[1]) + (y[2] + y[3])) * (1.f / D);
+    float q = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) q += (y[e] - mean) * (y[e] - mean);
+    const float rsd = rsqrtf(wave_sum(q) * (1.f / D) + 1e-5f);
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (y[e] - mean) * rsd * gm[e] + bt[e];
+    st8(tg + (size_t)m * a.ldt + 4 * lane, u32x2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])});
+  }
+}
+
 }  // namespace
+
+int spe_launch_decproj(const DecProjArgs& a, hipStream_t s) {
+  if (a.B <= 0) return 0;
+  if (a.Q < 1 || a.Q > QMAX || a.ldt % 8 || a.ldx % 8 || a.ldo % 8 || !a.tgt || !a.x || !a.wo || !a.bo || !a.g || !a.b)
+    return 1;
+  hipLaunchKernelGGL(decproj_kernel, dim3(a.B), dim3(NT), 0, s, a);
+  return (int)hipGetLastError();
+}
 
 // 1 = not applicable (the caller runs the separate launches)
 int spe_launch_decsa(const DecSaArgs& a, hipStream_t s) {
@@ -212,9 +266,9 @@ int spe_launch_decsa(const DecSaArgs& a, hipStream_t s) {
       !a.wo || !a.bqk || !a.bv || !a.bo || !a.qpos || !a.g || !a.b)
     return 1;
   DecSaArgs b = a;
-  // SPE_DECSA_STOP (kbench phase timing only): 5 = return at entry, 4 = after the loads, 1/2/3 =
-  // after the projections / attention / out-projection (kbench decsa, B = 64, Q = 11: 5.1 / 12.4 /
-  // 14.8 / ~20 / ~20.5 us of 22)
+  // SPE_DECSA_STOP (kbench phase timing only): 5 = return at entry, 1/2/3 = after the projections
+  // / attention / out-projection (kbench decsa, B = 64, Q = 11: 5.1 / 14.8 / ~20 / ~20.5 us of 22;
+  // a loads-only stop, 12.4 us, kept the 48 fragments live past their use and spilled the kernel)
   static const int stop = [] { const char* e = getenv("SPE_DECSA_STOP"); return e ? atoi(e) : 0; }();
   b.stop = stop;
   hipLaunchKernelGGL(decsa_kernel, dim3(b.B), dim3(NT), 0, s, b);

@@ -452,7 +452,17 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   // tgt = LayerNorm(tgt + dao . W^T + b) (REV/models/transformer.py:227-228, 233-234) as GEMM +
   // LayerNorm: at these few rows (B.Q) lnproj's one-workgroup-per-8-tiles form measured slower
   // (24 vs 18 us a layer: 6 workgroups each staging all of W)
+  static const bool decproj_on = [] { const char* e = getenv("SPE_DECPROJ"); return e ? atoi(e) != 0 : true; }();
   auto dec_proj_ln = [&](const Conv& wo, const float* lg, const float* lb) -> int {
+    if (decproj_on && m->esz == 2 && d == 256 && Q <= 64) {
+      // bf16: one workgroup per image, the rows in LDS from the GEMM to the LayerNorm (decsa.hip)
+      DecProjArgs pa{};
+      pa.tgt = P(w.tgt); pa.ldt = d; pa.x = P(w.dao); pa.ldx = d; pa.B = B; pa.Q = Q;
+      pa.wo = wo.w; pa.ldo = wo.Kpad; pa.bo = wo.bias; pa.g = lg; pa.b = lb;
+      CK(run_other(m, "dec.proj", 2.0 * Mq * d * d, 3.0 * Mq * d * m->esz + (double)d * d * m->esz, s,
+                   [&] { return spe_launch_decproj(pa, s); }));
+      return 0;
+    }
     GemmArgs g = linear_args(wo, P(w.dao), d, Mq, P(w.dtmp), d);
     g.R = P(w.tgt); g.ldr = d;
     CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR, s));

@@ -136,6 +136,15 @@ struct DecSaArgs {
   int stop;                        // (timing experiments only: set by the launcher from SPE_DECSA_STOP)
 };
 int spe_launch_decsa(const DecSaArgs& a, hipStream_t s);   // 1 = not applicable
+// tgt = LN(tgt + x . Wo^T + bo), one workgroup per image (decsa.hip; bf16, d = 256, Q <= 64)
+struct DecProjArgs {
+  void* tgt; int ldt;              // [B*Q][ldt] bf16, in place
+  const void* x; int ldx;          // [B*Q][ldx] bf16
+  int B, Q;
+  const void* wo; int ldo; const float* bo;
+  const float* g; const float* b;
+};
+int spe_launch_decproj(const DecProjArgs& a, hipStream_t s);   // 1 = not applicable
 
 // Fused FFN + residual + LayerNorm (bf16 only): y = LN(x + W2 relu(W1 x + b1) + b2).
 // x / y may alias (each block reads and writes only its own rows).

@@ -734,6 +734,35 @@ def test_decoder_self_attention_block(gpu_device, B, Q):
     assert torch.equal(t[:, D:].cpu(), x[:, D:].to(dt))   # nothing written past D
 
 
+@pytest.mark.parametrize("B,Q", [(3, 11), (2, 40), (1, 64), (0, 11)])
+def test_decoder_out_projection_norm(gpu_device, B, Q):
+    """decproj (decsa.hip): tgt = LN(tgt + x . Wo^T + bo) in place, one workgroup per image
+    (REV/models/transformer.py:233-234, the cross-attention's out-projection + norm2), against
+    torch fp32 on the same bf16 operands; 2e-2 * scale (bf16 output)."""
+    dt, D = torch.bfloat16, 256
+    g = torch.Generator(device="cpu").manual_seed(7 * B + Q)
+    ld = D + 8
+    t0 = torch.randn(max(B, 1) * Q, ld, generator=g)
+    x = torch.randn(max(B, 1) * Q, ld, generator=g).to(dt)
+    wo = (torch.randn(D, D, generator=g) / 16).to(dt)
+    bo = torch.randn(D, generator=g) * 0.1
+    gam, bet = 1 + 0.1 * torch.randn(D, generator=g), 0.1 * torch.randn(D, generator=g)
+    t = t0.to(dt).to(gpu_device)
+    dev = lambda a: a.to(gpu_device).contiguous()          # noqa: E731
+    xd, wod, bod, gd, bd = dev(x), dev(wo), dev(bo), dev(gam), dev(bet)
+    L = _lib.lib()
+    rc = L.spe_debug_decproj(None, _p(t), ld, _p(xd), ld, B, Q, _p(wod), D, _p(bod), _p(gd), _p(bd))
+    assert rc == 0, L.spe_last_error()
+    torch.cuda.synchronize()
+    if B == 0:
+        assert torch.equal(t.cpu(), t0.to(dt))
+        return
+    y = torch.nn.functional.layer_norm(x[:, :D].float() @ wo.float().T + bo + t0[:, :D].to(dt).float(), (D,), gam,
+                                       bet, 1e-5)
+    _close(t[:, :D].cpu(), y, 2e-2)
+    assert torch.equal(t[:, D:].cpu(), t0[:, D:].to(dt))
+
+
 @pytest.mark.parametrize("dtype", ["bf16", "fp32"])
 def test_layernorm(gpu_device, dtype):
     code, dt, tol = DT[dtype]
