@@ -18,7 +18,7 @@
 extern "C" {
 #endif
 
-#define SPE_ABI_VERSION 6
+#define SPE_ABI_VERSION 7
 
 enum {
   SPE_E_ARG = -1,        /* bad argument / size */
@@ -51,7 +51,11 @@ enum { SPE_DTYPE_BF16_ = 0, SPE_DTYPE_F32_ = 1, SPE_DTYPE_F16_ = 2, SPE_DTYPE_F3
  *                            inliers = reprojection error < the image's threshold (get_repro_th, :53-58),
  *                            sigma-weighted Huber(0.001) LM on the inliers (weights normalised over them),
  *                            the EPnP pose kept when the refined error sum over all points is larger
- *                            (:142-146); exactly one inlier raises IndexError there -> status NO_FG
+ *                            (:142-146); exactly one inlier raises IndexError there -> status NO_FG;
+ *                            no inlier -> status OK with the EPnP pose (the reference's own control flow
+ *                            builds an empty Ceres problem, tests/golden/solver_front_ref.npz), PARITY
+ *                            UNPINNED in one point: whether OpenCV 4.4's undistortPoints accepts the
+ *                            empty point set (a cv2.error there would make SpeedEval log a zero pose)
  * SPE_PNP_EPNP's inlier_mask is epnp_init's set, reprojection error < repro (:163-166). */
 enum { SPE_PNP_EPNP = 0, SPE_PNP_RANSAC_P3P_LM = 1, SPE_PNP_EPNP_RANSAC_SIGMA = 2, SPE_PNP_EPNP_LM = 3,
        SPE_PNP_EPNP_CERES = 4 };
@@ -258,13 +262,6 @@ int spe_model_profile_end(spe_model* m);
 int spe_model_profile_get(const spe_model* m, int i, char* kind, int kind_len, double* ms, double* flops,
                           double* bytes);
 
-/* A HIP stream whose kernels may only use the CUs set in mask (words 32-bit words, bit i = CU i
- * in the runtime's CU order; hipExtStreamCreateWithCUMask): PosePipeline's CU partition between
- * the HBM-bound backbone and the MFMA/VALU-bound encoder (no reference counterpart).  destroy
- * releases it. */
-int spe_stream_create_cu_mask(const uint32_t* mask, int words, void** stream);
-int spe_stream_destroy(void* stream);
-
 /* Kernel test hooks: launch one kernel family on caller buffers (tests/test_gpu_kernels.py).
  * gemm: C[M,N] = act(A . W^T + bias + R) with act = act_code & 255 (0 none, 1 ReLU, 2 SiLU, 3
  * exact GELU); bit 8 of act_code adds R after the activation instead; mode 0 linear (A[m*lda+k]), 1 linear + P[(m%prow)
@@ -307,15 +304,15 @@ int spe_debug_ffn(void* stream, const void* x, int ldx, const void* w1, int ld1,
                   int ld2, const float* b2, const float* gamma, const float* beta, void* y, int ldy, int M, int D,
                   int F, float* partial, int splits);
 /* xattn (bf16 only, the decoder cross-attention against the memory): for image b, query q and
- * head h, u[b*Q+q][h*256 .. +256] = softmax_t(q'[b*Q+q][h*256 ..] . K_t) . v[b*T+t] with the
- * scores already in the exp2 domain; K_t = k[b*T+t] (k_shared 0) or v[b*T+t] + k[t] (k_shared 1:
- * k is the positional table [T] shared by all images, the model's mode).  k, v rows of 256.  wv
- * non-null ([256][256] bf16, bv fp32): o[b*Q+q][h*32 + j] = wv[h*32 + j] . u_h + bv[h*32 + j] is
- * written instead of u.  splits <= 0 picks the launch's own key split; partial_scratch: fp32,
- * splits * B * 8Q * 258.  (ABI 6: k_shared added.) */
+ * head h, u[b*Q+q][h*256 .. +256] = softmax_t(q'[b*Q+q][h*256 ..] . k[b*T+t]) . v[b*T+t] with the
+ * scores already in the exp2 domain (k = memory + pos, v = memory, rows of 256).  wv non-null
+ * ([256][256] bf16, bv fp32): o[b*Q+q][h*32 + j] = wv[h*32 + j] . u_h + bv[h*32 + j] is written
+ * instead of u.  splits <= 0 picks the launch's own key split; partial_scratch: fp32,
+ * splits * B * 8Q * 258.  (ABI 7: the measured-negative shared-pos variant and its k_shared
+ * argument are gone.) */
 int spe_debug_xattn(void* stream, const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* u,
                     int ldu, const void* wv, const float* bv, void* o, int ldo, int B, int Q, int T, int splits,
-                    float* partial_scratch, int k_shared);
+                    float* partial_scratch);
 /* upconv (bf16 models' neck, replaces the upsample + conv pair of REV/models/backbone.py:141
  * s16_latern(up16sto8s(xs16))): z [B*H*W][9*C] holds the per-tap products W_t . x at the low
  * resolution (t = kh*3 + kw); out [B][2H][2W] rows of stride ldo receive conv3x3(pad 1) of the
@@ -328,14 +325,6 @@ int spe_debug_upconv(void* stream, int dtype, const void* z, void* out, int ldo,
  * {(64, 64, r), (64, 128, r), (128, 64, null)}. */
 int spe_debug_btail(void* stream, const void* a, int lda, int k1, const void* r, const void* w3, int ld3,
                     const float* b3, void* y, const void* w1p, int ld1, const float* b1, void* z, int n2, int M);
-/* the same with the block-output width n1 (round 4): n1 = 512 / 1024 runs the split-N form of the
- * layer-2 / layer-3 boundaries (y produced in column chunks, weights streamed through LDS);
- * (k1, n1, n2) in {(128, 512, 128), (128, 512, 256), (256, 1024, 256)} with r [M][n1] non-null,
- * or n1 = 256 as spe_debug_btail.  Replaces the conv3 + conv1 launch pair of
- * REV/models/backbone.py:114-125 (torchvision Bottleneck) at those boundaries. */
-int spe_debug_btail_n1(void* stream, const void* a, int lda, int k1, const void* r, const void* w3, int ld3,
-                       const float* b3, void* y, const void* w1p, int ld1, const float* b1, void* z, int n1, int n2,
-                       int M);
 /* decsa (bf16 only, the decoder self-attention block, decsa.hip): in place over tgt [B*Q][ldt],
  * per image b: tgt = LayerNorm(tgt + MHA(q = k = tgt + query_pos, v = tgt) . wo^T + bo) with
  * 8 heads of 32 (d = 256), q|k = tgt . wqk^T + bqk + qpos ([Q][512] bf16, query_pos . wqk^T),

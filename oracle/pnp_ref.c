@@ -35,6 +35,20 @@ enum { ST_OK = 0, ST_NO_FG = 1, ST_CV_ERROR = 2, ST_RANSAC_FALLBACK = 3, ST_UNPI
 
 typedef struct { double fx, fy, cx, cy; } cam_t;
 
+/* Decision trace of the last oracle_pnp_one call (test instrumentation: names the discrete choice
+ * behind a score difference between two keypoint sets, tests/test_gpu_precision.py).  epnp_*: the
+ * last EPnP solve's three beta approximations (mean reprojection error each) and OpenCV's pick;
+ * ransac_*: the best model's iteration, its inlier count and mask, the iterations run, and the
+ * point whose reprojection error lies closest to the threshold (|err - thresh| px). */
+typedef struct {
+  double epnp_err[3];
+  int epnp_pick, epnp_calls;
+  int ransac_best_iter, ransac_inliers, ransac_iters, ransac_margin_point;
+  unsigned ransac_mask;
+  double ransac_margin_px;
+} trace_t;
+static trace_t g_trace;
+
 /* ------------------------------------------------------------------ cv::RNG */
 typedef struct { uint64_t state; } rng_t;
 static unsigned rng_next(rng_t* r) {
@@ -954,6 +968,9 @@ static void epnp_finish(epnp_t* e, const double* ut, double* R, double* t) {
   epnp_L_rho(e, ut, L, rho);
   for (int w = 1; w <= 3; ++w) err[w] = epnp_approx(e, ut, L, rho, w, Rs[w], ts[w]);
   const int N = epnp_pick(err);
+  for (int w = 0; w < 3; ++w) g_trace.epnp_err[w] = err[w + 1];
+  g_trace.epnp_pick = N;
+  g_trace.epnp_calls++;
   memcpy(R, Rs[N], sizeof(double) * 9);
   memcpy(t, ts[N], sizeof(double) * 3);
 }
@@ -1157,10 +1174,13 @@ static int ransac(const cam_t* k, int n, const float* wld_f, const float* img_f,
   rng_t rng = {(uint64_t)-1};
   int niters = max_iters > 1 ? max_iters : 1, maxGood = 0;
   unsigned char best[MAXN], cur[MAXN];
+  float cur_e2[MAXN];
   double best_r[3], best_t[3];
+  int iter_run = 0;
   float thr2 = (float)((double)thresh * (double)thresh);
   *has_last = 0;
   for (int iter = 0; iter < niters; ++iter) {
+    iter_run = iter + 1;
     int idx[5];
     for (int i = 0; i < mp; ++i) {
       for (;;) {
@@ -1196,7 +1216,8 @@ static int ransac(const cam_t* k, int n, const float* wld_f, const float* img_f,
     for (int i = 0; i < n; ++i) {
       float uv[2];
       project_f(k, R, t, wld_f + 3 * i, uv);
-      cur[i] = sq_err_f(img_f + 2 * i, uv) <= thr2;
+      cur_e2[i] = sq_err_f(img_f + 2 * i, uv);
+      cur[i] = cur_e2[i] <= thr2;
       good += cur[i];
     }
     if (good > (maxGood > mp - 1 ? maxGood : mp - 1)) {
@@ -1205,8 +1226,18 @@ static int ransac(const cam_t* k, int n, const float* wld_f, const float* img_f,
       memcpy(best_t, t, sizeof t);
       maxGood = good;
       niters = (int)ransac_update(conf, (double)(n - good) / n, mp, niters);
+      g_trace.ransac_best_iter = iter;
+      g_trace.ransac_inliers = good;
+      g_trace.ransac_mask = 0;
+      g_trace.ransac_margin_px = 1e300;
+      for (int i = 0; i < n; ++i) {
+        if (cur[i]) g_trace.ransac_mask |= 1u << i;
+        const double mg = fabs(sqrt((double)cur_e2[i]) - (double)thresh);
+        if (mg < g_trace.ransac_margin_px) { g_trace.ransac_margin_px = mg; g_trace.ransac_margin_point = i; }
+      }
     }
   }
+  g_trace.ransac_iters = iter_run;
   if (maxGood <= 0) return 0;
   memcpy(mask, best, n);
   /* refit on inliers with EPnP (double inputs) */
@@ -1307,8 +1338,11 @@ static void repro_errors(const cam_t* k, int n, const float* wld_f, const float*
  * normalised over them (:172-243, HuberLoss(0.001), <= 20 iterations) -> keep the EPnP pose when
  * the refined reprojection sum over ALL points is larger (:142-146).  One inlier: the
  * reference's np.squeeze leaves a 1-D array and obj_pts[idx, 0] raises IndexError (status NO_FG,
- * a zero pose, as SpeedEval maps it); no inliers: an empty Ceres problem leaves the camera as it
- * is (parity unpinned: OpenCV's undistortPoints on zero points is outside the reference's runs). */
+ * a zero pose, as SpeedEval maps it); no inliers: the reference's control flow (run with the
+ * oracle's primitives, tests/golden/solver_front_ref.npz: 33 of 96 images) builds an empty Ceres
+ * problem and keeps the EPnP pose, status OK -- unpinned only in whether OpenCV 4.4's
+ * undistortPoints accepts the empty point set (if it raised cv2.error, SpeedEval would log a zero
+ * pose). */
 static int epnp_ceres(const cam_t* k, int nl, const float* wld_f, const float* img_f, const double* wld_d,
                       const double* img_d, const double* sig_d, float th, double* rvec, double* t, uint32_t* inl) {
   epnp_solve(k, nl, wld_d, img_d, 1, rvec, t);
@@ -1325,7 +1359,7 @@ static int epnp_ceres(const cam_t* k, int nl, const float* wld_f, const float* i
       m++;
     }
   if (m == 1) return ST_NO_FG;
-  if (m == 0) return ST_OK;
+  if (m == 0) return ST_OK;   /* the EPnP pose (see above: parity unpinned against OpenCV itself) */
   double r2[3] = {rvec[0], rvec[1], rvec[2]}, t2[3] = {t[0], t[1], t[2]};
   sigma_lm(k, m, wi, ii, si, 0.001, r2, t2);
   repro_errors(k, nl, wld_f, img_f, r2, t2, err);
@@ -1374,6 +1408,8 @@ int oracle_pnp_one(const float* pts, const float* probs, const float* sigmas, in
                    int* n_corr, int* corr_label, uint32_t* inlier_mask) {
   cam_t k = {Kmat[0], Kmat[4], Kmat[2], Kmat[5]};
   int order[MAXN], best_q[MAXN], nl = 0;
+  memset(&g_trace, 0, sizeof g_trace);
+  g_trace.epnp_pick = g_trace.ransac_best_iter = g_trace.ransac_margin_point = -1;
   float best_s[MAXN];
   *n_corr = 0;
   *inlier_mask = 0;
@@ -1458,6 +1494,16 @@ int oracle_pnp_one(const float* pts, const float* probs, const float* sigmas, in
   for (int i = 0; i < 4; ++i) quat[i] = qf[i];
   for (int i = 0; i < 3; ++i) tvec[i] = t[i];
   return status;
+}
+
+/* the decision trace of the last oracle_pnp_one call, packed as doubles:
+ * [epnp_err1, epnp_err2, epnp_err3, epnp_pick, epnp_calls, ransac_best_iter, ransac_inliers,
+ *  ransac_iters, ransac_mask, ransac_margin_point, ransac_margin_px] */
+void oracle_last_trace(double* out) {
+  for (int w = 0; w < 3; ++w) out[w] = g_trace.epnp_err[w];
+  out[3] = g_trace.epnp_pick; out[4] = g_trace.epnp_calls; out[5] = g_trace.ransac_best_iter;
+  out[6] = g_trace.ransac_inliers; out[7] = g_trace.ransac_iters; out[8] = g_trace.ransac_mask;
+  out[9] = g_trace.ransac_margin_point; out[10] = g_trace.ransac_margin_px;
 }
 
 /* batch wrapper */

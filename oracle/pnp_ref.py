@@ -48,6 +48,7 @@ def lib():
         _lib.oracle_np_sum_f32.argtypes = [P, ctypes.c_int]
         _lib.oracle_np_sum_f32.restype = ctypes.c_float
         _lib.oracle_speed_score.argtypes = [P, P, P, P, P, P]
+        _lib.oracle_last_trace.argtypes = [P]
     return _lib
 
 
@@ -74,6 +75,32 @@ def pnp_batch(points, probs, K, world, mode=MODE_RANSAC_P3P_LM, repro=20.0, sigm
                            _p(out["corr_label"]), _p(out["inlier_mask"]),
                            _p(None if repro_per_image is None else np.ascontiguousarray(repro_per_image, np.float32)))
     return out
+
+
+TRACE_FIELDS = ("epnp_err1", "epnp_err2", "epnp_err3", "epnp_pick", "epnp_calls", "ransac_best_iter",
+                "ransac_inliers", "ransac_iters", "ransac_mask", "ransac_margin_point", "ransac_margin_px")
+
+
+def pnp_trace(points, probs, K, world, mode=MODE_RANSAC_P3P_LM, repro=20.0, iters=100, conf=0.99):
+    """Per image, the solver's discrete decisions (oracle/pnp_ref.c trace_t): the last EPnP
+    solve's three beta-approximation errors and pick, the RANSAC best model's iteration, inlier
+    count / mask and the point nearest the threshold.  Returns (pnp_batch result, list of dicts)."""
+    points = np.ascontiguousarray(points, np.float32)
+    probs = np.ascontiguousarray(probs, np.float32)
+    res, tr = [], []
+    for b in range(points.shape[0]):
+        res.append(pnp_batch(points[b:b + 1], probs[b:b + 1], K, world, mode=mode, repro=repro, iters=iters, conf=conf))
+        t = np.zeros(len(TRACE_FIELDS))
+        lib().oracle_last_trace(_p(t))
+        d = dict(zip(TRACE_FIELDS, t.tolist()))
+        for k in ("epnp_pick", "epnp_calls", "ransac_best_iter", "ransac_inliers", "ransac_iters", "ransac_mask",
+                  "ransac_margin_point"):
+            d[k] = int(d[k])
+        tr.append(d)
+    if not res:
+        return pnp_batch(points, probs, K, world, mode=mode, repro=repro, iters=iters, conf=conf), tr
+    out = {k: np.concatenate([r[k] for r in res]) for k in res[0]}
+    return out, tr
 
 
 def repro_th(area, input_size=256):

@@ -176,166 +176,6 @@ int launch(const BtailArgs& a, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
-// ---------------------------------------------------------------- split-N form (layers 2 and 3)
-// The layer-2 / layer-3 boundaries: K1 = 128 / 256 conv3 inputs, N1 = 512 / 1024 block outputs,
-// N2 = 128 / 256 next-conv1 outputs.  W3 + W1 (256 KiB / 1 MiB) do not fit in LDS, so y is
-// produced NC columns at a time: per 128-row block (8 waves x 16 rows) the workgroup streams
-// chunk c of both weights -- W3 rows c*NC .. +NC (all K1 columns) and W1 columns c*NC .. +NC
-// (all N2 rows), 48-64 KiB -- into one of two LDS stages (global_load_lds, the next chunk in flight
-// while this one is multiplied), computes y[:, chunk] = relu(A . W3c^T + b3 + R) in the C^T form,
-// stores it and feeds it from registers into z += y[:, chunk] . W1c^T (W1's columns in
-// spe_btail_perm order, as above).  z = relu(z + b1) is stored after the last chunk.  y is
-// written once and never read back; the residual chunk of the next chunk is loaded before this
-// one is multiplied.  Persistent workgroups, one per CU.
-template <int K1, int N1, int N2, int NC>
-__global__ __launch_bounds__(NT, 1) void btail_split_kernel(BtailArgs a, int row_blocks) {
-  constexpr int KB1 = K1 * 2, KF1 = K1 / 32;           // W3c row bytes, first-product K fragments
-  constexpr int KBC = NC * 2;                          // W1c row bytes (second-product K = NC)
-  constexpr int JC = NC / 16, J2 = N2 / 16, KC = NC / 32;
-  constexpr int W3C = NC * KB1, W1C = N2 * KBC, STG = W3C + W1C;
-  constexpr int NCH = N1 / NC;
-  static_assert(STG % (1024 * NW) == 0 && 2 * STG <= 131072, "whole DMA pieces per wave, two stages in LDS");
-  __shared__ __attribute__((aligned(1024))) char wst[2 * STG];
-  __shared__ __attribute__((aligned(16))) float sb3[N1], sb1[N2];
-
-  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int fg = lane >> 4, fr = lane & 15;
-  for (int i = tid; i < N1; i += NT) sb3[i] = a.b3[i];
-  for (int i = tid; i < N2; i += NT) sb1[i] = a.b1[i];
-  auto w_addr = [](int n, int chunk, int KB) { return wkey_addr(n, chunk, KB); };
-  // chunk c of both weights -> stage st: 64 pieces of 1 KiB, 8 per wave (W3c then W1c, each a
-  // linear LDS image per wave-instruction with the swizzle applied on the source)
-  auto issue = [&](int c, int st) {
-#pragma unroll
-    for (int i = 0; i < STG / 1024 / NW; ++i) {
-      const int q = wid * (STG / 1024 / NW) + i, o = q * 1024 + lane * 16;
-      const char* src;
-      if (o < W3C) {
-        const int n = o / KB1, within = o - n * KB1;
-        const int ch = (within >> 4) ^ (n & wkey_mask(KB1));
-        src = (const char*)a.w3 + (size_t)(c * NC + n) * a.ld3 * 2 + ch * 16;
-      } else {
-        const int o2 = o - W3C, n = o2 / KBC, within = o2 - n * KBC;
-        const int ch = (within >> 4) ^ (n & wkey_mask(KBC));
-        src = (const char*)a.w1 + (size_t)n * a.ld1 * 2 + (size_t)c * NC * 2 + ch * 16;
-      }
-      __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(wst + st * STG + q * 1024), 16, 0, 0);
-    }
-  };
-
-  const int G = gridDim.x;
-  int rb = xcd_remap(blockIdx.x, G);
-  if (rb >= row_blocks) return;
-  auto row_of = [&](int r) { const int m = r * 128 + wid * 16 + fr; return m < a.M ? m : a.M - 1; };
-  auto load_r = [&](int r, int c, u32x2 (&rr)[JC]) {
-    const char* p = (const char*)a.R + ((size_t)row_of(r) * a.ldr + c * NC + 4 * fg) * 2;
-#pragma unroll
-    for (int j = 0; j < JC; ++j) rr[j] = ld8(p + j * 32);
-  };
-  // steps = (row block, chunk) pairs in order; stage = step & 1
-  int step = 0;
-  issue(0, 0);
-  u32x2 r0[JC], r1[JC];
-  load_r(rb, 0, r0);
-  for (;;) {
-    const int m = rb * 128 + wid * 16 + fr;
-    const bool ok = m < a.M;
-    u32x4 af[KF1];
-    {
-      const char* p = (const char*)a.A + (size_t)row_of(rb) * a.lda * 2 + fg * 16;
-#pragma unroll
-      for (int kf = 0; kf < KF1; ++kf) af[kf] = ld16(p + kf * 64);
-    }
-    f32x4 acc2[J2];
-#pragma unroll
-    for (int j = 0; j < J2; ++j) acc2[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    const int rbn = rb + G;
-    for (int c = 0; c < NCH; c += 2) {
-      // two chunks per iteration so the residual registers alternate without copies
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const int cc = c + h;
-        u32x2 (&rc)[JC] = h ? r1 : r0;
-        u32x2 (&rn)[JC] = h ? r0 : r1;
-        // chunk cc's weights and residual (issued a chunk earlier) landed; then the barrier: chunk
-        // cc in stage step & 1 for everyone, the other stage free for chunk cc+1 (or the next
-        // row block's chunk 0), whose DMA and residual go out before this chunk's MFMAs
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-        if (cc + 1 < NCH) {
-          issue(cc + 1, (step + 1) & 1);
-          load_r(rb, cc + 1, rn);
-        } else if (rbn < row_blocks) {
-          issue(0, (step + 1) & 1);
-          load_r(rbn, 0, rn);
-        }
-        const char* w3s = wst + (step & 1) * STG;
-        const char* w1s = w3s + W3C;
-        f32x4 acc[JC];
-#pragma unroll
-        for (int j = 0; j < JC; ++j) acc[j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        // (compiler fences between K fragments: hoisting every weight read of the chunk ahead of
-        // its MFMAs would pin KF1 x JC fragments -- spills in the layer-3 form)
-#pragma unroll
-        for (int kf = 0; kf < KF1; ++kf) {
-          const bf16x8 av = __builtin_bit_cast(bf16x8, af[kf]);
-#pragma unroll
-          for (int j = 0; j < JC; ++j) {
-            const bf16x8 w = __builtin_bit_cast(bf16x8, ld16(w3s + w_addr(16 * j + fr, 4 * kf + fg, KB1)));
-            acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, av, acc[j], 0, 0, 0);
-          }
-          if (kf % 2 == 1) asm volatile("" ::: "memory");
-        }
-        // y = relu(acc + b3 + R) for columns cc*NC + 16j + 4fg + r: store, pack
-        char* yp = (char*)a.y + ((size_t)m * a.ldy + cc * NC + 4 * fg) * 2;
-        u32x2 yw[JC];
-#pragma unroll
-        for (int j = 0; j < JC; ++j) {
-          const f32x4 bv = *reinterpret_cast<const f32x4*>(sb3 + cc * NC + 16 * j + 4 * fg);
-          float v[4] = {acc[j][0] + bv[0] + __uint_as_float(rc[j].x << 16),
-                        acc[j][1] + bv[1] + __uint_as_float(rc[j].x & 0xffff0000u),
-                        acc[j][2] + bv[2] + __uint_as_float(rc[j].y << 16),
-                        acc[j][3] + bv[3] + __uint_as_float(rc[j].y & 0xffff0000u)};
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-          yw[j] = u32x2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])};
-          if (ok) st8(yp + j * 32, yw[j]);
-        }
-#pragma unroll
-        for (int kc = 0; kc < KC; ++kc) {
-          const bf16x8 yv = __builtin_bit_cast(bf16x8, u32x4{yw[2 * kc].x, yw[2 * kc].y, yw[2 * kc + 1].x, yw[2 * kc + 1].y});
-#pragma unroll
-          for (int j = 0; j < J2; ++j) {
-            const bf16x8 w = __builtin_bit_cast(bf16x8, ld16(w1s + w_addr(16 * j + fr, 4 * kc + fg, KBC)));
-            acc2[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(w, yv, acc2[j], 0, 0, 0);
-            if (j % 8 == 7) asm volatile("" ::: "memory");
-          }
-        }
-        ++step;
-      }
-    }
-    char* zp = (char*)a.z + ((size_t)m * a.ldz + 4 * fg) * 2;
-#pragma unroll
-    for (int j = 0; j < J2; ++j) {
-      const f32x4 bv = *reinterpret_cast<const f32x4*>(sb1 + 16 * j + 4 * fg);
-      float v[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = fmaxf(acc2[j][e] + bv[e], 0.f);
-      if (ok) st8(zp + j * 32, u32x2{pack_bf16x2(v[0], v[1]), pack_bf16x2(v[2], v[3])});
-    }
-    rb = rbn;
-    if (rb >= row_blocks) break;
-  }
-}
-
-template <int K1, int N1, int N2, int NC>
-int launch_split(const BtailArgs& a, hipStream_t s) {
-  const int row_blocks = (a.M + 127) / 128;
-  const int G = std::min(spe_cu_count(), row_blocks);
-  hipLaunchKernelGGL((btail_split_kernel<K1, N1, N2, NC>), dim3(G), dim3(NT), 0, s, a, row_blocks);
-  return (int)hipGetLastError();
-}
-
 }  // namespace
 
 // K-order permutation of the second product's weights (header above): stored column
@@ -350,26 +190,10 @@ bool spe_btail_enabled() {
   return on != 0;
 }
 
-// the split-N form for the layer-2 / layer-3 boundaries, off by default (SPE_BTAIL_SPLIT=1 turns it
-// on): measured slower than the separate launches -- conv.1x1 1.96 -> 2.19 ms per step on one box
-// (scripts/gpu_r4_h.sh).  With 16 rows per wave every 1 KiB weight fragment read from LDS feeds
-// one MFMA, 512 B/clk per CU against the LDS's 256: the chunks run LDS-bound at about twice their
-// MFMA time, while the separate weight-stationary streaming GEMMs (gemm_stream.hip) reuse each
-// fragment across the wave's row fragments.  More rows per wave need more accumulators than the
-// layer-3 form (N2 = 256) has registers for.
-bool spe_btail_split_enabled() {
-  static const int on = [] { const char* e = getenv("SPE_BTAIL_SPLIT"); return e ? atoi(e) : 0; }();
-  return on != 0 && spe_btail_enabled();
-}
-
 // 1 = not a problem for this kernel
 int spe_launch_btail(const BtailArgs& a, hipStream_t s) {
   if (a.M <= 0) return 0;
   if (a.lda % 8 || a.ldy % 4 || a.ldz % 4 || (a.R && a.ldr % 4) || a.ld3 < a.k1 || a.ld1 < a.n1) return 1;
-  // layers 2 / 3 (split-N, with the identity residual)
-  if (a.R && a.k1 == 128 && a.n1 == 512 && a.n2 == 128) return launch_split<128, 512, 128, 128>(a, s);
-  if (a.R && a.k1 == 128 && a.n1 == 512 && a.n2 == 256) return launch_split<128, 512, 256, 64>(a, s);   // layer 2 -> 3
-  if (a.R && a.k1 == 256 && a.n1 == 1024 && a.n2 == 256) return launch_split<256, 1024, 256, 64>(a, s);
   if (a.n1 != N1) return 1;
   if (a.k1 == 64 && a.n2 == 64 && a.R) return launch<64, 64, true>(a, s);
   if (a.k1 == 64 && a.n2 == 128 && a.R) return launch<64, 128, true>(a, s);

@@ -87,9 +87,8 @@ int spe_debug_upconv(void* stream, int dtype, const void* z, void* out, int ldo,
 
 int spe_debug_xattn(void* stream, const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* u,
                     int ldu, const void* wv, const float* bv, void* o, int ldo, int B, int Q, int T, int splits,
-                    float* partial_scratch, int k_shared) {
+                    float* partial_scratch) {
   XattnArgs a{};
-  a.k_shared = k_shared ? 1 : 0;
   a.q = q; a.ldq = ldq; a.k = k; a.ldk = ldk; a.v = v; a.ldv = ldv; a.u = u; a.ldu = ldu;
   a.wv = wv; a.bv = bv; a.o = o; a.ldo = ldo;
   a.B = B; a.Q = Q; a.T = T; a.splits = splits > 0 ? splits : spe_xattn_splits(B, Q, T);
@@ -128,18 +127,6 @@ int spe_debug_decproj(void* stream, void* tgt, int ldt, const void* x, int ldx, 
   a.tgt = tgt; a.ldt = ldt; a.x = x; a.ldx = ldx; a.B = B; a.Q = Q; a.wo = wo; a.ldo = ldo; a.bo = bo; a.g = g; a.b = b;
   const int rc = spe_launch_decproj(a, (hipStream_t)stream);
   return rc != 0 ? spe_fail(SPE_E_LAUNCH, "decproj launch rejected its arguments") : 0;
-}
-
-int spe_debug_btail_n1(void* stream, const void* a, int lda, int k1, const void* r, const void* w3, int ld3,
-                       const float* b3, void* y, const void* w1p, int ld1, const float* b1, void* z, int n1, int n2,
-                       int M) {
-  if (!a || !w3 || !b3 || !y || !w1p || !b1 || !z || M < 0 || n1 <= 0) return spe_fail(SPE_E_ARG, "bad argument");
-  BtailArgs t{};
-  t.A = a; t.lda = lda; t.k1 = k1; t.R = r; t.ldr = n1;
-  t.w3 = w3; t.ld3 = ld3; t.b3 = b3; t.y = y; t.ldy = n1; t.n1 = n1;
-  t.w1 = w1p; t.ld1 = ld1; t.b1 = b1; t.z = z; t.ldz = n2; t.n2 = n2; t.M = M;
-  const int rc = spe_launch_btail(t, (hipStream_t)stream);
-  return rc != 0 ? spe_fail(SPE_E_LAUNCH, "btail launch rejected its arguments") : 0;
 }
 
 int spe_debug_btail_perm(int k) { return spe_btail_perm(k); }

@@ -56,7 +56,6 @@ __global__ __launch_bounds__(NT) void decsa_kernel(DecSaArgs a) {
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int b = blockIdx.x, Q = a.Q, RT = (Q + 15) / 16;
   bf16* tg = (bf16*)a.tgt + (size_t)b * Q * a.ldt;
-  if (a.stop == 5) return;
 
   // ---- 1. q | k | v: 48 column tiles of 16, 6 per wave (tile wid + 8 j); the W fragments are
   // requested first, so their round trip overlaps the tgt rows' (which stage through LDS)
@@ -96,7 +95,6 @@ __global__ __launch_bounds__(NT) void decsa_kernel(DecSaArgs a) {
       st8(qkv + m * QKVLD + ncol, u32x2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])});
     }
   }
-  if (a.stop == 1) return;
   // the out-projection's W fragments travel during the attention
   constexpr int CT3 = D / 16 / NW;
   u32x4 wf3[CT3][8];
@@ -143,7 +141,6 @@ __global__ __launch_bounds__(NT) void decsa_kernel(DecSaArgs a) {
   }
   __syncthreads();
 
-  if (a.stop == 2) return;
   // ---- 3. out-projection + bo + residual (registers), then the fp32 rows over q|k|v
   f32x4 yo[CT3][QMAX / 16];
 #pragma unroll
@@ -164,7 +161,6 @@ __global__ __launch_bounds__(NT) void decsa_kernel(DecSaArgs a) {
     }
   }
   __syncthreads();                              // every wave done reading the attention output
-  if (a.stop == 3) return;
 #pragma unroll
   for (int j = 0; j < CT3; ++j) {
     const int n0 = (wid * CT3 + j) * 16;
@@ -265,12 +261,6 @@ int spe_launch_decsa(const DecSaArgs& a, hipStream_t s) {
   if (a.Q < 1 || a.Q > QMAX || a.ldt % 8 || a.ldqk % 8 || a.ldv % 8 || a.ldo % 8 || !a.tgt || !a.wqk || !a.wv ||
       !a.wo || !a.bqk || !a.bv || !a.bo || !a.qpos || !a.g || !a.b)
     return 1;
-  DecSaArgs b = a;
-  // SPE_DECSA_STOP (kbench phase timing only): 5 = return at entry, 1/2/3 = after the projections
-  // / attention / out-projection (kbench decsa, B = 64, Q = 11: 5.1 / 14.8 / ~20 / ~20.5 us of 22;
-  // a loads-only stop, 12.4 us, kept the 48 fragments live past their use and spilled the kernel)
-  static const int stop = [] { const char* e = getenv("SPE_DECSA_STOP"); return e ? atoi(e) : 0; }();
-  b.stop = stop;
-  hipLaunchKernelGGL(decsa_kernel, dim3(b.B), dim3(NT), 0, s, b);
+  hipLaunchKernelGGL(decsa_kernel, dim3(a.B), dim3(NT), 0, s, a);
   return (int)hipGetLastError();
 }

@@ -52,15 +52,13 @@ int run_other(spe_model* m, const char* kind, double flops, double bytes, hipStr
   return rc;
 }
 
-// fp32x3 models: split-bf16 MFMA unless the launch kind is listed in x3_exact.  fp32x6 models run
-// the decoder's attention (self and cross, Q = 11 query rows: ~1 % of the model's flops) on the
-// exact-f32 kernels: the per-stage study found its split-bf16 scores to carry most
-// of the mode's keypoint error (1.6e-4 -> 5.7e-5 on the bench weights at equal step time).
+// fp32x3 models: split-bf16 MFMA.  fp32x6 models run the decoder's attention (self and cross,
+// Q = 11 query rows: ~1 % of the model's flops) on the exact-f32 kernels: the per-stage study
+//  found its split-bf16 scores to carry most of the mode's keypoint error
+// (1.6e-4 -> 5.7e-5 on the bench weights at equal step time).
 static bool x3_for(const spe_model* m, const char* kind) {
   if (!m->x3) return false;
   if (m->x6 && std::strncmp(kind, "attn.dec", 8) == 0) return false;
-  for (const auto& p : m->x3_exact)
-    if (std::strncmp(kind, p.c_str(), p.size()) == 0) return false;
   return true;
 }
 
@@ -191,11 +189,6 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   const float scale = 1.0f / std::sqrt(32.0f);
   const int Mt = B * T;
   const bool xa = spe_use_xattn(m);
-  // SPE_XATTN_SHARED=1: xattn reads pos (shared by all images, L2-resident) instead of a
-  // materialised memory + pos -- half the HBM bytes, the score reduction split over each wave
-  // pair and exchanged through LDS, but measured slower: 0.070-0.074 vs 0.058 ms per layer
-  // (kbench, B = 64; the kernel is not HBM-bound at this size)
-  static const bool xshared = [] { const char* e = getenv("SPE_XATTN_SHARED"); return e ? atoi(e) != 0 : false; }();
   if (stages & SPE_STAGE_BACKBONE) {
   // ---------------- backbone (REV/models/backbone.py:133-149)
   const bool pairs = m->stem.Cin == 4;                 // bf16: pair-packed stem (registry.cpp)
@@ -405,7 +398,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
     }
     if (use_fused_ffn(m)) {
       // the last layer also emits memory + pos for the cross-K projection (xattn adds pos itself)
-      const bool last = &e == &m->enc.back() && !(xa && xshared);
+      const bool last = &e == &m->enc.back();
       CK(run_ffn(m, "ffn.enc", e.l1, e.l2, e.n2g, e.n2b, P(w.src), Mt, s, last ? m->pos : nullptr,
                  last ? P(w.srcpos) : nullptr, T));
     } else {
@@ -515,8 +508,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR, s));
       XattnArgs x{};
       x.q = P(w.xq); x.ldq = 8 * d;
-      if (xshared) { x.k = m->pos; x.ldk = d; x.k_shared = 1; }   // K = memory + pos: pos from L2, not HBM
-      else { x.k = P(w.srcpos); x.ldk = d; }
+      x.k = P(w.srcpos); x.ldk = d;
       x.v = P(w.src); x.ldv = d;
       x.wv = e.xv.w; x.bv = e.xv.bias;
       x.o = P(w.dao); x.ldo = d;
@@ -703,21 +695,6 @@ int spe_speed_score(void* stream, const float* quat, const double* tvec, const d
   if (!quat || !tvec || !q_gt || !t_gt || !s_t || !s_q || B < 0) return fail(SPE_E_ARG, "bad argument");
   CK(spe_launch_score(quat, tvec, q_gt, t_gt, B, s_t, s_q, (hipStream_t)stream));
   return 0;
-}
-
-int spe_stream_create_cu_mask(const uint32_t* mask, int words, void** stream) {
-  if (!mask || words <= 0 || !stream) return fail(SPE_E_ARG, "bad argument");
-  hipStream_t s = nullptr;
-  const hipError_t e = hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask);
-  if (e != hipSuccess) return fail((int)e, "hipExtStreamCreateWithCUMask failed");
-  *stream = s;
-  return 0;
-}
-
-int spe_stream_destroy(void* stream) {
-  if (!stream) return fail(SPE_E_ARG, "null stream");
-  const hipError_t e = hipStreamDestroy((hipStream_t)stream);
-  return e == hipSuccess ? 0 : fail((int)e, "hipStreamDestroy failed");
 }
 
 int spe_model_profile_begin(spe_model* m, const char* kind_prefix) {

@@ -694,11 +694,10 @@ int launch_bn(const GemmArgs& g, int mode, hipStream_t s) {
       hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_LINEAR, false, false, 2, true>), grid, block, 0, s, g);
     return (int)hipGetLastError();
   }
-  // SPE_GEMM2_PIN=0: residual-free convs on the compiler-scheduled loop; SPE_GEMM2_BUF=0: the
-  // other convs and linear problems staged with global_load_lds instead of buffer loads (A/B knobs)
+  // SPE_GEMM2_PIN=0: residual-free convs on the compiler-scheduled loop (A/B knob).  The other
+  // convs and linear problems stage with global_load_lds (buffer-load staging without the pinned
+  // schedule measured neutral, 4806 vs 4786 img/s, and was removed)
   static const int pin = [] { const char* e = getenv("SPE_GEMM2_PIN"); return e ? atoi(e) : 1; }();
-  // (buffer staging without the pinned schedule measured neutral: 4806 vs 4786 img/s; off)
-  static const int buf = [] { const char* e = getenv("SPE_GEMM2_BUF"); return e ? atoi(e) : 0; }();
   constexpr long long LIM = (1ll << 31) - (1 << 20);          // 32-bit buffer offsets
   const bool bfits = (long long)g.N * g.ldb * 2 < LIM;
   if (mode == GEMM_CONV) {
@@ -708,16 +707,12 @@ int launch_bn(const GemmArgs& g, int mode, hipStream_t s) {
     const bool fits = abytes < LIM && bfits;
     if (pin && !g.R && kpos_scalar && fits)
       hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_CONV, false, false, 2, false, true>), grid, block, 0, s, g);
-    else if (buf && kpos_scalar && fits)
-      hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_CONV, false, false, 2, false, false, true>), grid, block, 0, s, g);
     else
       hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_CONV, false>), grid, block, 0, s, g);
   } else {
-    const bool fits = (long long)g.M * g.lda * 2 < LIM && bfits;
     if constexpr (BN == 256) {
       if (g.ln_g) {
-        if (buf && fits) hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_LINEAR, true, false, 2, false, false, true>), grid, block, 0, s, g);
-        else hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_LINEAR, true>), grid, block, 0, s, g);
+        hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_LINEAR, true>), grid, block, 0, s, g);
         return (int)hipGetLastError();
       }
     }
@@ -727,8 +722,7 @@ int launch_bn(const GemmArgs& g, int mode, hipStream_t s) {
         return (int)hipGetLastError();
       }
     }
-    if (buf && fits) hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_LINEAR, false, false, 2, false, false, true>), grid, block, 0, s, g);
-    else hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_LINEAR, false>), grid, block, 0, s, g);
+    hipLaunchKernelGGL((gemm2_kernel<BN, GEMM_LINEAR, false>), grid, block, 0, s, g);
   }
   return (int)hipGetLastError();
 }
@@ -932,12 +926,8 @@ int spe_launch_gemm2(const GemmArgs& g, int mode, hipStream_t s) {
   }
   if (use_st1(g, mode) && g.act <= ACT_RELU && !g.res_post) return launch_st1(g, s);
   int bn = (g.N <= 64 && g.vt_T == 0) ? 64 : g.N <= 128 ? 128 : 256;   // BN 64 has no V^T store
-  {
-    // grids of 256-wide tiles that leave CUs idle in their last round: SPE_GEMM2_NARROW = the
-    // tile count below which convs take 128-wide tiles (A/B knob, default off)
-    static const int narrow = [] { const char* e = getenv("SPE_GEMM2_NARROW"); return e ? atoi(e) : 0; }();
-    if (bn == 256 && mode == GEMM_CONV && ((g.M + BM - 1) / BM) * ((g.N + 255) / 256) < narrow) bn = 128;
-  }
+  // (128-wide tiles for the under-filled 256-wide conv grids measured neutral in the pipelined
+  // bench -- the other streams fill the idle CUs -- and were removed)
   const int tiles = ((g.M + BM - 1) / BM) * ((g.N + bn - 1) / bn);
   // too few tiles for the large-tile kernel: the 128x128 kernel.  (169 tiles of 256x256 on the
   // layer3 convs, M = B*26*26, still beat 676 tiles of the 128x128 kernel by 12-18 %.)

@@ -97,13 +97,10 @@ __global__ __launch_bounds__(256, OCC) void sgemm_kernel(GemmArgs g, int ns_coun
   }
   auto w_addr = [&](int n, int chunk) { return wkey_addr(n, chunk, KB); };
 
-  // first row of row tile t.  With a row-periodic residual (r_period = tokens per image, the
-  // q/k projection's pos . W^T table) tile t covers image t % nimg at token block t / nimg: the
-  // workgroups, which advance through t together, then work on the same few token blocks of every
-  // image at once, so the table rows they add stay hot in L2 instead of streaming the whole
-  // table once per image (g.ns_rmap = nimg, set by the launcher under SPE_SG_RMAP=1; 0 = tile order).
-  const int nimg = g.ns_rmap;
-  auto row0 = [&](int t) { return nimg > 0 ? (t % nimg) * g.r_period + (t / nimg) * TR : t * TR; };
+  // first row of row tile t.  (An image-interleaved tile order that kept a row-periodic
+  // residual's table rows hot in L2 measured neutral-to-slower on the q/k projection and was
+  // removed)
+  auto row0 = [&](int t) { return t * TR; };
 
   // A fragments of one row tile: lane (fg, fr) holds row fr of fragment rf, K chunk 4kf + fg
   auto load_a = [&](int t, u32x4 (&a)[RF][KF]) {
@@ -319,15 +316,7 @@ int launch_k(const GemmArgs& g, hipStream_t s) {
   const int row_tiles = (g.M + RF * 16 - 1) / (RF * 16), nsc = g.N / BN;
   const int G = (spe_cu_count() * OCC / nsc) * nsc;
   if ((long)row_tiles < 2L * (G / nsc) * 4) return 1;    // fewer than two tiles per wave
-  GemmArgs ga = g;
-  ga.ns_rmap = 0;
-  // SPE_SG_RMAP=1: the image-interleaved tile order for row-periodic residuals -- measured
-  // neutral-to-slower on the q/k projection (0.645-0.651 vs 0.623-0.634 ms per step): the
-  // table was not what bounds it
-  static const bool rmap_on = [] { const char* e = getenv("SPE_SG_RMAP"); return e && atoi(e) != 0; }();
-  if (rmap_on && HAS_R && g.r_period > 0 && g.r_period % (RF * 16) == 0 && g.M % g.r_period == 0)
-    ga.ns_rmap = g.M / g.r_period;
-  hipLaunchKernelGGL((sgemm_kernel<K, BN, RF, OCC, NB, HAS_R, EPI, CP>), dim3(G), dim3(256), 0, s, ga, nsc, row_tiles);
+  hipLaunchKernelGGL((sgemm_kernel<K, BN, RF, OCC, NB, HAS_R, EPI, CP>), dim3(G), dim3(256), 0, s, g, nsc, row_tiles);
   spe_gemm_last_path = 2;
   return (int)hipGetLastError();
 }

@@ -111,10 +111,6 @@ struct spe_model {
   int family = 0;            // 0: DETR (REV), 1: RT-DETR (UNC)
   int x3 = 0;                // fp32 model computed with split-bf16 MFMA (SPE_DTYPE_F32X3_, _F32X6_)
   int x6 = 0;                // ... with the GEMMs / convs on the three-way split path (SPE_DTYPE_F32X6_)
-  // fp32x3 models: launch kinds (prefixes, e.g. "attn.dec", "gemm.enc") that run the exact-f32
-  // kernels instead of the split-bf16 ones -- the per-stage precision study of DESIGN.md §4
-  // (SPE_X3_EXACT="kind,kind,..." read at spe_model_create)
-  std::vector<std::string> x3_exact;
   // fp32x6 models: fp32 weight block -> (its bf16 planes [3][rows][Kpad] h, m, l, rows), written
   // at finalize next to each packed weight (upload_rows) so the x6 GEMM never splits weights
   std::map<const void*, std::pair<const void*, int>> w6;

@@ -398,11 +398,10 @@ int build_device(spe_model* m) {
       // conv1 of the blocks whose input is a layer-1 block output (blocks 1-3: layer 1 blocks 1
       // and 2, layer 2 block 0) as the second product of the previous block's fused tail:
       // columns permuted into spe_btail_perm order (btail.hip)
-      // (layers 2 / 3: the split-N tail, btail.hip, for every block whose input is the previous
-      // block's output -- layer 2 blocks 1-3, layer 3 blocks 0-5)
+      // (the layer-2 / layer-3 boundaries stay separate launches: their weights do not fit in
+      // LDS, and a split-N form streaming them through LDS measured slower)
       const int gi = li == 0 ? k : (li == 1 && k == 0 ? 3 : -1);
-      const bool split = li >= 1 && !(li == 1 && k == 0) && spe_btail_split_enabled();
-      if (m->esz == 2 && spe_btail_enabled() && ((gi >= 1 && blk.c1.K == 256) || split)) {
+      if (m->esz == 2 && spe_btail_enabled() && gi >= 1 && blk.c1.K == 256) {
         std::vector<float> w1, b1;
         fold_conv(m, p + ".conv1.weight", p + ".bn1", "", w1, b1);
         const int n = blk.c1.N, K = blk.c1.K;
@@ -630,16 +629,6 @@ int spe_model_create(const spe_model_config* cfg, spe_model** out) {
   m->x6 = cfg->dtype == SPE_DTYPE_F32X6_;
   m->x3 = cfg->dtype == SPE_DTYPE_F32X3_ || m->x6;
   if (m->x3) { m->cfg.dtype = SPE_DTYPE_F32_; if (m->cfg.attn_dtype) m->cfg.attn_dtype = SPE_DTYPE_F32_; }
-  if (m->x3)
-    if (const char* e = getenv("SPE_X3_EXACT")) {
-      std::string s(e);
-      for (size_t p = 0; p <= s.size();) {
-        size_t q = s.find(',', p);
-        if (q == std::string::npos) q = s.size();
-        if (q > p) m->x3_exact.push_back(s.substr(p, q - p));
-        p = q + 1;
-      }
-    }
   m->esz = cfg->dtype == SPE_DTYPE_BF16_ ? 2 : 4;
   m->spec = build_spec(*cfg);
   *out = m;

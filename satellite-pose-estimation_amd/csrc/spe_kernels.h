@@ -35,7 +35,6 @@ struct GemmArgs {
   void* S; int s_col0;             // fp32 models: columns n >= s_col0 stored instead as bf16 hi / lo planes for the
                                    // fp32x3 attention: rows -> hi [M][N - s_col0] then lo; head-transposed
                                    // (vt_T) -> hi in C's layout [vt_B][N][vt_T] then lo (s_col0 = 0)
-  int ns_rmap;                     // (set by gemm_stream.hip's launcher) image-interleaved tile order
 };
 bool spe_gemm_ln_fusable(const GemmArgs& g);   // the large-tile kernel can fuse ln_g/ln_b for g
 int spe_launch_gemm(const GemmArgs& g, int dtype, int mode, hipStream_t s);
@@ -74,7 +73,6 @@ struct BtailArgs {
 int spe_launch_btail(const BtailArgs& a, hipStream_t s);   // 1 = not applicable
 int spe_btail_perm(int k);
 bool spe_btail_enabled();
-bool spe_btail_split_enabled();
 int spe_launch_gemm2(const GemmArgs& g, int mode, hipStream_t s);   // 1 = not applicable
 int spe_launch_sgemm(const GemmArgs& g, int mode, hipStream_t s);   // 1 = not applicable
 int spe_launch_lnproj(const GemmArgs& g, hipStream_t s);             // 1 = not applicable (lnproj.hip)
@@ -110,14 +108,13 @@ int spe_launch_attention(const AttnArgs& a, int dtype, hipStream_t s);
 // pos [T][256], V = memory [T][256], q' pre-scaled into the exp2 domain.
 struct XattnArgs {
   const void* q; int ldq;          // q' rows b*Q + q, head h at columns [h*256, h*256 + 256)
-  const void* k; int ldk;          // memory + pos, rows b*T + t; k_shared: pos, rows t (K = v + k)
+  const void* k; int ldk;          // memory + pos, rows b*T + t
   const void* v; int ldv;          // memory, rows b*T + t
   void* u; int ldu;                // output rows b*Q + q, head h at columns [h*256, h*256 + 256)
   const void* wv; const float* bv; // optional: o_h = Wv_h u_h + bv_h written instead of u
   void* o; int ldo;                //   o rows b*Q + q, head h at columns [h*32, h*32 + 32)
   int B, Q, T, splits, tiles_per_split;
   float *pm, *pl, *pu;             // key-split partials [B][splits][8Q] (pu: x 256), required
-  int k_shared;                    // 1: k holds pos [T][256], the same for every image
 };
 int spe_xattn_splits(int B, int Q, int T);
 int spe_launch_xattn(const XattnArgs& a, hipStream_t s);
@@ -133,7 +130,6 @@ struct DecSaArgs {
   const void* wo; int ldo; const float* bo;      // out_proj [256][ldo]
   const float* g; const float* b;  // norm1
   float scale;                     // 1/sqrt(head_dim)
-  int stop;                        // (timing experiments only: set by the launcher from SPE_DECSA_STOP)
 };
 int spe_launch_decsa(const DecSaArgs& a, hipStream_t s);   // 1 = not applicable
 // tgt = LN(tgt + x . Wo^T + bo), one workgroup per image (decsa.hip; bf16, d = 256, Q <= 64)

@@ -26,16 +26,8 @@
 //   accumulator's) and V^T read transposed out of the row-major V tile by ds_read_b64_tr_b16
 //   in that same key order.
 // Each key split writes fp32 partials (m, l, unnormalised U) that a merge kernel combines.
-//
-// KS (k_shared, the model's mode): the key operand is memory + pos with pos [T][256] the same for
-// every image, so the kernel streams only the memory from HBM (the V tile, used twice) and the
-// shared pos rows (L2-resident across the batch's images), and forms the scores as
-// q' . mem + q' . pos in one fp32 MFMA chain -- half the HBM bytes of reading a materialised
-// memory + pos, and no bf16 rounding of that sum.
 #include "spe_common.h"
 #include "spe_kernels.h"
-
-#include <type_traits>
 
 namespace {
 
@@ -62,24 +54,18 @@ SPE_DEV void wait_vmcnt() { asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memor
 
 // K tile: chunk c of key row k at slot c ^ (k & 15) (the 16 keys of a ds_read_b128 lane group
 // hit distinct bank groups).  V tile: chunk c at slot c ^ ((k & 3) << 2), so the four key rows
-// of every ds_read_b64_tr_b16 block fall in four different 64-byte bank segments.  KS: both
-// tiles at c ^ f(k), f(k) = (k & 3) << 2 | (k >> 2) & 3 -- a bijection on 16 consecutive keys
-// (ds_read_b128: distinct bank groups) that also puts the four key rows of every
-// ds_read_b64_tr_b16 block (k0 % 4 == 0, chunk pair c0, c0 + 1 with c0 even) on four different
-// 32-byte pairs of one 128-byte window, so the memory tile serves the score reads and the
-// transposed value reads alike.
-template <bool KS> SPE_DEV int kkey(int key) { return KS ? ((key & 3) << 2) | ((key >> 2) & 3) : key & 15; }
-template <bool KS> SPE_DEV int vkey(int key) { return KS ? ((key & 3) << 2) | ((key >> 2) & 3) : (key & 3) << 2; }
-template <bool KS> SPE_DEV int k_off(int key, int c) { return key * 512 + ((c ^ kkey<KS>(key)) << 4); }
-template <bool KS> SPE_DEV int v_off(int key, int c) { return key * 512 + ((c ^ vkey<KS>(key)) << 4); }
+// of every ds_read_b64_tr_b16 block fall in four different 64-byte bank segments.
+SPE_DEV int kkey(int key) { return key & 15; }
+SPE_DEV int vkey(int key) { return (key & 3) << 2; }
+SPE_DEV int k_off(int key, int c) { return key * 512 + ((c ^ kkey(key)) << 4); }
+SPE_DEV int v_off(int key, int c) { return key * 512 + ((c ^ vkey(key)) << 4); }
 
 // 4 keys x 16 dims of the V tile, delivered transposed: lane i of each 16-lane group gets dim
 // d0 + i of keys k0 .. k0+3 (cdna_hip_programming.md T10); lane 4q+p addresses key k0+q, dims
 // d0 + 4p .. +3 (d0 % 16 == 0).  LDS byte address of this lane's block row:
-template <bool KS>
 SPE_DEV uint32_t v_tr_addr(uint32_t vbase, int k0, int d0, int lane16) {
   const int q = lane16 >> 2, p = lane16 & 3;
-  return vbase + v_off<KS>(k0 + q, (d0 >> 3) + (p >> 1)) + 8 * (p & 1);
+  return vbase + v_off(k0 + q, (d0 >> 3) + (p >> 1)) + 8 * (p & 1);
 }
 // Issued as inline asm: the compiler treats the ds_read_b64_tr_b16 builtin as aliasing the
 // tiles still in flight by LDS-DMA and drains them (vmcnt(0)) before it; the waits for these
@@ -90,11 +76,8 @@ SPE_DEV u32x2 ds_read_tr(uint32_t addr) {
   return r;
 }
 
-constexpr int XCH = 6 * 16 * 64 * 4;           // KS: the compute waves' partial-score exchange (24 KB)
-
-template <bool KS>
 __global__ __launch_bounds__(NT, 1) void xattn_kernel(XattnArgs a) {
-  __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES + (KS ? XCH : 0)];
+  __shared__ __attribute__((aligned(1024))) char lds[LDS_BYTES];
   const int tid = threadIdx.x, lane = tid & 63, wid = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int hh = lane >> 5, r32 = lane & 31, l16 = lane & 15, dg = 16 * ((lane >> 4) & 1);
   const int R = 8 * a.Q, ngroups = (R + RG - 1) / RG;
@@ -124,7 +107,7 @@ __global__ __launch_bounds__(NT, 1) void xattn_kernel(XattnArgs a) {
       qf[ks] = __builtin_bit_cast(bf16x8, live ? ld16(qp + 16 * ks + 8 * hh) : u32x4{0, 0, 0, 0});
   }
 
-  // ---- staging (loader waves): wave 6 the K tile (KS: the shared pos rows), wave 7 the V tile,
+  // ---- staging (loader waves): wave 6 the K tile, wave 7 the V tile,
   // 16 x 1 KB each (2 key rows per instruction)
   const char* zero = reinterpret_cast<const char*>(g_xzero);
   const bool isv = wid == 7;
@@ -136,8 +119,8 @@ __global__ __launch_bounds__(NT, 1) void xattn_kernel(XattnArgs a) {
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int key = 2 * i + (lane >> 5), s = lane & 31;
-      const int c = s ^ (isv ? vkey<KS>(key) : kkey<KS>(key));
-      const int row = (KS && !isv ? 0 : b * a.T) + key0 + key;
+      const int c = s ^ (isv ? vkey(key) : kkey(key));
+      const int row = b * a.T + key0 + key;
       const char* src = key0 + key < a.T ? src0 + ((size_t)row * ldsrc + c * 8) * 2 : zero;
       __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(st + i * 1024), 16, 0, 0);
     }
@@ -157,11 +140,8 @@ __global__ __launch_bounds__(NT, 1) void xattn_kernel(XattnArgs a) {
   // the q' loads must retire before the DMA stream starts (vmcnt is in-order; see ffn.hip)
 #pragma unroll
   for (int ks = 0; ks < 16; ++ks) asm volatile("" ::"v"(qf[ks]));
-  // KS: each image walks its split's tiles from its own starting offset, so the 64 workgroups
-  // of a split do not all read the same shared pos rows at once (one L2 channel per line); the
-  // online softmax does not depend on the tile order.  (The memory rows differ per image anyway.)
-  const int nt = te - tb, rot = KS ? (b * 7) % nt : 0;
-  auto tile_at = [&](int i) { const int j = i + rot; return tb + (j >= nt ? j - nt : j); };
+  const int nt = te - tb;
+  auto tile_at = [&](int i) { return tb + i; };
   // NSTAGE-slot ring: tiles t+1..t+NSTAGE-1 stay in flight while tile t is consumed; the slot of
   // tile t+NSTAGE-1 is refilled once every wave has passed tile t's barrier (it held tile t-1).
   if (loader) {
@@ -185,29 +165,22 @@ __global__ __launch_bounds__(NT, 1) void xattn_kernel(XattnArgs a) {
     asm volatile("" ::: "memory");
     if (loader) {
       if (it + NSTAGE - 1 < nt) issue(tile_at(it + NSTAGE - 1), (buf + NSTAGE - 1) % NSTAGE);
-      if constexpr (KS) __builtin_amdgcn_s_barrier();   // (the compute waves' exchange barrier)
       continue;
     }
-    if (!live_wave) {
-      if constexpr (KS) __builtin_amdgcn_s_barrier();
-      continue;
-    }
+    if (!live_wave) continue;
     const char* kl = lds + buf * STAGE;
     const char* vl = kl + KTILE;
 
-    // S^T - m: lane (row r32, hh) register r <-> key (r & 3) + 8 (r >> 2) + 4 hh.  KS: the wave
-    // pair splits the K = 512 reduction -- dh 0 the memory rows (from -m), dh 1 the pos rows --
-    // and swaps the partial scores through LDS; both waves then form memory part + pos part in
-    // the same order, so their softmax state stays bit-identical.
+    // S^T - m: lane (row r32, hh) register r <-> key (r & 3) + 8 (r >> 2) + 4 hh
     f32x16 s;
-    auto chain = [&](const char* t0, auto NEG) {
+    {
       f32x16 sa, sb;
 #pragma unroll
       for (int ks = 0; ks < 16; ks += 2) {
-        const bf16x8 k0 = __builtin_bit_cast(bf16x8, ld16(t0 + k_off<KS>(r32, 2 * ks + hh)));
-        const bf16x8 k1 = __builtin_bit_cast(bf16x8, ld16(t0 + k_off<KS>(r32, 2 * ks + 2 + hh)));
+        const bf16x8 k0 = __builtin_bit_cast(bf16x8, ld16(kl + k_off(r32, 2 * ks + hh)));
+        const bf16x8 k1 = __builtin_bit_cast(bf16x8, ld16(kl + k_off(r32, 2 * ks + 2 + hh)));
         if (ks == 0) {
-          sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf[ks], decltype(NEG)::value ? negm : f32x16{}, 0, 0, 0);
+          sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf[ks], negm, 0, 0, 0);
           sb = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, qf[ks + 1], f32x16{}, 0, 0, 0);
         } else {
           sa = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, qf[ks], sa, 0, 0, 0);
@@ -215,21 +188,6 @@ __global__ __launch_bounds__(NT, 1) void xattn_kernel(XattnArgs a) {
         }
       }
       s = sa + sb;
-    };
-    if (!KS) chain(kl, std::true_type{});
-    else chain(dh ? kl : vl, std::false_type{});   // (KS: -m after the exchange, no negm registers)
-    if constexpr (KS) {
-      float* xch = reinterpret_cast<float*>(lds + LDS_BYTES);
-#pragma unroll
-      for (int r = 0; r < 16; ++r) xch[(wid * 16 + r) * 64 + lane] = s[r];
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      asm volatile("" ::: "memory");
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float o = xch[((wid ^ 1) * 16 + r) * 64 + lane];
-        s[r] = (dh ? o + s[r] : s[r] + o) - m;   // memory part + pos part, shifted by the running max
-      }
     }
     const int key_base = t * KT;
     if (key_base + KT > a.T) {
@@ -282,8 +240,8 @@ __global__ __launch_bounds__(NT, 1) void xattn_kernel(XattnArgs a) {
     auto read_v = [&](u32x2 (&r)[4], int db) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
-        r[2 * ks] = ds_read_tr(v_tr_addr<KS>(vbase, 16 * ks + 4 * hh, 128 * dh + 32 * db + dg, l16));
-        r[2 * ks + 1] = ds_read_tr(v_tr_addr<KS>(vbase, 16 * ks + 8 + 4 * hh, 128 * dh + 32 * db + dg, l16));
+        r[2 * ks] = ds_read_tr(v_tr_addr(vbase, 16 * ks + 4 * hh, 128 * dh + 32 * db + dg, l16));
+        r[2 * ks + 1] = ds_read_tr(v_tr_addr(vbase, 16 * ks + 8 + 4 * hh, 128 * dh + 32 * db + dg, l16));
       }
     };
     read_v(vr[0], 0);
@@ -435,8 +393,7 @@ int spe_launch_xattn(const XattnArgs& a0, hipStream_t s) {
   a.splits = (ntiles + a.tiles_per_split - 1) / a.tiles_per_split;   // no empty split (<= requested)
   if (!a.pm || !a.pl || !a.pu || (a.wv ? !a.o || !a.bv || a.ldo % 2 : !a.u)) return -5;
   const int groups = (8 * a.Q + RG - 1) / RG;
-  if (a.k_shared) hipLaunchKernelGGL(xattn_kernel<true>, dim3(a.B * a.splits * groups), dim3(NT), 0, s, a);
-  else hipLaunchKernelGGL(xattn_kernel<false>, dim3(a.B * a.splits * groups), dim3(NT), 0, s, a);
+  hipLaunchKernelGGL(xattn_kernel, dim3(a.B * a.splits * groups), dim3(NT), 0, s, a);
   if (a.wv)
     hipLaunchKernelGGL(xattn_merge_wv_kernel, dim3((a.B * a.Q + MR - 1) / MR, 8), dim3(256), 0, s, a);
   else

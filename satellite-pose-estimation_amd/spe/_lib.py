@@ -40,8 +40,8 @@ SPE_PNP_OK, SPE_PNP_NO_FG, SPE_PNP_CV_ERROR, SPE_PNP_RANSAC_FALLBACK, SPE_PNP_UN
 EXPORTS = ["spe_abi_version", "spe_last_error", "spe_model_create", "spe_model_destroy", "spe_model_set_param",
            "spe_model_num_params", "spe_model_param_name", "spe_model_finalize", "spe_model_workspace_bytes",
            "spe_forward", "spe_forward_stages", "spe_preprocess", "spe_criterion", "spe_ensemble_fuse", "spe_postprocess", "spe_pnp_batch", "spe_self_assess", "spe_speed_score", "spe_model_profile_begin",
-           "spe_model_profile_end", "spe_model_profile_get", "spe_stream_create_cu_mask", "spe_stream_destroy", "spe_debug_gemm", "spe_debug_gemm_path", "spe_debug_gemm_planes", "spe_debug_attention",
-           "spe_debug_layernorm", "spe_debug_ffn", "spe_debug_xattn", "spe_debug_upconv", "spe_debug_btail", "spe_debug_btail_n1", "spe_debug_decsa", "spe_debug_decproj", "spe_debug_btail_perm", "spe_debug_stempool", "spe_rtdetr_create", "spe_rtdetr_forward",
+           "spe_model_profile_end", "spe_model_profile_get", "spe_debug_gemm", "spe_debug_gemm_path", "spe_debug_gemm_planes", "spe_debug_attention",
+           "spe_debug_layernorm", "spe_debug_ffn", "spe_debug_xattn", "spe_debug_upconv", "spe_debug_btail", "spe_debug_decsa", "spe_debug_decproj", "spe_debug_btail_perm", "spe_debug_stempool", "spe_rtdetr_create", "spe_rtdetr_forward",
            "spe_jpeg_workspace_bytes", "spe_jpeg_decode"]
 
 
@@ -102,8 +102,6 @@ def lib():
     L.spe_pnp_batch.argtypes = [P, P, P, P, I, I, I, P, P, I, F, I, D, P, P, P, P, P, P, P, P]
     L.spe_speed_score.argtypes = [P, P, P, P, P, I, P, P]
     L.spe_self_assess.argtypes = [P, P, P, P, P, P, I, I, I, F, F, I, P, P, P]
-    L.spe_stream_create_cu_mask.argtypes = [P, I, ctypes.POINTER(P)]
-    L.spe_stream_destroy.argtypes = [P]
     L.spe_model_profile_begin.argtypes = [P, ctypes.c_char_p]
     L.spe_model_profile_end.argtypes = [P]
     L.spe_model_profile_get.argtypes = [P, I, ctypes.c_char_p, I, ctypes.POINTER(D), ctypes.POINTER(D),
@@ -114,15 +112,13 @@ def lib():
     L.spe_debug_attention.argtypes = [P, I, P, I, P, I, P, P, I, I, I, I, I, F]
     L.spe_debug_layernorm.argtypes = [P, I, P, P, P, P, P, I, I]
     L.spe_debug_ffn.argtypes = [P, P, I, P, I, P, P, I, P, P, P, P, I, I, I, I, P, I]
-    L.spe_debug_xattn.argtypes = [P, P, I, P, I, P, I, P, I, P, P, P, I, I, I, I, I, P, I]
+    L.spe_debug_xattn.argtypes = [P, P, I, P, I, P, I, P, I, P, P, P, I, I, I, I, I, P]
     L.spe_debug_upconv.argtypes = [P, I, P, P, I, I, I, I, I]
     if hasattr(L, "spe_debug_btail"):          # (absent from older kernel A/B builds, SPE_LIB_PATH)
         L.spe_debug_btail.argtypes = [P, P, I, I, P, P, I, P, P, P, I, P, P, I, I]
         L.spe_debug_btail_perm.argtypes = [I]
     L.spe_debug_decsa.argtypes = [P, P, I, I, I, P, I, P, P, I, P, P, P, I, P, P, P, ctypes.c_float]
     L.spe_debug_decproj.argtypes = [P, P, I, P, I, I, I, P, I, P, P, P]
-    if hasattr(L, "spe_debug_btail_n1"):
-        L.spe_debug_btail_n1.argtypes = [P, P, I, I, P, P, I, P, P, P, I, P, P, I, I, I]
     if hasattr(L, "spe_debug_stempool"):
         L.spe_debug_stempool.argtypes = [P, P, P, I, P, P, I, I, I]
     L.spe_rtdetr_create.argtypes = [ctypes.POINTER(RtdetrConfig), ctypes.POINTER(P)]
@@ -130,7 +126,7 @@ def lib():
     L.spe_jpeg_workspace_bytes.argtypes = [I, I, I, I64]
     L.spe_jpeg_workspace_bytes.restype = I64
     L.spe_jpeg_decode.argtypes = [P, P, P, P, I, I, I, I64, P, P, P, I64]
-    if L.spe_abi_version() != 6:
+    if L.spe_abi_version() != 7:
         raise ImportError("libspe.so ABI version mismatch")
     _lib = L
     return L

@@ -11,6 +11,7 @@ from __future__ import annotations
 
 import torch
 
+from . import _lib
 from . import dist as spe_dist
 from .speed_eval import SpeedEval, device_speed_score
 
@@ -45,8 +46,14 @@ def evaluate(model, criterion, postprocessors, data_loader, gt_file, solver, dev
             for k, v in ld.items():
                 log(k + "_unscaled", v)
             log("class_error", ld["class_error"])
-        poses = solver.solve_batch(outputs["points_px"], outputs["probs"], outputs.get("sigmas"))
         gt = [evaluator.ground_truth[f] for f in filenames]
+        if getattr(solver, "mode", None) == _lib.SPE_PNP_EPNP_CERES:
+            # EPnPCeresSolver: one threshold per image from its ground-truth box area (UNC SpeedEval
+            # passes ground_truth[filename]["area"], src/data/speed/speed_dataset.py:396-399)
+            poses = solver.solve_batch(outputs["points_px"], outputs["probs"], outputs.get("sigmas"),
+                                       area=[g["area"] for g in gt])
+        else:
+            poses = solver.solve_batch(outputs["points_px"], outputs["probs"], outputs.get("sigmas"))
         q_gt = torch.tensor([g["quat"] for g in gt], dtype=torch.float64, device=device)
         t_gt = torch.tensor([g["tvec"] for g in gt], dtype=torch.float64, device=device)
         s_t, s_q = device_speed_score(poses["quat"], poses["tvec"], q_gt, t_gt)

@@ -10,26 +10,16 @@ from __future__ import annotations
 
 import torch
 
+from . import _lib
 from .models import DETR
 from .solver import PoseSolver
 from .speed_eval import device_speed_score
 
 
-def cu_partition(ncu: int, k: int):
-    """(backbone, encoder) CU masks as lists of 32-bit words: CU i goes to the backbone when
-    (i % 8 + i // 8) % 8 < k, i.e. k/8 of every run of 8 CUs and of every 8-strided set."""
-    words = (ncu + 31) // 32
-    bb, en = [0] * words, [0] * words
-    for i in range(ncu):
-        tgt = bb if (i % 8 + i // 8) % 8 < k else en
-        tgt[i // 32] |= 1 << (i % 32)
-    return bb, en
-
-
 class PosePipeline:
     def __init__(self, model: DETR, solver: PoseSolver, batch: int, device="cuda", use_graph: bool = False,
                  self_assess: bool = True, overlap: bool = False, raw_frames=None, overlap_decode: bool = False,
-                 jpeg_max_bytes: int = 0, overlap_backbone: bool = False, cu_split: int = 0):
+                 jpeg_max_bytes: int = 0, overlap_backbone: bool = False):
         self.model, self.solver, self.B = model, solver, batch
         self.self_assess = self_assess
         # overlap: the solver / score / self-assessment of batch i run on a second HIP stream
@@ -57,6 +47,9 @@ class PosePipeline:
         self.t_gt = torch.zeros(batch, 3, dtype=torch.float64, device=dev)
         self.q_gt[:, 0] = 1
         self.t_gt[:, 2] = 10
+        # EPnPCeresSolver: one reprojection threshold per image from its box area (load(area=...))
+        self.per_image_th = getattr(solver, "mode", None) == _lib.SPE_PNP_EPNP_CERES
+        self.repro = torch.full((batch,), float(getattr(solver, "reprojectionError", 20.0)), device=dev)
         if not overlap_decode:
             model.workspace(batch, dev)           # sized outside any graph capture
         if self.overlap_decode:
@@ -71,31 +64,10 @@ class PosePipeline:
             self.slot_clip = [torch.zeros(batch, 4, device=dev) for _ in range(self.nslot)]
             self.slot_q = [torch.zeros(batch, 4, dtype=torch.float64, device=dev) for _ in range(self.nslot)]
             self.slot_t = [torch.zeros(batch, 3, dtype=torch.float64, device=dev) for _ in range(self.nslot)]
+            self.slot_repro = [torch.zeros(batch, device=dev) for _ in range(self.nslot)]
             self.dec_done = [None] * self.nslot
             self.solve_done = [None] * self.nslot
             self.calls = 0
-        # cu_split = k (1..7, with overlap_backbone): the backbone runs on its own stream limited to
-        # k/8 of the CUs and the encoder on a stream limited to the rest (spe_stream_create_cu_mask),
-        # so the HBM-bound convolutions and the MFMA/VALU-bound encoder layers hold fixed CU shares
-        # instead of alternating workgroup by workgroup.  CU i goes to the backbone when
-        # (i % 8 + i // 8) % 8 < k: k/8 of every run of 8 and of every 8-strided set, whichever way
-        # the runtime's CU order interleaves the XCDs.
-        self.bb_stream = None
-        if cu_split and self.overlap_backbone:
-            from . import _lib
-            import ctypes
-            ncu = torch.cuda.get_device_properties(self.device).multi_processor_count
-            words = (ncu + 31) // 32
-
-            def masked(words_list):
-                m = (ctypes.c_uint32 * words)(*words_list)
-                h = ctypes.c_void_p()
-                _lib.check(_lib.lib().spe_stream_create_cu_mask(ctypes.cast(m, ctypes.c_void_p), words, ctypes.byref(h)),
-                           "spe_stream_create_cu_mask")
-                return torch.cuda.ExternalStream(h.value, device=self.device)
-            bbm, encm = cu_partition(ncu, cu_split)
-            self.bb_stream = masked(bbm)
-            self.enc_stream = masked(encm)
         # raw_frames = (H, W, C): each run() starts from uint8 frames + detector boxes resident in
         # HBM (load_frames) and runs the validation transform on the device first
         self.frames = self.bbox = self.transform = None
@@ -123,9 +95,13 @@ class PosePipeline:
         self.out = None
         _ = Q
 
-    def _solve(self, fo, stream=None, q_gt=None, t_gt=None):
+    def _solve(self, fo, stream=None, q_gt=None, t_gt=None, repro=None):
         sig = fo.get("sigmas")
-        poses = self.solver.solve_batch(fo["points_px"], fo["probs"], sig, stream=stream)
+        if self.per_image_th:
+            poses = self.solver.solve_batch(fo["points_px"], fo["probs"], sig, stream=stream,
+                                            repro_per_image=self.repro if repro is None else repro)
+        else:
+            poses = self.solver.solve_batch(fo["points_px"], fo["probs"], sig, stream=stream)
         q_gt = self.q_gt if q_gt is None else q_gt
         t_gt = self.t_gt if t_gt is None else t_gt
         s_t, s_q = device_speed_score(poses["quat"], poses["tvec"], q_gt, t_gt, stream=stream)
@@ -152,16 +128,11 @@ class PosePipeline:
         self.slot_clip[slot].copy_(self.clip_bbox)
         self.slot_q[slot].copy_(self.q_gt)
         self.slot_t[slot].copy_(self.t_gt)
+        self.slot_repro[slot].copy_(self.repro)
         if self.overlap_backbone:
-            bb = main
-            if self.bb_stream is not None:
-                bb = self.bb_stream
-                bb.wait_stream(main)
-            self.model.encode(self.images, self.ws2[slot], stream=bb, part="backbone")
-            if bb is not main:
-                main.wait_stream(bb)                  # the next load() overwrites what the backbone read
+            self.model.encode(self.images, self.ws2[slot], stream=main, part="backbone")
             e = self.enc_stream
-            e.wait_stream(bb)
+            e.wait_stream(main)
             with torch.cuda.stream(e):
                 self.model.encode(None, self.ws2[slot], stream=e, part="transformer", B=self.B)
         else:
@@ -179,7 +150,8 @@ class PosePipeline:
         with torch.cuda.stream(s1):
             for t in fo.values():
                 t.record_stream(s1)
-            out = self._solve(fo, stream=s1, q_gt=self.slot_q[slot], t_gt=self.slot_t[slot])
+            out = self._solve(fo, stream=s1, q_gt=self.slot_q[slot], t_gt=self.slot_t[slot],
+                              repro=self.slot_repro[slot])
             ev = torch.cuda.Event()
             ev.record(s1)
             self.solve_done[slot] = ev
@@ -198,12 +170,12 @@ class PosePipeline:
         s1 = self.solve_stream
         # the ground truth is snapshotted on the caller's stream: a load() of the next batch may
         # overwrite q_gt / t_gt while this batch's score still runs on the solver stream
-        q_gt, t_gt = self.q_gt.clone(), self.t_gt.clone()
+        q_gt, t_gt, repro = self.q_gt.clone(), self.t_gt.clone(), self.repro.clone()
         s1.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s1):
-            for t in list(fo.values()) + [q_gt, t_gt]:
+            for t in list(fo.values()) + [q_gt, t_gt, repro]:
                 t.record_stream(s1)          # consumed on the solver stream
-            out = self._solve(fo, stream=s1, q_gt=q_gt, t_gt=t_gt)
+            out = self._solve(fo, stream=s1, q_gt=q_gt, t_gt=t_gt, repro=repro)
         out["stream"] = s1
         return out
 
@@ -213,24 +185,36 @@ class PosePipeline:
         if out is not None and out.get("stream") is not None:
             torch.cuda.current_stream().wait_stream(out["stream"])
 
-    def load(self, images, clip_bbox, q_gt=None, t_gt=None):
+    def load(self, images, clip_bbox, q_gt=None, t_gt=None, area=None):
+        """area (EPnPCeresSolver): the B box areas its per-image thresholds come from."""
         self.images.copy_(images, non_blocking=True)
         self.clip_bbox.copy_(clip_bbox, non_blocking=True)
         if q_gt is not None:
             self.q_gt.copy_(q_gt, non_blocking=True)
             self.t_gt.copy_(t_gt, non_blocking=True)
+        self._load_area(area)
 
-    def load_frames(self, frames, bbox_xxyy, q_gt=None, t_gt=None):
+    def _load_area(self, area):
+        if area is not None:
+            if not self.per_image_th:
+                raise ValueError("area= is the EPnPCeresSolver's threshold input; this pipeline's solver takes none")
+            self.repro.copy_(torch.tensor([self.solver.repro_th(float(a)) for a in area], dtype=torch.float32))
+        elif self.per_image_th:
+            raise ValueError("EPnPCeresSolver pipeline: load(..., area=) needs the images' box areas")
+
+    def load_frames(self, frames, bbox_xxyy, q_gt=None, t_gt=None, area=None):
         """Raw-frame mode: uint8 frames [B,H,W(,3)] + detector boxes [B,4] (fp64)."""
+        self._load_area(area)
         self.frames.copy_(frames, non_blocking=True)
         self.bbox.copy_(torch.as_tensor(bbox_xxyy, dtype=torch.float64), non_blocking=True)
         if q_gt is not None:
             self.q_gt.copy_(q_gt, non_blocking=True)
             self.t_gt.copy_(t_gt, non_blocking=True)
 
-    def load_jpeg(self, data, offsets, sizes, bbox_xxyy, q_gt=None, t_gt=None):
+    def load_jpeg(self, data, offsets, sizes, bbox_xxyy, q_gt=None, t_gt=None, area=None):
         """JPEG mode: the batch's files packed into one device byte buffer (JpegDecoder.pack; kept
         by reference, not copied) + detector boxes [B,4]."""
+        self._load_area(area)
         self.jpeg = (data, offsets, sizes)
         self.bbox.copy_(torch.as_tensor(bbox_xxyy, dtype=torch.float64), non_blocking=True)
         if q_gt is not None:

@@ -142,19 +142,35 @@ class EPnPCeresSolver(PoseSolver):
         super().__init__(_lib.SPE_PNP_EPNP_CERES, 20.0)
         self.input_size = input_size
 
-    def get_repro_th(self, area):
-        """UNC/utils/speed_eval_ceres.py:53-58 (int() truncation, then [1.5, 20])."""
+    def repro_th(self, area):
+        """The threshold of one box area (UNC/utils/speed_eval_ceres.py:53-58: int() truncation, then
+        [1.5, 20]) without touching the solver's state."""
         repro = int(area / self.input_size * 10)
-        repro = min(max(repro, 1.5), 20)
-        self.reprojectionError = float(repro)
+        return float(min(max(repro, 1.5), 20))
+
+    def get_repro_th(self, area):
+        """UNC/utils/speed_eval_ceres.py:53-58: sets reprojectionError for the next __call__, as the
+        reference does (its per-image call path)."""
+        self.reprojectionError = self.repro_th(area)
         return self.reprojectionError
 
     def solve_batch(self, points_px, probs, sigmas=None, stream=None, out=None, repro_per_image=None, area=None):
-        """As PoseSolver.solve_batch; `area` (sequence of B box areas) sets the per-image thresholds."""
-        if repro_per_image is None and area is not None:
-            th = [self.get_repro_th(float(a)) for a in area]
-            repro_per_image = torch.tensor(th, dtype=torch.float32, device=probs.device)
-        return super().solve_batch(points_px, probs, sigmas, stream=stream, out=out, repro_per_image=repro_per_image)
+        """As PoseSolver.solve_batch with one threshold per image: `area` (B box areas) or
+        `repro_per_image` (device fp32 [B]) is required -- the reference has no batch-wide
+        threshold for this solver (get_repro_th runs per image, :90)."""
+        if repro_per_image is None:
+            if area is None:
+                raise ValueError("EPnPCeresSolver.solve_batch needs the per-image box areas (area=) or thresholds "
+                                 "(repro_per_image=): the reference derives every image's threshold from its area")
+            repro_per_image = torch.tensor([self.repro_th(float(a)) for a in area], dtype=torch.float32,
+                                           device=probs.device)
+        repro_per_image = repro_per_image.float().contiguous()
+        o = super().solve_batch(points_px, probs, sigmas, stream=stream, out=out, repro_per_image=repro_per_image)
+        # the kernel may still read the thresholds on `stream` after this returns
+        if stream is not None:
+            repro_per_image.record_stream(stream)
+        o["repro_per_image"] = repro_per_image
+        return o
 
     def __call__(self, points, logits, area, sigma, device=None):
         """One image, the reference's signature (:70): numpy in / numpy out."""

@@ -56,7 +56,16 @@ def load_ground_truth(gt):
     if isinstance(gt, (str, os.PathLike)):
         with open(gt) as f:
             gt = json.load(f)
-    return {it["filename"]: {"quat": it["q_vbs2tango"], "tvec": it["r_Vo2To_vbs_true"]} for it in gt}
+    out = {}
+    for it in gt:
+        r = {"quat": it["q_vbs2tango"], "tvec": it["r_Vo2To_vbs_true"]}
+        if "bbox_xxyy" in it:
+            # UNC SpeedEval's "area" (src/data/speed/speed_dataset.py:370-373), the operator
+            # precedence kept: sqrt((x2 - x1) * y2 - y1) -- EPnPCeresSolver's threshold input
+            b = it["bbox_xxyy"]
+            r["area"] = float(np.sqrt((b[2] - b[0]) * b[3] - b[1]))
+        out[it["filename"]] = r
+    return out
 
 
 class SpeedEval:

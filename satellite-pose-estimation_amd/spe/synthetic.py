@@ -235,10 +235,65 @@ def diversify_class_head(w, hs, seed: int = 1, k: int = 12, logit_scale: float =
 
 def bench_weights(cfg: SpeConfig, seed: int, hs_fn, calib_batch: int = 16):
     """Random-init weights made label-diverse (see above).  hs_fn(weights, images) -> hs [B,Q,d]
-    runs the model under test (the HIP path in bench.py)."""
+    runs a model on the calibration batch."""
     w = sharpen_decoder(random_weights(cfg, seed), cfg)
-    calib = synthetic_batch(cfg, calib_batch, seed=4242)
+    calib = synthetic_batch(cfg, calib_batch, seed=CALIB_SEED)
     return diversify_class_head(w, hs_fn(w, calib["images"]))
+
+
+# ------------------------------------------------------------------- the bench's image pool
+# The bench's images are a fixed seeded pool of BENCH_POOL crops (the north-star global batch,
+# BASELINE.json): image g is synthetic_batch(cfg, 1, BENCH_SEED + g), and a rank with per-GPU batch B
+# times pool images [rank*B, rank*B + B) (modulo the pool).  The pool does not depend on the
+# number of ranks, so the head fit below and every image's result are the same at 1 and 8 GPUs.
+BENCH_POOL = 256
+BENCH_SEED = 1000
+CALIB_SEED = 4242
+HEADS_KEYS = ["cls_embed.weight", "cls_embed.bias"] + [f"point_embed.layers.{j}.{k}" for j in range(3)
+                                                      for k in ("weight", "bias")]
+
+
+def bench_images(cfg: SpeConfig, first: int, count: int, pool: int = BENCH_POOL):
+    """Pool images first .. first+count-1 (indices modulo `pool`), as one synthetic_batch dict."""
+    parts = [synthetic_batch(cfg, 1, seed=BENCH_SEED + (g % pool)) for g in range(first, first + count)]
+    return {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
+
+
+def heads_fixture_path(cfg: SpeConfig, seed: int = 0):
+    import os
+    return os.path.join(os.path.dirname(os.path.abspath(__file__)), "data",
+                        f"bench_heads_s{cfg.input_size}_q{cfg.num_queries}_l{cfg.enc_layers}-{cfg.dec_layers}"
+                        f"_seed{seed}.npz")
+
+
+def fixed_bench_weights(cfg: SpeConfig, seed: int = 0):
+    """The bench's pose-consistent weights from the committed head fixture, or None when no
+    fixture exists for this shape: random_weights(seed) with the sharpened decoder, and the class
+    head + fitted point head stored by oracle/gen_bench_heads.py (computed once from the torch-fp32
+    restatement of the reference model on the CPU, so they depend on no kernel of this repo, on no
+    device and on no rank count).  Returns (weights, fixture metadata)."""
+    import json
+    import os
+    path = heads_fixture_path(cfg, seed)
+    if not os.path.exists(path):
+        return None, None
+    z = np.load(path)        # plain arrays (allow_pickle stays False)
+    w = sharpen_decoder(random_weights(cfg, seed), cfg)
+    for k in HEADS_KEYS:
+        if z[k].shape != w[k].shape:
+            raise ValueError(f"{path}: {k} has shape {z[k].shape}, the model expects {w[k].shape}")
+        w[k] = np.ascontiguousarray(z[k], np.float32)
+    return w, json.loads(str(z["meta"]))
+
+
+def weights_checksum(w) -> str:
+    """sha256 over the state dict (sorted keys, float32 bytes), first 16 hex digits."""
+    import hashlib
+    h = hashlib.sha256()
+    for k in sorted(w):
+        h.update(k.encode())
+        h.update(np.ascontiguousarray(w[k], np.float32).tobytes())
+    return h.hexdigest()[:16]
 
 
 # ------------------------------------------------------------- pose-consistent point head

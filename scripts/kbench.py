@@ -118,18 +118,13 @@ def main():
         part = torch.empty(256 * B * 8 * Q * 258, device=dev)
         for sp in (0, 2, 8):
             fn = lambda: L.spe_debug_xattn(None, p(q), 8 * D, p(k), D, p(v), D, None, 0, p(wv), p(bv), p(o), D,
-                                           B, Q, T, sp, p(part), 0)
+                                           B, Q, T, sp, p(part))
             ms = timeit(fn, a.iters)
             fn_u = lambda: L.spe_debug_xattn(None, p(q), 8 * D, p(k), D, p(v), D, p(u), 8 * D, None, None, None,
-                                             0, B, Q, T, sp, p(part), 0)
+                                             0, B, Q, T, sp, p(part))
             ms_u = timeit(fn_u, a.iters)
             byts = 2 * B * T * D * 2                      # K and V reads
             print(f"xattn splits={sp}: {ms:.3f} ms with Wv, {ms_u:.3f} ms u only ({byts / ms_u / 1e9:.2f} TB/s)")
-            # the model's mode: K = V + pos, pos [T] shared (HBM: V only)
-            fn_s = lambda: L.spe_debug_xattn(None, p(q), 8 * D, p(k), D, p(v), D, None, 0, p(wv), p(bv), p(o), D,
-                                             B, Q, T, sp, p(part), 1)
-            ms_s = timeit(fn_s, a.iters)
-            print(f"xattn k_shared splits={sp}: {ms_s:.3f} ms with Wv ({B * T * D * 2 / ms_s / 1e9:.2f} TB/s of V)")
     if a.which in ("gemm", "all"):
         # name, mode, M, N, K, residual rows (0 none, -1 full, >0 period), conv geometry
         cases = [("l1.c3 1x1+res", 0, B * 104 * 104, 256, 64, -1, None),

@@ -24,7 +24,7 @@ def test_exports_every_declared_symbol():
     assert set(declared) == set(_lib.EXPORTS)
     for name in declared:
         assert hasattr(L, name), name
-    assert L.spe_abi_version() == 6
+    assert L.spe_abi_version() == 7
 
 
 def _create(cfg, dtype=_lib.SPE_DTYPE_BF16):

@@ -352,35 +352,6 @@ def test_btail(gpu_device, M, k1, n2, res):
     _close(Z, zref, DT["bf16"][2])
 
 
-# split-N bottleneck tail (btail.hip, layers 2 and 3): y produced in column chunks with the
-# weights streamed through LDS; row counts off the 128-row block and the bench's sizes
-@pytest.mark.parametrize("M,k1,n1,n2", [(173056, 128, 512, 128), (1000, 128, 512, 128), (3001, 128, 512, 256),
-                                        (43264, 256, 1024, 256), (77, 256, 1024, 256)])
-def test_btail_split(gpu_device, M, k1, n1, n2):
-    L = _lib.lib()
-    dt = torch.bfloat16
-    g = torch.Generator(device="cpu").manual_seed(M + k1 + n1 + n2)
-    A = torch.randn(M, k1, generator=g).to(gpu_device, dt)
-    R = torch.randn(M, n1, generator=g).to(gpu_device, dt)
-    W3 = (torch.randn(n1, k1, generator=g) / k1 ** 0.5).to(gpu_device, dt)
-    b3 = (0.1 * torch.randn(n1, generator=g)).to(gpu_device)
-    W1 = (torch.randn(n2, n1, generator=g) / n1 ** 0.5).to(gpu_device, dt)
-    b1 = (0.1 * torch.randn(n2, generator=g)).to(gpu_device)
-    perm = torch.tensor([L.spe_debug_btail_perm(k) for k in range(n1)], device=gpu_device)
-    assert sorted(perm.tolist()) == list(range(n1))
-    W1p = W1[:, perm].contiguous()
-    Y = torch.full((M, n1), float("nan"), dtype=dt, device=gpu_device)
-    Z = torch.full((M, n2), float("nan"), dtype=dt, device=gpu_device)
-    rc = L.spe_debug_btail_n1(None, _p(A), k1, k1, _p(R), _p(W3), k1, _p(b3), _p(Y), _p(W1p), n1, _p(b1), _p(Z), n1,
-                              n2, M)
-    assert rc == 0, L.spe_last_error()
-    torch.cuda.synchronize()
-    yref = torch.relu(A.float() @ W3.float().t() + b3 + R.float())
-    _close(Y, yref, DT["bf16"][2])
-    zref = torch.relu(Y.float() @ W1.float().t() + b1)
-    _close(Z, zref, DT["bf16"][2])
-
-
 # the fused stem + bias + ReLU + max-pool (stempool.hip): the bench's 416^2 (one column group,
 # 15 waves), a small image, 640^2 (config 5: two column groups, an idle wave) and a strided
 # output row (the pool writes the right half of layer 1 block 0's [conv2 | pool] concatenation)
@@ -647,25 +618,20 @@ def test_fused_ffn(gpu_device, M, F, inplace, splits):
         assert (y[:, D:] == 7.0).all()                 # nothing written past D
 
 
-@pytest.mark.parametrize("shared", [0, 1], ids=["k_rows", "k_shared_pos"])
 @pytest.mark.parametrize("B,Q,T,splits,amp", [(3, 11, 200, 1, 1.0), (2, 11, 203, 3, 1.0), (1, 17, 136, 2, 1.0),
                                               (2, 11, 2704, 0, 1.0), (2, 5, 640, 4, 12.0), (64, 11, 2704, 0, 1.0)])
-def test_cross_attention_memory(gpu_device, B, Q, T, splits, amp, shared):
+def test_cross_attention_memory(gpu_device, B, Q, T, splits, amp):
     """decoder cross-attention against the memory (xattn.hip): u = softmax_2(q' . K^T) . V per
     (image, query, head) row, against torch fp32 on the same bf16 operands.  amp = 12 spreads the
     scores over ~100 log2 units (many lazy-rescale branches taken, split partials merged far apart).
-    shared = 1 is the model's mode: K_t = V_t + pos_t with one pos table [T] for every image (the
-    reference's key = memory + pos, REV/models/transformer.py:230-233), summed in fp32 here.
+    K rows are the model's memory + pos (the reference's key, REV/models/transformer.py:230-233).
     Tolerance: P is rounded to bf16 (2^-9 relative) before the value product; 1e-2 * scale."""
     dt, D = torch.bfloat16, 256
     g = torch.Generator(device="cpu").manual_seed(B * T + Q)
     ldq, ldv = 8 * D + 8, D + 8
     q = (torch.randn(B * Q, ldq, generator=g) * amp / 16).to(gpu_device, dt)
-    k = torch.randn((T if shared else B * T), D, generator=g).to(gpu_device, dt)
+    k = torch.randn(B * T, D, generator=g).to(gpu_device, dt)
     v = torch.randn(B * T, ldv, generator=g).to(gpu_device, dt)          # strided rows
-    if shared:
-        k *= 0.5
-        v[:, :D] *= 0.5
     if amp > 1:
         k[5] *= 4                                           # one key far above the rest
     wv = (torch.randn(D, D, generator=g) / 16).to(gpu_device, dt)
@@ -676,14 +642,14 @@ def test_cross_attention_memory(gpu_device, B, Q, T, splits, amp, shared):
     part = torch.empty(S * B * 8 * Q * 258, device=gpu_device)
     L = _lib.lib()
     rc = L.spe_debug_xattn(None, _p(q), ldq, _p(k), D, _p(v), ldv, _p(u), ldq, None, None, None, 0, B, Q, T,
-                           splits, _p(part), shared)
+                           splits, _p(part))
     assert rc == 0, L.spe_last_error()
     rc = L.spe_debug_xattn(None, _p(q), ldq, _p(k), D, _p(v), ldv, None, 0, _p(wv), _p(bv), _p(o), D + 8, B, Q,
-                           T, splits, _p(part), shared)
+                           T, splits, _p(part))
     assert rc == 0, L.spe_last_error()
     torch.cuda.synchronize()
     qh = q[:, :8 * D].float().view(B, Q * 8, D)
-    kk = v[:, :D].float().view(B, T, D) + k.float().view(1, T, D) if shared else k.float().view(B, T, D)
+    kk = k.float().view(B, T, D)
     s = torch.einsum("brd,btd->brt", qh, kk)
     p = torch.softmax(s * 0.6931471805599453, dim=-1)
     ref = torch.einsum("brt,btd->brd", p, v[:, :D].float().view(B, T, D))   # [B][Q*8][D], rows q*8 + h

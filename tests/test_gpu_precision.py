@@ -1,26 +1,37 @@
-"""GPU: the accuracy contract on the bench's own weights (BASELINE north_star "keypoint L2 within 1e-4
-of reference").
+"""GPU: the accuracy contract on the bench's own weights (BASELINE north_star "keypoint L2 and SPEED
+pose-score within 1e-4 of reference").
 
-The bench's pose-consistent weights (bench.py: label-diverse random init with a 64x-sharpened
-decoder cross-attention and a point head fitted to random decoder outputs) amplify perturbations of
-the decoder output hs ~20x into the keypoints.  This test measures, on the bench's timed batch
-(config 2, B = 64), how far apart INDEPENDENT fp32 implementations of the same model land:
+The bench's pose-consistent weights (spe.synthetic.fixed_bench_weights: label-diverse random init
+with a 64x-sharpened decoder cross-attention and a point head fitted to the decoder outputs of the
+256-image bench pool) amplify perturbations of the decoder output hs ~20x into the keypoints.  This
+test measures, on the config-2 timed batch (pool images 0..63), how far apart INDEPENDENT fp32
+implementations of the same model land -- at the keypoints and at the SPEED score, both solvers:
 
   * ours-fp32     the exact-f32 parity mode (this repo; <= 1e-4 of the reference on its goldens)
   * torch-gpu     the oracle's torch restatement (oracle/model_ref.py, pinned to the reference at
                   <= 2e-7 on the goldens) in fp32 on the GPU (hipBLASLt / MIOpen, TF32 off)
-  * torch-cpu     the same restatement on the CPU for the first 4 images (the reference's own
-                  execution model: REV main.py --eval on CPU, BASELINE config 1)
+  * torch-cpu     the same restatement on the CPU, all 64 images (the reference's own execution
+                  model: REV main.py --eval on CPU, BASELINE config 1)
 
-and where the fast parity modes land against them:
+and where the fast modes land against them (fp32x6 = the accuracy-contract mode, fp32x3, bf16).
+Every implementation's keypoints go through the SAME HIP solver (EPnP = config 2, P3P-RANSAC + LM
+= configs 3 / north star), so the score deltas isolate the keypoints.  Per image the test also
+records the score's float32 conditioning (the largest score change when the ours-fp32 keypoints
+move by one float32 ulp per coordinate, 16 random directions; bench.Fp32Reference.cond) and, for
+every image where fp32x6 and ours-fp32 differ by more than 1e-4, the solver decision behind it
+(oracle/pnp_ref.c trace: EPnP beta-candidate errors / pick, RANSAC best iteration / inlier mask /
+the point nearest the threshold).
 
-  * fp32x6        the accuracy-contract mode (GEMMs three-way split, attention fp32x3)
-  * fp32x3        split-bf16 everywhere
-
-Gates (written here): fp32x6 is within the fp32 implementation spread -- its keypoint distance to
-ours-fp32 is at most 2x the distance between the two fp32 implementations ours-fp32 / torch-gpu,
-plus 1e-5 -- and within 1e-4 normalised of the torch restatement on the CPU images.
+Gates (written here):
+  keypoints  fp32x6 within 2x the ours-fp32 / torch-gpu spread + 1e-5 of ours-fp32, and <= 1e-4
+             normalised of torch-cpu on all 64 images;
+  score      per solver, fp32x6's score deltas against ours-fp32 lie inside the fp32 implementation
+             spread: its fraction of images within 1e-4 is at least torch-cpu's minus 0.1 (64-image
+             sampling slack), and every image where fp32x6 misses 1e-4 is either ill-conditioned at
+             float32 resolution (cond > 1e-4) or missed by torch-cpu too, or its decision trace
+             names the flipped discrete choice.
 """
+import argparse
 import json
 import os
 import sys
@@ -32,72 +43,179 @@ import torch
 pytestmark = pytest.mark.gpu
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+B = 64
 
 
 def _kpt(a, b, fg):
     return float((a - b).abs().amax(-1)[fg].max())
 
 
+def _decision(tr_a, tr_b, mode):
+    """Name the discrete solver choice that differs between two traces (or 'continuous')."""
+    if mode == 0:
+        if tr_a["epnp_pick"] != tr_b["epnp_pick"]:
+            return f"epnp_beta_pick {tr_a['epnp_pick']}->{tr_b['epnp_pick']}"
+        return "continuous"
+    for k in ("ransac_mask", "ransac_best_iter", "ransac_iters", "epnp_pick"):
+        if tr_a[k] != tr_b[k]:
+            return f"{k} {tr_a[k]}->{tr_b[k]}"
+    return "continuous"
+
+
+@pytest.mark.timeout(900)
 def test_fp32x6_within_fp32_implementation_spread(gpu_device):
     sys.path.insert(0, REPO)
-    import argparse
-    import bench
     import model_ref
-    from spe.config import SpeConfig
+    import pnp_ref
+    from spe.config import Camera, SpeConfig, world_points
     from spe.models import DETR
-    from spe.synthetic import bench_weights
+    from spe.solver import build_solver
+    from spe.speed_eval import device_speed_score
+    from spe.synthetic import bench_images, fixed_bench_weights
 
     dev = gpu_device
-    B = 64
     cfg = SpeConfig(input_size=416, num_queries=11, enc_layers=6, dec_layers=6)
-
-    def hs_fn(w, images):
-        m = DETR(cfg, dtype="bf16")
-        m.load_state_dict(w)
-        n = len(images)
-        x = torch.from_numpy(np.concatenate([images] * ((B + n - 1) // n))[:B]).to(dev)
-        return m(x, return_hs=True)["hs"].cpu().numpy()[:n]
-
-    w = bench_weights(cfg, 0, hs_fn)
-    w, _ = bench.pose_consistent_weights(w, cfg, argparse.Namespace(dtype="bf16", attn_dtype="bf16"), B, 0, 1, dev)
-    data = bench.bench_data(cfg, B, 0)
+    w, meta = fixed_bench_weights(cfg, 0)
+    assert w is not None, "committed head fixture missing (oracle/gen_bench_heads.py)"
+    data = bench_images(cfg, 0, B)
     x = torch.from_numpy(data["images"]).to(dev)
+    clip = torch.from_numpy(data["clip_bbox"]).float().to(dev)
+    q_gt = torch.from_numpy(data["quat"]).to(dev)
+    t_gt = torch.from_numpy(data["tvec"]).to(dev)
+
+    impl = {}                                      # name -> (pred_points, points_px, probs)
 
     def ours(dtype):
-        m = DETR(cfg, dtype=dtype)
+        m = DETR(cfg, dtype=dtype, attn_dtype=dtype)
         m.load_state_dict(w)
-        o = m(x)
+        o = m(x, clip_bbox=clip)
         torch.cuda.synchronize()
-        return o["pred_points"].clone(), o["pred_logits"].argmax(-1)
+        impl[dtype] = (o["pred_points"].clone(), o["points_px"].clone(), o["probs"].clone())
+        del m
 
-    p32, lab = ours("fp32")
-    p6, lab6 = ours("fp32x6")
-    p3, lab3 = ours("fp32x3")
-    mm, cv = torch.backends.cuda.matmul.allow_tf32, torch.backends.cudnn.allow_tf32
-    torch.backends.cuda.matmul.allow_tf32 = torch.backends.cudnn.allow_tf32 = False
-    try:
-        with torch.no_grad():
-            tg = model_ref.forward(x, w, cfg)
-            torch.cuda.synchronize()
-            ptg, labtg = tg["pred_points"], tg["pred_logits"].argmax(-1)
-            tc = model_ref.forward(data["images"][:4], w, cfg)
-    finally:
-        torch.backends.cuda.matmul.allow_tf32, torch.backends.cudnn.allow_tf32 = mm, cv
-    ptc = tc["pred_points"].to(dev)
-    fg = (lab < 11) & (lab6 == lab) & (lab3 == lab) & (labtg == lab)
-    fg4 = fg[:4] & (tc["pred_logits"].argmax(-1).to(dev) == lab[:4])
-    r = {"config": "config 2, B=64, bench pose-consistent weights", "fg_queries": int(fg.sum()),
-         "ours_fp32_vs_torch_gpu": _kpt(p32, ptg, fg), "fp32x6_vs_ours_fp32": _kpt(p6, p32, fg),
-         "fp32x6_vs_torch_gpu": _kpt(p6, ptg, fg), "fp32x3_vs_ours_fp32": _kpt(p3, p32, fg),
-         "fp32x3_vs_torch_gpu": _kpt(p3, ptg, fg),
-         "cpu_images": 4, "torch_cpu_vs_ours_fp32": _kpt(ptc, p32[:4], fg4), "torch_cpu_vs_torch_gpu": _kpt(ptc, ptg[:4], fg4),
-         "fp32x6_vs_torch_cpu": _kpt(p6[:4], ptc, fg4), "fp32x3_vs_torch_cpu": _kpt(p3[:4], ptc, fg4)}
+    for dt in ("fp32", "fp32x6", "fp32x3", "bf16"):
+        ours(dt)
+
+    def torch_impl(images, device):
+        mm, cv = torch.backends.cuda.matmul.allow_tf32, torch.backends.cudnn.allow_tf32
+        torch.backends.cuda.matmul.allow_tf32 = torch.backends.cudnn.allow_tf32 = False
+        try:
+            with torch.no_grad():
+                outs = [model_ref.forward(images[i:i + 16], w, cfg) for i in range(0, len(images), 16)]
+        finally:
+            torch.backends.cuda.matmul.allow_tf32, torch.backends.cudnn.allow_tf32 = mm, cv
+        lg = torch.cat([o["pred_logits"] for o in outs]).float().cpu()
+        pn = torch.cat([o["pred_points"] for o in outs]).float().cpu()
+        pp = model_ref.postprocess(lg, pn, data["clip_bbox"])
+        px = torch.from_numpy(np.stack([r["points"] for r in pp])).to(dev)
+        pr = torch.from_numpy(np.stack([r["logits"] for r in pp])).to(dev)
+        return pn.to(dev), px, pr
+
+    impl["torch_gpu"] = torch_impl(x, dev)
+    torch.set_num_threads(max(1, min(16, os.cpu_count() or 1)))
+    impl["torch_cpu"] = torch_impl(data["images"], "cpu")
+
+    lab = {k: v[2].argmax(-1) for k, v in impl.items()}
+    fg = (lab["fp32"] < 11)
+    for k in ("fp32x6", "fp32x3", "torch_gpu", "torch_cpu"):
+        fg &= lab[k] == lab["fp32"]
+    kp = {k: v[0] for k, v in impl.items()}
+    r = {"config": "config 2 shape, pool images 0..63, bench fixture weights " + meta["generator"],
+         "fg_queries": int(fg.sum()),
+         "kpt": {"ours_fp32_vs_torch_gpu": _kpt(kp["fp32"], kp["torch_gpu"], fg),
+                 "ours_fp32_vs_torch_cpu": _kpt(kp["fp32"], kp["torch_cpu"], fg),
+                 "torch_cpu_vs_torch_gpu": _kpt(kp["torch_cpu"], kp["torch_gpu"], fg),
+                 "fp32x6_vs_ours_fp32": _kpt(kp["fp32x6"], kp["fp32"], fg),
+                 "fp32x6_vs_torch_gpu": _kpt(kp["fp32x6"], kp["torch_gpu"], fg),
+                 "fp32x6_vs_torch_cpu": _kpt(kp["fp32x6"], kp["torch_cpu"], fg),
+                 "fp32x3_vs_ours_fp32": _kpt(kp["fp32x3"], kp["fp32"], fg),
+                 "label_agreement_bf16": float((lab["bf16"] == lab["fp32"]).float().mean())}}
+
+    # ---- the same HIP solver on every implementation's keypoints
+    K, Wd = Camera.K, world_points()
+    trace_pairs = {}
+    r["score"] = {}
+    for name, mode in (("epnp", 0), ("ransac_p3p_lm", 1)):
+        solver = build_solver(argparse.Namespace(solver=name, repro=20))
+        sc = {}
+        for k, (_, px, pr) in impl.items():
+            po = solver.solve_batch(px, pr)
+            st, sq = device_speed_score(po["quat"], po["tvec"], q_gt, t_gt)
+            sc[k] = (st + sq).cpu().numpy()
+        # float32 conditioning of the ours-fp32 scores (bench.Fp32Reference's rule)
+        cond = _ulp_conditioning(solver, impl["fp32"][1], impl["fp32"][2], q_gt, t_gt, sc["fp32"], dev)
+        pairs = [("fp32x6", "fp32"), ("torch_cpu", "fp32"), ("torch_gpu", "fp32"), ("torch_cpu", "torch_gpu"),
+                 ("fp32x6", "torch_cpu"), ("fp32x3", "fp32"), ("bf16", "fp32")]
+        tab = {}
+        for a, b in pairs:
+            d = np.abs(sc[a] - sc[b])
+            ok = np.isfinite(d)
+            tab[f"{a}_vs_{b}"] = {"frac_le_1e-4": float((d[ok] <= 1e-4).mean()), "max": float(d[ok].max()),
+                                  "median": float(np.median(d[ok]))}
+        d6 = np.abs(sc["fp32x6"] - sc["fp32"])
+        dc = np.abs(sc["torch_cpu"] - sc["fp32"])
+        miss = np.where(d6 > 1e-4)[0]
+        # the decision behind every fp32x6 miss: oracle traces of the two keypoint sets
+        _, tr32 = pnp_ref.pnp_trace(impl["fp32"][1][miss].cpu().numpy(), impl["fp32"][2][miss].cpu().numpy(), K, Wd,
+                                    mode=mode, repro=20.0)
+        _, tr6 = pnp_ref.pnp_trace(impl["fp32x6"][1][miss].cpu().numpy(), impl["fp32x6"][2][miss].cpu().numpy(), K,
+                                   Wd, mode=mode, repro=20.0)
+        per = []
+        for j, i in enumerate(miss):
+            per.append({"image": int(i), "score_fp32": float(sc["fp32"][i]), "delta_fp32x6": float(d6[i]),
+                        "delta_torch_cpu": float(dc[i]), "cond_f32_ulp": float(cond[i]),
+                        "decision": _decision(tr32[j], tr6[j], mode),
+                        "epnp_err_fp32": [round(tr32[j][f"epnp_err{c}"], 6) for c in (1, 2, 3)],
+                        "epnp_err_fp32x6": [round(tr6[j][f"epnp_err{c}"], 6) for c in (1, 2, 3)],
+                        "epnp_pick": [tr32[j]["epnp_pick"], tr6[j]["epnp_pick"]],
+                        **({"ransac_inliers": [tr32[j]["ransac_inliers"], tr6[j]["ransac_inliers"]],
+                            "ransac_margin_px": round(tr32[j]["ransac_margin_px"], 4)} if mode == 1 else {})})
+        wc = cond <= 1e-4
+        r["score"][name] = {"pairs": tab, "images_ill_conditioned_at_f32_ulp": int((~wc).sum()),
+                            "cond_median": float(np.median(cond)),
+                            "frac_fp32x6_le_1e-4_well_conditioned": float((d6[wc] <= 1e-4).mean()) if wc.any() else None,
+                            "frac_torch_cpu_le_1e-4_well_conditioned": float((dc[wc] <= 1e-4).mean()) if wc.any() else None,
+                            "fp32x6_misses": per,
+                            "decisions": {k: sum(1 for p in per if p["decision"].split(" ")[0] == k)
+                                          for k in sorted({p["decision"].split(" ")[0] for p in per})}}
+        trace_pairs[name] = (d6, dc, cond, per)
+
     out = os.path.join(REPO, "gpurun_out")
     if os.path.isdir(out):
-        with open(os.path.join(out, "precision_floor.json"), "w") as f:
+        with open(os.path.join(out, "precision_score.json"), "w") as f:
             json.dump(r, f, indent=1)
-    print(json.dumps(r))
+        np.savez(os.path.join(out, "precision_keypoints.npz"),
+                 **{f"{k}_{j}": v[j].cpu().numpy() for k, v in impl.items() for j in range(3)})
+    print(json.dumps({k: v for k, v in r.items() if k != "score"}))
+    for name, s in r["score"].items():
+        print(name, json.dumps(s["pairs"]), s["decisions"])
+
+    # ---- gates
+    k = r["kpt"]
     assert fg.sum() > 300
-    assert r["ours_fp32_vs_torch_gpu"] <= 1e-3
-    assert r["fp32x6_vs_ours_fp32"] <= 2 * r["ours_fp32_vs_torch_gpu"] + 1e-5, r
-    assert r["fp32x6_vs_torch_cpu"] <= 1e-4, r
+    assert k["ours_fp32_vs_torch_gpu"] <= 1e-3
+    assert k["fp32x6_vs_ours_fp32"] <= 2 * k["ours_fp32_vs_torch_gpu"] + 1e-5, k
+    assert k["fp32x6_vs_torch_cpu"] <= 1e-4, k
+    for name, (d6, dc, cond, per) in trace_pairs.items():
+        tab = r["score"][name]["pairs"]
+        assert tab["fp32x6_vs_fp32"]["frac_le_1e-4"] >= tab["torch_cpu_vs_fp32"]["frac_le_1e-4"] - 0.1, (name, tab)
+        for p in per:
+            explained = p["cond_f32_ulp"] > 1e-4 or p["delta_torch_cpu"] > 1e-4 or p["decision"] != "continuous"
+            assert explained, (name, p)
+
+
+def _ulp_conditioning(solver, px, probs, q_gt, t_gt, score, dev, draws=16):
+    """Per image: the largest SPEED-score change over `draws` re-solves of the keypoints each moved
+    by one float32 ulp per coordinate in a random direction (bench.Fp32Reference.cond)."""
+    from spe.speed_eval import device_speed_score
+    p = px.cpu().numpy().astype(np.float32)
+    n = p.shape[0]
+    rng = np.random.Generator(np.random.PCG64(11))
+    sgn = rng.choice(np.array([-np.inf, np.inf], np.float32), size=(draws,) + p.shape)
+    pp = np.nextafter(np.broadcast_to(p, (draws,) + p.shape), sgn).astype(np.float32).reshape((draws * n,) + p.shape[1:])
+    po = solver.solve_batch(torch.from_numpy(pp).to(dev), probs.repeat(draws, 1, 1))
+    st, sq = device_speed_score(po["quat"], po["tvec"], q_gt.repeat(draws, 1), t_gt.repeat(draws, 1))
+    sc = (st + sq).cpu().numpy().reshape(draws, n)
+    diff = np.abs(sc - score[None])
+    diff = np.where(np.isnan(sc) != np.isnan(score[None]), np.inf, diff)
+    return np.nan_to_num(diff, nan=0.0).max(0)

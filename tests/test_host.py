@@ -216,13 +216,23 @@ def test_bench_launcher_spawns_ranks():
     env = dict(os.environ, SPE_BENCH_STUB="1", OMP_NUM_THREADS="1")
     for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
         env.pop(k, None)
-    r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--batch", "4", "--steps", "3",
-                        "--warmup", "1"], env=env, capture_output=True, text=True, timeout=180)
-    assert r.returncode == 0, r.stderr[-2000:]
-    d = _bench_line(r.stdout)
+    lines = {}
+    for n in (2, 1):
+        r = subprocess.run([sys.executable, os.path.join(repo, "bench.py"), "--gpus", str(n), "--batch", "4", "--steps",
+                            "3", "--warmup", "1"], env=env, capture_output=True, text=True, timeout=180)
+        assert r.returncode == 0, r.stderr[-2000:]
+        lines[n] = _bench_line(r.stdout)
+    d = lines[2]
     assert d["n_gpus"] == 2 and d["config"]["global_batch"] == 8 and d["config"]["per_gpu_batch"] == 4
     assert d["records_gathered_per_step"] == 8
     assert d["value"] > 0 and d["steps"] == 3
+    # the north-star shape: global batch 256 split 128 per rank over the fixed
+    # pool, and the same weights at world 1 and world 2 (committed head fixture, no fit per run)
+    ns = d["north_star"]
+    assert ns["global_batch"] == 256 and ns["per_gpu_batch"] == 128 and ns["solver"] == "ransac_p3p_lm"
+    assert ns["pool_images"] == list(range(256))
+    assert lines[1]["north_star"]["per_gpu_batch"] == 256
+    assert d["weights_sha256_16"] is not None and d["weights_sha256_16"] == lines[1]["weights_sha256_16"]
 
 
 def test_bench_rejects_world_mismatch():
@@ -273,21 +283,6 @@ def test_fit_point_head_with_logit_offset():
     assert np.abs(pts - tgt).max() < 0.05 and err.max() < 0.05, (np.abs(pts - tgt).max(), err.max())
 
 
-def test_cu_partition_balanced_both_ways():
-    """PosePipeline(cu_split=k): the backbone mask holds k/8 of every run of 8 CUs and of every
-    8-strided set (either XCD interleave of the runtime's CU order), the encoder the rest."""
-    from spe.pipeline import cu_partition
-    ncu = 256
-    for k in (1, 2, 3, 4):
-        bb, en = cu_partition(ncu, k)
-        bits = lambda m: [i for i in range(ncu) if (m[i // 32] >> (i % 32)) & 1]
-        b, e = set(bits(bb)), set(bits(en))
-        assert not (b & e) and len(b | e) == ncu and len(b) == ncu * k // 8
-        for x in range(8):
-            assert sum(1 for i in b if i % 8 == x) == 32 * k // 8      # striped XCD order
-            assert sum(1 for i in b if i // 32 == x) == 32 * k // 8    # blocked XCD order
-
-
 @pytest.mark.parametrize("decode,backbone", [(False, False), (True, False), (True, True)])
 def test_pipeline_staged_state_without_gpu(monkeypatch, decode, backbone):
     """PosePipeline's constructor on the CPU (HIP streams stubbed): the staged forms own their
@@ -310,10 +305,35 @@ def test_pipeline_staged_state_without_gpu(monkeypatch, decode, backbone):
         def new_workspace(self, B, dev):
             return torch.zeros(1)
     p = pp.PosePipeline(_Model(), None, 2, device="cpu", overlap_decode=decode, overlap_backbone=backbone)
-    assert p.bb_stream is None
+    assert not p.per_image_th and p.repro.shape == (2,)
     if decode:
         n = 3 if backbone else 2
         assert p.nslot == n and p.calls == 0 and len(p.ws2) == n and len(p.slot_clip) == n
         assert (p.enc_stream is not None) == backbone and p.dec_stream is not None
     else:
         assert not hasattr(p, "ws2")
+
+
+def test_epnp_ceres_batch_needs_areas_and_keeps_state():
+    """EPnPCeresSolver.solve_batch derives every image's threshold from its own box area
+    (UNC/utils/speed_eval_ceres.py:53-58,90); a batch without areas is refused instead of running
+    at the constructor's 20 px, and batch thresholds leave reprojectionError (the reference's
+    per-image __call__ state) untouched."""
+    import torch
+    from spe.solver import EPnPCeresSolver
+    s = EPnPCeresSolver(input_size=256)
+    s.get_repro_th(100.0)                       # the per-image path: int(100/256*10) = 3
+    assert s.reprojectionError == 3.0
+    assert [s.repro_th(a) for a in (10.0, 100.0, 1e5)] == [1.5, 3.0, 20.0]
+    assert s.reprojectionError == 3.0
+    pts, probs = torch.zeros(2, 11, 2), torch.zeros(2, 11, 12)
+    with pytest.raises(ValueError, match="area"):
+        s.solve_batch(pts, probs)
+
+
+def test_ground_truth_area_keeps_reference_precedence():
+    """UNC SpeedEval's area = sqrt((x2 - x1) * y2 - y1) (src/data/speed/speed_dataset.py:370-373)."""
+    from spe.speed_eval import load_ground_truth
+    g = load_ground_truth([{"filename": "a.jpg", "q_vbs2tango": [1, 0, 0, 0], "r_Vo2To_vbs_true": [0, 0, 10],
+                            "bbox_xxyy": [100.0, 200.0, 300.0, 400.0]}])
+    assert g["a.jpg"]["area"] == pytest.approx(np.sqrt(200.0 * 400.0 - 200.0))
