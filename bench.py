@@ -27,7 +27,7 @@ sys.path.insert(0, os.path.join(REPO, "satellite-pose-estimation_amd"))
 # fp32x6 (the accuracy-contract mode) runs its GEMMs / convolutions on six bf16 MFMAs per product and
 # its attention as fp32x3: the ceiling for a launch depends on its class (peak_for).
 PEAK = {"bf16": {"mfma": 2500.0}, "fp32": {"mfma": 157.3}, "fp32x3": {"mfma": 2500.0 / 3},
-        "fp32x6": {"mfma": 2500.0 / 6}, "hbm": 8000.0}
+        "fp32x6": {"mfma": 2500.0 / 6}, "fp32h3": {"mfma": 2500.0 / 3}, "hbm": 8000.0}
 
 
 # BASELINE.json north_star: ">= 10k img/s on 8 x MI355X at 416x416 bs=256, RANSAC-PnP + GN refinement"
@@ -35,13 +35,18 @@ NORTH_STAR_GLOBAL_BATCH = 256
 PARITY_MODE_TEXT = {"fp32x6": "fp32 storage; GEMMs / convolutions at near-fp32 precision (three-way split, six bf16 "
                               "products), attention as fp32x3 (DESIGN.md section 4)",
                     "fp32x3": "fp32 storage, split-bf16 MFMA (hi.hi + hi.lo + lo.hi)",
-                    "fp32": "fp32 storage, exact-f32 MFMA"}
+                    "fp32": "fp32 storage, exact-f32 MFMA",
+                    "fp32h3": "fp32 storage; backbone / encoder GEMMs and convolutions at near-fp32 precision as three "
+                              "fp16 MFMAs on a power-of-two-scaled two-way fp16 split, decoder GEMMs as fp32x6, "
+                              "attention as fp32x3 (DESIGN.md section 4)"}
 
 
 def peak_for(dtype, kind):
     """MFMA ceiling (TFLOP/s of model flops) of launch class `kind` in mode `dtype`."""
     if dtype == "fp32x6" and kind.startswith("attn."):
         return PEAK["fp32x3"]["mfma"]
+    if dtype == "fp32h3" and kind.startswith("gemm.dec"):    # the decoder's few-row GEMMs stay on x6
+        return PEAK["fp32x6"]["mfma"]
     return PEAK[dtype]["mfma"]
 # profiler symbol of each launch class (to match profiles/*kernel_stats.csv rows)
 # (rocprofv3 prints the attention kernels mangled: it does not demangle the __bf16 / _Float16
@@ -86,7 +91,7 @@ def parse():
     p.add_argument("--layers", type=int, default=None)
     p.add_argument("--solver", default=None, choices=["epnp", "epnp_lm", "ransac_p3p_lm", "epnp_ransac_sigma", "epnp_ceres"])
     p.add_argument("--sigma-head", type=int, default=None, choices=[0, 1])
-    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp32x3", "fp32x6"],
+    p.add_argument("--dtype", default="bf16", choices=["bf16", "fp32", "fp32x3", "fp32x6", "fp32h3"],
                    help="bf16: throughput mode; fp32: exact-f32 MFMA parity mode; fp32x3: fp32 storage with "
                         "split-bf16 MFMA (the fast parity mode)")
     p.add_argument("--attn-dtype", dest="attn_dtype", default=None, choices=["bf16", "fp16"],
@@ -97,7 +102,7 @@ def parse():
                         "(default, DETR): label-diverse + the point head fitted on the timed batch so each "
                         "query predicts its label's landmark projection + N(0, 2 px) + 10%% outliers "
                         "(spe.synthetic.fit_point_head), so RANSAC finds consensus and the refinement runs")
-    p.add_argument("--parity-dtype", default="fp32x6", choices=["fp32x6", "fp32x3", "fp32"],
+    p.add_argument("--parity-dtype", default="fp32x6", choices=["fp32x6", "fp32h3", "fp32x3", "fp32"],
                    help="the parity mode timed after the main line in the same process (parity_mode object: its "
                         "own ms_per_step, value, roofline and accuracy against the exact-f32 mode)")
     p.add_argument("--no-parity", action="store_true", help="skip the parity_mode timing")
@@ -641,7 +646,8 @@ def time_mode(pipe, model, args, world, dev, dtype, attn_dtype, cfg, B, launch_t
     # (fp32x3 / fp32x6: attn_x3_kernel<true>, K / V^T pre-split by the projections, unless
     # SPE_ATTN_PRESPLIT=0)
     ps = "<true>" if os.environ.get("SPE_ATTN_PRESPLIT", "1") != "0" else "<false>"
-    symbol = ({"fp32": "attn_f32_kernel", "fp32x3": "attn_x3_kernel" + ps, "fp32x6": "attn_x3_kernel" + ps}[dtype]
+    symbol = ({"fp32": "attn_f32_kernel", "fp32x3": "attn_x3_kernel" + ps, "fp32x6": "attn_x3_kernel" + ps,
+               "fp32h3": "attn_x3_kernel" + ps}[dtype]
               if dominant == "attn.enc" and dtype != "bf16" else
               KIND_SYMBOL.get(dominant, dominant).replace("DF16b", "DF16_" if attn_dtype == "fp16" else "DF16b"))
     roofline = {"kernel": dominant, "kernel_symbol": symbol,

@@ -36,8 +36,12 @@ enum {
  * mode on the bench's amplifying weights too): fp32 storage, every GEMM / convolution with
  * near-fp32 precision (x = hi + mid + lo in bf16, the six products of relative order >= 2^-16), the
  * encoder attention contractions as F32X3_, the decoder attention (whose 64x-sharpened cross-attention
- * amplifies operand error most) in exact f32 */
-enum { SPE_DTYPE_BF16_ = 0, SPE_DTYPE_F32_ = 1, SPE_DTYPE_F16_ = 2, SPE_DTYPE_F32X3_ = 4, SPE_DTYPE_F32X6_ = 5 };
+ * amplifies operand error most) in exact f32; F32H3_ (round 5): F32X6_ with the backbone / encoder GEMMs and
+ * convolutions as three fp16 MFMAs on a two-way fp16 split (x.s = hi + lo, fp16 RNE each, s a power of two:
+ * per output channel for the weights, per tensor for the activations from the producer's max |x|),
+ * products hi.hi + hi.lo + lo.hi -- F32X6_'s accuracy (2^-22-level operands) at half its MFMAs */
+enum { SPE_DTYPE_BF16_ = 0, SPE_DTYPE_F32_ = 1, SPE_DTYPE_F16_ = 2, SPE_DTYPE_F32X3_ = 4, SPE_DTYPE_F32X6_ = 5,
+       SPE_DTYPE_F32H3_ = 6 };
 
 /* Solver modes.
  *  SPE_PNP_EPNP              cv2.solvePnPGeneric(EPNP) on all selected points
@@ -82,7 +86,7 @@ typedef struct {
   int nheads;           /* --nheads (8; head_dim must be 32) */
   int dim_feedforward;  /* --dim_feedforward (2048) */
   int sigma_head;       /* 1: UNC-style sigma head (sigma_embed.layers.*) */
-  int dtype;            /* SPE_DTYPE_BF16_ (bf16 storage, fp32 accumulate), SPE_DTYPE_F32_, _F32X3_ or _F32X6_ */
+  int dtype;            /* SPE_DTYPE_BF16_ (bf16 storage, fp32 accumulate), SPE_DTYPE_F32_, _F32X3_, _F32X6_ or _F32H3_ */
   int attn_dtype;       /* encoder self-attention operands (q, k, V^T): 0 = as dtype; SPE_DTYPE_F16_ =
                          * fp16 (bf16 models only; BASELINE config 5's "fp16 MFMA attention") */
 } spe_model_config;
@@ -282,8 +286,17 @@ int spe_debug_gemm(void* stream, int dtype, int mode, const void* A, int lda, co
 /* kernel family that served this thread's last gemm launch: 0 the 128x128 kernel, 1 the large-tile
  * kernels (gemm2.hip), 2 the persistent streaming kernel for short-K problems (gemm_stream.hip),
  * 3 the patch-staged 3x3 conv (pconv.hip), 4 the projection + residual + LayerNorm (lnproj.hip),
- * 5 the fp32x6 three-way split kernel (gemm.hip), 6 its LDS-DMA form (gemm.hip gemm_x6d) */
+ * 5 the fp32x6 three-way split kernel (gemm.hip), 6 its LDS-DMA form (gemm.hip gemm_x6d), 7 the fp32h3
+ * scaled fp16 split kernel (gemm.hip gemm_h3d) */
 int spe_debug_gemm_path(void);
+/* fp32h3 (gemm.hip gemm_h3d): C = act((A . W^T) + bias + R) on fp32 A (LINEAR or CONV geometry as
+ * spe_debug_gemm) with the weights given as the finalize form -- planes = fp16 [2][plane_rows][ldb]
+ * holding hi, lo of W[n] * 2^e_n, sinv[n] = 2^-e_n -- and amax_a = device max |A| (nullable: scale
+ * 1).  amax_c (nullable): max |stored C| * (amax_c_mul or 1) atomically maxed into it (float bits). */
+int spe_debug_gemm_h3(void* stream, int mode, const void* A, int lda, int H, int W, int Cin, int KH, int KW, int stride,
+                      int pad, int ldb, int M, int N, int K, const float* bias, const void* R, int ldr, int act_code,
+                      void* C, int ldc, const void* planes, int plane_rows, const float* sinv, const float* amax_a,
+                      float* amax_c, float amax_c_mul);
 /* the same launch with the weights also given pre-split (dtype SPE_DTYPE_F32X6_): planes = bf16
  * [3][plane_rows][ldb] holding hi, mid, lo of Bw (what spe_model_finalize writes for fp32x6 models) */
 int spe_debug_gemm_planes(void* stream, int dtype, int mode, const void* A, int lda, const void* P, int ldp, int prow,

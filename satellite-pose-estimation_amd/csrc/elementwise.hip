@@ -12,18 +12,25 @@
 namespace {
 
 template <typename T>
-__global__ void pack_input_kernel(const float* __restrict__ img, T* __restrict__ out, int B, int S) {
+__global__ void pack_input_kernel(const float* __restrict__ img, T* __restrict__ out, int B, int S, float* amax) {
   const size_t npx = (size_t)B * S * S;
+  float am = 0.f;
   for (size_t p = blockIdx.x * (size_t)blockDim.x + threadIdx.x; p < npx; p += (size_t)gridDim.x * blockDim.x) {
     const size_t b = p / ((size_t)S * S), hw = p - b * S * S;
     const float* src = img + b * 3 * S * S + hw;
     float v[8] = {src[0], src[(size_t)S * S], src[2 * (size_t)S * S], 0.f, 0.f, 0.f, 0.f, 0.f};
+    am = fmaxf(am, fmaxf(fabsf(v[0]), fmaxf(fabsf(v[1]), fabsf(v[2]))));
     if constexpr (sizeof(T) == 2) {
       st16(out + p * 8, pack16<T>(v));
     } else {
       st16(out + p * 8, pack16<T>(v));
       st16(out + p * 8 + 4, pack16<T>(v + 4));
     }
+  }
+  if (amax) {                                    // every lane reaches here (grid-stride loop)
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) am = fmaxf(am, __shfl_xor(am, o, 64));
+    if ((threadIdx.x & 63) == 0 && am > 0.f) atomicMax((unsigned*)amax, __float_as_uint(am));
   }
 }
 
@@ -273,10 +280,11 @@ inline int grid_for(size_t n, int block) {
 
 }  // namespace
 
-int spe_launch_pack_input(const float* img, void* out, int B, int S, int dtype, hipStream_t s) {
+int spe_launch_pack_input(const float* img, void* out, int B, int S, int dtype, hipStream_t s, float* amax) {
   const size_t n = (size_t)B * S * S;
-  if (dtype == SPE_DTYPE_BF16) hipLaunchKernelGGL(pack_input_kernel<bf16>, grid_for(n, 256), 256, 0, s, img, (bf16*)out, B, S);
-  else hipLaunchKernelGGL(pack_input_kernel<float>, grid_for(n, 256), 256, 0, s, img, (float*)out, B, S);
+  if (dtype == SPE_DTYPE_BF16)
+    hipLaunchKernelGGL(pack_input_kernel<bf16>, grid_for(n, 256), 256, 0, s, img, (bf16*)out, B, S, (float*)nullptr);
+  else hipLaunchKernelGGL(pack_input_kernel<float>, grid_for(n, 256), 256, 0, s, img, (float*)out, B, S, amax);
   return (int)hipGetLastError();
 }
 

@@ -68,11 +68,18 @@ int run_gemm(spe_model* m, const char* kind, const GemmArgs& g, int mode, hipStr
   const double r_rows = g.R ? (g.r_period > 0 ? (double)g.r_period : (double)g.M) : 0.0;
   const double bytes = (a_elems + (double)g.N * g.K + (double)g.M * g.N + r_rows * g.N) * E +
                        (mode == GEMM_LINEAR_ADD ? (double)g.prow * g.K * E : 0.0);
-  const int dt = !x3_for(m, kind) ? m->cfg.dtype : m->x6 ? (int)SPE_DTYPE_F32X6 : (int)SPE_DTYPE_F32X3;
+  int dt = !x3_for(m, kind) ? m->cfg.dtype : m->x6 ? (int)SPE_DTYPE_F32X6 : (int)SPE_DTYPE_F32X3;
   GemmArgs ga = g;
   if (dt == SPE_DTYPE_F32X6) {
     const auto it = m->w6.find(g.B);
     if (it != m->w6.end()) { ga.B6 = it->second.first; ga.b6_rows = it->second.second; }
+    // fp32h3: the GEMMs whose A operand has a published max |A| (the backbone and encoder) take the
+    // scaled fp16 split (gemm.hip gemm_h3d); the decoder's few-row GEMMs stay on x6
+    const auto ih = m->wh3.find(g.B);
+    if (m->h3 && g.amax_a && ih != m->wh3.end()) {
+      ga.H3 = ih->second.planes; ga.h3_rows = ih->second.rows; ga.h3_sinv = ih->second.sinv;
+      dt = SPE_DTYPE_F32H3;
+    }
   }
   return run_other(m, kind, 2.0 * g.M * g.N * g.K, bytes, s, [&] { return spe_launch_gemm(ga, dt, mode, s); });
 }
@@ -189,15 +196,26 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   const float scale = 1.0f / std::sqrt(32.0f);
   const int Mt = B * T;
   const bool xa = spe_use_xattn(m);
+  // fp32h3: each tensor a GEMM reads carries a device max |x| (the producer's published maximum,
+  // or a bound), the scale input of the scaled fp16 split (gemm.hip gemm_h3d).  Slots: backbone
+  // [0, SPE_AMAX_BB), the neck output (the encoder's first input) at SPE_AMAX_BB - 1, transformer
+  // [SPE_AMAX_BB, SPE_AMAX_SLOTS); each stage zeroes its own range first.
+  float* const amx = m->h3 ? (float*)P(w.amax) : nullptr;
+  float* const src_amax0 = amx ? amx + SPE_AMAX_BB - 1 : nullptr;
   if (stages & SPE_STAGE_BACKBONE) {
+  int na = 0;
+  auto slot = [&]() -> float* { return amx ? amx + na++ : nullptr; };
+  if (amx) CK((int)hipMemsetAsync(amx, 0, SPE_AMAX_BB * 4, s));
   // ---------------- backbone (REV/models/backbone.py:133-149)
   const bool pairs = m->stem.Cin == 4;                 // bf16: pair-packed stem (registry.cpp)
+  float* const x0_amax = slot();
   if (pairs)
     CK(run_other(m, "eltwise.pack", 0.0, (double)B * S * S * 12 + (double)B * (S + 6) * (S + 6) * 8, s,
                  [&] { return spe_launch_pack_input_pad4(images, P(w.x0), B, S, s); }));
   else
-    CK(run_other(m, "eltwise.pack", 0.0, (double)B * S * S * (12 + 8 * m->esz), s, [&] { return spe_launch_pack_input(images, P(w.x0), B, S, dt, s); }));
+    CK(run_other(m, "eltwise.pack", 0.0, (double)B * S * S * (12 + 8 * m->esz), s, [&] { return spe_launch_pack_input(images, P(w.x0), B, S, dt, s, x0_amax); }));
   int H = S / 2;
+  float* const stem_amax = slot();
   const int Hp = (H + 2 - 3) / 2 + 1;
   // bf16: layer1 block 0's conv3 + downsample run as one GEMM over [conv2 output | pool output]
   // (Block::c3ds), so the max-pool writes the right half of that concatenation (w.ds region,
@@ -218,12 +236,15 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       GemmArgs g = pairs ? conv_args(m->stem, P(w.x0), B, S + 6, S + 6, P(w.stem), 64)
                          : conv_args(m->stem, P(w.x0), B, S, S, P(w.stem), 64);
       g.act = ACT_RELU;
+      g.amax_a = x0_amax; g.amax_c = stem_amax;
       CK(run_gemm(m, "conv.stem", g, GEMM_CONV, s));
     }
     CK(run_other(m, "eltwise.maxpool", 0.0, (double)B * 64 * (H * H + Hp * Hp) * m->esz, s, [&] { return spe_launch_maxpool3s2(P(w.stem), P(pool_at), B, H, H, 64, Hp, Hp, dt, s, uld); }));
   }
   H = Hp;
   size_t cur = pool_at;                                 // (w.pool aliases bufA)
+  const float* cur_amax = stem_amax;                    // the max-pool's maximum is the stem's
+  const float* xs8_amax = nullptr;
   int cin = 64, cur_ld = uld;
   bool t1_ready = false;                                // this block's conv1 ran in the previous tail
   // conv3 (+ residual) + relu of block bi and the next block's conv1 as one launch (btail.hip)
@@ -245,15 +266,20 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
     // layer1: blocks 0-2, layer2: 3-6 (its output xs8 is kept for the neck), layer3: 7-12
     const size_t outbuf = (bi == 6) ? w.xs8 : (cur == w.bufA ? w.bufB : w.bufA);
     const int Ho = (H + 2 - 3) / blk.stride + 1;
+    float* const t1_amax = slot();
+    float* const t2_amax = slot();
+    float* const out_amax = slot();
     if (!t1_ready) {  // conv1 1x1 + bn1 + relu
       GemmArgs g = linear_args(blk.c1, P(cur), cur_ld, B * H * H, P(w.t1), blk.c1.N);
       g.act = ACT_RELU;
+      g.amax_a = cur_amax; g.amax_c = t1_amax;
       CK(run_gemm(m, "conv.1x1", g, GEMM_LINEAR, s));
     }
     t1_ready = false;
     {  // conv2 3x3 (stride on the 3x3, ResNet v1.5) + bn2 + relu
       GemmArgs g = conv_args(blk.c2, P(w.t1), B, H, H, fused ? P(w.ds) : P(w.t2), fused ? uld : blk.c2.N);
       g.act = ACT_RELU;
+      g.amax_a = t1_amax; g.amax_c = t2_amax;
       CK(run_gemm(m, "conv.3x3", g, GEMM_CONV, s));
     }
     if (fused) {  // relu(W3 t2 + Wds x + b3 + bds) over the concatenation
@@ -277,9 +303,11 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
     if (blk.has_ds) {
       if (blk.stride == 1) {
         GemmArgs g = linear_args(blk.ds, P(cur), cin, B * H * H, P(w.ds), blk.ds.N);
+        g.amax_a = cur_amax;
         CK(run_gemm(m, "conv.1x1", g, GEMM_LINEAR, s));
       } else {
         GemmArgs g = conv_args(blk.ds, P(cur), B, H, H, P(w.ds), blk.ds.N);
+        g.amax_a = cur_amax;
         CK(run_gemm(m, "conv.1x1s2", g, GEMM_CONV, s));
       }
       res = w.ds;
@@ -293,18 +321,23 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       if (rc == 1) {
         GemmArgs g = linear_args(blk.c3, P(w.t2), blk.c2.N, B * Ho * Ho, P(outbuf), blk.c3.N);
         g.R = P(res); g.ldr = blk.c3.N; g.act = ACT_RELU;
+        g.amax_a = t2_amax; g.amax_c = out_amax;
         CK(run_gemm(m, "conv.1x1", g, GEMM_LINEAR, s));
       }
       t1_ready = rc == 0;
     }
+    cur_amax = out_amax;
+    if (bi == 6) xs8_amax = out_amax;
     cin = cur_ld = blk.c3.N;
     H = Ho;
     cur = outbuf;
   }
   const size_t xs16 = cur;                              // [B, S/16, S/16, 1024]
+  float* const cat_amax = slot();
   {  // s8_latern 1x1 512->256 into channels [0,256) of the concat buffer
     GemmArgs g = linear_args(m->s8, P(w.xs8), 512, B * T, P(w.cat), 512);
     g.bias = nullptr;
+    g.amax_a = xs8_amax; g.amax_c = cat_amax;
     CK(run_gemm(m, "conv.neck", g, GEMM_LINEAR, s));
   }
   if (spe_use_upconv(m)) {
@@ -312,6 +345,9 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
     // (w.up holds Z [B*(S/16)^2][9*256]), then the bilinear combine into channels [256,512)
     const int h = S / 16, nz = m->s16taps.N;
     GemmArgs g = linear_args(m->s16taps, P(xs16), 1024, B * h * h, P(w.up), nz);
+    // the combine sums nine bilinear interpolations of Z (each a convex combination): its output
+    // is bounded by 9 max |Z|, published into the concat's slot
+    g.amax_a = cur_amax; g.amax_c = cat_amax; g.amax_c_mul = 9.f;
     CK(run_gemm(m, "conv.neck", g, GEMM_LINEAR, s));
     const double by = ((double)B * h * h * nz + (double)B * 4 * h * h * 256) * m->esz;
     CK(run_other(m, "eltwise.upconv", 0.0, by, s, [&] { return spe_launch_upconv_combine(P(w.up), (char*)P(w.cat) + 256 * m->esz, 512, B, h, h, 256, dt, s); }));
@@ -320,24 +356,34 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   {  // s16_latern 3x3 1024->256 into channels [256,512)
     GemmArgs g = conv_args(m->s16, P(w.up), B, F, F, (char*)P(w.cat) + 256 * m->esz, 512);
     g.bias = nullptr;
+    g.amax_a = cur_amax; g.amax_c = cat_amax;          // (bilinear upsampling keeps max |x|)
     CK(run_gemm(m, "conv.neck", g, GEMM_CONV, s));
   }
   }
   if (spe_use_neckfold(m)) {  // input_proj . output_conv as one 3x3 conv 512->256 -> src [B*T, 256]
     GemmArgs g = conv_args(m->neckip, P(w.cat), B, F, F, P(w.src), d);
+    g.amax_a = cat_amax; g.amax_c = src_amax0;
     CK(run_gemm(m, "conv.neck", g, GEMM_CONV, s));
   } else {
+  float* const neck_amax = slot();
   {  // output_conv 3x3 512->512 + bias
     GemmArgs g = conv_args(m->outc, P(w.cat), B, F, F, P(w.neck), 512);
+    g.amax_a = cat_amax; g.amax_c = neck_amax;
     CK(run_gemm(m, "conv.neck", g, GEMM_CONV, s));
   }
   {  // input_proj 1x1 512->256 + bias -> src [B*T, 256] (token order h*W+w)
     GemmArgs g = linear_args(m->inproj, P(w.neck), 512, B * T, P(w.src), d);
+    g.amax_a = neck_amax; g.amax_c = src_amax0;
     CK(run_gemm(m, "gemm.input_proj", g, GEMM_LINEAR, s));
   }
   }
+  if (na > SPE_AMAX_BB - 1) return fail(SPE_E_STATE, "fp32h3: backbone activation-scale slots exhausted");
   }  // SPE_STAGE_BACKBONE
   if (stages & SPE_STAGE_TRANSFORMER) {
+  float* const tam = amx ? amx + SPE_AMAX_BB : nullptr;
+  if (tam) CK((int)hipMemsetAsync(tam, 0, (SPE_AMAX_SLOTS - SPE_AMAX_BB) * 4, s));
+  const float* src_amax = src_amax0;
+  int li = 0;
 
   // ---------------- encoder (REV/models/transformer.py:154-167)
   // fp16 encoder attention operands (bf16 models, attn_dtype = SPE_DTYPE_F16_): the q/k and V^T
@@ -362,6 +408,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
     {
       GemmArgs g = linear_args(e.qk, P(w.src), d, Mt, P(w.qkv), 3 * d);
       g.out_f16 = f16attn;
+      g.amax_a = src_amax;
       if (presplit) { g.S = P(w.kpl); g.s_col0 = d; }
       const int mode = add_pos(m, g, m->pos, d, T, e.pos_qk, 2 * d);
       CK(run_gemm(m, "gemm.enc.qk", g, mode, s));
@@ -369,6 +416,8 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
     {
       GemmArgs g = linear_args(e.v, P(w.src), d, Mt, P(w.vt), 8);
       g.vt_T = T; g.vt_B = B; g.vt_swz = vt_swz;
+      // the attention output is a convex combination of V rows: max |V| bounds it
+      g.amax_a = src_amax; g.amax_c = tam ? tam + 2 * li : nullptr;
       g.out_f16 = f16attn || f16v;
       if (presplit) g.S = P(w.vt);               // hi plane then lo plane, in the fp32 V^T's bytes
       CK(run_gemm(m, "gemm.enc.v", g, GEMM_LINEAR, s));
@@ -387,6 +436,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       // out-proj + residual; bf16 large batches fuse norm1 into the GEMM epilogue, in place over src
       GemmArgs g = linear_args(e.o, P(w.ao), d, Mt, P(w.tmp), d);
       g.R = P(w.src); g.ldr = d;
+      g.amax_a = tam ? tam + 2 * li : nullptr;
       GemmArgs gf = g;
       gf.C = P(w.src); gf.ln_g = e.n1g; gf.ln_b = e.n1b;
       if (m->esz == 2 && spe_ln_fusable(gf)) {
@@ -395,6 +445,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
         CK(run_gemm(m, "gemm.enc.o", g, GEMM_LINEAR, s));
         CK(run_other(m, "ln.enc", 0.0, (double)Mt * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.tmp), e.n1g, e.n1b, P(w.src), nullptr, Mt, d, dt, s); }));
       }
+      src_amax = e.n1_bound;
     }
     if (use_fused_ffn(m)) {
       // the last layer also emits memory + pos for the cross-K projection (xattn adds pos itself)
@@ -405,16 +456,21 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       {
         GemmArgs g = linear_args(e.l1, P(w.src), d, Mt, P(w.ffn), ff);
         g.act = ACT_RELU;
+        g.amax_a = src_amax; g.amax_c = tam ? tam + 2 * li + 1 : nullptr;
         CK(run_gemm(m, "gemm.enc.ffn1", g, GEMM_LINEAR, s));
       }
       {
         GemmArgs g = linear_args(e.l2, P(w.ffn), ff, Mt, P(w.tmp), d);
         g.R = P(w.src); g.ldr = d;
+        g.amax_a = tam ? tam + 2 * li + 1 : nullptr;
         CK(run_gemm(m, "gemm.enc.ffn2", g, GEMM_LINEAR, s));
       }
       CK(run_other(m, "ln.enc", 0.0, (double)Mt * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.tmp), e.n2g, e.n2b, P(w.src), nullptr, Mt, d, dt, s); }));
     }
+    src_amax = e.n2_bound;
+    ++li;
   }
+  if (tam && 2 * li > SPE_AMAX_SLOTS - SPE_AMAX_BB) return fail(SPE_E_STATE, "fp32h3: encoder activation-scale slots exhausted");
   // memory = src.  Unless the layers attend to memory + pos / memory directly (xattn path),
   // project the cross-attention K (memory + pos) and V^T (memory) for all decoder layers.
   if (!xa) {
@@ -424,11 +480,13 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
     const bool have_srcpos = use_fused_ffn(m) && !m->enc.empty();
     GemmArgs g = linear_args(m->crossK, P(have_srcpos ? w.srcpos : w.src), d, Mt, P(w.ck), L * d);
     const int mode = have_srcpos ? GEMM_LINEAR : add_pos(m, g, m->pos, d, T, m->pos_crossK, L * d);
+    if (!have_srcpos) g.amax_a = src_amax;
     CK(run_gemm(m, "gemm.cross_kv", g, mode, s));
   }
   {
     GemmArgs g = linear_args(m->crossV, P(w.src), d, Mt, P(w.cvt), 8);
     g.vt_T = T; g.vt_B = B;
+    g.amax_a = src_amax;
     CK(run_gemm(m, "gemm.cross_kv", g, GEMM_LINEAR, s));
   }
   }

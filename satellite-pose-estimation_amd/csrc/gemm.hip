@@ -214,11 +214,13 @@ SPE_DEV void mma_step(const char* st, int wr, int wc, int lane, f32x4 (&acc)[4][
 // bias / residual / activation / head-transposed or row stores of a BM_ x BN tile whose fp32
 // accumulators are in LDS (ct, row stride EPI_LD), NT_ threads; bv = the thread's 8 bias values
 template <typename T, int BM_, int NT_, int BN_ = BN>
-SPE_DEV void store_tile(const GemmArgs& g, const float* ct, int m0, int n0, int tid, const float* bv) {
+SPE_DEV float store_tile(const GemmArgs& g, const float* ct, int m0, int n0, int tid, const float* bv) {
+  float am = 0.f;                                  // max |stored value| (g.amax_c)
+  const bool track = g.amax_c != nullptr;
   if (g.vt_T > 0) {
     // head-transposed store: column n = grp*256 + hd -> C[((grp*vt_B + b)*256 + hd)*T + tok]
     const int col = tid % BN_, n = n0 + col;
-    if (n >= g.N) return;
+    if (n >= g.N) return am;
     const float bn = g.bias ? g.bias[n] : 0.f;
     const int grp = n >> 8, hd = n & 255;
     for (int rg = (tid / BN_) * 8; rg < BM_; rg += (NT_ / BN_) * 8) {
@@ -227,6 +229,8 @@ SPE_DEV void store_tile(const GemmArgs& g, const float* ct, int m0, int n0, int 
       float v[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = ct[(rg + e) * EPI_LD + col] + bn;
+      if (track)
+        for (int e = 0; e < 8 && m + e < g.M; ++e) am = fmaxf(am, fabsf(v[e]));
       const int b = m / g.vt_T, tok = m - b * g.vt_T;
       const size_t rowbase = ((size_t)(grp * g.vt_B + b) * 256 + hd) * g.vt_T;
       if constexpr (sizeof(T) == 4) {
@@ -276,13 +280,13 @@ SPE_DEV void store_tile(const GemmArgs& g, const float* ct, int m0, int n0, int 
         }
       }
     }
-    return;
+    return am;
   }
 
   constexpr int CG = BN_ / 8;                       // 8-column groups per row
   const int cg = (tid % CG) * 8;
   const int n = n0 + cg;
-  if (n >= g.N) return;
+  if (n >= g.N) return am;
   const bool full = n + 8 <= g.N;
   for (int rr = tid / CG; rr < BM_; rr += NT_ / CG) {
     const int m = m0 + rr;
@@ -308,6 +312,8 @@ SPE_DEV void store_tile(const GemmArgs& g, const float* ct, int m0, int n0, int 
       for (int e = 0; e < 8; ++e) v[e] = apply_act(v[e], g.act);
     }
     if (g.R && g.res_post) add_res();
+    if (track)
+      for (int e = 0; e < 8 && n + e < g.N; ++e) am = fmaxf(am, fabsf(v[e]));
     if constexpr (sizeof(T) == 4) {
       if (g.S && n >= g.s_col0) {                // bf16 hi / lo planes (fp32x3 attention operands)
         const int ns = g.N - g.s_col0;
@@ -356,6 +362,15 @@ SPE_DEV void store_tile(const GemmArgs& g, const float* ct, int m0, int n0, int 
       }
     }
   }
+  return am;
+}
+
+// one atomic max per wave of the lanes' |value| maxima (all lanes of the wave active); float bits
+// compare as uint for values >= 0
+SPE_DEV void amax_publish(float am, float* slot, float mul) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) am = fmaxf(am, __shfl_xor(am, o, 64));
+  if ((threadIdx.x & 63) == 0 && am > 0.f) atomicMax((unsigned*)slot, __float_as_uint(am * (mul > 0.f ? mul : 1.f)));
 }
 
 template <typename T, int MODE, bool X3 = false>
@@ -421,7 +436,8 @@ __global__ __launch_bounds__(NT, 2) void gemm_kernel(GemmArgs g) {
   }
   __syncthreads();
 
-  store_tile<T, BM, NT>(g, ct, m0, n0, tid, bv);
+  const float am = store_tile<T, BM, NT>(g, ct, m0, n0, tid, bv);
+  if (g.amax_c) amax_publish(am, g.amax_c, g.amax_c_mul);
 }
 
 // ------------------------------------------------------------------ fp32x6 (near-fp32) kernel
@@ -629,7 +645,8 @@ __global__ __launch_bounds__(X6Geo<BMX>::NT, BMX == 256 ? 1 : 2) void gemm_x6_ke
           ct[(wr * 64 + i * 16 + q * 4 + r) * EPI_LD + wc * 64 + j * 16 + c] = acc[i][j][r];
   }
   __syncthreads();
-  store_tile<float, G::BM, G::NT>(g, ct, m0, n0, tid, bv);
+  const float am = store_tile<float, G::BM, G::NT>(g, ct, m0, n0, tid, bv);
+  if (g.amax_c) amax_publish(am, g.amax_c, g.amax_c_mul);
 }
 
 template <int BMX>
@@ -899,7 +916,8 @@ __device__ __forceinline__ void gemm_x6d_body(const GemmArgs& g) {
       for (int r = 0; r < 16; ++r)
         ct[(wr * 32 * FI + 32 * i + 8 * (r >> 2) + 4 * hi + (r & 3)) * EPI_LD + wc * 64 + 32 * j + l31] = acc[i][j][r];
   __syncthreads();
-  store_tile<float, D6_BM, D6_NT, D6_BN>(g, ct, m0, n0, tid, bv);
+  const float am = store_tile<float, D6_BM, D6_NT, D6_BN>(g, ct, m0, n0, tid, bv);
+  if (g.amax_c) amax_publish(am, g.amax_c, g.amax_c_mul);
 }
 
 // (non-template entry points: the host stubs of a template of this body were not emitted)
@@ -944,6 +962,287 @@ int launch_x6d(const GemmArgs& g, int mode, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// ---------------------------------------------------------------- fp32h3, LDS-DMA staged
+// fp32 operands at near-fp32 precision on HALF the x6 kernel's MFMAs: fp16 carries 11 significand
+// bits against bf16's 8, so a two-way split x.s = hi + lo (fp16 RNE each, the remainder exact in
+// fp32) represents x to ~2^-22 -- bf16's three-way split to ~2^-24 -- and the three products
+// lo.hi + hi.lo + hi.hi (small first) on v_mfma_f32_32x32x16_f16 (the bf16 rate) give an fp32-level
+// product.  fp16's range needs scales, powers of two so they cost no precision: the weights are
+// split at finalize per output channel (h3_sinv[n] = 2^-e_n undoes it), the activations per tensor
+// from max |A| (amax_a, published by the producing launch: 2^13 / amax rounded down to a power of
+// two puts the tensor's largest element in [2^12, 2^13), so hi <= 65504 always and a value 2^-36 of
+// the maximum still splits to fp32 accuracy).  oracle/study_split_precision.py: this scheme moves
+// the bench weights' keypoints 2.2e-5 from exact fp32, the x6 scheme 2.2e-5, fp32x3 3.9e-4.
+// Geometry: 4 waves stacked in M, wave tile 32 x 32 FJ (FJ = 4: 128 x 128, FJ = 2: 128 x 64 for N <= 64),
+// so every A row is split by exactly one wave (the x6 kernel's 2 x 2 waves split each row twice);
+// per K-step (32) and wave 6 FJ MFMAs, 16 fp32 values split per lane.  LDS stage: A [128][128 B]
+// fp32 (chunk c of row r at slot c ^ ((r >> 1) & 7)) + B planes [2][BN][64 B] fp16 (chunk c at
+// c ^ ((r >> 2) & 3)), both by buffer_load ... lds with the swizzle on the source address; two
+// stages + one barrier per step; the same pinned two-phase pipeline as gemm_x6d_body.
+constexpr int H3_BM = 128, H3_NT = 256, H3_A = H3_BM * 128;
+template <int FJ> struct H3Geo {
+  static constexpr int BN = 32 * FJ;
+  static constexpr int PB = BN * 64, STAGE = H3_A + 2 * PB;
+  static constexpr int NBQ = 2 * BN / 64;              // B DMA pieces per wave per step
+  static constexpr int SMEM = 2 * STAGE > H3_BM * EPI_LD * 4 ? 2 * STAGE : H3_BM * EPI_LD * 4;
+  static constexpr int NQ = 3 * FJ;                    // MFMAs per fragment set (K-step half)
+};
+
+// 4 fp32 -> (x s) fp16 planes hi, lo (4 values each)
+SPE_DEV void split2h(u32x4 x, float sc, u32x2& h, u32x2& l) {
+  const f32x4 f = __builtin_bit_cast(f32x4, x) * sc;
+  const f16x2 h0 = __builtin_convertvector((f32x2){f[0], f[1]}, f16x2);
+  const f16x2 h1 = __builtin_convertvector((f32x2){f[2], f[3]}, f16x2);
+  const f32x2 b0 = __builtin_convertvector(h0, f32x2), b1 = __builtin_convertvector(h1, f32x2);
+  const f16x2 l0 = __builtin_convertvector((f32x2){f[0] - b0[0], f[1] - b0[1]}, f16x2);
+  const f16x2 l1 = __builtin_convertvector((f32x2){f[2] - b1[0], f[3] - b1[1]}, f16x2);
+  h = u32x2{__builtin_bit_cast(uint32_t, h0), __builtin_bit_cast(uint32_t, h1)};
+  l = u32x2{__builtin_bit_cast(uint32_t, l0), __builtin_bit_cast(uint32_t, l1)};
+}
+
+template <int FJ> struct H3Frag {
+  u32x4 b[2][FJ];
+  u32x4 raw[2];
+  u32x2 ph[2], pl[2];
+};
+
+// the A operand's scale: 2^(13 - e) with max |A| in [2^(e-1), 2^e)
+SPE_DEV void h3_scale(const float* amax, float& sa, float& inv) {
+  sa = inv = 1.f;
+  if (!amax) return;
+  const float am = *amax;
+  if (!(am > 0.f) || !(am <= 3.0e38f)) return;
+  const int e = __builtin_amdgcn_frexp_expf(am);
+  sa = __builtin_ldexpf(1.f, 13 - e);
+  inv = __builtin_ldexpf(1.f, e - 13);
+}
+
+template <int MODE, int FJ, bool PL = false>
+__device__ __forceinline__ void gemm_h3d_body(const GemmArgs& g) {
+  using G = H3Geo<FJ>;
+  constexpr int BNH = G::BN, PB = G::PB, STG = G::STAGE, NBQ = G::NBQ, NQ = G::NQ;
+  __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tilesN = (g.N + BNH - 1) / BNH;
+  const int t = xcd_remap(blockIdx.x, gridDim.x);
+  const int m0 = (t / tilesN) * H3_BM, n0 = (t % tilesN) * BNH;
+  const int nk = (g.K + 31) >> 5;
+  const long long abytes = MODE == GEMM_CONV ? (long long)(g.M / (g.Ho * g.Wo)) * g.H * g.W * g.Cin * 4
+                                             : (long long)g.M * g.lda * 4;
+  const size_t pstride = (size_t)g.h3_rows * g.ldb;
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, (int)abytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)g.H3, (short)0, (int)(2 * pstride * 2), 0x00020000);
+  float sa, inv_sa;
+  h3_scale(g.amax_a, sa, inv_sa);
+
+  // ---- DMA pieces of this wave: A pieces wid + 4q (rows 8p .. 8p+7, lane -> row 8p + lane/8,
+  // slot lane & 7), B pieces wid + 4q (plane p / (BN/16), rows 16 (p % (BN/16)) + lane/4, slot lane & 3)
+  int avo[4], ih0[4], iw0[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int row = (wid + 4 * q) * 8 + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7), m = m0 + row;
+    if constexpr (MODE == GEMM_CONV) {
+      const int hw = g.Ho * g.Wo, mm = m < g.M ? m : 0;
+      const int b = mm / hw, r = mm - b * hw, oh = r / g.Wo, ow = r - oh * g.Wo;
+      ih0[q] = m < g.M ? oh * g.stride - g.pad : -(1 << 28);
+      iw0[q] = ow * g.stride - g.pad;
+      avo[q] = b * g.H * g.W * g.Cin + (PL ? 0 : c * 4);
+    } else {
+      avo[q] = m < g.M ? m * g.lda * 4 + c * 16 : D6_BAD;
+      ih0[q] = iw0[q] = 0;
+    }
+  }
+  int bvo[NBQ];
+#pragma unroll
+  for (int q = 0; q < NBQ; ++q) {
+    const int p = wid + 4 * q, plane = p / (BNH / 16), row = (p % (BNH / 16)) * 16 + (lane >> 2);
+    const int c = (lane & 3) ^ ((row >> 2) & 3), n = n0 + row;
+    bvo[q] = n < g.N ? (int)((plane * pstride + (size_t)n * g.ldb) * 2) + c * 16 : D6_BAD;
+  }
+  const int ck = (lane & 7) ^ ((wid * 4 + (lane >> 4)) & 7);
+  auto issue = [&](int ks, int stg) {
+    char* base = smem + stg * STG;
+    int kh = 0, kw = 0, ci = 0;
+    bool kv = true;
+    if constexpr (MODE == GEMM_CONV) {
+      if constexpr (PL) {
+        const int k = ks * 32 + ck * 4, tap = k / g.Cin;
+        ci = k - tap * g.Cin;
+        kh = tap / g.KW;
+        kw = tap - kh * g.KW;
+        kv = k < g.K;
+      } else {
+        conv_k_decode(ks * 32, g.Cin, g.KW, g.KH * g.KW, kh, kw, ci);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      int off;
+      if constexpr (MODE == GEMM_CONV) {
+        const int ih = ih0[q] + kh, iw = iw0[q] + kw;
+        const bool v = kv && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+        off = v ? (avo[q] + (ih * g.W + iw) * g.Cin + ci) * 4 : D6_BAD;
+      } else {
+        off = avo[q];
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lds_ptr6_t)(base + (wid + 4 * q) * 1024), 16, off,
+                                               MODE == GEMM_CONV ? 0 : ks * 128, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < NBQ; ++q)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lds_ptr6_t)(base + H3_A + (wid + 4 * q) * 1024), 16, bvo[q],
+                                               ks * 64, 0, 0);
+  };
+
+  // ---- fragment offsets: A row 32 wid + (lane & 31), 16-byte chunks 4kk + 2(lane >> 5) + h;
+  // B row 32 j + (lane & 31), chunk 2kk + (lane >> 5)
+  const int l31 = lane & 31, hi = lane >> 5;
+  int aoff[2][2], boff[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      aoff[kk][h] = (wid * 32 + l31) * 128 + (((4 * kk + 2 * hi + h) ^ ((l31 >> 1) & 7)) << 4);
+    boff[kk] = H3_A + l31 * 64 + (((2 * kk + hi) ^ ((l31 >> 2) & 3)) << 4);
+  }
+  auto mf = [](u32x4 x, u32x4 y, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, x), __builtin_bit_cast(f16x8, y), c, 0, 0, 0);
+  };
+  f32x16 acc[FJ];
+#pragma unroll
+  for (int j = 0; j < FJ; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+
+  using Frag = H3Frag<FJ>;
+  auto read_b = [&](const char* st, int kk, Frag& f) {
+#pragma unroll
+    for (int j = 0; j < FJ; ++j)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) f.b[p][j] = ld16(st + boff[kk] + p * PB + j * 2048);
+  };
+  auto read_a = [&](const char* st, int kk, Frag& f) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) f.raw[h] = ld16(st + aoff[kk][h]);
+  };
+  auto split_a = [&](Frag& f, int h) { split2h(f.raw[h], sa, f.ph[h], f.pl[h]); };
+  // MFMA number q (0 .. NQ-1) of a set: accumulator q / 3, product q % 3 (lo.hi, hi.lo, hi.hi)
+  auto mma1 = [&](const Frag& f, int q) {
+    const int j = q / 3, t = q % 3;
+    const u32x4 xa = t == 0 ? cat2(f.pl[0], f.pl[1]) : cat2(f.ph[0], f.ph[1]);
+    const u32x4 xb = t == 1 ? f.b[1][j] : f.b[0][j];
+    acc[j] = mf(xa, xb, acc[j]);
+  };
+#define H3_MMA(F, LO, HI)                                \
+  _Pragma("unroll") for (int q = LO; q < HI; ++q) mma1(F, q); \
+  __builtin_amdgcn_sched_barrier(0);
+
+  // Software pipeline over K-step halves as in gemm_x6d_body: phase A multiplies X (kk = 0) while
+  // Y (kk = 1) is read and split; one barrier; phase B multiplies Y while the next step's X is read
+  // from the other stage, whose DMA was issued a whole step earlier.
+  issue(0, 0);
+  issue(1, 1);
+  __builtin_amdgcn_s_waitcnt(d6_waitcnt_vm(4 + NBQ));
+  __syncthreads();
+  Frag X, Y;
+  read_b(smem, 0, X);
+  read_a(smem, 0, X);
+  split_a(X, 0);
+  split_a(X, 1);
+  constexpr int QA = NQ / 3;                           // MFMAs before / between the two splits (phase A)
+  constexpr int Q1 = NQ / 6 > 0 ? NQ / 6 : 1, Q2 = Q1 + NQ / 4, Q3 = Q2 + NQ / 4;   // phase B
+  for (int ks = 0; ks < nk; ++ks) {
+    const char* st = smem + (ks & 1) * STG;
+    const char* sn = smem + ((ks + 1) & 1) * STG;
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- phase A: X's MFMAs, Y read + split
+    read_b(st, 1, Y);
+    read_a(st, 1, Y);
+    H3_MMA(X, 0, QA)
+    split_a(Y, 0);
+    H3_MMA(X, QA, 2 * QA)
+    split_a(Y, 1);
+    H3_MMA(X, 2 * QA, NQ)
+    __builtin_amdgcn_s_waitcnt(d6_waitcnt_vm0() & ~(15 << 8));  // vmcnt(0) lgkmcnt(0)
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    // ---- phase B: Y's MFMAs, step ks+2's DMA, step ks+1's X read + split
+    issue(ks + 2, ks & 1);
+    H3_MMA(Y, 0, Q1)
+    read_b(sn, 0, X);
+    read_a(sn, 0, X);
+    H3_MMA(Y, Q1, Q2)
+    split_a(X, 0);
+    H3_MMA(Y, Q2, Q3)
+    split_a(X, 1);
+    H3_MMA(Y, Q3, NQ)
+  }
+#undef H3_MMA
+  __builtin_amdgcn_s_waitcnt(d6_waitcnt_vm0());
+  __syncthreads();
+
+  float bv[8];
+  {
+    const int n = n0 + (tid % (BNH / 8)) * 8;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bv[e] = (g.bias && n + e < g.N) ? g.bias[n + e] : 0.f;
+  }
+  float* ct = reinterpret_cast<float*>(smem);
+  // 32x32 accumulator: lane holds rows 8 (r >> 2) + 4 (lane >> 5) + (r & 3), column lane & 31;
+  // the column's scale 2^-e_n / s_a (exact) before the bias / residual / activation epilogue
+#pragma unroll
+  for (int j = 0; j < FJ; ++j) {
+    const int n = n0 + 32 * j + l31;
+    const float cs = n < g.N ? g.h3_sinv[n] * inv_sa : 0.f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      ct[(wid * 32 + 8 * (r >> 2) + 4 * hi + (r & 3)) * EPI_LD + 32 * j + l31] = acc[j][r] * cs;
+  }
+  __syncthreads();
+  const float am = store_tile<float, H3_BM, H3_NT, BNH>(g, ct, m0, n0, tid, bv);
+  if (g.amax_c) amax_publish(am, g.amax_c, g.amax_c_mul);
+}
+
+__global__ __launch_bounds__(H3_NT, 2) void gemm_h3d_linear(GemmArgs g) { gemm_h3d_body<GEMM_LINEAR, 4>(g); }
+__global__ __launch_bounds__(H3_NT, 2) void gemm_h3d_linear_n64(GemmArgs g) { gemm_h3d_body<GEMM_LINEAR, 2>(g); }
+__global__ __launch_bounds__(H3_NT, 2) void gemm_h3d_conv(GemmArgs g) { gemm_h3d_body<GEMM_CONV, 4>(g); }
+__global__ __launch_bounds__(H3_NT, 2) void gemm_h3d_conv_n64(GemmArgs g) { gemm_h3d_body<GEMM_CONV, 2>(g); }
+__global__ __launch_bounds__(H3_NT, 2) void gemm_h3d_conv_pl(GemmArgs g) { gemm_h3d_body<GEMM_CONV, 4, true>(g); }
+__global__ __launch_bounds__(H3_NT, 2) void gemm_h3d_conv_pl_n64(GemmArgs g) { gemm_h3d_body<GEMM_CONV, 2, true>(g); }
+
+// 1 = not a problem for the h3 kernel (the caller runs the x6 path)
+int launch_h3d(const GemmArgs& g, int mode, hipStream_t s) {
+  if (!g.H3 || !g.h3_sinv || (mode != GEMM_LINEAR && mode != GEMM_CONV) || (g.lda & 3)) return 1;
+  const bool pl = mode == GEMM_CONV && (g.Cin & 31);
+  if (pl ? ((g.Cin & 3) || (g.K & 3) || g.K != g.Cin * g.KH * g.KW) : (g.K & 31)) return 1;
+  if ((reinterpret_cast<uintptr_t>(g.A) & 15) || (reinterpret_cast<uintptr_t>(g.H3) & 15) || (g.ldb & 7)) return 1;
+  constexpr long long LIM = (1LL << 31) - (1LL << 24);
+  if ((long long)2 * g.h3_rows * g.ldb * 2 >= LIM || g.h3_rows < g.N) return 1;
+  if (mode == GEMM_CONV) {
+    if ((long long)(g.M / (g.Ho * g.Wo)) * g.H * g.W * g.Cin * 4 >= LIM) return 1;
+  } else if ((long long)(g.M + H3_BM) * g.lda * 4 + (long long)g.K * 4 >= LIM) {
+    return 1;
+  }
+  const bool narrow = g.N <= 64;
+  const int bn = narrow ? 64 : 128;
+  const int tiles = ((g.M + H3_BM - 1) / H3_BM) * ((g.N + bn - 1) / bn);
+  if (tiles <= 0) return 0;
+  const dim3 grid(tiles), block(H3_NT);
+  if (mode == GEMM_CONV && pl) {
+    if (narrow) hipLaunchKernelGGL(gemm_h3d_conv_pl_n64, grid, block, 0, s, g);
+    else hipLaunchKernelGGL(gemm_h3d_conv_pl, grid, block, 0, s, g);
+  } else if (mode == GEMM_CONV) {
+    if (narrow) hipLaunchKernelGGL(gemm_h3d_conv_n64, grid, block, 0, s, g);
+    else hipLaunchKernelGGL(gemm_h3d_conv, grid, block, 0, s, g);
+  } else {
+    if (narrow) hipLaunchKernelGGL(gemm_h3d_linear_n64, grid, block, 0, s, g);
+    else hipLaunchKernelGGL(gemm_h3d_linear, grid, block, 0, s, g);
+  }
+  return (int)hipGetLastError();
+}
+
 template <typename T, bool X3 = false>
 int launch_t(const GemmArgs& g, int mode, hipStream_t s) {
   const int tiles = ((g.M + BM - 1) / BM) * ((g.N + BN - 1) / BN);
@@ -980,6 +1279,12 @@ int spe_launch_gemm(const GemmArgs& g, int dtype, int mode, hipStream_t s) {
   }
   spe_gemm_last_path = 0;
   if (dtype == SPE_DTYPE_F32X3) return launch_t<float, true>(g, mode, s);
+  if (dtype == SPE_DTYPE_F32H3) {
+    spe_gemm_last_path = 7;
+    const int rc = launch_h3d(g, mode, s);
+    if (rc != 1) return rc;
+    dtype = SPE_DTYPE_F32X6;                     // shapes the h3 kernel does not serve: the x6 path
+  }
   if (dtype == SPE_DTYPE_F32X6) {
     // few-row problems (the decoder's B*Q rows) would leave most CUs idle on 256 x 128 tiles:
     // they take the 128 x 128 geometry (at 2.7x the exact-f32 kernel's matrix rate per tile)

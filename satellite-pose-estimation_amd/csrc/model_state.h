@@ -28,6 +28,9 @@ struct Block {
 struct Enc {
   Conv qk, v, o, l1, l2;
   float *n1g, *n1b, *n2g, *n2b;
+  // fp32h3: device bounds on |norm1 / norm2 output| (max|gamma| sqrt(D - 1) + max|beta|: |x - mean|
+  // / std <= sqrt(D - 1)), the scale input of the GEMMs that read them
+  float *n1_bound = nullptr, *n2_bound = nullptr;
   void* pos_qk = nullptr;   // bf16 / fp32x6 models: pos . W_qk^T [tokens][512] (row-periodic residual)
 };
 
@@ -42,12 +45,17 @@ struct Dec {
   void* xq_r = nullptr;     // [Q][8*256] bf16: query_pos . Wqk^T + bqk (scaled)
 };
 
+// fp32h3 activation-scale slots in the workspace: [0, SPE_AMAX_BB) written by the backbone stage,
+// [SPE_AMAX_BB, SPE_AMAX_SLOTS) by the transformer stage (each stage zeroes its own range first)
+constexpr int SPE_AMAX_BB = 96, SPE_AMAX_SLOTS = 128;
+
 struct Ws {                // workspace layout (byte offsets)
   size_t x0, stem, pool, bufA, bufB, t1, t2, ds, xs8, up, cat, neck;
   size_t src, srcpos, qkv, vt, ao, tmp, ffn, ck, cvt;
   size_t kpl;                // fp32x3 / fp32x6: the encoder K as bf16 hi / lo planes (0 = none)
   size_t tgt, dtmp, dqkv, dvt, dao, dqc, dffn, dffnpart, hs;
   size_t xq, xu, xpm, xpl, xpu;           // cross-attention against the memory (xattn.hip)
+  size_t amax;               // fp32h3: max |activation| slots (SPE_AMAX_SLOTS floats; backbone, then transformer)
   size_t total;
 };
 
@@ -111,9 +119,14 @@ struct spe_model {
   int family = 0;            // 0: DETR (REV), 1: RT-DETR (UNC)
   int x3 = 0;                // fp32 model computed with split-bf16 MFMA (SPE_DTYPE_F32X3_, _F32X6_)
   int x6 = 0;                // ... with the GEMMs / convs on the three-way split path (SPE_DTYPE_F32X6_)
+  int h3 = 0;                // ... and the backbone / encoder GEMMs on the scaled fp16 split path (SPE_DTYPE_F32H3_)
   // fp32x6 models: fp32 weight block -> (its bf16 planes [3][rows][Kpad] h, m, l, rows), written
   // at finalize next to each packed weight (upload_rows) so the x6 GEMM never splits weights
   std::map<const void*, std::pair<const void*, int>> w6;
+  // fp32h3 models: fp32 weight block -> its fp16 planes [2][rows][Kpad] (hi, lo of the row scaled by
+  // 2^e_r) and the per-row 2^-e_r (upload_rows)
+  struct H3W { const void* planes; int rows; const float* sinv; };
+  std::map<const void*, H3W> wh3;
   RtModel* rt = nullptr;
   spe_model_config cfg{};
   int esz = 2;

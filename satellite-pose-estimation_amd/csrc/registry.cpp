@@ -116,6 +116,8 @@ void* upload_rows(spe_model* m, const std::vector<float>& rows, int N, int K, in
   const size_t n = (size_t)N * Kpad;
   void* dst = dalloc(m, n * m->esz);
   void* pl = (m->x6 && m->esz == 4) ? dalloc(m, 3 * n * 2) : nullptr;   // sized in both passes
+  void* ph = (m->h3 && m->esz == 4) ? dalloc(m, 2 * n * 2) : nullptr;
+  float* sinv = (m->h3 && m->esz == 4) ? (float*)dalloc(m, (size_t)N * 4) : nullptr;
   if (!m->dmem) return nullptr;
   if (m->esz == 2) {
     std::vector<uint16_t> h(n, 0);
@@ -138,6 +140,30 @@ void* upload_rows(spe_model* m, const std::vector<float>& rows, int N, int K, in
       }
       m->upload_err |= (int)hipMemcpy(pl, b.data(), b.size() * 2, hipMemcpyHostToDevice);
       m->w6[dst] = {pl, N};
+    }
+    if (ph) {
+      // fp32h3: row r scaled by 2^e_r (max |w_r| 2^e_r in [2^12, 2^13)), split into fp16 hi = RNE(x),
+      // lo = RNE(x - hi) (x - hi exact in fp32); 2^-e_r undoes the scale in the GEMM epilogue
+      std::vector<_Float16> b(2 * n, (_Float16)0.f);
+      std::vector<float> si(N, 1.f);
+      for (int r = 0; r < N; ++r) {
+        float am = 0.f;
+        for (int k = 0; k < K; ++k) am = std::max(am, std::fabs(h[(size_t)r * Kpad + k]));
+        int ex = 0;
+        if (am > 0.f && std::isfinite(am)) std::frexp(am, &ex);
+        const float sc = am > 0.f ? std::ldexp(1.f, 13 - ex) : 1.f;
+        si[r] = am > 0.f ? std::ldexp(1.f, ex - 13) : 1.f;
+        for (int k = 0; k < K; ++k) {
+          const size_t i = (size_t)r * Kpad + k;
+          const float x = h[i] * sc;
+          const _Float16 hi = (_Float16)x;
+          b[i] = hi;
+          b[n + i] = (_Float16)(x - (float)hi);
+        }
+      }
+      m->upload_err |= (int)hipMemcpy(ph, b.data(), b.size() * 2, hipMemcpyHostToDevice);
+      m->upload_err |= (int)hipMemcpy(sinv, si.data(), si.size() * 4, hipMemcpyHostToDevice);
+      m->wh3[dst] = {ph, N, sinv};
     }
   }
   return dst;
@@ -478,6 +504,20 @@ int build_device(spe_model* m) {
     e.l2 = make_linear(m, p + ".linear2.weight", p + ".linear2.bias", 0, d, ff);
     e.n1g = upload_key(m, p + ".norm1.weight"); e.n1b = upload_key(m, p + ".norm1.bias");
     e.n2g = upload_key(m, p + ".norm2.weight"); e.n2b = upload_key(m, p + ".norm2.bias");
+    if (m->h3) {
+      // |LayerNorm(x)_i| <= max|gamma| sqrt(D - 1) + max|beta| (|x_i - mean| / std <= sqrt(D - 1))
+      auto bound = [&](const std::string& n) {
+        float g = 0.f, b = 0.f;
+        if (m->dmem) {
+          for (float v : m->host[n + ".weight"]) g = std::max(g, std::fabs(v));
+          for (float v : m->host[n + ".bias"]) b = std::max(b, std::fabs(v));
+        }
+        const float v = g * std::sqrt((float)(d - 1)) + b;
+        return upload_f32(m, &v, 1);
+      };
+      e.n1_bound = bound(p + ".norm1");
+      e.n2_bound = bound(p + ".norm2");
+    }
     m->enc.push_back(e);
   }
   m->dec.clear();
@@ -600,6 +640,7 @@ Ws spe_plan(const spe_model* m, int B) {
   w.dffn = take((size_t)B * Q * ff * E);
   w.dffnpart = take((size_t)std::max(1, spe_ffn_splits((int)(B * Q), (int)ff)) * B * Q * d * 4);   // split-F partials
   w.hs = take((size_t)B * Q * d * 4);
+  w.amax = take(m->h3 ? SPE_AMAX_SLOTS * 4 : 0);
   w.total = off;
   return w;
 }
@@ -617,7 +658,7 @@ int spe_model_create(const spe_model_config* cfg, spe_model** out) {
   if (cfg->num_queries < 1 || cfg->num_queries > 64) return fail(SPE_E_ARG, "num_queries must be in [1, 64]");
   if (cfg->dim_feedforward % 64) return fail(SPE_E_ARG, "dim_feedforward must be a multiple of 64");
   if (cfg->dtype != SPE_DTYPE_BF16_ && cfg->dtype != SPE_DTYPE_F32_ && cfg->dtype != SPE_DTYPE_F32X3_ &&
-      cfg->dtype != SPE_DTYPE_F32X6_)
+      cfg->dtype != SPE_DTYPE_F32X6_ && cfg->dtype != SPE_DTYPE_F32H3_)
     return fail(SPE_E_ARG, "bad dtype");
   if (cfg->attn_dtype != 0 && cfg->attn_dtype != cfg->dtype &&
       !(cfg->attn_dtype == SPE_DTYPE_F16_ && cfg->dtype == SPE_DTYPE_BF16_))
@@ -626,7 +667,8 @@ int spe_model_create(const spe_model_config* cfg, spe_model** out) {
   m->cfg = *cfg;
   // fp32x3: the fp32 model (storage, layouts, kernels' fp32 paths) with split-bf16 MFMA compute;
   // fp32x6: the same with the GEMMs / convolutions on the three-way split (x6) path
-  m->x6 = cfg->dtype == SPE_DTYPE_F32X6_;
+  m->h3 = cfg->dtype == SPE_DTYPE_F32H3_;
+  m->x6 = cfg->dtype == SPE_DTYPE_F32X6_ || m->h3;
   m->x3 = cfg->dtype == SPE_DTYPE_F32X3_ || m->x6;
   if (m->x3) { m->cfg.dtype = SPE_DTYPE_F32_; if (m->cfg.attn_dtype) m->cfg.attn_dtype = SPE_DTYPE_F32_; }
   m->esz = cfg->dtype == SPE_DTYPE_BF16_ ? 2 : 4;

@@ -7,7 +7,8 @@
 enum { SPE_DTYPE_BF16 = 0, SPE_DTYPE_F32 = 1, SPE_DTYPE_F16 = 2,    // F16: attention operands only
        SPE_DTYPE_BF16_F16V = 3,     // attention only: bf16 q/k, fp16 V^T and P (bf16 models' encoder)
        SPE_DTYPE_F32X3 = 4,         // fp32 storage, split-bf16 (hi.hi + hi.lo + lo.hi) MFMA compute
-       SPE_DTYPE_F32X6 = 5 };       // fp32 storage, three-way split-bf16 (6 products, ~fp32) MFMA compute (GEMMs)
+       SPE_DTYPE_F32X6 = 5,         // fp32 storage, three-way split-bf16 (6 products, ~fp32) MFMA compute (GEMMs)
+       SPE_DTYPE_F32H3 = 6 };       // fp32 storage, scaled two-way split-fp16 (3 products, ~fp32) MFMA compute (GEMMs)
 enum { GEMM_LINEAR = 0, GEMM_LINEAR_ADD = 1, GEMM_CONV = 2 };
 // GEMM epilogue activations: ReLU (ResNet, DETR FFN), SiLU (UNC hybrid encoder ConvNormLayer,
 // hybrid_encoder.py:17-37), exact-erf GELU (UNC AIFI FFN, torch nn.GELU default)
@@ -35,6 +36,13 @@ struct GemmArgs {
   void* S; int s_col0;             // fp32 models: columns n >= s_col0 stored instead as bf16 hi / lo planes for the
                                    // fp32x3 attention: rows -> hi [M][N - s_col0] then lo; head-transposed
                                    // (vt_T) -> hi in C's layout [vt_B][N][vt_T] then lo (s_col0 = 0)
+  // fp32h3 (gemm.hip gemm_h3d): the weights as fp16 planes [2][h3_rows][ldb] (hi, lo of W[n] * 2^e_n)
+  // with h3_sinv[n] = 2^-e_n; amax_a: device max |A| (the A operand's scale 2^13 / amax rounded to
+  // a power of two; null = 1).  amax_c (fp32 GEMMs): max |stored output| * (amax_c_mul or 1) is
+  // atomically maxed into *amax_c (float bits as uint, >= 0) -- the next GEMM's amax_a
+  const void* H3; int h3_rows; const float* h3_sinv;
+  const float* amax_a;
+  float* amax_c; float amax_c_mul;
 };
 bool spe_gemm_ln_fusable(const GemmArgs& g);   // the large-tile kernel can fuse ln_g/ln_b for g
 int spe_launch_gemm(const GemmArgs& g, int dtype, int mode, hipStream_t s);
@@ -163,7 +171,8 @@ int spe_ffn_splits(int M, int F);  // split count spe_launch_ffn_ln would use fo
 
 int spe_launch_preprocess(const uint8_t* frames, int B, int H, int W, int C, const double* bbox, int S,
                           float* images, float* clip_bbox, int32_t* status, hipStream_t s);
-int spe_launch_pack_input(const float* img, void* out, int B, int S, int dtype, hipStream_t s);
+// amax (fp32 output only, nullable): max |image| atomically maxed in (the stem GEMM's fp32h3 scale input)
+int spe_launch_pack_input(const float* img, void* out, int B, int S, int dtype, hipStream_t s, float* amax = nullptr);
 // bf16 [B][S+6][S+6][4], zero border of 3 (the pair-packed stem's input, forward.cpp)
 int spe_launch_pack_input_pad4(const float* img, void* out, int B, int S, hipStream_t s);
 // bf16 pair-packed stem (x: spe_launch_pack_input_pad4 layout, w: [64][ldw] k = (kh*8 + kw)*4 + ci)

@@ -21,6 +21,7 @@ pytestmark = pytest.mark.gpu
 DT = {"bf16": (_lib.SPE_DTYPE_BF16, torch.bfloat16, 1e-2), "fp32": (_lib.SPE_DTYPE_F32, torch.float32, 1e-4),
       "fp32x3": (_lib.SPE_DTYPE_F32X3, torch.float32, 1e-4),
       "fp32x6": (_lib.SPE_DTYPE_F32X6, torch.float32, 1e-4),
+      "fp32h3": (_lib.SPE_DTYPE_F32H3, torch.float32, 1e-4),
       "fp16": (_lib.SPE_DTYPE_F16, torch.float16, 2e-3)}
 
 
@@ -879,16 +880,47 @@ def _gemm_planes(mode, A, Wp, M, N, K, lda, C, ldc, bias=None, R=None, ldr=0, re
     return L.spe_debug_gemm_path()
 
 
-def _split_gemm_err(gpu_device, case, dtype, planes=False, want_path=None):
+def _h3_planes(Wp):
+    """fp32 [N][ldb] -> (fp16 [2][N][ldb] hi, lo of W[n] * 2^e_n, fp32 2^-e_n [N]) with max |W[n]| 2^e_n
+    in [2^12, 2^13) (what spe_model_finalize writes for fp32h3 models)."""
+    am = Wp.abs().amax(1).double()
+    e = torch.where(am > 0, torch.frexp(am).exponent.double(), torch.zeros_like(am))
+    sc = torch.where(am > 0, torch.pow(2.0, 13 - e), torch.ones_like(am)).float()[:, None]
+    x = Wp * sc
+    h = x.to(torch.float16)
+    lo = (x - h.float()).to(torch.float16)
+    return torch.stack([h, lo]).contiguous(), (1.0 / sc[:, 0]).contiguous()
+
+
+def _gemm_h3(mode, A, Wp, M, N, K, lda, C, ldc, bias=None, R=None, ldr=0, relu=0, conv=(0, 0, 0, 1, 1, 1, 0)):
+    """one fp32h3 launch (gemm path 7) with A's max |x| on the device; checks the published max |C|."""
+    L = _lib.lib()
+    H, Wd, Cin, KH, KW, stride, pad = conv
+    planes, sinv = _h3_planes(Wp)
+    amax_a = A.abs().max().reshape(1).contiguous()
+    amax_c = torch.zeros(1, device=A.device)
+    rc = L.spe_debug_gemm_h3(None, mode, _p(A), lda, H, Wd, Cin, KH, KW, stride, pad, Wp.shape[1], M, N, K, _p(bias),
+                             _p(R), ldr, relu, _p(C), ldc, _p(planes), Wp.shape[0], _p(sinv), _p(amax_a),
+                             _p(amax_c), 0.0)
+    assert rc == 0, L.spe_last_error()
+    torch.cuda.synchronize()
+    assert L.spe_debug_gemm_path() == 7
+    stored = C[:, :N] if C.dim() == 2 else C
+    assert amax_c.item() == stored.abs().max().item(), (amax_c.item(), stored.abs().max().item())
+    return 7
+
+
+def _split_gemm_err(gpu_device, case, dtype, planes=False, want_path=None, amp=1.0):
     """max |C - C_fp64| / max |C_fp64| of one launch of `dtype` on `case` (planes: fp32x6 with the
-    weights pre-split, as the models launch it; want_path: the kernel that must have run)."""
+    weights pre-split, as the models launch it; dtype fp32h3: the scaled fp16 split with its
+    finalize-form planes; want_path: the kernel that must have run; amp scales A)."""
     g = torch.Generator(device="cpu").manual_seed(len(case))
     dev, f = gpu_device, torch.float32
     if case.startswith("conv"):
         B, H, Cin, Cout, k, st, pd = {"conv3x3": (2, 26, 256, 256, 3, 1, 1), "conv3x3_n64": (2, 26, 64, 64, 3, 1, 1),
                                       "conv1x1s2": (2, 52, 512, 256, 1, 2, 0),
                                       "conv7x7s2_c8": (2, 40, 8, 64, 7, 2, 3)}[case]
-        x = torch.randn(B, Cin, H, H, generator=g, dtype=torch.float64)
+        x = torch.randn(B, Cin, H, H, generator=g, dtype=torch.float64) * amp
         w = torch.randn(Cout, Cin, k, k, generator=g, dtype=torch.float64) / (Cin * k * k) ** 0.5
         ref = F.conv2d(x, w, stride=st, padding=pd).permute(0, 2, 3, 1).reshape(-1, Cout)
         A = x.permute(0, 2, 3, 1).contiguous().to(dev, f)
@@ -898,7 +930,9 @@ def _split_gemm_err(gpu_device, case, dtype, planes=False, want_path=None):
         if K % 64:                                     # weight rows padded to 64 elements
             Wp = torch.nn.functional.pad(Wp, (0, 64 - K % 64))
         C = torch.zeros(M, Cout, dtype=f, device=dev)
-        if planes:
+        if dtype == "fp32h3":
+            _gemm_h3(2, A, Wp, M, Cout, K, 0, C, Cout, conv=(H, H, Cin, k, k, st, pd))
+        elif planes:
             path = _gemm_planes(2, A, Wp, M, Cout, K, 0, C, Cout, conv=(H, H, Cin, k, k, st, pd))
             assert want_path is None or path == want_path, path
         else:
@@ -907,7 +941,7 @@ def _split_gemm_err(gpu_device, case, dtype, planes=False, want_path=None):
     else:
         M, N, K = {"vt": (2 * 2704, 256, 256), "linear_n64": (3000, 64, 256), "linear_n40": (3000, 40, 256)}.get(
             case, (3000, 200, 512))
-        A = torch.randn(M, K, generator=g, dtype=torch.float64)
+        A = torch.randn(M, K, generator=g, dtype=torch.float64) * amp
         Wt = torch.randn(N, K, generator=g, dtype=torch.float64) / K ** 0.5
         bias = torch.randn(N, generator=g, dtype=torch.float64)
         ref = A @ Wt.t() + bias
@@ -924,6 +958,9 @@ def _split_gemm_err(gpu_device, case, dtype, planes=False, want_path=None):
             _gemm(dtype, 0, A.to(dev, f), _padded_weight(Wt.to(dev, f), K, f), M, N, K, K, K, C, 4,
                   bias=bias.to(dev, f), vt=(T, Bv))
             got = C.view(N // 256, Bv, 256, T).permute(1, 3, 0, 2).reshape(M, N)
+        elif dtype == "fp32h3":
+            _gemm_h3(0, A.to(dev, f), _padded_weight(Wt.to(dev, f), K, f), M, N, K, K, C, ldc, bias=bias.to(dev, f), **kw)
+            got = C[:, :N]
         elif planes:
             path = _gemm_planes(0, A.to(dev, f), _padded_weight(Wt.to(dev, f), K, f), M, N, K, K, C, ldc,
                                 bias=bias.to(dev, f), **kw)
@@ -961,6 +998,21 @@ def test_gemm_x6_dma_close_to_fp64(gpu_device, case):
     kernel."""
     err = _split_gemm_err(gpu_device, case, "fp32x6", planes=True, want_path=6)
     e32 = _split_gemm_err(gpu_device, case, "fp32")
+    assert err <= max(1e-6, 2 * e32), (err, e32)
+
+
+@pytest.mark.parametrize("case,amp", [("linear", 1.0), ("linear_add_relu_res", 1.0), ("conv3x3", 1.0), ("conv1x1s2", 1.0),
+                                      ("linear_n64", 1.0), ("linear_n40", 1.0), ("conv3x3_n64", 1.0),
+                                      ("conv7x7s2_c8", 1.0), ("linear", 1e-7), ("linear", 1e6), ("conv3x3", 3e-5)])
+def test_gemm_h3_close_to_fp64(gpu_device, case, amp):
+    """fp32h3 (the scaled two-way fp16 split, three fp16 MFMAs; gemm path 7) at the exact-f32 MFMA
+    kernel's own error on the same problem -- ragged M and N tiles, residual + ReLU epilogue, padded
+    3x3 / strided 1x1 implicit GEMMs, the 128 x 64 tile, the stem's 8-channel 7x7 with per-lane tap
+    decode -- also for activations far below fp16's normal range (amp 1e-7, 3e-5) and far above its
+    maximum (1e6): the power-of-two scale from max |A| keeps them at fp32 accuracy.  The published
+    max |C| equals the stored output's exactly."""
+    err = _split_gemm_err(gpu_device, case, "fp32h3", amp=amp)
+    e32 = _split_gemm_err(gpu_device, case, "fp32", amp=amp)
     assert err <= max(1e-6, 2 * e32), (err, e32)
 
 

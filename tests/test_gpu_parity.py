@@ -57,10 +57,11 @@ def _check_sigmas(o, g, log_tol, rel_tol):
     assert (np.abs(sg - g["pp_sigmas"]) / g["pp_sigmas"]).max() <= rel_tol
 
 
-@pytest.mark.parametrize("dtype", ["fp32", "fp32x3", "fp32x6"])
+@pytest.mark.parametrize("dtype", ["fp32", "fp32x3", "fp32x6", "fp32h3"])
 @pytest.mark.parametrize("tag", GOLDEN_TAGS)
 def test_forward_fp32_matches_reference(gpu_device, tag, dtype):
-    """The parity modes: exact-f32 MFMA, and fp32 storage with split-bf16 MFMA (fp32x3)."""
+    """The parity modes: exact-f32 MFMA, fp32 storage with split-bf16 MFMA (fp32x3), the three-way
+    bf16 split (fp32x6) and the scaled two-way fp16 split (fp32h3)."""
     g, cfg = _golden(tag)
     b = synthetic_batch(cfg, int(g["batch"]), int(g["image_seed"]))
     m = _model(cfg, dtype, int(g["weight_seed"]))
