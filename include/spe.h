@@ -292,11 +292,13 @@ int spe_debug_gemm_path(void);
 /* fp32h3 (gemm.hip gemm_h3d): C = act((A . W^T) + bias + R) on fp32 A (LINEAR or CONV geometry as
  * spe_debug_gemm) with the weights given as the finalize form -- planes = fp16 [2][plane_rows][ldb]
  * holding hi, lo of W[n] * 2^e_n, sinv[n] = 2^-e_n -- and amax_a = device max |A| (nullable: scale
- * 1).  amax_c (nullable): max |stored C| * (amax_c_mul or 1) atomically maxed into it (float bits). */
+ * 1).  amax_c (nullable): max |stored C| * (amax_c_mul or 1) atomically maxed into it (float bits).
+ * ln_g / ln_b (nullable; LINEAR, N == 256): C = LayerNorm(A . W^T + bias + R) (eps 1e-5) from the
+ * 256-wide tile's epilogue -- the encoder's out-projection + norm1 and linear2 + norm2 in fp32h3. */
 int spe_debug_gemm_h3(void* stream, int mode, const void* A, int lda, int H, int W, int Cin, int KH, int KW, int stride,
                       int pad, int ldb, int M, int N, int K, const float* bias, const void* R, int ldr, int act_code,
                       void* C, int ldc, const void* planes, int plane_rows, const float* sinv, const float* amax_a,
-                      float* amax_c, float amax_c_mul);
+                      float* amax_c, float amax_c_mul, const float* ln_g, const float* ln_b);
 /* the same launch with the weights also given pre-split (dtype SPE_DTYPE_F32X6_): planes = bf16
  * [3][plane_rows][ldb] holding hi, mid, lo of Bw (what spe_model_finalize writes for fp32x6 models) */
 int spe_debug_gemm_planes(void* stream, int dtype, int mode, const void* A, int lda, const void* P, int ldp, int prow,

@@ -381,7 +381,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   }  // SPE_STAGE_BACKBONE
   if (stages & SPE_STAGE_TRANSFORMER) {
   float* const tam = amx ? amx + SPE_AMAX_BB : nullptr;
-  if (tam) CK((int)hipMemsetAsync(tam, 0, (SPE_AMAX_SLOTS - SPE_AMAX_BB) * 4, s));
+  if (tam) CK((int)hipMemsetAsync(tam, 0, (SPE_AMAX_DEC - SPE_AMAX_BB) * 4, s));
   const float* src_amax = src_amax0;
   int li = 0;
 
@@ -439,7 +439,9 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       g.amax_a = tam ? tam + 2 * li : nullptr;
       GemmArgs gf = g;
       gf.C = P(w.src); gf.ln_g = e.n1g; gf.ln_b = e.n1b;
-      if (m->esz == 2 && spe_ln_fusable(gf)) {
+      // fp32h3: the 256-wide h3 tile applies norm1 in its epilogue (gemm.hip gemm_h3d_linear_ln)
+      const bool h3ln = m->h3 && g.amax_a && d == 256;
+      if ((m->esz == 2 && spe_ln_fusable(gf)) || h3ln) {
         CK(run_gemm(m, "gemm.enc.o", gf, GEMM_LINEAR, s));
       } else {
         CK(run_gemm(m, "gemm.enc.o", g, GEMM_LINEAR, s));
@@ -463,14 +465,20 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
         GemmArgs g = linear_args(e.l2, P(w.ffn), ff, Mt, P(w.tmp), d);
         g.R = P(w.src); g.ldr = d;
         g.amax_a = tam ? tam + 2 * li + 1 : nullptr;
-        CK(run_gemm(m, "gemm.enc.ffn2", g, GEMM_LINEAR, s));
+        if (m->h3 && g.amax_a && d == 256) {
+          // fp32h3: linear2 + residual + norm2 in one launch, in place over src
+          g.C = P(w.src); g.ln_g = e.n2g; g.ln_b = e.n2b;
+          CK(run_gemm(m, "gemm.enc.ffn2", g, GEMM_LINEAR, s));
+        } else {
+          CK(run_gemm(m, "gemm.enc.ffn2", g, GEMM_LINEAR, s));
+          CK(run_other(m, "ln.enc", 0.0, (double)Mt * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.tmp), e.n2g, e.n2b, P(w.src), nullptr, Mt, d, dt, s); }));
+        }
       }
-      CK(run_other(m, "ln.enc", 0.0, (double)Mt * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.tmp), e.n2g, e.n2b, P(w.src), nullptr, Mt, d, dt, s); }));
     }
     src_amax = e.n2_bound;
     ++li;
   }
-  if (tam && 2 * li > SPE_AMAX_SLOTS - SPE_AMAX_BB) return fail(SPE_E_STATE, "fp32h3: encoder activation-scale slots exhausted");
+  if (tam && 2 * li > SPE_AMAX_DEC - SPE_AMAX_BB - 1) return fail(SPE_E_STATE, "fp32h3: encoder activation-scale slots exhausted");
   // memory = src.  Unless the layers attend to memory + pos / memory directly (xattn path),
   // project the cross-attention K (memory + pos) and V^T (memory) for all decoder layers.
   if (!xa) {
@@ -486,7 +494,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   {
     GemmArgs g = linear_args(m->crossV, P(w.src), d, Mt, P(w.cvt), 8);
     g.vt_T = T; g.vt_B = B;
-    g.amax_a = src_amax;
+    g.amax_a = src_amax; g.amax_c = amx ? amx + SPE_AMAX_DEC - 1 : nullptr;   // bounds every cross-attention output
     CK(run_gemm(m, "gemm.cross_kv", g, GEMM_LINEAR, s));
   }
   }
@@ -500,11 +508,19 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   // batch i+1's backbone with two workspaces)
   const int Mq = B * Q;
   CK((int)hipMemsetAsync(P(w.tgt), 0, (size_t)Mq * d * m->esz, s));
+  // fp32h3 decoder scales: tgt's from its LayerNorm bounds (zeros before the first layer: any scale
+  // serves), the attention outputs' from their V (self: the sv GEMM's published maximum; cross: the
+  // crossV GEMM's, transformer stage), the FFN hidden's from the linear1 GEMM
+  float* const dam = amx ? amx + SPE_AMAX_DEC : nullptr;
+  if (dam) CK((int)hipMemsetAsync(dam, 0, (SPE_AMAX_SLOTS - SPE_AMAX_DEC) * 4, s));
+  if (dam && 2 * L > SPE_AMAX_SLOTS - SPE_AMAX_DEC) return fail(SPE_E_STATE, "fp32h3: decoder activation-scale slots exhausted");
+  const float* tgt_amax = m->h3 && L > 0 ? m->dec[0].n1_bound : nullptr;
+  const float* const cross_v_amax = amx ? amx + SPE_AMAX_DEC - 1 : nullptr;
   // tgt = LayerNorm(tgt + dao . W^T + b) (REV/models/transformer.py:227-228, 233-234) as GEMM +
   // LayerNorm: at these few rows (B.Q) lnproj's one-workgroup-per-8-tiles form measured slower
   // (24 vs 18 us a layer: 6 workgroups each staging all of W)
   static const bool decproj_on = [] { const char* e = getenv("SPE_DECPROJ"); return e ? atoi(e) != 0 : true; }();
-  auto dec_proj_ln = [&](const Conv& wo, const float* lg, const float* lb) -> int {
+  auto dec_proj_ln = [&](const Conv& wo, const float* lg, const float* lb, const float* x_amax) -> int {
     if (decproj_on && m->esz == 2 && d == 256 && Q <= 64) {
       // bf16: one workgroup per image, the rows in LDS from the GEMM to the LayerNorm (decsa.hip)
       DecProjArgs pa{};
@@ -516,6 +532,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
     }
     GemmArgs g = linear_args(wo, P(w.dao), d, Mq, P(w.dtmp), d);
     g.R = P(w.tgt); g.ldr = d;
+    g.amax_a = x_amax;
     CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR, s));
     CK(run_other(m, "ln.dec", 0.0, (double)Mq * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.dtmp), lg, lb, P(w.tgt), nullptr, Mq, d, dt, s); }));
     return 0;
@@ -541,11 +558,13 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
     {
       GemmArgs g = linear_args(e.sqk, P(w.tgt), d, Mq, P(w.dqkv), 3 * d);
       const int mode = add_pos(m, g, m->qpos, d, Q, e.qpos_sqk, 2 * d);
+      g.amax_a = tgt_amax;
       CK(run_gemm(m, "gemm.dec", g, mode, s));
     }
     {
       GemmArgs g = linear_args(e.sv, P(w.tgt), d, Mq, P(w.dvt), 8);
       g.vt_T = Q; g.vt_B = B;
+      g.amax_a = tgt_amax; g.amax_c = dam ? dam + 2 * l : nullptr;
       CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR, s));
     }
     {
@@ -557,8 +576,9 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       a.B = B; a.H = c.nheads; a.Tq = Q; a.Tk = Q; a.scale = scale;
       CK(run_attn(m, "attn.dec_self", a, dt, s));
     }
-    CK(dec_proj_ln(e.so, e.n1g, e.n1b));
+    CK(dec_proj_ln(e.so, e.n1g, e.n1b, dam ? dam + 2 * l : nullptr));
     }
+    if (m->h3) tgt_amax = e.n1_bound;
     if (xa) {
       // q' = (tgt + query_pos) . Wqk^T + bqk: the query-side fold of Wq and Wk (xattn.hip)
       GemmArgs g = linear_args(e.xq, P(w.tgt), d, Mq, P(w.xq), 8 * d);
@@ -579,6 +599,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
     {
       GemmArgs g = linear_args(e.cq, P(w.tgt), d, Mq, P(w.dqc), d);
       const int mode = add_pos(m, g, m->qpos, d, Q, e.qpos_cq, d);
+      g.amax_a = tgt_amax;
       CK(run_gemm(m, "gemm.dec", g, mode, s));
     }
     {
@@ -591,7 +612,8 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       CK(run_attn(m, "attn.dec_cross", a, dt, s));
     }
     }
-    CK(dec_proj_ln(e.co, e.n2g, e.n2b));
+    CK(dec_proj_ln(e.co, e.n2g, e.n2b, cross_v_amax));
+    if (m->h3) tgt_amax = e.n2_bound;
     if (use_fused_ffn(m)) {
       CK(run_ffn(m, "ffn.dec", e.l1, e.l2, e.n3g, e.n3b, P(w.tgt), Mq, s, nullptr, nullptr, 0,
                  (float*)P(w.dffnpart)));
@@ -599,15 +621,18 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       {
         GemmArgs g = linear_args(e.l1, P(w.tgt), d, Mq, P(w.dffn), ff);
         g.act = ACT_RELU;
+        g.amax_a = tgt_amax; g.amax_c = dam ? dam + 2 * l + 1 : nullptr;
         CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR, s));
       }
       {
         GemmArgs g = linear_args(e.l2, P(w.dffn), ff, Mq, P(w.dtmp), d);
         g.R = P(w.tgt); g.ldr = d;
+        g.amax_a = dam ? dam + 2 * l + 1 : nullptr;
         CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR, s));
       }
       CK(run_other(m, "ln.dec", 0.0, (double)Mq * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.dtmp), e.n3g, e.n3b, P(w.tgt), nullptr, Mq, d, dt, s); }));
     }
+    if (m->h3) tgt_amax = e.n3_bound;
     if (out->aux_logits && out->aux_points && l + 1 < L) {
       // aux output of layer l: the shared decoder_norm (REV/models/transformer.py:117-124) and
       // the same heads (REV/models/detr_speed.py:83-99), into the aux slices

@@ -37,6 +37,7 @@ struct Enc {
 struct Dec {
   Conv sqk, sv, so, cq, co, l1, l2;
   float *n1g, *n1b, *n2g, *n2b, *n3g, *n3b;
+  float *n1_bound = nullptr, *n2_bound = nullptr, *n3_bound = nullptr;   // fp32h3 (see Enc)
   void* qpos_sqk = nullptr; // bf16 / fp32x6 models: query_pos . W_sqk^T [Q][512]
   void* qpos_cq = nullptr;  // bf16 models: query_pos . W_cq^T [Q][256]
   // cross-attention against the memory (spe_use_xattn, xattn.hip): q' = tgt . Wqk^T + xq_r
@@ -47,7 +48,8 @@ struct Dec {
 
 // fp32h3 activation-scale slots in the workspace: [0, SPE_AMAX_BB) written by the backbone stage,
 // [SPE_AMAX_BB, SPE_AMAX_SLOTS) by the transformer stage (each stage zeroes its own range first)
-constexpr int SPE_AMAX_BB = 96, SPE_AMAX_SLOTS = 128;
+// (the transformer stage's range is [SPE_AMAX_BB, SPE_AMAX_DEC), the decoder stage's [SPE_AMAX_DEC, SPE_AMAX_SLOTS))
+constexpr int SPE_AMAX_BB = 96, SPE_AMAX_DEC = 112, SPE_AMAX_SLOTS = 128;
 
 struct Ws {                // workspace layout (byte offsets)
   size_t x0, stem, pool, bufA, bufB, t1, t2, ds, xs8, up, cat, neck;

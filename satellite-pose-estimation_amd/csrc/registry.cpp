@@ -175,6 +175,18 @@ float* upload_f32(spe_model* m, const float* p, size_t n) {
   return dst;
 }
 
+// fp32h3: a device bound on |LayerNorm `key` output| of width D: max|gamma| sqrt(D - 1) + max|beta|
+// (|x_i - mean| / std <= sqrt(D - 1) for any row) -- the scale input of the GEMMs reading it
+float* ln_bound(spe_model* m, const std::string& key, int D) {
+  float g = 0.f, b = 0.f;
+  if (m->dmem) {
+    for (float v : m->host[key + ".weight"]) g = std::max(g, std::fabs(v));
+    for (float v : m->host[key + ".bias"]) b = std::max(b, std::fabs(v));
+  }
+  const float v = g * std::sqrt((float)(D - 1)) + b;
+  return upload_f32(m, &v, 1);
+}
+
 void* upload_T(spe_model* m, const std::vector<float>& v) {
   void* dst = dalloc(m, v.size() * m->esz);
   if (!m->dmem) return nullptr;
@@ -505,18 +517,8 @@ int build_device(spe_model* m) {
     e.n1g = upload_key(m, p + ".norm1.weight"); e.n1b = upload_key(m, p + ".norm1.bias");
     e.n2g = upload_key(m, p + ".norm2.weight"); e.n2b = upload_key(m, p + ".norm2.bias");
     if (m->h3) {
-      // |LayerNorm(x)_i| <= max|gamma| sqrt(D - 1) + max|beta| (|x_i - mean| / std <= sqrt(D - 1))
-      auto bound = [&](const std::string& n) {
-        float g = 0.f, b = 0.f;
-        if (m->dmem) {
-          for (float v : m->host[n + ".weight"]) g = std::max(g, std::fabs(v));
-          for (float v : m->host[n + ".bias"]) b = std::max(b, std::fabs(v));
-        }
-        const float v = g * std::sqrt((float)(d - 1)) + b;
-        return upload_f32(m, &v, 1);
-      };
-      e.n1_bound = bound(p + ".norm1");
-      e.n2_bound = bound(p + ".norm2");
+      e.n1_bound = ln_bound(m, p + ".norm1", d);
+      e.n2_bound = ln_bound(m, p + ".norm2", d);
     }
     m->enc.push_back(e);
   }
@@ -535,6 +537,11 @@ int build_device(spe_model* m) {
     e.n1g = upload_key(m, p + ".norm1.weight"); e.n1b = upload_key(m, p + ".norm1.bias");
     e.n2g = upload_key(m, p + ".norm2.weight"); e.n2b = upload_key(m, p + ".norm2.bias");
     e.n3g = upload_key(m, p + ".norm3.weight"); e.n3b = upload_key(m, p + ".norm3.bias");
+    if (m->h3) {
+      e.n1_bound = ln_bound(m, p + ".norm1", d);
+      e.n2_bound = ln_bound(m, p + ".norm2", d);
+      e.n3_bound = ln_bound(m, p + ".norm3", d);
+    }
     if (spe_use_xattn(m)) fold_cross_attention(m, p, e);
     m->dec.push_back(e);
     const auto& w = m->host[p + ".multihead_attn.in_proj_weight"];
