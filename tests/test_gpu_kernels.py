@@ -1037,9 +1037,9 @@ def test_gemm_h3_layernorm_epilogue(gpu_device, M, K):
     Ad = A.to(dev, f)
     amax_a = Ad.abs().max().reshape(1).contiguous()
     C = R.to(dev, f).contiguous()                               # in place: C = R
-    rc = L.spe_debug_gemm_h3(None, 0, _p(Ad), K, 0, 0, 0, 1, 1, 1, 0, Wp.shape[1], M, N, K, _p(b.to(dev, f)), _p(C), N, 0,
-                             _p(C), N, _p(planes), N, _p(sinv), _p(amax_a), None, 0.0, _p(gam.to(dev, f)),
-                             _p(bet.to(dev, f)))
+    bd, gd, btd = b.to(dev, f), gam.to(dev, f), bet.to(dev, f)  # (kept alive across the launch)
+    rc = L.spe_debug_gemm_h3(None, 0, _p(Ad), K, 0, 0, 0, 1, 1, 1, 0, Wp.shape[1], M, N, K, _p(bd), _p(C), N, 0,
+                             _p(C), N, _p(planes), N, _p(sinv), _p(amax_a), None, 0.0, _p(gd), _p(btd))
     assert rc == 0, L.spe_last_error()
     torch.cuda.synchronize()
     assert L.spe_debug_gemm_path() == 7
