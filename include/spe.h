@@ -287,7 +287,7 @@ int spe_debug_gemm(void* stream, int dtype, int mode, const void* A, int lda, co
  * kernels (gemm2.hip), 2 the persistent streaming kernel for short-K problems (gemm_stream.hip),
  * 3 the patch-staged 3x3 conv (pconv.hip), 4 the projection + residual + LayerNorm (lnproj.hip),
  * 5 the fp32x6 three-way split kernel (gemm.hip), 6 its LDS-DMA form (gemm.hip gemm_x6d), 7 the fp32h3
- * scaled fp16 split kernel (gemm.hip gemm_h3d) */
+ * scaled fp16 split kernel (gemm.hip gemm_h3d), 8 its persistent row-store form (gemm.hip gemm_h3p) */
 int spe_debug_gemm_path(void);
 /* fp32h3 (gemm.hip gemm_h3d): C = act((A . W^T) + bias + R) on fp32 A (LINEAR or CONV geometry as
  * spe_debug_gemm) with the weights given as the finalize form -- planes = fp16 [2][plane_rows][ldb]

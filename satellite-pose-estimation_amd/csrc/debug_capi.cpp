@@ -65,7 +65,7 @@ int spe_debug_gemm_h3(void* stream, int mode, const void* A, int lda, int H, int
   g.amax_c_mul = amax_c_mul;
   g.ln_g = ln_g; g.ln_b = ln_b;
   const int rc = spe_launch_gemm(g, SPE_DTYPE_F32H3, mode, (hipStream_t)stream);
-  if (rc == 0 && spe_gemm_last_path != 7) return spe_fail(SPE_E_LAUNCH, "shape not served by the fp32h3 kernel");
+  if (rc == 0 && spe_gemm_last_path != 7 && spe_gemm_last_path != 8) return spe_fail(SPE_E_LAUNCH, "shape not served by the fp32h3 kernel");
   return rc < 0 ? spe_fail(SPE_E_LAUNCH, "gemm launch rejected its arguments") : rc;
 }
 

@@ -30,7 +30,7 @@ __global__ void pack_input_kernel(const float* __restrict__ img, T* __restrict__
   if (amax) {                                    // every lane reaches here (grid-stride loop)
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) am = fmaxf(am, __shfl_xor(am, o, 64));
-    if ((threadIdx.x & 63) == 0 && am > 0.f) atomicMax((unsigned*)amax, __float_as_uint(am));
+    if ((threadIdx.x & 63) == 0 && am > 0.f) amax_update(amax, am);
   }
 }
 

@@ -370,7 +370,7 @@ SPE_DEV float store_tile(const GemmArgs& g, const float* ct, int m0, int n0, int
 SPE_DEV void amax_publish(float am, float* slot, float mul) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) am = fmaxf(am, __shfl_xor(am, o, 64));
-  if ((threadIdx.x & 63) == 0 && am > 0.f) atomicMax((unsigned*)slot, __float_as_uint(am * (mul > 0.f ? mul : 1.f)));
+  if ((threadIdx.x & 63) == 0 && am > 0.f) amax_update(slot, am * (mul > 0.f ? mul : 1.f));
 }
 
 template <typename T, int MODE, bool X3 = false>
@@ -1246,6 +1246,298 @@ __global__ __launch_bounds__(H3_NT, 2) void gemm_h3d_conv_pl(GemmArgs g) { gemm_
 __global__ __launch_bounds__(H3_NT, 2) void gemm_h3d_conv_pl_n64(GemmArgs g) { gemm_h3d_body<GEMM_CONV, 2, true>(g); }
 __global__ __launch_bounds__(H3_NT, 1) void gemm_h3d_linear_ln(GemmArgs g) { gemm_h3d_body<GEMM_LINEAR, 8, false, true>(g); }
 
+// Persistent form of gemm_h3d for row-store epilogues (bias, residual / row-periodic residual,
+// activation, fp32 C, max |C|): one workgroup per occupancy slot walks its tiles (round i: tile
+// i * grid + xcd_remap(block), so an XCD's workgroups share A panels), and the K-steps of
+// consecutive tiles form ONE pipeline -- the DMA of the next tile's first steps is issued while the
+// current tile's last steps multiply, so no workgroup starts cold.  The accumulators are the
+// transposed product (weights as the MFMA's first operand: a lane holds one output row and columns
+// 8q + 4(lane >> 5) + 0..3), stored straight from registers with 16-byte buffer stores -- no LDS
+// round trip, no barrier -- and left in flight: vmcnt counts loads and stores in issue order, so
+// the step after a tile's epilogue waits vmcnt(S) (its DMA is older than the S stores) and only the
+// step after that drains them.  To keep that count exact every lane issues all S stores (rows past
+// M go to an out-of-range offset, which the buffer unit drops), the per-column bias and scale come
+// by LDS-DMA with the tile's first step (two regions, by tile parity), a residual tile is loaded
+// into registers before the DMA of the step that ends the tile, and max |C| is published once per
+// workgroup.  Needs nk >= 2 (the bias region of tile i + 2 is written after tile i's epilogue).
+// (The non-persistent kernel with its stores removed ran the encoder's linear1 in 0.63 instead of
+// 1.14 ms: the store phase, not the MFMAs, was half of that launch.)
+constexpr int H3P_EPI = 2 * 128 * 4;                 // bias[BN] + sinv[BN] floats (BN <= 128) per region
+template <int MODE, int FJ, bool PL, bool RES>
+__device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
+  using G = H3Geo<FJ>;
+  constexpr int BNH = G::BN, PB = G::PB, STG = G::STAGE, NBQ = G::NBQ, NQ = G::NQ;
+  constexpr int S_ST = FJ * 4;                         // 16-byte stores per lane per tile
+  __shared__ __attribute__((aligned(1024))) char smem[2 * STG + 2 * H3P_EPI];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tilesN = (g.N + BNH - 1) / BNH, ntiles = ((g.M + H3_BM - 1) / H3_BM) * tilesN;
+  const int GR = gridDim.x, w0 = xcd_remap(blockIdx.x, GR);
+  const int nk = (g.K + 31) >> 5;
+  const int total = w0 < ntiles ? ((ntiles - 1 - w0) / GR + 1) * nk : 0;
+  const long long abytes = MODE == GEMM_CONV ? (long long)(g.M / (g.Ho * g.Wo)) * g.H * g.W * g.Cin * 4
+                                             : (long long)g.M * g.lda * 4;
+  const size_t pstride = (size_t)g.h3_rows * g.ldb;
+  const __amdgpu_buffer_rsrc_t rsa = __builtin_amdgcn_make_buffer_rsrc((void*)g.A, (short)0, (int)abytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsb =
+      __builtin_amdgcn_make_buffer_rsrc((void*)g.H3, (short)0, (int)(2 * pstride * 2), 0x00020000);
+  const __amdgpu_buffer_rsrc_t rse = __builtin_amdgcn_make_buffer_rsrc((void*)g.h3_sinv, (short)0, g.N * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsbias =
+      __builtin_amdgcn_make_buffer_rsrc((void*)(g.bias ? g.bias : g.h3_sinv), (short)0, g.N * 4, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsc =
+      __builtin_amdgcn_make_buffer_rsrc(g.C, (short)0, (int)((long long)g.M * g.ldc * 4), 0x00020000);
+  float sa, inv_sa;
+  h3_scale(g.amax_a, sa, inv_sa);
+  if (total == 0) return;
+
+  // ---- issue side: the tile / K-step of the next DMA and that tile's per-lane source offsets
+  int it = w0, iks = 0, iord = 0;
+  int avo[4], ih0[4], iw0[4], bvo[NBQ], evo = 0;
+  auto setup = [&](int t) {
+    const int m0 = (t / tilesN) * H3_BM, n0 = (t % tilesN) * BNH;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int row = (wid + 4 * q) * 8 + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7), m = m0 + row;
+      if constexpr (MODE == GEMM_CONV) {
+        const int hw = g.Ho * g.Wo, mm = m < g.M ? m : 0;
+        const int b = mm / hw, r = mm - b * hw, oh = r / g.Wo, ow = r - oh * g.Wo;
+        ih0[q] = m < g.M ? oh * g.stride - g.pad : -(1 << 28);
+        iw0[q] = ow * g.stride - g.pad;
+        avo[q] = b * g.H * g.W * g.Cin + (PL ? 0 : c * 4);
+      } else {
+        avo[q] = m < g.M ? m * g.lda * 4 + c * 16 : D6_BAD;
+        ih0[q] = iw0[q] = 0;
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < NBQ; ++q) {
+      const int p = wid + 4 * q, plane = p / (BNH / 16), row = (p % (BNH / 16)) * 16 + (lane >> 2);
+      const int c = (lane & 3) ^ ((row >> 2) & 3), n = n0 + row;
+      bvo[q] = n < g.N ? (int)((plane * pstride + (size_t)n * g.ldb) * 2) + c * 16 : D6_BAD;
+    }
+    const int en = n0 + (lane & 63) + (wid & 1) * 64;     // waves 0/1: sinv, waves 2/3: bias
+    evo = en < g.N && en < n0 + BNH ? en * 4 : D6_BAD;
+  };
+  const int ck = (lane & 7) ^ ((wid * 4 + (lane >> 4)) & 7);
+  auto issue_next = [&](int stg) {
+    char* base = smem + stg * STG;
+    int kh = 0, kw = 0, ci = 0;
+    bool kv = true;
+    if constexpr (MODE == GEMM_CONV) {
+      if constexpr (PL) {
+        const int k = iks * 32 + ck * 4, tap = k / g.Cin;
+        ci = k - tap * g.Cin;
+        kh = tap / g.KW;
+        kw = tap - kh * g.KW;
+        kv = k < g.K;
+      } else {
+        conv_k_decode(iks * 32, g.Cin, g.KW, g.KH * g.KW, kh, kw, ci);
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      int off;
+      if constexpr (MODE == GEMM_CONV) {
+        const int ih = ih0[q] + kh, iw = iw0[q] + kw;
+        const bool v = kv && ih >= 0 && ih < g.H && iw >= 0 && iw < g.W;
+        off = v ? (avo[q] + (ih * g.W + iw) * g.Cin + ci) * 4 : D6_BAD;
+      } else {
+        off = avo[q];
+      }
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lds_ptr6_t)(base + (wid + 4 * q) * 1024), 16, off,
+                                               MODE == GEMM_CONV ? 0 : iks * 128, 0, 0);
+    }
+#pragma unroll
+    for (int q = 0; q < NBQ; ++q)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lds_ptr6_t)(base + H3_A + (wid + 4 * q) * 1024), 16, bvo[q],
+                                               iks * 64, 0, 0);
+    if (iks == 0) {                                  // the tile's sinv / bias columns, 4 bytes a lane
+      char* eb = smem + 2 * STG + (iord & 1) * H3P_EPI + (wid >> 1) * (128 * 4) + (wid & 1) * 256;
+      if (wid < 2) __builtin_amdgcn_raw_ptr_buffer_load_lds(rse, (lds_ptr6_t)eb, 4, evo, 0, 0, 0);
+      else __builtin_amdgcn_raw_ptr_buffer_load_lds(rsbias, (lds_ptr6_t)eb, 4, g.bias ? evo : D6_BAD, 0, 0, 0);
+    }
+    if (++iks == nk) {                               // past the last tile: keep issuing the last tile's
+      iks = 0;                                       // offsets (in range or dropped), never consumed
+      ++iord;
+      it += GR;
+      if (it < ntiles) setup(it);
+    }
+  };
+
+  // ---- fragment offsets (as gemm_h3d_body)
+  const int l31 = lane & 31, hi = lane >> 5;
+  int aoff[2][2], boff[2];
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h)
+      aoff[kk][h] = (wid * 32 + l31) * 128 + (((4 * kk + 2 * hi + h) ^ ((l31 >> 1) & 7)) << 4);
+    boff[kk] = H3_A + l31 * 64 + (((2 * kk + hi) ^ ((l31 >> 2) & 3)) << 4);
+  }
+  auto mf = [](u32x4 x, u32x4 y, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, x), __builtin_bit_cast(f16x8, y), c, 0, 0, 0);
+  };
+  f32x16 acc[FJ];
+#pragma unroll
+  for (int j = 0; j < FJ; ++j)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+  using Frag = H3Frag<FJ>;
+  auto read_b = [&](const char* st, int kk, Frag& f) {
+#pragma unroll
+    for (int j = 0; j < FJ; ++j)
+#pragma unroll
+      for (int p = 0; p < 2; ++p) f.b[p][j] = ld16(st + boff[kk] + p * PB + j * 2048);
+  };
+  auto read_a = [&](const char* st, int kk, Frag& f) {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) f.raw[h] = ld16(st + aoff[kk][h]);
+  };
+  auto split_a = [&](Frag& f, int h) { split2h(f.raw[h], sa, f.ph[h], f.pl[h]); };
+  // transposed product: C^T[n][m] += W[n][k] A[m][k]
+  auto mma1 = [&](const Frag& f, int q) {
+    const int j = q / 3, t = q % 3;
+    const u32x4 xa = t == 0 ? cat2(f.pl[0], f.pl[1]) : cat2(f.ph[0], f.ph[1]);
+    const u32x4 xb = t == 1 ? f.b[1][j] : f.b[0][j];
+    acc[j] = mf(xb, xa, acc[j]);
+  };
+#define H3P_MMA(F, LO, HI)                               \
+  _Pragma("unroll") for (int q = LO; q < HI; ++q) mma1(F, q); \
+  __builtin_amdgcn_sched_barrier(0);
+
+  // ---- epilogue state: the computing tile
+  int cord = 0, cks = 0;
+  float runmax = 0.f;
+  u32x4 rres[RES ? FJ * 4 : 1];
+  auto tile_mn = [&](int ord, int& m0, int& n0) {
+    const int t = w0 + ord * GR;
+    m0 = (t / tilesN) * H3_BM;
+    n0 = (t % tilesN) * BNH;
+  };
+  auto load_res = [&]() {
+    if constexpr (RES) {
+      int m0, n0;
+      tile_mn(cord, m0, n0);
+      const int m = m0 + wid * 32 + l31;
+      const size_t rrow = (size_t)(g.r_period > 0 ? (m < g.M ? m : 0) % g.r_period : (m < g.M ? m : 0)) * g.ldr;
+#pragma unroll
+      for (int j = 0; j < FJ; ++j)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int n = n0 + 32 * j + 8 * q + 4 * hi;
+          rres[4 * j + q] = n < g.N ? ld16((const float*)g.R + rrow + n) : u32x4{0, 0, 0, 0};
+        }
+    }
+  };
+  auto epilogue = [&]() {
+    int m0, n0;
+    tile_mn(cord, m0, n0);
+    const int m = m0 + wid * 32 + l31;
+    const float* eb = reinterpret_cast<const float*>(smem + 2 * STG + (cord & 1) * H3P_EPI);
+#pragma unroll
+    for (int j = 0; j < FJ; ++j)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int c = 32 * j + 8 * q + 4 * hi, n = n0 + c;
+        const f32x4 sv = *reinterpret_cast<const f32x4*>(eb + c);
+        const f32x4 bv = *reinterpret_cast<const f32x4*>(eb + 128 + c);
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[j][4 * q + e] * (sv[e] * inv_sa) + bv[e];
+        if constexpr (RES) {
+          float rv[4];
+          unpack16<float>(rres[4 * j + q], rv);
+          if (!g.res_post) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += rv[e];
+          }
+          if (g.act) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], g.act);
+          }
+          if (g.res_post) {
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] += rv[e];
+          }
+        } else if (g.act) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] = apply_act(v[e], g.act);
+        }
+        const bool ok = m < g.M && n < g.N;
+        if (ok) runmax = fmaxf(runmax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+        __builtin_amdgcn_raw_buffer_store_b128(pack16<float>(v), rsc, ok ? (m * g.ldc + n) * 4 : D6_BAD, 0, 0);
+      }
+#pragma unroll
+    for (int j = 0; j < FJ; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+  };
+
+  setup(w0);
+  issue_next(0);
+  issue_next(1);
+  __builtin_amdgcn_s_waitcnt(d6_waitcnt_vm(4 + NBQ));
+  __syncthreads();
+  Frag X, Y;
+  read_b(smem, 0, X);
+  read_a(smem, 0, X);
+  split_a(X, 0);
+  split_a(X, 1);
+  constexpr int QA = NQ / 3;
+  constexpr int Q1 = NQ / 6 > 0 ? NQ / 6 : 1, Q2 = Q1 + NQ / 4, Q3 = Q2 + NQ / 4;
+  for (int gs = 0; gs < total; ++gs) {
+    const char* st = smem + (gs & 1) * STG;
+    const char* sn = smem + ((gs + 1) & 1) * STG;
+    const bool prev_epi = gs > 0 && cks == 0;        // the previous step stored a tile
+    const bool last = cks == nk - 1;
+    __builtin_amdgcn_sched_barrier(0);
+    read_b(st, 1, Y);
+    read_a(st, 1, Y);
+    H3P_MMA(X, 0, QA)
+    split_a(Y, 0);
+    H3P_MMA(X, QA, 2 * QA)
+    split_a(Y, 1);
+    H3P_MMA(X, 2 * QA, NQ)
+    // this step's successor's DMA is older than the previous epilogue's S stores, if there was one
+    if (prev_epi) __builtin_amdgcn_s_waitcnt(d6_waitcnt_vm(S_ST) & ~(15 << 8));
+    else __builtin_amdgcn_s_waitcnt(d6_waitcnt_vm0() & ~(15 << 8));
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    if (RES && last) load_res();
+    __builtin_amdgcn_sched_barrier(0);
+    issue_next(gs & 1);
+    H3P_MMA(Y, 0, Q1)
+    read_b(sn, 0, X);
+    read_a(sn, 0, X);
+    H3P_MMA(Y, Q1, Q2)
+    split_a(X, 0);
+    H3P_MMA(Y, Q2, Q3)
+    split_a(X, 1);
+    H3P_MMA(Y, Q3, NQ)
+    if (last) {
+      epilogue();
+      ++cord;
+      cks = 0;
+    } else {
+      ++cks;
+    }
+  }
+#undef H3P_MMA
+  __builtin_amdgcn_s_waitcnt(d6_waitcnt_vm0());
+  if (g.amax_c) amax_publish(runmax, g.amax_c, g.amax_c_mul);
+}
+
+__global__ __launch_bounds__(H3_NT, 2) void gemm_h3p_linear(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 4, false, false>(g); }
+__global__ __launch_bounds__(H3_NT, 2) void gemm_h3p_linear_n64(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 2, false, false>(g); }
+__global__ __launch_bounds__(H3_NT, 2) void gemm_h3p_linear_r(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 4, false, true>(g); }
+__global__ __launch_bounds__(H3_NT, 2) void gemm_h3p_linear_r_n64(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 2, false, true>(g); }
+__global__ __launch_bounds__(H3_NT, 2) void gemm_h3p_conv(GemmArgs g) { gemm_h3p_body<GEMM_CONV, 4, false, false>(g); }
+__global__ __launch_bounds__(H3_NT, 2) void gemm_h3p_conv_n64(GemmArgs g) { gemm_h3p_body<GEMM_CONV, 2, false, false>(g); }
+__global__ __launch_bounds__(H3_NT, 2) void gemm_h3p_conv_r(GemmArgs g) { gemm_h3p_body<GEMM_CONV, 4, false, true>(g); }
+__global__ __launch_bounds__(H3_NT, 2) void gemm_h3p_conv_r_n64(GemmArgs g) { gemm_h3p_body<GEMM_CONV, 2, false, true>(g); }
+__global__ __launch_bounds__(H3_NT, 2) void gemm_h3p_conv_pl(GemmArgs g) { gemm_h3p_body<GEMM_CONV, 4, true, false>(g); }
+__global__ __launch_bounds__(H3_NT, 2) void gemm_h3p_conv_pl_n64(GemmArgs g) { gemm_h3p_body<GEMM_CONV, 2, true, false>(g); }
+
 // 1 = not a problem for the h3 kernel (the caller runs the x6 path)
 int launch_h3d(const GemmArgs& g, int mode, hipStream_t s) {
   if (!g.H3 || !g.h3_sinv || (mode != GEMM_LINEAR && mode != GEMM_CONV) || (g.lda & 3)) return 1;
@@ -1271,6 +1563,33 @@ int launch_h3d(const GemmArgs& g, int mode, hipStream_t s) {
   const int tiles = ((g.M + H3_BM - 1) / H3_BM) * ((g.N + bn - 1) / bn);
   if (tiles <= 0) return 0;
   const dim3 grid(tiles), block(H3_NT);
+  // the persistent form for plain row stores (gemm_h3p_body)
+  const bool res = g.R != nullptr;
+  if (g.vt_T <= 0 && !g.S && g.K >= 64 && !(g.N & 3) && !(g.ldc & 3) && !(reinterpret_cast<uintptr_t>(g.C) & 15) &&
+      (long long)g.M * g.ldc * 4 < LIM && (!res || (!pl && !(g.ldr & 3) && !(reinterpret_cast<uintptr_t>(g.R) & 15)))) {
+    const int ncu = spe_cu_count();
+    const dim3 pg(tiles < 2 * ncu || ncu <= 0 ? tiles : 2 * ncu);
+    if (mode == GEMM_CONV && pl) {
+      if (narrow) hipLaunchKernelGGL(gemm_h3p_conv_pl_n64, pg, block, 0, s, g);
+      else hipLaunchKernelGGL(gemm_h3p_conv_pl, pg, block, 0, s, g);
+    } else if (mode == GEMM_CONV) {
+      if (res) {
+        if (narrow) hipLaunchKernelGGL(gemm_h3p_conv_r_n64, pg, block, 0, s, g);
+        else hipLaunchKernelGGL(gemm_h3p_conv_r, pg, block, 0, s, g);
+      } else {
+        if (narrow) hipLaunchKernelGGL(gemm_h3p_conv_n64, pg, block, 0, s, g);
+        else hipLaunchKernelGGL(gemm_h3p_conv, pg, block, 0, s, g);
+      }
+    } else if (res) {
+      if (narrow) hipLaunchKernelGGL(gemm_h3p_linear_r_n64, pg, block, 0, s, g);
+      else hipLaunchKernelGGL(gemm_h3p_linear_r, pg, block, 0, s, g);
+    } else {
+      if (narrow) hipLaunchKernelGGL(gemm_h3p_linear_n64, pg, block, 0, s, g);
+      else hipLaunchKernelGGL(gemm_h3p_linear, pg, block, 0, s, g);
+    }
+    spe_gemm_last_path = 8;
+    return (int)hipGetLastError();
+  }
   if (mode == GEMM_CONV && pl) {
     if (narrow) hipLaunchKernelGGL(gemm_h3d_conv_pl_n64, grid, block, 0, s, g);
     else hipLaunchKernelGGL(gemm_h3d_conv_pl, grid, block, 0, s, g);

@@ -105,6 +105,17 @@ SPE_DEV float wave_max(float v) {
   return v;
 }
 
+// Published max |x| of a tensor (the fp32h3 activation scales): a float >= 0 kept as its bit
+// pattern, raised with an unsigned atomic max.  Every producing wave publishes, so the atomics of
+// a launch all hit one L2 line: 10^5 of them serialise there for ~1 ms.  The slot is read first
+// (a relaxed agent-scope load; a stale value is never larger than the current one, so a skipped
+// update is always covered) and the atomic goes out only when this wave's value is larger --
+// a few times per launch instead of once per wave.
+SPE_DEV void amax_update(float* slot, float v) {
+  const unsigned cur = __hip_atomic_load((unsigned*)slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (__float_as_uint(v) > cur) atomicMax((unsigned*)slot, __float_as_uint(v));
+}
+
 // Bijective XCD-aware remap of a 1-D grid: blocks that land on one XCD (b % 8 equal under
 // round-robin dispatch) get a contiguous range of tile ids, so neighbouring tiles that share
 // operand panels hit the same L2.  Speed only, never correctness.

@@ -16,7 +16,8 @@ sys.path.insert(0, os.path.join(REPO, "satellite-pose-estimation_amd"))
 from spe import _lib  # noqa: E402
 
 DT = {"fp32": _lib.SPE_DTYPE_F32, "fp32x3": _lib.SPE_DTYPE_F32X3, "fp32x6": _lib.SPE_DTYPE_F32X6,
-      "fp32x6bp": _lib.SPE_DTYPE_F32X6}       # bp: weights pre-split into bf16 planes, as the model has them
+      "fp32x6bp": _lib.SPE_DTYPE_F32X6,       # bp: weights pre-split into bf16 planes, as the model has them
+      "fp32h3": _lib.SPE_DTYPE_F32H3}         # scaled fp16 planes + per-channel scales, as the model has them
 # name: (M, N, K) linear, or (B, H, Cin, Cout, k, stride, pad) conv
 SHAPES = {
     "enc.ffn1": (64 * 2704, 2048, 256), "enc.ffn2": (64 * 2704, 256, 2048), "enc.qk": (64 * 2704, 512, 256),
@@ -30,6 +31,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default="")
+    ap.add_argument("--dtypes", default=",".join(DT))
     a = ap.parse_args()
     L = _lib.lib()
     dev = torch.device("cuda", 0)
@@ -57,9 +59,20 @@ def main():
         r = W - h.float()
         m_ = r.to(torch.bfloat16)
         planes = torch.stack([h, m_, (r - m_.float()).to(torch.bfloat16)]).contiguous()
+        am = W.abs().amax(1).double()
+        sc = torch.pow(2.0, 13 - torch.frexp(am).exponent.double()).float()[:, None]
+        hh = (W * sc).to(torch.float16)
+        h3p = torch.stack([hh, (W * sc - hh.float()).to(torch.float16)]).contiguous()
+        h3s = (1.0 / sc[:, 0]).contiguous()
+        amax_a = A.abs().max().reshape(1).contiguous()
         row = [name]
         for dn, dt in DT.items():
-            if dn == "fp32x6bp":
+            if dn not in a.dtypes.split(","):
+                continue
+            if dn == "fp32h3":
+                fn = lambda: L.spe_debug_gemm_h3(None, mode, p(A), K if mode == 0 else 0, *conv, ldb, M, N, K, p(bias),
+                                                 None, 0, 1, p(C), N, p(h3p), N, p(h3s), p(amax_a), None, 0.0, None, None)
+            elif dn == "fp32x6bp":
                 fn = lambda: L.spe_debug_gemm_planes(None, dt, mode, p(A), K if mode == 0 else 0, None, 0, 1, *conv, p(W),
                                                      ldb, M, N, K, p(bias), None, 0, 1, p(C), N, p(planes), N)
             else:
