@@ -36,17 +36,17 @@ PARITY_MODE_TEXT = {"fp32x6": "fp32 storage; GEMMs / convolutions at near-fp32 p
                               "products), attention as fp32x3 (DESIGN.md section 4)",
                     "fp32x3": "fp32 storage, split-bf16 MFMA (hi.hi + hi.lo + lo.hi)",
                     "fp32": "fp32 storage, exact-f32 MFMA",
-                    "fp32h3": "fp32 storage; backbone / encoder GEMMs and convolutions at near-fp32 precision as three "
-                              "fp16 MFMAs on a power-of-two-scaled two-way fp16 split, decoder GEMMs as fp32x6, "
-                              "attention as fp32x3 (DESIGN.md section 4)"}
+                    "fp32h3": "fp32 storage; GEMMs and convolutions at near-fp32 precision as three fp16 MFMAs on a "
+                              "power-of-two-scaled two-way fp16 split, encoder attention as fp32x3, decoder attention "
+                              "exact fp32 (DESIGN.md section 4)"}
 
 
 def peak_for(dtype, kind):
     """MFMA ceiling (TFLOP/s of model flops) of launch class `kind` in mode `dtype`."""
-    if dtype == "fp32x6" and kind.startswith("attn."):
+    if dtype in ("fp32x6", "fp32h3") and kind.startswith("attn.dec"):   # the decoder's attention: exact f32
+        return PEAK["fp32"]["mfma"]
+    if dtype in ("fp32x6", "fp32h3") and kind.startswith("attn."):     # the encoder's: fp32x3
         return PEAK["fp32x3"]["mfma"]
-    if dtype == "fp32h3" and kind.startswith("gemm.dec"):    # the decoder's few-row GEMMs stay on x6
-        return PEAK["fp32x6"]["mfma"]
     return PEAK[dtype]["mfma"]
 # profiler symbol of each launch class (to match profiles/*kernel_stats.csv rows)
 # (rocprofv3 prints the attention kernels mangled: it does not demangle the __bf16 / _Float16

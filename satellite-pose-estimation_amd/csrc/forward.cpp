@@ -73,8 +73,8 @@ int run_gemm(spe_model* m, const char* kind, const GemmArgs& g, int mode, hipStr
   if (dt == SPE_DTYPE_F32X6) {
     const auto it = m->w6.find(g.B);
     if (it != m->w6.end()) { ga.B6 = it->second.first; ga.b6_rows = it->second.second; }
-    // fp32h3: the GEMMs whose A operand has a published max |A| (the backbone and encoder) take the
-    // scaled fp16 split (gemm.hip gemm_h3d); the decoder's few-row GEMMs stay on x6
+    // fp32h3: the GEMMs whose A operand has a known max |A| (published by its producer, or a LayerNorm
+    // / attention bound) take the scaled fp16 split (gemm.hip gemm_h3d / gemm_h3p); the rest stay on x6
     const auto ih = m->wh3.find(g.B);
     if (m->h3 && g.amax_a && ih != m->wh3.end()) {
       ga.H3 = ih->second.planes; ga.h3_rows = ih->second.rows; ga.h3_sinv = ih->second.sinv;
@@ -439,9 +439,9 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       g.amax_a = tam ? tam + 2 * li : nullptr;
       GemmArgs gf = g;
       gf.C = P(w.src); gf.ln_g = e.n1g; gf.ln_b = e.n1b;
-      // fp32h3: the 256-wide h3 tile applies norm1 in its epilogue (gemm.hip gemm_h3d_linear_ln)
-      const bool h3ln = m->h3 && g.amax_a && d == 256;
-      if ((m->esz == 2 && spe_ln_fusable(gf)) || h3ln) {
+      // (fp32h3 runs the persistent GEMM + the LayerNorm kernel: 0.15 + 0.06 ms a layer against 0.31 ms
+      // for gemm_h3d_linear_ln's fused 256-wide tile, which ends every tile cold)
+      if (m->esz == 2 && spe_ln_fusable(gf)) {
         CK(run_gemm(m, "gemm.enc.o", gf, GEMM_LINEAR, s));
       } else {
         CK(run_gemm(m, "gemm.enc.o", g, GEMM_LINEAR, s));
@@ -465,14 +465,9 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
         GemmArgs g = linear_args(e.l2, P(w.ffn), ff, Mt, P(w.tmp), d);
         g.R = P(w.src); g.ldr = d;
         g.amax_a = tam ? tam + 2 * li + 1 : nullptr;
-        if (m->h3 && g.amax_a && d == 256) {
-          // fp32h3: linear2 + residual + norm2 in one launch, in place over src
-          g.C = P(w.src); g.ln_g = e.n2g; g.ln_b = e.n2b;
-          CK(run_gemm(m, "gemm.enc.ffn2", g, GEMM_LINEAR, s));
-        } else {
-          CK(run_gemm(m, "gemm.enc.ffn2", g, GEMM_LINEAR, s));
-          CK(run_other(m, "ln.enc", 0.0, (double)Mt * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.tmp), e.n2g, e.n2b, P(w.src), nullptr, Mt, d, dt, s); }));
-        }
+        // (fp32h3 likewise: the persistent GEMM + LayerNorm, 0.65 + 0.06 against 0.85 ms fused)
+        CK(run_gemm(m, "gemm.enc.ffn2", g, GEMM_LINEAR, s));
+        CK(run_other(m, "ln.enc", 0.0, (double)Mt * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.tmp), e.n2g, e.n2b, P(w.src), nullptr, Mt, d, dt, s); }));
       }
     }
     src_amax = e.n2_bound;

@@ -1263,15 +1263,29 @@ __global__ __launch_bounds__(H3_NT, 1) void gemm_h3d_linear_ln(GemmArgs g) { gem
 // (The non-persistent kernel with its stores removed ran the encoder's linear1 in 0.63 instead of
 // 1.14 ms: the store phase, not the MFMAs, was half of that launch.)
 constexpr int H3P_EPI = 2 * 128 * 4;                 // bias[BN] + sinv[BN] floats (BN <= 128) per region
-template <int MODE, int FJ, bool PL, bool RES>
+// WM: waves stacked in M (4: 128-row tiles, two workgroups per CU; 8: 256-row tiles, one 8-wave
+// workgroup per CU); NS: LDS stages (the DMA runs NS - 1 K-steps ahead).  With NS = 3 a tile's
+// stores are waited for only 2.5 steps after they were issued (the DMA issued after them), and a
+// 256-row tile halves the number of tile boundaries per row: the short-K problems (K = 256: eight
+// K-steps a tile) had spent a third of their time in the store drain after each tile.
+template <int FJ, int WM, int NS> struct H3PGeo {
+  static constexpr int BM = 32 * WM, BN = 32 * FJ, NT = 64 * WM;
+  static constexpr int AB = BM * 128, PB = BN * 64, STG = AB + 2 * PB;
+  static constexpr int NBQ = BN / (8 * WM);           // B DMA pieces per wave per step
+  static constexpr int NQ = 3 * FJ;
+  static constexpr int D = 4 + NBQ;                   // DMA instructions per wave per step (bias pieces aside)
+  static constexpr int SMEM = NS * STG + 2 * H3P_EPI;
+};
+template <int MODE, int FJ, bool PL, bool RES, int WM = 4, int NS = 2>
 __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
-  using G = H3Geo<FJ>;
-  constexpr int BNH = G::BN, PB = G::PB, STG = G::STAGE, NBQ = G::NBQ, NQ = G::NQ;
+  using G = H3PGeo<FJ, WM, NS>;
+  constexpr int BM = G::BM, BNH = G::BN, PB = G::PB, STG = G::STG, NBQ = G::NBQ, NQ = G::NQ, D = G::D;
+  static_assert(NBQ >= 1 && (NS == 2 || NS == 3), "geometry");
   constexpr int S_ST = FJ * 4;                         // 16-byte stores per lane per tile
-  __shared__ __attribute__((aligned(1024))) char smem[2 * STG + 2 * H3P_EPI];
+  __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int tilesN = (g.N + BNH - 1) / BNH, ntiles = ((g.M + H3_BM - 1) / H3_BM) * tilesN;
+  const int tilesN = (g.N + BNH - 1) / BNH, ntiles = ((g.M + BM - 1) / BM) * tilesN;
   const int GR = gridDim.x, w0 = xcd_remap(blockIdx.x, GR);
   const int nk = (g.K + 31) >> 5;
   const int total = w0 < ntiles ? ((ntiles - 1 - w0) / GR + 1) * nk : 0;
@@ -1294,10 +1308,10 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
   int it = w0, iks = 0, iord = 0;
   int avo[4], ih0[4], iw0[4], bvo[NBQ], evo = 0;
   auto setup = [&](int t) {
-    const int m0 = (t / tilesN) * H3_BM, n0 = (t % tilesN) * BNH;
+    const int m0 = (t / tilesN) * BM, n0 = (t % tilesN) * BNH;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-      const int row = (wid + 4 * q) * 8 + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7), m = m0 + row;
+      const int row = (wid + WM * q) * 8 + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7), m = m0 + row;
       if constexpr (MODE == GEMM_CONV) {
         const int hw = g.Ho * g.Wo, mm = m < g.M ? m : 0;
         const int b = mm / hw, r = mm - b * hw, oh = r / g.Wo, ow = r - oh * g.Wo;
@@ -1311,11 +1325,11 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
     }
 #pragma unroll
     for (int q = 0; q < NBQ; ++q) {
-      const int p = wid + 4 * q, plane = p / (BNH / 16), row = (p % (BNH / 16)) * 16 + (lane >> 2);
+      const int p = wid + WM * q, plane = p / (BNH / 16), row = (p % (BNH / 16)) * 16 + (lane >> 2);
       const int c = (lane & 3) ^ ((row >> 2) & 3), n = n0 + row;
       bvo[q] = n < g.N ? (int)((plane * pstride + (size_t)n * g.ldb) * 2) + c * 16 : D6_BAD;
     }
-    const int en = n0 + (lane & 63) + (wid & 1) * 64;     // waves 0/1: sinv, waves 2/3: bias
+    const int en = n0 + lane + (wid & 1) * 64;         // waves 0/1: sinv, waves 2/3: bias
     evo = en < g.N && en < n0 + BNH ? en * 4 : D6_BAD;
   };
   const int ck = (lane & 7) ^ ((wid * 4 + (lane >> 4)) & 7);
@@ -1344,15 +1358,15 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
       } else {
         off = avo[q];
       }
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lds_ptr6_t)(base + (wid + 4 * q) * 1024), 16, off,
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lds_ptr6_t)(base + (wid + WM * q) * 1024), 16, off,
                                                MODE == GEMM_CONV ? 0 : iks * 128, 0, 0);
     }
 #pragma unroll
     for (int q = 0; q < NBQ; ++q)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lds_ptr6_t)(base + H3_A + (wid + 4 * q) * 1024), 16, bvo[q],
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lds_ptr6_t)(base + G::AB + (wid + WM * q) * 1024), 16, bvo[q],
                                                iks * 64, 0, 0);
-    if (iks == 0) {                                  // the tile's sinv / bias columns, 4 bytes a lane
-      char* eb = smem + 2 * STG + (iord & 1) * H3P_EPI + (wid >> 1) * (128 * 4) + (wid & 1) * 256;
+    if (iks == 0 && wid < 4) {                       // the tile's sinv / bias columns, 4 bytes a lane
+      char* eb = smem + NS * STG + (iord & 1) * H3P_EPI + (wid >> 1) * (128 * 4) + (wid & 1) * 256;
       if (wid < 2) __builtin_amdgcn_raw_ptr_buffer_load_lds(rse, (lds_ptr6_t)eb, 4, evo, 0, 0, 0);
       else __builtin_amdgcn_raw_ptr_buffer_load_lds(rsbias, (lds_ptr6_t)eb, 4, g.bias ? evo : D6_BAD, 0, 0, 0);
     }
@@ -1372,7 +1386,7 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
 #pragma unroll
     for (int h = 0; h < 2; ++h)
       aoff[kk][h] = (wid * 32 + l31) * 128 + (((4 * kk + 2 * hi + h) ^ ((l31 >> 1) & 7)) << 4);
-    boff[kk] = H3_A + l31 * 64 + (((2 * kk + hi) ^ ((l31 >> 2) & 3)) << 4);
+    boff[kk] = G::AB + l31 * 64 + (((2 * kk + hi) ^ ((l31 >> 2) & 3)) << 4);
   }
   auto mf = [](u32x4 x, u32x4 y, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, x), __builtin_bit_cast(f16x8, y), c, 0, 0, 0);
@@ -1411,7 +1425,7 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
   u32x4 rres[RES ? FJ * 4 : 1];
   auto tile_mn = [&](int ord, int& m0, int& n0) {
     const int t = w0 + ord * GR;
-    m0 = (t / tilesN) * H3_BM;
+    m0 = (t / tilesN) * BM;
     n0 = (t % tilesN) * BNH;
   };
   auto load_res = [&]() {
@@ -1433,7 +1447,7 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
     int m0, n0;
     tile_mn(cord, m0, n0);
     const int m = m0 + wid * 32 + l31;
-    const float* eb = reinterpret_cast<const float*>(smem + 2 * STG + (cord & 1) * H3P_EPI);
+    const float* eb = reinterpret_cast<const float*>(smem + NS * STG + (cord & 1) * H3P_EPI);
 #pragma unroll
     for (int j = 0; j < FJ; ++j)
 #pragma unroll
@@ -1476,7 +1490,8 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
   setup(w0);
   issue_next(0);
   issue_next(1);
-  __builtin_amdgcn_s_waitcnt(d6_waitcnt_vm(4 + NBQ));
+  if constexpr (NS == 3) issue_next(2);
+  __builtin_amdgcn_s_waitcnt(d6_waitcnt_vm((NS - 1) * D));   // step 0's DMA (the bias pieces are older)
   __syncthreads();
   Frag X, Y;
   read_b(smem, 0, X);
@@ -1485,10 +1500,12 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
   split_a(X, 1);
   constexpr int QA = NQ / 3;
   constexpr int Q1 = NQ / 6 > 0 ? NQ / 6 : 1, Q2 = Q1 + NQ / 4, Q3 = Q2 + NQ / 4;
+  int sc = 0;                                        // gs % NS
+  int since = 1 << 20;                               // steps since the last epilogue
   for (int gs = 0; gs < total; ++gs) {
-    const char* st = smem + (gs & 1) * STG;
-    const char* sn = smem + ((gs + 1) & 1) * STG;
-    const bool prev_epi = gs > 0 && cks == 0;        // the previous step stored a tile
+    const int sn_i = sc + 1 == NS ? 0 : sc + 1;
+    const char* st = smem + sc * STG;
+    const char* sn = smem + sn_i * STG;
     const bool last = cks == nk - 1;
     __builtin_amdgcn_sched_barrier(0);
     read_b(st, 1, Y);
@@ -1498,14 +1515,15 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
     H3P_MMA(X, QA, 2 * QA)
     split_a(Y, 1);
     H3P_MMA(X, 2 * QA, NQ)
-    // this step's successor's DMA is older than the previous epilogue's S stores, if there was one
-    if (prev_epi) __builtin_amdgcn_s_waitcnt(d6_waitcnt_vm(S_ST) & ~(15 << 8));
-    else __builtin_amdgcn_s_waitcnt(d6_waitcnt_vm0() & ~(15 << 8));
+    // wait for step gs + 1's DMA: the younger operations are the later DMA steps (NS - 2 of them)
+    // and, when a tile ended within the last NS - 1 steps, its S stores
+    if (since < NS - 1) __builtin_amdgcn_s_waitcnt(d6_waitcnt_vm((NS - 2) * D + S_ST) & ~(15 << 8));
+    else __builtin_amdgcn_s_waitcnt(d6_waitcnt_vm((NS - 2) * D) & ~(15 << 8));
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_sched_barrier(0);
     if (RES && last) load_res();
     __builtin_amdgcn_sched_barrier(0);
-    issue_next(gs & 1);
+    issue_next(sc);                                  // step gs + NS into the stage just consumed
     H3P_MMA(Y, 0, Q1)
     read_b(sn, 0, X);
     read_a(sn, 0, X);
@@ -1514,29 +1532,36 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
     H3P_MMA(Y, Q2, Q3)
     split_a(X, 1);
     H3P_MMA(Y, Q3, NQ)
+    ++since;
     if (last) {
       epilogue();
       ++cord;
       cks = 0;
+      since = 0;
     } else {
       ++cks;
     }
+    sc = sn_i;
   }
 #undef H3P_MMA
   __builtin_amdgcn_s_waitcnt(d6_waitcnt_vm0());
   if (g.amax_c) amax_publish(runmax, g.amax_c, g.amax_c_mul);
 }
 
-__global__ __launch_bounds__(H3_NT, 2) void gemm_h3p_linear(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 4, false, false>(g); }
-__global__ __launch_bounds__(H3_NT, 2) void gemm_h3p_linear_n64(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 2, false, false>(g); }
-__global__ __launch_bounds__(H3_NT, 2) void gemm_h3p_linear_r(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 4, false, true>(g); }
-__global__ __launch_bounds__(H3_NT, 2) void gemm_h3p_linear_r_n64(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 2, false, true>(g); }
-__global__ __launch_bounds__(H3_NT, 2) void gemm_h3p_conv(GemmArgs g) { gemm_h3p_body<GEMM_CONV, 4, false, false>(g); }
-__global__ __launch_bounds__(H3_NT, 2) void gemm_h3p_conv_n64(GemmArgs g) { gemm_h3p_body<GEMM_CONV, 2, false, false>(g); }
-__global__ __launch_bounds__(H3_NT, 2) void gemm_h3p_conv_r(GemmArgs g) { gemm_h3p_body<GEMM_CONV, 4, false, true>(g); }
-__global__ __launch_bounds__(H3_NT, 2) void gemm_h3p_conv_r_n64(GemmArgs g) { gemm_h3p_body<GEMM_CONV, 2, false, true>(g); }
-__global__ __launch_bounds__(H3_NT, 2) void gemm_h3p_conv_pl(GemmArgs g) { gemm_h3p_body<GEMM_CONV, 4, true, false>(g); }
-__global__ __launch_bounds__(H3_NT, 2) void gemm_h3p_conv_pl_n64(GemmArgs g) { gemm_h3p_body<GEMM_CONV, 2, true, false>(g); }
+#define H3P_KERNELS(SUF, WM, NS, OCC)                                                                                  \
+  __global__ __launch_bounds__(64 * WM, OCC) void gemm_h3p_linear##SUF(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 4, false, false, WM, NS>(g); } \
+  __global__ __launch_bounds__(64 * WM, OCC) void gemm_h3p_linear_n64##SUF(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 2, false, false, WM, NS>(g); } \
+  __global__ __launch_bounds__(64 * WM, OCC) void gemm_h3p_linear_r##SUF(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 4, false, true, WM, NS>(g); } \
+  __global__ __launch_bounds__(64 * WM, OCC) void gemm_h3p_linear_r_n64##SUF(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 2, false, true, WM, NS>(g); } \
+  __global__ __launch_bounds__(64 * WM, OCC) void gemm_h3p_conv##SUF(GemmArgs g) { gemm_h3p_body<GEMM_CONV, 4, false, false, WM, NS>(g); } \
+  __global__ __launch_bounds__(64 * WM, OCC) void gemm_h3p_conv_n64##SUF(GemmArgs g) { gemm_h3p_body<GEMM_CONV, 2, false, false, WM, NS>(g); } \
+  __global__ __launch_bounds__(64 * WM, OCC) void gemm_h3p_conv_r##SUF(GemmArgs g) { gemm_h3p_body<GEMM_CONV, 4, false, true, WM, NS>(g); } \
+  __global__ __launch_bounds__(64 * WM, OCC) void gemm_h3p_conv_r_n64##SUF(GemmArgs g) { gemm_h3p_body<GEMM_CONV, 2, false, true, WM, NS>(g); } \
+  __global__ __launch_bounds__(64 * WM, OCC) void gemm_h3p_conv_pl##SUF(GemmArgs g) { gemm_h3p_body<GEMM_CONV, 4, true, false, WM, NS>(g); } \
+  __global__ __launch_bounds__(64 * WM, OCC) void gemm_h3p_conv_pl_n64##SUF(GemmArgs g) { gemm_h3p_body<GEMM_CONV, 2, true, false, WM, NS>(g); }
+H3P_KERNELS(, 4, 2, 2)
+H3P_KERNELS(_w8, 8, 3, 1)
+#undef H3P_KERNELS
 
 // 1 = not a problem for the h3 kernel (the caller runs the x6 path)
 int launch_h3d(const GemmArgs& g, int mode, hipStream_t s) {
@@ -1568,25 +1593,34 @@ int launch_h3d(const GemmArgs& g, int mode, hipStream_t s) {
   if (g.vt_T <= 0 && !g.S && g.K >= 64 && !(g.N & 3) && !(g.ldc & 3) && !(reinterpret_cast<uintptr_t>(g.C) & 15) &&
       (long long)g.M * g.ldc * 4 < LIM && (!res || (!pl && !(g.ldr & 3) && !(reinterpret_cast<uintptr_t>(g.R) & 15)))) {
     const int ncu = spe_cu_count();
-    const dim3 pg(tiles < 2 * ncu || ncu <= 0 ? tiles : 2 * ncu);
+    // 256-row tiles, three stages, one 8-wave workgroup per CU when they fill the chip and K gives
+    // at least three steps a tile; else 128-row tiles, two stages, two workgroups per CU
+    const int tiles8 = ((g.M + 255) / 256) * ((g.N + bn - 1) / bn);
+    const bool w8 = tiles8 >= ncu && g.K >= 96;
+    const dim3 pg(w8 ? (tiles8 < ncu ? tiles8 : ncu) : (tiles < 2 * ncu || ncu <= 0 ? tiles : 2 * ncu));
+    const dim3 pb(w8 ? 512 : 256);
+#define H3P_GO(K) hipLaunchKernelGGL(K, pg, pb, 0, s, g)
+#define H3P_SEL(NAME) do { if (w8) H3P_GO(NAME##_w8); else H3P_GO(NAME); } while (0)
     if (mode == GEMM_CONV && pl) {
-      if (narrow) hipLaunchKernelGGL(gemm_h3p_conv_pl_n64, pg, block, 0, s, g);
-      else hipLaunchKernelGGL(gemm_h3p_conv_pl, pg, block, 0, s, g);
+      if (narrow) H3P_SEL(gemm_h3p_conv_pl_n64);
+      else H3P_SEL(gemm_h3p_conv_pl);
     } else if (mode == GEMM_CONV) {
       if (res) {
-        if (narrow) hipLaunchKernelGGL(gemm_h3p_conv_r_n64, pg, block, 0, s, g);
-        else hipLaunchKernelGGL(gemm_h3p_conv_r, pg, block, 0, s, g);
+        if (narrow) H3P_SEL(gemm_h3p_conv_r_n64);
+        else H3P_SEL(gemm_h3p_conv_r);
       } else {
-        if (narrow) hipLaunchKernelGGL(gemm_h3p_conv_n64, pg, block, 0, s, g);
-        else hipLaunchKernelGGL(gemm_h3p_conv, pg, block, 0, s, g);
+        if (narrow) H3P_SEL(gemm_h3p_conv_n64);
+        else H3P_SEL(gemm_h3p_conv);
       }
     } else if (res) {
-      if (narrow) hipLaunchKernelGGL(gemm_h3p_linear_r_n64, pg, block, 0, s, g);
-      else hipLaunchKernelGGL(gemm_h3p_linear_r, pg, block, 0, s, g);
+      if (narrow) H3P_SEL(gemm_h3p_linear_r_n64);
+      else H3P_SEL(gemm_h3p_linear_r);
     } else {
-      if (narrow) hipLaunchKernelGGL(gemm_h3p_linear_n64, pg, block, 0, s, g);
-      else hipLaunchKernelGGL(gemm_h3p_linear, pg, block, 0, s, g);
+      if (narrow) H3P_SEL(gemm_h3p_linear_n64);
+      else H3P_SEL(gemm_h3p_linear);
     }
+#undef H3P_SEL
+#undef H3P_GO
     spe_gemm_last_path = 8;
     return (int)hipGetLastError();
   }

@@ -20,7 +20,7 @@ DT = {"fp32": _lib.SPE_DTYPE_F32, "fp32x3": _lib.SPE_DTYPE_F32X3, "fp32x6": _lib
       "fp32h3": _lib.SPE_DTYPE_F32H3}         # scaled fp16 planes + per-channel scales, as the model has them
 # name: (M, N, K) linear, or (B, H, Cin, Cout, k, stride, pad) conv
 SHAPES = {
-    "enc.ffn1": (64 * 2704, 2048, 256), "enc.ffn2": (64 * 2704, 256, 2048), "enc.qk": (64 * 2704, 512, 256),
+    "enc.ffn1": (64 * 2704, 2048, 256), "cross.k": (64 * 2704, 1536, 256), "enc.ffn2": (64 * 2704, 256, 2048), "enc.qk": (64 * 2704, 512, 256),
     "l1.conv1": (64 * 104 * 104, 64, 256), "l3.conv3": (64 * 26 * 26, 1024, 256),
     "l1.3x3": (64, 104, 64, 64, 3, 1, 1), "l2.3x3": (64, 52, 128, 128, 3, 1, 1), "l3.3x3": (64, 26, 256, 256, 3, 1, 1),
     "neck.3x3": (64, 52, 512, 256, 3, 1, 1),
