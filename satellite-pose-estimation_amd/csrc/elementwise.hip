@@ -28,9 +28,14 @@ __global__ void pack_input_kernel(const float* __restrict__ img, T* __restrict__
     }
   }
   if (amax) {                                    // every lane reaches here (grid-stride loop)
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) am = fmaxf(am, __shfl_xor(am, o, 64));
-    if ((threadIdx.x & 63) == 0 && am > 0.f) amax_update(amax, am);
+    __shared__ float wm[4];                        // one slot update per workgroup (256 threads)
+    am = wave_max(am);
+    if ((threadIdx.x & 63) == 0) wm[threadIdx.x >> 6] = am;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      am = fmaxf(fmaxf(wm[0], wm[1]), fmaxf(wm[2], wm[3]));
+      if (am > 0.f) amax_update(amax, am);
+    }
   }
 }
 
@@ -284,7 +289,8 @@ int spe_launch_pack_input(const float* img, void* out, int B, int S, int dtype, 
   const size_t n = (size_t)B * S * S;
   if (dtype == SPE_DTYPE_BF16)
     hipLaunchKernelGGL(pack_input_kernel<bf16>, grid_for(n, 256), 256, 0, s, img, (bf16*)out, B, S, (float*)nullptr);
-  else hipLaunchKernelGGL(pack_input_kernel<float>, grid_for(n, 256), 256, 0, s, img, (float*)out, B, S, amax);
+  else   // (fp32: at most 4096 workgroups, each publishing its max |x| once)
+    hipLaunchKernelGGL(pack_input_kernel<float>, std::min(grid_for(n, 256), 4096), 256, 0, s, img, (float*)out, B, S, amax);
   return (int)hipGetLastError();
 }
 

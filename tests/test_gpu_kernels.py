@@ -919,7 +919,7 @@ def _split_gemm_err(gpu_device, case, dtype, planes=False, want_path=None, amp=1
     dev, f = gpu_device, torch.float32
     if case.startswith("conv"):
         B, H, Cin, Cout, k, st, pd = {"conv3x3": (2, 26, 256, 256, 3, 1, 1), "conv3x3_n64": (2, 26, 64, 64, 3, 1, 1),
-                                      "conv1x1s2": (2, 52, 512, 256, 1, 2, 0), "conv3x3_w8": (16, 104, 64, 128, 3, 1, 1),
+                                      "conv1x1s2": (2, 52, 512, 256, 1, 2, 0), "conv3x3_big": (16, 104, 64, 128, 3, 1, 1),
                                       "conv7x7s2_c8": (2, 40, 8, 64, 7, 2, 3)}[case]
         x = torch.randn(B, Cin, H, H, generator=g, dtype=torch.float64) * amp
         w = torch.randn(Cout, Cin, k, k, generator=g, dtype=torch.float64) / (Cin * k * k) ** 0.5
@@ -943,14 +943,14 @@ def _split_gemm_err(gpu_device, case, dtype, planes=False, want_path=None, amp=1
     else:
         M, N, K = {"vt": (2 * 2704, 256, 256), "linear_n64": (3000, 64, 256), "linear_n40": (3000, 40, 256),
                    "linear_many_res": (150001, 256, 64), "linear_many_n64": (150001, 64, 128),
-                   "linear_w8_res": (150001, 256, 256)}.get(case, (3000, 200, 512))
+                   "linear_big_res": (150001, 256, 256)}.get(case, (3000, 200, 512))
         A = torch.randn(M, K, generator=g, dtype=torch.float64) * amp
         Wt = torch.randn(N, K, generator=g, dtype=torch.float64) / K ** 0.5
         bias = torch.randn(N, generator=g, dtype=torch.float64)
         ref = A @ Wt.t() + bias
         kw = {}
         ldc = N + 8
-        if case in ("linear_add_relu_res", "linear_many_res", "linear_w8_res"):
+        if case in ("linear_add_relu_res", "linear_many_res", "linear_big_res"):
             R = torch.randn(M, ldc, generator=g, dtype=torch.float64)
             ref = torch.relu(ref + R[:, :N])
             kw = dict(R=R.to(dev, f), ldr=ldc, relu=1)
@@ -1009,18 +1009,17 @@ def test_gemm_x6_dma_close_to_fp64(gpu_device, case):
 @pytest.mark.parametrize("case,amp", [("linear", 1.0), ("linear_add_relu_res", 1.0), ("conv3x3", 1.0), ("conv1x1s2", 1.0),
                                       ("linear_n64", 1.0), ("linear_n40", 1.0), ("conv3x3_n64", 1.0),
                                       ("conv7x7s2_c8", 1.0), ("linear", 1e-7), ("linear", 1e6), ("conv3x3", 3e-5),
-                                      ("linear_many_res", 1.0), ("linear_many_n64", 1.0), ("linear_w8_res", 1.0),
-                                      ("conv3x3_w8", 1.0)])
+                                      ("linear_many_res", 1.0), ("linear_many_n64", 1.0), ("linear_big_res", 1.0),
+                                      ("conv3x3_big", 1.0)])
 def test_gemm_h3_close_to_fp64(gpu_device, case, amp):
     """fp32h3 (the scaled two-way fp16 split, three fp16 MFMAs) at the exact-f32 MFMA kernel's own
     error on the same problem -- ragged M and N tiles, residual + ReLU epilogue, padded 3x3 / strided
     1x1 implicit GEMMs, the 128 x 64 tile, the stem's 8-channel 7x7 with per-lane tap decode -- also
     for activations far below fp16's normal range (amp 1e-7, 3e-5) and far above its maximum (1e6):
     the power-of-two scale from max |A| keeps them at fp32 accuracy.  These row-store problems run
-    the persistent form (gemm path 8); the *_many / *_w8 cases give each workgroup several tiles
-    with a ragged last tile: linear_many_res the 128-row two-stage form at K = 64 (a tile boundary
-    every second step, 2344 tiles on 512 slots), linear_many_n64, linear_w8_res and conv3x3_w8 the
-    256-row three-stage 8-wave form (K = 128, 256, 576).  The published max |C| equals the stored output's exactly."""
+    the persistent form (gemm path 8); the *_many / *_big cases give each workgroup several tiles
+    with a ragged last tile (linear_many_res at K = 64: a tile boundary every second step, 2344
+    tiles on 512 slots; linear_many_n64, linear_big_res, conv3x3_big: K = 128, 256, 576).  The published max |C| equals the stored output's exactly."""
     err = _split_gemm_err(gpu_device, case, "fp32h3", amp=amp, want_path=8)
     e32 = _split_gemm_err(gpu_device, case, "fp32", amp=amp)
     assert err <= max(1e-6, 2 * e32), (err, e32)
