@@ -454,6 +454,17 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       const bool last = &e == &m->enc.back();
       CK(run_ffn(m, "ffn.enc", e.l1, e.l2, e.n2g, e.n2b, P(w.src), Mt, s, last ? m->pos : nullptr,
                  last ? P(w.srcpos) : nullptr, T));
+    } else if (m->h3 && e.ffn_w2p && src_amax && m->wh3.count(e.l1.w)) {
+      // fp32h3: linear1 + ReLU + linear2 + residual + norm2 in one pass, in place over src
+      FfnH3Args a{};
+      a.x = (const float*)P(w.src); a.ldx = d; a.y = (float*)P(w.src); a.ldy = d;
+      a.M = Mt; a.D = d; a.F = ff;
+      a.w1 = m->wh3.at(e.l1.w).planes; a.ld1 = e.l1.Kpad; a.meta1 = e.ffn_meta1;
+      a.w2 = e.ffn_w2p; a.ld2 = ff; a.sinv2 = m->wh3.at(e.l2.w).sinv; a.b2 = e.l2.bias;
+      a.gamma = e.n2g; a.beta = e.n2b;
+      a.amax_x = src_amax; a.sh = e.ffn_sh;
+      const double fl = 4.0 * Mt * (double)d * ff, by = 2.0 * Mt * d * 4.0 + 2.0 * 2.0 * 2.0 * d * ff;
+      CK(run_other(m, "ffn.enc", fl, by, s, [&] { return spe_launch_ffn_h3(a, s); }));
     } else {
       {
         GemmArgs g = linear_args(e.l1, P(w.src), d, Mt, P(w.ffn), ff);

@@ -32,6 +32,11 @@ struct Enc {
   // / std <= sqrt(D - 1)), the scale input of the GEMMs that read them
   float *n1_bound = nullptr, *n2_bound = nullptr;
   void* pos_qk = nullptr;   // bf16 / fp32x6 models: pos . W_qk^T [tokens][512] (row-periodic residual)
+  // fp32h3, the one-pass FFN (ffn_h3.hip): (2^-e1, b1) per 32-unit chunk, W2's planes with the columns
+  // in spe_ffn_h3_perm order, and the hidden activation's power-of-two scale from its static bound
+  float* ffn_meta1 = nullptr;
+  void* ffn_w2p = nullptr;
+  float ffn_sh = 0.f;
 };
 
 struct Dec {

@@ -175,6 +175,66 @@ float* upload_f32(spe_model* m, const float* p, size_t n) {
   return dst;
 }
 
+// fp32h3, the one-pass encoder FFN (ffn_h3.hip): e.ffn_meta1 = (2^-e1, b1) per 32-unit hidden chunk
+// (e1 as upload_rows scales linear1's rows), e.ffn_w2p = linear2's fp16 planes with each chunk's
+// columns in spe_ffn_h3_perm order (rows scaled as upload_rows does: the same 2^-e2 as e.l2's planes),
+// e.ffn_sh = 2^(13 - e) for the bound B on |ReLU(x W1^T + b1)| in [2^(e-1), 2^e): B = max_j |b1_j| +
+// ||W1_j||_2 (max|gamma1| sqrt(D) + ||beta1||_2), ||x||_2 of a LayerNorm output never exceeding the
+// latter (sum of the normalised squares = D var / (var + eps) <= D)
+static void ffn_h3_prepare(spe_model* m, Enc& e, const std::string& p, int d, int ff) {
+  if (!m->h3 || d != 256 || ff % 32 || ff % 8) return;
+  const size_t n2 = (size_t)d * ff;
+  e.ffn_meta1 = (float*)dalloc(m, (size_t)ff * 2 * 4);
+  e.ffn_w2p = dalloc(m, 2 * n2 * 2);
+  if (!m->dmem) return;
+  const auto& w1 = m->host[p + ".linear1.weight"];
+  const auto& b1 = m->host[p + ".linear1.bias"];
+  const auto& w2 = m->host[p + ".linear2.weight"];
+  const auto& g1 = m->host[p + ".norm1.weight"];
+  const auto& be1 = m->host[p + ".norm1.bias"];
+  double gmax = 0.0, bn = 0.0;
+  for (float v : g1) gmax = std::max(gmax, (double)std::fabs(v));
+  for (float v : be1) bn += (double)v * v;
+  const double rx = gmax * std::sqrt((double)d) + std::sqrt(bn);
+  std::vector<float> meta((size_t)ff * 2);
+  double bound = 0.0;
+  for (int j = 0; j < ff; ++j) {
+    float am = 0.f;
+    double nn = 0.0;
+    for (int k = 0; k < d; ++k) {
+      const float v = w1[(size_t)j * d + k];
+      am = std::max(am, std::fabs(v));
+      nn += (double)v * v;
+    }
+    int ex = 0;
+    if (am > 0.f && std::isfinite(am)) std::frexp(am, &ex);
+    const int c = j / 32, u = j % 32;
+    meta[(size_t)c * 64 + u] = am > 0.f ? std::ldexp(1.f, ex - 13) : 1.f;
+    meta[(size_t)c * 64 + 32 + u] = b1[j];
+    bound = std::max(bound, std::fabs((double)b1[j]) + std::sqrt(nn) * rx);
+  }
+  int eb = 0;
+  std::frexp(bound > 0.0 ? bound * (1.0 + 1e-6) : 1.0, &eb);
+  e.ffn_sh = std::ldexp(1.f, 13 - eb);
+  std::vector<_Float16> planes(2 * n2);
+  for (int n = 0; n < d; ++n) {
+    float am = 0.f;
+    for (int k = 0; k < ff; ++k) am = std::max(am, std::fabs(w2[(size_t)n * ff + k]));
+    int ex = 0;
+    if (am > 0.f && std::isfinite(am)) std::frexp(am, &ex);
+    const float sc = am > 0.f ? std::ldexp(1.f, 13 - ex) : 1.f;
+    for (int k = 0; k < ff; ++k) {
+      const int src = (k / 32) * 32 + spe_ffn_h3_perm(k % 32);
+      const float x = w2[(size_t)n * ff + src] * sc;
+      const _Float16 hi = (_Float16)x;
+      planes[(size_t)n * ff + k] = hi;
+      planes[n2 + (size_t)n * ff + k] = (_Float16)(x - (float)hi);
+    }
+  }
+  m->upload_err |= (int)hipMemcpy(e.ffn_meta1, meta.data(), meta.size() * 4, hipMemcpyHostToDevice);
+  m->upload_err |= (int)hipMemcpy(e.ffn_w2p, planes.data(), planes.size() * 2, hipMemcpyHostToDevice);
+}
+
 // fp32h3: a device bound on |LayerNorm `key` output| of width D: max|gamma| sqrt(D - 1) + max|beta|
 // (|x_i - mean| / std <= sqrt(D - 1) for any row) -- the scale input of the GEMMs reading it
 float* ln_bound(spe_model* m, const std::string& key, int D) {
@@ -519,6 +579,7 @@ int build_device(spe_model* m) {
     if (m->h3) {
       e.n1_bound = ln_bound(m, p + ".norm1", d);
       e.n2_bound = ln_bound(m, p + ".norm2", d);
+      ffn_h3_prepare(m, e, p, d, ff);
     }
     m->enc.push_back(e);
   }

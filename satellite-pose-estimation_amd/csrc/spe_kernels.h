@@ -167,6 +167,22 @@ struct FfnArgs {
   int row0;                        // first row of this launch's tiles (internal: the FFN tail launch)
 };
 int spe_launch_ffn_ln(const FfnArgs& a, hipStream_t s);
+// fp32h3 encoder FFN + residual + LayerNorm in one pass (ffn_h3.hip): fp32 x / y [M][256], W1 as its
+// h3 finalize planes fp16 [2][F][ld1] (rows scaled by 2^e1), meta1 [F/32][64] = (2^-e1, b1) of each
+// 32-unit hidden chunk, W2 as fp16 planes [2][256][ld2] (rows scaled by 2^e2) with the columns of
+// every 32-wide chunk in spe_ffn_h3_perm order, sinv2 = 2^-e2; amax_x = the bound on |x| (the A
+// scale), sh = the power-of-two scale of the hidden activation (from its static bound)
+struct FfnH3Args {
+  const float* x; int ldx;
+  float* y; int ldy;
+  int M, D, F;
+  const void* w1; int ld1; const float* meta1;
+  const void* w2; int ld2; const float* sinv2; const float* b2;
+  const float* gamma; const float* beta;
+  const float* amax_x; float sh;
+};
+int spe_launch_ffn_h3(const FfnH3Args& a, hipStream_t s);
+int spe_ffn_h3_perm(int p);
 int spe_ffn_splits(int M, int F);  // split count spe_launch_ffn_ln would use for M rows (1 = none)
 
 int spe_launch_preprocess(const uint8_t* frames, int B, int H, int W, int C, const double* bbox, int S,
