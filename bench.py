@@ -102,7 +102,7 @@ def parse():
                         "(default, DETR): label-diverse + the point head fitted on the timed batch so each "
                         "query predicts its label's landmark projection + N(0, 2 px) + 10%% outliers "
                         "(spe.synthetic.fit_point_head), so RANSAC finds consensus and the refinement runs")
-    p.add_argument("--parity-dtype", default="fp32x6", choices=["fp32x6", "fp32h3", "fp32x3", "fp32"],
+    p.add_argument("--parity-dtype", default="fp32h3", choices=["fp32h3", "fp32x6", "fp32x3", "fp32"],
                    help="the parity mode timed after the main line in the same process (parity_mode object: its "
                         "own ms_per_step, value, roofline and accuracy against the exact-f32 mode)")
     p.add_argument("--no-parity", action="store_true", help="skip the parity_mode timing")

@@ -299,6 +299,16 @@ int spe_debug_gemm_h3(void* stream, int mode, const void* A, int lda, int H, int
                       int pad, int ldb, int M, int N, int K, const float* bias, const void* R, int ldr, int act_code,
                       void* C, int ldc, const void* planes, int plane_rows, const float* sinv, const float* amax_a,
                       float* amax_c, float amax_c_mul, const float* ln_g, const float* ln_b);
+/* fp32h3 one-pass encoder FFN (ffn_h3.hip): y = LayerNorm(x + ReLU(x W1^T + b1) W2^T + b2) (eps 1e-5)
+ * on fp32 x / y [M][256] (y may be x), F hidden units.  w1 = fp16 [2][F][ld1] hi, lo of W1[j] 2^e1_j;
+ * meta1 = [F/32][64] floats: 2^-e1 of the chunk's 32 units, then their b1; w2 = fp16 [2][256][ld2]
+ * hi, lo of W2[n] 2^e2_n with the columns of each 32-wide chunk permuted by spe_debug_ffn_h3_perm;
+ * sinv2 = 2^-e2; amax_x = device bound on |x|; sh = the hidden activation's power-of-two scale. */
+int spe_debug_ffn_h3(void* stream, const float* x, int ldx, float* y, int ldy, int M, int F, const void* w1, int ld1,
+                     const float* meta1, const void* w2, int ld2, const float* sinv2, const float* b2,
+                     const float* gamma, const float* beta, const float* amax_x, float sh);
+/* position p (0..31) of a 32-wide hidden chunk in that column order -> the hidden unit it holds */
+int spe_debug_ffn_h3_perm(int p);
 /* the same launch with the weights also given pre-split (dtype SPE_DTYPE_F32X6_): planes = bf16
  * [3][plane_rows][ldb] holding hi, mid, lo of Bw (what spe_model_finalize writes for fp32x6 models) */
 int spe_debug_gemm_planes(void* stream, int dtype, int mode, const void* A, int lda, const void* P, int ldp, int prow,

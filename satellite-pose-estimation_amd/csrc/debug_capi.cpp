@@ -71,6 +71,19 @@ int spe_debug_gemm_h3(void* stream, int mode, const void* A, int lda, int H, int
 
 int spe_debug_gemm_path(void) { return spe_gemm_last_path; }
 
+int spe_debug_ffn_h3(void* stream, const float* x, int ldx, float* y, int ldy, int M, int F, const void* w1, int ld1,
+                     const float* meta1, const void* w2, int ld2, const float* sinv2, const float* b2,
+                     const float* gamma, const float* beta, const float* amax_x, float sh) {
+  FfnH3Args a{};
+  a.x = x; a.ldx = ldx; a.y = y; a.ldy = ldy; a.M = M; a.D = 256; a.F = F;
+  a.w1 = w1; a.ld1 = ld1; a.meta1 = meta1; a.w2 = w2; a.ld2 = ld2; a.sinv2 = sinv2; a.b2 = b2;
+  a.gamma = gamma; a.beta = beta; a.amax_x = amax_x; a.sh = sh;
+  const int rc = spe_launch_ffn_h3(a, (hipStream_t)stream);
+  return rc < 0 ? spe_fail(SPE_E_ARG, "ffn_h3 launch rejected its arguments") : rc;
+}
+
+int spe_debug_ffn_h3_perm(int p) { return p >= 0 && p < 32 ? spe_ffn_h3_perm(p) : -1; }
+
 int spe_debug_attention(void* stream, int dtype, const void* q, int ldq, const void* k, int ldk, const void* vt,
                         void* o, int ldo, int B, int H, int Tq, int Tk, float scale) {
   AttnArgs a{};

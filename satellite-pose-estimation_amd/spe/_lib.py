@@ -40,7 +40,7 @@ SPE_PNP_OK, SPE_PNP_NO_FG, SPE_PNP_CV_ERROR, SPE_PNP_RANSAC_FALLBACK, SPE_PNP_UN
 EXPORTS = ["spe_abi_version", "spe_last_error", "spe_model_create", "spe_model_destroy", "spe_model_set_param",
            "spe_model_num_params", "spe_model_param_name", "spe_model_finalize", "spe_model_workspace_bytes",
            "spe_forward", "spe_forward_stages", "spe_preprocess", "spe_criterion", "spe_ensemble_fuse", "spe_postprocess", "spe_pnp_batch", "spe_self_assess", "spe_speed_score", "spe_model_profile_begin",
-           "spe_model_profile_end", "spe_model_profile_get", "spe_debug_gemm", "spe_debug_gemm_path", "spe_debug_gemm_h3", "spe_debug_gemm_planes", "spe_debug_attention",
+           "spe_model_profile_end", "spe_model_profile_get", "spe_debug_gemm", "spe_debug_gemm_path", "spe_debug_gemm_h3", "spe_debug_ffn_h3", "spe_debug_ffn_h3_perm", "spe_debug_gemm_planes", "spe_debug_attention",
            "spe_debug_layernorm", "spe_debug_ffn", "spe_debug_xattn", "spe_debug_upconv", "spe_debug_btail", "spe_debug_decsa", "spe_debug_decproj", "spe_debug_btail_perm", "spe_debug_stempool", "spe_rtdetr_create", "spe_rtdetr_forward",
            "spe_jpeg_workspace_bytes", "spe_jpeg_decode"]
 
@@ -109,6 +109,8 @@ def lib():
     L.spe_debug_gemm.argtypes = [P, I, I, P, I, P, I, I] + [I] * 7 + [P, I, I, I, I, P, P, I, I, P, I, I, I, I, I, P, P, I]
     L.spe_debug_gemm_path.argtypes = []
     L.spe_debug_gemm_h3.argtypes = [P, I, P, I] + [I] * 7 + [I, I, I, I, P, P, I, I, P, I, P, I, P, P, P, ctypes.c_float, P, P]
+    L.spe_debug_ffn_h3.argtypes = [P, P, I, P, I, I, I, P, I, P, P, I, P, P, P, P, P, ctypes.c_float]
+    L.spe_debug_ffn_h3_perm.argtypes = [I]
     L.spe_debug_gemm_planes.argtypes = [P, I, I, P, I, P, I, I] + [I] * 7 + [P, I, I, I, I, P, P, I, I, P, I, P, I]
     L.spe_debug_attention.argtypes = [P, I, P, I, P, I, P, P, I, I, I, I, I, F]
     L.spe_debug_layernorm.argtypes = [P, I, P, P, P, P, P, I, I]

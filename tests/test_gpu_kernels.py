@@ -6,9 +6,11 @@ pre-rounded to bf16 so only accumulation order and the bf16 output rounding rema
 max|d| <= 1e-2 * scale (scale = max|reference|, at least 1).
 """
 import ctypes
+import math
 import os
 
 import numpy as np
+
 import pytest
 import torch
 import torch.nn.functional as F
@@ -1054,6 +1056,59 @@ def test_gemm_h3_layernorm_epilogue(gpu_device, M, K):
     assert L.spe_debug_gemm_path() == 7
     err = (C.double().cpu() - ref).abs().max().item()
     assert err <= 2e-5, err
+
+
+def _h3_row_planes(W):
+    """fp32 [N][K] -> (fp16 [2][N][K] hi, lo of W[n] 2^e_n, 2^-e_n) -- the h3 finalize form."""
+    am = W.abs().amax(1).double()
+    e = torch.where(am > 0, torch.frexp(am).exponent.double(), torch.zeros_like(am))
+    sc = torch.where(am > 0, torch.pow(2.0, 13 - e), torch.ones_like(am)).float()[:, None]
+    x = W * sc
+    h = x.to(torch.float16)
+    return torch.stack([h, (x - h.float()).to(torch.float16)]).contiguous(), (1.0 / sc[:, 0]).contiguous()
+
+
+@pytest.mark.parametrize("M,F,inplace,loose", [(2 * 2704, 2048, True, False), (1000, 2048, False, True),
+                                               (77, 96, True, False), (0, 64, False, False)])
+def test_ffn_h3_one_pass(gpu_device, M, F, inplace, loose):
+    """fp32h3 one-pass encoder FFN (ffn_h3.hip; REV/models/transformer.py:164-167): LayerNorm(x +
+    ReLU(x W1^T + b1) W2^T + b2) with x a LayerNorm output, against fp64, within 2e-5 (the fused
+    LayerNorm GEMM's bound) -- whole 128-row tiles and a ragged one, 64 / 3 hidden chunks, in place
+    (y = x, as the model runs it) and not, the hidden scale from the tight bound and from one 2^10
+    too loose (the split keeps fp32-level error); M = 0 launches nothing."""
+    L = _lib.lib()
+    dev, f = gpu_device, torch.float32
+    g = torch.Generator(device="cpu").manual_seed(M + F)
+    D = 256
+    x = F_.layer_norm(torch.randn(max(M, 1), D, generator=g, dtype=torch.float64), (D,)) * 1.3 + 0.05
+    x = x[:M]
+    W1 = torch.randn(F, D, generator=g, dtype=torch.float64) / 16
+    b1 = torch.randn(F, generator=g, dtype=torch.float64) * 0.1
+    W2 = torch.randn(D, F, generator=g, dtype=torch.float64) / F ** 0.5
+    b2 = torch.randn(D, generator=g, dtype=torch.float64) * 0.1
+    gam = 1 + 0.1 * torch.randn(D, generator=g, dtype=torch.float64)
+    bet = 0.1 * torch.randn(D, generator=g, dtype=torch.float64)
+    hid = torch.relu(x @ W1.t() + b1)
+    ref = F_.layer_norm(x + hid @ W2.t() + b2, (D,), gam, bet, 1e-5)
+    hmax = hid.abs().max().item() if M else 1.0
+    bound = hmax * (1024.0 if loose else 1.0) * (1 + 1e-6)
+    sh = 2.0 ** (13 - math.frexp(bound)[1])
+    w1p, s1 = _h3_row_planes(W1.to(f))
+    meta = torch.stack([s1.view(F // 32, 32), b1.to(f).view(F // 32, 32)], 1).reshape(-1).contiguous()
+    perm = torch.tensor([L.spe_debug_ffn_h3_perm(p) for p in range(32)])
+    cols = (torch.arange(F) // 32) * 32 + perm[torch.arange(F) % 32]
+    w2p, s2 = _h3_row_planes(W2.to(f)[:, cols].contiguous())
+    xd = x.to(dev, f).contiguous()
+    yd = xd if inplace else torch.zeros_like(xd)
+    amax = (xd.abs().max() if M else torch.ones(())).reshape(1).to(dev).contiguous()
+    keep = [t.to(dev).contiguous() for t in (w1p, meta, w2p, s2, b2.to(f), gam.to(f), bet.to(f))]
+    rc = L.spe_debug_ffn_h3(None, _p(xd), D, _p(yd), D, M, F, _p(keep[0]), D, _p(keep[1]), _p(keep[2]), F,
+                            _p(keep[3]), _p(keep[4]), _p(keep[5]), _p(keep[6]), _p(amax), sh)
+    assert rc == 0, L.spe_last_error()
+    torch.cuda.synchronize()
+    if M:
+        err = (yd.double().cpu() - ref).abs().max().item()
+        assert err <= 2e-5, err
 
 
 def _bf16_planes(x):

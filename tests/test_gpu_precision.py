@@ -164,34 +164,37 @@ def test_fp32x6_within_fp32_implementation_spread(gpu_device):
             ok = np.isfinite(d)
             tab[f"{a}_vs_{b}"] = {"frac_le_1e-4": float((d[ok] <= 1e-4).mean()), "max": float(d[ok].max()),
                                   "median": float(np.median(d[ok]))}
-        d6 = np.abs(sc["fp32x6"] - sc["fp32"])
         dc = np.abs(sc["torch_cpu"] - sc["fp32"])
         dg = np.abs(sc["torch_gpu"] - sc["fp32"])
-        miss = np.where(d6 > 1e-4)[0]
-        # the decision behind every fp32x6 miss: oracle traces of the two keypoint sets
-        _, tr32 = pnp_ref.pnp_trace(impl["fp32"][1][miss].cpu().numpy(), impl["fp32"][2][miss].cpu().numpy(), K, Wd,
-                                    mode=mode, repro=20.0)
-        _, tr6 = pnp_ref.pnp_trace(impl["fp32x6"][1][miss].cpu().numpy(), impl["fp32x6"][2][miss].cpu().numpy(), K,
-                                   Wd, mode=mode, repro=20.0)
-        per = []
-        for j, i in enumerate(miss):
-            per.append({"image": int(i), "score_fp32": float(sc["fp32"][i]), "delta_fp32x6": float(d6[i]),
-                        "delta_torch_cpu": float(dc[i]), "delta_torch_gpu": float(dg[i]), "cond_f32_ulp": float(cond[i]),
-                        "decision": _decision(tr32[j], tr6[j], mode),
-                        "epnp_err_fp32": [round(tr32[j][f"epnp_err{c}"], 6) for c in (1, 2, 3)],
-                        "epnp_err_fp32x6": [round(tr6[j][f"epnp_err{c}"], 6) for c in (1, 2, 3)],
-                        "epnp_pick": [tr32[j]["epnp_pick"], tr6[j]["epnp_pick"]],
-                        **({"ransac_inliers": [tr32[j]["ransac_inliers"], tr6[j]["ransac_inliers"]],
-                            "ransac_margin_px": round(tr32[j]["ransac_margin_px"], 4)} if mode == 1 else {})})
         wc = cond <= 1e-4
         r["score"][name] = {"pairs": tab, "images_ill_conditioned_at_f32_ulp": int((~wc).sum()),
                             "cond_median": float(np.median(cond)),
-                            "frac_fp32x6_le_1e-4_well_conditioned": float((d6[wc] <= 1e-4).mean()) if wc.any() else None,
                             "frac_torch_cpu_le_1e-4_well_conditioned": float((dc[wc] <= 1e-4).mean()) if wc.any() else None,
-                            "fp32x6_misses": per,
-                            "decisions": {k: sum(1 for p in per if p["decision"].split(" ")[0] == k)
-                                          for k in sorted({p["decision"].split(" ")[0] for p in per})}}
-        trace_pairs[name] = (d6, dc, cond, per)
+                            "decisions": {}}
+        for cand in ("fp32x6", "fp32h3"):
+            d6 = np.abs(sc[cand] - sc["fp32"])
+            miss = np.where(d6 > 1e-4)[0]
+            # the decision behind every miss: oracle traces of the two keypoint sets
+            _, tr32 = pnp_ref.pnp_trace(impl["fp32"][1][miss].cpu().numpy(), impl["fp32"][2][miss].cpu().numpy(), K,
+                                        Wd, mode=mode, repro=20.0)
+            _, tr6 = pnp_ref.pnp_trace(impl[cand][1][miss].cpu().numpy(), impl[cand][2][miss].cpu().numpy(), K,
+                                       Wd, mode=mode, repro=20.0)
+            per = []
+            for j, i in enumerate(miss):
+                per.append({"image": int(i), "score_fp32": float(sc["fp32"][i]), f"delta_{cand}": float(d6[i]),
+                            "delta_torch_cpu": float(dc[i]), "delta_torch_gpu": float(dg[i]),
+                            "cond_f32_ulp": float(cond[i]), "decision": _decision(tr32[j], tr6[j], mode),
+                            "epnp_err_fp32": [round(tr32[j][f"epnp_err{c}"], 6) for c in (1, 2, 3)],
+                            f"epnp_err_{cand}": [round(tr6[j][f"epnp_err{c}"], 6) for c in (1, 2, 3)],
+                            "epnp_pick": [tr32[j]["epnp_pick"], tr6[j]["epnp_pick"]],
+                            **({"ransac_inliers": [tr32[j]["ransac_inliers"], tr6[j]["ransac_inliers"]],
+                                "ransac_margin_px": round(tr32[j]["ransac_margin_px"], 4)} if mode == 1 else {})})
+            r["score"][name][f"frac_{cand}_le_1e-4_well_conditioned"] = \
+                float((d6[wc] <= 1e-4).mean()) if wc.any() else None
+            r["score"][name][f"{cand}_misses"] = per
+            r["score"][name]["decisions"][cand] = {k: sum(1 for p in per if p["decision"].split(" ")[0] == k)
+                                                   for k in sorted({p["decision"].split(" ")[0] for p in per})}
+        trace_pairs[name] = cond
 
     out = os.path.join(REPO, "gpurun_out")
     if os.path.isdir(out):
