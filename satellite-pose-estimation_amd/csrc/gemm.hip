@@ -1677,7 +1677,10 @@ int launch_h3d(const GemmArgs& g, int mode, hipStream_t s) {
       return (int)hipGetLastError();
     }
   }
-  if (g.vt_T <= 0 && !g.S && g.K >= 64 && !(g.N & 3) && !(g.ldc & 3) && !(reinterpret_cast<uintptr_t>(g.C) & 15) &&
+  // (long-K problems keep the non-persistent kernel: the layer-3 3x3, K = 2304, measured 0.213 vs
+  // 0.245 ms and the neck, K = 4608, 1.35 vs 1.39 ms; up to K = 1152 the persistent form is as fast
+  // or faster)
+  if (g.vt_T <= 0 && !g.S && g.K >= 64 && g.K <= 1280 && !(g.N & 3) && !(g.ldc & 3) && !(reinterpret_cast<uintptr_t>(g.C) & 15) &&
       (long long)g.M * g.ldc * 4 < LIM && (!res || (!pl && !(g.ldr & 3) && !(reinterpret_cast<uintptr_t>(g.R) & 15)))) {
     const int ncu = spe_cu_count();
     // (the 256-row, three-stage, 8-wave form -- H3PGeo<4, 8, 3> -- measured 0-5 % slower on every

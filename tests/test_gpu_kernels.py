@@ -1022,7 +1022,8 @@ def test_gemm_h3_close_to_fp64(gpu_device, case, amp):
     the persistent form (gemm path 8); the *_many / *_big cases give each workgroup several tiles
     with a ragged last tile (linear_many_res at K = 64: a tile boundary every second step, 2344
     tiles on 512 slots; linear_many_n64, linear_big_res, conv3x3_big: K = 128, 256, 576).  The published max |C| equals the stored output's exactly."""
-    err = _split_gemm_err(gpu_device, case, "fp32h3", amp=amp, want_path=8)
+    # (K = 2304, the layer-3 3x3: the non-persistent kernel, path 7; every other case persistent)
+    err = _split_gemm_err(gpu_device, case, "fp32h3", amp=amp, want_path=7 if case == "conv3x3" else 8)
     e32 = _split_gemm_err(gpu_device, case, "fp32", amp=amp)
     assert err <= max(1e-6, 2 * e32), (err, e32)
 
