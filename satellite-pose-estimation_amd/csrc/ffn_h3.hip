@@ -28,9 +28,11 @@ constexpr int FH_BM = 128, FH_NT = 256, FH_HC = 32, FH_D = 256;
 constexpr int FH_W1 = 2 * FH_HC * FH_D * 2;     // 32 KB: [plane][32 rows][512 B]
 constexpr int FH_W2 = 2 * FH_D * FH_HC * 2;     // 32 KB: [plane][256 rows][64 B]
 constexpr int FH_META = 2 * FH_HC * 4;          // 2^-e1[32], b1[32]
-constexpr int FH_SLOT = FH_W1 + FH_W2 + FH_META;
+constexpr int FH_S1 = FH_W1 + FH_META;          // W1 ring slot: the chunk's planes + (2^-e1, b1)
+constexpr int FH_R2 = 2 * FH_S1;                // W2 ring: 2 slots of FH_W2 from here
 constexpr int FH_EPI = 4 * FH_D * 4;            // 2^-e2, b2, gamma2, beta2
-constexpr int FH_SMEM = 2 * FH_SLOT + FH_EPI;
+constexpr int FH_EP = FH_R2 + 2 * FH_W2;
+constexpr int FH_SMEM = FH_EP + FH_EPI;
 constexpr int FH_BAD = 0x7ffffff0;
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
@@ -66,7 +68,7 @@ __global__ __launch_bounds__(FH_NT, 1) void ffn_h3_kernel(FfnH3Args a) {
 
   // ---- epilogue parameters to LDS (published by the first barrier)
   {
-    float* ep = reinterpret_cast<float*>(smem + 2 * FH_SLOT);
+    float* ep = reinterpret_cast<float*>(smem + FH_EP);
     ep[tid] = a.sinv2[tid];
     ep[FH_D + tid] = a.b2[tid];
     ep[2 * FH_D + tid] = a.gamma[tid];
@@ -78,26 +80,34 @@ __global__ __launch_bounds__(FH_NT, 1) void ffn_h3_kernel(FfnH3Args a) {
   const __amdgpu_buffer_rsrc_t r1 = __builtin_amdgcn_make_buffer_rsrc((void*)a.w1, (short)0, (int)(2 * p1), 0x00020000);
   const __amdgpu_buffer_rsrc_t r2 = __builtin_amdgcn_make_buffer_rsrc((void*)a.w2, (short)0, (int)(2 * p2), 0x00020000);
   const __amdgpu_buffer_rsrc_t rm = __builtin_amdgcn_make_buffer_rsrc((void*)a.meta1, (short)0, a.F * 8, 0x00020000);
-  auto issue = [&](int c, int slot) {
-    char* base = smem + slot * FH_SLOT;
+  // W1 and W2 chunks in separate two-slot rings: iteration c multiplies chunk c + 1's phase 1 (W1 slot
+  // (c + 1) & 1) beside chunk c's phase 2 (W2 slot c & 1) and refills W1 slot c & 1 with chunk c + 2
+  // and W2 slot (c + 1) & 1 with chunk c + 1, one iteration ahead of their use
+  auto issue_w1 = [&](int c, int slot) {
+    char* base = smem + slot * FH_S1;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {                      // W1: piece k = w + 4i: plane k >> 4, rows 2 (k & 15) + hi
+    for (int i = 0; i < 8; ++i) {                      // piece k = w + 4i: plane k >> 4, rows 2 (k & 15) + hi
       const int k = wid + 4 * i, p = k >> 4, row = 2 * (k & 15) + hi, pos = l31;
       const int ch = pos ^ (row & 15);
       const int off = (int)(p * p1) + (c * FH_HC + row) * a.ld1 * 2 + ch * 16;
       __builtin_amdgcn_raw_ptr_buffer_load_lds(r1, (lds_ptr_t)(base + k * 1024), 16, off, 0, 0, 0);
     }
+    if (wid == 0)
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(rm, (lds_ptr_t)(base + FH_W1), 4, (c * 64 + lane) * 4, 0, 0, 0);
+  };
+  auto issue_w2 = [&](int c, int slot) {
+    char* base = smem + FH_R2 + slot * FH_W2;
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {                      // W2: piece k: plane k >> 4, rows 16 (k & 15) + lane / 4
+    for (int i = 0; i < 8; ++i) {                      // piece k: plane k >> 4, rows 16 (k & 15) + lane / 4
       const int k = wid + 4 * i, p = k >> 4, n = 16 * (k & 15) + (lane >> 2), pos = lane & 3;
       const int ch = pos ^ ((n >> 2) & 3);
       const int off = (int)(p * p2) + n * a.ld2 * 2 + c * FH_HC * 2 + ch * 16;
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(r2, (lds_ptr_t)(base + FH_W1 + k * 1024), 16, off, 0, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r2, (lds_ptr_t)(base + k * 1024), 16, off, 0, 0, 0);
     }
-    if (wid == 0)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(rm, (lds_ptr_t)(base + FH_W1 + FH_W2), 4, (c * 64 + lane) * 4, 0, 0, 0);
   };
-  issue(0, 0);
+  issue_w1(0, 0);
+  if (nch > 1) issue_w1(1, 1);
+  issue_w2(0, 0);
 
   // ---- x rows of this wave: split planes in registers (B operand of phase 1)
   const int row = m0 + wid * 32 + l31;
@@ -130,20 +140,15 @@ __global__ __launch_bounds__(FH_NT, 1) void ffn_h3_kernel(FfnH3Args a) {
   // W2 row 32 j + l31, chunk 2 kb + hi at (chunk ^ ((row >> 2) & 3))
   const int w1o = l31 * 512, w1x = l31 & 15;
   const int w2x = (l31 >> 2) & 3;
-  __builtin_amdgcn_s_waitcnt(0);                      // chunk 0 (and the epilogue parameters)
-  __syncthreads();
-  for (int c = 0; c < nch; ++c) {
-    const char* sl = smem + (c & 1) * FH_SLOT;
-    if (c + 1 < nch) issue(c + 1, (c + 1) & 1);       // the slot chunk c - 1 used: free since the barrier
-    // ---- phase 1: H^T[32 hidden][32 tokens] over K = 256 (16 K-blocks)
-    f32x16 hacc;
+  // ---- phase 1 of a chunk: H^T[32 hidden][32 tokens] over K = 256 (16 K-blocks), W1 slot s1
+  auto phase1 = [&](const char* s1, f32x16& hacc) {
 #pragma unroll
     for (int r = 0; r < 16; ++r) hacc[r] = 0.f;
     u32x4 fa[3][2];
     auto rd1 = [&](int kb, u32x4* f) {
       const int off = w1o + (((2 * kb + hi) ^ w1x) << 4);
-      f[0] = ld16(sl + off);                          // hi plane
-      f[1] = ld16(sl + FH_W1 / 2 + off);              // lo plane
+      f[0] = ld16(s1 + off);                          // hi plane
+      f[1] = ld16(s1 + FH_W1 / 2 + off);              // lo plane
     };
     rd1(0, fa[0]);
     rd1(1, fa[1]);
@@ -156,28 +161,31 @@ __global__ __launch_bounds__(FH_NT, 1) void ffn_h3_kernel(FfnH3Args a) {
       hacc = mf(f[0], xh[kb], hacc);
       __builtin_amdgcn_sched_barrier(0);
     }
-    // ---- h = ReLU(hacc 2^-e1 / s_x + b1), scaled by s_h and split: lane rows 8 (r >> 2) + 4 hi + (r & 3)
-    u32x4 hh[2], hl[2];
-    {
-      const float* meta = reinterpret_cast<const float*>(sl + FH_W1 + FH_W2);
-      float hv[16];
+  };
+  // ---- h = ReLU(hacc 2^-e1 / s_x + b1) s_h, split: lane rows 8 (r >> 2) + 4 hi + (r & 3); in steps
+  // (0..3: the four row groups, 4 / 5: the two K-block splits) so phase 2's MFMAs can carry them
+  float hv[16];
+  auto hconv = [&](const char* s1, const f32x16& hacc, int step, u32x4* hh, u32x4* hl) {
+    if (step < 4) {
+      const float* meta = reinterpret_cast<const float*>(s1 + FH_W1);
+      const f32x4 si = *reinterpret_cast<const f32x4*>(meta + 8 * step + 4 * hi);
+      const f32x4 bi = *reinterpret_cast<const f32x4*>(meta + FH_HC + 8 * step + 4 * hi);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f32x4 si = *reinterpret_cast<const f32x4*>(meta + 8 * q + 4 * hi);
-        const f32x4 bi = *reinterpret_cast<const f32x4*>(meta + FH_HC + 8 * q + 4 * hi);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) hv[4 * q + e] = fmaxf(hacc[4 * q + e] * (si[e] * inv_sx) + bi[e], 0.f) * sh;
-      }
-      h_split8(hv, hh[0], hl[0]);
-      h_split8(hv + 8, hh[1], hl[1]);
+      for (int e = 0; e < 4; ++e)
+        hv[4 * step + e] = fmaxf(hacc[4 * step + e] * (si[e] * inv_sx) + bi[e], 0.f) * sh;
+    } else {
+      h_split8(hv + 8 * (step - 4), hh[step - 4], hl[step - 4]);
     }
-    // ---- phase 2: out^T[256][32 tokens] += W2_c h^T (8 column blocks x 2 K-blocks)
+  };
+  // ---- phase 2 of chunk c from W2 slot s2 with h (hh, hl), chunk c + 1's conversion interleaved
+  auto phase2 = [&](const char* s2, const u32x4* hh, const u32x4* hl, bool conv, const char* s1n,
+                    const f32x16& haccn, u32x4* hhn, u32x4* hln) {
     u32x4 fb[3][2];
     auto rd2 = [&](int t, u32x4* f) {                 // t = 2 j + kb
       const int j = t >> 1, kb = t & 1;
-      const int off = FH_W1 + (32 * j + l31) * 64 + (((2 * kb + hi) ^ w2x) << 4);
-      f[0] = ld16(sl + off);
-      f[1] = ld16(sl + FH_W2 / 2 + off);
+      const int off = (32 * j + l31) * 64 + (((2 * kb + hi) ^ w2x) << 4);
+      f[0] = ld16(s2 + off);
+      f[1] = ld16(s2 + FH_W2 / 2 + off);
     };
     rd2(0, fb[0]);
     rd2(1, fb[1]);
@@ -189,15 +197,41 @@ __global__ __launch_bounds__(FH_NT, 1) void ffn_h3_kernel(FfnH3Args a) {
       acc[j] = mf(f[1], hh[kb], acc[j]);
       acc[j] = mf(f[0], hl[kb], acc[j]);
       acc[j] = mf(f[0], hh[kb], acc[j]);
+      if (conv && t >= 4 && t < 10) hconv(s1n, haccn, t - 4, hhn, hln);
       __builtin_amdgcn_sched_barrier(0);
     }
-    __builtin_amdgcn_s_waitcnt(0);                    // chunk c + 1 landed (this wave's pieces)
-    __syncthreads();                                   // ... all pieces; slot c & 1 free
+  };
+
+  __builtin_amdgcn_s_waitcnt(0);                      // W1 chunks 0, 1, W2 chunk 0, epilogue parameters
+  __syncthreads();
+  u32x4 hh[2], hl[2], hhn[2], hln[2];
+  {
+    f32x16 hacc;
+    phase1(smem, hacc);
+#pragma unroll
+    for (int st = 0; st < 6; ++st) hconv(smem, hacc, st, hh, hl);
+  }
+  __syncthreads();                                     // W1 slot 0 read by every wave: free for chunk 2
+  for (int c = 0; c < nch; ++c) {
+    const bool more = c + 1 < nch;
+    if (c + 2 < nch) issue_w1(c + 2, c & 1);
+    if (more) issue_w2(c + 1, (c + 1) & 1);
+    const char* s1n = smem + ((c + 1) & 1) * FH_S1;
+    f32x16 haccn;
+    if (more) phase1(s1n, haccn);
+    else
+#pragma unroll
+      for (int r = 0; r < 16; ++r) haccn[r] = 0.f;
+    phase2(smem + FH_R2 + (c & 1) * FH_W2, hh, hl, more, s1n, haccn, hhn, hln);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) { hh[i] = hhn[i]; hl[i] = hln[i]; }
+    __builtin_amdgcn_s_waitcnt(0);                    // this wave's pieces of W1 c + 2, W2 c + 1
+    __syncthreads();                                   // ... everyone's; the slots read this iteration free
   }
 
   // ---- epilogue: v = acc 2^-e2 / s_h + b2 + x, LayerNorm over the token's 256 columns
   // (lane: token l31, columns 32 j + 8 q + 4 hi + 0..3)
-  const float* ep = reinterpret_cast<const float*>(smem + 2 * FH_SLOT);
+  const float* ep = reinterpret_cast<const float*>(smem + FH_EP);
   const float* xr = (const float*)a.x + (size_t)(rok ? row : 0) * a.ldx;
   float sum = 0.f;
 #pragma unroll

@@ -104,3 +104,17 @@ def test_forward_stage_flags_validated():
         assert L.spe_forward_stages(h, None, images, 1, dummy, 1 << 40, None, stages) == -1
         assert b"not a DETR model" not in L.spe_last_error()
     L.spe_model_destroy(h)
+
+
+def test_ffn_h3_hidden_order_is_a_permutation():
+    """The one-pass fp32h3 FFN's W2 column order (ffn_h3.hip): a permutation of each 32-unit chunk
+    that puts, for K-block kb and lane half h, the hidden units the phase-1 accumulator lane holds
+    (8 (r >> 2) + 4 h + (r & 3), r = 8 kb .. 8 kb + 7) at positions 16 kb + 8 h + 0..7."""
+    L = _lib.lib()
+    perm = [L.spe_debug_ffn_h3_perm(p) for p in range(32)]
+    assert sorted(perm) == list(range(32))
+    for p in range(32):
+        kb, h, e = p // 16, (p // 8) % 2, p % 8
+        r = 8 * kb + e
+        assert perm[p] == 8 * (r // 4) + 4 * h + r % 4
+    assert L.spe_debug_ffn_h3_perm(32) == -1 and L.spe_debug_ffn_h3_perm(-1) == -1
