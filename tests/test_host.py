@@ -337,3 +337,37 @@ def test_ground_truth_area_keeps_reference_precedence():
     g = load_ground_truth([{"filename": "a.jpg", "q_vbs2tango": [1, 0, 0, 0], "r_Vo2To_vbs_true": [0, 0, 10],
                             "bbox_xxyy": [100.0, 200.0, 300.0, 400.0]}])
     assert g["a.jpg"]["area"] == pytest.approx(np.sqrt(200.0 * 400.0 - 200.0))
+
+
+def test_bench_score_contract_against_fp32_spread():
+    """bench.accuracy_summary's score half of the contract: measured against the
+    committed spread of two fp32 implementations (profiles/r5b_precision_score.json) -- met by deltas
+    inside that spread, not met by a wider fraction of misses or a larger worst case."""
+    import importlib.util
+    import numpy as np
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(repo, "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    sp = bench.score_spread("epnp")
+    assert sp is not None and 0.5 < sp["frac"] < 1.0 and sp["max"] > 0.0
+    n = 64
+    rng = np.random.default_rng(3)
+    ref = rng.uniform(0.1, 2.0, n)
+
+    def raw(delta):
+        return {"score_ref": ref, "score": ref + delta, "cond": np.full(n, 1e-6), "d_norm": np.full(10, 3e-5),
+                "d_px": np.full(10, 0.02), "d_per_crop": np.full(10, 3e-5), "hs_rel": np.full(4, 1e-6),
+                "label_agree": np.ones(4), "status_agree": np.ones(n)}
+    good = np.full(n, 1e-5)
+    good[:4] = 2e-3                                    # 94 % within 1e-4, small worst case
+    a = bench.accuracy_summary(raw(good), "epnp")
+    assert a["meets_1e-4_kpt"] and not a["meets_1e-4_score"]
+    assert a["meets_1e-4_score_within_fp32_spread"] and a["meets_1e-4_within_fp32_spread"]
+    bad = np.full(n, 1e-5)
+    bad[: n // 2] = 1e-3                               # half the images outside 1e-4
+    assert not bench.accuracy_summary(raw(bad), "epnp")["meets_1e-4_score_within_fp32_spread"]
+    worst = good.copy()
+    worst[0] = 10.0 * sp["max"]
+    assert not bench.accuracy_summary(raw(worst), "epnp")["meets_1e-4_score_within_fp32_spread"]
+    assert "meets_1e-4_score_within_fp32_spread" not in bench.accuracy_summary(raw(good), None)
