@@ -40,6 +40,7 @@ def main():
     ap.add_argument("--only", default="")
     ap.add_argument("--attn-dtype", type=int, default=0, help="0 bf16, 1 fp32, 2 fp16, 3 bf16 q/k + fp16 V^T/P, 4 fp32x3")
     ap.add_argument("--dma", action="store_true", help="the encoder's LDS-DMA attention kernel (V^T key order as stored)")
+    ap.add_argument("--presplit", action="store_true", help="fp32x3: K and V^T as the bf16 hi / lo planes the models pass")
     a = ap.parse_args()
     L = _lib.lib()
     dev = torch.device("cuda", 0)
@@ -55,7 +56,15 @@ def main():
         o = torch.empty(B * T, D, dtype=torch.float32 if f32 else torch.bfloat16, device=dev)
         kp = ctypes.c_void_p(qk.data_ptr() + 256 * qk.element_size())
         code = a.attn_dtype | (0x100 if a.dma else 0)
-        fn = lambda: L.spe_debug_attention(None, code, p(qk), 512, kp, 512, p(vt), p(o), D, B, H, T, T, 32 ** -0.5)
+        ldk = 512
+        if a.presplit and a.attn_dtype == 4:             # (the planes kept alive in `keep`)
+            kf = qk[:, 256:].contiguous()
+            kh = kf.to(torch.bfloat16)
+            vh = vt.to(torch.bfloat16)
+            keep = [torch.cat([kh.reshape(-1), (kf - kh.float()).to(torch.bfloat16).reshape(-1)]),
+                    torch.cat([vh.reshape(-1), (vt - vh.float()).to(torch.bfloat16).reshape(-1)])]
+            kp, vt, ldk, code = ctypes.c_void_p(keep[0].data_ptr()), keep[1], 256, code | 0x200
+        fn = lambda: L.spe_debug_attention(None, code, p(qk), 512, kp, ldk, p(vt), p(o), D, B, H, T, T, 32 ** -0.5)
         ms = timeit(fn, a.iters)
         fl = 4.0 * B * H * T * T * 32
         print(f"attn.enc  {ms:.3f} ms  {fl / ms / 1e9:.1f} TF/s")
