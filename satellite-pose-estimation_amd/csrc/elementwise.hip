@@ -11,7 +11,7 @@
 
 namespace {
 
-template <typename T>
+template <typename T, int CP = 8>
 __global__ void pack_input_kernel(const float* __restrict__ img, T* __restrict__ out, int B, int S, float* amax) {
   const size_t npx = (size_t)B * S * S;
   float am = 0.f;
@@ -22,6 +22,8 @@ __global__ void pack_input_kernel(const float* __restrict__ img, T* __restrict__
     am = fmaxf(am, fmaxf(fabsf(v[0]), fmaxf(fabsf(v[1]), fabsf(v[2]))));
     if constexpr (sizeof(T) == 2) {
       st16(out + p * 8, pack16<T>(v));
+    } else if constexpr (CP == 4) {
+      st16(out + p * 4, pack16<T>(v));
     } else {
       st16(out + p * 8, pack16<T>(v));
       st16(out + p * 8 + 4, pack16<T>(v + 4));
@@ -285,12 +287,16 @@ inline int grid_for(size_t n, int block) {
 
 }  // namespace
 
-int spe_launch_pack_input(const float* img, void* out, int B, int S, int dtype, hipStream_t s, float* amax) {
+int spe_launch_pack_input(const float* img, void* out, int B, int S, int dtype, hipStream_t s, float* amax, int cpad) {
   const size_t n = (size_t)B * S * S;
   if (dtype == SPE_DTYPE_BF16)
     hipLaunchKernelGGL(pack_input_kernel<bf16>, grid_for(n, 256), 256, 0, s, img, (bf16*)out, B, S, (float*)nullptr);
   else   // (fp32: at most 4096 workgroups, each publishing its max |x| once)
-    hipLaunchKernelGGL(pack_input_kernel<float>, std::min(grid_for(n, 256), 4096), 256, 0, s, img, (float*)out, B, S, amax);
+  {
+    const int grid = std::min(grid_for(n, 256), 4096);
+    if (cpad == 4) hipLaunchKernelGGL((pack_input_kernel<float, 4>), grid, 256, 0, s, img, (float*)out, B, S, amax);
+    else hipLaunchKernelGGL((pack_input_kernel<float, 8>), grid, 256, 0, s, img, (float*)out, B, S, amax);
+  }
   return (int)hipGetLastError();
 }
 

@@ -207,13 +207,14 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   auto slot = [&]() -> float* { return amx ? amx + na++ : nullptr; };
   if (amx) CK((int)hipMemsetAsync(amx, 0, SPE_AMAX_BB * 4, s));
   // ---------------- backbone (REV/models/backbone.py:133-149)
-  const bool pairs = m->stem.Cin == 4;                 // bf16: pair-packed stem (registry.cpp)
+  const bool pairs = m->esz == 2 && m->stem.Cin == 4;  // bf16: pair-packed stem (registry.cpp)
   float* const x0_amax = slot();
   if (pairs)
     CK(run_other(m, "eltwise.pack", 0.0, (double)B * S * S * 12 + (double)B * (S + 6) * (S + 6) * 8, s,
                  [&] { return spe_launch_pack_input_pad4(images, P(w.x0), B, S, s); }));
   else
-    CK(run_other(m, "eltwise.pack", 0.0, (double)B * S * S * (12 + 8 * m->esz), s, [&] { return spe_launch_pack_input(images, P(w.x0), B, S, dt, s, x0_amax); }));
+    CK(run_other(m, "eltwise.pack", 0.0, (double)B * S * S * (12 + m->stem.Cin * m->esz), s,
+                 [&] { return spe_launch_pack_input(images, P(w.x0), B, S, dt, s, x0_amax, m->stem.Cin); }));
   int H = S / 2;
   float* const stem_amax = slot();
   const int Hp = (H + 2 - 3) / 2 + 1;

@@ -456,7 +456,9 @@ int build_device(spe_model* m) {
     c.bias = upload_f32(m, bias.data(), bias.size());
     m->stem = c;
   } else {
-    m->stem = make_conv(m, b + ".conv1.weight", b + ".bn1", "", 8, 2, 3);
+    // fp32 models: 3 channels padded to 4 (K = 7*7*4 = 196: half the 8-channel form's products; the
+    // 16-byte chunk is one pixel); bf16 with SPE_STEM_PAIRS=0: 8 channels (a 16-byte bf16 chunk)
+    m->stem = make_conv(m, b + ".conv1.weight", b + ".bn1", "", m->esz == 4 ? 4 : 8, 2, 3);
   }
   m->blocks.clear();
   const int nblk[3] = {3, 4, 6};

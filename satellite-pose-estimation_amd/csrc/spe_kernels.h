@@ -188,7 +188,9 @@ int spe_ffn_splits(int M, int F);  // split count spe_launch_ffn_ln would use fo
 int spe_launch_preprocess(const uint8_t* frames, int B, int H, int W, int C, const double* bbox, int S,
                           float* images, float* clip_bbox, int32_t* status, hipStream_t s);
 // amax (fp32 output only, nullable): max |image| atomically maxed in (the stem GEMM's fp32h3 scale input)
-int spe_launch_pack_input(const float* img, void* out, int B, int S, int dtype, hipStream_t s, float* amax = nullptr);
+// cpad: channels per packed pixel (8; fp32 models' DETR stem: 4, one 16-byte chunk)
+int spe_launch_pack_input(const float* img, void* out, int B, int S, int dtype, hipStream_t s, float* amax = nullptr,
+                          int cpad = 8);
 // bf16 [B][S+6][S+6][4], zero border of 3 (the pair-packed stem's input, forward.cpp)
 int spe_launch_pack_input_pad4(const float* img, void* out, int B, int S, hipStream_t s);
 // bf16 pair-packed stem (x: spe_launch_pack_input_pad4 layout, w: [64][ldw] k = (kh*8 + kw)*4 + ci)
