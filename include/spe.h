@@ -293,12 +293,12 @@ int spe_debug_gemm_path(void);
  * spe_debug_gemm) with the weights given as the finalize form -- planes = fp16 [2][plane_rows][ldb]
  * holding hi, lo of W[n] * 2^e_n, sinv[n] = 2^-e_n -- and amax_a = device max |A| (nullable: scale
  * 1).  amax_c (nullable): max |stored C| * (amax_c_mul or 1) atomically maxed into it (float bits).
- * ln_g / ln_b (nullable; LINEAR, N == 256): C = LayerNorm(A . W^T + bias + R) (eps 1e-5) from the
- * 256-wide tile's epilogue -- the encoder's out-projection + norm1 and linear2 + norm2 in fp32h3. */
+ * (Round 5 removed its LayerNorm-epilogue form: the model runs the persistent GEMM + the LayerNorm
+ * kernel, measured faster.) */
 int spe_debug_gemm_h3(void* stream, int mode, const void* A, int lda, int H, int W, int Cin, int KH, int KW, int stride,
                       int pad, int ldb, int M, int N, int K, const float* bias, const void* R, int ldr, int act_code,
                       void* C, int ldc, const void* planes, int plane_rows, const float* sinv, const float* amax_a,
-                      float* amax_c, float amax_c_mul, const float* ln_g, const float* ln_b);
+                      float* amax_c, float amax_c_mul);
 /* fp32h3 one-pass encoder FFN (ffn_h3.hip): y = LayerNorm(x + ReLU(x W1^T + b1) W2^T + b2) (eps 1e-5)
  * on fp32 x / y [M][256] (y may be x), F hidden units.  w1 = fp16 [2][F][ld1] hi, lo of W1[j] 2^e1_j;
  * meta1 = [F/32][64] floats: 2^-e1 of the chunk's 32 units, then their b1; w2 = fp16 [2][256][ld2]

@@ -52,7 +52,7 @@ int spe_debug_gemm_planes(void* stream, int dtype, int mode, const void* A, int 
 int spe_debug_gemm_h3(void* stream, int mode, const void* A, int lda, int H, int W, int Cin, int KH, int KW, int stride,
                       int pad, int ldb, int M, int N, int K, const float* bias, const void* R, int ldr, int act_code,
                       void* C, int ldc, const void* planes, int plane_rows, const float* sinv, const float* amax_a,
-                      float* amax_c, float amax_c_mul, const float* ln_g, const float* ln_b) {
+                      float* amax_c, float amax_c_mul) {
   if (!A || !C || !planes || !sinv || M < 0 || N <= 0 || K <= 0) return spe_fail(SPE_E_ARG, "bad argument");
   GemmArgs g{};
   g.A = A; g.lda = lda;
@@ -63,7 +63,6 @@ int spe_debug_gemm_h3(void* stream, int mode, const void* A, int lda, int H, int
   g.bias = bias; g.R = R; g.ldr = ldr; g.act = act_code & 255; g.C = C; g.ldc = ldc;
   g.H3 = planes; g.h3_rows = plane_rows; g.h3_sinv = sinv; g.amax_a = amax_a; g.amax_c = amax_c;
   g.amax_c_mul = amax_c_mul;
-  g.ln_g = ln_g; g.ln_b = ln_b;
   const int rc = spe_launch_gemm(g, SPE_DTYPE_F32H3, mode, (hipStream_t)stream);
   if (rc == 0 && spe_gemm_last_path != 7 && spe_gemm_last_path != 8) return spe_fail(SPE_E_LAUNCH, "shape not served by the fp32h3 kernel");
   return rc < 0 ? spe_fail(SPE_E_LAUNCH, "gemm launch rejected its arguments") : rc;

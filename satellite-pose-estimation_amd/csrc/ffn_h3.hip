@@ -33,7 +33,6 @@ constexpr int FH_R2 = 2 * FH_S1;                // W2 ring: 2 slots of FH_W2 fro
 constexpr int FH_EPI = 4 * FH_D * 4;            // 2^-e2, b2, gamma2, beta2
 constexpr int FH_EP = FH_R2 + 2 * FH_W2;
 constexpr int FH_SMEM = FH_EP + FH_EPI;
-constexpr int FH_BAD = 0x7ffffff0;
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
 SPE_DEV u32x4 h_pack(const float* v) {

@@ -441,7 +441,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       GemmArgs gf = g;
       gf.C = P(w.src); gf.ln_g = e.n1g; gf.ln_b = e.n1b;
       // (fp32h3 runs the persistent GEMM + the LayerNorm kernel: 0.15 + 0.06 ms a layer against 0.31 ms
-      // for gemm_h3d_linear_ln's fused 256-wide tile, which ends every tile cold)
+      // for the fused 256-wide h3 tile with a LayerNorm epilogue, which ended every tile cold; removed)
       if (m->esz == 2 && spe_ln_fusable(gf)) {
         CK(run_gemm(m, "gemm.enc.o", gf, GEMM_LINEAR, s));
       } else {

@@ -1017,15 +1017,11 @@ SPE_DEV void h3_scale(const float* amax, float& sa, float& inv) {
   inv = __builtin_ldexpf(1.f, e - 13);
 }
 
-// LN (FJ = 8, N == 256): one workgroup holds whole 256-wide rows, and the epilogue applies the
-// post-norm LayerNorm (g.ln_g / g.ln_b, eps 1e-5, two-pass variance like layernorm_kernel, after bias
-// and residual) before the store -- the encoder's out-projection + norm1 and linear2 + norm2
-// (REV/models/transformer.py:162-167) in one launch, no fp32 pre-norm round trip through HBM.
-template <int MODE, int FJ, bool PL = false, bool LN = false>
+template <int MODE, int FJ, bool PL = false>
 __device__ __forceinline__ void gemm_h3d_body(const GemmArgs& g) {
   using G = H3Geo<FJ>;
   constexpr int BNH = G::BN, PB = G::PB, STG = G::STAGE, NBQ = G::NBQ, NQ = G::NQ;
-  constexpr int LDL = LN ? BNH + 4 : EPI_LD;            // epilogue tile row stride (floats)
+  constexpr int LDL = EPI_LD;                          // epilogue tile row stride (floats)
   constexpr int SMEM = 2 * STG > H3_BM * LDL * 4 ? 2 * STG : H3_BM * LDL * 4;
   __shared__ __attribute__((aligned(1024))) char smem[SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1201,41 +1197,14 @@ __device__ __forceinline__ void gemm_h3d_body(const GemmArgs& g) {
       ct[(wid * 32 + 8 * (r >> 2) + 4 * hi + (r & 3)) * LDL + 32 * j + l31] = acc[j][r] * cs;
   }
   __syncthreads();
-  if constexpr (LN) {
-    // wave wid normalises rows 32 wid .. +32, one row per step: lane holds columns 4 lane .. +3
-    const f32x4 bb = g.bias ? *reinterpret_cast<const f32x4*>(g.bias + 4 * lane) : f32x4{0.f, 0.f, 0.f, 0.f};
-    const f32x4 ga = *reinterpret_cast<const f32x4*>(g.ln_g + 4 * lane);
-    const f32x4 be = *reinterpret_cast<const f32x4*>(g.ln_b + 4 * lane);
-    for (int rr = 0; rr < 32; ++rr) {
-      const int row = wid * 32 + rr, m = m0 + row;
-      if (m >= g.M) break;
-      float v[4];
-      unpack16<float>(ld16(ct + row * LDL + 4 * lane), v);
+  float bv[8];
+  {
+    const int n = n0 + (tid % (BNH / 8)) * 8;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] += bb[e];
-      if (g.R) {
-        float r4[4];
-        unpack16<float>(ld16((const float*)g.R + (size_t)m * g.ldr + 4 * lane), r4);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] += r4[e];
-      }
-      const float mean = wave_sum(v[0] + v[1] + v[2] + v[3]) * (1.f / BNH);
-      const float d0 = v[0] - mean, d1 = v[1] - mean, d2 = v[2] - mean, d3 = v[3] - mean;
-      const float var = wave_sum(d0 * d0 + d1 * d1 + d2 * d2 + d3 * d3) * (1.f / BNH);
-      const float rs = rsqrtf(var + 1e-5f);
-      float y[4] = {d0 * rs * ga[0] + be[0], d1 * rs * ga[1] + be[1], d2 * rs * ga[2] + be[2], d3 * rs * ga[3] + be[3]};
-      st16((float*)g.C + (size_t)m * g.ldc + 4 * lane, pack16<float>(y));
-    }
-  } else {
-    float bv[8];
-    {
-      const int n = n0 + (tid % (BNH / 8)) * 8;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) bv[e] = (g.bias && n + e < g.N) ? g.bias[n + e] : 0.f;
-    }
-    const float am = store_tile<float, H3_BM, H3_NT, BNH>(g, ct, m0, n0, tid, bv);
-    if (g.amax_c) amax_publish(am, g.amax_c, g.amax_c_mul);
+    for (int e = 0; e < 8; ++e) bv[e] = (g.bias && n + e < g.N) ? g.bias[n + e] : 0.f;
   }
+  const float am = store_tile<float, H3_BM, H3_NT, BNH>(g, ct, m0, n0, tid, bv);
+  if (g.amax_c) amax_publish(am, g.amax_c, g.amax_c_mul);
 }
 
 __global__ __launch_bounds__(H3_NT, 2) void gemm_h3d_linear(GemmArgs g) { gemm_h3d_body<GEMM_LINEAR, 4>(g); }
@@ -1244,7 +1213,6 @@ __global__ __launch_bounds__(H3_NT, 2) void gemm_h3d_conv(GemmArgs g) { gemm_h3d
 __global__ __launch_bounds__(H3_NT, 2) void gemm_h3d_conv_n64(GemmArgs g) { gemm_h3d_body<GEMM_CONV, 2>(g); }
 __global__ __launch_bounds__(H3_NT, 2) void gemm_h3d_conv_pl(GemmArgs g) { gemm_h3d_body<GEMM_CONV, 4, true>(g); }
 __global__ __launch_bounds__(H3_NT, 2) void gemm_h3d_conv_pl_n64(GemmArgs g) { gemm_h3d_body<GEMM_CONV, 2, true>(g); }
-__global__ __launch_bounds__(H3_NT, 1) void gemm_h3d_linear_ln(GemmArgs g) { gemm_h3d_body<GEMM_LINEAR, 8, false, true>(g); }
 
 // Persistent form of gemm_h3d for row-store epilogues (bias, residual / row-periodic residual,
 // activation, fp32 C, max |C|): one workgroup per occupancy slot walks its tiles (round i: tile
@@ -1642,13 +1610,6 @@ int launch_h3d(const GemmArgs& g, int mode, hipStream_t s) {
   } else if ((long long)(g.M + H3_BM) * g.lda * 4 + (long long)g.K * 4 >= LIM) {
     return 1;
   }
-  if (g.ln_g) {                                   // whole 256-wide rows per workgroup + LayerNorm
-    if (mode != GEMM_LINEAR || g.N != 256 || !g.ln_b || g.act || g.vt_T || g.S || g.amax_c || (g.ldc & 3) ||
-        (g.R && (g.ldr & 3)))
-      return -5;
-    if (g.M > 0) hipLaunchKernelGGL(gemm_h3d_linear_ln, dim3((g.M + H3_BM - 1) / H3_BM), dim3(H3_NT), 0, s, g);
-    return (int)hipGetLastError();
-  }
   const bool narrow = g.N <= 64;
   const int bn = narrow ? 64 : 128;
   const int tiles = ((g.M + H3_BM - 1) / H3_BM) * ((g.N + bn - 1) / bn);
@@ -1752,8 +1713,8 @@ int spe_launch_gemm(const GemmArgs& g, int dtype, int mode, hipStream_t s) {
   if (mode == GEMM_CONV && (g.Cin % ce) && !pairs) return -3;
   if (g.ldb % 64) return -4;                                 // weights padded to 64 elements
   if ((g.lda % ce) || (g.ldc % (g.out_f32 ? 4 : ce)) || (g.R && (g.ldr % ce))) return -5;
-  // fused LayerNorm: the large-tile bf16 kernel and the fp32h3 kernel's 256-wide form only
-  if (g.ln_g && dtype != SPE_DTYPE_BF16 && dtype != SPE_DTYPE_F32H3) return -5;
+  // fused LayerNorm: the large-tile bf16 kernel only
+  if (g.ln_g && dtype != SPE_DTYPE_BF16) return -5;
   if (dtype == SPE_DTYPE_BF16) {                 // 256-row tiles when they fill the chip
     spe_gemm_last_path = 1;
     const int rc = spe_launch_gemm2(g, mode, s);
@@ -1765,7 +1726,6 @@ int spe_launch_gemm(const GemmArgs& g, int dtype, int mode, hipStream_t s) {
     spe_gemm_last_path = 7;
     const int rc = launch_h3d(g, mode, s);
     if (rc != 1) return rc;
-    if (g.ln_g) return -5;                       // (the x6 kernels have no LayerNorm epilogue)
     dtype = SPE_DTYPE_F32X6;                     // shapes the h3 kernel does not serve: the x6 path
   }
   if (dtype == SPE_DTYPE_F32X6) {

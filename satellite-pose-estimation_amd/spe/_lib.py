@@ -108,7 +108,7 @@ def lib():
                                         ctypes.POINTER(D)]
     L.spe_debug_gemm.argtypes = [P, I, I, P, I, P, I, I] + [I] * 7 + [P, I, I, I, I, P, P, I, I, P, I, I, I, I, I, P, P, I]
     L.spe_debug_gemm_path.argtypes = []
-    L.spe_debug_gemm_h3.argtypes = [P, I, P, I] + [I] * 7 + [I, I, I, I, P, P, I, I, P, I, P, I, P, P, P, ctypes.c_float, P, P]
+    L.spe_debug_gemm_h3.argtypes = [P, I, P, I] + [I] * 7 + [I, I, I, I, P, P, I, I, P, I, P, I, P, P, P, ctypes.c_float]
     L.spe_debug_ffn_h3.argtypes = [P, P, I, P, I, I, I, P, I, P, P, I, P, P, P, P, P, ctypes.c_float]
     L.spe_debug_ffn_h3_perm.argtypes = [I]
     L.spe_debug_gemm_planes.argtypes = [P, I, I, P, I, P, I, I] + [I] * 7 + [P, I, I, I, I, P, P, I, I, P, I, P, I]

@@ -71,7 +71,7 @@ def main():
                 continue
             if dn == "fp32h3":
                 fn = lambda: L.spe_debug_gemm_h3(None, mode, p(A), K if mode == 0 else 0, *conv, ldb, M, N, K, p(bias),
-                                                 None, 0, 1, p(C), N, p(h3p), N, p(h3s), p(amax_a), None, 0.0, None, None)
+                                                 None, 0, 1, p(C), N, p(h3p), N, p(h3s), p(amax_a), None, 0.0)
             elif dn == "fp32x6bp":
                 fn = lambda: L.spe_debug_gemm_planes(None, dt, mode, p(A), K if mode == 0 else 0, None, 0, 1, *conv, p(W),
                                                      ldb, M, N, K, p(bias), None, 0, 1, p(C), N, p(planes), N)

@@ -903,7 +903,7 @@ def _gemm_h3(mode, A, Wp, M, N, K, lda, C, ldc, bias=None, R=None, ldr=0, relu=0
     amax_c = torch.zeros(1, device=A.device)
     rc = L.spe_debug_gemm_h3(None, mode, _p(A), lda, H, Wd, Cin, KH, KW, stride, pad, Wp.shape[1], M, N, K, _p(bias),
                              _p(R), ldr, relu, _p(C), ldc, _p(planes), Wp.shape[0], _p(sinv), _p(amax_a),
-                             _p(amax_c), 0.0, None, None)
+                             _p(amax_c), 0.0)
     assert rc == 0, L.spe_last_error()
     torch.cuda.synchronize()
     path = L.spe_debug_gemm_path()
@@ -1026,37 +1026,6 @@ def test_gemm_h3_close_to_fp64(gpu_device, case, amp):
     err = _split_gemm_err(gpu_device, case, "fp32h3", amp=amp, want_path=7 if case == "conv3x3" else 8)
     e32 = _split_gemm_err(gpu_device, case, "fp32", amp=amp)
     assert err <= max(1e-6, 2 * e32), (err, e32)
-
-
-@pytest.mark.parametrize("M", [2 * 2704, 1000, 77])
-@pytest.mark.parametrize("K", [256, 2048])
-def test_gemm_h3_layernorm_epilogue(gpu_device, M, K):
-    """fp32h3's 256-wide tile with the post-norm LayerNorm epilogue (the encoder's out-projection +
-    norm1, linear2 + norm2, REV/models/transformer.py:162-167), in place over the residual like the
-    model launches it: within fp32 rounding of LayerNorm(A W^T + b + R) computed in fp64."""
-    L = _lib.lib()
-    N, dev, f = 256, gpu_device, torch.float32
-    g = torch.Generator(device="cpu").manual_seed(M + K)
-    A = torch.randn(M, K, generator=g, dtype=torch.float64)
-    Wt = torch.randn(N, K, generator=g, dtype=torch.float64) / K ** 0.5
-    b = torch.randn(N, generator=g, dtype=torch.float64) * 0.1
-    R = torch.randn(M, N, generator=g, dtype=torch.float64)
-    gam = 1 + 0.1 * torch.randn(N, generator=g, dtype=torch.float64)
-    bet = 0.1 * torch.randn(N, generator=g, dtype=torch.float64)
-    ref = F_.layer_norm(A @ Wt.t() + b + R, (N,), gam, bet, 1e-5)
-    Wp = _padded_weight(Wt.to(dev, f), K, f)
-    planes, sinv = _h3_planes(Wp)
-    Ad = A.to(dev, f)
-    amax_a = Ad.abs().max().reshape(1).contiguous()
-    C = R.to(dev, f).contiguous()                               # in place: C = R
-    bd, gd, btd = b.to(dev, f), gam.to(dev, f), bet.to(dev, f)  # (kept alive across the launch)
-    rc = L.spe_debug_gemm_h3(None, 0, _p(Ad), K, 0, 0, 0, 1, 1, 1, 0, Wp.shape[1], M, N, K, _p(bd), _p(C), N, 0,
-                             _p(C), N, _p(planes), N, _p(sinv), _p(amax_a), None, 0.0, _p(gd), _p(btd))
-    assert rc == 0, L.spe_last_error()
-    torch.cuda.synchronize()
-    assert L.spe_debug_gemm_path() == 7
-    err = (C.double().cpu() - ref).abs().max().item()
-    assert err <= 2e-5, err
 
 
 def _h3_row_planes(W):
