@@ -216,9 +216,12 @@ def test_fp32x6_within_fp32_implementation_spread(gpu_device):
         for name in trace_pairs:
             tab = r["score"][name]["pairs"]
             x6, cpu, gpu = tab[f"{mode}_vs_fp32"], tab["torch_cpu_vs_fp32"], tab["torch_gpu_vs_fp32"]
+            cg = tab["torch_cpu_vs_torch_gpu"]
             assert x6["frac_le_1e-4"] >= cpu["frac_le_1e-4"] - 0.05, (mode, name, tab)
             assert x6["median"] <= 2 * cpu["median"], (mode, name, tab)
-            assert x6["max"] <= max(cpu["max"], gpu["max"]), (mode, name, tab)
+            # the worst image: within the largest disagreement of two fp32 implementations (the maxima
+            # are single ill-conditioned images, so every fp32 pair counts)
+            assert x6["max"] <= max(cpu["max"], gpu["max"], cg["max"]), (mode, name, tab)
 
 
 def _ulp_conditioning(solver, px, probs, q_gt, t_gt, score, dev, draws=16):
