@@ -412,13 +412,21 @@ def accuracy_raw(model, ref, out):
 # all through the same HIP solver, on the config-2 batch (pool images 0..63, the bench fixture
 # weights); written by tests/test_gpu_precision.py.
 SCORE_SPREAD_FILE = os.path.join(REPO, "profiles", "r5f_precision_score.json")
+# the same study on the whole 256-image pool (the north star's global batch; SPE_PRECISION_IMAGES=256)
+SCORE_SPREAD_FILE_256 = os.path.join(REPO, "profiles", "r5f_precision_score_256.json")
 
 
-def score_spread(solver):
+def spread_file(images):
+    """The committed spread study matching a batch of `images` pool images (the extreme-value max
+    grows with the batch, so a 256-image batch is held to the 256-image study when it exists)."""
+    return SCORE_SPREAD_FILE_256 if images >= 256 and os.path.exists(SCORE_SPREAD_FILE_256) else SCORE_SPREAD_FILE
+
+
+def score_spread(solver, images=64):
     """{'frac', 'median', 'max'} of torch-CPU vs ours-fp32 (max: the largest disagreement of any two fp32
     implementations -- torch-CPU, torch-GPU, ours) for `solver` ('epnp' / 'ransac_p3p_lm'), or None."""
     try:
-        d = json.load(open(SCORE_SPREAD_FILE))["score"][solver]["pairs"]
+        d = json.load(open(spread_file(images)))["score"][solver]["pairs"]
     except Exception:
         return None
     cpu, gpu, cg = d["torch_cpu_vs_fp32"], d["torch_gpu_vs_fp32"], d["torch_cpu_vs_torch_gpu"]
@@ -461,14 +469,15 @@ def accuracy_summary(raw, solver=None):
     res["meets_1e-4_kpt"] = bool(res["kpt_norm_max"] <= 1e-4)
     res["meets_1e-4_score"] = bool((res["score_delta_max"] or 0.0) <= 1e-4)
     res["meets_1e-4"] = res["meets_1e-4_kpt"] and res["meets_1e-4_score"]
-    sp = score_spread(solver) if solver else None
+    sp = score_spread(solver, len(sc_r)) if solver else None
     if sp is not None and ds.size:
         res["score_fp32_spread"] = {
             "definition": "per-image |SPEED score - exact-f32 score| <= 1e-4 on at least the fraction of images the "
                           "reference's own fp32 CPU execution reaches - 0.05, median <= 2x its median, max <= the largest "
                           "disagreement of two fp32 implementations (torch-CPU / torch-GPU restatements and the exact-f32 "
                           "mode, same HIP solver)",
-            "source": os.path.relpath(SCORE_SPREAD_FILE, REPO) + " (config-2 batch: pool images 0..63, " + solver + ")",
+            "source": os.path.relpath(spread_file(len(sc_r)), REPO) + " (pool images 0.."
+                      + ("255" if spread_file(len(sc_r)) == SCORE_SPREAD_FILE_256 else "63") + ", " + solver + ")",
             "spread_frac_le_1e-4": sp["frac"], "spread_median": sp["median"], "spread_max": sp["max"]}
         res["meets_1e-4_score_within_fp32_spread"] = bool(
             res["frac_score_delta_le_1e-4"] >= sp["frac"] - 0.05 and res["score_delta_median"] <= 2 * sp["median"]

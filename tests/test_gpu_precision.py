@@ -51,7 +51,9 @@ import torch
 pytestmark = pytest.mark.gpu
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-B = 64
+# pool images 0..B-1: 64 = the config-2 batch (the suite's case); SPE_PRECISION_IMAGES=256 repeats the
+# study on the north star's global batch (the whole pool; gpurun_out/precision_score_256.json)
+B = int(os.environ.get("SPE_PRECISION_IMAGES", "64"))
 
 
 def _kpt(a, b, fg):
@@ -198,9 +200,10 @@ def test_fp32x6_within_fp32_implementation_spread(gpu_device):
 
     out = os.path.join(REPO, "gpurun_out")
     if os.path.isdir(out):
-        with open(os.path.join(out, "precision_score.json"), "w") as f:
+        sfx = "" if B == 64 else f"_{B}"
+        with open(os.path.join(out, f"precision_score{sfx}.json"), "w") as f:
             json.dump(r, f, indent=1)
-        np.savez(os.path.join(out, "precision_keypoints.npz"),
+        np.savez(os.path.join(out, f"precision_keypoints{sfx}.npz"),
                  **{f"{k}_{j}": v[j].cpu().numpy() for k, v in impl.items() for j in range(3)})
     print(json.dumps({k: v for k, v in r.items() if k != "score"}))
     for name, s in r["score"].items():
