@@ -698,9 +698,11 @@ Ws spe_plan(const spe_model* m, int B) {
   const size_t R = 8 * Q, XS = xa ? (size_t)spe_xattn_splits(B, (int)Q, (int)T) : 0;
   w.xq = take(xa ? (size_t)B * Q * 8 * d * E : 0);
   w.xu = take(xa ? (size_t)B * Q * 8 * d * E : 0);
-  w.xpm = take(XS > 1 ? XS * B * R * 4 : 0);
-  w.xpl = take(XS > 1 ? XS * B * R * 4 : 0);
-  w.xpu = take(XS > 1 ? XS * B * R * d * 4 : 0);
+  // (the cross-attention writes its per-split partials for every split count, 1 included: from
+  // B = 256 on a single split covers the chip, and unallocated partials aliased tgt -- NaN decoder)
+  w.xpm = take(xa ? XS * B * R * 4 : 0);
+  w.xpl = take(xa ? XS * B * R * 4 : 0);
+  w.xpu = take(xa ? XS * B * R * d * 4 : 0);
   w.tgt = take((size_t)B * Q * d * E);
   w.dtmp = take((size_t)B * Q * d * E);
   w.dqkv = take((size_t)B * Q * 3 * d * E);

@@ -138,6 +138,25 @@ def test_forward_bf16_batch_independence_full_size(gpu_device, input_size, nq, b
         assert np.abs(full[k][lo:] - p).max() <= tol, k
 
 
+@pytest.mark.parametrize("batch", [256, 300])
+def test_forward_bf16_large_batch_single_xattn_split(gpu_device, batch):
+    """From B = 256 on the decoder cross-attention against the memory runs one key split per image
+    (spe_xattn_splits); its partials must still have workspace of their own (they once aliased tgt and
+    the decoder output went NaN at B >= 256 -- the north star's global batch on one GPU).  The first
+    images of a large batch stay within the bf16 bounds of the same images at B = 8."""
+    cfg = SpeConfig(input_size=128, num_queries=11, enc_layers=2, dec_layers=2)
+    m = _model(cfg, "bf16", 11, None)
+    b = synthetic_batch(cfg, batch, 77)
+    img = torch.from_numpy(b["images"]).to(gpu_device)
+    big = m(img)
+    small = m(img[:8].contiguous())
+    torch.cuda.synchronize()
+    for k, tol in (("pred_points", 2e-2), ("pred_logits", 0.25)):
+        x = big[k].cpu().numpy()
+        assert np.isfinite(x).all(), k
+        assert np.abs(x[:8] - small[k].cpu().numpy()).max() <= tol, k
+
+
 def _solve(mode, pts, probs, sig, repro=20.0):
     from spe.solver import PoseSolver
     s = PoseSolver(mode=mode, repro=repro)

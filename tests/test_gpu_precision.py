@@ -111,7 +111,10 @@ def test_fp32x6_within_fp32_implementation_spread(gpu_device):
         torch.backends.cuda.matmul.allow_tf32 = torch.backends.cudnn.allow_tf32 = False
         try:
             with torch.no_grad():
-                outs = [model_ref.forward(images[i:i + 16], w, cfg) for i in range(0, len(images), 16)]
+                outs = []
+                for i in range(0, len(images), 16):       # (progress lines: a long CPU pass stays visible)
+                    outs.append(model_ref.forward(images[i:i + 16], w, cfg))
+                    print(f"torch {device}: {i + 16}/{len(images)} images", flush=True)
         finally:
             torch.backends.cuda.matmul.allow_tf32, torch.backends.cudnn.allow_tf32 = mm, cv
         lg = torch.cat([o["pred_logits"] for o in outs]).float().cpu()
