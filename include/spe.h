@@ -362,6 +362,25 @@ int spe_debug_decsa(void* stream, void* tgt, int ldt, int B, int Q, const void* 
  * Q <= 64 (one workgroup per image). */
 int spe_debug_decproj(void* stream, void* tgt, int ldt, const void* x, int ldx, int B, int Q, const void* wo, int ldo,
                       const float* bo, const float* g, const float* b);
+/* decxproj (bf16 only, decsa.hip, ABI 7 addition): the cross-attention's tail in place over tgt:
+ * merges the key-split partials spe_debug_xattn left in partial_scratch (same B, Q, T, splits),
+ * o[b*Q+q][h*32 + j] = wv[h*32 + j] . u_h + bv[h*32 + j] rounded to bf16, then
+ * tgt = LayerNorm(tgt + o . wo^T + bo) -- xattn's merge kernel and decproj as one launch, Q <= 16. */
+int spe_debug_decxproj(void* stream, void* tgt, int ldt, float* partial_scratch, int splits, int T, int B, int Q,
+                       const void* wv, int ldwv, const float* bv, const void* wo, int ldo, const float* bo,
+                       const float* g, const float* b);
+/* The decoder kernels (decsa, decproj, decxproj) read fragment-packed weights: bf16 rows
+ * w [N][ld] (K = 256, N % 16 == 0) -> dst [N/16][8][64][8], lane l's A fragment of column tile t,
+ * K-step ks at ((t*8 + ks)*64 + l)*8 (ABI 7 addition).  Their hooks take row-major weights with
+ * ld > 0 (packed into scratch per call) or packed ones with ld == 0. */
+int spe_debug_wfrag_pack(void* stream, const void* w, int ld, int N, void* dst);
+/* decffn (bf16, decsa.hip + ffn.hip's reduce, ABI 7 addition): y [M][ldy] = LayerNorm(x + W2
+ * relu(W1 x + b1) + b2) for few rows, d = 256, F % 256 == 0, through fp32 partials
+ * [F/256][M][256]; x and y may alias.  w1 [F][ld1], w2 [256][ld2] row-major (or packed with ld 0:
+ * w1 as spe_debug_wfrag_pack of [F] rows, w2 per 256-wide chunk of columns at chunk * 256 * 256). */
+int spe_debug_decffn(void* stream, const void* x, int ldx, int M, int F, const void* w1, int ld1, const float* b1,
+                     const void* w2, int ld2, const float* b2, const float* gamma, const float* beta, void* y, int ldy,
+                     float* partial);
 /* the K-column order btail's second product expects: stored column k holds channel perm(k) */
 int spe_debug_btail_perm(int k);
 /* stempool (bf16, stempool.hip): out [B][Po][Po] rows of stride ldo (Po = S/4 for S % 4 == 0) =

@@ -142,23 +142,104 @@ int spe_debug_btail(void* stream, const void* a, int lda, int k1, const void* r,
   return rc != 0 ? spe_fail(SPE_E_LAUNCH, "btail launch rejected its arguments") : 0;
 }
 
+// The decoder kernels read fragment-packed weights (spe_launch_wfrag_pack).  The hooks take
+// row-major rows (ld > 0) and pack them into scratch of their own, released after the launch has
+// completed, or already-packed weights (ld == 0, spe_debug_wfrag_pack: timing loops).
+namespace {
+struct Frags {
+  std::vector<void*> bufs;
+  hipStream_t s;
+  int err = 0;
+  explicit Frags(hipStream_t st) : s(st) {}
+  const void* get(const void* w, int ld, int N) {
+    if (ld == 0 || !w) return w;
+    void* p = nullptr;
+    if (hipMalloc(&p, (size_t)N * 256 * 2) != hipSuccess) { err = 1; return nullptr; }
+    bufs.push_back(p);
+    if (spe_launch_wfrag_pack(w, ld, N, p, s) != 0) err = 1;
+    return p;
+  }
+  ~Frags() {
+    if (bufs.empty()) return;
+    (void)hipStreamSynchronize(s);
+    for (void* p : bufs) (void)hipFree(p);
+  }
+};
+}  // namespace
+
+int spe_debug_wfrag_pack(void* stream, const void* w, int ld, int N, void* dst) {
+  const int rc = spe_launch_wfrag_pack(w, ld, N, dst, (hipStream_t)stream);
+  return rc != 0 ? spe_fail(SPE_E_ARG, "wfrag_pack: bad argument") : 0;
+}
+
 int spe_debug_decsa(void* stream, void* tgt, int ldt, int B, int Q, const void* wqk, int ldqk, const float* bqk,
                     const void* wv, int ldv, const float* bv, const void* qpos, const void* wo, int ldo,
                     const float* bo, const float* g, const float* b, float scale) {
+  Frags f((hipStream_t)stream);
   DecSaArgs a{};
   a.tgt = tgt; a.ldt = ldt; a.B = B; a.Q = Q;
-  a.wqk = wqk; a.ldqk = ldqk; a.bqk = bqk; a.wv = wv; a.ldv = ldv; a.bv = bv; a.qpos = qpos;
-  a.wo = wo; a.ldo = ldo; a.bo = bo; a.g = g; a.b = b; a.scale = scale;
+  a.wqk = f.get(wqk, ldqk, 512); a.bqk = bqk; a.wv = f.get(wv, ldv, 256); a.bv = bv; a.qpos = qpos;
+  a.wo = f.get(wo, ldo, 256); a.bo = bo; a.g = g; a.b = b; a.scale = scale;
+  if (f.err) return spe_fail(SPE_E_ARG, "decsa: weight packing failed");
   const int rc = spe_launch_decsa(a, (hipStream_t)stream);
   return rc != 0 ? spe_fail(SPE_E_LAUNCH, "decsa launch rejected its arguments") : 0;
 }
 
 int spe_debug_decproj(void* stream, void* tgt, int ldt, const void* x, int ldx, int B, int Q, const void* wo, int ldo,
                       const float* bo, const float* g, const float* b) {
+  Frags f((hipStream_t)stream);
   DecProjArgs a{};
-  a.tgt = tgt; a.ldt = ldt; a.x = x; a.ldx = ldx; a.B = B; a.Q = Q; a.wo = wo; a.ldo = ldo; a.bo = bo; a.g = g; a.b = b;
+  a.tgt = tgt; a.ldt = ldt; a.x = x; a.ldx = ldx; a.B = B; a.Q = Q; a.wo = f.get(wo, ldo, 256); a.bo = bo;
+  a.g = g; a.b = b;
+  if (f.err) return spe_fail(SPE_E_ARG, "decproj: weight packing failed");
   const int rc = spe_launch_decproj(a, (hipStream_t)stream);
   return rc != 0 ? spe_fail(SPE_E_LAUNCH, "decproj launch rejected its arguments") : 0;
+}
+
+int spe_debug_decxproj(void* stream, void* tgt, int ldt, float* partial_scratch, int splits, int T, int B, int Q,
+                       const void* wv, int ldwv, const float* bv, const void* wo, int ldo, const float* bo,
+                       const float* g, const float* b) {
+  if (!partial_scratch || T < 1 || B < 0 || Q < 1) return spe_fail(SPE_E_ARG, "bad argument");
+  Frags f((hipStream_t)stream);
+  DecProjArgs a{};
+  a.tgt = tgt; a.ldt = ldt; a.B = B; a.Q = Q; a.wo = f.get(wo, ldo, 256); a.bo = bo; a.g = g; a.b = b;
+  const int req = splits > 0 ? splits : spe_xattn_splits(B, Q, T);
+  const size_t rows = (size_t)req * B * 8 * Q;  // spe_debug_xattn's scratch layout
+  a.pm = partial_scratch; a.pl = partial_scratch + rows; a.pu = partial_scratch + 2 * rows;
+  a.splits = spe_xattn_launch_splits(T, req);
+  a.wv = f.get(wv, ldwv, 256); a.bv = bv;
+  if (f.err) return spe_fail(SPE_E_ARG, "decxproj: weight packing failed");
+  const int rc = spe_launch_decproj(a, (hipStream_t)stream);
+  return rc != 0 ? spe_fail(SPE_E_LAUNCH, "decxproj launch rejected its arguments") : 0;
+}
+
+int spe_debug_decffn(void* stream, const void* x, int ldx, int M, int F, const void* w1, int ld1, const float* b1,
+                     const void* w2, int ld2, const float* b2, const float* gamma, const float* beta, void* y, int ldy,
+                     float* partial) {
+  if (!x || !w1 || !w2 || !y || !partial || M < 0 || F < 256 || F % 256) return spe_fail(SPE_E_ARG, "bad argument");
+  Frags f((hipStream_t)stream);
+  DecFfnArgs a{};
+  a.x = x; a.ldx = ldx; a.M = M; a.F = F; a.b1 = b1; a.partial = partial;
+  a.w1 = f.get(w1, ld1, F);
+  if (ld2 == 0) {
+    a.w2 = w2;
+  } else {                                      // W2 packed per 256-wide hidden chunk
+    void* p = nullptr;
+    if (hipMalloc(&p, (size_t)256 * F * 2) != hipSuccess) return spe_fail(SPE_E_ARG, "decffn: scratch");
+    f.bufs.push_back(p);
+    for (int c0 = 0; c0 < F; c0 += 256)
+      if (spe_launch_wfrag_pack((const char*)w2 + (size_t)c0 * 2, ld2, 256, (char*)p + (size_t)c0 * 256 * 2,
+                                (hipStream_t)stream))
+        f.err = 1;
+    a.w2 = p;
+  }
+  if (f.err) return spe_fail(SPE_E_ARG, "decffn: weight packing failed");
+  FfnArgs r{};
+  r.x = x; r.ldx = ldx; r.y = y; r.ldy = ldy; r.M = M; r.D = 256; r.F = F;
+  r.b2 = b2; r.gamma = gamma; r.beta = beta; r.splits = F / 256; r.partial = partial;
+  int rc = spe_launch_decffn(a, (hipStream_t)stream);
+  if (!rc) rc = spe_launch_ffn_reduce_ln(r, (hipStream_t)stream);
+  return rc != 0 ? spe_fail(SPE_E_LAUNCH, "decffn launch rejected its arguments") : 0;
 }
 
 int spe_debug_btail_perm(int k) { return spe_btail_perm(k); }

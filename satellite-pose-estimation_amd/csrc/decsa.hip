@@ -29,18 +29,20 @@ constexpr int XLD = D + 8;                 // x rows in LDS (bf16 elements): 528
 constexpr int QKVLD = 3 * D + 8;           // q | k | v rows (bf16): 1552 B
 constexpr int YLD = D + 4;                 // fp32 rows before the LayerNorm
 
-// W fragments of one 16-column tile (A operand of the C^T form): lane l holds row n0 + (l & 15),
-// k 8 (l >> 4) .. +8 of each of the 8 32-wide K steps.  All of a wave's tiles are fetched before
-// the first MFMA (the few rows give each tile only RT x 8 MFMAs: the L2 round trip is the cost).
-SPE_DEV void w_frags(u32x4 (&wf)[8], const bf16* w, int ldw, int n0, int lane) {
-  const bf16* wp = w + (size_t)(n0 + (lane & 15)) * ldw + 8 * (lane >> 4);
+// W fragments of one 16-column tile (A operand of the C^T form): lane l holds row 16 t + (l & 15),
+// k 8 (l >> 4) .. +8 of each of the 8 32-wide K steps.  The weights are stored fragment-packed
+// (spe_launch_wfrag_pack), so each K-step is one contiguous 1 KB wave load; from row-major rows
+// every lane of a load sat on its own 128-byte line, 16 lines per 16 lanes.  All of a wave's tiles
+// are fetched before the first MFMA (the few rows give each tile only RT x 8 MFMAs).
+SPE_DEV void w_frags(u32x4 (&wf)[8], const void* w, int tile, int lane) {
+  const bf16* wp = (const bf16*)w + ((size_t)tile * 8 * 64 + lane) * 8;
 #pragma unroll
-  for (int ks = 0; ks < 8; ++ks) wf[ks] = ld16(wp + 32 * ks);
+  for (int ks = 0; ks < 8; ++ks) wf[ks] = ld16(wp + 512 * ks);
 }
 // D^T tile (16 output columns x 16 rows m0..) = W . x[m0..]^T over K = 256; B = x row m0 + (l & 15)
-SPE_DEV f32x4 tile_wx(const u32x4 (&wf)[8], const bf16* xs, int xld, int m0, int lane) {
+SPE_DEV f32x4 tile_wx(const u32x4 (&wf)[8], const bf16* xs, int xld, int m0, int lane,
+                      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f}) {
   const bf16* xp = xs + (m0 + (lane & 15)) * xld + 8 * (lane >> 4);
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < 8; ++ks)
     acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, wf[ks]),
@@ -66,7 +68,7 @@ __global__ __launch_bounds__(NT) void decsa_kernel(DecSaArgs a) {
   for (int j = 0; j < CT1; ++j) {
     const int n0 = tile1(j) * 16;
     const bool isv = n0 >= 2 * D;
-    w_frags(wf1[j], isv ? (const bf16*)a.wv : (const bf16*)a.wqk, isv ? a.ldv : a.ldqk, isv ? n0 - 2 * D : n0, lane);
+    w_frags(wf1[j], isv ? a.wv : a.wqk, (isv ? n0 - 2 * D : n0) / 16, lane);
   }
   // tgt rows -> LDS (rows past Q zero)
   for (int i = tid; i < RT * 16 * (D / 8); i += NT) {
@@ -99,7 +101,7 @@ __global__ __launch_bounds__(NT) void decsa_kernel(DecSaArgs a) {
   constexpr int CT3 = D / 16 / NW;
   u32x4 wf3[CT3][8];
 #pragma unroll
-  for (int j = 0; j < CT3; ++j) w_frags(wf3[j], (const bf16*)a.wo, a.ldo, (wid * CT3 + j) * 16, lane);
+  for (int j = 0; j < CT3; ++j) w_frags(wf3[j], a.wo, wid * CT3 + j, lane);
   __syncthreads();
 
   // ---- 2. attention: four lanes per (query i, head h), 8 of the head's 32 dims each (the score's
@@ -204,7 +206,7 @@ __global__ __launch_bounds__(NT) void decproj_kernel(DecProjArgs a) {
   constexpr int CT3 = D / 16 / NW;
   u32x4 wf[CT3][8];
 #pragma unroll
-  for (int j = 0; j < CT3; ++j) w_frags(wf[j], (const bf16*)a.wo, a.ldo, (wid * CT3 + j) * 16, lane);
+  for (int j = 0; j < CT3; ++j) w_frags(wf[j], a.wo, wid * CT3 + j, lane);
   for (int i = tid; i < RT * 16 * (D / 8); i += NT) {
     const int r = i / (D / 8), c = i % (D / 8);
     st16(xs + r * XLD + 8 * c, r < Q ? ld16(xg + (size_t)r * a.ldx + 8 * c) : u32x4{0, 0, 0, 0});
@@ -245,11 +247,144 @@ __global__ __launch_bounds__(NT) void decproj_kernel(DecProjArgs a) {
   }
 }
 
+// The cross-attention's tail and its out-projection + norm2 as one launch per layer (Q <= 16):
+//   u_h = the key-split merge of xattn.hip's partials, o_h = Wv_h u_h + bv_h rounded to bf16 (the
+//   rounding the separate merge kernel stored), tgt = LayerNorm(tgt + o . Wo^T + bo)
+// (REV/models/transformer.py:230-234) -- xattn's merge + value-projection kernel and decproj as one
+// launch, u never leaving LDS.  u enters the value projection's bf16 MFMAs as hi + lo planes (u to
+// about 2^-17 relative, as the separate kernel's fp32 FMAs had it).
+constexpr int QX = 16, ULD = 8 * D + 8;    // u planes [16][2048 + 8] bf16: 4112 B rows, conflict-free b128 reads
+constexpr float XNEG = -1.0e30f;
+__global__ __launch_bounds__(NT) void decxproj_kernel(DecProjArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16 uh[QX * ULD];
+  __shared__ __attribute__((aligned(16))) bf16 ul[QX * ULD];
+  __shared__ __attribute__((aligned(16))) bf16 rs[QX * XLD];    // tgt rows (the residual)
+  __shared__ __attribute__((aligned(16))) bf16 xs[QX * XLD];    // o rows
+  __shared__ float sm[8 * QX], sil[8 * QX];
+  float* ys = reinterpret_cast<float*>(uh);                      // fp32 rows once u has been read
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int b = blockIdx.x, Q = a.Q, R = 8 * Q, S = a.splits;
+  bf16* tg = (bf16*)a.tgt + (size_t)b * Q * a.ldt;
+  // wave wid: head wid of the value projection and columns 32 wid .. +32 of the out-projection;
+  // both sets of W fragments travel while the partials are merged
+  u32x4 wvf[2][8], wf[2][8];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    w_frags(wvf[j], a.wv, 2 * wid + j, lane);
+    w_frags(wf[j], a.wo, 2 * wid + j, lane);
+  }
+  f32x4 bvv[2], bov[2];                         // biases and the LayerNorm affine: loaded up front too
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    bvv[j] = *reinterpret_cast<const f32x4*>(a.bv + 32 * wid + 16 * j + 4 * (lane >> 4));
+    bov[j] = *reinterpret_cast<const f32x4*>(a.bo + 32 * wid + 16 * j + 4 * (lane >> 4));
+  }
+  const f32x4 gm = *reinterpret_cast<const f32x4*>(a.g + 4 * lane);
+  const f32x4 bt = *reinterpret_cast<const f32x4*>(a.b + 4 * lane);
+  for (int i = tid; i < QX * (D / 8); i += NT) {
+    const int r = i / (D / 8), c = i % (D / 8);
+    st16(rs + r * XLD + 8 * c, r < Q ? ld16(tg + (size_t)r * a.ldt + 8 * c) : u32x4{0, 0, 0, 0});
+  }
+  for (int i = tid; i < (QX - Q) * D; i += NT) {   // u rows past Q: zero (8 x 256 values = 256 chunks a row)
+    const int r = Q + i / D, c = i % D;
+    st16(uh + r * ULD + 8 * c, u32x4{0, 0, 0, 0});
+    st16(ul + r * ULD + 8 * c, u32x4{0, 0, 0, 0});
+  }
+  // 1. per attention row r = 8 q + h: M = max_s m_s and 1 / sum_s 2^(m_s - M) l_s
+  const size_t base = (size_t)b * S * R;
+  if (tid < R) {
+    float M = XNEG;
+    for (int s = 0; s < S; ++s) M = fmaxf(M, a.pm[base + (size_t)s * R + tid]);
+    float L = 0.f;
+    for (int s = 0; s < S; ++s) {
+      const size_t pr = base + (size_t)s * R + tid;
+      L += __builtin_amdgcn_exp2f(a.pm[pr] - M) * a.pl[pr];
+    }
+    sm[tid] = M;
+    sil[tid] = 1.f / L;
+  }
+  __syncthreads();
+  // 2. u = sum_s 2^(m_s - M) U_s / L, 16 dims an item, into row q, columns 256 h .. of the planes
+  for (int it = tid; it < R * 16; it += NT) {
+    const int r = it >> 4, c = it & 15;
+    const float M = sm[r];
+    const float* pmr = a.pm + base + r;
+    const float* pur = a.pu + (base + r) * D + 16 * c;
+    f32x4 u[4] = {};
+#pragma unroll 2
+    for (int s = 0; s < S; ++s) {
+      const float w = __builtin_amdgcn_exp2f(pmr[(size_t)s * R] - M);
+      const f32x4* p = reinterpret_cast<const f32x4*>(pur + (size_t)s * R * D);
+#pragma unroll
+      for (int g = 0; g < 4; ++g) u[g] += w * p[g];
+    }
+    const float il = sil[r];
+    uint32_t hi[8], lo[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float x0 = u[e >> 1][2 * (e & 1)] * il, x1 = u[e >> 1][2 * (e & 1) + 1] * il;
+      hi[e] = pack_bf16x2(x0, x1);
+      lo[e] = pack_bf16x2(x0 - __uint_as_float(hi[e] << 16), x1 - __uint_as_float(hi[e] & 0xffff0000u));
+    }
+    const int off = (r >> 3) * ULD + (r & 7) * D + 16 * c;
+    st16(uh + off, u32x4{hi[0], hi[1], hi[2], hi[3]});
+    st16(uh + off + 8, u32x4{hi[4], hi[5], hi[6], hi[7]});
+    st16(ul + off, u32x4{lo[0], lo[1], lo[2], lo[3]});
+    st16(ul + off + 8, u32x4{lo[4], lo[5], lo[6], lo[7]});
+  }
+  __syncthreads();
+  // 3. o_h = Wv_h (u_hi + u_lo) + bv_h, bf16 rows into xs
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n0 = 32 * wid + 16 * j;
+    f32x4 acc = tile_wx(wvf[j], uh + wid * D, ULD, 0, lane);
+    acc = tile_wx(wvf[j], ul + wid * D, ULD, 0, lane, acc);
+    const f32x4 bias = bvv[j];
+    st8(xs + (lane & 15) * XLD + n0 + 4 * (lane >> 4),
+        u32x2{pack_bf16x2(acc[0] + bias[0], acc[1] + bias[1]), pack_bf16x2(acc[2] + bias[2], acc[3] + bias[3])});
+  }
+  __syncthreads();                              // o visible; u dead (ys reuses its plane)
+  // 4. out-projection + bo + residual, then the LayerNorm (decproj's phases)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n0 = 32 * wid + 16 * j;
+    const f32x4 bias = bov[j];
+    f32x4 acc = tile_wx(wf[j], xs, XLD, 0, lane);
+    const int m = lane & 15;
+    const u32x2 r = ld8(rs + m * XLD + n0 + 4 * (lane >> 4));
+    acc[0] += bias[0] + __uint_as_float(r.x << 16);
+    acc[1] += bias[1] + __uint_as_float(r.x & 0xffff0000u);
+    acc[2] += bias[2] + __uint_as_float(r.y << 16);
+    acc[3] += bias[3] + __uint_as_float(r.y & 0xffff0000u);
+    *reinterpret_cast<f32x4*>(ys + m * YLD + n0 + 4 * (lane >> 4)) = acc;
+  }
+  __syncthreads();
+  for (int m = wid; m < Q; m += NW) {
+    const f32x4 y = *reinterpret_cast<const f32x4*>(ys + m * YLD + 4 * lane);
+    const float mean = wave_sum((y[0] + y[1]) + (y[2] + y[3])) * (1.f / D);
+    float q = 0.f;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) q += (y[e] - mean) * (y[e] - mean);
+    const float rsd = rsqrtf(wave_sum(q) * (1.f / D) + 1e-5f);
+    float o[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) o[e] = (y[e] - mean) * rsd * gm[e] + bt[e];
+    st8(tg + (size_t)m * a.ldt + 4 * lane, u32x2{pack_bf16x2(o[0], o[1]), pack_bf16x2(o[2], o[3])});
+  }
+}
+
 }  // namespace
 
 int spe_launch_decproj(const DecProjArgs& a, hipStream_t s) {
   if (a.B <= 0) return 0;
-  if (a.Q < 1 || a.Q > QMAX || a.ldt % 8 || a.ldx % 8 || a.ldo % 8 || !a.tgt || !a.x || !a.wo || !a.bo || !a.g || !a.b)
+  if (a.pm) {                                   // the merge form (x comes from the partials)
+    if (a.Q < 1 || a.Q > QX || a.splits < 1 || a.ldt % 8 || !a.pl || !a.pu || !a.wv ||
+        !a.bv || !a.tgt || !a.wo || !a.bo || !a.g || !a.b)
+      return 1;
+    hipLaunchKernelGGL(decxproj_kernel, dim3(a.B), dim3(NT), 0, s, a);
+    return (int)hipGetLastError();
+  }
+  if (a.Q < 1 || a.Q > QMAX || a.ldt % 8 || a.ldx % 8 || !a.tgt || !a.x || !a.wo || !a.bo || !a.g || !a.b)
     return 1;
   hipLaunchKernelGGL(decproj_kernel, dim3(a.B), dim3(NT), 0, s, a);
   return (int)hipGetLastError();
@@ -258,9 +393,75 @@ int spe_launch_decproj(const DecProjArgs& a, hipStream_t s) {
 // 1 = not applicable (the caller runs the separate launches)
 int spe_launch_decsa(const DecSaArgs& a, hipStream_t s) {
   if (a.B <= 0) return 0;
-  if (a.Q < 1 || a.Q > QMAX || a.ldt % 8 || a.ldqk % 8 || a.ldv % 8 || a.ldo % 8 || !a.tgt || !a.wqk || !a.wv ||
+  if (a.Q < 1 || a.Q > QMAX || a.ldt % 8 || !a.tgt || !a.wqk || !a.wv ||
       !a.wo || !a.bqk || !a.bv || !a.bo || !a.qpos || !a.g || !a.b)
     return 1;
   hipLaunchKernelGGL(decsa_kernel, dim3(a.B), dim3(NT), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+namespace {
+// The decoder FFN's split-F product for few rows (bf16, d = 256; REV/models/transformer.py:236-238):
+// workgroup (16-row tile, 256-wide hidden chunk c): H = relu(x . W1c^T + b1c) rounded to bf16 (the
+// rounding ffn.hip's hidden has), partial_c = H . W2c^T in fp32; ffn.hip's reduce kernel then
+// writes y = LN(x + sum_c partial_c + b2).  B.Q = 704 rows give 44 x 8 = 352 workgroups, each
+// with its 256 KB of weight fragments in flight from the start (the 128-row split-F tiles of
+// ffn.hip ran 48 workgroups through an 8-step chunk loop).  W1 fragment-packed as [F] rows, W2
+// per chunk (columns 256 c .. of [256][F] packed as a [256][256] block).
+__global__ __launch_bounds__(NT) void decffn_kernel(DecFfnArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16 xs[16 * XLD];
+  __shared__ __attribute__((aligned(16))) bf16 hs[16 * XLD];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nc = a.F / D, c = blockIdx.x % nc, r0 = (blockIdx.x / nc) * 16;
+  u32x4 w1f[2][8], w2f[2][8];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    w_frags(w1f[j], a.w1, 16 * c + 2 * wid + j, lane);
+    w_frags(w2f[j], (const bf16*)a.w2 + (size_t)c * D * D, 2 * wid + j, lane);
+  }
+  f32x4 b1v[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) b1v[j] = *reinterpret_cast<const f32x4*>(a.b1 + D * c + 32 * wid + 16 * j + 4 * (lane >> 4));
+  if (tid < 16 * (D / 8)) {
+    const int r = tid / (D / 8), q = tid % (D / 8);
+    st16(xs + r * XLD + 8 * q, r0 + r < a.M ? ld16((const bf16*)a.x + (size_t)(r0 + r) * a.ldx + 8 * q) : u32x4{0, 0, 0, 0});
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const f32x4 acc = tile_wx(w1f[j], xs, XLD, 0, lane);
+    float h[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) h[e] = fmaxf(acc[e] + b1v[j][e], 0.f);
+    st8(hs + (lane & 15) * XLD + 32 * wid + 16 * j + 4 * (lane >> 4),
+        u32x2{pack_bf16x2(h[0], h[1]), pack_bf16x2(h[2], h[3])});
+  }
+  __syncthreads();
+  const int m = r0 + (lane & 15);
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const f32x4 acc = tile_wx(w2f[j], hs, XLD, 0, lane);
+    if (m < a.M) *reinterpret_cast<f32x4*>(a.partial + ((size_t)c * a.M + m) * D + 32 * wid + 16 * j + 4 * (lane >> 4)) = acc;
+  }
+}
+
+__global__ __launch_bounds__(256) void wfrag_pack_kernel(const bf16* w, int ld, int N, bf16* dst) {
+  const int i = blockIdx.x * 256 + threadIdx.x;   // one 16-byte fragment: (tile, K-step, lane)
+  if (i >= N * 32) return;
+  const int l = i & 63, ks = (i >> 6) & 7, t = i >> 9;
+  st16(dst + (size_t)i * 8, ld16(w + (size_t)(16 * t + (l & 15)) * ld + 32 * ks + 8 * (l >> 4)));
+}
+}  // namespace
+
+int spe_launch_wfrag_pack(const void* w, int ld, int N, void* dst, hipStream_t s) {
+  if (!w || !dst || N < 16 || N % 16 || ld < D || ld % 8) return -5;
+  hipLaunchKernelGGL(wfrag_pack_kernel, dim3((N * 32 + 255) / 256), dim3(256), 0, s, (const bf16*)w, ld, N, (bf16*)dst);
+  return (int)hipGetLastError();
+}
+
+int spe_launch_decffn(const DecFfnArgs& a, hipStream_t s) {
+  if (a.M <= 0) return 0;
+  if (!a.x || !a.w1 || !a.b1 || !a.w2 || !a.partial || a.F < D || a.F % D || a.ldx % 8) return -5;
+  hipLaunchKernelGGL(decffn_kernel, dim3(((a.M + 15) / 16) * (a.F / D)), dim3(NT), 0, s, a);
   return (int)hipGetLastError();
 }

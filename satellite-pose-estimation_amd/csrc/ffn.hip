@@ -573,6 +573,14 @@ int spe_ffn_splits(int M, int F) {
   return s;
 }
 
+int spe_launch_ffn_reduce_ln(const FfnArgs& a, hipStream_t s) {
+  if (a.M <= 0) return 0;
+  if (a.D != D || !a.partial || a.splits < 1 || a.ldx % 8 || a.ldy % 8 || (a.ypos && (!a.pos || a.pos_period <= 0)))
+    return -5;
+  hipLaunchKernelGGL(ffn_reduce_ln_kernel, dim3((a.M + 3) / 4), dim3(256), 0, s, a);
+  return (int)hipGetLastError();
+}
+
 int spe_launch_ffn_ln(const FfnArgs& a0, hipStream_t s) {
   FfnArgs a = a0;
   a.row0 = 0;

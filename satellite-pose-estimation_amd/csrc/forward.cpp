@@ -527,12 +527,12 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   // LayerNorm: at these few rows (B.Q) lnproj's one-workgroup-per-8-tiles form measured slower
   // (24 vs 18 us a layer: 6 workgroups each staging all of W)
   static const bool decproj_on = [] { const char* e = getenv("SPE_DECPROJ"); return e ? atoi(e) != 0 : true; }();
-  auto dec_proj_ln = [&](const Conv& wo, const float* lg, const float* lb, const float* x_amax) -> int {
-    if (decproj_on && m->esz == 2 && d == 256 && Q <= 64) {
+  auto dec_proj_ln = [&](const Conv& wo, const void* fwo, const float* lg, const float* lb, const float* x_amax) -> int {
+    if (decproj_on && fwo && Q <= 64) {
       // bf16: one workgroup per image, the rows in LDS from the GEMM to the LayerNorm (decsa.hip)
       DecProjArgs pa{};
       pa.tgt = P(w.tgt); pa.ldt = d; pa.x = P(w.dao); pa.ldx = d; pa.B = B; pa.Q = Q;
-      pa.wo = wo.w; pa.ldo = wo.Kpad; pa.bo = wo.bias; pa.g = lg; pa.b = lb;
+      pa.wo = fwo; pa.bo = wo.bias; pa.g = lg; pa.b = lb;
       CK(run_other(m, "dec.proj", 2.0 * Mq * d * d, 3.0 * Mq * d * m->esz + (double)d * d * m->esz, s,
                    [&] { return spe_launch_decproj(pa, s); }));
       return 0;
@@ -547,16 +547,18 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   // bf16: the self-attention block (projections, attention, out-projection, norm1) as one
   // launch per layer (decsa.hip); SPE_DECSA=0 runs the separate launches for A/B runs
   static const bool decsa_on = [] { const char* e = getenv("SPE_DECSA"); return e ? atoi(e) != 0 : true; }();
+  // bf16: the decoder FFN as decsa.hip's 16-row split-F kernel; SPE_DECFFN=0 runs ffn.hip's for A/B runs
+  static const bool decffn_on = [] { const char* e = getenv("SPE_DECFFN"); return e ? atoi(e) != 0 : true; }();
   for (int l = 0; l < L; ++l) {
     const Dec& e = m->dec[l];
-    const bool sa_fused = decsa_on && m->esz == 2 && d == 256 && c.nheads == 8 && Q <= 64 && e.qpos_sqk;
+    const bool sa_fused = decsa_on && e.fsqk && c.nheads == 8 && Q <= 64 && e.qpos_sqk;
     if (sa_fused) {
       DecSaArgs sa{};
       sa.tgt = P(w.tgt); sa.ldt = d; sa.B = B; sa.Q = Q;
-      sa.wqk = e.sqk.w; sa.ldqk = e.sqk.Kpad; sa.bqk = e.sqk.bias;
-      sa.wv = e.sv.w; sa.ldv = e.sv.Kpad; sa.bv = e.sv.bias;
+      sa.wqk = e.fsqk; sa.bqk = e.sqk.bias;
+      sa.wv = e.fsv; sa.bv = e.sv.bias;
       sa.qpos = e.qpos_sqk;
-      sa.wo = e.so.w; sa.ldo = e.so.Kpad; sa.bo = e.so.bias;
+      sa.wo = e.fso; sa.bo = e.so.bias;
       sa.g = e.n1g; sa.b = e.n1b; sa.scale = scale;
       const double fl = 2.0 * Mq * d * (4.0 * d) + 4.0 * B * 8.0 * Q * Q * 32;
       const double by = 2.0 * Mq * d * m->esz + 4.0 * d * d * m->esz;
@@ -583,9 +585,10 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       a.B = B; a.H = c.nheads; a.Tq = Q; a.Tk = Q; a.scale = scale;
       CK(run_attn(m, "attn.dec_self", a, dt, s));
     }
-    CK(dec_proj_ln(e.so, e.n1g, e.n1b, dam ? dam + 2 * l : nullptr));
+    CK(dec_proj_ln(e.so, e.fso, e.n1g, e.n1b, dam ? dam + 2 * l : nullptr));
     }
     if (m->h3) tgt_amax = e.n1_bound;
+    bool xtail = false;                         // the merge + value + out-projection + norm2 ran in one launch
     if (xa) {
       // q' = (tgt + query_pos) . Wqk^T + bqk: the query-side fold of Wq and Wk (xattn.hip)
       GemmArgs g = linear_args(e.xq, P(w.tgt), d, Mq, P(w.xq), 8 * d);
@@ -599,9 +602,23 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       x.o = P(w.dao); x.ldo = d;
       x.B = B; x.Q = Q; x.T = T; x.splits = spe_xattn_splits(B, Q, T);
       x.pm = (float*)P(w.xpm); x.pl = (float*)P(w.xpl); x.pu = (float*)P(w.xpu);
-      const double fl = 4.0 * B * 8.0 * Q * (double)T * d + 2.0 * Mq * 8.0 * d * 32;
+      // Q <= 16: the split merge and the value projection move into the out-projection + norm2
+      // launch (decsa.hip decxproj_kernel), the per-split partials its only input
+      xtail = decproj_on && e.fxv && Q <= 16;
+      x.partials_only = xtail;
+      const double fl = 4.0 * B * 8.0 * Q * (double)T * d + (xtail ? 0.0 : 2.0 * Mq * 8.0 * d * 32);
       const double by = 2.0 * B * (double)T * d * m->esz + 2.0 * Mq * 8.0 * d * m->esz;
       CK(run_other(m, "attn.dec_cross", fl, by, s, [&] { return spe_launch_xattn(x, s); }));
+      if (xtail) {
+        DecProjArgs pa{};
+        pa.tgt = P(w.tgt); pa.ldt = d; pa.B = B; pa.Q = Q;
+        pa.wo = e.fco; pa.bo = e.co.bias; pa.g = e.n2g; pa.b = e.n2b;
+        pa.pm = x.pm; pa.pl = x.pl; pa.pu = x.pu; pa.splits = spe_xattn_launch_splits(T, x.splits);
+        pa.wv = e.fxv; pa.bv = e.xv.bias;
+        const double pfl = 2.0 * Mq * 8.0 * d * 32 + 2.0 * Mq * d * d;
+        const double pby = (double)pa.splits * B * 8.0 * Q * (d + 2) * 4 + 2.0 * Mq * d * m->esz + 2.0 * d * d * m->esz;
+        CK(run_other(m, "dec.xproj", pfl, pby, s, [&] { return spe_launch_decproj(pa, s); }));
+      }
     } else {
     {
       GemmArgs g = linear_args(e.cq, P(w.tgt), d, Mq, P(w.dqc), d);
@@ -619,9 +636,24 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       CK(run_attn(m, "attn.dec_cross", a, dt, s));
     }
     }
-    CK(dec_proj_ln(e.co, e.n2g, e.n2b, cross_v_amax));
+    if (!xtail) CK(dec_proj_ln(e.co, e.fco, e.n2g, e.n2b, cross_v_amax));
     if (m->h3) tgt_amax = e.n2_bound;
-    if (use_fused_ffn(m)) {
+    if (e.fl1 && decffn_on) {
+      // bf16: one workgroup per (16 rows, 256 hidden units), all of its weight fragments in flight
+      // from the start (decsa.hip), then ffn.hip's split-F reduce + norm3
+      DecFfnArgs fa{};
+      fa.x = P(w.tgt); fa.ldx = d; fa.M = Mq; fa.F = ff;
+      fa.w1 = e.fl1; fa.b1 = e.l1.bias; fa.w2 = e.fl2; fa.partial = (float*)P(w.dffnpart);
+      FfnArgs ra{};
+      ra.x = P(w.tgt); ra.ldx = d; ra.y = P(w.tgt); ra.ldy = d; ra.M = Mq; ra.D = d; ra.F = ff;
+      ra.b2 = e.l2.bias; ra.gamma = e.n3g; ra.beta = e.n3b; ra.splits = ff / 256; ra.partial = fa.partial;
+      const double fl = 4.0 * Mq * (double)d * ff;
+      const double by = 2.0 * Mq * d * m->esz + 2.0 * (double)d * ff * m->esz + 2.0 * ra.splits * Mq * d * 4;
+      CK(run_other(m, "ffn.dec", fl, by, s, [&] {
+        const int rc = spe_launch_decffn(fa, s);
+        return rc ? rc : spe_launch_ffn_reduce_ln(ra, s);
+      }));
+    } else if (use_fused_ffn(m)) {
       CK(run_ffn(m, "ffn.dec", e.l1, e.l2, e.n3g, e.n3b, P(w.tgt), Mq, s, nullptr, nullptr, 0,
                  (float*)P(w.dffnpart)));
     } else {

@@ -49,6 +49,9 @@ struct Dec {
   // with Wq/Wk folded per head at finalize; xv = the value projection rows of in_proj
   Conv xq, xv;
   void* xq_r = nullptr;     // [Q][8*256] bf16: query_pos . Wqk^T + bqk (scaled)
+  // bf16, d = 256: sqk / sv / so / co / xv fragment-packed for the decoder kernels (decsa.hip)
+  void *fsqk = nullptr, *fsv = nullptr, *fso = nullptr, *fco = nullptr, *fxv = nullptr;
+  void *fl1 = nullptr, *fl2 = nullptr;   // linear1 / linear2 packed (fl2 per 256-wide hidden chunk; F % 256 == 0)
 };
 
 // fp32h3 activation-scale slots in the workspace: [0, SPE_AMAX_BB) written by the backbone stage,

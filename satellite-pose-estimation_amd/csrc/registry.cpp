@@ -606,6 +606,17 @@ int build_device(spe_model* m) {
       e.n3_bound = ln_bound(m, p + ".norm3", d);
     }
     if (spe_use_xattn(m)) fold_cross_attention(m, p, e);
+    if (m->esz == 2 && d == 256) {              // filled at finalize (spe_launch_wfrag_pack)
+      e.fsqk = dalloc(m, (size_t)2 * d * d * 2);
+      e.fsv = dalloc(m, (size_t)d * d * 2);
+      e.fso = dalloc(m, (size_t)d * d * 2);
+      e.fco = dalloc(m, (size_t)d * d * 2);
+      if (spe_use_xattn(m)) e.fxv = dalloc(m, (size_t)d * d * 2);
+      if (ff % 256 == 0) {
+        e.fl1 = dalloc(m, (size_t)ff * d * 2);
+        e.fl2 = dalloc(m, (size_t)d * ff * 2);
+      }
+    }
     m->dec.push_back(e);
     const auto& w = m->host[p + ".multihead_attn.in_proj_weight"];
     const auto& bb = m->host[p + ".multihead_attn.in_proj_bias"];
@@ -710,7 +721,9 @@ Ws spe_plan(const spe_model* m, int B) {
   w.dao = take((size_t)B * Q * d * E);
   w.dqc = take((size_t)B * Q * d * E);
   w.dffn = take((size_t)B * Q * ff * E);
-  w.dffnpart = take((size_t)std::max(1, spe_ffn_splits((int)(B * Q), (int)ff)) * B * Q * d * 4);   // split-F partials
+  // split-F partials (ffn.hip's split count, or one per 256-wide hidden chunk for decsa.hip's decffn)
+  const int fsplit = std::max(spe_ffn_splits((int)(B * Q), (int)ff), m->esz == 2 && d == 256 && ff % 256 == 0 ? (int)ff / 256 : 1);
+  w.dffnpart = take((size_t)std::max(1, fsplit) * B * Q * d * 4);
   w.hs = take((size_t)B * Q * d * 4);
   w.amax = take(m->h3 ? SPE_AMAX_SLOTS * 4 : 0);
   w.total = off;
@@ -810,6 +823,13 @@ int spe_model_finalize(spe_model* m) {
     for (auto& l : m->dec) {
       rc |= proj(m->qpos, Q, l.sqk, l.qpos_sqk);
       if (l.qpos_cq) rc |= proj(m->qpos, Q, l.cq, l.qpos_cq);
+      auto pack = [&](const Conv& w, void* dst) { return dst ? spe_launch_wfrag_pack(w.w, w.Kpad, w.N, dst, nullptr) : 0; };
+      rc |= pack(l.sqk, l.fsqk) | pack(l.sv, l.fsv) | pack(l.so, l.fso) | pack(l.co, l.fco) | pack(l.xv, l.fxv);
+      if (l.fl1) {
+        rc |= pack(l.l1, l.fl1);
+        for (int c0 = 0; c0 < l.l2.K; c0 += 256)
+          rc |= spe_launch_wfrag_pack((const char*)l.l2.w + (size_t)c0 * 2, l.l2.Kpad, d, (char*)l.fl2 + (size_t)c0 * d * 2, nullptr);
+      }
     }
     e = hipDeviceSynchronize();
     if (rc || e != hipSuccess) return fail(SPE_E_LAUNCH, "positional projection precompute failed");

@@ -123,19 +123,23 @@ struct XattnArgs {
   void* o; int ldo;                //   o rows b*Q + q, head h at columns [h*32, h*32 + 32)
   int B, Q, T, splits, tiles_per_split;
   float *pm, *pl, *pu;             // key-split partials [B][splits][8Q] (pu: x 256), required
+  bool partials_only;              // stop at the partials (decproj's merge form consumes them)
 };
 int spe_xattn_splits(int B, int Q, int T);
+int spe_xattn_launch_splits(int T, int splits);   // the split count a launch with `splits` runs (partials' layout)
 int spe_launch_xattn(const XattnArgs& a, hipStream_t s);
 
 // Decoder self-attention block (bf16 only, decsa.hip), one workgroup per image, in place over tgt:
 // tgt = LN(tgt + SelfAttn(q = k = tgt + qpos, v = tgt) . Wo^T + bo), 8 heads of 32, d = 256.
+// The decoder kernels' weights are fragment-packed (spe_launch_wfrag_pack): [N/16][8][64][8] bf16,
+// the 16-byte MFMA A fragment of lane l for column tile t and K-step ks at ((t*8 + ks)*64 + l)*8.
 struct DecSaArgs {
   void* tgt; int ldt;              // [B*Q][ldt] bf16
   int B, Q;                        // Q <= 64
-  const void* wqk; int ldqk; const float* bqk;   // in_proj rows 0..511 [512][ldqk] bf16, bias fp32
-  const void* wv; int ldv; const float* bv;      // in_proj rows 512..767
+  const void* wqk; const float* bqk;   // in_proj rows 0..511 (packed), bias fp32
+  const void* wv; const float* bv;     // in_proj rows 512..767 (packed)
   const void* qpos;                // [Q][512] bf16: query_pos . Wqk^T
-  const void* wo; int ldo; const float* bo;      // out_proj [256][ldo]
+  const void* wo; const float* bo;     // out_proj (packed)
   const float* g; const float* b;  // norm1
   float scale;                     // 1/sqrt(head_dim)
 };
@@ -145,9 +149,24 @@ struct DecProjArgs {
   void* tgt; int ldt;              // [B*Q][ldt] bf16, in place
   const void* x; int ldx;          // [B*Q][ldx] bf16
   int B, Q;
-  const void* wo; int ldo; const float* bo;
+  const void* wo; const float* bo; // out_proj (packed)
   const float* g; const float* b;
+  // merge form (pm set, Q <= 16): x is the cross-attention's output computed here from xattn's
+  // key-split partials (XattnArgs::partials_only) -- o_h = Wv_h u_h + bv_h, heads of 32
+  const float *pm, *pl, *pu; int splits;
+  const void* wv; const float* bv; // value rows of in_proj (packed)
 };
+// The decoder FFN's split-F product (decsa.hip, bf16, d = 256): partial [F/256][M][256] fp32 =
+// relu(x . W1c^T + b1c) . W2c^T per 256-wide hidden chunk c; spe_launch_ffn_reduce_ln finishes.
+// w1: W1 [F][256] fragment-packed; w2: chunk c's columns of W2 [256][F] packed at c * 256 * 256.
+struct DecFfnArgs {
+  const void* x; int ldx; int M, F;
+  const void* w1; const float* b1; const void* w2;
+  float* partial;
+};
+int spe_launch_decffn(const DecFfnArgs& a, hipStream_t s);
+// bf16 rows W [N][ld] (K = 256, N % 16 == 0) -> the fragment-packed layout above
+int spe_launch_wfrag_pack(const void* w, int ld, int N, void* dst, hipStream_t s);
 int spe_launch_decproj(const DecProjArgs& a, hipStream_t s);   // 1 = not applicable
 
 // Fused FFN + residual + LayerNorm (bf16 only): y = LN(x + W2 relu(W1 x + b1) + b2).
@@ -167,6 +186,8 @@ struct FfnArgs {
   int row0;                        // first row of this launch's tiles (internal: the FFN tail launch)
 };
 int spe_launch_ffn_ln(const FfnArgs& a, hipStream_t s);
+// y = LN(x + sum_s partial[s] + b2) over a.splits fp32 partials [splits][M][256] (ffn.hip)
+int spe_launch_ffn_reduce_ln(const FfnArgs& a, hipStream_t s);
 // fp32h3 encoder FFN + residual + LayerNorm in one pass (ffn_h3.hip): fp32 x / y [M][256], W1 as its
 // h3 finalize planes fp16 [2][F][ld1] (rows scaled by 2^e1), meta1 [F/32][64] = (2^-e1, b1) of each
 // 32-unit hidden chunk, W2 as fp16 planes [2][256][ld2] (rows scaled by 2^e2) with the columns of

@@ -384,16 +384,22 @@ int spe_xattn_splits(int B, int Q, int T) {
   return (ntiles + tps - 1) / tps;              // every split non-empty
 }
 
+int spe_xattn_launch_splits(int T, int splits) {
+  const int ntiles = (T + KT - 1) / KT, tps = (ntiles + splits - 1) / splits;
+  return (ntiles + tps - 1) / tps;              // no empty split (<= requested)
+}
+
 int spe_launch_xattn(const XattnArgs& a0, hipStream_t s) {
   XattnArgs a = a0;
   if (a.B <= 0) return 0;
-  if (a.ldq % 8 || a.ldk % 8 || a.ldv % 8 || a.ldu % 8 || a.splits < 1) return -5;
+  if (a.ldq % 8 || a.ldk % 8 || a.ldv % 8 || a.ldu % 8 || a.splits < 1 || a.T < 1) return -5;
   const int ntiles = (a.T + KT - 1) / KT;
   a.tiles_per_split = (ntiles + a.splits - 1) / a.splits;
-  a.splits = (ntiles + a.tiles_per_split - 1) / a.tiles_per_split;   // no empty split (<= requested)
-  if (!a.pm || !a.pl || !a.pu || (a.wv ? !a.o || !a.bv || a.ldo % 2 : !a.u)) return -5;
+  a.splits = spe_xattn_launch_splits(a.T, a.splits);
+  if (!a.pm || !a.pl || !a.pu || (!a.partials_only && (a.wv ? !a.o || !a.bv || a.ldo % 2 : !a.u))) return -5;
   const int groups = (8 * a.Q + RG - 1) / RG;
   hipLaunchKernelGGL(xattn_kernel, dim3(a.B * a.splits * groups), dim3(NT), 0, s, a);
+  if (a.partials_only) return (int)hipGetLastError();
   if (a.wv)
     hipLaunchKernelGGL(xattn_merge_wv_kernel, dim3((a.B * a.Q + MR - 1) / MR, 8), dim3(256), 0, s, a);
   else

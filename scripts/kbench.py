@@ -20,6 +20,13 @@ def p(t):
     return ctypes.c_void_p(t.data_ptr())
 
 
+def _pack(L, w):
+    """bf16 rows [N][256] -> the decoder kernels' fragment-packed layout (spe_debug_wfrag_pack)"""
+    out = torch.empty_like(w)
+    assert L.spe_debug_wfrag_pack(None, p(w), w.shape[1], w.shape[0], p(out)) == 0
+    return out
+
+
 def timeit(fn, iters):
     fn()
     torch.cuda.synchronize()
@@ -101,6 +108,13 @@ def main():
                 continue
             ms = timeit(fn, a.iters)
             print(f"ffn.dec M={M} splits={sp}: {ms * 1e3:.1f} us")
+        # decsa.hip's decffn: (16 rows, 256 hidden) workgroups over packed weights, + the reduce
+        f1 = _pack(L, w1)
+        f2 = torch.cat([_pack(L, w2[:, c:c + 256].contiguous()) for c in range(0, F, 256)])
+        fn = lambda: L.spe_debug_decffn(None, p(x), D, M, F, p(f1), 0, p(b1), p(f2), 0, p(b2), p(gm), p(bt), p(y),
+                                        D, p(part))
+        assert fn() == 0
+        print(f"decffn M={M}: {timeit(fn, a.iters) * 1e3:.1f} us")
     if a.which in ("decsa", "all"):
         # the decoder's fused self-attention block (decsa.hip), B images of Q = 11 rows
         Q = 11
@@ -111,7 +125,9 @@ def main():
         qpos = torch.zeros(Q, 2 * D, device=dev, dtype=torch.bfloat16)
         bqk, bv, bo, bt = (torch.zeros(n, device=dev) for n in (2 * D, D, D, D))
         gm = torch.ones(D, device=dev)
-        fn = lambda: L.spe_debug_decsa(None, p(t), D, B, Q, p(wqk), D, p(bqk), p(wv), D, p(bv), p(qpos), p(wo), D,
+        pk = lambda w: _pack(L, w)                      # noqa: E731  (fragment-packed once, ld = 0)
+        fqk, fv, fo = pk(wqk), pk(wv), pk(wo)
+        fn = lambda: L.spe_debug_decsa(None, p(t), D, B, Q, p(fqk), 0, p(bqk), p(fv), 0, p(bv), p(qpos), p(fo), 0,
                                        p(bo), p(gm), p(bt), 32 ** -0.5)
         ms = timeit(fn, a.iters)
         print(f"decsa B={B} Q={Q}: {ms * 1e3:.1f} us")
@@ -134,6 +150,17 @@ def main():
             ms_u = timeit(fn_u, a.iters)
             byts = 2 * B * T * D * 2                      # K and V reads
             print(f"xattn splits={sp}: {ms:.3f} ms with Wv, {ms_u:.3f} ms u only ({byts / ms_u / 1e9:.2f} TB/s)")
+        # the cross-attention's tail: separate merge + Wv kernel then decproj, against decxproj
+        t = torch.randn(B * Q, D, generator=g).to(dev, torch.bfloat16)
+        wo = (torch.randn(D, D, generator=g) / 16).to(dev, torch.bfloat16)
+        bo, bt, gm = torch.zeros(D, device=dev), torch.zeros(D, device=dev), torch.ones(D, device=dev)
+        L.spe_debug_xattn(None, p(q), 8 * D, p(k), D, p(v), D, p(u), 8 * D, None, None, None, 0, B, Q, T, 0, p(part))
+        fwo, fwv = _pack(L, wo), _pack(L, wv)
+        fn_dp = lambda: L.spe_debug_decproj(None, p(t), D, p(o), D, B, Q, p(fwo), 0, p(bo), p(gm), p(bt))
+        fn_xp = lambda: L.spe_debug_decxproj(None, p(t), D, p(part), 0, T, B, Q, p(fwv), 0, p(bv), p(fwo), 0, p(bo),
+                                             p(gm), p(bt))
+        print(f"decproj B={B} Q={Q}: {timeit(fn_dp, a.iters) * 1e3:.1f} us; "
+              f"decxproj (merge + Wv + Wo + LN): {timeit(fn_xp, a.iters) * 1e3:.1f} us")
     if a.which in ("gemm", "all"):
         # name, mode, M, N, K, residual rows (0 none, -1 full, >0 period), conv geometry
         cases = [("l1.c3 1x1+res", 0, B * 104 * 104, 256, 64, -1, None),

@@ -664,6 +664,80 @@ def test_cross_attention_memory(gpu_device, B, Q, T, splits, amp):
     assert (o[:, D:] == 7.0).all()
 
 
+@pytest.mark.parametrize("B,Q,T,splits,amp", [(3, 11, 200, 1, 1.0), (2, 11, 203, 3, 1.0), (1, 16, 136, 2, 1.0),
+                                              (64, 11, 2704, 0, 1.0), (2, 5, 640, 4, 12.0), (1, 1, 2704, 0, 1.0)])
+def test_cross_attention_tail_fused(gpu_device, B, Q, T, splits, amp):
+    """decxproj (decsa.hip): the key-split merge of xattn's partials, the value projection
+    o_h = Wv_h u_h + bv_h (bf16) and tgt = LN(tgt + o . Wo^T + bo) in one launch per image
+    (REV/models/transformer.py:230-234), against torch fp32 on the same bf16 operands with the
+    separate path's rounding of o.  The partials come from the xattn kernel itself; 2e-2 * scale."""
+    dt, D = torch.bfloat16, 256
+    g = torch.Generator(device="cpu").manual_seed(3 * B * T + Q)
+    ldq, ldt = 8 * D + 8, D + 8
+    q = (torch.randn(B * Q, ldq, generator=g) * amp / 16).to(gpu_device, dt)
+    k = torch.randn(B * T, D, generator=g).to(gpu_device, dt)
+    v = torch.randn(B * T, D, generator=g).to(gpu_device, dt)
+    if amp > 1:
+        k[5] *= 4
+    wv = (torch.randn(D, D, generator=g) / 16).to(gpu_device, dt)
+    bv = torch.randn(D, generator=g).to(gpu_device)
+    wo = (torch.randn(D, D, generator=g) / 16).to(gpu_device, dt)
+    bo = (torch.randn(D, generator=g) * 0.1).to(gpu_device)
+    gam = (1 + 0.1 * torch.randn(D, generator=g)).to(gpu_device)
+    bet = (0.1 * torch.randn(D, generator=g)).to(gpu_device)
+    t0 = torch.randn(B * Q, ldt, generator=g)
+    t = t0.to(dt).to(gpu_device)
+    u = torch.empty(B * Q, ldq, dtype=dt, device=gpu_device)
+    S = splits if splits > 0 else 256
+    part = torch.empty(S * B * 8 * Q * 258, device=gpu_device)
+    L = _lib.lib()
+    rc = L.spe_debug_xattn(None, _p(q), ldq, _p(k), D, _p(v), D, _p(u), ldq, None, None, None, 0, B, Q, T,
+                           splits, _p(part))
+    assert rc == 0, L.spe_last_error()
+    rc = L.spe_debug_decxproj(None, _p(t), ldt, _p(part), splits, T, B, Q, _p(wv), D, _p(bv), _p(wo), D, _p(bo),
+                              _p(gam), _p(bet))
+    assert rc == 0, L.spe_last_error()
+    torch.cuda.synchronize()
+    s = torch.einsum("brd,btd->brt", q[:, :8 * D].float().view(B, Q * 8, D), k.float().view(B, T, D))
+    ref_u = torch.einsum("brt,btd->brd", torch.softmax(s * 0.6931471805599453, dim=-1), v.float().view(B, T, D))
+    o = torch.einsum("bqhn,hjn->bqhj", ref_u.view(B, Q, 8, D), wv.float().view(8, 32, D)) + bv.view(8, 32)
+    o = o.reshape(B * Q, D).to(dt).float()
+    y = torch.nn.functional.layer_norm(o @ wo.float().T + bo + t0[:, :D].to(dt).float().to(gpu_device), (D,),
+                                       gam, bet, 1e-5)
+    _close(t[:, :D], y, 2e-2)
+    assert torch.equal(t[:, D:].cpu(), t0[:, D:].to(dt))   # nothing written past D
+
+
+@pytest.mark.parametrize("M,F", [(704, 2048), (33, 2048), (16, 256), (2816, 1024), (1, 512)])
+def test_decoder_ffn_split_chunks(gpu_device, M, F):
+    """decffn (decsa.hip) + ffn.hip's reduce: y = LN(x + W2 relu(W1 x + b1) + b2) in place for the
+    decoder's few rows (REV/models/transformer.py:236-238), one workgroup per (16 rows, 256 hidden
+    units), against torch fp32 on the same bf16 operands with the hidden rounded to bf16 as the
+    kernel does; 2e-2 * scale (bf16 output).  M = 2816: the north star's 256 images per GPU."""
+    dt, D = torch.bfloat16, 256
+    g = torch.Generator(device="cpu").manual_seed(M + F)
+    ldx = D + 8
+    x0 = torch.randn(M, ldx, generator=g)
+    w1 = (torch.randn(F, D, generator=g) / 16).to(dt)
+    w2 = (torch.randn(D, F, generator=g) / 45).to(dt)
+    b1, b2 = torch.randn(F, generator=g) * 0.1, torch.randn(D, generator=g) * 0.1
+    gam, bet = 1 + 0.1 * torch.randn(D, generator=g), 0.1 * torch.randn(D, generator=g)
+    dev = lambda a: a.to(gpu_device).contiguous()          # noqa: E731
+    x = x0.to(dt).to(gpu_device)
+    part = torch.empty(F // 256 * M * D, device=gpu_device)
+    args = [dev(w1), dev(b1), dev(w2), dev(b2), dev(gam), dev(bet)]
+    L = _lib.lib()
+    rc = L.spe_debug_decffn(None, _p(x), ldx, M, F, _p(args[0]), D, _p(args[1]), _p(args[2]), F, _p(args[3]),
+                            _p(args[4]), _p(args[5]), _p(x), ldx, _p(part))
+    assert rc == 0, L.spe_last_error()
+    torch.cuda.synchronize()
+    xb = x0[:, :D].to(dt).float()
+    h = torch.relu(xb @ w1.float().T + b1).to(dt).float()
+    y = torch.nn.functional.layer_norm(xb + h @ w2.float().T + b2, (D,), gam, bet, 1e-5)
+    _close(x[:, :D].cpu(), y, 2e-2)
+    assert torch.equal(x[:, D:].cpu(), x0[:, D:].to(dt))   # nothing written past D
+
+
 @pytest.mark.parametrize("B,Q", [(3, 11), (2, 40), (1, 64), (4, 1), (0, 11)])
 def test_decoder_self_attention_block(gpu_device, B, Q):
     """decsa.hip: tgt = LN(tgt + MHA(q = k = tgt + query_pos, v = tgt) . Wo^T + bo) in place, one
