@@ -381,6 +381,11 @@ int spe_debug_wfrag_pack(void* stream, const void* w, int ld, int N, void* dst);
 int spe_debug_decffn(void* stream, const void* x, int ldx, int M, int F, const void* w1, int ld1, const float* b1,
                      const void* w2, int ld2, const float* b2, const float* gamma, const float* beta, void* y, int ldy,
                      float* partial);
+/* decq (bf16, decsa.hip, ABI 7 addition): y [M][ldy] = x . w^T + bias + r[m % period] over K = 256,
+ * N % 256 == 0 (the decoder cross-attention's folded query projection); w [N][ldw] row-major or
+ * packed with ldw 0; bias (fp32) and r (bf16 [period][ldr]) nullable. */
+int spe_debug_decq(void* stream, const void* x, int ldx, int M, int N, const void* w, int ldw, const float* bias,
+                   const void* r, int ldr, int period, void* y, int ldy);
 /* the K-column order btail's second product expects: stored column k holds channel perm(k) */
 int spe_debug_btail_perm(int k);
 /* stempool (bf16, stempool.hip): out [B][Po][Po] rows of stride ldo (Po = S/4 for S % 4 == 0) =

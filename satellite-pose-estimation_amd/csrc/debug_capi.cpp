@@ -242,6 +242,18 @@ int spe_debug_decffn(void* stream, const void* x, int ldx, int M, int F, const v
   return rc != 0 ? spe_fail(SPE_E_LAUNCH, "decffn launch rejected its arguments") : 0;
 }
 
+int spe_debug_decq(void* stream, const void* x, int ldx, int M, int N, const void* w, int ldw, const float* bias,
+                   const void* r, int ldr, int period, void* y, int ldy) {
+  if (!x || !w || !y || M < 0 || N < 256 || N % 256) return spe_fail(SPE_E_ARG, "bad argument");
+  Frags f((hipStream_t)stream);
+  DecQArgs a{};
+  a.x = x; a.ldx = ldx; a.M = M; a.N = N; a.w = f.get(w, ldw, N); a.bias = bias;
+  a.R = r; a.ldr = ldr; a.period = period; a.y = y; a.ldy = ldy;
+  if (f.err) return spe_fail(SPE_E_ARG, "decq: weight packing failed");
+  const int rc = spe_launch_decq(a, (hipStream_t)stream);
+  return rc != 0 ? spe_fail(SPE_E_LAUNCH, "decq launch rejected its arguments") : 0;
+}
+
 int spe_debug_btail_perm(int k) { return spe_btail_perm(k); }
 
 int spe_debug_stempool(void* stream, const void* x, const void* w, int ldw, const float* bias, void* out, int ldo,

@@ -445,6 +445,42 @@ __global__ __launch_bounds__(NT) void decffn_kernel(DecFfnArgs a) {
   }
 }
 
+// y = x . W^T (+ bias) + R[m % period] in bf16 over K = 256 for the decoder's few rows: the
+// cross-attention's folded query projection q' (2048 columns, R = query_pos . Wqk^T + bqk), one
+// workgroup per (16 rows, 256 columns) with its 128 KB of packed W fragments requested up front.
+__global__ __launch_bounds__(NT) void decq_kernel(DecQArgs a) {
+  __shared__ __attribute__((aligned(16))) bf16 xs[16 * XLD];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int nc = a.N / D, c = blockIdx.x % nc, r0 = (blockIdx.x / nc) * 16;
+  u32x4 wf[2][8];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) w_frags(wf[j], a.w, 16 * c + 2 * wid + j, lane);
+  if (tid < 16 * (D / 8)) {
+    const int r = tid / (D / 8), q = tid % (D / 8);
+    st16(xs + r * XLD + 8 * q, r0 + r < a.M ? ld16((const bf16*)a.x + (size_t)(r0 + r) * a.ldx + 8 * q) : u32x4{0, 0, 0, 0});
+  }
+  const int m = r0 + (lane & 15);
+  u32x2 rv[2] = {};
+  f32x4 bv[2] = {};
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int n = D * c + 32 * wid + 16 * j + 4 * (lane >> 4);
+    if (m < a.M && a.R) rv[j] = ld8((const bf16*)a.R + (size_t)(m % a.period) * a.ldr + n);
+    if (a.bias) bv[j] = *reinterpret_cast<const f32x4*>(a.bias + n);
+  }
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const f32x4 acc = tile_wx(wf[j], xs, XLD, 0, lane);
+    const int n = D * c + 32 * wid + 16 * j + 4 * (lane >> 4);
+    const float o0 = acc[0] + bv[j][0] + __uint_as_float(rv[j].x << 16);
+    const float o1 = acc[1] + bv[j][1] + __uint_as_float(rv[j].x & 0xffff0000u);
+    const float o2 = acc[2] + bv[j][2] + __uint_as_float(rv[j].y << 16);
+    const float o3 = acc[3] + bv[j][3] + __uint_as_float(rv[j].y & 0xffff0000u);
+    if (m < a.M) st8((bf16*)a.y + (size_t)m * a.ldy + n, u32x2{pack_bf16x2(o0, o1), pack_bf16x2(o2, o3)});
+  }
+}
+
 __global__ __launch_bounds__(256) void wfrag_pack_kernel(const bf16* w, int ld, int N, bf16* dst) {
   const int i = blockIdx.x * 256 + threadIdx.x;   // one 16-byte fragment: (tile, K-step, lane)
   if (i >= N * 32) return;
@@ -463,5 +499,13 @@ int spe_launch_decffn(const DecFfnArgs& a, hipStream_t s) {
   if (a.M <= 0) return 0;
   if (!a.x || !a.w1 || !a.b1 || !a.w2 || !a.partial || a.F < D || a.F % D || a.ldx % 8) return -5;
   hipLaunchKernelGGL(decffn_kernel, dim3(((a.M + 15) / 16) * (a.F / D)), dim3(NT), 0, s, a);
+  return (int)hipGetLastError();
+}
+
+int spe_launch_decq(const DecQArgs& a, hipStream_t s) {
+  if (a.M <= 0) return 0;
+  if (!a.x || !a.w || !a.y || a.N < D || a.N % D || a.ldx % 8 || a.ldy % 4 || (a.R && (a.period < 1 || a.ldr % 4)))
+    return -5;
+  hipLaunchKernelGGL(decq_kernel, dim3(((a.M + 15) / 16) * (a.N / D)), dim3(NT), 0, s, a);
   return (int)hipGetLastError();
 }

@@ -547,7 +547,8 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   // bf16: the self-attention block (projections, attention, out-projection, norm1) as one
   // launch per layer (decsa.hip); SPE_DECSA=0 runs the separate launches for A/B runs
   static const bool decsa_on = [] { const char* e = getenv("SPE_DECSA"); return e ? atoi(e) != 0 : true; }();
-  // bf16: the decoder FFN as decsa.hip's 16-row split-F kernel; SPE_DECFFN=0 runs ffn.hip's for A/B runs
+  // bf16: the decoder FFN and the cross-attention's query projection as decsa.hip's 16-row kernels;
+  // SPE_DECFFN=0 runs ffn.hip's FFN and the GEMM for A/B runs
   static const bool decffn_on = [] { const char* e = getenv("SPE_DECFFN"); return e ? atoi(e) != 0 : true; }();
   for (int l = 0; l < L; ++l) {
     const Dec& e = m->dec[l];
@@ -591,9 +592,19 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
     bool xtail = false;                         // the merge + value + out-projection + norm2 ran in one launch
     if (xa) {
       // q' = (tgt + query_pos) . Wqk^T + bqk: the query-side fold of Wq and Wk (xattn.hip)
-      GemmArgs g = linear_args(e.xq, P(w.tgt), d, Mq, P(w.xq), 8 * d);
-      g.R = e.xq_r; g.ldr = 8 * d; g.r_period = Q;
-      CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR, s));
+      if (e.fxq && decffn_on) {
+        // (16 rows, 256 columns) workgroups over the packed weights (decsa.hip)
+        DecQArgs qa{};
+        qa.x = P(w.tgt); qa.ldx = d; qa.M = Mq; qa.N = 8 * d;
+        qa.w = e.fxq; qa.bias = e.xq.bias; qa.R = e.xq_r; qa.ldr = 8 * d; qa.period = Q;
+        qa.y = P(w.xq); qa.ldy = 8 * d;
+        CK(run_other(m, "gemm.dec", 2.0 * Mq * d * 8.0 * d, 2.0 * Mq * (d + 8.0 * d) * m->esz + 2.0 * 8 * d * d * m->esz, s,
+                     [&] { return spe_launch_decq(qa, s); }));
+      } else {
+        GemmArgs g = linear_args(e.xq, P(w.tgt), d, Mq, P(w.xq), 8 * d);
+        g.R = e.xq_r; g.ldr = 8 * d; g.r_period = Q;
+        CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR, s));
+      }
       XattnArgs x{};
       x.q = P(w.xq); x.ldq = 8 * d;
       x.k = P(w.srcpos); x.ldk = d;

@@ -51,6 +51,7 @@ struct Dec {
   void* xq_r = nullptr;     // [Q][8*256] bf16: query_pos . Wqk^T + bqk (scaled)
   // bf16, d = 256: sqk / sv / so / co / xv fragment-packed for the decoder kernels (decsa.hip)
   void *fsqk = nullptr, *fsv = nullptr, *fso = nullptr, *fco = nullptr, *fxv = nullptr;
+  void *fxq = nullptr;                   // xq packed (the folded cross-attention query projection)
   void *fl1 = nullptr, *fl2 = nullptr;   // linear1 / linear2 packed (fl2 per 256-wide hidden chunk; F % 256 == 0)
 };
 

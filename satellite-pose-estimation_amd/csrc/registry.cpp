@@ -611,7 +611,10 @@ int build_device(spe_model* m) {
       e.fsv = dalloc(m, (size_t)d * d * 2);
       e.fso = dalloc(m, (size_t)d * d * 2);
       e.fco = dalloc(m, (size_t)d * d * 2);
-      if (spe_use_xattn(m)) e.fxv = dalloc(m, (size_t)d * d * 2);
+      if (spe_use_xattn(m)) {
+        e.fxv = dalloc(m, (size_t)d * d * 2);
+        e.fxq = dalloc(m, (size_t)e.xq.N * d * 2);
+      }
       if (ff % 256 == 0) {
         e.fl1 = dalloc(m, (size_t)ff * d * 2);
         e.fl2 = dalloc(m, (size_t)d * ff * 2);
@@ -824,7 +827,7 @@ int spe_model_finalize(spe_model* m) {
       rc |= proj(m->qpos, Q, l.sqk, l.qpos_sqk);
       if (l.qpos_cq) rc |= proj(m->qpos, Q, l.cq, l.qpos_cq);
       auto pack = [&](const Conv& w, void* dst) { return dst ? spe_launch_wfrag_pack(w.w, w.Kpad, w.N, dst, nullptr) : 0; };
-      rc |= pack(l.sqk, l.fsqk) | pack(l.sv, l.fsv) | pack(l.so, l.fso) | pack(l.co, l.fco) | pack(l.xv, l.fxv);
+      rc |= pack(l.sqk, l.fsqk) | pack(l.sv, l.fsv) | pack(l.so, l.fso) | pack(l.co, l.fco) | pack(l.xv, l.fxv) | pack(l.xq, l.fxq);
       if (l.fl1) {
         rc |= pack(l.l1, l.fl1);
         for (int c0 = 0; c0 < l.l2.K; c0 += 256)

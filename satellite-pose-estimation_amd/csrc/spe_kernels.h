@@ -165,6 +165,14 @@ struct DecFfnArgs {
   float* partial;
 };
 int spe_launch_decffn(const DecFfnArgs& a, hipStream_t s);
+// y [M][ldy] = x . W^T (+ bias) + R[m % period] (decsa.hip; bf16, K = 256, N % 256 == 0; W packed)
+struct DecQArgs {
+  const void* x; int ldx; int M, N;
+  const void* w; const float* bias;
+  const void* R; int ldr; int period;   // optional row-periodic residual, bf16
+  void* y; int ldy;
+};
+int spe_launch_decq(const DecQArgs& a, hipStream_t s);
 // bf16 rows W [N][ld] (K = 256, N % 16 == 0) -> the fragment-packed layout above
 int spe_launch_wfrag_pack(const void* w, int ld, int N, void* dst, hipStream_t s);
 int spe_launch_decproj(const DecProjArgs& a, hipStream_t s);   // 1 = not applicable

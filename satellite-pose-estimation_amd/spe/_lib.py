@@ -41,7 +41,7 @@ EXPORTS = ["spe_abi_version", "spe_last_error", "spe_model_create", "spe_model_d
            "spe_model_num_params", "spe_model_param_name", "spe_model_finalize", "spe_model_workspace_bytes",
            "spe_forward", "spe_forward_stages", "spe_preprocess", "spe_criterion", "spe_ensemble_fuse", "spe_postprocess", "spe_pnp_batch", "spe_self_assess", "spe_speed_score", "spe_model_profile_begin",
            "spe_model_profile_end", "spe_model_profile_get", "spe_debug_gemm", "spe_debug_gemm_path", "spe_debug_gemm_h3", "spe_debug_ffn_h3", "spe_debug_ffn_h3_perm", "spe_debug_gemm_planes", "spe_debug_attention",
-           "spe_debug_layernorm", "spe_debug_ffn", "spe_debug_xattn", "spe_debug_upconv", "spe_debug_btail", "spe_debug_decsa", "spe_debug_decproj", "spe_debug_decxproj", "spe_debug_wfrag_pack", "spe_debug_decffn", "spe_debug_btail_perm", "spe_debug_stempool", "spe_rtdetr_create", "spe_rtdetr_forward",
+           "spe_debug_layernorm", "spe_debug_ffn", "spe_debug_xattn", "spe_debug_upconv", "spe_debug_btail", "spe_debug_decsa", "spe_debug_decproj", "spe_debug_decxproj", "spe_debug_wfrag_pack", "spe_debug_decffn", "spe_debug_decq", "spe_debug_btail_perm", "spe_debug_stempool", "spe_rtdetr_create", "spe_rtdetr_forward",
            "spe_jpeg_workspace_bytes", "spe_jpeg_decode"]
 
 
@@ -124,6 +124,7 @@ def lib():
     L.spe_debug_decproj.argtypes = [P, P, I, P, I, I, I, P, I, P, P, P]
     L.spe_debug_wfrag_pack.argtypes = [P, P, I, I, P]
     L.spe_debug_decffn.argtypes = [P, P, I, I, I, P, I, P, P, I, P, P, P, P, I, P]
+    L.spe_debug_decq.argtypes = [P, P, I, I, I, P, I, P, P, I, I, P, I]
     L.spe_debug_decxproj.argtypes = [P, P, I, P, I, I, I, I, P, I, P, P, I, P, P, P]
     if hasattr(L, "spe_debug_stempool"):
         L.spe_debug_stempool.argtypes = [P, P, P, I, P, P, I, I, I]

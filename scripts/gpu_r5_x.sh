@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 TAG=${PROF_TAG:-r5x}
 mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_kernels.py \
-  -k "cross_attention or decoder_out_projection or decoder_self or decoder_ffn or ffn" > gpurun_out/${TAG}_tests.log 2>&1 \
+  -k "cross_attention or decoder_out_projection or decoder_self or decoder_ffn or ffn or query_projection" > gpurun_out/${TAG}_tests.log 2>&1 \
   || { grep -E "^E |FAILED|Error" gpurun_out/${TAG}_tests.log | head -20; exit 4; }
 tail -1 gpurun_out/${TAG}_tests.log
 timeout -k 10 400 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_parity.py \

@@ -115,6 +115,14 @@ def main():
                                         D, p(part))
         assert fn() == 0
         print(f"decffn M={M}: {timeit(fn, a.iters) * 1e3:.1f} us")
+        # the cross-attention's folded query projection q' (2048 columns, row-periodic residual)
+        wq = (torch.randn(8 * D, D, generator=g) / 16).to(dev, torch.bfloat16)
+        rq = torch.randn(11, 8 * D, generator=g).to(dev, torch.bfloat16)
+        yq = torch.empty(M, 8 * D, dtype=torch.bfloat16, device=dev)
+        fq = _pack(L, wq)
+        fn = lambda: L.spe_debug_decq(None, p(x), D, M, 8 * D, p(fq), 0, None, p(rq), 8 * D, 11, p(yq), 8 * D)
+        assert fn() == 0
+        print(f"decq M={M} N=2048: {timeit(fn, a.iters) * 1e3:.1f} us")
     if a.which in ("decsa", "all"):
         # the decoder's fused self-attention block (decsa.hip), B images of Q = 11 rows
         Q = 11

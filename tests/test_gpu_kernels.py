@@ -708,6 +708,36 @@ def test_cross_attention_tail_fused(gpu_device, B, Q, T, splits, amp):
     assert torch.equal(t[:, D:].cpu(), t0[:, D:].to(dt))   # nothing written past D
 
 
+@pytest.mark.parametrize("M,N,period,bias", [(704, 2048, 11, False), (37, 2048, 11, True), (2816, 512, 40, False),
+                                              (5, 256, 0, True)])
+def test_decoder_query_projection(gpu_device, M, N, period, bias):
+    """decq (decsa.hip): y = x . W^T (+ b) + R[m % period], bf16, K = 256 -- the cross-attention's
+    folded query projection (xattn.hip; R = query_pos . Wqk^T + bqk), one workgroup per (16 rows,
+    256 columns), against torch fp32 on the same bf16 operands; 1e-2 * scale (bf16 output)."""
+    dt, D = torch.bfloat16, 256
+    g = torch.Generator(device="cpu").manual_seed(M + N + period)
+    ldx, ldy = D + 8, N + 8
+    x = torch.randn(M, ldx, generator=g).to(dt)
+    w = (torch.randn(N, D, generator=g) / 16).to(dt)
+    b = torch.randn(N, generator=g) if bias else None
+    r = torch.randn(max(period, 1), N, generator=g).to(dt) if period else None
+    y = torch.full((M, ldy), 7.0, dtype=dt, device=gpu_device)
+    dev = lambda a: a.to(gpu_device).contiguous() if a is not None else None   # noqa: E731
+    xd, wd, bd, rd = dev(x), dev(w), dev(b), dev(r)
+    L = _lib.lib()
+    rc = L.spe_debug_decq(None, _p(xd), ldx, M, N, _p(wd), D, _p(bd) if bias else None, _p(rd) if period else None,
+                          N, period, _p(y), ldy)
+    assert rc == 0, L.spe_last_error()
+    torch.cuda.synchronize()
+    ref = x[:, :D].float() @ w.float().T
+    if bias:
+        ref += b
+    if period:
+        ref += r.float()[torch.arange(M) % period]
+    _close(y[:, :N].cpu(), ref, 1e-2)
+    assert (y[:, N:] == 7.0).all()
+
+
 @pytest.mark.parametrize("M,F", [(704, 2048), (33, 2048), (16, 256), (2816, 1024), (1, 512)])
 def test_decoder_ffn_split_chunks(gpu_device, M, F):
     """decffn (decsa.hip) + ffn.hip's reduce: y = LN(x + W2 relu(W1 x + b1) + b2) in place for the
