@@ -323,11 +323,18 @@ int spe_launch_pconv(const GemmArgs& g, hipStream_t s) {
     return launch_pc<256, 64, 1>(g, c.geo, s);
   }
   if (g.N % 256 == 0) {
-    PcChoice c2{};
-    const bool a = choose_block(g, 192, 256, cus, c), bq = choose_block(g, 256, 256, cus, c2);
-    if (!a && !bq) return 1;
-    // per-tile time ~ BM: compare rounds x BM
-    if (bq && (!a || (long long)c2.rounds * 256 <= (long long)c.rounds * 192)) return launch_pc<256, 256, 2>(g, c2.geo, s);
+    PcChoice c2{}, c3{};
+    const bool a = choose_block(g, 192, 256, cus, c), bq = choose_block(g, 256, 256, cus, c2),
+               h = choose_block(g, 256, 128, cus, c3);
+    if (!a && !bq && !h) return 1;
+    // per-tile time ~ BM x BN: the fewest rounds x tile area.  (At 32 images the 26x26 layer-3
+    // convs are 128 tiles of 192 x 256 -- one round on half the chip; 192 tiles of 256 x 128
+    // take one round of two thirds of the work each.)
+    const long long big = 1LL << 62;
+    const long long ca = a ? c.rounds * 192LL * 256 : big, cb = bq ? c2.rounds * 256LL * 256 : big,
+                    ch = h ? c3.rounds * 256LL * 128 : big;
+    if (ch < ca && ch < cb) return launch_pc<256, 128, 2>(g, c3.geo, s);
+    if (cb <= ca) return launch_pc<256, 256, 2>(g, c2.geo, s);
     return launch_pc<192, 256, 2>(g, c.geo, s);
   }
   if (g.N % 128 == 0) {

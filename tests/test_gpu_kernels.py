@@ -301,11 +301,13 @@ def test_gemm_large_tile_conv(gpu_device, Cin, Cout, k, s, p):
 # patch-staged 3x3 kernel (pconv.hip): stride 1 / pad 1, Cin % 64 == 0, Cout % 64 == 0 (64: one
 # patch buffer, two workgroups per CU; 128-multiples / 256-multiples: double-buffered patches).
 # Shapes: the bench's layer 1-3 convs and neck at small B, odd image sizes (partial blocks in both
-# directions), several column tiles, and the one-buffer patch refetch across channel blocks.
+# directions), several column tiles, and the one-buffer patch refetch across channel blocks.  (32, 26, 26,
+# 256, 256): the north star's 32 images per GPU at layer 3, where 256 x 128 tiles fill the chip better.
 @pytest.mark.parametrize("B,H,W,Cin,Cout,relu", [(3, 104, 104, 64, 64, 1), (2, 52, 52, 128, 128, 1),
                                                  (2, 26, 26, 256, 256, 1), (1, 52, 52, 1024, 256, 0),
                                                  (2, 13, 17, 128, 64, 1), (2, 9, 40, 64, 512, 0),
-                                                 (5, 7, 7, 256, 128, 1), (1, 30, 61, 192, 384, 1)])
+                                                 (5, 7, 7, 256, 128, 1), (1, 30, 61, 192, 384, 1),
+                                                 (32, 26, 26, 256, 256, 1)])
 def test_patch_conv3x3(gpu_device, B, H, W, Cin, Cout, relu):
     _, dt, tol = DT["bf16"]
     g = torch.Generator(device="cpu").manual_seed(B * H * W + Cin + Cout)
