@@ -50,9 +50,11 @@ SPE_DEV f32x4 tile_wx(const u32x4 (&wf)[8], const bf16* xs, int xld, int m0, int
   return acc;                                // lane: row m0 + (l & 15), columns n0 + 4 (l >> 4) + e
 }
 
+// QM: the rows the LDS is sized for (16: Q <= 16, a quarter of the 64-row form's 133 KB)
+template <int QM>
 __global__ __launch_bounds__(NT) void decsa_kernel(DecSaArgs a) {
-  __shared__ __attribute__((aligned(16))) bf16 xs[QMAX * XLD];
-  __shared__ __attribute__((aligned(16))) char big[QMAX * QKVLD * 2];   // q|k|v, then the fp32 rows
+  __shared__ __attribute__((aligned(16))) bf16 xs[QM * XLD];
+  __shared__ __attribute__((aligned(16))) char big[QM * QKVLD * 2];   // q|k|v, then the fp32 rows
   bf16* qkv = reinterpret_cast<bf16*>(big);
   float* ys = reinterpret_cast<float*>(big);
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
@@ -144,13 +146,13 @@ __global__ __launch_bounds__(NT) void decsa_kernel(DecSaArgs a) {
   __syncthreads();
 
   // ---- 3. out-projection + bo + residual (registers), then the fp32 rows over q|k|v
-  f32x4 yo[CT3][QMAX / 16];
+  f32x4 yo[CT3][QM / 16];
 #pragma unroll
   for (int j = 0; j < CT3; ++j) {
     const int n0 = (wid * CT3 + j) * 16;
     const f32x4 bias = *reinterpret_cast<const f32x4*>(a.bo + n0 + 4 * (lane >> 4));
 #pragma unroll
-    for (int rt = 0; rt < QMAX / 16; ++rt) {
+    for (int rt = 0; rt < QM / 16; ++rt) {
       if (rt >= RT) break;
       f32x4 acc = tile_wx(wf3[j], qkv, QKVLD, rt * 16, lane);
       const int m = rt * 16 + (lane & 15);
@@ -167,7 +169,7 @@ __global__ __launch_bounds__(NT) void decsa_kernel(DecSaArgs a) {
   for (int j = 0; j < CT3; ++j) {
     const int n0 = (wid * CT3 + j) * 16;
 #pragma unroll
-    for (int rt = 0; rt < QMAX / 16; ++rt) {
+    for (int rt = 0; rt < QM / 16; ++rt) {
       if (rt >= RT) break;
       const int m = rt * 16 + (lane & 15);
       *reinterpret_cast<f32x4*>(ys + m * YLD + n0 + 4 * (lane >> 4)) = yo[j][rt];
@@ -195,10 +197,11 @@ __global__ __launch_bounds__(NT) void decsa_kernel(DecSaArgs a) {
 // tgt = LayerNorm(tgt + x . Wo^T + bo) per image: the cross-attention's out-projection + norm2
 // (REV/models/transformer.py:233-234), decsa's phase 3 on its own -- one launch instead of a
 // few-row GEMM and a LayerNorm, the rows never leaving LDS between them.
+template <int QM>
 __global__ __launch_bounds__(NT) void decproj_kernel(DecProjArgs a) {
-  __shared__ __attribute__((aligned(16))) bf16 rs[QMAX * XLD];   // tgt rows (the residual)
-  __shared__ __attribute__((aligned(16))) bf16 xs[QMAX * XLD];   // input rows
-  __shared__ __attribute__((aligned(16))) float ys[QMAX * YLD];
+  __shared__ __attribute__((aligned(16))) bf16 rs[QM * XLD];   // tgt rows (the residual)
+  __shared__ __attribute__((aligned(16))) bf16 xs[QM * XLD];   // input rows
+  __shared__ __attribute__((aligned(16))) float ys[QM * YLD];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int b = blockIdx.x, Q = a.Q, RT = (Q + 15) / 16;
   bf16* tg = (bf16*)a.tgt + (size_t)b * Q * a.ldt;
@@ -218,7 +221,7 @@ __global__ __launch_bounds__(NT) void decproj_kernel(DecProjArgs a) {
     const int n0 = (wid * CT3 + j) * 16;
     const f32x4 bias = *reinterpret_cast<const f32x4*>(a.bo + n0 + 4 * (lane >> 4));
 #pragma unroll
-    for (int rt = 0; rt < QMAX / 16; ++rt) {
+    for (int rt = 0; rt < QM / 16; ++rt) {
       if (rt >= RT) break;
       f32x4 acc = tile_wx(wf[j], xs, XLD, rt * 16, lane);
       const int m = rt * 16 + (lane & 15);
@@ -260,18 +263,16 @@ __global__ __launch_bounds__(NT) void decxproj_kernel(DecProjArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 ul[QX * ULD];
   __shared__ __attribute__((aligned(16))) bf16 rs[QX * XLD];    // tgt rows (the residual)
   __shared__ __attribute__((aligned(16))) bf16 xs[QX * XLD];    // o rows
-  __shared__ float sm[8 * QX], sil[8 * QX];
   float* ys = reinterpret_cast<float*>(uh);                      // fp32 rows once u has been read
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int b = blockIdx.x, Q = a.Q, R = 8 * Q, S = a.splits;
   bf16* tg = (bf16*)a.tgt + (size_t)b * Q * a.ldt;
   // wave wid: head wid of the value projection and columns 32 wid .. +32 of the out-projection;
-  // both sets of W fragments travel while the partials are merged
+  // Wv's fragments travel while the partials are merged
   u32x4 wvf[2][8], wf[2][8];
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
     w_frags(wvf[j], a.wv, 2 * wid + j, lane);
-    w_frags(wf[j], a.wo, 2 * wid + j, lane);
   }
   f32x4 bvv[2], bov[2];                         // biases and the LayerNorm affine: loaded up front too
 #pragma unroll
@@ -290,35 +291,40 @@ __global__ __launch_bounds__(NT) void decxproj_kernel(DecProjArgs a) {
     st16(uh + r * ULD + 8 * c, u32x4{0, 0, 0, 0});
     st16(ul + r * ULD + 8 * c, u32x4{0, 0, 0, 0});
   }
-  // 1. per attention row r = 8 q + h: M = max_s m_s and 1 / sum_s 2^(m_s - M) l_s
+  // 1. u = sum_s 2^(m_s - M) U_s / sum_s 2^(m_s - M) l_s per attention row r = 8 q + h, 16 dims an
+  // item, merged online four splits at a time (all four splits' loads in flight together), into row
+  // q, columns 256 h .. of the planes
   const size_t base = (size_t)b * S * R;
-  if (tid < R) {
-    float M = XNEG;
-    for (int s = 0; s < S; ++s) M = fmaxf(M, a.pm[base + (size_t)s * R + tid]);
-    float L = 0.f;
-    for (int s = 0; s < S; ++s) {
-      const size_t pr = base + (size_t)s * R + tid;
-      L += __builtin_amdgcn_exp2f(a.pm[pr] - M) * a.pl[pr];
-    }
-    sm[tid] = M;
-    sil[tid] = 1.f / L;
-  }
-  __syncthreads();
-  // 2. u = sum_s 2^(m_s - M) U_s / L, 16 dims an item, into row q, columns 256 h .. of the planes
   for (int it = tid; it < R * 16; it += NT) {
     const int r = it >> 4, c = it & 15;
-    const float M = sm[r];
-    const float* pmr = a.pm + base + r;
-    const float* pur = a.pu + (base + r) * D + 16 * c;
+    float M = XNEG, L = 0.f;
     f32x4 u[4] = {};
-#pragma unroll 2
-    for (int s = 0; s < S; ++s) {
-      const float w = __builtin_amdgcn_exp2f(pmr[(size_t)s * R] - M);
-      const f32x4* p = reinterpret_cast<const f32x4*>(pur + (size_t)s * R * D);
+    for (int s0 = 0; s0 < S; s0 += 4) {
+      float ms[4], ls[4];
+      f32x4 us[4][4];
 #pragma unroll
-      for (int g = 0; g < 4; ++g) u[g] += w * p[g];
+      for (int j = 0; j < 4; ++j) {
+        const size_t pr = base + (size_t)min(s0 + j, S - 1) * R + r;
+        ms[j] = s0 + j < S ? a.pm[pr] : XNEG;
+        ls[j] = a.pl[pr];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) us[j][g] = *reinterpret_cast<const f32x4*>(a.pu + pr * D + 16 * c + 4 * g);
+      }
+      const float Mn = fmaxf(fmaxf(M, fmaxf(ms[0], ms[1])), fmaxf(ms[2], ms[3]));
+      const float sc = __builtin_amdgcn_exp2f(M - Mn);
+      L *= sc;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) u[g] *= sc;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float w = __builtin_amdgcn_exp2f(ms[j] - Mn);   // 0 for the padded splits
+        L += w * ls[j];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) u[g] += w * us[j][g];
+      }
+      M = Mn;
     }
-    const float il = sil[r];
+    const float il = 1.f / L;
     uint32_t hi[8], lo[8];
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
@@ -332,6 +338,9 @@ __global__ __launch_bounds__(NT) void decxproj_kernel(DecProjArgs a) {
     st16(ul + off, u32x4{lo[0], lo[1], lo[2], lo[3]});
     st16(ul + off + 8, u32x4{lo[4], lo[5], lo[6], lo[7]});
   }
+  // Wo's fragments travel during the value projection (fetched here, not up front: registers)
+#pragma unroll
+  for (int j = 0; j < 2; ++j) w_frags(wf[j], a.wo, 2 * wid + j, lane);
   __syncthreads();
   // 3. o_h = Wv_h (u_hi + u_lo) + bv_h, bf16 rows into xs
 #pragma unroll
@@ -386,7 +395,8 @@ int spe_launch_decproj(const DecProjArgs& a, hipStream_t s) {
   }
   if (a.Q < 1 || a.Q > QMAX || a.ldt % 8 || a.ldx % 8 || !a.tgt || !a.x || !a.wo || !a.bo || !a.g || !a.b)
     return 1;
-  hipLaunchKernelGGL(decproj_kernel, dim3(a.B), dim3(NT), 0, s, a);
+  if (a.Q <= 16) hipLaunchKernelGGL(decproj_kernel<16>, dim3(a.B), dim3(NT), 0, s, a);
+  else hipLaunchKernelGGL(decproj_kernel<QMAX>, dim3(a.B), dim3(NT), 0, s, a);
   return (int)hipGetLastError();
 }
 
@@ -396,7 +406,8 @@ int spe_launch_decsa(const DecSaArgs& a, hipStream_t s) {
   if (a.Q < 1 || a.Q > QMAX || a.ldt % 8 || !a.tgt || !a.wqk || !a.wv ||
       !a.wo || !a.bqk || !a.bv || !a.bo || !a.qpos || !a.g || !a.b)
     return 1;
-  hipLaunchKernelGGL(decsa_kernel, dim3(a.B), dim3(NT), 0, s, a);
+  if (a.Q <= 16) hipLaunchKernelGGL(decsa_kernel<16>, dim3(a.B), dim3(NT), 0, s, a);
+  else hipLaunchKernelGGL(decsa_kernel<QMAX>, dim3(a.B), dim3(NT), 0, s, a);
   return (int)hipGetLastError();
 }
 
