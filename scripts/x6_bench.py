@@ -32,6 +32,7 @@ def main():
     ap.add_argument("--iters", type=int, default=10)
     ap.add_argument("--only", default="")
     ap.add_argument("--dtypes", default=",".join(DT))
+    ap.add_argument("--batch", type=int, default=64, help="images (the shapes' M scale with it)")
     a = ap.parse_args()
     L = _lib.lib()
     dev = torch.device("cuda", 0)
@@ -41,11 +42,13 @@ def main():
             continue
         if len(sh) == 3:
             M, N, K = sh
+            M = M // 64 * a.batch
             conv = (0, 0, 0, 1, 1, 1, 0)
             A = torch.randn(M, K, device=dev)
             mode = 0
         else:
             B, H, Cin, N, k, st, pd = sh
+            B = a.batch
             Ho = (H + 2 * pd - k) // st + 1
             M, K = B * Ho * Ho, Cin * k * k
             conv = (H, H, Cin, k, k, st, pd)
