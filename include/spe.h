@@ -324,7 +324,8 @@ int spe_debug_layernorm(void* stream, int dtype, const void* x, const float* gam
                         float* out_f32, int M, int D);
 /* ffn (bf16 only): y = LayerNorm(x + W2 relu(W1 x + b1) + b2), D == 256, F % 32 == 0; x and y may
  * alias.  W1 [F][ld1], W2 [D][ld2], biases / LayerNorm affine fp32.  partial (nullable, fp32
- * [splits][M][D]) selects the split-over-F form used for few rows (splits divides F/32). */
+ * [splits][M][D]) selects the split-over-F form used for few rows (splits divides F/32).  ld2 == 0
+ * (ABI 7 addition): W2 is chunk-packed [F/32][D][32], the bf16 model's encoder form. */
 int spe_debug_ffn(void* stream, const void* x, int ldx, const void* w1, int ld1, const float* b1, const void* w2,
                   int ld2, const float* b2, const float* gamma, const float* beta, void* y, int ldy, int M, int D,
                   int F, float* partial, int splits);

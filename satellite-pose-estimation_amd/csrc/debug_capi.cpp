@@ -106,6 +106,10 @@ int spe_debug_ffn(void* stream, const void* x, int ldx, const void* w1, int ld1,
   FfnArgs a{};
   a.x = x; a.ldx = ldx; a.w1 = w1; a.ld1 = ld1; a.b1 = b1; a.w2 = w2; a.ld2 = ld2; a.b2 = b2;
   a.gamma = gamma; a.beta = beta; a.y = y; a.ldy = ldy; a.M = M; a.D = D; a.F = F;
+  if (ld2 == 0) {                               // w2 chunk-packed [F/32][256][32] (the model's bf16 encoder form)
+    a.w2_chunked = 1;
+    a.ld2 = F;
+  }
   a.partial = partial; a.splits = splits;
   int rc = spe_launch_ffn_ln(a, (hipStream_t)stream);
   return rc < 0 ? spe_fail(SPE_E_LAUNCH, "ffn launch rejected its arguments") : rc;

@@ -64,7 +64,8 @@ SPE_DEV void issue_chunk(const FfnArgs& a, int ch, char* st, int wid, int lane) 
 #pragma unroll
   for (int i = 0; i < 4; ++i) {                 // W2: 16 instructions x 16 rows of 64 B
     const int ins = wid * 4 + i, n = 16 * ins + (lane >> 2), c = (lane & 3) ^ w2_key(n);
-    const char* src = (const char*)a.w2 + ((size_t)n * a.ld2 + ch * HC + c * 8) * 2;
+    const char* src = (const char*)a.w2 + (a.w2_chunked ? ((size_t)ch * D * HC + n * HC + c * 8) * 2
+                                                        : ((size_t)n * a.ld2 + ch * HC + c * 8) * 2);
     __builtin_amdgcn_global_load_lds((const void*)src, (lds_ptr_t)(st + W1_BYTES + ins * 1024), 16, 0, 0);
   }
 }
@@ -79,14 +80,14 @@ struct ChunkDma {
   int vo1[4], vo2[4];
   SPE_DEV void init(const FfnArgs& a, int wid, int lane) {
     r1 = __builtin_amdgcn_make_buffer_rsrc((void*)a.w1, (short)0, a.F * a.ld1 * 2, 0x00020000);
-    r2 = __builtin_amdgcn_make_buffer_rsrc((void*)a.w2, (short)0, D * a.ld2 * 2, 0x00020000);
+    r2 = __builtin_amdgcn_make_buffer_rsrc((void*)a.w2, (short)0, D * (a.w2_chunked ? a.F : a.ld2) * 2, 0x00020000);
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int ins = wid * 4 + i;
       const int R = 2 * ins + (lane >> 5), c = (lane & 31) ^ (R & 15);
       vo1[i] = (w1_src_row(R) * a.ld1 + c * 8) * 2;
       const int n = 16 * ins + (lane >> 2), c2 = (lane & 3) ^ w2_key(n);
-      vo2[i] = (n * a.ld2 + c2 * 8) * 2;
+      vo2[i] = ((a.w2_chunked ? n * HC : n * a.ld2) + c2 * 8) * 2;
     }
   }
   // piece i of 8 (0-3: W1, 4-7: W2), for spreading a chunk's DMA between MFMAs
@@ -95,17 +96,20 @@ struct ChunkDma {
       __builtin_amdgcn_raw_ptr_buffer_load_lds(r1, (lds_ptr_t)(st + (wid * 4 + i) * 1024), 16, vo1[i], ch * HC * a.ld1 * 2, 0, 0);
     else
       __builtin_amdgcn_raw_ptr_buffer_load_lds(r2, (lds_ptr_t)(st + W1_BYTES + (wid * 4 + i - 4) * 1024), 16, vo2[i - 4],
-                                               ch * HC * 2, 0, 0);
+                                               so2(a, ch), 0, 0);
   }
   SPE_DEV void issue(const FfnArgs& a, int ch, char* st, int wid) const {
-    const int so1 = ch * HC * a.ld1 * 2, so2 = ch * HC * 2;
+    const int so1 = ch * HC * a.ld1 * 2, s2 = so2(a, ch);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(r1, (lds_ptr_t)(st + (wid * 4 + i) * 1024), 16, vo1[i], so1, 0, 0);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(r2, (lds_ptr_t)(st + W1_BYTES + (wid * 4 + i) * 1024), 16, vo2[i], so2, 0, 0);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(r2, (lds_ptr_t)(st + W1_BYTES + (wid * 4 + i) * 1024), 16, vo2[i], s2, 0, 0);
   }
+  // chunk ch's W2 columns: 64 bytes of every row at a 4 KB row stride, or (w2_chunked) one
+  // contiguous 16 KB block -- the strided form's 256 lines per chunk fall into few L2 sets
+  SPE_DEV static int so2(const FfnArgs& a, int ch) { return a.w2_chunked ? ch * D * HC * 2 : ch * HC * 2; }
 };
 // ReLU of two packed bf16: negative values (sign bit set) are negative as int16
 SPE_DEV uint32_t relu_bf16x2(uint32_t v) {
@@ -571,6 +575,22 @@ int spe_ffn_splits(int M, int F) {
   int s = 1;
   while (s < 32 && (F / HC) % (2 * s) == 0 && ((M + BM - 1) / BM) * 2 * s <= 64) s *= 2;
   return s;
+}
+
+namespace {
+__global__ __launch_bounds__(256) void ffn_w2_chunk_pack_kernel(const bf16* w, int ld, int F, bf16* dst) {
+  const int i = blockIdx.x * 256 + threadIdx.x;   // one 16-byte piece: (chunk, row, 8 columns)
+  if (i >= D * F / 8) return;
+  const int q = i & 3, n = (i >> 2) & (D - 1), ch = i >> 10;
+  st16(dst + (size_t)i * 8, ld16(w + (size_t)n * ld + ch * HC + 8 * q));
+}
+}  // namespace
+
+int spe_launch_ffn_w2_chunk_pack(const void* w2, int ld2, int F, void* dst, hipStream_t s) {
+  if (!w2 || !dst || F < HC || F % HC || ld2 < F || ld2 % 8) return -5;
+  hipLaunchKernelGGL(ffn_w2_chunk_pack_kernel, dim3((D * F / 8 + 255) / 256), dim3(256), 0, s, (const bf16*)w2, ld2, F,
+                     (bf16*)dst);
+  return (int)hipGetLastError();
 }
 
 int spe_launch_ffn_reduce_ln(const FfnArgs& a, hipStream_t s) {

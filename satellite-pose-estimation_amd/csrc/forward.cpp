@@ -103,14 +103,16 @@ GemmArgs linear_args(const Conv& c, const void* A, int lda, int M, void* C, int 
 
 // Fused linear1 -> ReLU -> linear2 -> +residual -> LayerNorm over x (in place), bf16 models.
 int run_ffn(spe_model* m, const char* kind, const Conv& l1, const Conv& l2, const float* g, const float* b,
-            void* x, int M, hipStream_t s, const void* pos, void* ypos, int period, float* partial) {
+            void* x, int M, hipStream_t s, const void* pos, void* ypos, int period, float* partial,
+            const void* w2_chunked) {
   FfnArgs a{};
   a.pos = pos; a.ypos = ypos; a.pos_period = period;
   a.splits = partial ? spe_ffn_splits(M, l1.N) : 1;
   a.partial = a.splits > 1 ? partial : nullptr;
   a.x = x; a.ldx = l1.K;
   a.w1 = l1.w; a.ld1 = l1.Kpad; a.b1 = l1.bias;
-  a.w2 = l2.w; a.ld2 = l2.Kpad; a.b2 = l2.bias;
+  a.w2 = w2_chunked ? w2_chunked : l2.w; a.ld2 = l2.Kpad; a.b2 = l2.bias;
+  a.w2_chunked = w2_chunked != nullptr;        // W2 chunk-packed at finalize (ffn.hip)
   a.gamma = g; a.beta = b;
   a.y = x; a.ldy = l1.K;
   a.M = M; a.D = l1.K; a.F = l1.N;
@@ -454,7 +456,7 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       // the last layer also emits memory + pos for the cross-K projection (xattn adds pos itself)
       const bool last = &e == &m->enc.back();
       CK(run_ffn(m, "ffn.enc", e.l1, e.l2, e.n2g, e.n2b, P(w.src), Mt, s, last ? m->pos : nullptr,
-                 last ? P(w.srcpos) : nullptr, T));
+                 last ? P(w.srcpos) : nullptr, T, nullptr, e.ffn_w2c));
     } else if (m->h3 && e.ffn_w2p && src_amax && m->wh3.count(e.l1.w)) {
       // fp32h3: linear1 + ReLU + linear2 + residual + norm2 in one pass, in place over src
       FfnH3Args a{};

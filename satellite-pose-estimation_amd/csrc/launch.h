@@ -13,4 +13,4 @@ GemmArgs linear_args(const Conv& c, const void* A, int lda, int M, void* C, int 
 GemmArgs conv_args(const Conv& c, const void* X, int B, int H, int W, void* Y, int ldc);
 int run_ffn(spe_model* m, const char* kind, const Conv& l1, const Conv& l2, const float* g, const float* b, void* x,
             int M, hipStream_t s, const void* pos = nullptr, void* ypos = nullptr, int period = 0,
-            float* partial = nullptr);
+            float* partial = nullptr, const void* w2_chunked = nullptr);

@@ -37,6 +37,7 @@ struct Enc {
   float* ffn_meta1 = nullptr;
   void* ffn_w2p = nullptr;
   float ffn_sh = 0.f;
+  void* ffn_w2c = nullptr;  // bf16: linear2's weight chunk-packed for the fused FFN (spe_launch_ffn_w2_chunk_pack)
 };
 
 struct Dec {

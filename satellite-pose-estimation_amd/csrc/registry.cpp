@@ -583,6 +583,8 @@ int build_device(spe_model* m) {
       e.n2_bound = ln_bound(m, p + ".norm2", d);
       ffn_h3_prepare(m, e, p, d, ff);
     }
+    // bf16 fused FFN: linear2 chunk-packed at finalize (each 32-unit chunk's columns contiguous)
+    if (m->cfg.dtype == SPE_DTYPE_BF16_ && d == 256 && ff % 32 == 0) e.ffn_w2c = dalloc(m, (size_t)d * ff * 2);
     m->enc.push_back(e);
   }
   m->dec.clear();
@@ -821,7 +823,10 @@ int spe_model_finalize(spe_model* m) {
       return spe_launch_gemm(g, m->esz == 2 ? SPE_DTYPE_BF16 : SPE_DTYPE_F32, GEMM_LINEAR, nullptr);
     };
     int rc = 0;
-    for (auto& l : m->enc) rc |= proj(m->pos, T, l.qk, l.pos_qk);
+    for (auto& l : m->enc) {
+      rc |= proj(m->pos, T, l.qk, l.pos_qk);
+      if (l.ffn_w2c) rc |= spe_launch_ffn_w2_chunk_pack(l.l2.w, l.l2.Kpad, l.l2.K, l.ffn_w2c, nullptr);
+    }
     if (m->pos_crossK) rc |= proj(m->pos, T, m->crossK, m->pos_crossK);
     for (auto& l : m->dec) {
       rc |= proj(m->qpos, Q, l.sqk, l.qpos_sqk);

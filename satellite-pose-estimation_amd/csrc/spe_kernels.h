@@ -192,7 +192,10 @@ struct FfnArgs {
   int pos_period;
   int splits; float* partial;      // optional split over F for few rows: fp32 [splits][M][256] workspace
   int row0;                        // first row of this launch's tiles (internal: the FFN tail launch)
+  int w2_chunked;                  // w2 stored chunk-packed [F/32][256][32] (spe_launch_ffn_w2_chunk_pack); ld2 unused
 };
+// W2 [256][ld2] bf16 -> [F/32][256][32]: each 32-unit hidden chunk's columns as one contiguous block
+int spe_launch_ffn_w2_chunk_pack(const void* w2, int ld2, int F, void* dst, hipStream_t s);
 int spe_launch_ffn_ln(const FfnArgs& a, hipStream_t s);
 // y = LN(x + sum_s partial[s] + b2) over a.splits fp32 partials [splits][M][256] (ffn.hip)
 int spe_launch_ffn_reduce_ln(const FfnArgs& a, hipStream_t s);

@@ -89,6 +89,11 @@ def main():
         ms = timeit(fn, a.iters)
         fl = 4.0 * B * T * D * F
         print(f"ffn.enc   {ms:.3f} ms  {fl / ms / 1e9:.1f} TF/s")
+        w2c = w2.view(D, F // 32, 32).permute(1, 0, 2).contiguous()     # chunk-packed W2 (the model's form)
+        fn = lambda: L.spe_debug_ffn(None, p(x), D, p(w1), D, p(b1), p(w2c), 0, p(b2), p(gm), p(bt), p(y), D,
+                                     B * T, D, F, None, 0)
+        ms = timeit(fn, a.iters)
+        print(f"ffn.enc chunk-packed W2  {ms:.3f} ms  {fl / ms / 1e9:.1f} TF/s")
     if a.which in ("ffndec", "all"):
         # the decoder's few-row FFN (M = B * 11): split-F partials over `splits` workgroups per
         # 128-row tile, then the reduce + LayerNorm kernel

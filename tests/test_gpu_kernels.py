@@ -591,14 +591,16 @@ def test_attention_large_score_range(gpu_device, mode, gain):
     _close(O, ref, 2e-2)
 
 
+@pytest.mark.parametrize("chunked", [0, 1])
 @pytest.mark.parametrize("M,F,inplace,splits", [(333, 2048, True, 0), (128, 64, False, 0), (1000, 2048, False, 0),
                                                 (5, 32, True, 0), (704, 2048, True, 16), (300, 2048, False, 32),
                                                 (77, 128, False, 2), (17003, 2048, False, 0), (640, 1024, True, 0),
                                                 # whole 192-row rounds + a 128-row tail launch on 256 CUs
                                                 (54152, 2048, True, 0), (70000, 2048, False, 0)])
-def test_fused_ffn(gpu_device, M, F, inplace, splits):
+def test_fused_ffn(gpu_device, M, F, inplace, splits, chunked):
     """bf16 fused linear1 -> ReLU -> linear2 -> +x -> LayerNorm against torch fp32 on bf16-rounded
-    operands; the hidden activation is rounded to bf16 on chip exactly as the unfused path stores it."""
+    operands; the hidden activation is rounded to bf16 on chip exactly as the unfused path stores it.
+    chunked: W2 passed chunk-packed [F/32][256][32] (ld2 = 0), the bf16 model's encoder form."""
     dt, D = torch.bfloat16, 256
     g = torch.Generator(device="cpu").manual_seed(M + F)
     ld = D + 8 if not inplace else D
@@ -614,8 +616,9 @@ def test_fused_ffn(gpu_device, M, F, inplace, splits):
     ref = F_.layer_norm(xs + h @ w2.float().t() + b2, (D,), gam, bet, 1e-5)
     y = x if inplace else torch.full((M, ld), 7.0, dtype=dt, device=gpu_device)
     part = torch.empty(max(splits, 1), M, D, device=gpu_device) if splits else None
-    rc = _lib.lib().spe_debug_ffn(None, _p(x), ld, _p(w1), D, _p(b1), _p(w2), F, _p(b2), _p(gam), _p(bet), _p(y), ld,
-                                  M, D, F, _p(part), splits)
+    w2a, ld2 = (w2.view(D, F // 32, 32).permute(1, 0, 2).contiguous(), 0) if chunked else (w2, F)
+    rc = _lib.lib().spe_debug_ffn(None, _p(x), ld, _p(w1), D, _p(b1), _p(w2a), ld2, _p(b2), _p(gam), _p(bet), _p(y),
+                                  ld, M, D, F, _p(part), splits)
     assert rc == 0, _lib.lib().spe_last_error()
     torch.cuda.synchronize()
     _close(y[:, :D], ref, 3e-2)
