@@ -366,7 +366,7 @@ int spe_debug_decproj(void* stream, void* tgt, int ldt, const void* x, int ldx, 
 /* decxproj (bf16 only, decsa.hip, ABI 7 addition): the cross-attention's tail in place over tgt:
  * merges the key-split partials spe_debug_xattn left in partial_scratch (same B, Q, T, splits),
  * o[b*Q+q][h*32 + j] = wv[h*32 + j] . u_h + bv[h*32 + j] rounded to bf16, then
- * tgt = LayerNorm(tgt + o . wo^T + bo) -- xattn's merge kernel and decproj as one launch, Q <= 16. */
+ * tgt = LayerNorm(tgt + o . wo^T + bo) -- xattn's merge kernel and decproj as one launch, Q <= 48. */
 int spe_debug_decxproj(void* stream, void* tgt, int ldt, float* partial_scratch, int splits, int T, int B, int Q,
                        const void* wv, int ldwv, const float* bv, const void* wo, int ldo, const float* bo,
                        const float* g, const float* b);

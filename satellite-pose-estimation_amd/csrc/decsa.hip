@@ -250,30 +250,28 @@ __global__ __launch_bounds__(NT) void decproj_kernel(DecProjArgs a) {
   }
 }
 
-// The cross-attention's tail and its out-projection + norm2 as one launch per layer (Q <= 16):
+// The cross-attention's tail and its out-projection + norm2 as one launch per layer (Q <= 48):
 //   u_h = the key-split merge of xattn.hip's partials, o_h = Wv_h u_h + bv_h rounded to bf16 (the
 //   rounding the separate merge kernel stored), tgt = LayerNorm(tgt + o . Wo^T + bo)
 // (REV/models/transformer.py:230-234) -- xattn's merge + value-projection kernel and decproj as one
 // launch, u never leaving LDS.  u enters the value projection's bf16 MFMAs as hi + lo planes (u to
-// about 2^-17 relative, as the separate kernel's fp32 FMAs had it).
-constexpr int QX = 16, ULD = 8 * D + 8;    // u planes [16][2048 + 8] bf16: 4112 B rows, conflict-free b128 reads
+// about 2^-17 relative, as the separate kernel's fp32 FMAs had it), 16 queries at a time.
+constexpr int QX = 16, QXM = 48, ULD = 8 * D + 8;   // u planes [16][2048 + 8] bf16: 4112 B rows, conflict-free b128 reads
 constexpr float XNEG = -1.0e30f;
 __global__ __launch_bounds__(NT) void decxproj_kernel(DecProjArgs a) {
   __shared__ __attribute__((aligned(16))) bf16 uh[QX * ULD];
   __shared__ __attribute__((aligned(16))) bf16 ul[QX * ULD];
-  __shared__ __attribute__((aligned(16))) bf16 rs[QX * XLD];    // tgt rows (the residual)
-  __shared__ __attribute__((aligned(16))) bf16 xs[QX * XLD];    // o rows
+  __shared__ __attribute__((aligned(16))) bf16 xs[QXM * XLD];   // o rows
   float* ys = reinterpret_cast<float*>(uh);                      // fp32 rows once u has been read
+  static_assert(QXM * YLD * 4 <= QX * ULD * 2, "ys fits the hi plane");
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
-  const int b = blockIdx.x, Q = a.Q, R = 8 * Q, S = a.splits;
+  const int b = blockIdx.x, Q = a.Q, R = 8 * Q, S = a.splits, QC = (Q + QX - 1) / QX;
   bf16* tg = (bf16*)a.tgt + (size_t)b * Q * a.ldt;
   // wave wid: head wid of the value projection and columns 32 wid .. +32 of the out-projection;
-  // Wv's fragments travel while the partials are merged
+  // Wv's fragments travel while the first partials are merged
   u32x4 wvf[2][8], wf[2][8];
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    w_frags(wvf[j], a.wv, 2 * wid + j, lane);
-  }
+  for (int j = 0; j < 2; ++j) w_frags(wvf[j], a.wv, 2 * wid + j, lane);
   f32x4 bvv[2], bov[2];                         // biases and the LayerNorm affine: loaded up front too
 #pragma unroll
   for (int j = 0; j < 2; ++j) {
@@ -282,90 +280,101 @@ __global__ __launch_bounds__(NT) void decxproj_kernel(DecProjArgs a) {
   }
   const f32x4 gm = *reinterpret_cast<const f32x4*>(a.g + 4 * lane);
   const f32x4 bt = *reinterpret_cast<const f32x4*>(a.b + 4 * lane);
-  for (int i = tid; i < QX * (D / 8); i += NT) {
-    const int r = i / (D / 8), c = i % (D / 8);
-    st16(rs + r * XLD + 8 * c, r < Q ? ld16(tg + (size_t)r * a.ldt + 8 * c) : u32x4{0, 0, 0, 0});
-  }
-  for (int i = tid; i < (QX - Q) * D; i += NT) {   // u rows past Q: zero (8 x 256 values = 256 chunks a row)
-    const int r = Q + i / D, c = i % D;
-    st16(uh + r * ULD + 8 * c, u32x4{0, 0, 0, 0});
-    st16(ul + r * ULD + 8 * c, u32x4{0, 0, 0, 0});
-  }
-  // 1. u = sum_s 2^(m_s - M) U_s / sum_s 2^(m_s - M) l_s per attention row r = 8 q + h, 16 dims an
-  // item, merged online four splits at a time (all four splits' loads in flight together), into row
-  // q, columns 256 h .. of the planes
   const size_t base = (size_t)b * S * R;
-  for (int it = tid; it < R * 16; it += NT) {
-    const int r = it >> 4, c = it & 15;
-    float M = XNEG, L = 0.f;
-    f32x4 u[4] = {};
-    for (int s0 = 0; s0 < S; s0 += 4) {
-      float ms[4], ls[4];
-      f32x4 us[4][4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const size_t pr = base + (size_t)min(s0 + j, S - 1) * R + r;
-        ms[j] = s0 + j < S ? a.pm[pr] : XNEG;
-        ls[j] = a.pl[pr];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) us[j][g] = *reinterpret_cast<const f32x4*>(a.pu + pr * D + 16 * c + 4 * g);
-      }
-      const float Mn = fmaxf(fmaxf(M, fmaxf(ms[0], ms[1])), fmaxf(ms[2], ms[3]));
-      const float sc = __builtin_amdgcn_exp2f(M - Mn);
-      L *= sc;
-#pragma unroll
-      for (int g = 0; g < 4; ++g) u[g] *= sc;
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float w = __builtin_amdgcn_exp2f(ms[j] - Mn);   // 0 for the padded splits
-        L += w * ls[j];
-#pragma unroll
-        for (int g = 0; g < 4; ++g) u[g] += w * us[j][g];
-      }
-      M = Mn;
+  // 1. u = sum_s 2^(m_s - M) U_s / sum_s 2^(m_s - M) l_s per attention row r = 8 q + h of queries
+  // q0 .. q0 + 16, 16 dims an item, merged online four splits at a time (all four splits' loads in
+  // flight together), into plane row q - q0, columns 256 h ..
+  auto merge = [&](int q0) {
+    const int nq = min(QX, Q - q0);
+    for (int i = tid; i < (QX - nq) * D; i += NT) {   // plane rows past the queries: zero (256 chunks a row)
+      const int r = nq + i / D, c = i % D;
+      st16(uh + r * ULD + 8 * c, u32x4{0, 0, 0, 0});
+      st16(ul + r * ULD + 8 * c, u32x4{0, 0, 0, 0});
     }
-    const float il = 1.f / L;
-    uint32_t hi[8], lo[8];
+    for (int it = tid; it < 8 * nq * 16; it += NT) {
+      const int r = 8 * q0 + (it >> 4), c = it & 15;
+      float M = XNEG, L = 0.f;
+      f32x4 u[4] = {};
+      for (int s0 = 0; s0 < S; s0 += 4) {
+        float ms[4], ls[4];
+        f32x4 us[4][4];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float x0 = u[e >> 1][2 * (e & 1)] * il, x1 = u[e >> 1][2 * (e & 1) + 1] * il;
-      hi[e] = pack_bf16x2(x0, x1);
-      lo[e] = pack_bf16x2(x0 - __uint_as_float(hi[e] << 16), x1 - __uint_as_float(hi[e] & 0xffff0000u));
+        for (int j = 0; j < 4; ++j) {
+          const size_t pr = base + (size_t)min(s0 + j, S - 1) * R + r;
+          ms[j] = s0 + j < S ? a.pm[pr] : XNEG;
+          ls[j] = a.pl[pr];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) us[j][g] = *reinterpret_cast<const f32x4*>(a.pu + pr * D + 16 * c + 4 * g);
+        }
+        const float Mn = fmaxf(fmaxf(M, fmaxf(ms[0], ms[1])), fmaxf(ms[2], ms[3]));
+        const float sc = __builtin_amdgcn_exp2f(M - Mn);
+        L *= sc;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) u[g] *= sc;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float w = __builtin_amdgcn_exp2f(ms[j] - Mn);   // 0 for the padded splits
+          L += w * ls[j];
+#pragma unroll
+          for (int g = 0; g < 4; ++g) u[g] += w * us[j][g];
+        }
+        M = Mn;
+      }
+      const float il = 1.f / L;
+      uint32_t hi[8], lo[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float x0 = u[e >> 1][2 * (e & 1)] * il, x1 = u[e >> 1][2 * (e & 1) + 1] * il;
+        hi[e] = pack_bf16x2(x0, x1);
+        lo[e] = pack_bf16x2(x0 - __uint_as_float(hi[e] << 16), x1 - __uint_as_float(hi[e] & 0xffff0000u));
+      }
+      const int off = ((r >> 3) - q0) * ULD + (r & 7) * D + 16 * c;
+      st16(uh + off, u32x4{hi[0], hi[1], hi[2], hi[3]});
+      st16(uh + off + 8, u32x4{hi[4], hi[5], hi[6], hi[7]});
+      st16(ul + off, u32x4{lo[0], lo[1], lo[2], lo[3]});
+      st16(ul + off + 8, u32x4{lo[4], lo[5], lo[6], lo[7]});
     }
-    const int off = (r >> 3) * ULD + (r & 7) * D + 16 * c;
-    st16(uh + off, u32x4{hi[0], hi[1], hi[2], hi[3]});
-    st16(uh + off + 8, u32x4{hi[4], hi[5], hi[6], hi[7]});
-    st16(ul + off, u32x4{lo[0], lo[1], lo[2], lo[3]});
-    st16(ul + off + 8, u32x4{lo[4], lo[5], lo[6], lo[7]});
+  };
+  // 2. o_h = Wv_h (u_hi + u_lo) + bv_h, bf16 rows q0 .. into xs
+  auto value_proj = [&](int q0) {
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int n0 = 32 * wid + 16 * j;
+      f32x4 acc = tile_wx(wvf[j], uh + wid * D, ULD, 0, lane);
+      acc = tile_wx(wvf[j], ul + wid * D, ULD, 0, lane, acc);
+      const f32x4 bias = bvv[j];
+      st8(xs + (q0 + (lane & 15)) * XLD + n0 + 4 * (lane >> 4),
+          u32x2{pack_bf16x2(acc[0] + bias[0], acc[1] + bias[1]), pack_bf16x2(acc[2] + bias[2], acc[3] + bias[3])});
+    }
+  };
+  for (int rc = 0; rc + 1 < QC; ++rc) {
+    merge(QX * rc);
+    __syncthreads();
+    value_proj(QX * rc);
+    __syncthreads();                            // the planes free for the next queries
   }
-  // Wo's fragments travel during the value projection (fetched here, not up front: registers)
+  merge(QX * (QC - 1));
+  // Wo's fragments travel during the last value projection (not up front: registers)
 #pragma unroll
   for (int j = 0; j < 2; ++j) w_frags(wf[j], a.wo, 2 * wid + j, lane);
   __syncthreads();
-  // 3. o_h = Wv_h (u_hi + u_lo) + bv_h, bf16 rows into xs
+  value_proj(QX * (QC - 1));
+  __syncthreads();                              // o visible; the hi plane becomes ys
+  // 3. out-projection + bo + residual (tgt as stored), then the LayerNorm (decproj's phases)
+  for (int rt = 0; rt < QC; ++rt) {
 #pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int n0 = 32 * wid + 16 * j;
-    f32x4 acc = tile_wx(wvf[j], uh + wid * D, ULD, 0, lane);
-    acc = tile_wx(wvf[j], ul + wid * D, ULD, 0, lane, acc);
-    const f32x4 bias = bvv[j];
-    st8(xs + (lane & 15) * XLD + n0 + 4 * (lane >> 4),
-        u32x2{pack_bf16x2(acc[0] + bias[0], acc[1] + bias[1]), pack_bf16x2(acc[2] + bias[2], acc[3] + bias[3])});
-  }
-  __syncthreads();                              // o visible; u dead (ys reuses its plane)
-  // 4. out-projection + bo + residual, then the LayerNorm (decproj's phases)
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int n0 = 32 * wid + 16 * j;
-    const f32x4 bias = bov[j];
-    f32x4 acc = tile_wx(wf[j], xs, XLD, 0, lane);
-    const int m = lane & 15;
-    const u32x2 r = ld8(rs + m * XLD + n0 + 4 * (lane >> 4));
-    acc[0] += bias[0] + __uint_as_float(r.x << 16);
-    acc[1] += bias[1] + __uint_as_float(r.x & 0xffff0000u);
-    acc[2] += bias[2] + __uint_as_float(r.y << 16);
-    acc[3] += bias[3] + __uint_as_float(r.y & 0xffff0000u);
-    *reinterpret_cast<f32x4*>(ys + m * YLD + n0 + 4 * (lane >> 4)) = acc;
+    for (int j = 0; j < 2; ++j) {
+      const int n0 = 32 * wid + 16 * j;
+      const f32x4 bias = bov[j];
+      f32x4 acc = tile_wx(wf[j], xs, XLD, 16 * rt, lane);
+      const int m = 16 * rt + (lane & 15);
+      const u32x2 r = m < Q ? ld8(tg + (size_t)m * a.ldt + n0 + 4 * (lane >> 4)) : u32x2{0, 0};
+      acc[0] += bias[0] + __uint_as_float(r.x << 16);
+      acc[1] += bias[1] + __uint_as_float(r.x & 0xffff0000u);
+      acc[2] += bias[2] + __uint_as_float(r.y << 16);
+      acc[3] += bias[3] + __uint_as_float(r.y & 0xffff0000u);
+      *reinterpret_cast<f32x4*>(ys + m * YLD + n0 + 4 * (lane >> 4)) = acc;
+    }
   }
   __syncthreads();
   for (int m = wid; m < Q; m += NW) {
@@ -387,7 +396,7 @@ __global__ __launch_bounds__(NT) void decxproj_kernel(DecProjArgs a) {
 int spe_launch_decproj(const DecProjArgs& a, hipStream_t s) {
   if (a.B <= 0) return 0;
   if (a.pm) {                                   // the merge form (x comes from the partials)
-    if (a.Q < 1 || a.Q > QX || a.splits < 1 || a.ldt % 8 || !a.pl || !a.pu || !a.wv ||
+    if (a.Q < 1 || a.Q > QXM || a.splits < 1 || a.ldt % 8 || !a.pl || !a.pu || !a.wv ||
         !a.bv || !a.tgt || !a.wo || !a.bo || !a.g || !a.b)
       return 1;
     hipLaunchKernelGGL(decxproj_kernel, dim3(a.B), dim3(NT), 0, s, a);

@@ -615,9 +615,9 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       x.o = P(w.dao); x.ldo = d;
       x.B = B; x.Q = Q; x.T = T; x.splits = spe_xattn_splits(B, Q, T);
       x.pm = (float*)P(w.xpm); x.pl = (float*)P(w.xpl); x.pu = (float*)P(w.xpu);
-      // Q <= 16: the split merge and the value projection move into the out-projection + norm2
+      // Q <= 48: the split merge and the value projection move into the out-projection + norm2
       // launch (decsa.hip decxproj_kernel), the per-split partials its only input
-      xtail = decproj_on && e.fxv && Q <= 16;
+      xtail = decproj_on && e.fxv && Q <= 48;
       x.partials_only = xtail;
       const double fl = 4.0 * B * 8.0 * Q * (double)T * d + (xtail ? 0.0 : 2.0 * Mq * 8.0 * d * 32);
       const double by = 2.0 * B * (double)T * d * m->esz + 2.0 * Mq * 8.0 * d * m->esz;

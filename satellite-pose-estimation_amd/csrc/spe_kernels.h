@@ -151,7 +151,7 @@ struct DecProjArgs {
   int B, Q;
   const void* wo; const float* bo; // out_proj (packed)
   const float* g; const float* b;
-  // merge form (pm set, Q <= 16): x is the cross-attention's output computed here from xattn's
+  // merge form (pm set, Q <= 48): x is the cross-attention's output computed here from xattn's
   // key-split partials (XattnArgs::partials_only) -- o_h = Wv_h u_h + bv_h, heads of 32
   const float *pm, *pl, *pu; int splits;
   const void* wv; const float* bv; // value rows of in_proj (packed)

@@ -670,10 +670,13 @@ def test_cross_attention_memory(gpu_device, B, Q, T, splits, amp):
 
 
 @pytest.mark.parametrize("B,Q,T,splits,amp", [(3, 11, 200, 1, 1.0), (2, 11, 203, 3, 1.0), (1, 16, 136, 2, 1.0),
-                                              (64, 11, 2704, 0, 1.0), (2, 5, 640, 4, 12.0), (1, 1, 2704, 0, 1.0)])
+                                              (64, 11, 2704, 0, 1.0), (2, 5, 640, 4, 12.0), (1, 1, 2704, 0, 1.0),
+                                              (16, 40, 6400, 0, 1.0), (2, 33, 300, 5, 12.0), (1, 48, 64, 1, 1.0),
+                                              (3, 17, 200, 2, 1.0)])
 def test_cross_attention_tail_fused(gpu_device, B, Q, T, splits, amp):
     """decxproj (decsa.hip): the key-split merge of xattn's partials, the value projection
-    o_h = Wv_h u_h + bv_h (bf16) and tgt = LN(tgt + o . Wo^T + bo) in one launch per image
+    o_h = Wv_h u_h + bv_h (bf16) and tgt = LN(tgt + o . Wo^T + bo) in one launch per image, 16
+    queries per pass (Q = 40 at 6400 keys: BASELINE config 5's shape)
     (REV/models/transformer.py:230-234), against torch fp32 on the same bf16 operands with the
     separate path's rounding of o.  The partials come from the xattn kernel itself; 2e-2 * scale."""
     dt, D = torch.bfloat16, 256
