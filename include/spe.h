@@ -18,7 +18,7 @@
 extern "C" {
 #endif
 
-#define SPE_ABI_VERSION 7
+#define SPE_ABI_VERSION 8
 
 enum {
   SPE_E_ARG = -1,        /* bad argument / size */
@@ -317,7 +317,9 @@ int spe_debug_gemm_planes(void* stream, int dtype, int mode, const void* A, int 
                           const void* planes, int plane_rows);
 /* attention: dtype | 0x100 = V^T in the 16-bit DMA kernel's key order; dtype SPE_DTYPE_F32X3_ | 0x200 =
  * k and vt given as bf16 hi planes ([B*Tk][ldk] and [B][H][32][Tk]), each followed by its lo plane
- * (what the fp32x3 / fp32x6 models' projection epilogues write; Tk % 8 == 0) */
+ * (what the fp32x3 / fp32x6 models' projection epilogues write; Tk % 8 == 0); | 0x200 | 0x100 = those
+ * planes with V^T in that key order (Tk % 16 == 0: the LDS-DMA split kernel, attn_split.hip), and
+ * | 0x400 on top = the V^T planes as fp16 hi / lo (the fp32h3 model's form, here unscaled) (ABI 8) */
 int spe_debug_attention(void* stream, int dtype, const void* q, int ldq, const void* k, int ldk, const void* vt,
                         void* o, int ldo, int B, int H, int Tq, int Tk, float scale);
 int spe_debug_layernorm(void* stream, int dtype, const void* x, const float* gamma, const float* beta, void* out,

@@ -824,7 +824,12 @@ int spe_launch_attention(const AttnArgs& a, int dtype, hipStream_t s) {
   if (a.B <= 0 || a.Tq <= 0 || a.Tk <= 0) return 0;
   const int ce = (dtype == SPE_DTYPE_F32 || dtype == SPE_DTYPE_F32X3) ? 4 : 8;
   if ((a.ldq % ce) || (a.ldk % ce) || (a.ldo % 4)) return -5;
-  if (a.presplit && (dtype != SPE_DTYPE_F32X3 || a.Tk % 8 || a.ldk % 8 || a.vt_swz)) return -5;
+  if (a.presplit && (dtype != SPE_DTYPE_F32X3 || a.Tk % 8 || a.ldk % 8)) return -5;
+  if (a.v_f16 && !(a.presplit && a.vt_swz)) return -5;
+  if (a.presplit && a.vt_swz) {                    // V^T planes in vt_pos order: the LDS-DMA split kernel
+    const int rc = spe_launch_attention_split(a, s);
+    return rc == 1 ? -5 : rc;
+  }
   dim3 grid(a.B * a.H * ((a.Tq + 127) / 128)), block(NT);
   if (a.vt_swz && (a.Tk % 16 || (dtype != SPE_DTYPE_F16 && dtype != SPE_DTYPE_BF16 && dtype != SPE_DTYPE_BF16_F16V)))
     return -5;                                     // (swizzled V^T: 16-bit operands, whole quads per row)

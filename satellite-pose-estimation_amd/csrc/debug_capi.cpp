@@ -63,8 +63,10 @@ int spe_debug_gemm_h3(void* stream, int mode, const void* A, int lda, int H, int
   g.bias = bias; g.R = R; g.ldr = ldr; g.act = act_code & 255; g.C = C; g.ldc = ldc;
   g.H3 = planes; g.h3_rows = plane_rows; g.h3_sinv = sinv; g.amax_a = amax_a; g.amax_c = amax_c;
   g.amax_c_mul = amax_c_mul;
-  const int rc = spe_launch_gemm(g, SPE_DTYPE_F32H3, mode, (hipStream_t)stream);
-  if (rc == 0 && spe_gemm_last_path != 7 && spe_gemm_last_path != 8) return spe_fail(SPE_E_LAUNCH, "shape not served by the fp32h3 kernel");
+  // (the h3 kernels only: through spe_launch_gemm an unserved shape would run the x6 kernel, which
+  // reads the fp16 planes as fp32 weights)
+  const int rc = spe_launch_gemm_h3(g, mode, (hipStream_t)stream);
+  if (rc == 1) return spe_fail(SPE_E_LAUNCH, "shape not served by the fp32h3 kernel");
   return rc < 0 ? spe_fail(SPE_E_LAUNCH, "gemm launch rejected its arguments") : rc;
 }
 
@@ -90,6 +92,7 @@ int spe_debug_attention(void* stream, int dtype, const void* q, int ldq, const v
   a.B = B; a.H = H; a.Tq = Tq; a.Tk = Tk; a.scale = scale;
   a.vt_swz = (dtype >> 8) & 1;
   a.presplit = (dtype >> 9) & 1;
+  a.v_f16 = (dtype >> 10) & 1;                     // (unscaled fp16 V^T planes: v_amax null)
   int rc = spe_launch_attention(a, dtype & 255, (hipStream_t)stream);
   return rc < 0 ? spe_fail(SPE_E_LAUNCH, "attention launch rejected its arguments") : rc;
 }

@@ -407,6 +407,10 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
   // fp32 K / V^T, split per tile inside the attention)
   static const int ps_env = [] { const char* e = getenv("SPE_ATTN_PRESPLIT"); return e ? atoi(e) : 1; }();
   const bool presplit = ps_env && w.kpl && x3_for(m, "attn.enc") && T % 8 == 0;
+  // ... with V^T in the 16-bit key order (T % 16 == 0): the LDS-DMA split kernel (attn_split.hip); the
+  // fp32h3 model's V^T planes are then fp16 of V * 2^-ev, ev from max |src| . max_n |Wv[n]|_1 + max |bv|
+  const int split_swz = presplit && T % 16 == 0;
+  const int split_f16 = split_swz && m->h3 && src_amax0;
   for (const Enc& e : m->enc) {
     {
       GemmArgs g = linear_args(e.qk, P(w.src), d, Mt, P(w.qkv), 3 * d);
@@ -423,6 +427,8 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       g.amax_a = src_amax; g.amax_c = tam ? tam + 2 * li : nullptr;
       g.out_f16 = f16attn || f16v;
       if (presplit) g.S = P(w.vt);               // hi plane then lo plane, in the fp32 V^T's bytes
+      if (split_swz) g.vt_swz = 1;
+      if (split_f16) { g.s_f16 = 1; g.s_l1 = e.v.l1max; g.s_bmax = e.v.bmax; }
       CK(run_gemm(m, "gemm.enc.v", g, GEMM_LINEAR, s));
     }
     {
@@ -430,7 +436,8 @@ int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, v
       a.q = P(w.qkv); a.ldq = 3 * d;
       a.k = presplit ? P(w.kpl) : (char*)P(w.qkv) + d * m->esz; a.ldk = presplit ? d : 3 * d;
       a.presplit = presplit;
-      a.vt = P(w.vt); a.vt_swz = vt_swz;
+      a.vt = P(w.vt); a.vt_swz = vt_swz || split_swz;
+      if (split_f16) { a.v_f16 = 1; a.v_amax = src_amax; a.v_l1 = e.v.l1max; a.v_bmax = e.v.bmax; }
       a.o = P(w.ao); a.ldo = d;
       a.B = B; a.H = c.nheads; a.Tq = T; a.Tk = T; a.scale = scale;
       CK(run_attn(m, "attn.enc", a, attn_dt, s));

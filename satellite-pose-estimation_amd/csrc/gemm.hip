@@ -234,25 +234,42 @@ SPE_DEV float store_tile(const GemmArgs& g, const float* ct, int m0, int n0, int
       const int b = m / g.vt_T, tok = m - b * g.vt_T;
       const size_t rowbase = ((size_t)(grp * g.vt_B + b) * 256 + hd) * g.vt_T;
       if constexpr (sizeof(T) == 4) {
-        if (g.S) {                               // bf16 hi / lo planes (fp32x3 attention operands)
+        if (g.S) {                               // bf16 (fp16: s_f16) hi / lo planes (split attention operands)
           const size_t lo = (size_t)g.vt_B * g.N * g.vt_T;
-          if ((g.vt_T & 7) == 0 && m + 8 <= g.M) {   // 8 consecutive tokens of one row: 16-byte stores
-            float hv[8], lv[8];
+          const float sf = g.s_f16 ? vplane_scale(g.amax_a, g.s_l1, g.s_bmax) : 1.f;
+          if ((g.vt_T & 7) == 0 && m + 8 <= g.M) {   // 8 consecutive tokens of one row: two quads
+            u32x2 hq[2], lq[2];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              hv[e] = to_f32(from_f32<bf16>(v[e]));
-              lv[e] = v[e] - hv[e];
+            for (int qd = 0; qd < 2; ++qd) {
+              float w[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) w[e] = v[4 * qd + e] * sf;
+              if (g.s_f16) {
+                split_f16x4(w, hq[qd], lq[qd]);
+              } else {
+                hq[qd] = u32x2{pack_bf16x2(w[0], w[1]), pack_bf16x2(w[2], w[3])};
+                lq[qd] = u32x2{pack_bf16x2(w[0] - __uint_as_float(hq[qd].x << 16), w[1] - __uint_as_float(hq[qd].x & 0xffff0000u)),
+                               pack_bf16x2(w[2] - __uint_as_float(hq[qd].y << 16), w[3] - __uint_as_float(hq[qd].y & 0xffff0000u))};
+              }
+              const size_t at = rowbase + (g.vt_swz ? vt_pos(tok + 4 * qd) : tok + 4 * qd);
+              st8((bf16*)g.S + at, hq[qd]);
+              st8((bf16*)g.S + lo + at, lq[qd]);
             }
-            st16((bf16*)g.S + rowbase + tok, pack16<bf16>(hv));
-            st16((bf16*)g.S + lo + rowbase + tok, pack16<bf16>(lv));
             continue;
           }
           for (int e = 0; e < 8 && m + e < g.M; ++e) {
             const int me = m + e, be = me / g.vt_T, te = me - be * g.vt_T;
-            const size_t idx = ((size_t)(grp * g.vt_B + be) * 256 + hd) * g.vt_T + te;
-            const bf16 h = from_f32<bf16>(v[e]);
-            ((bf16*)g.S)[idx] = h;
-            ((bf16*)g.S)[lo + idx] = from_f32<bf16>(v[e] - to_f32(h));
+            const size_t idx = ((size_t)(grp * g.vt_B + be) * 256 + hd) * g.vt_T + (g.vt_swz ? vt_pos(te) : te);
+            const float w = v[e] * sf;
+            if (g.s_f16) {
+              const f16 h = (f16)w;
+              ((f16*)g.S)[idx] = h;
+              ((f16*)g.S)[lo + idx] = (f16)(w - (float)h);
+            } else {
+              const bf16 h = from_f32<bf16>(w);
+              ((bf16*)g.S)[idx] = h;
+              ((bf16*)g.S)[lo + idx] = from_f32<bf16>(w - to_f32(h));
+            }
           }
           continue;
         }
@@ -1279,6 +1296,7 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
       __builtin_amdgcn_make_buffer_rsrc(g.S ? g.S : g.C, (short)0, g.S ? (int)sbytes : 0, 0x00020000);
   float sa, inv_sa;
   h3_scale(g.amax_a, sa, inv_sa);
+  const float vsf = EPI == 2 && g.S && g.s_f16 ? vplane_scale(g.amax_a, g.s_l1, g.s_bmax) : 1.f;
   if (total == 0) return;
 
   // ---- issue side: the tile / K-step of the next DMA and that tile's per-lane source offsets
@@ -1445,7 +1463,7 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
           const int mr = mb + 8 * q;
           const bool ok = mr < g.M && n < g.N;
           const int b = mr / g.vt_T, tok = mr - b * g.vt_T;
-          const int idx = ok ? ((grp * g.vt_B + b) * 256 + hd) * g.vt_T + tok : 0;
+          const int idx = ok ? ((grp * g.vt_B + b) * 256 + hd) * g.vt_T + (g.vt_swz ? vt_pos(tok) : tok) : 0;
           float v[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
@@ -1455,7 +1473,14 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
           if (ok) runmax = fmaxf(runmax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
           if (g.S) {
             u32x2 h, l;
-            hilo(v, h, l);
+            if (g.s_f16) {
+              float w[4];
+#pragma unroll
+              for (int e = 0; e < 4; ++e) w[e] = v[e] * vsf;
+              split_f16x4(w, h, l);
+            } else {
+              hilo(v, h, l);
+            }
             __builtin_amdgcn_raw_buffer_store_b64(h, rss, ok ? idx * 2 : D6_BAD, 0, 0);
             __builtin_amdgcn_raw_buffer_store_b64(l, rss, ok ? (int)((lo + idx) * 2) : D6_BAD, 0, 0);
           } else {
@@ -1630,7 +1655,8 @@ int launch_h3d(const GemmArgs& g, int mode, hipStream_t s) {
       spe_gemm_last_path = 8;
       return (int)hipGetLastError();
     }
-    if (mode == GEMM_LINEAR && !narrow && g.K >= 64 && g.vt_T > 0 && !res && !g.vt_swz && !g.out_f16 &&
+    if (mode == GEMM_LINEAR && !narrow && g.K >= 64 && g.vt_T > 0 && !res && !g.out_f16 &&
+        (!g.vt_swz || (g.S && g.vt_T % 16 == 0)) && (!g.s_f16 || g.S) &&
         g.vt_T % 4 == 0 && g.M == g.vt_B * g.vt_T && !(g.N & 255) && (!g.S || g.s_col0 == 0) &&
         (long long)g.vt_B * g.N * g.vt_T * 4 < LIM && !(reinterpret_cast<uintptr_t>(g.C) & 15)) {
       hipLaunchKernelGGL(gemm_h3p_linear_vt, pg, pb, 0, s, g);
@@ -1739,4 +1765,10 @@ int spe_launch_gemm(const GemmArgs& g, int dtype, int mode, hipStream_t s) {
     return tiles6 >= 128 ? launch_x6(g, mode, s) : launch_x6_geo<128>(g, mode, s);
   }
   return dtype == SPE_DTYPE_BF16 ? launch_t<bf16>(g, mode, s) : launch_t<float>(g, mode, s);
+}
+
+int spe_launch_gemm_h3(const GemmArgs& g, int mode, hipStream_t s) {
+  if ((g.K & 3) || (g.ldb % 64) || (g.lda & 3) || (g.ldc & 3) || (g.R && (g.ldr & 3)) || g.ln_g) return -5;
+  spe_gemm_last_path = 7;
+  return launch_h3d(g, mode, s);                 // 1: not served (nothing launched)
 }

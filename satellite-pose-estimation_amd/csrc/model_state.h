@@ -14,6 +14,7 @@ struct Conv {              // conv / linear packed as [N][Kpad] in T, bias fp32
   void* w = nullptr;
   float* bias = nullptr;
   int N = 0, K = 0, Kpad = 0, Cin = 0, KH = 1, KW = 1, stride = 1, pad = 0;
+  float l1max = 0.f, bmax = 0.f;   // linears: max_n sum_k |W[n][k]| and max |bias| (|y| <= max |x| l1max + bmax)
 };
 
 struct Block {

@@ -339,6 +339,12 @@ Conv make_linear(spe_model* m, const std::string& wkey, const std::string& bkey,
   c.w = upload_rows(m, rows, n, K, c.Kpad);
   const auto& b = m->host[bkey];
   c.bias = upload_f32(m, b.data() + r0, n);
+  for (int r = 0; r < n; ++r) {
+    double s = 0.0;
+    for (int k = 0; k < K; ++k) s += std::fabs(rows[(size_t)r * K + k]);
+    c.l1max = std::max(c.l1max, (float)(s * (1.0 + 1e-6)));     // (rounded up past the fp32 sum's error)
+    c.bmax = std::max(c.bmax, std::fabs(b[r0 + r]));
+  }
   return c;
 }
 

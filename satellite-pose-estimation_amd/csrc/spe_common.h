@@ -141,3 +141,20 @@ SPE_DEV float apply_act(float v, int act) {
 // cycles of the bottleneck-tail kernels).
 SPE_DEV constexpr int wkey_mask(int KB) { return (KB / 16 < 16 ? KB / 16 : 16) - 1; }
 SPE_DEV constexpr int wkey_addr(int n, int chunk, int KB) { return n * KB + ((chunk ^ (n & wkey_mask(KB))) << 4); }
+
+// fp16 hi / lo planes of a tensor with a bounded range (GemmArgs::s_f16 -> AttnArgs::v_f16): the
+// factor 2^(14 - e) applied before the split, with bound = amax * l1 + bmax in [2^(e-1), 2^e), keeps
+// every scaled |x| below 2^14 (fp16 max 65504); 1 without a finite positive bound.  Producer and
+// consumer evaluate this same expression on the same inputs, so they agree on the power of two.
+SPE_DEV float vplane_scale(const float* amax, float l1, float bmax) {
+  if (!amax) return 1.f;
+  const float bound = __builtin_fmaf(*amax, l1, bmax);
+  if (!(bound > 0.f) || !(bound <= 3.0e38f)) return 1.f;
+  return __builtin_ldexpf(1.f, 14 - __builtin_amdgcn_frexp_expf(bound));
+}
+// four fp32 values -> fp16 hi = RNE(x) and lo = RNE(x - hi) (x - hi exact in fp32), two words each
+SPE_DEV void split_f16x4(const float* v, u32x2& h, u32x2& l) {
+  const f16x2 h0 = __builtin_convertvector(f32x2{v[0], v[1]}, f16x2), h1 = __builtin_convertvector(f32x2{v[2], v[3]}, f16x2);
+  h = u32x2{__builtin_bit_cast(uint32_t, h0), __builtin_bit_cast(uint32_t, h1)};
+  l = u32x2{pack_f16x2(v[0] - (float)h0[0], v[1] - (float)h0[1]), pack_f16x2(v[2] - (float)h1[0], v[3] - (float)h1[1])};
+}

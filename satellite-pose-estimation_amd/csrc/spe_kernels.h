@@ -43,9 +43,15 @@ struct GemmArgs {
   const void* H3; int h3_rows; const float* h3_sinv;
   const float* amax_a;
   float* amax_c; float amax_c_mul;
+  // head-transposed S planes as fp16 instead of bf16 (the fp32h3 encoder attention's value operand):
+  // hi / lo of x * vplane_scale(amax_a, s_l1, s_bmax), s_l1 = max_n sum_k |W[n][k]|, s_bmax = max |bias|
+  int s_f16; float s_l1, s_bmax;
 };
 bool spe_gemm_ln_fusable(const GemmArgs& g);   // the large-tile kernel can fuse ln_g/ln_b for g
 int spe_launch_gemm(const GemmArgs& g, int dtype, int mode, hipStream_t s);
+// the fp32h3 kernels only: 1 (nothing launched) for a shape they do not serve, where spe_launch_gemm
+// would fall through to the x6 path
+int spe_launch_gemm_h3(const GemmArgs& g, int mode, hipStream_t s);
 
 // Implicit-GEMM conv K order.  Multi-tap convs with Cin % 64 == 0 use channel-block-major order
 // k = ((ci / 64) * KH*KW + tap) * 64 + ci % 64, so one 64-channel slice of the input window is
@@ -107,8 +113,12 @@ struct AttnArgs {
   int B, H, Tq, Tk;
   float scale;                     // softmax scale (1/sqrt(head_dim))
   int presplit;                    // fp32x3: k and vt are bf16 hi planes (k [B*Tk][ldk], vt [B][H][32][Tk]),
-                                   // each followed by its lo plane (GemmArgs::S); Tk % 8 == 0
+                                   // each followed by its lo plane (GemmArgs::S); Tk % 8 == 0.  With vt_swz
+                                   // (V^T in vt_pos order, Tk % 16 == 0) the LDS-DMA split kernel (attn_split.hip)
+  int v_f16;                       // presplit + vt_swz: the V^T planes are fp16 hi / lo of V * vplane_scale(
+  const float* v_amax; float v_l1, v_bmax;   //   v_amax, v_l1, v_bmax) (GemmArgs::s_f16), P split to fp16
 };
+int spe_launch_attention_split(const AttnArgs& a, hipStream_t s);
 int spe_launch_attention(const AttnArgs& a, int dtype, hipStream_t s);
 
 // Decoder cross-attention against the encoder memory (bf16 path, xattn.hip): per image b and

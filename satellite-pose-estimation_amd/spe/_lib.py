@@ -25,6 +25,11 @@ if os.environ.get("SPE_GRAPH_CAPTURE") == "1":
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("SPE_LIB_PATH") or os.path.join(_HERE, "libspe.so")   # override: kernel A/B builds
 
+# the include/spe.h version this binding is written against: any other library is refused, including
+# one named by SPE_LIB_PATH (an A/B build of an older tree would otherwise be called with this
+# binding's argument lists)
+ABI_VERSION = 8
+
 P = ctypes.c_void_p
 I = ctypes.c_int
 I64 = ctypes.c_int64
@@ -74,14 +79,17 @@ class SpeError(RuntimeError):
 _lib = None
 
 
-def lib():
-    global _lib
-    if _lib is not None:
-        return _lib
-    if not os.path.exists(LIB_PATH):
-        raise ImportError(f"libspe.so not built ({LIB_PATH}); run __graft_entry__.build()")
-    L = ctypes.CDLL(LIB_PATH)
+def load(path: str):
+    """CDLL of `path` with the argument types bound; ImportError unless it is ABI_VERSION's library."""
+    if not os.path.exists(path):
+        raise ImportError(f"libspe.so not built ({path}); run __graft_entry__.build()")
+    L = ctypes.CDLL(path)
+    if not hasattr(L, "spe_abi_version"):
+        raise ImportError(f"{path} exports no spe_abi_version")
     L.spe_abi_version.restype = I
+    v = L.spe_abi_version()
+    if v != ABI_VERSION:
+        raise ImportError(f"{path}: ABI version {v}, this binding needs {ABI_VERSION}")
     L.spe_last_error.restype = ctypes.c_char_p
     L.spe_model_create.argtypes = [ctypes.POINTER(ModelConfig), ctypes.POINTER(P)]
     L.spe_model_destroy.argtypes = [P]
@@ -117,26 +125,28 @@ def lib():
     L.spe_debug_ffn.argtypes = [P, P, I, P, I, P, P, I, P, P, P, P, I, I, I, I, P, I]
     L.spe_debug_xattn.argtypes = [P, P, I, P, I, P, I, P, I, P, P, P, I, I, I, I, I, P]
     L.spe_debug_upconv.argtypes = [P, I, P, P, I, I, I, I, I]
-    if hasattr(L, "spe_debug_btail"):          # (absent from older kernel A/B builds, SPE_LIB_PATH)
-        L.spe_debug_btail.argtypes = [P, P, I, I, P, P, I, P, P, P, I, P, P, I, I]
-        L.spe_debug_btail_perm.argtypes = [I]
+    L.spe_debug_btail.argtypes = [P, P, I, I, P, P, I, P, P, P, I, P, P, I, I]
+    L.spe_debug_btail_perm.argtypes = [I]
     L.spe_debug_decsa.argtypes = [P, P, I, I, I, P, I, P, P, I, P, P, P, I, P, P, P, ctypes.c_float]
     L.spe_debug_decproj.argtypes = [P, P, I, P, I, I, I, P, I, P, P, P]
     L.spe_debug_wfrag_pack.argtypes = [P, P, I, I, P]
     L.spe_debug_decffn.argtypes = [P, P, I, I, I, P, I, P, P, I, P, P, P, P, I, P]
     L.spe_debug_decq.argtypes = [P, P, I, I, I, P, I, P, P, I, I, P, I]
     L.spe_debug_decxproj.argtypes = [P, P, I, P, I, I, I, I, P, I, P, P, I, P, P, P]
-    if hasattr(L, "spe_debug_stempool"):
-        L.spe_debug_stempool.argtypes = [P, P, P, I, P, P, I, I, I]
+    L.spe_debug_stempool.argtypes = [P, P, P, I, P, P, I, I, I]
     L.spe_rtdetr_create.argtypes = [ctypes.POINTER(RtdetrConfig), ctypes.POINTER(P)]
     L.spe_rtdetr_forward.argtypes = [P, P, P, I, P, I64, ctypes.POINTER(RtdetrOutputs)]
     L.spe_jpeg_workspace_bytes.argtypes = [I, I, I, I64]
     L.spe_jpeg_workspace_bytes.restype = I64
     L.spe_jpeg_decode.argtypes = [P, P, P, P, I, I, I, I64, P, P, P, I64]
-    if L.spe_abi_version() != 7:
-        raise ImportError("libspe.so ABI version mismatch")
-    _lib = L
     return L
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        _lib = load(LIB_PATH)
+    return _lib
 
 
 def check(rc: int, what: str):

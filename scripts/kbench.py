@@ -48,6 +48,9 @@ def main():
     ap.add_argument("--attn-dtype", type=int, default=0, help="0 bf16, 1 fp32, 2 fp16, 3 bf16 q/k + fp16 V^T/P, 4 fp32x3")
     ap.add_argument("--dma", action="store_true", help="the encoder's LDS-DMA attention kernel (V^T key order as stored)")
     ap.add_argument("--presplit", action="store_true", help="fp32x3: K and V^T as the bf16 hi / lo planes the models pass")
+    ap.add_argument("--split-dma", action="store_true",
+                    help="with --presplit: V^T planes in vt_pos key order -> the LDS-DMA split kernel (attn_split.hip)")
+    ap.add_argument("--f16v", action="store_true", help="with --split-dma: fp16 V^T planes (the fp32h3 model's form)")
     a = ap.parse_args()
     L = _lib.lib()
     dev = torch.device("cuda", 0)
@@ -67,9 +70,16 @@ def main():
         if a.presplit and a.attn_dtype == 4:             # (the planes kept alive in `keep`)
             kf = qk[:, 256:].contiguous()
             kh = kf.to(torch.bfloat16)
-            vh = vt.to(torch.bfloat16)
+            vdt2 = torch.bfloat16
+            if a.split_dma:                              # keys to vt_pos order (a permutation: timing only)
+                t = torch.arange(T, device=dev)
+                vs = torch.empty_like(vt)
+                vs[..., (t & ~12) | ((t & 4) << 1) | ((t & 8) >> 1)] = vt
+                vt, code = vs, code | 0x100 | (0x400 if a.f16v else 0)
+                vdt2 = torch.float16 if a.f16v else torch.bfloat16
+            vh = vt.to(vdt2)
             keep = [torch.cat([kh.reshape(-1), (kf - kh.float()).to(torch.bfloat16).reshape(-1)]),
-                    torch.cat([vh.reshape(-1), (vt - vh.float()).to(torch.bfloat16).reshape(-1)])]
+                    torch.cat([vh.reshape(-1), (vt - vh.float()).to(vdt2).reshape(-1)])]
             kp, vt, ldk, code = ctypes.c_void_p(keep[0].data_ptr()), keep[1], 256, code | 0x200
         fn = lambda: L.spe_debug_attention(None, code, p(qk), 512, kp, ldk, p(vt), p(o), D, B, H, T, T, 32 ** -0.5)
         ms = timeit(fn, a.iters)

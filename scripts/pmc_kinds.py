@@ -20,7 +20,8 @@ import os
 from collections import defaultdict
 
 SKIP = ("pnp_", "score_kernel", "self_assess", "at::", "void at", "rocprim", "hipcub", "__amd_rocclr", "Cijk")
-FAMILY = {"attn.enc": ("attn16",), "attn.dec_self": ("attn16",), "attn.dec_cross": ("xattn",),
+FAMILY = {"attn.enc": ("attn16", "attn_x3", "attn_h3", "attn_f32"), "attn.dec_self": ("attn16", "attn_f32"),
+          "attn.dec_cross": ("xattn", "attn_f32"),
           "ffn.enc": ("ffn_",), "ffn.dec": ("ffn_",)}
 
 
@@ -72,6 +73,7 @@ def main():
     ap.add_argument("dir")
     ap.add_argument("--table", required=True)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--mode", default="bf16", help="the bench dtype the passes ran (recorded in the note)")
     a = ap.parse_args()
     table = json.load(open(a.table))
     res = defaultdict(lambda: {"launches": 0, "algorithmic_bytes": 0.0, "fetch_bytes": 0.0, "write_bytes": 0.0,
@@ -94,7 +96,7 @@ def main():
                   "fetch_MB": r["fetch_bytes"] / 1e6, "write_MB": r["write_bytes"] / 1e6,
                   "counter_over_algorithmic": tb / r["algorithmic_bytes"] if r["algorithmic_bytes"] else None,
                   "kernels": sorted(r["kernels"])}
-    s = json.dumps({"note": "per bench step (B=64, config 2, bf16, serialised --no-overlap); FETCH x2 (gfx950), KiB->B",
+    s = json.dumps({"note": f"per bench step (B=64, config 2, {a.mode}, serialised --no-overlap); FETCH x2 (gfx950), KiB->B",
                     "classes": out}, indent=1)
     print(s)
     if a.out:

@@ -3,6 +3,7 @@ parameter registry speaks the reference's state_dict key space (no GPU compute h
 import ctypes
 import os
 import re
+import sys
 
 import numpy as np
 import pytest
@@ -24,7 +25,26 @@ def test_exports_every_declared_symbol():
     assert set(declared) == set(_lib.EXPORTS)
     for name in declared:
         assert hasattr(L, name), name
-    assert L.spe_abi_version() == 7
+    assert L.spe_abi_version() == _lib.ABI_VERSION == 8
+
+
+@pytest.mark.parametrize("version", [7, 9])
+def test_other_abi_version_is_refused(tmp_path, version):
+    """A library of another ABI (e.g. an A/B build of the v7 tree, whose spe_debug_gemm_h3 took two more
+    arguments) is refused at load, SPE_LIB_PATH included, before any call is bound."""
+    import subprocess
+    src = tmp_path / "old.c"
+    src.write_text(f"int spe_abi_version(void) {{ return {version}; }}\n")
+    so = tmp_path / "libspe_old.so"
+    subprocess.check_call(["gcc", "-shared", "-fPIC", "-o", str(so), str(src)])
+    with pytest.raises(ImportError, match=f"ABI version {version}"):
+        _lib.load(str(so))
+    code = ("import os, sys; sys.path.insert(0, %r); os.environ['SPE_LIB_PATH'] = %r\n"
+            "from spe import _lib\n"
+            "try:\n    _lib.lib()\nexcept ImportError as e:\n    print('refused', e)\n") % (
+        os.path.join(REPO, "satellite-pose-estimation_amd"), str(so))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert "refused" in out.stdout and f"ABI version {version}" in out.stdout, out.stdout + out.stderr
 
 
 def _create(cfg, dtype=_lib.SPE_DTYPE_BF16):

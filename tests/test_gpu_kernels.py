@@ -1245,6 +1245,81 @@ def test_attention_x3_close_to_fp64(gpu_device, B, H, Tq, Tk):
     assert err <= 5e-5, err
 
 
+def _vt_pos(T):
+    """the 16-bit attention operands' key order (spe_kernels.h vt_pos): stored position of key t"""
+    t = torch.arange(T)
+    return (t & ~12) | ((t & 4) << 1) | ((t & 8) >> 1)
+
+
+def _split_planes(K, VT, f16v):
+    """K -> bf16 hi / lo planes; V^T [B][H][32][T] -> hi / lo planes in vt_pos key order, bf16 or fp16"""
+    vs = torch.empty_like(VT)
+    vs[..., _vt_pos(VT.shape[-1]).to(VT.device)] = VT
+    dt = torch.float16 if f16v else torch.bfloat16
+    h = vs.to(dt)
+    return _bf16_planes(K), torch.cat([h.reshape(-1), (vs - h.float()).to(dt).reshape(-1)])
+
+
+@pytest.mark.parametrize("f16v", [0, 1])
+@pytest.mark.parametrize("B,H,Tq,Tk", [(1, 8, 300, 336), (2, 8, 2704, 2704), (3, 8, 11, 2704), (2, 8, 40, 48),
+                                       (1, 8, 64, 64), (1, 8, 130, 192)])
+def test_attention_split_dma_close_to_fp64(gpu_device, f16v, B, H, Tq, Tk):
+    """The LDS-DMA split-operand encoder attention (attn_split.hip) on the planes the fp32 models'
+    projection epilogues write: K bf16 hi / lo, V^T hi / lo in vt_pos order (bf16, or fp16 as in
+    fp32h3), against an fp64 softmax.  The scores carry the bf16 split's ~2^-17 per product; the
+    value product ~2^-17 (bf16 P) or ~2^-21 (fp16 P)."""
+    g = torch.Generator(device="cpu").manual_seed(Tq * 7 + Tk + f16v)
+    ld = H * 32
+    Q = torch.randn(B * Tq, ld + 16, generator=g, dtype=torch.float64) * 2
+    K = torch.randn(B * Tk, ld, generator=g, dtype=torch.float64) * 2
+    V = torch.randn(B, H, Tk, 32, generator=g, dtype=torch.float64)
+    dev = gpu_device
+    Qd, Kd = Q.to(dev, torch.float32), K.to(dev, torch.float32)
+    VTd = V.transpose(-1, -2).contiguous().to(dev, torch.float32)
+    Kp, VTp = _split_planes(Kd, VTd, f16v)
+    O = torch.full((B * Tq, ld), float("nan"), dtype=torch.float32, device=dev)
+    code = _lib.SPE_DTYPE_F32X3 | 0x100 | 0x200 | (0x400 if f16v else 0)
+    rc = _lib.lib().spe_debug_attention(None, code, _p(Qd), ld + 16, _p(Kp), ld, _p(VTp), _p(O), ld, B, H, Tq, Tk,
+                                        32 ** -0.5)
+    assert rc == 0
+    torch.cuda.synchronize()
+    q = Qd.double().cpu()[:, :ld].view(B, Tq, H, 32).transpose(1, 2)
+    k = Kd.double().cpu().view(B, Tk, H, 32).transpose(1, 2)
+    ref = torch.softmax(q @ k.transpose(-1, -2) * 32 ** -0.5, -1) @ VTd.double().cpu().transpose(-1, -2)
+    ref = ref.transpose(1, 2).reshape(B * Tq, ld)
+    err = (O.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
+    assert err <= 5e-5, err
+
+
+@pytest.mark.parametrize("f16v", [0, 1])
+@pytest.mark.parametrize("gain", [3.0, 12.0, 40.0])
+def test_attention_split_dma_large_score_range(gpu_device, f16v, gain):
+    """The split kernel's lazy softmax when late keys dominate: a stale running max lets some p pass
+    2^12, the lane-sum test must send that tile through the recompute + rescale path."""
+    B, H, T = 2, 8, 336
+    g = torch.Generator(device="cpu").manual_seed(int(gain) + 100 * f16v)
+    Q = torch.randn(B * T, 256, generator=g, dtype=torch.float64)
+    K = torch.randn(B * T, 256, generator=g, dtype=torch.float64)
+    K[T - 90:T] *= gain
+    K[2 * T - 20:] *= gain / 2
+    V = torch.randn(B, H, T, 32, generator=g, dtype=torch.float64)
+    dev = gpu_device
+    Qd, Kd = Q.to(dev, torch.float32), K.to(dev, torch.float32)
+    VTd = V.transpose(-1, -2).contiguous().to(dev, torch.float32)
+    Kp, VTp = _split_planes(Kd, VTd, f16v)
+    O = torch.zeros(B * T, 256, dtype=torch.float32, device=dev)
+    code = _lib.SPE_DTYPE_F32X3 | 0x100 | 0x200 | (0x400 if f16v else 0)
+    assert _lib.lib().spe_debug_attention(None, code, _p(Qd), 256, _p(Kp), 256, _p(VTp), _p(O), 256, B, H, T, T,
+                                          32 ** -0.5) == 0
+    torch.cuda.synchronize()
+    q = Qd.double().cpu().view(B, T, H, 32).transpose(1, 2)
+    k = Kd.double().cpu().view(B, T, H, 32).transpose(1, 2)
+    ref = torch.softmax(q @ k.transpose(-1, -2) * 32 ** -0.5, -1) @ V
+    ref = ref.transpose(1, 2).reshape(B * T, 256)
+    err = (O.double().cpu() - ref).abs().max().item() / ref.abs().max().item()
+    assert err <= 5e-5 * max(1.0, gain / 8), err
+
+
 @pytest.mark.parametrize("dtype,gain", [("fp32x3", 3.0), ("fp32x3", 12.0), ("fp32x3", 40.0), ("fp32", 12.0),
                                         ("fp32", 40.0)])
 def test_attention_fp32_modes_large_score_range(gpu_device, dtype, gain):
