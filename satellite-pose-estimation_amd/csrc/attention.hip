@@ -383,11 +383,7 @@ __global__ __launch_bounds__(DMA ? 64 * DMA_WAVES : NT, DMA ? 16 / DMA_WAVES : S
       // reads made the compiler wait for every read, V included, before the first MFMA)
       if (!wave_live && kt + 2 < ntiles) issue(kt + 2, (S + 2) % 3);
     } else {
-#ifdef SPE_X_NOSTAGE
-      if (more && kt == 0) st.load(a, b, h, kt + 1, tid);
-#else
       if (more) st.load(a, b, h, kt + 1, tid);
-#endif
     }
     if (wave_live) {
       // every fragment read of this step is issued up front; V lands during QK^T + softmax
@@ -485,14 +481,8 @@ __global__ __launch_bounds__(DMA ? 64 * DMA_WAVES : NT, DMA ? 16 / DMA_WAVES : S
           o = AV::mfma(__builtin_bit_cast(vv8, vf[sub][ks]), __builtin_bit_cast(vv8, pw[sub][ks]), o);
     }
     if constexpr (!DMA) {
-#ifdef SPE_X_NOSTAGE
-      if (more && kt == 0) st.store(smem + ((kt + 1) & 1) * SLOT, smem + ((kt + 1) & 1) * SLOT + KBYTES, tid);
-#else
       if (more) st.store(smem + ((kt + 1) & 1) * SLOT, smem + ((kt + 1) & 1) * SLOT + KBYTES, tid);
-#endif
-#ifndef SPE_X_NOBAR
       __syncthreads();
-#endif
     }
   };
   if constexpr (DMA) {

@@ -11,16 +11,25 @@
 // lo = RNE(p - hi): 2^-21 relative per p), bf16 otherwise.
 //
 // Against the register-staged attn_x3_kernel (attention.hip) this kernel: stages the four planes of a
-// 64-key tile global -> LDS by buffer_load ... lds through a three-slot ring (each wave issues one 1 KB
-// piece of each plane, two tiles in flight, one barrier per tile, no staging registers or ds_writes);
-// reads every fragment at a per-lane base + immediate offset (ring unrolled by its three slots);
-// masks keys only in the peeled last tile; skips the per-tile max (lazy softmax, the bf16 DMA
-// kernel's rule: a tile is exponentiated against the stale running max and its fp32 row sum is the
-// overflow test -- only a lane sum above LAZY_LIMIT, i.e. some p > 2^12, recomputes the scores from
-// the K tile still in LDS and takes the max / rescale path); and splits P to fp16 with one
-// v_cvt_pkrtz_f16_f32 per pair and the remainders in fp32 (3 VALU per pair against 6 for the bf16
-// split).  Built with -fno-slp-vectorize: the row sums stay scalar v_add_f32 (packed f32 adds beside
-// MFMAs cost more issue than they save, MI355X_MICROARCH.md).
+// 64-key tile global -> LDS by buffer_load ... lds through a ring of NSLOT = 4 slots (each wave issues
+// one 1 KB piece of each plane per tile, two tiles ahead, one barrier per tile, no staging registers
+// or ds_writes); reads every fragment at a per-lane base + immediate offset (the loop unrolled by the
+// ring's slots); masks keys only in a tile that reaches past Tk; skips the per-tile max (lazy softmax,
+// the bf16 DMA kernel's rule: a tile is exponentiated against the stale running max and its fp32 row
+// sum is the overflow test -- only a lane sum above LAZY_LIMIT, i.e. some p > 2^12, recomputes the
+// scores from the K tile still in LDS and takes the max / rescale path); splits P to fp16 with one
+// v_cvt_pkrtz_f16_f32 per pair and v_fma_mix for the remainders (3 VALU per pair against 6 for the
+// bf16 split); and software-pipelines the tiles: step kt issues tile kt+1's score MFMAs with tile kt's
+// exp2 / row sums in their gaps (sched_group_barrier), then tile kt's value product with the P split
+// in its gaps.  Built with -fno-slp-vectorize: the row sums stay scalar v_add_f32 (packed f32 adds
+// beside MFMAs cost more issue than they save, MI355X_MICROARCH.md).
+//
+// Measured (kbench, B = 64, 2704 tokens, fp16 V planes): 1.74 ms for attn_x3_kernel -> 1.50 ms; the
+// PMC passes put the SIMD's instruction issue at ~87 % busy (2 waves x 1066 issue cycles per 2453-cycle
+// wave-tile), MFMA 57 % at 1.51 GHz.  Per 64-key tile and wave the issue floor is ~24 MFMA x 8 + 32
+// v_exp x 8 + 32 sums + 48 split VALU = ~830 cycles against 768 matrix cycles.  P as one RNE fp16 term
+// (no lo part: 20 instead of 24 MFMAs, 1.26 ms) moved the bench keypoints 1.7e-4 from exact f32 and
+// failed the precision gate (tests/test_gpu_precision.py): the split stays.
 #include "spe_common.h"
 #include "spe_kernels.h"
 #include <type_traits>
@@ -31,6 +40,11 @@ constexpr int NT = 256;                 // 4 waves x 32 queries
 constexpr int KT = 64;                  // keys per tile
 constexpr int PLANE = 4096;             // one plane of a tile: K 64 keys x 64 B / V^T 32 rows x 128 B
 constexpr int SLOT = 4 * PLANE;         // [K hi | K lo | V^T hi | V^T lo]
+#ifndef SPE_SPLIT_SLOTS
+#define SPE_SPLIT_SLOTS 4
+#endif
+constexpr int NSLOT = SPE_SPLIT_SLOTS;  // LDS ring depth: 3 (48 KB, three work-groups per CU) or 4
+static_assert(NSLOT == 3 || NSLOT == 4, "ring");
 constexpr float LOG2E = 1.4426950408889634f;
 constexpr float NEG_BIG = -1.0e30f;
 constexpr float RESCALE_SLACK = 8.0f;
@@ -72,8 +86,8 @@ SPE_DEV float pair_max(const f32x16& s0, const f32x16& s1) {
 }
 
 template <bool F16V>
-__global__ __launch_bounds__(NT, 3) void attn_split_kernel(AttnArgs a) {
-  __shared__ __attribute__((aligned(1024))) char smem[3 * SLOT];
+__global__ __launch_bounds__(NT, NSLOT == 3 ? 3 : 2) void attn_split_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(1024))) char smem[NSLOT * SLOT];
   const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
   const int hh = lane >> 5, r32 = lane & 31;
   const int qblocks = (a.Tq + 127) / 128;
@@ -156,6 +170,7 @@ __global__ __launch_bounds__(NT, 3) void attn_split_kernel(AttnArgs a) {
   const int ntiles = (a.Tk + KT - 1) / KT;
   issue(0, 0);
   if (ntiles > 1) issue(1, 1);
+  if (NSLOT == 4 && ntiles > 2) issue(2, 2);
 
   auto scores = [&](const char* sl, f32x16& s0, f32x16& s1) {
 #pragma unroll
@@ -171,75 +186,47 @@ __global__ __launch_bounds__(NT, 3) void attn_split_kernel(AttnArgs a) {
       s = mfma_bf(kh1, qh[1], s);
     }
   };
-
-  // one 64-key tile; SC = ring slot (compile-time), MASK = the tile reaches past Tk
-  auto step = [&](int kt, auto SC, auto MASKC) {
-    constexpr int S = decltype(SC)::value;
-    constexpr bool MASK = decltype(MASKC)::value;
-    const char* sl = smem + S * SLOT;
-    // this wave's pieces of tile kt landed (tile kt+1's may stay in flight); the barrier makes the
-    // tile visible to all and retires tile kt-1, whose slot takes tile kt+2
-    if (kt + 1 < ntiles) __builtin_amdgcn_s_waitcnt(waitcnt_vm(4));
-    else __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
-    __builtin_amdgcn_s_barrier();
-    if (!wave_live) {
-      if (kt + 2 < ntiles) issue(kt + 2, (S + 2) % 3);
-      return;
+  // keys past Tk (only a last tile that reaches past it; wave-uniform tests)
+  auto mask = [&](int kt, f32x16& s0, f32x16& s1) {
+    if ((kt + 1) * KT > a.Tk) mask16(s0, s1, kt * KT, a.Tk);
+  };
+  // the max path: the first tile sets m; later ones move it (rescaling o and l) only when some lane's
+  // tile max passed it by more than RESCALE_SLACK.  Returns the shift d applied to m.
+  auto maxpath = [&](bool first, f32x16& s0, f32x16& s1) {
+    const float mx = pair_max(s0, s1);     // relative to m
+    float d = 0.f;
+    if (first || __any(mx > RESCALE_SLACK)) {
+      d = first ? mx : __builtin_fmaxf(mx, 0.f);
+      if (!first) {
+        const float alpha = __builtin_amdgcn_exp2f(-d);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) o[r] *= alpha;
+        l *= alpha;
+      }
+      m += d;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) { s0[r] -= d; s1[r] -= d; negm[r] = -m; }
     }
-    f32x16 s0, s1;
-    scores(sl, s0, s1);
-    // (issued after the score MFMAs: a DMA ahead of the fragment reads makes the compiler wait for
-    // all of them before the first MFMA)
-    if (kt + 2 < ntiles) issue(kt + 2, (S + 2) % 3);
-    // exp2 of the shifted scores and the lane's row sum over its 32 keys
-    auto expsum = [&]() {
-      float t0 = 0.f, t1 = 0.f, t2 = 0.f, t3 = 0.f;
+    return d;
+  };
+  // exp2 of the shifted scores in place and the lane's row sum over its 32 keys
+  auto expsum = [&](f32x16& s0, f32x16& s1) {
+    float t0 = 0.f, t1 = 0.f, t2 = 0.f, t3 = 0.f;
 #pragma unroll
-      for (int r = 0; r < 16; r += 2) {
-        s0[r] = __builtin_amdgcn_exp2f(s0[r]);
-        s0[r + 1] = __builtin_amdgcn_exp2f(s0[r + 1]);
-        s1[r] = __builtin_amdgcn_exp2f(s1[r]);
-        s1[r + 1] = __builtin_amdgcn_exp2f(s1[r + 1]);
-        t0 += s0[r];
-        t1 += s0[r + 1];
-        t2 += s1[r];
-        t3 += s1[r + 1];
-      }
-      return (t0 + t1) + (t2 + t3);
-    };
-    // the max path: the first tile sets m; later ones move it (rescaling o and l) only when some
-    // lane's tile max passed it by more than RESCALE_SLACK
-    auto maxpath = [&](bool first) {
-      const float mx = pair_max(s0, s1);     // relative to m
-      if (first || __any(mx > RESCALE_SLACK)) {
-        const float d = first ? mx : __builtin_fmaxf(mx, 0.f);
-        if (!first) {
-          const float alpha = __builtin_amdgcn_exp2f(-d);
-#pragma unroll
-          for (int r = 0; r < 16; ++r) o[r] *= alpha;
-          l *= alpha;
-        }
-        m += d;
-#pragma unroll
-        for (int r = 0; r < 16; ++r) { s0[r] -= d; s1[r] -= d; negm[r] = -m; }
-      }
-    };
-    if constexpr (MASK) mask16(s0, s1, kt * KT, a.Tk);
-    float t;
-    if (kt == 0) {
-      maxpath(true);
-      t = expsum();
-    } else {
-      t = expsum();
-      if (__any(t > LAZY_LIMIT)) {           // some p > 2^12 against the stale max: redo with the max
-        scores(sl, s0, s1);
-        if constexpr (MASK) mask16(s0, s1, kt * KT, a.Tk);
-        maxpath(false);
-        t = expsum();
-      }
+    for (int r = 0; r < 16; r += 2) {
+      s0[r] = __builtin_amdgcn_exp2f(s0[r]);
+      s0[r + 1] = __builtin_amdgcn_exp2f(s0[r + 1]);
+      s1[r] = __builtin_amdgcn_exp2f(s1[r]);
+      s1[r + 1] = __builtin_amdgcn_exp2f(s1[r + 1]);
+      t0 += s0[r];
+      t1 += s0[r + 1];
+      t2 += s1[r];
+      t3 += s1[r + 1];
     }
-    l += t;
-    // value product: O^T += V^T . P^T, P split in registers
+    return (t0 + t1) + (t2 + t3);
+  };
+  // value product O^T += V^T . P^T of one tile, P split in registers
+  auto pv = [&](const char* sl, const f32x16& s0, const f32x16& s1) {
 #pragma unroll
     for (int sub = 0; sub < 2; ++sub) {
       const f32x16& p = sub ? s1 : s0;
@@ -276,38 +263,101 @@ __global__ __launch_bounds__(NT, 3) void attn_split_kernel(AttnArgs a) {
       }
     }
   };
+
+  // Software pipeline over the tiles: step kt issues the score MFMAs of tile kt+1 (into the other
+  // score buffer) and, independent of them, exponentiates tile kt's scores computed one step earlier,
+  // so the in-order wave fills the MFMA gaps with that VALU; then tile kt's value product.  Ring of
+  // NSLOT slots, tile j in slot j % NSLOT: step kt reads K of tile kt+1 and V^T of tile kt; after its
+  // barrier (every wave done with step kt-1) tile kt+NSLOT-1 goes into tile kt-1's slot.
+  f32x16 sa0, sa1, sb0, sb1;
+  {
+    if (NSLOT == 4 && ntiles > 2) __builtin_amdgcn_s_waitcnt(waitcnt_vm(8));
+    else if (ntiles > 1) __builtin_amdgcn_s_waitcnt(waitcnt_vm(4));
+    else __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+    __builtin_amdgcn_s_barrier();
+    if (wave_live) {
+      scores(smem, sa0, sa1);
+      mask(0, sa0, sa1);
+      maxpath(true, sa0, sa1);
+    }
+  }
+  // SC: the slot of tile kt (compile-time: every fragment read is base + immediate offset)
+  auto step = [&](int kt, auto SC, f32x16& c0, f32x16& c1, f32x16& n0, f32x16& n1) {
+    constexpr int S = decltype(SC)::value;
+    const char* sl = smem + S * SLOT;
+    // tile kt+1 landed (NSLOT 4: tile kt+2's pieces may stay in flight); after the barrier tile kt+1 is
+    // visible to all and tile kt-1's slot takes tile kt+NSLOT-1 (no fragment read of this step
+    // touches that slot: the DMA goes out first)
+    if (NSLOT == 4 && kt + 2 < ntiles) __builtin_amdgcn_s_waitcnt(waitcnt_vm(4));
+    else __builtin_amdgcn_s_waitcnt(waitcnt_vm(0));
+    __builtin_amdgcn_s_barrier();
+    if (kt + NSLOT - 1 < ntiles) issue(kt + NSLOT - 1, (S + NSLOT - 1) % NSLOT);
+    if (wave_live) {
+      // tile kt+1's score MFMAs (the last step's read a stale slot: 12 MFMAs per work-group
+      // row, unused) with tile kt's exp2 / row sums in their gaps: two v_exp_f32 and two v_add_f32
+      // (24 issue cycles) per 32-cycle MFMA
+      scores(smem + ((S + 1) % NSLOT) * SLOT, n0, n1);
+      float t = expsum(c0, c1);
+      __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+      for (int i = 0; i < 12; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (i == 1) __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 5, 0);
+      }
+      // lazy softmax: tile kt was shifted by the running max as it stood when its scores were
+      // formed; a lane sum past LAZY_LIMIT (some p > 2^12) recomputes them from the K tile still in
+      // its slot and takes the max path (tile kt+1's scores, formed with the old m, move by the
+      // same shift)
+      if (__any(t > LAZY_LIMIT)) {
+        scores(sl, c0, c1);
+        mask(kt, c0, c1);
+        const float d = maxpath(false, c0, c1);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) { n0[r] -= d; n1[r] -= d; }
+        t = expsum(c0, c1);
+      }
+      l += t;
+      pv(sl, c0, c1);
+      constexpr int PM = 3, PS = 12;     // MFMAs / split VALU per 16-key group
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x002, PS, 0);
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int j = 0; j < PM; ++j) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          if (j == 0 && g < 3) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+          if (g < 3) __builtin_amdgcn_sched_group_barrier(0x002, PS / PM, 0);
+        }
+      if (kt + 1 < ntiles) mask(kt + 1, n0, n1);
+    }
+  };
   using C0 = std::integral_constant<int, 0>;
   using C1 = std::integral_constant<int, 1>;
   using C2 = std::integral_constant<int, 2>;
-  using NOM = std::false_type;
-  using MSK = std::true_type;
-  // every tile but the last unmasked; the last one masked only if it reaches past Tk
-  const int nfull = (a.Tk % KT) ? ntiles - 1 : ntiles;
+  using C3 = std::integral_constant<int, NSLOT == 4 ? 3 : 0>;
+  using C4 = std::integral_constant<int, NSLOT == 4 ? 0 : 1>;
+  using C5 = std::integral_constant<int, NSLOT == 4 ? 1 : 2>;
+  // unrolled by lcm(2, NSLOT) (score buffers alternate, ring slots cycle), slots as immediates
+  constexpr int U = NSLOT == 4 ? 4 : 6;
   int kt = 0;
-  for (; kt + 3 <= nfull; kt += 3) {
-    step(kt, C0{}, NOM{});
-    step(kt + 1, C1{}, NOM{});
-    step(kt + 2, C2{}, NOM{});
-  }
-  // 0-2 unmasked tiles left, then the masked one (if any); slots continue 0, 1, 2
-  const int rest = nfull - kt;
-  if (nfull < ntiles) {
-    if (rest == 0) {
-      step(kt, C0{}, MSK{});
-    } else if (rest == 1) {
-      step(kt, C0{}, NOM{});
-      step(kt + 1, C1{}, MSK{});
-    } else {
-      step(kt, C0{}, NOM{});
-      step(kt + 1, C1{}, NOM{});
-      step(kt + 2, C2{}, MSK{});
+  for (; kt + U <= ntiles; kt += U) {
+    step(kt, C0{}, sa0, sa1, sb0, sb1);
+    step(kt + 1, C1{}, sb0, sb1, sa0, sa1);
+    step(kt + 2, C2{}, sa0, sa1, sb0, sb1);
+    step(kt + 3, C3{}, sb0, sb1, sa0, sa1);
+    if constexpr (U == 6) {
+      step(kt + 4, C4{}, sa0, sa1, sb0, sb1);
+      step(kt + 5, C5{}, sb0, sb1, sa0, sa1);
     }
-  } else if (rest == 1) {
-    step(kt, C0{}, NOM{});
-  } else if (rest == 2) {
-    step(kt, C0{}, NOM{});
-    step(kt + 1, C1{}, NOM{});
   }
+  const int rest = ntiles - kt;
+  if (rest >= 1) step(kt, C0{}, sa0, sa1, sb0, sb1);
+  if (rest >= 2) step(kt + 1, C1{}, sb0, sb1, sa0, sa1);
+  if (rest >= 3) step(kt + 2, C2{}, sa0, sa1, sb0, sb1);
+  if (U == 6 && rest >= 4) step(kt + 3, C3{}, sb0, sb1, sa0, sa1);
+  if (U == 6 && rest >= 5) step(kt + 4, C4{}, sa0, sa1, sb0, sb1);
 
   if (!wave_live || q >= a.Tq) return;
   const float lt = l + __shfl_xor(l, 32, 64);   // the lane pair's two key halves

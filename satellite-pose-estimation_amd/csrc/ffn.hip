@@ -418,22 +418,15 @@ __global__ __launch_bounds__(NT, 1) void ffn_pipe_kernel(FfnArgs a) {
   // every fragment read is a lane base + an immediate offset: no per-read address VALU)
   auto sched_step = [&](int c, auto SC) {
     constexpr int S = decltype(SC)::value;
-#ifndef SPE_X_FFN_NODMA
     if (c + 2 < nch) wait_vmcnt<LOADS>();        // chunk c+1 landed, c+2 may stay in flight
     else wait_vmcnt<0>();
-#endif
-#ifndef SPE_X_FFN_NOBAR
     sync();
-#endif
     const char* st = lds + S * STAGE;
     const char* st1 = lds + ((S + 1) % NST) * STAGE;
     // read r in consumption order: r < 24 -> block k = r / 3: W1(c+1) ks = k jb 0, W2(c) nb = k,
     // W1(c+1) ks = k jb 1 (block k feeds interleaved steps MB*k .. MB*k + MB-1);
     // r >= 24 -> W2(c) nb = r - 16 (the tail)
     auto rd = [&](int r) {
-#ifdef SPE_X_FFN_NOLDS
-      if (c > 0) return;
-#endif
       if (r < 24) {
         const int k = r / 3, q = r % 3;
         if (q == 1) wb[k] = ld16(st + W1_BYTES + w2_off(16 * k + c16, g));
@@ -456,9 +449,7 @@ __global__ __launch_bounds__(NT, 1) void ffn_pipe_kernel(FfnArgs a) {
     for (int t = 0; t < 8 * MB; ++t) {
       const int upto = PRE + (3 * (t + 1) + MB - 1) / MB < 32 ? PRE + (3 * (t + 1) + MB - 1) / MB : 32;
       for (; issued < upto; ++issued) rd(issued);
-#ifndef SPE_X_FFN_NODMA
       if (t % MB == 1 % MB) dma.piece(a, c + 3, dst, wid, t / MB);
-#endif
       p1(2 * t);
       p1(2 * t + 1);
       p2(t);
@@ -488,26 +479,14 @@ __global__ __launch_bounds__(NT, 1) void ffn_pipe_kernel(FfnArgs a) {
     }
   } else
   for (int c = 0; c + 1 < nch; ++c) {
-#ifndef SPE_X_FFN_NODMA
     if (c + 2 < nch) wait_vmcnt<LOADS>();        // chunk c+1 landed, c+2 may stay in flight
     else wait_vmcnt<0>();
-#endif
-#ifndef SPE_X_FFN_NOBAR
     sync();
-#endif
     const char* st = lds + (c % NST) * STAGE;
     const char* st1 = lds + ((c + 1) % NST) * STAGE;
-#ifdef SPE_X_FFN_NOLDS
-    if (c == 0) {
-#endif
     read_w2(st);
     read_w1(st1);
-#ifdef SPE_X_FFN_NOLDS
-    }
-#endif
-#ifndef SPE_X_FFN_NODMA
     if (c + 3 < nch) dma.issue(a, c + 3, lds + ((c + 3) % NST) * STAGE, wid);
-#endif
     __builtin_amdgcn_sched_barrier(0);
     init_h(c + 1);
     // two phase-1 MFMAs per phase-2 MFMA until H(c+1) is complete, then the rest of phase 2

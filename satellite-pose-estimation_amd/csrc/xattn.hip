@@ -164,9 +164,7 @@ __global__ __launch_bounds__(NT, 1) void xattn_kernel(XattnArgs a) {
     __builtin_amdgcn_s_barrier();
     asm volatile("" ::: "memory");
     if (loader) {
-#ifndef SPE_X_XATTN_NODMA                         // (lab ablation builds only: timing, wrong results)
       if (it + NSTAGE - 1 < nt) issue(tile_at(it + NSTAGE - 1), (buf + NSTAGE - 1) % NSTAGE);
-#endif
       continue;
     }
     if (!live_wave) continue;
@@ -175,9 +173,6 @@ __global__ __launch_bounds__(NT, 1) void xattn_kernel(XattnArgs a) {
 
     // S^T - m: lane (row r32, hh) register r <-> key (r & 3) + 8 (r >> 2) + 4 hh
     f32x16 s;
-#ifdef SPE_X_XATTN_NOSCORE
-    s = negm;
-#else
     {
       f32x16 sa, sb;
 #pragma unroll
@@ -194,7 +189,6 @@ __global__ __launch_bounds__(NT, 1) void xattn_kernel(XattnArgs a) {
       }
       s = sa + sb;
     }
-#endif
     const int key_base = t * KT;
     if (key_base + KT > a.T) {
 #pragma unroll
@@ -250,9 +244,6 @@ __global__ __launch_bounds__(NT, 1) void xattn_kernel(XattnArgs a) {
         r[2 * ks + 1] = ds_read_tr(v_tr_addr(vbase, 16 * ks + 8 + 4 * hh, 128 * dh + 32 * db + dg, l16));
       }
     };
-#ifdef SPE_X_XATTN_NOPV
-    acc[0][0] += pb[0][0] + pb[1][0];           // (keeps P live)
-#else
     read_v(vr[0], 0);
 #pragma unroll
     for (int db = 0; db < DB; ++db) {
@@ -270,7 +261,6 @@ __global__ __launch_bounds__(NT, 1) void xattn_kernel(XattnArgs a) {
             __builtin_bit_cast(bf16x8, u32x4{r[2 * ks].x, r[2 * ks].y, r[2 * ks + 1].x, r[2 * ks + 1].y}), pb[ks],
             acc[db], 0, 0, 0);
     }
-#endif
   }
   if (!live_wave) return;
   // ---- partials: m, l (summed over the two lane halves) and the unnormalised U^T rows; lane
