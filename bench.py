@@ -106,6 +106,13 @@ def parse():
                    help="the parity mode timed after the main line in the same process (parity_mode object: its "
                         "own ms_per_step, value, roofline and accuracy against the exact-f32 mode)")
     p.add_argument("--no-parity", action="store_true", help="skip the parity_mode timing")
+    p.add_argument("--host-input-last", action="store_true",
+                   help="time the host_input object after the device-resident line (default: before it; timed "
+                        "second it measured ~12 %% slower in this process, while scripts/lab/host_input_ab.py, "
+                        "alternating the two pipelines, measures 10.38 vs 10.40 ms)")
+    p.add_argument("--no-host-input", action="store_true",
+                   help="skip the host_input object (the same step fed from pinned host memory: 8-bit crops "
+                        "copied H2D every step on a copy stream, REV/engine.py:92)")
     p.add_argument("--north-star", action="store_true",
                    help="also time the north-star shape at N = 1 (default only for N > 1): global batch 256 over the "
                         "ranks, RANSAC-P3P + LM, bf16 and the parity dtype, accuracy against exact f32")
@@ -710,6 +717,51 @@ def time_mode(pipe, model, args, world, dev, dtype, attn_dtype, cfg, B, launch_t
             "kernel_time_ms_per_step": {k: v[0] for k, v in sorted(tot.items(), key=lambda kv: -kv[1][0])}}
 
 
+def _lib_mode_ceres():
+    from spe import _lib
+    return _lib.SPE_PNP_EPNP_CERES
+
+
+def host_input_line(args, model, solver, cfg, world, rank, dev, overlap, B):
+    """The timed step fed the way the reference's evaluate() loop is (REV/engine.py:92,
+    samples.to(device)): every step's batch -- the 8-bit grayscale crops [B,S,S] that to_tensor +
+    Normalize turn into the model input (spe_forward_stages_u8 normalises them in the stem's input
+    pack), boxes and ground truth -- comes from pinned host memory through an H2D copy on a copy
+    stream, overlapped with the previous batch's compute.  Two pool batches alternate."""
+    import torch
+    from spe.pipeline import PosePipeline
+    from spe.synthetic import bench_images
+    pool = bench_images(cfg, rank * B, 2 * B)
+    pipe = PosePipeline(model, solver, B, device=dev, host_input=True, **overlap)
+    pipe.load_host(torch.from_numpy(pool["crops_u8"]), torch.from_numpy(pool["clip_bbox"]),
+                   torch.from_numpy(pool["quat"]), torch.from_numpy(pool["tvec"]))
+    torch.cuda.synchronize()
+    tm = time_mode(pipe, model, args, world, dev, args.dtype, args.attn_dtype, cfg, B)
+    # the PCIe rate of one batch's crops alone (pinned -> device, no compute beside it)
+    h, d = pipe.host["crops"][:B], pipe.dev_crops[0]
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(10):
+        d.copy_(h, non_blocking=True)
+    e1.record()
+    torch.cuda.synchronize()
+    copy_ms = e0.elapsed_time(e1) / 10
+    res = {"value": B * world * args.steps / tm["elapsed"], "unit": "images/s",
+           "ms_per_step": 1e3 * tm["elapsed"] / args.steps,
+           "input": f"8-bit grayscale crops [B,{cfg.input_size},{cfg.input_size}] + boxes + ground truth in pinned "
+                    "host memory, copied H2D every step on a copy stream (REV/engine.py:92); normalised on the "
+                    "device in the stem's input pack (bit-identical to the fp32 batch)",
+           "h2d_bytes_per_step": pipe.h2d_bytes,
+           "fp32_batch_bytes_per_step": B * 3 * cfg.input_size ** 2 * 4,
+           "h2d_copy_ms_alone": copy_ms, "h2d_GBps_alone": pipe.dev_crops[0].numel() / copy_ms / 1e6,
+           "kernel_time_ms_per_step": tm["kernel_time_ms_per_step"],
+           "dominant_avg_launch_ms": tm["roofline"]["avg_launch_ms"]}
+    del pipe
+    torch.cuda.synchronize()
+    return res
+
+
 def bench_weights_for(args, cfg, rcfg, rank, world, dev):
     """(weights, fit info, provenance) of a bench run.  DETR pose-consistent weights come from the
     committed head fixture when one exists for the shape (spe.synthetic.fixed_bench_weights:
@@ -897,10 +949,22 @@ def main():
                   area=image_areas(data, solver))
     torch.cuda.synchronize()
 
+    host = None
+    host_ok = (rcfg is None and not args.raw_frames and not args.no_host_input
+               and getattr(solver, "mode", None) != _lib_mode_ceres())
+    if host_ok and not args.host_input_last:
+        host = host_input_line(args, model, solver, cfg, world, rank, dev, overlap, B)
     tm = time_mode(pipe, model, args, world, dev, args.dtype, args.attn_dtype, cfg, B, args.launch_table)
     out = tm["out"]
     score = float((out["s_t"] + out["s_q"]).mean().item())
     status = out["poses"]["status"].cpu()
+
+    # ---- host input: the same step with every batch copied from pinned host memory
+    if host_ok:
+        if host is None:
+            host = host_input_line(args, model, solver, cfg, world, rank, dev, overlap, B)
+        host["value_vs_device_resident"] = host["value"] / (B * world * args.steps / tm["elapsed"])
+        host["timed_before_device_resident"] = not args.host_input_last
 
     # ---- parity mode: the same weights, batch and pipeline in the fast parity dtype, timed the
     # same way (its own steps between barriers), with its accuracy against the exact-f32 mode
@@ -978,6 +1042,9 @@ def main():
             result["keypoints_vs_gt_px"].update(fit)
         if acc is not None:
             result["accuracy_vs_fp32"] = acc
+    if host is not None:
+        result["value_host_input"] = host["value"]
+        result["host_input"] = host
     if parity is not None:
         result["parity_mode"] = parity
     if ns is not None:

@@ -176,6 +176,15 @@ int spe_forward(spe_model* m, void* stream, const float* images, int batch, void
 enum { SPE_STAGE_ENCODE = 1, SPE_STAGE_DECODE = 2, SPE_STAGE_BACKBONE = 4, SPE_STAGE_TRANSFORMER = 8 };
 int spe_forward_stages(spe_model* m, void* stream, const float* images, int batch, void* workspace,
                        int64_t workspace_bytes, const spe_forward_outputs* out, int stages);
+/* The same stages fed with the 8-bit crops the validation transform produces before to_tensor +
+ * Normalize (REV/datasets/speed.py:25-41, 209-233): crops = device [B][S][S][channels] u8 (channels 1:
+ * grayscale, which Image.convert('RGB') replicates into three channels -- the SPEED frames -- or 3
+ * RGB), normalised (u8 / 255 - mean) / std in fp32 inside the stem's input pack: bit-identical to
+ * spe_forward_stages on the fp32 batch normalised that way, at a quarter (RGB) or a twelfth (gray) of
+ * its bytes -- the form a host-side loader hands over PCIe (REV/engine.py:92 samples.to(device)).
+ * (ABI 8 addition) */
+int spe_forward_stages_u8(spe_model* m, void* stream, const uint8_t* crops, int channels, int batch, void* workspace,
+                          int64_t workspace_bytes, const spe_forward_outputs* out, int stages);
 
 /* Validation input pipeline on the device (SpeedTrain.__getitem__ with train=False,
  * REV/datasets/speed.py:209-233): generate_clip_bbox_val (:246-258), Pillow crop,

@@ -1,6 +1,6 @@
 // HBM-bound helpers of the backbone / transformer, vectorised 16 B per lane.
-//   pack_input   NCHW fp32 crop batch (REV/datasets/speed.py:25-41 output contract)
-//                -> NHWC with channels padded to 8 (stem implicit-GEMM operand)
+//   pack_input   NCHW fp32 crop batch (REV/datasets/speed.py:25-41 output contract), or the 8-bit
+//                crops it is normalised from -> NHWC with channels padded to 8 (stem operand)
 //   maxpool3s2   torchvision ResNet stem max-pool (3x3, stride 2, pad 1)
 //   upsample2x   nn.UpsamplingBilinear2d(scale_factor=2) == align_corners=True
 //                (REV/models/backbone.py:127,141)
@@ -11,14 +11,34 @@
 
 namespace {
 
-template <typename T, int CP = 8>
-__global__ void pack_input_kernel(const float* __restrict__ img, T* __restrict__ out, int B, int S, float* amax) {
+// input sources of the pack kernels: three channel values of pixel hw of image b
+struct SrcF32 {
+  const float* p; int S;
+  SPE_DEV void load(size_t b, size_t hw, float v[3]) const {
+    const float* src = p + b * 3 * S * S + hw;
+    v[0] = src[0]; v[1] = src[(size_t)S * S]; v[2] = src[2 * (size_t)S * S];
+  }
+};
+// 8-bit crops [B][S][S][C]: to_tensor (u8 / 255) + Normalize ((x - mean) / std), fp32, IEEE division
+// (ch = 1: one gray value feeds all three channels, as Image.convert('RGB') replicates it)
+struct SrcU8 {
+  const uint8_t* p; int S, C;
+  SPE_DEV void load(size_t b, size_t hw, float v[3]) const {
+    const float mean[3] = {0.485f, 0.456f, 0.406f}, stdv[3] = {0.229f, 0.224f, 0.225f};
+    const uint8_t* src = p + (b * S * S + hw) * C;
+#pragma unroll
+    for (int c = 0; c < 3; ++c) v[c] = ((float)src[C == 1 ? 0 : c] / 255.f - mean[c]) / stdv[c];
+  }
+};
+
+template <typename T, int CP = 8, typename Src = SrcF32>
+__global__ void pack_input_kernel(Src img, T* __restrict__ out, int B, int S, float* amax) {
   const size_t npx = (size_t)B * S * S;
   float am = 0.f;
   for (size_t p = blockIdx.x * (size_t)blockDim.x + threadIdx.x; p < npx; p += (size_t)gridDim.x * blockDim.x) {
     const size_t b = p / ((size_t)S * S), hw = p - b * S * S;
-    const float* src = img + b * 3 * S * S + hw;
-    float v[8] = {src[0], src[(size_t)S * S], src[2 * (size_t)S * S], 0.f, 0.f, 0.f, 0.f, 0.f};
+    float v[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    img.load(b, hw, v);
     am = fmaxf(am, fmaxf(fabsf(v[0]), fmaxf(fabsf(v[1]), fabsf(v[2]))));
     if constexpr (sizeof(T) == 2) {
       st16(out + p * 8, pack16<T>(v));
@@ -45,7 +65,8 @@ __global__ void pack_input_kernel(const float* __restrict__ img, T* __restrict__
 // 3-pixel zero border materialised (channel 3 zero), so a 16-byte chunk is two horizontally
 // adjacent pixels and every tap of the 7x7/s2 window is in range.  The border is rewritten on
 // every call (the buffer is shared with later activations).
-__global__ void pack_input_pad4_kernel(const float* __restrict__ img, bf16* __restrict__ out, int B, int S) {
+template <typename Src>
+__global__ void pack_input_pad4_kernel(Src img, bf16* __restrict__ out, int B, int S) {
   const int P = S + 6;
   const size_t npx = (size_t)B * P * P;
   for (size_t p = blockIdx.x * (size_t)blockDim.x + threadIdx.x; p < npx; p += (size_t)gridDim.x * blockDim.x) {
@@ -53,8 +74,9 @@ __global__ void pack_input_pad4_kernel(const float* __restrict__ img, bf16* __re
     const int r = (int)(p - b * P * P), y = r / P - 3, x = r % P - 3;
     u32x2 v{0, 0};
     if (y >= 0 && y < S && x >= 0 && x < S) {
-      const float* src = img + b * 3 * S * S + (size_t)y * S + x;
-      v = u32x2{pack_bf16x2(src[0], src[(size_t)S * S]), pack_bf16x2(src[2 * (size_t)S * S], 0.f)};
+      float c[3];
+      img.load(b, (size_t)y * S + x, c);
+      v = u32x2{pack_bf16x2(c[0], c[1]), pack_bf16x2(c[2], 0.f)};
     }
     st8(out + p * 4, v);
   }
@@ -287,22 +309,33 @@ inline int grid_for(size_t n, int block) {
 
 }  // namespace
 
-int spe_launch_pack_input(const float* img, void* out, int B, int S, int dtype, hipStream_t s, float* amax, int cpad) {
+int spe_launch_pack_input(const ImageSrc& img, void* out, int B, int S, int dtype, hipStream_t s, float* amax, int cpad) {
   const size_t n = (size_t)B * S * S;
-  if (dtype == SPE_DTYPE_BF16)
-    hipLaunchKernelGGL(pack_input_kernel<bf16>, grid_for(n, 256), 256, 0, s, img, (bf16*)out, B, S, (float*)nullptr);
-  else   // (fp32: at most 4096 workgroups, each publishing its max |x| once)
-  {
+  if (!img.f32 && !(img.u8 && (img.ch == 1 || img.ch == 3))) return -5;
+  const SrcF32 sf{img.f32, S};
+  const SrcU8 su{img.u8, S, img.ch};
+  if (dtype == SPE_DTYPE_BF16) {
+    if (img.f32) hipLaunchKernelGGL((pack_input_kernel<bf16, 8, SrcF32>), grid_for(n, 256), 256, 0, s, sf, (bf16*)out, B, S, (float*)nullptr);
+    else hipLaunchKernelGGL((pack_input_kernel<bf16, 8, SrcU8>), grid_for(n, 256), 256, 0, s, su, (bf16*)out, B, S, (float*)nullptr);
+  } else {   // (fp32: at most 4096 workgroups, each publishing its max |x| once)
     const int grid = std::min(grid_for(n, 256), 4096);
-    if (cpad == 4) hipLaunchKernelGGL((pack_input_kernel<float, 4>), grid, 256, 0, s, img, (float*)out, B, S, amax);
-    else hipLaunchKernelGGL((pack_input_kernel<float, 8>), grid, 256, 0, s, img, (float*)out, B, S, amax);
+    if (img.f32) {
+      if (cpad == 4) hipLaunchKernelGGL((pack_input_kernel<float, 4, SrcF32>), grid, 256, 0, s, sf, (float*)out, B, S, amax);
+      else hipLaunchKernelGGL((pack_input_kernel<float, 8, SrcF32>), grid, 256, 0, s, sf, (float*)out, B, S, amax);
+    } else {
+      if (cpad == 4) hipLaunchKernelGGL((pack_input_kernel<float, 4, SrcU8>), grid, 256, 0, s, su, (float*)out, B, S, amax);
+      else hipLaunchKernelGGL((pack_input_kernel<float, 8, SrcU8>), grid, 256, 0, s, su, (float*)out, B, S, amax);
+    }
   }
   return (int)hipGetLastError();
 }
 
-int spe_launch_pack_input_pad4(const float* img, void* out, int B, int S, hipStream_t s) {
+int spe_launch_pack_input_pad4(const ImageSrc& img, void* out, int B, int S, hipStream_t s) {
   const size_t n = (size_t)B * (S + 6) * (S + 6);
-  hipLaunchKernelGGL(pack_input_pad4_kernel, grid_for(n, 256), 256, 0, s, img, (bf16*)out, B, S);
+  if (img.f32) hipLaunchKernelGGL(pack_input_pad4_kernel<SrcF32>, grid_for(n, 256), 256, 0, s, SrcF32{img.f32, S}, (bf16*)out, B, S);
+  else if (img.u8 && (img.ch == 1 || img.ch == 3))
+    hipLaunchKernelGGL(pack_input_pad4_kernel<SrcU8>, grid_for(n, 256), 256, 0, s, SrcU8{img.u8, S, img.ch}, (bf16*)out, B, S);
+  else return -5;
   return (int)hipGetLastError();
 }
 

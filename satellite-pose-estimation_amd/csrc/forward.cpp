@@ -175,13 +175,28 @@ int spe_forward(spe_model* m, void* stream, const float* images, int B, void* wo
   return spe_forward_stages(m, stream, images, B, workspace, ws_bytes, out, SPE_STAGE_ENCODE | SPE_STAGE_DECODE);
 }
 
+static int forward_stages(spe_model* m, void* stream, const ImageSrc& images, int B, void* workspace, int64_t ws_bytes,
+                          const spe_forward_outputs* out, int stages);
+
 int spe_forward_stages(spe_model* m, void* stream, const float* images, int B, void* workspace, int64_t ws_bytes,
                        const spe_forward_outputs* out, int stages) {
+  return forward_stages(m, stream, ImageSrc{images, nullptr, 0}, B, workspace, ws_bytes, out, stages);
+}
+
+int spe_forward_stages_u8(spe_model* m, void* stream, const uint8_t* crops, int channels, int B, void* workspace,
+                          int64_t ws_bytes, const spe_forward_outputs* out, int stages) {
+  if ((stages & (SPE_STAGE_ENCODE | SPE_STAGE_BACKBONE)) && (!crops || (channels != 1 && channels != 3)))
+    return fail(SPE_E_ARG, "u8 crops: device pointer, 1 or 3 channels");
+  return forward_stages(m, stream, ImageSrc{nullptr, crops, channels}, B, workspace, ws_bytes, out, stages);
+}
+
+static int forward_stages(spe_model* m, void* stream, const ImageSrc& images, int B, void* workspace, int64_t ws_bytes,
+                          const spe_forward_outputs* out, int stages) {
   if (!m || !workspace || B <= 0 ||
       (stages & ~(SPE_STAGE_ENCODE | SPE_STAGE_DECODE | SPE_STAGE_BACKBONE | SPE_STAGE_TRANSFORMER)) || !stages)
     return fail(SPE_E_ARG, "bad argument");
   if (stages & SPE_STAGE_ENCODE) stages |= SPE_STAGE_BACKBONE | SPE_STAGE_TRANSFORMER;
-  if ((stages & SPE_STAGE_BACKBONE) && !images) return fail(SPE_E_ARG, "null images");
+  if ((stages & SPE_STAGE_BACKBONE) && !images.f32 && !images.u8) return fail(SPE_E_ARG, "null images");
   if ((stages & SPE_STAGE_DECODE) && (!out || !out->logits || !out->points)) return fail(SPE_E_ARG, "null outputs");
   if (m->family != 0) return fail(SPE_E_ARG, "not a DETR model (use spe_rtdetr_forward)");
   if (!m->finalized) return fail(SPE_E_STATE, "model not finalized");

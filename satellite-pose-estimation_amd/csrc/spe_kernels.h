@@ -229,12 +229,24 @@ int spe_ffn_splits(int M, int F);  // split count spe_launch_ffn_ln would use fo
 
 int spe_launch_preprocess(const uint8_t* frames, int B, int H, int W, int C, const double* bbox, int S,
                           float* images, float* clip_bbox, int32_t* status, hipStream_t s);
+// The model input: the ImageNet-normalised fp32 batch [B][3][S][S] (f32), or the 8-bit crops
+// [B][S][S][ch] (u8, ch = 1 grayscale -- SPEED's frames, Image.convert('RGB') replicating them --
+// or 3 RGB) that to_tensor + Normalize (REV/datasets/speed.py:25-41) turn into it: the pack kernels
+// normalise u8 / 255, (x - mean) / std in fp32, the reference's operation order (bit-identical to
+// the f32 input computed the same way)
+struct ImageSrc {
+  const float* f32; const uint8_t* u8; int ch;
+};
 // amax (fp32 output only, nullable): max |image| atomically maxed in (the stem GEMM's fp32h3 scale input)
 // cpad: channels per packed pixel (8; fp32 models' DETR stem: 4, one 16-byte chunk)
-int spe_launch_pack_input(const float* img, void* out, int B, int S, int dtype, hipStream_t s, float* amax = nullptr,
+int spe_launch_pack_input(const ImageSrc& img, void* out, int B, int S, int dtype, hipStream_t s, float* amax = nullptr,
                           int cpad = 8);
+inline int spe_launch_pack_input(const float* img, void* out, int B, int S, int dtype, hipStream_t s,
+                                 float* amax = nullptr, int cpad = 8) {
+  return spe_launch_pack_input(ImageSrc{img, nullptr, 0}, out, B, S, dtype, s, amax, cpad);
+}
 // bf16 [B][S+6][S+6][4], zero border of 3 (the pair-packed stem's input, forward.cpp)
-int spe_launch_pack_input_pad4(const float* img, void* out, int B, int S, hipStream_t s);
+int spe_launch_pack_input_pad4(const ImageSrc& img, void* out, int B, int S, hipStream_t s);
 // bf16 pair-packed stem (x: spe_launch_pack_input_pad4 layout, w: [64][ldw] k = (kh*8 + kw)*4 + ci)
 // + bias + ReLU + 3x3/s2/p1 max-pool in one pass (stempool.hip); out [B][Po][Po] rows of stride
 // ldo.  Returns 1 when the shape does not fit the kernel.

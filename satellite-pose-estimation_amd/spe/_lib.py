@@ -44,7 +44,7 @@ SPE_PNP_OK, SPE_PNP_NO_FG, SPE_PNP_CV_ERROR, SPE_PNP_RANSAC_FALLBACK, SPE_PNP_UN
 # every symbol include/spe.h declares (checked by tests/test_capi.py)
 EXPORTS = ["spe_abi_version", "spe_last_error", "spe_model_create", "spe_model_destroy", "spe_model_set_param",
            "spe_model_num_params", "spe_model_param_name", "spe_model_finalize", "spe_model_workspace_bytes",
-           "spe_forward", "spe_forward_stages", "spe_preprocess", "spe_criterion", "spe_ensemble_fuse", "spe_postprocess", "spe_pnp_batch", "spe_self_assess", "spe_speed_score", "spe_model_profile_begin",
+           "spe_forward", "spe_forward_stages", "spe_forward_stages_u8", "spe_preprocess", "spe_criterion", "spe_ensemble_fuse", "spe_postprocess", "spe_pnp_batch", "spe_self_assess", "spe_speed_score", "spe_model_profile_begin",
            "spe_model_profile_end", "spe_model_profile_get", "spe_debug_gemm", "spe_debug_gemm_path", "spe_debug_gemm_h3", "spe_debug_ffn_h3", "spe_debug_ffn_h3_perm", "spe_debug_gemm_planes", "spe_debug_attention",
            "spe_debug_layernorm", "spe_debug_ffn", "spe_debug_xattn", "spe_debug_upconv", "spe_debug_btail", "spe_debug_decsa", "spe_debug_decproj", "spe_debug_decxproj", "spe_debug_wfrag_pack", "spe_debug_decffn", "spe_debug_decq", "spe_debug_btail_perm", "spe_debug_stempool", "spe_rtdetr_create", "spe_rtdetr_forward",
            "spe_jpeg_workspace_bytes", "spe_jpeg_decode"]
@@ -103,6 +103,7 @@ def load(path: str):
     L.spe_model_workspace_bytes.restype = I64
     L.spe_forward.argtypes = [P, P, P, I, P, I64, ctypes.POINTER(ForwardOutputs)]
     L.spe_forward_stages.argtypes = [P, P, P, I, P, I64, ctypes.POINTER(ForwardOutputs), I]
+    L.spe_forward_stages_u8.argtypes = [P, P, P, I, I, P, I64, ctypes.POINTER(ForwardOutputs), I]
     L.spe_postprocess.argtypes = [P, P, P, P, I, I, P, P]
     L.spe_preprocess.argtypes = [P, P, I, I, I, I, P, I, P, P, P]
     L.spe_ensemble_fuse.argtypes = [P, P, P, I, I, I, I, P, P]

@@ -139,8 +139,24 @@ class DETR(nn.Module):
         stage = {None: _lib.SPE_STAGE_ENCODE, "backbone": _lib.SPE_STAGE_BACKBONE,
                  "transformer": _lib.SPE_STAGE_TRANSFORMER}[part]
         B = images.shape[0] if images is not None else int(B)
+        if images is not None and images.dtype == torch.uint8:
+            ch = self._crop_channels(images)
+            _lib.check(_lib.lib().spe_forward_stages_u8(self._h, _lib.stream_ptr(stream), _lib.ptr(images), ch, B,
+                                                        _lib.ptr(ws), ws.numel(), None, stage), "spe_forward_stages_u8")
+            return
         _lib.check(_lib.lib().spe_forward_stages(self._h, _lib.stream_ptr(stream), _lib.ptr(images), B, _lib.ptr(ws),
                                                  ws.numel(), None, stage), "spe_forward_stages")
+
+    def _crop_channels(self, crops):
+        """8-bit crops [B,S,S] (grayscale) or [B,S,S,3] (RGB), contiguous on the device -> channels."""
+        S = self.cfg.input_size
+        if not crops.is_cuda or not crops.is_contiguous():
+            raise ValueError("u8 crops: a contiguous device tensor")
+        if crops.dim() == 3 and tuple(crops.shape[1:]) == (S, S):
+            return 1
+        if crops.dim() == 4 and tuple(crops.shape[1:]) == (S, S, 3):
+            return 3
+        raise ValueError(f"u8 crops: expected [B,{S},{S}] or [B,{S},{S},3], got {tuple(crops.shape)}")
 
     def decode(self, B, ws, clip_bbox=None, stream=None, return_hs=False):
         """Decode stage (decoder, heads, fused PostProcess) of the memory an encode() left in `ws`."""
@@ -163,6 +179,19 @@ class DETR(nn.Module):
         images = samples.tensors if isinstance(samples, NestedTensor) else samples
         if not images.is_cuda:
             raise RuntimeError("DETR (HIP) expects device tensors; call samples.to('cuda')")
+        if images.dtype == torch.uint8:
+            # the 8-bit crops to_tensor + Normalize would make the batch from (spe_forward_stages_u8)
+            ch = self._crop_channels(images)
+            B, dev = images.shape[0], images.device
+            if clip_bbox is not None:
+                clip_bbox = clip_bbox.to(device=dev, dtype=torch.float32).contiguous()
+            out, o = self._outputs(B, dev, clip_bbox, return_hs)
+            ws = self.workspace(B, dev, stream)
+            _lib.check(_lib.lib().spe_forward_stages_u8(self._h, _lib.stream_ptr(stream), _lib.ptr(images), ch, B,
+                                                        _lib.ptr(ws), ws.numel(), ctypes.byref(o),
+                                                        _lib.SPE_STAGE_ENCODE | _lib.SPE_STAGE_DECODE),
+                       "spe_forward_stages_u8")
+            return out
         images = images.contiguous().float()
         B, C, H, W = images.shape
         S = self.cfg.input_size

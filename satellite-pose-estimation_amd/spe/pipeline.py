@@ -16,10 +16,29 @@ from .solver import PoseSolver
 from .speed_eval import device_speed_score
 
 
+_STREAMS = {}
+
+
+def pipeline_stream(device, role: str):
+    """One HIP stream per (device, role) for every pipeline of the process.  A process has a few
+    hardware queues (GPU_MAX_HW_QUEUES, 4 by default) that its streams are dealt onto; pipelines
+    that each made their own streams (the bench times a parity and a host-input line beside the main
+    one) would keep adding streams that end up sharing queues.  Pipelines on one device therefore
+    share their solver / decoder / encoder / copy streams (work on them is stream-ordered, correct
+    for any interleaving of the pipelines)."""
+    d = torch.device(device)
+    idx = d.index if d.index is not None or d.type != "cuda" else torch.cuda.current_device()
+    key = (d.type, idx, role)
+    st = _STREAMS.get(key)
+    if st is None:
+        _STREAMS[key] = st = torch.cuda.Stream(device=d)
+    return st
+
+
 class PosePipeline:
     def __init__(self, model: DETR, solver: PoseSolver, batch: int, device="cuda", use_graph: bool = False,
                  self_assess: bool = True, overlap: bool = False, raw_frames=None, overlap_decode: bool = False,
-                 jpeg_max_bytes: int = 0, overlap_backbone: bool = False):
+                 jpeg_max_bytes: int = 0, overlap_backbone: bool = False, host_input: bool = False):
         self.model, self.solver, self.B = model, solver, batch
         self.self_assess = self_assess
         # overlap: the solver / score / self-assessment of batch i run on a second HIP stream
@@ -37,7 +56,7 @@ class PosePipeline:
         self.overlap_decode = (overlap_decode or overlap_backbone) and not use_graph
         self.overlap_backbone = overlap_backbone and self.overlap_decode
         self.overlap = (overlap or self.overlap_decode) and not use_graph
-        self.solve_stream = torch.cuda.Stream(device=device) if self.overlap else None
+        self.solve_stream = pipeline_stream(device, "solve") if self.overlap else None
         self.device = torch.device(device)
         S, Q = model.cfg.input_size, model.cfg.num_queries
         dev = self.device
@@ -53,8 +72,8 @@ class PosePipeline:
         if not overlap_decode:
             model.workspace(batch, dev)           # sized outside any graph capture
         if self.overlap_decode:
-            self.dec_stream = torch.cuda.Stream(device=device)
-            self.enc_stream = torch.cuda.Stream(device=device) if self.overlap_backbone else None
+            self.dec_stream = pipeline_stream(device, "decode")
+            self.enc_stream = pipeline_stream(device, "encode") if self.overlap_backbone else None
             self.nslot = 3 if self.overlap_backbone else 2
             # the staged slots own their workspaces: a direct model(...) call or another
             # pipeline on the same model never writes into a slot's encoder memory
@@ -90,6 +109,22 @@ class PosePipeline:
             self.decoder = JpegDecoder(H, W, jpeg_max_bytes)
             self.jpeg = None
             self.dec_out = {"frames": self.frames, "status": torch.zeros(batch, dtype=torch.int32, device=dev)}
+        # host_input: each run() takes its batch from pinned host memory (load_host: the 8-bit crops
+        # to_tensor + Normalize make the model input from, plus boxes / ground truth), the next B of
+        # the pool in turn, as REV/engine.py:92's samples.to(device) does per batch.  The H2D copy goes
+        # on its own stream into the batch's slot buffers and the backbone waits for it only; with
+        # the staged overlap the copy of batch i runs under batch i-1's compute.
+        self.host_input = host_input
+        if host_input:
+            if use_graph or raw_frames is not None:
+                raise ValueError("host_input: eager, crop-level input (no graph, no raw frames)")
+            n = self.nslot if self.overlap_decode else 1
+            self.copy_stream = pipeline_stream(device, "copy")
+            self.host = None
+            self.host_next = 0
+            self.dev_crops = [None] * n
+            self.copied = [None] * n
+            self.h2d_bytes = 0
         self.use_graph = use_graph
         self.graph = None
         self.out = None
@@ -114,6 +149,51 @@ class PosePipeline:
         if self.decoder is not None:
             self.decoder(*self.jpeg, out=self.dec_out)
 
+    def _h2d(self, slot, after=()):
+        """Host-input mode: copy the next pool batch (pinned) into this slot's device buffers on the
+        copy stream, after the events in `after` (the slot's previous batch done with them); returns
+        the copy's completion event."""
+        h = self.host
+        if h is None:
+            raise RuntimeError("host_input pipeline: load_host() first")
+        j = self.host_next
+        self.host_next = (j + self.B) % h["crops"].shape[0]
+        cs = self.copy_stream
+        for ev in after:
+            if ev is not None:
+                cs.wait_event(ev)
+        if self.dev_crops[slot] is None:
+            self.dev_crops[slot] = torch.empty((self.B,) + tuple(h["crops"].shape[1:]), dtype=torch.uint8,
+                                               device=self.device)
+        clip = self.slot_clip[slot] if self.overlap_decode else self.clip_bbox
+        q = self.slot_q[slot] if self.overlap_decode else self.q_gt
+        t = self.slot_t[slot] if self.overlap_decode else self.t_gt
+        with torch.cuda.stream(cs):
+            self.dev_crops[slot].copy_(h["crops"][j:j + self.B], non_blocking=True)
+            clip.copy_(h["clip"][j:j + self.B], non_blocking=True)
+            q.copy_(h["q"][j:j + self.B], non_blocking=True)
+            t.copy_(h["t"][j:j + self.B], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(cs)
+        self.h2d_bytes = self.dev_crops[slot].numel() + clip.numel() * 4 + (q.numel() + t.numel()) * 8
+        return ev
+
+    def load_host(self, crops, clip_bbox, q_gt, t_gt):
+        """Host-input mode: the pool every run() takes its next B images from -- 8-bit crops
+        [N,S,S] / [N,S,S,3], boxes [N,4], quaternions [N,4], translations [N,3] (N a multiple of
+        B), kept in pinned host memory."""
+        if not self.host_input:
+            raise ValueError("load_host: pipeline built without host_input")
+        if crops.shape[0] % self.B or crops.dtype != torch.uint8:
+            raise ValueError("load_host: uint8 crops, a whole number of batches")
+        self.host = {"crops": crops.contiguous().pin_memory(),
+                     "clip": clip_bbox.to(torch.float32).contiguous().pin_memory(),
+                     "q": q_gt.to(torch.float64).contiguous().pin_memory(),
+                     "t": t_gt.to(torch.float64).contiguous().pin_memory()}
+        self.copy_stream.synchronize()                 # (a prefetch of the previous pool is dropped)
+        self.copied = [None] * len(self.copied)
+        self.host_next = 0
+
     def _body_staged(self):
         main = torch.cuda.current_stream()
         slot = self.calls % self.nslot
@@ -121,22 +201,34 @@ class PosePipeline:
         self._decode()
         if self.transform is not None:
             self.transform(self.frames, self.bbox, out=self.pp_out)
-        if self.dec_done[slot] is not None:
-            main.wait_event(self.dec_done[slot])      # batch i-nslot's decoder is done with this workspace
-        if self.solve_done[slot] is not None:
-            main.wait_event(self.solve_done[slot])    # ... and its solver / score with the slot's snapshots
-        self.slot_clip[slot].copy_(self.clip_bbox)
-        self.slot_q[slot].copy_(self.q_gt)
-        self.slot_t[slot].copy_(self.t_gt)
-        self.slot_repro[slot].copy_(self.repro)
+        images = self.images
+        if self.host_input:
+            # the copy into this slot was issued one run() ahead (below); the slot's previous batch
+            # (i - nslot) is done with its crops / snapshots once its decoder and solver are
+            ev = self.copied[slot]
+            if ev is None:
+                ev = self._h2d(slot, after=(self.dec_done[slot], self.solve_done[slot]))
+            self.copied[slot] = None
+            main.wait_event(ev)
+            images = self.dev_crops[slot]
+            self.slot_repro[slot].copy_(self.repro)
+        else:
+            if self.dec_done[slot] is not None:
+                main.wait_event(self.dec_done[slot])      # batch i-nslot's decoder is done with this workspace
+            if self.solve_done[slot] is not None:
+                main.wait_event(self.solve_done[slot])    # ... and its solver / score with the slot's snapshots
+            self.slot_clip[slot].copy_(self.clip_bbox)
+            self.slot_q[slot].copy_(self.q_gt)
+            self.slot_t[slot].copy_(self.t_gt)
+            self.slot_repro[slot].copy_(self.repro)
         if self.overlap_backbone:
-            self.model.encode(self.images, self.ws2[slot], stream=main, part="backbone")
+            self.model.encode(images, self.ws2[slot], stream=main, part="backbone")
             e = self.enc_stream
             e.wait_stream(main)
             with torch.cuda.stream(e):
                 self.model.encode(None, self.ws2[slot], stream=e, part="transformer", B=self.B)
         else:
-            self.model.encode(self.images, self.ws2[slot], stream=main)
+            self.model.encode(images, self.ws2[slot], stream=main)
             e = main
         d = self.dec_stream
         d.wait_stream(e)
@@ -156,6 +248,10 @@ class PosePipeline:
             ev.record(s1)
             self.solve_done[slot] = ev
         out["stream"] = s1
+        if self.host_input:
+            # prefetch: the next batch's H2D goes out now, under this batch's compute
+            nxt = self.calls % self.nslot
+            self.copied[nxt] = self._h2d(nxt, after=(self.dec_done[nxt], self.solve_done[nxt]))
         return out
 
     def _body(self):
@@ -164,7 +260,14 @@ class PosePipeline:
         self._decode()
         if self.transform is not None:
             self.transform(self.frames, self.bbox, out=self.pp_out)
-        fo = self.model(self.images, clip_bbox=self.clip_bbox)
+        images = self.images
+        if self.host_input:
+            # one slot: the copy waits for the previous forward (which read the crops) on this stream
+            prev = torch.cuda.Event()
+            prev.record(torch.cuda.current_stream())
+            torch.cuda.current_stream().wait_event(self._h2d(0, after=(prev,)))
+            images = self.dev_crops[0]
+        fo = self.model(images, clip_bbox=self.clip_bbox)
         if not self.overlap:
             return self._solve(fo)
         s1 = self.solve_stream

@@ -135,8 +135,10 @@ def clip_bbox_val(bbox, image_size=(Camera.nu, Camera.nv)):
 
 
 def synthetic_batch(cfg: SpeConfig, B: int, seed: int = 0, dtype=np.float32):
-    """B synthetic SPEED crops. Returns dict with images [B,3,S,S] (ImageNet-normalised),
-    quat [B,4], tvec [B,3], landmarks [B,11,2] (image px), clip_bbox [B,4]."""
+    """B synthetic SPEED crops. Returns dict with images [B,3,S,S] (ImageNet-normalised, fp32),
+    crops_u8 [B,S,S] (the 8-bit grayscale crops `images` is the to_tensor + Normalize of, in fp32 --
+    spe_forward_stages_u8's input), quat [B,4], tvec [B,3], landmarks [B,11,2] (image px),
+    clip_bbox [B,4]."""
     rng = np.random.Generator(np.random.PCG64(seed))
     S = cfg.input_size
     W = world_points()
@@ -145,6 +147,7 @@ def synthetic_batch(cfg: SpeConfig, B: int, seed: int = 0, dtype=np.float32):
     boxes = np.stack([clip_bbox_val([l[:, 0].min(), l[:, 1].min(), l[:, 0].max(), l[:, 1].max()]) for l in lm])
     ys, xs = np.meshgrid(np.arange(S, dtype=np.float32) + 0.5, np.arange(S, dtype=np.float32) + 0.5, indexing="ij")
     imgs = np.empty((B, 3, S, S), dtype=np.float32)
+    crops = np.empty((B, S, S), dtype=np.uint8)
     for i in range(B):
         x1, y1, x2, y2 = boxes[i]
         sx, sy = S / max(x2 - x1, 1e-3), S / max(y2 - y1, 1e-3)
@@ -153,10 +156,13 @@ def synthetic_batch(cfg: SpeConfig, B: int, seed: int = 0, dtype=np.float32):
         for (u, v) in lm[i]:
             cx, cy = (u - x1) * sx, (v - y1) * sy
             g += 200.0 * np.exp(-((xs - cx) ** 2 + (ys - cy) ** 2) / (2 * sig * sig))
-        g = np.clip(np.round(g), 0, 255) / 255.0
+        u8 = np.clip(np.round(g), 0, 255)
+        crops[i] = u8.astype(np.uint8)
+        g = u8 / 255.0                                   # (float32: to_tensor's u8 / 255)
         for c in range(3):
             imgs[i, c] = (g - IMAGENET_MEAN[c]) / IMAGENET_STD[c]
-    return {"images": imgs.astype(dtype), "quat": q, "tvec": t, "landmarks": lm, "clip_bbox": boxes}
+    return {"images": imgs.astype(dtype), "crops_u8": crops, "quat": q, "tvec": t, "landmarks": lm,
+            "clip_bbox": boxes}
 
 
 def synthetic_frames(B: int, seed: int = 0, height: int = Camera.nv, width: int = Camera.nu, channels: int = 1):

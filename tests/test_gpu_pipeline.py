@@ -274,3 +274,70 @@ def test_pipeline_from_jpeg_matches_raw_frames(gpu_device, small_model):
     assert torch.equal(jp.frames, raw.frames)
     for k in ("status", "quat", "tvec"):
         assert torch.equal(a["poses"][k], b["poses"][k]), k
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp32", "fp32h3"])
+def test_u8_crops_equal_normalised_batch(gpu_device, small_model, dtype):
+    """spe_forward_stages_u8: the 8-bit crops (grayscale [B,S,S] and RGB [B,S,S,3]) normalised in the
+    stem's input pack give bit-identical outputs to the fp32 batch to_tensor + Normalize makes of
+    them (REV/datasets/speed.py:25-41; numpy float32, the reference's operation order)."""
+    from spe.models import DETR
+    cfg, w, _ = small_model
+    m = DETR(cfg, dtype=dtype)
+    m.load_state_dict(w)
+    b = synthetic_batch(cfg, 6, 77)
+    dev = gpu_device
+    clip = torch.from_numpy(b["clip_bbox"]).float().to(dev)
+    mean = np.array([0.485, 0.456, 0.406], np.float32)
+    std = np.array([0.229, 0.224, 0.225], np.float32)
+    rgb = np.random.Generator(np.random.PCG64(5)).integers(0, 256, (6, cfg.input_size, cfg.input_size, 3), np.uint8)
+    for crops in (b["crops_u8"], rgb):
+        u = crops.astype(np.float32)
+        if u.ndim == 3:
+            u = u[..., None].repeat(3, -1)
+        x = np.stack([(u[..., c] / np.float32(255) - mean[c]) / std[c] for c in range(3)], 1)
+        if crops is b["crops_u8"]:
+            assert np.array_equal(x, b["images"])
+        ref = m(torch.from_numpy(x).to(dev), clip_bbox=clip)
+        got = m(torch.from_numpy(crops).to(dev), clip_bbox=clip)
+        torch.cuda.synchronize()
+        for k in ("pred_logits", "pred_points", "points_px", "probs"):
+            assert torch.equal(got[k], ref[k]), (dtype, crops.ndim, k)
+
+
+@pytest.mark.parametrize("staged", [False, True])
+def test_pipeline_host_input_matches_device_resident(gpu_device, small_model, staged):
+    """Host-input pipeline (every run() copies the next pool batch's 8-bit crops, boxes and ground
+    truth from pinned host memory on a copy stream; REV/engine.py:92) over consecutive batches that
+    cycle the pool and reuse every slot: poses and scores bit for bit those of the device-resident
+    pipeline fed each batch's fp32 images."""
+    from spe.models import DETR
+    from spe.pipeline import PosePipeline
+    from spe.solver import build_solver
+    cfg, w, _ = small_model
+    m = DETR(cfg, dtype="bf16")
+    m.load_state_dict(w)
+    B, dev = 8, gpu_device
+    solver = build_solver(argparse.Namespace(solver="ransac_p3p_lm", repro=20))
+    kw = dict(overlap_decode=True, overlap_backbone=True) if staged else dict(overlap=True)
+    host = PosePipeline(m, solver, B, device=dev, host_input=True, **kw)
+    batches = [synthetic_batch(cfg, B, 900 + k) for k in range(3)]
+    cat = {k: np.concatenate([bb[k] for bb in batches]) for k in ("crops_u8", "clip_bbox", "quat", "tvec")}
+    host.load_host(torch.from_numpy(cat["crops_u8"]), torch.from_numpy(cat["clip_bbox"]),
+                   torch.from_numpy(cat["quat"]), torch.from_numpy(cat["tvec"]))
+    order = [0, 1, 2, 0, 1, 2, 0]                     # the pool cycles; 7 runs reuse all three slots
+    outs = [host.run() for _ in order]
+    torch.cuda.synchronize()
+    ref = PosePipeline(m, solver, B, device=dev)
+    for k, o in zip(order, outs):
+        bb = batches[k]
+        ref.load(torch.from_numpy(bb["images"]).to(dev), torch.from_numpy(bb["clip_bbox"]).float().to(dev),
+                 torch.from_numpy(bb["quat"]).to(dev), torch.from_numpy(bb["tvec"]).to(dev))
+        r = ref.run()
+        torch.cuda.synchronize()
+        for f in ("points_px", "probs"):
+            assert torch.equal(o["forward"][f], r["forward"][f]), f
+        for f in ("status", "quat", "tvec"):
+            assert torch.equal(o["poses"][f], r["poses"][f]), f
+        assert torch.equal(o["s_t"], r["s_t"]) and torch.equal(o["s_q"], r["s_q"])
+    assert host.h2d_bytes == B * cfg.input_size ** 2 + B * 4 * 4 + B * 7 * 8
