@@ -376,6 +376,9 @@ class Fp32Reference:
         self.t_gt = torch.from_numpy(data["tvec"]).to(dev)
         st, sq = device_speed_score(self.pr["quat"], self.pr["tvec"], self.q_gt, self.t_gt)
         self.score = (st + sq).cpu().numpy()
+        # the self-assessment filter's flag (sigma head, BASELINE config 4)
+        self.reliable = (solver.self_assess(self.r["probs"], self.r["sigmas"], self.pr)["reliable"].bool()
+                         if self.r.get("sigmas") is not None else None)
         # float32 conditioning of each image's score (same HIP solver, one batch of B * ULP_DRAWS)
         B = self.score.shape[0]
         M = self.ULP_DRAWS
@@ -411,7 +414,9 @@ def accuracy_raw(model, ref, out):
     return {"hs_rel": hs_rel.cpu().numpy(), "label_agree": (lab_b == lab_r).cpu().numpy().ravel(),
             "d_px": d.cpu().numpy(), "d_norm": dn.cpu().numpy(), "d_per_crop": (d / wcrop[fg]).cpu().numpy(),
             "score_ref": ref.score, "score": (out["s_t"] + out["s_q"]).cpu().numpy(), "cond": ref.cond,
-            "status_agree": (ref.pr["status"] == out["poses"]["status"]).cpu().numpy()}
+            "status_agree": (ref.pr["status"] == out["poses"]["status"]).cpu().numpy(),
+            **({"reliable": (out["assess"]["reliable"].bool() == ref.reliable).cpu().numpy()}
+               if ref.reliable is not None and "assess" in out else {})}
 
 
 # The fp32 implementation spread of the per-image SPEED score:
@@ -423,30 +428,65 @@ SCORE_SPREAD_FILE = os.path.join(REPO, "profiles", "r5f_precision_score.json")
 SCORE_SPREAD_FILE_256 = os.path.join(REPO, "profiles", "r5f_precision_score_256.json")
 
 
-def spread_file(images):
-    """The committed spread study matching a batch of `images` pool images (the extreme-value max
-    grows with the batch, so a 256-image batch is held to the 256-image study when it exists)."""
+# configs 4 and 5 (tests/test_gpu_precision.py::test_fp32h3_within_fp32_spread_config, their own
+# solvers and shapes: sigma-weighted EPnP-RANSAC / 640x640 Q40 with P3P-RANSAC + LM)
+SCORE_SPREAD_FILE_CFG = {4: os.path.join(REPO, "profiles", "r6_precision_score_c4.json"),
+                         5: os.path.join(REPO, "profiles", "r6_precision_score_c5.json")}
+
+
+def spread_file(images, config=2):
+    """The committed spread study matching a batch of `images` pool images of BASELINE config
+    `config` (the extreme-value max grows with the batch, so a 256-image batch is held to the
+    256-image study when it exists)."""
+    if config in SCORE_SPREAD_FILE_CFG:
+        return SCORE_SPREAD_FILE_CFG[config]
     return SCORE_SPREAD_FILE_256 if images >= 256 and os.path.exists(SCORE_SPREAD_FILE_256) else SCORE_SPREAD_FILE
 
 
-def score_spread(solver, images=64):
+def score_spread(solver, images=64, config=2):
     """{'frac', 'median', 'max'} of torch-CPU vs ours-fp32 (max: the largest disagreement of any two fp32
-    implementations -- torch-CPU, torch-GPU, ours) for `solver` ('epnp' / 'ransac_p3p_lm'), or None."""
+    implementations -- torch-CPU, torch-GPU, ours) for `solver` on config `config`'s shape, or None."""
     try:
-        d = json.load(open(spread_file(images)))["score"][solver]["pairs"]
+        st = json.load(open(spread_file(images, config)))["score"][solver]
     except Exception:
         return None
+    per = st.get("per_image")
+    if per is not None and len(per["torch_cpu_vs_fp32"]) >= images:
+        # the study's per-image deltas on exactly the bench's images (pool images 0..images-1)
+        import numpy as np
+        d = {k: np.asarray(v[:images], np.float64) for k, v in per.items()}
+        cpu = d["torch_cpu_vs_fp32"][np.isfinite(d["torch_cpu_vs_fp32"])]
+        mx = max(float(np.nanmax(v)) for v in d.values())
+        return {"frac": float((cpu <= 1e-4).mean()), "median": float(np.median(cpu)), "max": mx, "images": images}
+    d = st["pairs"]
     cpu, gpu, cg = d["torch_cpu_vs_fp32"], d["torch_gpu_vs_fp32"], d["torch_cpu_vs_torch_gpu"]
     return {"frac": cpu["frac_le_1e-4"], "median": cpu["median"], "max": max(cpu["max"], gpu["max"], cg["max"])}
 
 
-def accuracy_summary(raw, solver=None):
+def reliable_spread(config, images=64):
+    """torch-CPU's agreement with the exact-f32 mode on the self-assessment `reliable` flag (config 4's
+    study; over its first `images` images when it holds them per image), or None."""
+    try:
+        r = json.load(open(spread_file(images, config)))["reliable"]
+    except Exception:
+        return None
+    per = r.get("per_image_torch_cpu_vs_fp32")
+    if per is not None and len(per) >= images:
+        return float(sum(per[:images]) / images)
+    return r["torch_cpu_vs_fp32"]
+
+
+def accuracy_summary(raw, solver=None, config=2):
     """Accuracy of a timed mode against the fp32 parity mode: keypoint deltas of the foreground
     queries both label alike, label agreement, hs relative error, and the SPEED-score delta of the
     two modes' poses through the same solver -- overall, and over the images whose score is
     well-conditioned at float32 resolution (Fp32Reference.cond <= 1e-4).
-    `meets_1e-4_score_within_fp32_spread`: the score half of the contract against the spread of two
-    fp32 implementations of the reference (score_spread; the gates of tests/test_gpu_precision.py)."""
+    `score_within_fp32_spread`: the score half of the contract held to the spread of two fp32
+    implementations of the reference instead of the strict 1e-4 (score_spread; the gates of
+    tests/test_gpu_precision.py) -- the strict per-image `meets_1e-4_score` stays reported beside it;
+    `meets_1e-4_within_fp32_spread` = `meets_1e-4_kpt` and `score_within_fp32_spread`.  With the sigma
+    head: `reliable_agreement`, the share of images whose self-assessment flag equals the exact-f32
+    mode's (config 4)."""
     import numpy as np
     sc_r, sc_b, cond = raw["score_ref"], raw["score"], raw["cond"]
     both = np.isfinite(sc_r) & np.isfinite(sc_b)
@@ -476,24 +516,32 @@ def accuracy_summary(raw, solver=None):
     res["meets_1e-4_kpt"] = bool(res["kpt_norm_max"] <= 1e-4)
     res["meets_1e-4_score"] = bool((res["score_delta_max"] or 0.0) <= 1e-4)
     res["meets_1e-4"] = res["meets_1e-4_kpt"] and res["meets_1e-4_score"]
-    sp = score_spread(solver, len(sc_r)) if solver else None
+    if "reliable" in raw:
+        res["reliable_agreement"] = float(raw["reliable"].mean())
+        rs = reliable_spread(config, len(raw["reliable"]))
+        if rs is not None:
+            res["reliable_agreement_torch_cpu_vs_fp32"] = rs
+            res["reliable_within_fp32_spread"] = bool(res["reliable_agreement"] >= rs - 0.05)
+    sp = score_spread(solver, len(sc_r), config) if solver else None
     if sp is not None and ds.size:
         res["score_fp32_spread"] = {
             "definition": "per-image |SPEED score - exact-f32 score| <= 1e-4 on at least the fraction of images the "
                           "reference's own fp32 CPU execution reaches - 0.05, median <= 2x its median, max <= the largest "
                           "disagreement of two fp32 implementations (torch-CPU / torch-GPU restatements and the exact-f32 "
                           "mode, same HIP solver)",
-            "source": os.path.relpath(spread_file(len(sc_r)), REPO) + " (pool images 0.."
-                      + ("255" if spread_file(len(sc_r)) == SCORE_SPREAD_FILE_256 else "63") + ", " + solver + ")",
-            "spread_frac_le_1e-4": sp["frac"], "spread_median": sp["median"], "spread_max": sp["max"]}
-        res["meets_1e-4_score_within_fp32_spread"] = bool(
+            "source": os.path.relpath(spread_file(len(sc_r), config), REPO) + " (pool images 0.."
+                      + str(sp["images"] - 1 if "images" in sp else
+                            255 if spread_file(len(sc_r), config) == SCORE_SPREAD_FILE_256 else 63) + ", " + solver + ")",
+            "spread_frac_le_1e-4": sp["frac"], "spread_median": sp["median"], "spread_max": sp["max"],
+            **({"spread_images": sp["images"]} if "images" in sp else {})}
+        res["score_within_fp32_spread"] = bool(
             res["frac_score_delta_le_1e-4"] >= sp["frac"] - 0.05 and res["score_delta_median"] <= 2 * sp["median"]
             and res["score_delta_max"] <= sp["max"])
-        res["meets_1e-4_within_fp32_spread"] = res["meets_1e-4_kpt"] and res["meets_1e-4_score_within_fp32_spread"]
+        res["meets_1e-4_within_fp32_spread"] = res["meets_1e-4_kpt"] and res["score_within_fp32_spread"]
     return res
 
 
-def accuracy_vs_fp32(model, ref, out, world=1, solver=None):
+def accuracy_vs_fp32(model, ref, out, world=1, solver=None, config=2):
     """accuracy_summary over all ranks' images (one all_gather_object of the raw deltas)."""
     import numpy as np
     raw = accuracy_raw(model, ref, out)
@@ -502,7 +550,7 @@ def accuracy_vs_fp32(model, ref, out, world=1, solver=None):
         parts = [None] * world
         dist.all_gather_object(parts, raw)
         raw = {k: np.concatenate([p[k] for p in parts]) for k in raw}
-    return accuracy_summary(raw, solver)
+    return accuracy_summary(raw, solver, config)
 
 
 def traffic_for(kind, grid, attn_dtype):
@@ -973,7 +1021,8 @@ def main():
     ref = None
     if rcfg is None and not args.raw_frames and not args.no_accuracy and (args.dtype != "fp32" or want_parity):
         ref = Fp32Reference(cfg, w, data, solver, dev)
-    acc = accuracy_vs_fp32(model, ref, out, world, args.solver) if (ref is not None and args.dtype != "fp32") else None
+    acc = (accuracy_vs_fp32(model, ref, out, world, args.solver, args.config)
+           if (ref is not None and args.dtype != "fp32") else None)
     if want_parity:
         del pipe
         pm = DETR(cfg, dtype=args.parity_dtype)
@@ -991,7 +1040,7 @@ def main():
         parity["roofline"] = pt["roofline"]
         parity["kernel_time_ms_per_step"] = pt["kernel_time_ms_per_step"]
         if ref is not None:
-            parity["accuracy_vs_fp32"] = accuracy_vs_fp32(pm, ref, pt["out"], world, args.solver)
+            parity["accuracy_vs_fp32"] = accuracy_vs_fp32(pm, ref, pt["out"], world, args.solver, args.config)
         del ppipe, pm
         torch.cuda.synchronize()
         torch.cuda.empty_cache()

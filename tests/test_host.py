@@ -363,11 +363,11 @@ def test_bench_score_contract_against_fp32_spread():
     good[:4] = 2e-3                                    # 94 % within 1e-4, small worst case
     a = bench.accuracy_summary(raw(good), "epnp")
     assert a["meets_1e-4_kpt"] and not a["meets_1e-4_score"]
-    assert a["meets_1e-4_score_within_fp32_spread"] and a["meets_1e-4_within_fp32_spread"]
+    assert a["score_within_fp32_spread"] and a["meets_1e-4_within_fp32_spread"]
     bad = np.full(n, 1e-5)
     bad[: n // 2] = 1e-3                               # half the images outside 1e-4
-    assert not bench.accuracy_summary(raw(bad), "epnp")["meets_1e-4_score_within_fp32_spread"]
+    assert not bench.accuracy_summary(raw(bad), "epnp")["score_within_fp32_spread"]
     worst = good.copy()
     worst[0] = 10.0 * sp["max"]
-    assert not bench.accuracy_summary(raw(worst), "epnp")["meets_1e-4_score_within_fp32_spread"]
-    assert "meets_1e-4_score_within_fp32_spread" not in bench.accuracy_summary(raw(good), None)
+    assert not bench.accuracy_summary(raw(worst), "epnp")["score_within_fp32_spread"]
+    assert "score_within_fp32_spread" not in bench.accuracy_summary(raw(good), None)
