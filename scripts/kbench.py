@@ -104,6 +104,37 @@ def main():
                                      B * T, D, F, None, 0)
         ms = timeit(fn, a.iters)
         print(f"ffn.enc chunk-packed W2  {ms:.3f} ms  {fl / ms / 1e9:.1f} TF/s")
+    if a.which in ("ffnh3",):
+        # the fp32h3 one-pass encoder FFN (ffn_h3.hip) at the bench's M = B * 2704 rows, weights in the
+        # finalize form (h3 row planes, W2 columns in spe_ffn_h3_perm order); numerics: test_ffn_h3_one_pass
+        import math
+        M = B * T
+        x = torch.nn.functional.layer_norm(torch.randn(M, D, generator=g), (D,)).to(dev)
+        W1 = torch.randn(F, D, generator=g) / 16
+        W2 = torch.randn(D, F, generator=g) / F ** 0.5
+
+        def planes(W):
+            am = W.abs().amax(1)
+            e = torch.frexp(am).exponent.float()
+            sc = torch.pow(2.0, 13 - e)[:, None]
+            xx = W * sc
+            h = xx.to(torch.float16)
+            return torch.stack([h, (xx - h.float()).to(torch.float16)]).contiguous(), (1.0 / sc[:, 0]).contiguous()
+        w1p, s1 = planes(W1)
+        meta = torch.stack([s1.view(F // 32, 32), torch.zeros(F // 32, 32)], 1).reshape(-1).contiguous()
+        perm = torch.tensor([L.spe_debug_ffn_h3_perm(q) for q in range(32)])
+        cols = (torch.arange(F) // 32) * 32 + perm[torch.arange(F) % 32]
+        w2p, s2 = planes(W2[:, cols].contiguous())
+        keep = [t.to(dev).contiguous() for t in (w1p, meta, w2p, s2, torch.zeros(D), torch.ones(D), torch.zeros(D))]
+        amax = x.abs().max().reshape(1).contiguous()
+        sh = 2.0 ** (13 - math.frexp(64.0)[1])
+        y = torch.empty_like(x)
+        fn = lambda: L.spe_debug_ffn_h3(None, p(x), D, p(y), D, M, F, p(keep[0]), D, p(keep[1]), p(keep[2]), F,
+                                         p(keep[3]), p(keep[4]), p(keep[5]), p(keep[6]), p(amax), sh)
+        assert fn() == 0
+        ms = timeit(fn, a.iters)
+        fl = 4.0 * M * D * F
+        print(f"ffn.enc h3  {ms:.3f} ms  {fl / ms / 1e9:.1f} TF/s")
     if a.which in ("ffndec", "all"):
         # the decoder's few-row FFN (M = B * 11): split-F partials over `splits` workgroups per
         # 128-row tile, then the reduce + LayerNorm kernel

@@ -14,7 +14,7 @@ import os
 
 def short(name):
     n = name.replace("(anonymous namespace)::", "")
-    for key in ("attn_split_kernel", "gemm_h3d", "gemm_x6d_kernel", "gemm_x6_kernel", "attn_x3_kernel", "sgemm_kernel", "gemm2_kernel", "gemm_kernel", "ffn_pipe_kernel", "attn_bf16", "attn_f32", "ffn_ln", "layernorm", "heads", "pnp_kernel",
+    for key in ("attn_split_kernel", "ffn_h3_kernel", "gemm_h3d", "gemm_x6d_kernel", "gemm_x6_kernel", "attn_x3_kernel", "sgemm_kernel", "gemm2_kernel", "gemm_kernel", "ffn_pipe_kernel", "attn_bf16", "attn_f32", "ffn_ln", "layernorm", "heads", "pnp_kernel",
                 "maxpool", "upsample", "pack_input", "postprocess", "score"):
         if key in n:
             return n[n.find(key):].replace("(GemmArgs", "(").split("(")[0][:64]
