@@ -219,6 +219,14 @@ static int forward_stages(spe_model* m, void* stream, const ImageSrc& images, in
   // [SPE_AMAX_BB, SPE_AMAX_SLOTS); each stage zeroes its own range first.
   float* const amx = m->h3 ? (float*)P(w.amax) : nullptr;
   float* const src_amax0 = amx ? amx + SPE_AMAX_BB - 1 : nullptr;
+  // (the slot counts are checked before anything is launched: a slot handed out past its range would
+  // be the encoder's input scale or a transformer slot, overwritten before an error could return)
+  if (amx && (stages & SPE_STAGE_BACKBONE) && 2 + 3 * (int)m->blocks.size() + 2 > SPE_AMAX_BB - 1)
+    return fail(SPE_E_STATE, "fp32h3: backbone activation-scale slots exhausted");
+  if (amx && (stages & SPE_STAGE_TRANSFORMER) && 2 * (int)m->enc.size() > SPE_AMAX_DEC - SPE_AMAX_BB - 1)
+    return fail(SPE_E_STATE, "fp32h3: encoder activation-scale slots exhausted");
+  if (amx && (stages & SPE_STAGE_DECODE) && 2 * c.dec_layers > SPE_AMAX_SLOTS - SPE_AMAX_DEC)
+    return fail(SPE_E_STATE, "fp32h3: decoder activation-scale slots exhausted");
   if (stages & SPE_STAGE_BACKBONE) {
   int na = 0;
   auto slot = [&]() -> float* { return amx ? amx + na++ : nullptr; };
@@ -395,7 +403,7 @@ static int forward_stages(spe_model* m, void* stream, const ImageSrc& images, in
     CK(run_gemm(m, "gemm.input_proj", g, GEMM_LINEAR, s));
   }
   }
-  if (na > SPE_AMAX_BB - 1) return fail(SPE_E_STATE, "fp32h3: backbone activation-scale slots exhausted");
+  if (na > SPE_AMAX_BB - 1) return fail(SPE_E_STATE, "fp32h3: backbone slot count out of step with the up-front check");
   }  // SPE_STAGE_BACKBONE
   if (stages & SPE_STAGE_TRANSFORMER) {
   float* const tam = amx ? amx + SPE_AMAX_BB : nullptr;

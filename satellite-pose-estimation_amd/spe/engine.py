@@ -19,6 +19,16 @@ from .speed_eval import SpeedEval, device_speed_score
 @torch.no_grad()
 def evaluate(model, criterion, postprocessors, data_loader, gt_file, solver, device, output_dir=None):
     evaluator = SpeedEval(gt_file, solver)
+    ceres = getattr(solver, "mode", None) == _lib.SPE_PNP_EPNP_CERES
+    if ceres:
+        # EPnPCeresSolver's per-image thresholds come from the ground-truth box areas: refuse up front a
+        # ground truth without them (load_ground_truth sets "area" only from bbox_xxyy).  The area-driven
+        # threshold itself is parity unpinned: the REV SpeedEval calls the solver without an area
+        # (REV/datasets/speed.py:399, commented out); UNC's passes it (speed_dataset.py:396-399).
+        missing = [f for f, g in evaluator.ground_truth.items() if "area" not in g]
+        if missing:
+            raise ValueError(f"EPnPCeresSolver evaluation needs ground-truth box areas (bbox_xxyy); "
+                             f"{len(missing)} entries lack them, e.g. {missing[0]}")
     meters = {}
 
     def log(k, v):
@@ -47,7 +57,7 @@ def evaluate(model, criterion, postprocessors, data_loader, gt_file, solver, dev
                 log(k + "_unscaled", v)
             log("class_error", ld["class_error"])
         gt = [evaluator.ground_truth[f] for f in filenames]
-        if getattr(solver, "mode", None) == _lib.SPE_PNP_EPNP_CERES:
+        if ceres:
             # EPnPCeresSolver: one threshold per image from its ground-truth box area (UNC SpeedEval
             # passes ground_truth[filename]["area"], src/data/speed/speed_dataset.py:396-399)
             poses = solver.solve_batch(outputs["points_px"], outputs["probs"], outputs.get("sigmas"),

@@ -371,3 +371,15 @@ def test_bench_score_contract_against_fp32_spread():
     worst[0] = 10.0 * sp["max"]
     assert not bench.accuracy_summary(raw(worst), "epnp")["score_within_fp32_spread"]
     assert "score_within_fp32_spread" not in bench.accuracy_summary(raw(good), None)
+
+
+def test_evaluate_ceres_refuses_ground_truth_without_areas():
+    """evaluate() with the EPnPCeresSolver checks up front that every ground-truth entry
+    carries the box area its per-image threshold comes from, instead of a KeyError mid-evaluation."""
+    from spe.engine import evaluate
+    from spe.solver import EPnPCeresSolver
+    gt = [{"filename": "img000001.jpg", "q_vbs2tango": [1, 0, 0, 0], "r_Vo2To_vbs_true": [0, 0, 10]},
+          {"filename": "img000002.jpg", "q_vbs2tango": [1, 0, 0, 0], "r_Vo2To_vbs_true": [0, 0, 9],
+           "bbox_xxyy": [10, 20, 110, 140]}]
+    with pytest.raises(ValueError, match="box areas"):
+        evaluate(None, None, None, [], gt, EPnPCeresSolver(input_size=256), "cpu")
