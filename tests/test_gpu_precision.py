@@ -56,6 +56,16 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 B = int(os.environ.get("SPE_PRECISION_IMAGES", "64"))
 
 
+def _progress(msg):
+    """A progress line on stdout and, when a gpurun_out/ scratch directory exists, appended to a file
+    there: the CPU restatement passes run for minutes with pytest capturing stdout."""
+    print(msg, flush=True)
+    out = os.path.join(REPO, "gpurun_out")
+    if os.path.isdir(out):
+        with open(os.path.join(out, "precision_progress.log"), "a") as f:
+            f.write(msg + "\n")
+
+
 def _kpt(a, b, fg):
     return float((a - b).abs().amax(-1)[fg].max())
 
@@ -114,7 +124,7 @@ def test_fp32x6_within_fp32_implementation_spread(gpu_device):
                 outs = []
                 for i in range(0, len(images), 16):       # (progress lines: a long CPU pass stays visible)
                     outs.append(model_ref.forward(images[i:i + 16], w, cfg))
-                    print(f"torch {device}: {i + 16}/{len(images)} images", flush=True)
+                    _progress(f"torch {device}: {i + 16}/{len(images)} images")
         finally:
             torch.backends.cuda.matmul.allow_tf32, torch.backends.cudnn.allow_tf32 = mm, cv
         lg = torch.cat([o["pred_logits"] for o in outs]).float().cpu()
@@ -281,8 +291,11 @@ def test_fp32h3_within_fp32_spread_config(gpu_device, config):
     cfg = SpeConfig(input_size=cc["size"], num_queries=cc["queries"], enc_layers=cc["layers"],
                     dec_layers=cc["layers"], sigma_head=cc["sigma_head"])
     args = argparse.Namespace(weights="pose-consistent")
+    _progress(f"config {config}: bench weights")
     w, _, wsource = bench.bench_weights_for(args, cfg, None, 0, 1, dev)
-    nb = int(os.environ.get("SPE_PRECISION_IMAGES_CFG", "64"))
+    _progress(f"config {config}: weights ready ({wsource})")
+    # (config 5: the 32 images of its bench line -- the 640 x 640 CPU restatement is the long pole)
+    nb = int(os.environ.get("SPE_PRECISION_IMAGES_CFG", "64" if config == 4 else "32"))
     data = bench_images(cfg, 0, nb)
     x = torch.from_numpy(data["images"]).to(dev)
     clip = torch.from_numpy(data["clip_bbox"]).float().to(dev)
@@ -290,6 +303,7 @@ def test_fp32h3_within_fp32_spread_config(gpu_device, config):
     t_gt = torch.from_numpy(data["tvec"]).to(dev)
     impl = {}                                      # name -> (pred_points, points_px, probs, sigmas)
     for dt in ("fp32", "fp32h3", "bf16"):
+        _progress(f"config {config}: {dt} forward")
         m = DETR(cfg, dtype=dt, attn_dtype="fp16" if (dt == "bf16" and config == 5) else dt)
         m.load_state_dict(w)
         outs = [m(x[i:i + 16], clip_bbox=clip[i:i + 16]) for i in range(0, nb, 16)]
@@ -306,7 +320,7 @@ def test_fp32h3_within_fp32_spread_config(gpu_device, config):
                 outs = []
                 for i in range(0, len(images), 8):
                     outs.append(model_ref.forward(images[i:i + 8], w, cfg))
-                    print(f"torch {device}: {i + 8}/{len(images)} images", flush=True)
+                    _progress(f"config {config} torch {device}: {i + 8}/{len(images)} images")
         finally:
             torch.backends.cuda.matmul.allow_tf32, torch.backends.cudnn.allow_tf32 = mm, cv
         lg = torch.cat([o["pred_logits"] for o in outs]).float().cpu()
@@ -368,7 +382,7 @@ def test_fp32h3_within_fp32_spread_config(gpu_device, config):
     print(json.dumps(r))
 
     k = r["kpt"]
-    assert fg.sum() > 100
+    assert fg.sum() > 50
     assert k["fp32h3_vs_ours_fp32"] <= 2 * k["ours_fp32_vs_torch_gpu"] + 1e-5, k
     # 1e-4 of torch-CPU, or -- where two fp32 implementations already disagree by more (config 5's
     # 640 / Q40 shape: ours-fp32 vs torch-CPU 1.4e-4, profiles/r6_precision_score_c5.json) -- within
