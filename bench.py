@@ -741,17 +741,18 @@ def time_mode(pipe, model, args, world, dev, dtype, attn_dtype, cfg, B, launch_t
         achieved = (k_by / max(k_n, 1)) / (avg_ms * 1e-3) / 1e9
         peak, unit = PEAK["hbm"], "GB/s"
     prof_ms = tot[dominant][0] / max(tot[dominant][1], 1)
-    # (fp32x3 / fp32x6: attn_x3_kernel<true>, K / V^T pre-split by the projections, unless
-    # SPE_ATTN_PRESPLIT=0)
-    ps = "<true>" if os.environ.get("SPE_ATTN_PRESPLIT", "1") != "0" else "<false>"
-    symbol = ({"fp32": "attn_f32_kernel", "fp32x3": "attn_x3_kernel" + ps, "fp32x6": "attn_x3_kernel" + ps,
-               "fp32h3": "attn_x3_kernel" + ps}[dtype]
+    # (fp32x3 / fp32x6 / fp32h3: K / V^T pre-split by the projections in the 16-bit key order -> the
+    # LDS-DMA split kernel attn_split.hip, fp16 V planes in fp32h3; SPE_ATTN_PRESPLIT=0: attn_x3_kernel)
+    split = os.environ.get("SPE_ATTN_PRESPLIT", "1") != "0" and cfg.tokens % 16 == 0
+    sym3 = "attn_split_kernel<false>" if split else "attn_x3_kernel<false>"
+    symbol = ({"fp32": "attn_f32_kernel", "fp32x3": sym3, "fp32x6": sym3,
+               "fp32h3": "attn_split_kernel<true>" if split else "attn_x3_kernel<false>"}[dtype]
               if dominant == "attn.enc" and dtype != "bf16" else
               KIND_SYMBOL.get(dominant, dominant).replace("DF16b", "DF16_" if attn_dtype == "fp16" else "DF16b"))
     roofline = {"kernel": dominant, "kernel_symbol": symbol,
                 "bound": "mfma" if mfma_bound else "hbm", "achieved": achieved,
                 "peak": peak, "unit": unit, "frac": achieved / peak,
-                "traffic": traffic_for(dominant, launch_grid(dominant, B, cfg), attn_dtype) if dtype == "bf16" else None,
+                "traffic": traffic_for(dominant, launch_grid(dominant, B, cfg), attn_dtype),
                 "launches": k_n, "avg_launch_ms": avg_ms,
                 # the timed-region launches share the CUs with the next batch's backbone (stream
                 # overlap); the per-launch profiled step times each launch between events on its

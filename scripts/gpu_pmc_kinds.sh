@@ -9,7 +9,7 @@ mkdir -p $D
 for C in FETCH_SIZE WRITE_SIZE; do
   timeout -s KILL 300 rocprofv3 --kernel-trace --pmc $C --kernel-exclude-regex "Cijk|at::|rocprim|hipcub|rocclr" \
     --output-format csv -d $D/$C -o run -- \
-    python3 bench.py --steps 1 --warmup 1 --no-overlap --no-cpu-baseline --no-accuracy --no-parity ${BENCH_ARGS:-} \
+    python3 bench.py --steps 1 --warmup 1 --no-overlap --no-cpu-baseline --no-accuracy --no-parity --no-host-input ${BENCH_ARGS:-} \
     --launch-table $D/lt.json > $D/$C.log 2>&1 || { echo "pmc pass $C failed"; tail -5 $D/$C.log; exit 6; }
   find $D/$C -name "*kernel_trace*" -delete
 done

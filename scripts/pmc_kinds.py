@@ -20,7 +20,7 @@ import os
 from collections import defaultdict
 
 SKIP = ("pnp_", "score_kernel", "self_assess", "at::", "void at", "rocprim", "hipcub", "__amd_rocclr", "Cijk")
-FAMILY = {"attn.enc": ("attn16", "attn_x3", "attn_h3", "attn_f32"), "attn.dec_self": ("attn16", "attn_f32"),
+FAMILY = {"attn.enc": ("attn16", "attn_x3", "attn_split", "attn_f32"), "attn.dec_self": ("attn16", "attn_f32"),
           "attn.dec_cross": ("xattn", "attn_f32"),
           "ffn.enc": ("ffn_",), "ffn.dec": ("ffn_",)}
 
