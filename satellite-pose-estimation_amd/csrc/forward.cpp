@@ -225,7 +225,7 @@ static int forward_stages(spe_model* m, void* stream, const ImageSrc& images, in
     return fail(SPE_E_STATE, "fp32h3: backbone activation-scale slots exhausted");
   if (amx && (stages & SPE_STAGE_TRANSFORMER) && 2 * (int)m->enc.size() > SPE_AMAX_DEC - SPE_AMAX_BB - 1)
     return fail(SPE_E_STATE, "fp32h3: encoder activation-scale slots exhausted");
-  if (amx && (stages & SPE_STAGE_DECODE) && 2 * c.dec_layers > SPE_AMAX_SLOTS - SPE_AMAX_DEC)
+  if (amx && (stages & SPE_STAGE_DECODE) && 3 * c.dec_layers > SPE_AMAX_SLOTS - SPE_AMAX_DEC)
     return fail(SPE_E_STATE, "fp32h3: decoder activation-scale slots exhausted");
   if (stages & SPE_STAGE_BACKBONE) {
   int na = 0;
@@ -520,6 +520,13 @@ static int forward_stages(spe_model* m, void* stream, const ImageSrc& images, in
   if (tam && 2 * li > SPE_AMAX_DEC - SPE_AMAX_BB - 1) return fail(SPE_E_STATE, "fp32h3: encoder activation-scale slots exhausted");
   // memory = src.  Unless the layers attend to memory + pos / memory directly (xattn path),
   // project the cross-attention K (memory + pos) and V^T (memory) for all decoder layers.
+  if (xa && m->h3) {
+    // fp32h3: the memory once as fp16 planes for all decoder layers (xattn_h3.hip): key planes of
+    // memory + pos into srcpos, value planes into xvp
+    CK(run_other(m, "eltwise.xsplit", 0.0, (double)Mt * d * (4 + 8 + 8) + (double)T * d * 4, s, [&] {
+      return spe_launch_xattn_h3_split((const float*)P(w.src), (const float*)m->pos, src_amax, P(w.srcpos), P(w.xvp), B, T, s);
+    }));
+  }
   if (!xa) {
   {
     // bf16 fused path: the last FFN wrote memory + pos (rounded once, like the reference's
@@ -552,7 +559,10 @@ static int forward_stages(spe_model* m, void* stream, const ImageSrc& images, in
   // crossV GEMM's, transformer stage), the FFN hidden's from the linear1 GEMM
   float* const dam = amx ? amx + SPE_AMAX_DEC : nullptr;
   if (dam) CK((int)hipMemsetAsync(dam, 0, (SPE_AMAX_SLOTS - SPE_AMAX_DEC) * 4, s));
-  if (dam && 2 * L > SPE_AMAX_SLOTS - SPE_AMAX_DEC) return fail(SPE_E_STATE, "fp32h3: decoder activation-scale slots exhausted");
+  if (dam && 3 * L > SPE_AMAX_SLOTS - SPE_AMAX_DEC) return fail(SPE_E_STATE, "fp32h3: decoder activation-scale slots exhausted");
+  // fp32h3 cross-attention against the memory: the memory's bound (the last encoder norm2's) scales
+  // its planes; layer l's output raises slot dam + 2L + l
+  const float* const mem_bound = m->h3 && xa && !m->enc.empty() ? m->enc.back().n2_bound : nullptr;
   const float* tgt_amax = m->h3 && L > 0 ? m->dec[0].n1_bound : nullptr;
   const float* const cross_v_amax = amx ? amx + SPE_AMAX_DEC - 1 : nullptr;
   // tgt = LayerNorm(tgt + dao . W^T + b) (REV/models/transformer.py:227-228, 233-234) as GEMM +
@@ -622,6 +632,7 @@ static int forward_stages(spe_model* m, void* stream, const ImageSrc& images, in
     }
     if (m->h3) tgt_amax = e.n1_bound;
     bool xtail = false;                         // the merge + value + out-projection + norm2 ran in one launch
+    const float* cross_o_amax = cross_v_amax;   // fp32h3: the out-projection's scale input
     if (xa) {
       // q' = (tgt + query_pos) . Wqk^T + bqk: the query-side fold of Wq and Wk (xattn.hip)
       if (e.fxq && decffn_on) {
@@ -635,32 +646,51 @@ static int forward_stages(spe_model* m, void* stream, const ImageSrc& images, in
       } else {
         GemmArgs g = linear_args(e.xq, P(w.tgt), d, Mq, P(w.xq), 8 * d);
         g.R = e.xq_r; g.ldr = 8 * d; g.r_period = Q;
+        g.amax_a = tgt_amax;                    // fp32h3: the h3 GEMM's scale input
         CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR, s));
       }
-      XattnArgs x{};
-      x.q = P(w.xq); x.ldq = 8 * d;
-      x.k = P(w.srcpos); x.ldk = d;
-      x.v = P(w.src); x.ldv = d;
-      x.wv = e.xv.w; x.bv = e.xv.bias;
-      x.o = P(w.dao); x.ldo = d;
-      x.B = B; x.Q = Q; x.T = T; x.splits = spe_xattn_splits(B, Q, T);
-      x.pm = (float*)P(w.xpm); x.pl = (float*)P(w.xpl); x.pu = (float*)P(w.xpu);
-      // Q <= 48: the split merge and the value projection move into the out-projection + norm2
-      // launch (decsa.hip decxproj_kernel), the per-split partials its only input
-      xtail = decproj_on && e.fxv && Q <= 48;
-      x.partials_only = xtail;
-      const double fl = 4.0 * B * 8.0 * Q * (double)T * d + (xtail ? 0.0 : 2.0 * Mq * 8.0 * d * 32);
-      const double by = 2.0 * B * (double)T * d * m->esz + 2.0 * Mq * 8.0 * d * m->esz;
-      CK(run_other(m, "attn.dec_cross", fl, by, s, [&] { return spe_launch_xattn(x, s); }));
-      if (xtail) {
-        DecProjArgs pa{};
-        pa.tgt = P(w.tgt); pa.ldt = d; pa.B = B; pa.Q = Q;
-        pa.wo = e.fco; pa.bo = e.co.bias; pa.g = e.n2g; pa.b = e.n2b;
-        pa.pm = x.pm; pa.pl = x.pl; pa.pu = x.pu; pa.splits = spe_xattn_launch_splits(T, x.splits);
-        pa.wv = e.fxv; pa.bv = e.xv.bias;
-        const double pfl = 2.0 * Mq * 8.0 * d * 32 + 2.0 * Mq * d * d;
-        const double pby = (double)pa.splits * B * 8.0 * Q * (d + 2) * 4 + 2.0 * Mq * d * m->esz + 2.0 * d * d * m->esz;
-        CK(run_other(m, "dec.xproj", pfl, pby, s, [&] { return spe_launch_decproj(pa, s); }));
+      if (m->h3) {
+        // fp32h3: scores and value sums against the memory's fp16 planes, three products each; the
+        // merge applies Wv / bv in fp32 and raises max |o| for the out-projection
+        XattnArgs x{};
+        x.q = P(w.xq); x.ldq = 8 * d;
+        x.k = P(w.srcpos); x.ldk = 2 * d;
+        x.v = P(w.xvp); x.ldv = 2 * d;
+        x.wv = e.xv.w; x.bv = e.xv.bias;
+        x.o = P(w.dao); x.ldo = d;
+        x.B = B; x.Q = Q; x.T = T; x.splits = spe_xattn_splits(B, Q, T);
+        x.pm = (float*)P(w.xpm); x.pl = (float*)P(w.xpl); x.pu = (float*)P(w.xpu);
+        x.mem_amax = mem_bound; x.o_amax = dam ? dam + 2 * L + l : nullptr;
+        const double fl = 4.0 * B * 8.0 * Q * (double)T * d + 2.0 * Mq * 8.0 * d * 32;
+        const double by = 2.0 * B * (double)T * 2 * d * 2 + 2.0 * Mq * 8.0 * d * 4;
+        CK(run_other(m, "attn.dec_cross", fl, by, s, [&] { return spe_launch_xattn_h3(x, s); }));
+        cross_o_amax = x.o_amax;
+      } else {
+        XattnArgs x{};
+        x.q = P(w.xq); x.ldq = 8 * d;
+        x.k = P(w.srcpos); x.ldk = d;
+        x.v = P(w.src); x.ldv = d;
+        x.wv = e.xv.w; x.bv = e.xv.bias;
+        x.o = P(w.dao); x.ldo = d;
+        x.B = B; x.Q = Q; x.T = T; x.splits = spe_xattn_splits(B, Q, T);
+        x.pm = (float*)P(w.xpm); x.pl = (float*)P(w.xpl); x.pu = (float*)P(w.xpu);
+        // Q <= 48: the split merge and the value projection move into the out-projection + norm2
+        // launch (decsa.hip decxproj_kernel), the per-split partials its only input
+        xtail = decproj_on && e.fxv && Q <= 48;
+        x.partials_only = xtail;
+        const double fl = 4.0 * B * 8.0 * Q * (double)T * d + (xtail ? 0.0 : 2.0 * Mq * 8.0 * d * 32);
+        const double by = 2.0 * B * (double)T * d * m->esz + 2.0 * Mq * 8.0 * d * m->esz;
+        CK(run_other(m, "attn.dec_cross", fl, by, s, [&] { return spe_launch_xattn(x, s); }));
+        if (xtail) {
+          DecProjArgs pa{};
+          pa.tgt = P(w.tgt); pa.ldt = d; pa.B = B; pa.Q = Q;
+          pa.wo = e.fco; pa.bo = e.co.bias; pa.g = e.n2g; pa.b = e.n2b;
+          pa.pm = x.pm; pa.pl = x.pl; pa.pu = x.pu; pa.splits = spe_xattn_launch_splits(T, x.splits);
+          pa.wv = e.fxv; pa.bv = e.xv.bias;
+          const double pfl = 2.0 * Mq * 8.0 * d * 32 + 2.0 * Mq * d * d;
+          const double pby = (double)pa.splits * B * 8.0 * Q * (d + 2) * 4 + 2.0 * Mq * d * m->esz + 2.0 * d * d * m->esz;
+          CK(run_other(m, "dec.xproj", pfl, pby, s, [&] { return spe_launch_decproj(pa, s); }));
+        }
       }
     } else {
     {
@@ -679,7 +709,7 @@ static int forward_stages(spe_model* m, void* stream, const ImageSrc& images, in
       CK(run_attn(m, "attn.dec_cross", a, dt, s));
     }
     }
-    if (!xtail) CK(dec_proj_ln(e.co, e.fco, e.n2g, e.n2b, cross_v_amax));
+    if (!xtail) CK(dec_proj_ln(e.co, e.fco, e.n2g, e.n2b, cross_o_amax));
     if (m->h3) tgt_amax = e.n2_bound;
     if (e.fl1 && decffn_on) {
       // bf16: one workgroup per (16 rows, 256 hidden units), all of its weight fragments in flight

@@ -60,7 +60,7 @@ struct Dec {
 // fp32h3 activation-scale slots in the workspace: [0, SPE_AMAX_BB) written by the backbone stage,
 // [SPE_AMAX_BB, SPE_AMAX_SLOTS) by the transformer stage (each stage zeroes its own range first)
 // (the transformer stage's range is [SPE_AMAX_BB, SPE_AMAX_DEC), the decoder stage's [SPE_AMAX_DEC, SPE_AMAX_SLOTS))
-constexpr int SPE_AMAX_BB = 96, SPE_AMAX_DEC = 112, SPE_AMAX_SLOTS = 128;
+constexpr int SPE_AMAX_BB = 96, SPE_AMAX_DEC = 112, SPE_AMAX_SLOTS = 136;   // decoder: 3 slots a layer
 
 struct Ws {                // workspace layout (byte offsets)
   size_t x0, stem, pool, bufA, bufB, t1, t2, ds, xs8, up, cat, neck;
@@ -68,6 +68,7 @@ struct Ws {                // workspace layout (byte offsets)
   size_t kpl;                // fp32x3 / fp32x6: the encoder K as bf16 hi / lo planes (0 = none)
   size_t tgt, dtmp, dqkv, dvt, dao, dqc, dffn, dffnpart, hs;
   size_t xq, xu, xpm, xpl, xpu;           // cross-attention against the memory (xattn.hip)
+  size_t xvp;                // fp32h3: the memory's fp16 value planes (xattn_h3.hip; the key planes go to srcpos)
   size_t amax;               // fp32h3: max |activation| slots (SPE_AMAX_SLOTS floats; backbone, then transformer)
   size_t total;
 };
@@ -169,11 +170,18 @@ int spe_rtdetr_build_device(spe_model* m);
 int64_t spe_rtdetr_workspace(const spe_model* m, int B);
 
 // bf16 models take the decoder cross-attention against the memory itself (xattn.hip) when the
-// last encoder layer can emit memory + pos (fused FFN)
+// last encoder layer can emit memory + pos (fused FFN); fp32h3 models too, on the memory's fp16
+// planes (xattn_h3.hip), when the 8 * Q attention rows fit one 96-row work-group group (Q <= 12:
+// BASELINE configs 2-4 and the north star).  At config 5 (Q = 40: four groups, each re-reading the
+// memory) the fold measured no gain (48.75 vs 48.96 ms a step) and moved one of the precision study's
+// 32 images to a RANSAC outcome none of three fp32 implementations reach, so
+// Q > 12 keeps the projected K / V^T and the exact-f32 attention.  SPE_XATTN_H3=0: that path for
+// every Q (A/B runs).
 inline bool spe_use_xattn(const spe_model* m) {
+  static const bool h3 = [] { const char* e = getenv("SPE_XATTN_H3"); return e ? atoi(e) != 0 : true; }();
   const auto& c = m->cfg;
-  return c.dtype == SPE_DTYPE_BF16_ && c.hidden_dim == 256 && c.nheads == 8 && c.dim_feedforward % 32 == 0 &&
-         c.enc_layers > 0;
+  return (c.dtype == SPE_DTYPE_BF16_ || (h3 && m->h3 && 8 * c.num_queries <= 96)) && c.hidden_dim == 256 &&
+         c.nheads == 8 && c.dim_feedforward % 32 == 0 && c.enc_layers > 0;
 }
 // bf16 and fp32x3 models evaluate s16_latern(up16sto8s(xs16)) at the low resolution (one
 // per-tap GEMM + upconv_combine: exact by linearity, a different rounding order); the exact-f32

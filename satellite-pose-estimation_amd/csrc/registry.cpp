@@ -725,6 +725,7 @@ Ws spe_plan(const spe_model* m, int B) {
   w.xpm = take(xa ? XS * B * R * 4 : 0);
   w.xpl = take(xa ? XS * B * R * 4 : 0);
   w.xpu = take(xa ? XS * B * R * d * 4 : 0);
+  w.xvp = take(xa && m->h3 ? (size_t)B * T * d * 4 : 0);   // [B*T][512] fp16 (srcpos holds the key planes)
   w.tgt = take((size_t)B * Q * d * E);
   w.dtmp = take((size_t)B * Q * d * E);
   w.dqkv = take((size_t)B * Q * 3 * d * E);

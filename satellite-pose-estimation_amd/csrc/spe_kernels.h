@@ -134,10 +134,19 @@ struct XattnArgs {
   int B, Q, T, splits, tiles_per_split;
   float *pm, *pl, *pu;             // key-split partials [B][splits][8Q] (pu: x 256), required
   bool partials_only;              // stop at the partials (decproj's merge form consumes them)
+  // fp32h3 (xattn_h3.hip): q' fp32; k / v the fp16 planes [B*T][512] (hi | lo) written by
+  // spe_launch_xattn_h3_split from a memory bounded by *mem_amax; wv / bv / o fp32; max |o| raised into
+  // *o_amax (the out-projection GEMM's scale input)
+  const float* mem_amax; float* o_amax;
 };
 int spe_xattn_splits(int B, int Q, int T);
 int spe_xattn_launch_splits(int T, int splits);   // the split count a launch with `splits` runs (partials' layout)
 int spe_launch_xattn(const XattnArgs& a, hipStream_t s);
+// fp32h3: kp = fp16 hi | lo of (mem + pos) * 2^sk, vp = of mem * 2^sv (powers of two from *mem_amax,
+// vplane_scale), rows b*T + t of 512 halves; mem [B*T][256] fp32, pos [T][256] fp32
+int spe_launch_xattn_h3_split(const float* mem, const float* pos, const float* mem_amax, void* kp, void* vp, int B,
+                              int T, hipStream_t s);
+int spe_launch_xattn_h3(const XattnArgs& a, hipStream_t s);
 
 // Decoder self-attention block (bf16 only, decsa.hip), one workgroup per image, in place over tgt:
 // tgt = LN(tgt + SelfAttn(q = k = tgt + qpos, v = tgt) . Wo^T + bo), 8 heads of 32, d = 256.

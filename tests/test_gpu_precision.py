@@ -370,6 +370,9 @@ def test_fp32h3_within_fp32_spread_config(gpu_device, config):
     # is held to the spread on exactly those images (bench.score_spread)
     per = {f"{a}_vs_{b}": [float(v) for v in np.abs(sc[a] - sc[b])]
            for a, b in (("torch_cpu", "fp32"), ("torch_gpu", "fp32"), ("torch_cpu", "torch_gpu"))}
+    # (fp32h3's own per-image deltas, for the record; bench.score_spread reads the fp32 pairs only)
+    r["fp32h3_per_image"] = {f"fp32h3_vs_{b}": [float(v) for v in np.abs(sc["fp32h3"] - sc[b])]
+                             for b in ("fp32", "torch_cpu", "torch_gpu")}
     r["score"] = {cc["solver"]: {"pairs": tab, "per_image": per}}
     if rel:
         r["reliable"] = {f"{a}_vs_fp32": float((rel[a] == rel["fp32"]).mean()) for a in rel if a != "fp32"}
