@@ -18,7 +18,7 @@
 extern "C" {
 #endif
 
-#define SPE_ABI_VERSION 8
+#define SPE_ABI_VERSION 9
 
 enum {
   SPE_E_ARG = -1,        /* bad argument / size */
@@ -350,6 +350,15 @@ int spe_debug_ffn(void* stream, const void* x, int ldx, const void* w1, int ld1,
 int spe_debug_xattn(void* stream, const void* q, int ldq, const void* k, int ldk, const void* v, int ldv, void* u,
                     int ldu, const void* wv, const float* bv, void* o, int ldo, int B, int Q, int T, int splits,
                     float* partial_scratch);
+/* xattn_h3 (fp32h3, xattn_h3.hip, ABI 9 addition): the same cross-attention at fp32-level products --
+ * q' fp32 [B*Q][ldq] (exp2 domain), mem fp32 [B*T][256], pos fp32 [T][256], keys mem + pos, values mem,
+ * *mem_amax (device) >= max |mem|: mem is first written as fp16 hi / lo planes into plane_scratch
+ * (B*T*2048 bytes), then o[b*Q+q][h*32 + j] = wv[h*32 + j] . u_h + bv[h*32 + j] (wv [256][256] fp32) is
+ * written in fp32 and max |o| raised into *o_amax (nullable; an unsigned-max slot, zero it first).
+ * splits <= 0: the launch's own key split; partial_scratch as spe_debug_xattn's. */
+int spe_debug_xattn_h3(void* stream, const float* q, int ldq, const float* mem, const float* pos, const float* mem_amax,
+                       const float* wv, const float* bv, float* o, int ldo, float* o_amax, int B, int Q, int T,
+                       int splits, float* partial_scratch, void* plane_scratch);
 /* upconv (bf16 models' neck, replaces the upsample + conv pair of REV/models/backbone.py:141
  * s16_latern(up16sto8s(xs16))): z [B*H*W][9*C] holds the per-tap products W_t . x at the low
  * resolution (t = kh*3 + kw); out [B][2H][2W] rows of stride ldo receive conv3x3(pad 1) of the

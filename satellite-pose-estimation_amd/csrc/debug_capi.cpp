@@ -138,6 +138,28 @@ int spe_debug_xattn(void* stream, const void* q, int ldq, const void* k, int ldk
   return rc < 0 ? spe_fail(SPE_E_LAUNCH, "xattn launch rejected its arguments") : rc;
 }
 
+int spe_debug_xattn_h3(void* stream, const float* q, int ldq, const float* mem, const float* pos, const float* mem_amax,
+                       const float* wv, const float* bv, float* o, int ldo, float* o_amax, int B, int Q, int T,
+                       int splits, float* partial_scratch, void* plane_scratch) {
+  if (!q || !mem || !pos || !mem_amax || !wv || !bv || !o || !partial_scratch || !plane_scratch || B < 0 || Q < 1 ||
+      T < 1)
+    return spe_fail(SPE_E_ARG, "bad argument");
+  hipStream_t s = (hipStream_t)stream;
+  char* kp = (char*)plane_scratch;
+  char* vp = kp + (size_t)B * T * 1024;
+  if (spe_launch_xattn_h3_split(mem, pos, mem_amax, kp, vp, B, T, s) != 0)
+    return spe_fail(SPE_E_LAUNCH, "xattn_h3 split launch failed");
+  XattnArgs a{};
+  a.q = q; a.ldq = ldq; a.k = kp; a.ldk = 512; a.v = vp; a.ldv = 512;
+  a.wv = wv; a.bv = bv; a.o = o; a.ldo = ldo;
+  a.B = B; a.Q = Q; a.T = T; a.splits = splits > 0 ? splits : spe_xattn_splits(B, Q, T);
+  const size_t rows = (size_t)a.splits * B * 8 * Q;
+  a.pm = partial_scratch; a.pl = partial_scratch + rows; a.pu = partial_scratch + 2 * rows;
+  a.mem_amax = mem_amax; a.o_amax = o_amax;
+  const int rc = spe_launch_xattn_h3(a, s);
+  return rc != 0 ? spe_fail(SPE_E_LAUNCH, "xattn_h3 launch rejected its arguments") : 0;
+}
+
 int spe_debug_btail(void* stream, const void* a, int lda, int k1, const void* r, const void* w3, int ld3,
                     const float* b3, void* y, const void* w1p, int ld1, const float* b1, void* z, int n2, int M) {
   if (!a || !w3 || !b3 || !y || !w1p || !b1 || !z || M < 0) return spe_fail(SPE_E_ARG, "bad argument");

@@ -28,7 +28,7 @@ LIB_PATH = os.environ.get("SPE_LIB_PATH") or os.path.join(_HERE, "libspe.so")   
 # the include/spe.h version this binding is written against: any other library is refused, including
 # one named by SPE_LIB_PATH (an A/B build of an older tree would otherwise be called with this
 # binding's argument lists)
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -46,7 +46,7 @@ EXPORTS = ["spe_abi_version", "spe_last_error", "spe_model_create", "spe_model_d
            "spe_model_num_params", "spe_model_param_name", "spe_model_finalize", "spe_model_workspace_bytes",
            "spe_forward", "spe_forward_stages", "spe_forward_stages_u8", "spe_preprocess", "spe_criterion", "spe_ensemble_fuse", "spe_postprocess", "spe_pnp_batch", "spe_self_assess", "spe_speed_score", "spe_model_profile_begin",
            "spe_model_profile_end", "spe_model_profile_get", "spe_debug_gemm", "spe_debug_gemm_path", "spe_debug_gemm_h3", "spe_debug_ffn_h3", "spe_debug_ffn_h3_perm", "spe_debug_gemm_planes", "spe_debug_attention",
-           "spe_debug_layernorm", "spe_debug_ffn", "spe_debug_xattn", "spe_debug_upconv", "spe_debug_btail", "spe_debug_decsa", "spe_debug_decproj", "spe_debug_decxproj", "spe_debug_wfrag_pack", "spe_debug_decffn", "spe_debug_decq", "spe_debug_btail_perm", "spe_debug_stempool", "spe_rtdetr_create", "spe_rtdetr_forward",
+           "spe_debug_layernorm", "spe_debug_ffn", "spe_debug_xattn", "spe_debug_xattn_h3", "spe_debug_upconv", "spe_debug_btail", "spe_debug_decsa", "spe_debug_decproj", "spe_debug_decxproj", "spe_debug_wfrag_pack", "spe_debug_decffn", "spe_debug_decq", "spe_debug_btail_perm", "spe_debug_stempool", "spe_rtdetr_create", "spe_rtdetr_forward",
            "spe_jpeg_workspace_bytes", "spe_jpeg_decode"]
 
 
@@ -125,6 +125,7 @@ def load(path: str):
     L.spe_debug_layernorm.argtypes = [P, I, P, P, P, P, P, I, I]
     L.spe_debug_ffn.argtypes = [P, P, I, P, I, P, P, I, P, P, P, P, I, I, I, I, P, I]
     L.spe_debug_xattn.argtypes = [P, P, I, P, I, P, I, P, I, P, P, P, I, I, I, I, I, P]
+    L.spe_debug_xattn_h3.argtypes = [P, P, I, P, P, P, P, P, P, I, P, I, I, I, I, P, P]
     L.spe_debug_upconv.argtypes = [P, I, P, P, I, I, I, I, I]
     L.spe_debug_btail.argtypes = [P, P, I, I, P, P, I, P, P, P, I, P, P, I, I]
     L.spe_debug_btail_perm.argtypes = [I]

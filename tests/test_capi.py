@@ -25,10 +25,10 @@ def test_exports_every_declared_symbol():
     assert set(declared) == set(_lib.EXPORTS)
     for name in declared:
         assert hasattr(L, name), name
-    assert L.spe_abi_version() == _lib.ABI_VERSION == 8
+    assert L.spe_abi_version() == _lib.ABI_VERSION == 9
 
 
-@pytest.mark.parametrize("version", [7, 9])
+@pytest.mark.parametrize("version", [8, 10])
 def test_other_abi_version_is_refused(tmp_path, version):
     """A library of another ABI (e.g. an A/B build of the v7 tree, whose spe_debug_gemm_h3 took two more
     arguments) is refused at load, SPE_LIB_PATH included, before any call is bound."""

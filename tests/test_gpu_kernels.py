@@ -669,6 +669,56 @@ def test_cross_attention_memory(gpu_device, B, Q, T, splits, amp):
     assert (o[:, D:] == 7.0).all()
 
 
+@pytest.mark.parametrize("B,Q,T,splits,amp", [(3, 11, 200, 1, 1.0), (2, 12, 203, 3, 1.0), (1, 17, 136, 2, 1.0),
+                                              (2, 11, 2704, 0, 1.0), (2, 5, 640, 4, 12.0), (64, 11, 2704, 0, 4.0)])
+def test_cross_attention_memory_h3(gpu_device, B, Q, T, splits, amp):
+    """fp32h3 decoder cross-attention against the memory (xattn_h3.hip): the memory split into fp16 hi / lo
+    planes of (mem + pos) * 2^sk and mem * 2^sv, three fp16 products per score and value term, the
+    key-split merge and o_h = Wv_h u_h + bv_h in fp32 (REV/models/transformer.py:230-233 folded), against
+    fp64 on the same fp32 operands.  Q = 12 fills the 96-row group; Q = 17 takes two groups; T = 203 ends
+    in a partial 32-key tile; amp spreads the scores over ~30 log2 units (one key 4x above the rest) so
+    the lazy rescale and far-apart split partials are exercised.  The memory's bound is a loose LayerNorm-
+    style bound (4x max |mem|: the model's ln_bound), pos in [-1, 1].  Tolerance 2e-5 * scale: the
+    products' 2^-22 splits and fp32 accumulation, against the bf16 kernel's 1e-2."""
+    D = 256
+    g = torch.Generator(device="cpu").manual_seed(7 * B * T + Q)
+    ldq, ldo = 8 * D + 4, D + 4
+    q = torch.randn(B * Q, ldq, generator=g, dtype=torch.float64) * amp / 16
+    mem = torch.randn(B * T, D, generator=g, dtype=torch.float64)
+    pos = torch.rand(T, D, generator=g, dtype=torch.float64) * 2 - 1
+    if amp > 1:
+        mem[5] *= 4
+    wv = torch.randn(D, D, generator=g, dtype=torch.float64) / 16
+    bv = torch.randn(D, generator=g, dtype=torch.float64)
+    q32, mem32, pos32 = q.float(), mem.float(), pos.float()
+    wv32, bv32 = wv.float(), bv.float()
+    amax = torch.tensor([4.0 * float(mem32.abs().max())], device=gpu_device)
+    dq, dm, dp = q32.to(gpu_device), mem32.to(gpu_device), pos32.to(gpu_device)
+    dwv, dbv = wv32.to(gpu_device), bv32.to(gpu_device)
+    o = torch.full((B * Q, ldo), 7.0, device=gpu_device)
+    oam = torch.zeros(1, device=gpu_device)
+    S = splits if splits > 0 else 256
+    part = torch.empty(S * B * 8 * Q * 258, device=gpu_device)
+    planes = torch.empty(B * T * 2048, dtype=torch.uint8, device=gpu_device)
+    L = _lib.lib()
+    rc = L.spe_debug_xattn_h3(None, _p(dq), ldq, _p(dm), _p(dp), _p(amax), _p(dwv), _p(dbv), _p(o), ldo, _p(oam),
+                              B, Q, T, splits, _p(part), _p(planes))
+    assert rc == 0, L.spe_last_error()
+    torch.cuda.synchronize()
+    # fp64 reference on the fp32 operands (keys = the fp32 sum mem + pos, as the reference forms them)
+    k = (mem32 + pos32.repeat(B, 1)).double().view(B, T, D)
+    s = torch.einsum("brd,btd->brt", q32[:, :8 * D].double().view(B, Q * 8, D), k)
+    p = torch.softmax(s * math.log(2.0), dim=-1)
+    u = torch.einsum("brt,btd->brd", p, mem32.double().view(B, T, D))
+    ref = torch.einsum("bqhn,hjn->bqhj", u.view(B, Q, 8, D), wv32.double().view(8, 32, D)) + bv32.double().view(8, 32)
+    ref = ref.reshape(B * Q, D)
+    got = o[:, :D].double().cpu()
+    err = float((got - ref).abs().max() / ref.abs().max())
+    assert err <= 2e-5, err
+    assert (o[:, D:] == 7.0).all()                      # nothing written past D
+    assert abs(float(oam) - float(o[:, :D].abs().max())) == 0.0   # the published max |o|
+
+
 @pytest.mark.parametrize("B,Q,T,splits,amp", [(3, 11, 200, 1, 1.0), (2, 11, 203, 3, 1.0), (1, 16, 136, 2, 1.0),
                                               (64, 11, 2704, 0, 1.0), (2, 5, 640, 4, 12.0), (1, 1, 2704, 0, 1.0),
                                               (16, 40, 6400, 0, 1.0), (2, 33, 300, 5, 12.0), (1, 48, 64, 1, 1.0),
