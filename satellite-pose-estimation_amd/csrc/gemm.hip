@@ -1621,6 +1621,13 @@ H3P_KERNELS(, 4, 2, 2)
 __global__ __launch_bounds__(256, 2) void gemm_h3p_linear_s(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 4, false, false, 4, 2, 1>(g); }
 __global__ __launch_bounds__(256, 2) void gemm_h3p_linear_s_r(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 4, false, true, 4, 2, 1>(g); }
 __global__ __launch_bounds__(256, 2) void gemm_h3p_linear_vt(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 4, false, false, 4, 2, 2>(g); }
+// few-row problems (the decoder's B*Q rows): 64-column tiles -- twice the work-groups on a grid that
+// leaves most CUs idle -- with a third stage (74 KB of LDS); measured 1.19 -> 1.02 ms for the fp32h3
+// decoder's 42 GEMMs, and slower on the full-size launches (q/k 1.60 -> 1.80 ms: DESIGN.md section 0)
+__global__ __launch_bounds__(256, 2) void gemm_h3p_linear_fr(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 2, false, false, 4, 3>(g); }
+__global__ __launch_bounds__(256, 2) void gemm_h3p_linear_r_fr(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 2, false, true, 4, 3>(g); }
+__global__ __launch_bounds__(256, 2) void gemm_h3p_linear_vt_fr(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 2, false, false, 4, 3, 2>(g); }
+constexpr int H3_FEW_ROWS = 4096;
 
 // 1 = not a problem for the h3 kernel (the caller runs the x6 path)
 int launch_h3d(const GemmArgs& g, int mode, hipStream_t s) {
@@ -1659,7 +1666,12 @@ int launch_h3d(const GemmArgs& g, int mode, hipStream_t s) {
         (!g.vt_swz || (g.S && g.vt_T % 16 == 0)) && (!g.s_f16 || g.S) &&
         g.vt_T % 4 == 0 && g.M == g.vt_B * g.vt_T && !(g.N & 255) && (!g.S || g.s_col0 == 0) &&
         (long long)g.vt_B * g.N * g.vt_T * 4 < LIM && !(reinterpret_cast<uintptr_t>(g.C) & 15)) {
-      hipLaunchKernelGGL(gemm_h3p_linear_vt, pg, pb, 0, s, g);
+      if (g.M <= H3_FEW_ROWS) {
+        const int t2 = ((g.M + H3_BM - 1) / H3_BM) * ((g.N + 63) / 64);
+        hipLaunchKernelGGL(gemm_h3p_linear_vt_fr, dim3(t2 < 2 * ncu || ncu <= 0 ? t2 : 2 * ncu), pb, 0, s, g);
+      } else {
+        hipLaunchKernelGGL(gemm_h3p_linear_vt, pg, pb, 0, s, g);
+      }
       spe_gemm_last_path = 8;
       return (int)hipGetLastError();
     }
@@ -1675,7 +1687,12 @@ int launch_h3d(const GemmArgs& g, int mode, hipStream_t s) {
     const dim3 pg(tiles < 2 * ncu || ncu <= 0 ? tiles : 2 * ncu), pb(256);
 #define H3P_GO(K) hipLaunchKernelGGL(K, pg, pb, 0, s, g)
 #define H3P_SEL(NAME) H3P_GO(NAME)
-    if (mode == GEMM_CONV && pl) {
+    if (mode == GEMM_LINEAR && !narrow && g.M <= H3_FEW_ROWS) {
+      const int t2 = ((g.M + H3_BM - 1) / H3_BM) * ((g.N + 63) / 64);
+      const dim3 pg2(t2 < 2 * ncu || ncu <= 0 ? t2 : 2 * ncu);
+      if (res) hipLaunchKernelGGL(gemm_h3p_linear_r_fr, pg2, pb, 0, s, g);
+      else hipLaunchKernelGGL(gemm_h3p_linear_fr, pg2, pb, 0, s, g);
+    } else if (mode == GEMM_CONV && pl) {
       if (narrow) H3P_SEL(gemm_h3p_conv_pl_n64);
       else H3P_SEL(gemm_h3p_conv_pl);
     } else if (mode == GEMM_CONV) {
