@@ -41,8 +41,12 @@ PARITY_MODE_TEXT = {"fp32x6": "fp32 storage; GEMMs / convolutions at near-fp32 p
                               "exact fp32 (DESIGN.md section 4)"}
 
 
-def peak_for(dtype, kind):
-    """MFMA ceiling (TFLOP/s of model flops) of launch class `kind` in mode `dtype`."""
+def peak_for(dtype, kind, queries=None):
+    """MFMA ceiling (TFLOP/s of model flops) of launch class `kind` in mode `dtype` (`queries`: the
+    model's Q -- fp32h3's decoder cross-attention runs on the three-fp16-product kernel for Q <= 12,
+    xattn_h3.hip, and on the exact-f32 one otherwise)."""
+    if dtype == "fp32h3" and kind == "attn.dec_cross" and queries is not None and queries <= 12:
+        return PEAK["fp32h3"]["mfma"]
     if dtype in ("fp32x6", "fp32h3") and kind.startswith("attn.dec"):   # the decoder's attention: exact f32
         return PEAK["fp32"]["mfma"]
     if dtype in ("fp32x6", "fp32h3") and kind.startswith("attn."):     # the encoder's: fp32x3
@@ -699,7 +703,7 @@ def time_mode(pipe, model, args, world, dev, dtype, attn_dtype, cfg, B, launch_t
         t = tot.setdefault(k, [0.0, 0])
         t[0] += ms.value
         t[1] += 1
-        floor_ms = 1e3 * max(fl.value / (peak_for(dtype, k) * 1e12), by.value / (PEAK["hbm"] * 1e9))
+        floor_ms = 1e3 * max(fl.value / (peak_for(dtype, k, cfg.num_queries) * 1e12), by.value / (PEAK["hbm"] * 1e9))
         table.append({"i": i, "kind": k, "ms": ms.value, "flops": fl.value, "bytes": by.value,
                       "floor_ms": floor_ms, "frac": floor_ms / max(ms.value, 1e-9)})
     dominant = max(tot, key=lambda k: tot[k][0])
@@ -733,10 +737,10 @@ def time_mode(pipe, model, args, world, dev, dtype, attn_dtype, cfg, B, launch_t
     avg_ms = k_ms / max(k_n, 1)
     # bound by the class's own arithmetic intensity against the ridge point (2500 TF/s / 8 TB/s
     # = 312 flop/B): the K <= 256 1x1 convs are HBM-bound, attention / FFN / 3x3 convs MFMA-bound
-    mfma_bound = k_fl * PEAK["hbm"] * 1e9 > k_by * peak_for(dtype, dominant) * 1e12
+    mfma_bound = k_fl * PEAK["hbm"] * 1e9 > k_by * peak_for(dtype, dominant, cfg.num_queries) * 1e12
     if mfma_bound:
         achieved = (k_fl / max(k_n, 1)) / (avg_ms * 1e-3) / 1e12
-        peak, unit = peak_for(dtype, dominant), "TFLOP/s"
+        peak, unit = peak_for(dtype, dominant, cfg.num_queries), "TFLOP/s"
     else:
         achieved = (k_by / max(k_n, 1)) / (avg_ms * 1e-3) / 1e9
         peak, unit = PEAK["hbm"], "GB/s"

@@ -523,7 +523,7 @@ static int forward_stages(spe_model* m, void* stream, const ImageSrc& images, in
   if (xa && m->h3) {
     // fp32h3: the memory once as fp16 planes for all decoder layers (xattn_h3.hip): key planes of
     // memory + pos into srcpos, value planes into xvp
-    CK(run_other(m, "eltwise.xsplit", 0.0, (double)Mt * d * (4 + 8 + 8) + (double)T * d * 4, s, [&] {
+    CK(run_other(m, "eltwise.xsplit", 0.0, (double)Mt * d * (4 + 4 + 4) + (double)T * d * 4, s, [&] {
       return spe_launch_xattn_h3_split((const float*)P(w.src), (const float*)m->pos, src_amax, P(w.srcpos), P(w.xvp), B, T, s);
     }));
   }
