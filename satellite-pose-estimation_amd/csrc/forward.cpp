@@ -34,6 +34,52 @@ hipEvent_t next_event(spe_model* m) {
   return p.pool[p.next_event++];
 }
 
+// fp32h3 activation-scale ledger (one per forward call): every slot of a range the call zeroes must be
+// raised by an earlier launch of the same call (GemmArgs::amax_c, the input pack, the cross-attention
+// merge) before a launch reads it as its scale (amax_a and the like) -- a consumer without a producer
+// would otherwise run at scale 1 in silence (h3_scale), losing precision or overflowing fp16.  Slots
+// of ranges this call did not zero (a stage run by an earlier call) are not checked.
+struct AmaxLedger {
+  const float* base = nullptr;
+  unsigned char state[SPE_AMAX_SLOTS] = {};     // 0 unchecked, 1 zeroed and awaiting a producer, 2 raised
+  int index(const float* p) const {
+    const long d = base && p ? (long)(p - base) : -1;
+    return d >= 0 && d < SPE_AMAX_SLOTS ? (int)d : -1;
+  }
+  void zeroed(int first, int n) {
+    for (int i = first; i < first + n; ++i) state[i] = 1;
+  }
+  void raised(const float* p) {
+    const int i = index(p);
+    if (i >= 0) state[i] = 2;
+  }
+  bool ok(const float* p) const {
+    const int i = index(p);
+    return i < 0 || state[i] != 1;
+  }
+};
+thread_local AmaxLedger* g_ledger = nullptr;
+struct LedgerScope {
+  AmaxLedger ledger;
+  explicit LedgerScope(const float* base) {
+    ledger.base = base;
+    g_ledger = base ? &ledger : nullptr;
+  }
+  ~LedgerScope() { g_ledger = nullptr; }
+};
+// a launch reading `in` and raising `out`: SPE_E_STATE if `in` has no producer yet
+int ledger_use(const float* in, const float* out, const char* kind) {
+  if (!g_ledger) return 0;
+  if (!g_ledger->ok(in)) {
+    char b[160];
+    snprintf(b, sizeof b, "fp32h3: %s reads activation-scale slot %d before any launch raised it", kind,
+             g_ledger->index(in));
+    return spe_fail(SPE_E_STATE, b);
+  }
+  g_ledger->raised(out);
+  return 0;
+}
+
 bool prof_match(const spe_model* m, const char* kind) {
   return m->prof.on && std::strncmp(kind, m->prof.filter.c_str(), m->prof.filter.size()) == 0;
 }
@@ -63,6 +109,7 @@ static bool x3_for(const spe_model* m, const char* kind) {
 }
 
 int run_gemm(spe_model* m, const char* kind, const GemmArgs& g, int mode, hipStream_t s) {
+  if (const int rc = ledger_use(g.amax_a, g.amax_c, kind)) return rc;
   const double E = m->esz;
   const double a_elems = mode == GEMM_CONV ? (double)(g.M / (g.Ho * g.Wo)) * g.H * g.W * g.Cin : (double)g.M * g.K;
   const double r_rows = g.R ? (g.r_period > 0 ? (double)g.r_period : (double)g.M) : 0.0;
@@ -88,6 +135,7 @@ int run_attn(spe_model* m, const char* kind, const AttnArgs& a, int dtype, hipSt
   const double flops = 4.0 * a.B * a.H * (double)a.Tq * a.Tk * 32;
   const double bytes = (double)a.B * a.H * 32 * (2.0 * a.Tq + 2.0 * a.Tk) * m->esz;
   const int dt = (x3_for(m, kind) && dtype == SPE_DTYPE_F32) ? (int)SPE_DTYPE_F32X3 : dtype;
+  if (const int rc = ledger_use(a.v_amax, nullptr, kind)) return rc;
   return run_other(m, kind, flops, bytes, s, [&] { return spe_launch_attention(a, dt, s); });
 }
 
@@ -219,6 +267,7 @@ static int forward_stages(spe_model* m, void* stream, const ImageSrc& images, in
   // [SPE_AMAX_BB, SPE_AMAX_SLOTS); each stage zeroes its own range first.
   float* const amx = m->h3 ? (float*)P(w.amax) : nullptr;
   float* const src_amax0 = amx ? amx + SPE_AMAX_BB - 1 : nullptr;
+  LedgerScope ledger_scope(amx);
   // (the slot counts are checked before anything is launched: a slot handed out past its range would
   // be the encoder's input scale or a transformer slot, overwritten before an error could return)
   if (amx && (stages & SPE_STAGE_BACKBONE) && 2 + 3 * (int)m->blocks.size() + 2 > SPE_AMAX_BB - 1)
@@ -231,6 +280,7 @@ static int forward_stages(spe_model* m, void* stream, const ImageSrc& images, in
   int na = 0;
   auto slot = [&]() -> float* { return amx ? amx + na++ : nullptr; };
   if (amx) CK((int)hipMemsetAsync(amx, 0, SPE_AMAX_BB * 4, s));
+  if (amx) ledger_scope.ledger.zeroed(0, SPE_AMAX_BB);
   // ---------------- backbone (REV/models/backbone.py:133-149)
   const bool pairs = m->esz == 2 && m->stem.Cin == 4;  // bf16: pair-packed stem (registry.cpp)
   float* const x0_amax = slot();
@@ -240,6 +290,7 @@ static int forward_stages(spe_model* m, void* stream, const ImageSrc& images, in
   else
     CK(run_other(m, "eltwise.pack", 0.0, (double)B * S * S * (12 + m->stem.Cin * m->esz), s,
                  [&] { return spe_launch_pack_input(images, P(w.x0), B, S, dt, s, x0_amax, m->stem.Cin); }));
+  CK(ledger_use(nullptr, x0_amax, "eltwise.pack"));
   int H = S / 2;
   float* const stem_amax = slot();
   const int Hp = (H + 2 - 3) / 2 + 1;
@@ -408,6 +459,7 @@ static int forward_stages(spe_model* m, void* stream, const ImageSrc& images, in
   if (stages & SPE_STAGE_TRANSFORMER) {
   float* const tam = amx ? amx + SPE_AMAX_BB : nullptr;
   if (tam) CK((int)hipMemsetAsync(tam, 0, (SPE_AMAX_DEC - SPE_AMAX_BB) * 4, s));
+  if (tam) ledger_scope.ledger.zeroed(SPE_AMAX_BB, SPE_AMAX_DEC - SPE_AMAX_BB);
   const float* src_amax = src_amax0;
   int li = 0;
 
@@ -497,6 +549,7 @@ static int forward_stages(spe_model* m, void* stream, const ImageSrc& images, in
       a.gamma = e.n2g; a.beta = e.n2b;
       a.amax_x = src_amax; a.sh = e.ffn_sh;
       const double fl = 4.0 * Mt * (double)d * ff, by = 2.0 * Mt * d * 4.0 + 2.0 * 2.0 * 2.0 * d * ff;
+      CK(ledger_use(a.amax_x, nullptr, "ffn.enc"));
       CK(run_other(m, "ffn.enc", fl, by, s, [&] { return spe_launch_ffn_h3(a, s); }));
     } else {
       {
@@ -523,6 +576,7 @@ static int forward_stages(spe_model* m, void* stream, const ImageSrc& images, in
   if (xa && m->h3) {
     // fp32h3: the memory once as fp16 planes for all decoder layers (xattn_h3.hip): key planes of
     // memory + pos into srcpos, value planes into xvp
+    CK(ledger_use(src_amax, nullptr, "eltwise.xsplit"));
     CK(run_other(m, "eltwise.xsplit", 0.0, (double)Mt * d * (4 + 4 + 4) + (double)T * d * 4, s, [&] {
       return spe_launch_xattn_h3_split((const float*)P(w.src), (const float*)m->pos, src_amax, P(w.srcpos), P(w.xvp), B, T, s);
     }));
@@ -559,6 +613,7 @@ static int forward_stages(spe_model* m, void* stream, const ImageSrc& images, in
   // crossV GEMM's, transformer stage), the FFN hidden's from the linear1 GEMM
   float* const dam = amx ? amx + SPE_AMAX_DEC : nullptr;
   if (dam) CK((int)hipMemsetAsync(dam, 0, (SPE_AMAX_SLOTS - SPE_AMAX_DEC) * 4, s));
+  if (dam) ledger_scope.ledger.zeroed(SPE_AMAX_DEC, SPE_AMAX_SLOTS - SPE_AMAX_DEC);
   if (dam && 3 * L > SPE_AMAX_SLOTS - SPE_AMAX_DEC) return fail(SPE_E_STATE, "fp32h3: decoder activation-scale slots exhausted");
   // fp32h3 cross-attention against the memory: the memory's bound (the last encoder norm2's) scales
   // its planes; layer l's output raises slot dam + 2L + l
@@ -663,6 +718,7 @@ static int forward_stages(spe_model* m, void* stream, const ImageSrc& images, in
         x.mem_amax = mem_bound; x.o_amax = dam ? dam + 2 * L + l : nullptr;
         const double fl = 4.0 * B * 8.0 * Q * (double)T * d + 2.0 * Mq * 8.0 * d * 32;
         const double by = 2.0 * B * (double)T * 2 * d * 2 + 2.0 * Mq * 8.0 * d * 4;
+        CK(ledger_use(x.mem_amax, x.o_amax, "attn.dec_cross"));
         CK(run_other(m, "attn.dec_cross", fl, by, s, [&] { return spe_launch_xattn_h3(x, s); }));
         cross_o_amax = x.o_amax;
       } else {
