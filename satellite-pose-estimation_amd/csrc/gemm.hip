@@ -1334,10 +1334,18 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
     bool kv = true;
     if constexpr (MODE == GEMM_CONV) {
       if constexpr (PL) {
-        const int k = iks * 32 + ck * 4, tap = k / g.Cin;
-        ci = k - tap * g.Cin;
-        kh = tap / g.KW;
-        kw = tap - kh * g.KW;
+        const int k = iks * 32 + ck * 4;
+        if (g.Cin == 4 && g.KW == 7) {                 // the fp32 stem (7x7, 4 channels): constant divisors
+          const unsigned tap = (unsigned)k >> 2;
+          ci = k & 3;
+          kh = (int)(tap / 7u);
+          kw = (int)tap - kh * 7;
+        } else {
+          const int tap = k / g.Cin;
+          ci = k - tap * g.Cin;
+          kh = tap / g.KW;
+          kw = tap - kh * g.KW;
+        }
         kv = k < g.K;
       } else {
         conv_k_decode(iks * 32, g.Cin, g.KW, g.KH * g.KW, kh, kw, ci);
