@@ -1275,9 +1275,11 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
   __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int tilesN = (g.N + BNH - 1) / BNH, ntiles = ((g.M + BM - 1) / BM) * tilesN;
+  // split-K (GemmArgs::ksplit, few-row linear launches): tile t = split * ntiles0 + output tile
+  const int ksp = g.ksplit > 1 ? g.ksplit : 1;
+  const int tilesN = (g.N + BNH - 1) / BNH, ntiles0 = ((g.M + BM - 1) / BM) * tilesN, ntiles = ntiles0 * ksp;
   const int GR = gridDim.x, w0 = xcd_remap(blockIdx.x, GR);
-  const int nk = (g.K + 31) >> 5;
+  const int nk = ((g.K + 31) >> 5) / ksp;
   const int total = w0 < ntiles ? ((ntiles - 1 - w0) / GR + 1) * nk : 0;
   const long long abytes = MODE == GEMM_CONV ? (long long)(g.M / (g.Ho * g.Wo)) * g.H * g.W * g.Cin * 4
                                              : (long long)g.M * g.lda * 4;
@@ -1288,7 +1290,7 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
   const __amdgpu_buffer_rsrc_t rse = __builtin_amdgcn_make_buffer_rsrc((void*)g.h3_sinv, (short)0, g.N * 4, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsbias =
       __builtin_amdgcn_make_buffer_rsrc((void*)(g.bias ? g.bias : g.h3_sinv), (short)0, g.N * 4, 0x00020000);
-  const long long cbytes = EPI == 2 ? (long long)g.vt_B * g.N * g.vt_T * 4 : (long long)g.M * g.ldc * 4;
+  const long long cbytes = EPI == 2 ? (long long)g.vt_B * g.N * g.vt_T * 4 : (long long)ksp * g.M * g.ldc * 4;
   const __amdgpu_buffer_rsrc_t rsc = __builtin_amdgcn_make_buffer_rsrc(g.C, (short)0, (int)cbytes, 0x00020000);
   const int ns = g.N - g.s_col0;                       // EPI 1: columns in the planes
   const long long sbytes = EPI == 2 ? (long long)g.vt_B * g.N * g.vt_T * 4 : (long long)g.M * ns * 4;
@@ -1300,10 +1302,12 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
   if (total == 0) return;
 
   // ---- issue side: the tile / K-step of the next DMA and that tile's per-lane source offsets
-  int it = w0, iks = 0, iord = 0;
+  int it = w0, iks = 0, iord = 0, ikb = 0;            // ikb: the split's first K-step
   int avo[4], ih0[4], iw0[4], bvo[NBQ], evo = 0;
   auto setup = [&](int t) {
-    const int m0 = (t / tilesN) * BM, n0 = (t % tilesN) * BNH;
+    const int tt = t % ntiles0;
+    ikb = (t / ntiles0) * nk;
+    const int m0 = (tt / tilesN) * BM, n0 = (tt % tilesN) * BNH;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int row = (wid + WM * q) * 8 + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7), m = m0 + row;
@@ -1334,7 +1338,7 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
     bool kv = true;
     if constexpr (MODE == GEMM_CONV) {
       if constexpr (PL) {
-        const int k = iks * 32 + ck * 4;
+        const int k = (ikb + iks) * 32 + ck * 4;
         if (g.Cin == 4 && g.KW == 7) {                 // the fp32 stem (7x7, 4 channels): constant divisors
           const unsigned tap = (unsigned)k >> 2;
           ci = k & 3;
@@ -1348,7 +1352,7 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
         }
         kv = k < g.K;
       } else {
-        conv_k_decode(iks * 32, g.Cin, g.KW, g.KH * g.KW, kh, kw, ci);
+        conv_k_decode((ikb + iks) * 32, g.Cin, g.KW, g.KH * g.KW, kh, kw, ci);
       }
     }
 #pragma unroll
@@ -1362,12 +1366,12 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
         off = avo[q];
       }
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lds_ptr6_t)(base + (wid + WM * q) * 1024), 16, off,
-                                               MODE == GEMM_CONV ? 0 : iks * 128, 0, 0);
+                                               MODE == GEMM_CONV ? 0 : (ikb + iks) * 128, 0, 0);
     }
 #pragma unroll
     for (int q = 0; q < NBQ; ++q)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lds_ptr6_t)(base + G::AB + (wid + WM * q) * 1024), 16, bvo[q],
-                                               iks * 64, 0, 0);
+                                               (ikb + iks) * 64, 0, 0);
     if (iks == 0 && wid < 4) {                       // the tile's sinv / bias columns, 4 bytes a lane
       char* eb = smem + NS * STG + (iord & 1) * H3P_EPI + (wid >> 1) * (128 * 4) + (wid & 1) * 256;
       if (wid < 2) __builtin_amdgcn_raw_ptr_buffer_load_lds(rse, (lds_ptr6_t)eb, 4, evo, 0, 0, 0);
@@ -1428,7 +1432,7 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
   float runmax = 0.f;
   u32x4 rres[RES ? FJ * 4 : 1];
   auto tile_mn = [&](int ord, int& m0, int& n0) {
-    const int t = w0 + ord * GR;
+    const int t = (w0 + ord * GR) % ntiles0;
     m0 = (t / tilesN) * BM;
     n0 = (t % tilesN) * BNH;
   };
@@ -1542,7 +1546,8 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
           __builtin_amdgcn_raw_buffer_store_b64(h, rss, ok ? so * 2 : D6_BAD, 0, 0);
           __builtin_amdgcn_raw_buffer_store_b64(l, rss, ok ? (g.M * ns + so) * 2 : D6_BAD, 0, 0);
         } else {
-          __builtin_amdgcn_raw_buffer_store_b128(pack16<float>(v), rsc, ok ? (m * g.ldc + n) * 4 : D6_BAD, 0, 0);
+          const int cs = ksp > 1 ? ((w0 + cord * GR) / ntiles0) * g.M * g.ldc : 0;   // the split's partial
+          __builtin_amdgcn_raw_buffer_store_b128(pack16<float>(v), rsc, ok ? (cs + m * g.ldc + n) * 4 : D6_BAD, 0, 0);
           if constexpr (EPI == 1) __builtin_amdgcn_raw_buffer_store_b64(u32x2{0, 0}, rsc, D6_BAD, 0, 0);
         }
       }
@@ -1687,7 +1692,9 @@ int launch_h3d(const GemmArgs& g, int mode, hipStream_t s) {
   // (long-K problems keep the non-persistent kernel: the layer-3 3x3, K = 2304, measured 0.213 vs
   // 0.245 ms and the neck, K = 4608, 1.35 vs 1.39 ms; up to K = 1152 the persistent form is as fast
   // or faster)
-  if (g.vt_T <= 0 && !g.S && g.K >= 64 && g.K <= 1280 && !(g.N & 3) && !(g.ldc & 3) && !(reinterpret_cast<uintptr_t>(g.C) & 15) &&
+  // (few-row linear problems take the 64-column form at any K: the decoder's K = 2048 linear2, split in K)
+  const bool few = mode == GEMM_LINEAR && !narrow && g.M <= H3_FEW_ROWS;
+  if (g.vt_T <= 0 && !g.S && g.K >= 64 && (g.K <= 1280 || few) && !(g.N & 3) && !(g.ldc & 3) && !(reinterpret_cast<uintptr_t>(g.C) & 15) &&
       (long long)g.M * g.ldc * 4 < LIM && (!res || (!pl && !(g.ldr & 3) && !(reinterpret_cast<uintptr_t>(g.R) & 15)))) {
     const int ncu = spe_cu_count();
     // (the 256-row, three-stage, 8-wave form -- H3PGeo<4, 8, 3> -- measured 0-5 % slower on every
@@ -1695,8 +1702,9 @@ int launch_h3d(const GemmArgs& g, int mode, hipStream_t s) {
     const dim3 pg(tiles < 2 * ncu || ncu <= 0 ? tiles : 2 * ncu), pb(256);
 #define H3P_GO(K) hipLaunchKernelGGL(K, pg, pb, 0, s, g)
 #define H3P_SEL(NAME) H3P_GO(NAME)
-    if (mode == GEMM_LINEAR && !narrow && g.M <= H3_FEW_ROWS) {
-      const int t2 = ((g.M + H3_BM - 1) / H3_BM) * ((g.N + 63) / 64);
+    if (few) {
+      if (g.ksplit > 1 && (res || g.bias || g.act || g.amax_c || ((g.K + 31) >> 5) % g.ksplit)) return -5;
+      const int t2 = ((g.M + H3_BM - 1) / H3_BM) * ((g.N + 63) / 64) * (g.ksplit > 1 ? g.ksplit : 1);
       const dim3 pg2(t2 < 2 * ncu || ncu <= 0 ? t2 : 2 * ncu);
       if (res) hipLaunchKernelGGL(gemm_h3p_linear_r_fr, pg2, pb, 0, s, g);
       else hipLaunchKernelGGL(gemm_h3p_linear_fr, pg2, pb, 0, s, g);
@@ -1723,6 +1731,7 @@ int launch_h3d(const GemmArgs& g, int mode, hipStream_t s) {
     spe_gemm_last_path = 8;
     return (int)hipGetLastError();
   }
+  if (g.ksplit > 1) return -5;                   // split-K: the persistent few-row form only
   if (mode == GEMM_CONV && pl) {
     if (narrow) hipLaunchKernelGGL(gemm_h3d_conv_pl_n64, grid, block, 0, s, g);
     else hipLaunchKernelGGL(gemm_h3d_conv_pl, grid, block, 0, s, g);
@@ -1758,6 +1767,7 @@ int spe_launch_gemm(const GemmArgs& g, int dtype, int mode, hipStream_t s) {
   constexpr int CEb = 8, CEf = 4;
   const int ce = dtype == SPE_DTYPE_BF16 ? CEb : CEf;
   if (g.K % ce) return -2;                                   // K must be whole 16-byte chunks
+  if (g.ksplit > 1 && dtype != SPE_DTYPE_F32H3) return -5;
   // (Cin == 4 pairs: see spe_launch_gemm2 -- a chunk is two adjacent in-range pixels)
   const bool pairs = mode == GEMM_CONV && ce == 8 && g.Cin == 4 && g.pad == 0 && g.KW % 2 == 0 &&
                      (g.Wo - 1) * g.stride + g.KW <= g.W && (g.Ho - 1) * g.stride + g.KH <= g.H;
@@ -1777,6 +1787,7 @@ int spe_launch_gemm(const GemmArgs& g, int dtype, int mode, hipStream_t s) {
     spe_gemm_last_path = 7;
     const int rc = launch_h3d(g, mode, s);
     if (rc != 1) return rc;
+    if (g.ksplit > 1) return -5;                 // split-K partials: the h3 few-row kernel only
     dtype = SPE_DTYPE_F32X6;                     // shapes the h3 kernel does not serve: the x6 path
   }
   if (dtype == SPE_DTYPE_F32X6) {
