@@ -1268,10 +1268,10 @@ template <int MODE, int FJ, bool PL, bool RES, int WM = 4, int NS = 2, int EPI =
 __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
   using G = H3PGeo<FJ, WM, NS>;
   constexpr int BM = G::BM, BNH = G::BN, PB = G::PB, STG = G::STG, NBQ = G::NBQ, NQ = G::NQ, D = G::D;
-  constexpr bool TR = EPI != 2;                        // transposed accumulators (row stores)
-  static_assert(!(EPI == 2 && RES), "no residual on head-transposed stores");
+  constexpr bool TR = EPI != 2 && EPI != 3;            // transposed accumulators (row stores)
+  static_assert(!((EPI == 2 || EPI == 3) && RES), "no residual on head-transposed stores");
   static_assert(NBQ >= 1 && (NS == 2 || NS == 3), "geometry");
-  constexpr int S_ST = FJ * 4 * (EPI == 0 ? 1 : 2);    // stores per lane per tile
+  constexpr int S_ST = FJ * 4 * (EPI == 0 ? 1 : EPI == 3 ? 4 : 2);    // stores per lane per tile
   __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1290,7 +1290,7 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
   const __amdgpu_buffer_rsrc_t rse = __builtin_amdgcn_make_buffer_rsrc((void*)g.h3_sinv, (short)0, g.N * 4, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsbias =
       __builtin_amdgcn_make_buffer_rsrc((void*)(g.bias ? g.bias : g.h3_sinv), (short)0, g.N * 4, 0x00020000);
-  const long long cbytes = EPI == 2 ? (long long)g.vt_B * g.N * g.vt_T * 4 : (long long)ksp * g.M * g.ldc * 4;
+  const long long cbytes = EPI >= 2 ? (long long)g.vt_B * g.N * g.vt_T * 4 : (long long)ksp * g.M * g.ldc * 4;
   const __amdgpu_buffer_rsrc_t rsc = __builtin_amdgcn_make_buffer_rsrc(g.C, (short)0, (int)cbytes, 0x00020000);
   const int ns = g.N - g.s_col0;                       // EPI 1: columns in the planes
   const long long sbytes = EPI == 2 ? (long long)g.vt_B * g.N * g.vt_T * 4 : (long long)g.M * ns * 4;
@@ -1462,8 +1462,8 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
       const float r2 = v[2] - __uint_as_float(h.y << 16), r3 = v[3] - __uint_as_float(h.y & 0xffff0000u);
       l = u32x2{pack_bf16x2(r0, r1), pack_bf16x2(r2, r3)};
     };
-    if constexpr (EPI == 2) {
-      const int mb = m0 + wid * 32 + 4 * hi;         // + 8 q: four consecutive tokens of one image
+    if constexpr (EPI == 2 || EPI == 3) {
+      const int mb = m0 + wid * 32 + 4 * hi;         // + 8 q: four consecutive tokens (EPI 2: of one image)
       const long long lo = (long long)g.vt_B * g.N * g.vt_T;
 #pragma unroll
       for (int j = 0; j < FJ; ++j) {
@@ -1483,7 +1483,17 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
             if (g.act) v[e] = apply_act(v[e], g.act);
           }
           if (ok) runmax = fmaxf(runmax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
-          if (g.S) {
+          if constexpr (EPI == 3) {
+            // any vt_T (the decoder's Q = 11 queries): the four tokens may span two images, one
+            // 4-byte store each (fp32 V^T, no planes, no vt_swz)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int me = mr + e, be = me / g.vt_T, te = me - be * g.vt_T;
+              const bool oke = me < g.M && n < g.N;
+              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[e]), rsc,
+                                                    oke ? (((grp * g.vt_B + be) * 256 + hd) * g.vt_T + te) * 4 : D6_BAD, 0, 0);
+            }
+          } else if (g.S) {
             u32x2 h, l;
             if (g.s_f16) {
               float w[4];
@@ -1640,6 +1650,7 @@ __global__ __launch_bounds__(256, 2) void gemm_h3p_linear_vt(GemmArgs g) { gemm_
 __global__ __launch_bounds__(256, 2) void gemm_h3p_linear_fr(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 2, false, false, 4, 3>(g); }
 __global__ __launch_bounds__(256, 2) void gemm_h3p_linear_r_fr(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 2, false, true, 4, 3>(g); }
 __global__ __launch_bounds__(256, 2) void gemm_h3p_linear_vt_fr(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 2, false, false, 4, 3, 2>(g); }
+__global__ __launch_bounds__(256, 2) void gemm_h3p_linear_vtg_fr(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 2, false, false, 4, 3, 3>(g); }
 constexpr int H3_FEW_ROWS = 4096;
 
 // 1 = not a problem for the h3 kernel (the caller runs the x6 path)
@@ -1685,6 +1696,15 @@ int launch_h3d(const GemmArgs& g, int mode, hipStream_t s) {
       } else {
         hipLaunchKernelGGL(gemm_h3p_linear_vt, pg, pb, 0, s, g);
       }
+      spe_gemm_last_path = 8;
+      return (int)hipGetLastError();
+    }
+    // few-row head-transposed fp32 stores at any vt_T (the decoder self-attention's V^T, Q = 11)
+    if (mode == GEMM_LINEAR && !narrow && g.K >= 64 && g.vt_T > 0 && g.vt_T % 4 && !g.S && !res && !g.out_f16 &&
+        !g.vt_swz && g.M <= H3_FEW_ROWS && g.M == g.vt_B * g.vt_T && !(g.N & 255) &&
+        (long long)g.vt_B * g.N * g.vt_T * 4 < LIM) {
+      const int t2 = ((g.M + H3_BM - 1) / H3_BM) * ((g.N + 63) / 64);
+      hipLaunchKernelGGL(gemm_h3p_linear_vtg_fr, dim3(t2 < 2 * ncu || ncu <= 0 ? t2 : 2 * ncu), pb, 0, s, g);
       spe_gemm_last_path = 8;
       return (int)hipGetLastError();
     }
