@@ -542,39 +542,7 @@ __global__ __launch_bounds__(256) void ffn_reduce_ln_kernel(FfnArgs a) {
   }
 }
 
-// fp32 rows of 256: y = LayerNorm(x + b + sum_s partial[s]) -- the fp32h3 decoder FFN's split-K
-// linear2 finished with its bias, residual and norm3 (one wave per row, 4 columns a lane; the
-// partials summed in split order)
-__global__ __launch_bounds__(256) void reduce_ln_f32_kernel(const float* x, const float* partial, int splits,
-                                                            const float* b, const float* gamma, const float* beta,
-                                                            float* y, int M) {
-  const int lane = threadIdx.x & 63, m = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (m >= M) return;
-  const int n = 4 * lane;
-  f32x4 acc = *reinterpret_cast<const f32x4*>(partial + (size_t)m * D + n);
-  for (int s = 1; s < splits; ++s) acc += *reinterpret_cast<const f32x4*>(partial + ((size_t)s * M + m) * D + n);
-  const f32x4 v = acc + *reinterpret_cast<const f32x4*>(b + n) + *reinterpret_cast<const f32x4*>(x + (size_t)m * D + n);
-  const float mean = wave_sum(v[0] + v[1] + v[2] + v[3]) * (1.f / D);
-  float q = 0.f;
-#pragma unroll
-  for (int r = 0; r < 4; ++r) q += (v[r] - mean) * (v[r] - mean);
-  const float rs = rsqrtf(wave_sum(q) * (1.f / D) + 1e-5f);
-  const f32x4 ga = *reinterpret_cast<const f32x4*>(gamma + n), be = *reinterpret_cast<const f32x4*>(beta + n);
-  float o[4];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) o[r] = (v[r] - mean) * rs * ga[r] + be[r];
-  st16(y + (size_t)m * D + n, pack16<float>(o));
-}
-
 }  // namespace
-
-int spe_launch_reduce_ln_f32(const float* x, const float* partial, int splits, const float* b, const float* gamma,
-                             const float* beta, float* y, int M, hipStream_t s) {
-  if (M <= 0) return 0;
-  if (!x || !partial || splits < 1 || !b || !gamma || !beta || !y) return -1;
-  hipLaunchKernelGGL(reduce_ln_f32_kernel, dim3((M + 3) / 4), dim3(256), 0, s, x, partial, splits, b, gamma, beta, y, M);
-  return (int)hipGetLastError();
-}
 
 // Rows below this many full row tiles per CU-wave run split-F (two launches, fp32 partials).
 constexpr int SPLIT_ROWS = 128 * 64;

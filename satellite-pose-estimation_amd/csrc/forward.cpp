@@ -792,29 +792,13 @@ static int forward_stages(spe_model* m, void* stream, const ImageSrc& images, in
         g.amax_a = tgt_amax; g.amax_c = dam ? dam + 2 * l + 1 : nullptr;
         CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR, s));
       }
-      // fp32h3 with the cross-attention fold (Q <= 12): linear2 (K = 2048 over 704 rows: a long serial K
-      // loop on a few work-groups) split four ways in K into fp32 partials, finished with bias + residual
-      // + norm3 in one pass.  (At config 5 the split's summation order moved the keypoints 1.26e-4 ->
-      // 1.33e-4 from the reference's torch-CPU execution, past that config's fp32 spread of 1.28e-4:
-      // the unfolded decoder keeps the single K chain.)
-      const int l2split = m->h3 && xa && Mq <= 4096 && ff % 128 == 0 ? DEC_L2_SPLIT : 1;
       {
-        GemmArgs g = linear_args(e.l2, P(w.dffn), ff, Mq, l2split > 1 ? P(w.dffnpart) : P(w.dtmp), d);
-        if (l2split > 1) {
-          g.bias = nullptr; g.ksplit = l2split;
-        } else {
-          g.R = P(w.tgt); g.ldr = d;
-        }
+        GemmArgs g = linear_args(e.l2, P(w.dffn), ff, Mq, P(w.dtmp), d);
+        g.R = P(w.tgt); g.ldr = d;
         g.amax_a = dam ? dam + 2 * l + 1 : nullptr;
         CK(run_gemm(m, "gemm.dec", g, GEMM_LINEAR, s));
       }
-      if (l2split > 1)
-        CK(run_other(m, "ln.dec", 0.0, (double)Mq * d * (2 + l2split) * 4, s, [&] {
-          return spe_launch_reduce_ln_f32((const float*)P(w.tgt), (const float*)P(w.dffnpart), l2split, e.l2.bias, e.n3g,
-                                          e.n3b, (float*)P(w.tgt), Mq, s);
-        }));
-      else
-        CK(run_other(m, "ln.dec", 0.0, (double)Mq * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.dtmp), e.n3g, e.n3b, P(w.tgt), nullptr, Mq, d, dt, s); }));
+      CK(run_other(m, "ln.dec", 0.0, (double)Mq * d * 2 * m->esz, s, [&] { return spe_launch_layernorm(P(w.dtmp), e.n3g, e.n3b, P(w.tgt), nullptr, Mq, d, dt, s); }));
     }
     if (m->h3) tgt_amax = e.n3_bound;
     if (out->aux_logits && out->aux_points && l + 1 < L) {

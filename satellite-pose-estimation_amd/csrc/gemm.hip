@@ -1268,18 +1268,16 @@ template <int MODE, int FJ, bool PL, bool RES, int WM = 4, int NS = 2, int EPI =
 __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
   using G = H3PGeo<FJ, WM, NS>;
   constexpr int BM = G::BM, BNH = G::BN, PB = G::PB, STG = G::STG, NBQ = G::NBQ, NQ = G::NQ, D = G::D;
-  constexpr bool TR = EPI != 2 && EPI != 3;            // transposed accumulators (row stores)
-  static_assert(!((EPI == 2 || EPI == 3) && RES), "no residual on head-transposed stores");
+  constexpr bool TR = EPI != 2;                        // transposed accumulators (row stores)
+  static_assert(!(EPI == 2 && RES), "no residual on head-transposed stores");
   static_assert(NBQ >= 1 && (NS == 2 || NS == 3), "geometry");
-  constexpr int S_ST = FJ * 4 * (EPI == 0 ? 1 : EPI == 3 ? 4 : 2);    // stores per lane per tile
+  constexpr int S_ST = FJ * 4 * (EPI == 0 ? 1 : 2);    // stores per lane per tile
   __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
-  // split-K (GemmArgs::ksplit, few-row linear launches): tile t = split * ntiles0 + output tile
-  const int ksp = g.ksplit > 1 ? g.ksplit : 1;
-  const int tilesN = (g.N + BNH - 1) / BNH, ntiles0 = ((g.M + BM - 1) / BM) * tilesN, ntiles = ntiles0 * ksp;
+  const int tilesN = (g.N + BNH - 1) / BNH, ntiles = ((g.M + BM - 1) / BM) * tilesN;
   const int GR = gridDim.x, w0 = xcd_remap(blockIdx.x, GR);
-  const int nk = ((g.K + 31) >> 5) / ksp;
+  const int nk = (g.K + 31) >> 5;
   const int total = w0 < ntiles ? ((ntiles - 1 - w0) / GR + 1) * nk : 0;
   const long long abytes = MODE == GEMM_CONV ? (long long)(g.M / (g.Ho * g.Wo)) * g.H * g.W * g.Cin * 4
                                              : (long long)g.M * g.lda * 4;
@@ -1290,7 +1288,7 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
   const __amdgpu_buffer_rsrc_t rse = __builtin_amdgcn_make_buffer_rsrc((void*)g.h3_sinv, (short)0, g.N * 4, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsbias =
       __builtin_amdgcn_make_buffer_rsrc((void*)(g.bias ? g.bias : g.h3_sinv), (short)0, g.N * 4, 0x00020000);
-  const long long cbytes = EPI >= 2 ? (long long)g.vt_B * g.N * g.vt_T * 4 : (long long)ksp * g.M * g.ldc * 4;
+  const long long cbytes = EPI == 2 ? (long long)g.vt_B * g.N * g.vt_T * 4 : (long long)g.M * g.ldc * 4;
   const __amdgpu_buffer_rsrc_t rsc = __builtin_amdgcn_make_buffer_rsrc(g.C, (short)0, (int)cbytes, 0x00020000);
   const int ns = g.N - g.s_col0;                       // EPI 1: columns in the planes
   const long long sbytes = EPI == 2 ? (long long)g.vt_B * g.N * g.vt_T * 4 : (long long)g.M * ns * 4;
@@ -1302,12 +1300,10 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
   if (total == 0) return;
 
   // ---- issue side: the tile / K-step of the next DMA and that tile's per-lane source offsets
-  int it = w0, iks = 0, iord = 0, ikb = 0;            // ikb: the split's first K-step
+  int it = w0, iks = 0, iord = 0;
   int avo[4], ih0[4], iw0[4], bvo[NBQ], evo = 0;
   auto setup = [&](int t) {
-    const int tt = t % ntiles0;
-    ikb = (t / ntiles0) * nk;
-    const int m0 = (tt / tilesN) * BM, n0 = (tt % tilesN) * BNH;
+    const int m0 = (t / tilesN) * BM, n0 = (t % tilesN) * BNH;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
       const int row = (wid + WM * q) * 8 + (lane >> 3), c = (lane & 7) ^ ((row >> 1) & 7), m = m0 + row;
@@ -1338,7 +1334,7 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
     bool kv = true;
     if constexpr (MODE == GEMM_CONV) {
       if constexpr (PL) {
-        const int k = (ikb + iks) * 32 + ck * 4;
+        const int k = iks * 32 + ck * 4;
         if (g.Cin == 4 && g.KW == 7) {                 // the fp32 stem (7x7, 4 channels): constant divisors
           const unsigned tap = (unsigned)k >> 2;
           ci = k & 3;
@@ -1352,7 +1348,7 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
         }
         kv = k < g.K;
       } else {
-        conv_k_decode((ikb + iks) * 32, g.Cin, g.KW, g.KH * g.KW, kh, kw, ci);
+        conv_k_decode(iks * 32, g.Cin, g.KW, g.KH * g.KW, kh, kw, ci);
       }
     }
 #pragma unroll
@@ -1366,12 +1362,12 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
         off = avo[q];
       }
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsa, (lds_ptr6_t)(base + (wid + WM * q) * 1024), 16, off,
-                                               MODE == GEMM_CONV ? 0 : (ikb + iks) * 128, 0, 0);
+                                               MODE == GEMM_CONV ? 0 : iks * 128, 0, 0);
     }
 #pragma unroll
     for (int q = 0; q < NBQ; ++q)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lds_ptr6_t)(base + G::AB + (wid + WM * q) * 1024), 16, bvo[q],
-                                               (ikb + iks) * 64, 0, 0);
+                                               iks * 64, 0, 0);
     if (iks == 0 && wid < 4) {                       // the tile's sinv / bias columns, 4 bytes a lane
       char* eb = smem + NS * STG + (iord & 1) * H3P_EPI + (wid >> 1) * (128 * 4) + (wid & 1) * 256;
       if (wid < 2) __builtin_amdgcn_raw_ptr_buffer_load_lds(rse, (lds_ptr6_t)eb, 4, evo, 0, 0, 0);
@@ -1432,7 +1428,7 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
   float runmax = 0.f;
   u32x4 rres[RES ? FJ * 4 : 1];
   auto tile_mn = [&](int ord, int& m0, int& n0) {
-    const int t = (w0 + ord * GR) % ntiles0;
+    const int t = w0 + ord * GR;
     m0 = (t / tilesN) * BM;
     n0 = (t % tilesN) * BNH;
   };
@@ -1462,8 +1458,8 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
       const float r2 = v[2] - __uint_as_float(h.y << 16), r3 = v[3] - __uint_as_float(h.y & 0xffff0000u);
       l = u32x2{pack_bf16x2(r0, r1), pack_bf16x2(r2, r3)};
     };
-    if constexpr (EPI == 2 || EPI == 3) {
-      const int mb = m0 + wid * 32 + 4 * hi;         // + 8 q: four consecutive tokens (EPI 2: of one image)
+    if constexpr (EPI == 2) {
+      const int mb = m0 + wid * 32 + 4 * hi;         // + 8 q: four consecutive tokens of one image
       const long long lo = (long long)g.vt_B * g.N * g.vt_T;
 #pragma unroll
       for (int j = 0; j < FJ; ++j) {
@@ -1483,17 +1479,7 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
             if (g.act) v[e] = apply_act(v[e], g.act);
           }
           if (ok) runmax = fmaxf(runmax, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
-          if constexpr (EPI == 3) {
-            // any vt_T (the decoder's Q = 11 queries): the four tokens may span two images, one
-            // 4-byte store each (fp32 V^T, no planes, no vt_swz)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const int me = mr + e, be = me / g.vt_T, te = me - be * g.vt_T;
-              const bool oke = me < g.M && n < g.N;
-              __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[e]), rsc,
-                                                    oke ? (((grp * g.vt_B + be) * 256 + hd) * g.vt_T + te) * 4 : D6_BAD, 0, 0);
-            }
-          } else if (g.S) {
+          if (g.S) {
             u32x2 h, l;
             if (g.s_f16) {
               float w[4];
@@ -1556,8 +1542,7 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
           __builtin_amdgcn_raw_buffer_store_b64(h, rss, ok ? so * 2 : D6_BAD, 0, 0);
           __builtin_amdgcn_raw_buffer_store_b64(l, rss, ok ? (g.M * ns + so) * 2 : D6_BAD, 0, 0);
         } else {
-          const int cs = ksp > 1 ? ((w0 + cord * GR) / ntiles0) * g.M * g.ldc : 0;   // the split's partial
-          __builtin_amdgcn_raw_buffer_store_b128(pack16<float>(v), rsc, ok ? (cs + m * g.ldc + n) * 4 : D6_BAD, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(pack16<float>(v), rsc, ok ? (m * g.ldc + n) * 4 : D6_BAD, 0, 0);
           if constexpr (EPI == 1) __builtin_amdgcn_raw_buffer_store_b64(u32x2{0, 0}, rsc, D6_BAD, 0, 0);
         }
       }
@@ -1650,7 +1635,6 @@ __global__ __launch_bounds__(256, 2) void gemm_h3p_linear_vt(GemmArgs g) { gemm_
 __global__ __launch_bounds__(256, 2) void gemm_h3p_linear_fr(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 2, false, false, 4, 3>(g); }
 __global__ __launch_bounds__(256, 2) void gemm_h3p_linear_r_fr(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 2, false, true, 4, 3>(g); }
 __global__ __launch_bounds__(256, 2) void gemm_h3p_linear_vt_fr(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 2, false, false, 4, 3, 2>(g); }
-__global__ __launch_bounds__(256, 2) void gemm_h3p_linear_vtg_fr(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 2, false, false, 4, 3, 3>(g); }
 constexpr int H3_FEW_ROWS = 4096;
 
 // 1 = not a problem for the h3 kernel (the caller runs the x6 path)
@@ -1699,22 +1683,11 @@ int launch_h3d(const GemmArgs& g, int mode, hipStream_t s) {
       spe_gemm_last_path = 8;
       return (int)hipGetLastError();
     }
-    // few-row head-transposed fp32 stores at any vt_T (the decoder self-attention's V^T, Q = 11)
-    if (mode == GEMM_LINEAR && !narrow && g.K >= 64 && g.vt_T > 0 && g.vt_T % 4 && !g.S && !res && !g.out_f16 &&
-        !g.vt_swz && g.M <= H3_FEW_ROWS && g.M == g.vt_B * g.vt_T && !(g.N & 255) &&
-        (long long)g.vt_B * g.N * g.vt_T * 4 < LIM) {
-      const int t2 = ((g.M + H3_BM - 1) / H3_BM) * ((g.N + 63) / 64);
-      hipLaunchKernelGGL(gemm_h3p_linear_vtg_fr, dim3(t2 < 2 * ncu || ncu <= 0 ? t2 : 2 * ncu), pb, 0, s, g);
-      spe_gemm_last_path = 8;
-      return (int)hipGetLastError();
-    }
   }
   // (long-K problems keep the non-persistent kernel: the layer-3 3x3, K = 2304, measured 0.213 vs
   // 0.245 ms and the neck, K = 4608, 1.35 vs 1.39 ms; up to K = 1152 the persistent form is as fast
   // or faster)
-  // (few-row linear problems take the 64-column form at any K: the decoder's K = 2048 linear2, split in K)
-  const bool few = mode == GEMM_LINEAR && !narrow && g.M <= H3_FEW_ROWS;
-  if (g.vt_T <= 0 && !g.S && g.K >= 64 && (g.K <= 1280 || few) && !(g.N & 3) && !(g.ldc & 3) && !(reinterpret_cast<uintptr_t>(g.C) & 15) &&
+  if (g.vt_T <= 0 && !g.S && g.K >= 64 && g.K <= 1280 && !(g.N & 3) && !(g.ldc & 3) && !(reinterpret_cast<uintptr_t>(g.C) & 15) &&
       (long long)g.M * g.ldc * 4 < LIM && (!res || (!pl && !(g.ldr & 3) && !(reinterpret_cast<uintptr_t>(g.R) & 15)))) {
     const int ncu = spe_cu_count();
     // (the 256-row, three-stage, 8-wave form -- H3PGeo<4, 8, 3> -- measured 0-5 % slower on every
@@ -1722,9 +1695,8 @@ int launch_h3d(const GemmArgs& g, int mode, hipStream_t s) {
     const dim3 pg(tiles < 2 * ncu || ncu <= 0 ? tiles : 2 * ncu), pb(256);
 #define H3P_GO(K) hipLaunchKernelGGL(K, pg, pb, 0, s, g)
 #define H3P_SEL(NAME) H3P_GO(NAME)
-    if (few) {
-      if (g.ksplit > 1 && (res || g.bias || g.act || g.amax_c || ((g.K + 31) >> 5) % g.ksplit)) return -5;
-      const int t2 = ((g.M + H3_BM - 1) / H3_BM) * ((g.N + 63) / 64) * (g.ksplit > 1 ? g.ksplit : 1);
+    if (mode == GEMM_LINEAR && !narrow && g.M <= H3_FEW_ROWS) {
+      const int t2 = ((g.M + H3_BM - 1) / H3_BM) * ((g.N + 63) / 64);
       const dim3 pg2(t2 < 2 * ncu || ncu <= 0 ? t2 : 2 * ncu);
       if (res) hipLaunchKernelGGL(gemm_h3p_linear_r_fr, pg2, pb, 0, s, g);
       else hipLaunchKernelGGL(gemm_h3p_linear_fr, pg2, pb, 0, s, g);
@@ -1751,7 +1723,6 @@ int launch_h3d(const GemmArgs& g, int mode, hipStream_t s) {
     spe_gemm_last_path = 8;
     return (int)hipGetLastError();
   }
-  if (g.ksplit > 1) return -5;                   // split-K: the persistent few-row form only
   if (mode == GEMM_CONV && pl) {
     if (narrow) hipLaunchKernelGGL(gemm_h3d_conv_pl_n64, grid, block, 0, s, g);
     else hipLaunchKernelGGL(gemm_h3d_conv_pl, grid, block, 0, s, g);
@@ -1787,7 +1758,6 @@ int spe_launch_gemm(const GemmArgs& g, int dtype, int mode, hipStream_t s) {
   constexpr int CEb = 8, CEf = 4;
   const int ce = dtype == SPE_DTYPE_BF16 ? CEb : CEf;
   if (g.K % ce) return -2;                                   // K must be whole 16-byte chunks
-  if (g.ksplit > 1 && dtype != SPE_DTYPE_F32H3) return -5;
   // (Cin == 4 pairs: see spe_launch_gemm2 -- a chunk is two adjacent in-range pixels)
   const bool pairs = mode == GEMM_CONV && ce == 8 && g.Cin == 4 && g.pad == 0 && g.KW % 2 == 0 &&
                      (g.Wo - 1) * g.stride + g.KW <= g.W && (g.Ho - 1) * g.stride + g.KH <= g.H;
@@ -1807,7 +1777,6 @@ int spe_launch_gemm(const GemmArgs& g, int dtype, int mode, hipStream_t s) {
     spe_gemm_last_path = 7;
     const int rc = launch_h3d(g, mode, s);
     if (rc != 1) return rc;
-    if (g.ksplit > 1) return -5;                 // split-K partials: the h3 few-row kernel only
     dtype = SPE_DTYPE_F32X6;                     // shapes the h3 kernel does not serve: the x6 path
   }
   if (dtype == SPE_DTYPE_F32X6) {

@@ -61,7 +61,6 @@ struct Dec {
 // [SPE_AMAX_BB, SPE_AMAX_SLOTS) by the transformer stage (each stage zeroes its own range first)
 // (the transformer stage's range is [SPE_AMAX_BB, SPE_AMAX_DEC), the decoder stage's [SPE_AMAX_DEC, SPE_AMAX_SLOTS))
 constexpr int SPE_AMAX_BB = 96, SPE_AMAX_DEC = 112, SPE_AMAX_SLOTS = 136;   // decoder: 3 slots a layer
-constexpr int DEC_L2_SPLIT = 4;   // fp32h3 decoder linear2: K split (forward.cpp; partials in Ws::dffnpart)
 
 struct Ws {                // workspace layout (byte offsets)
   size_t x0, stem, pool, bufA, bufB, t1, t2, ds, xs8, up, cat, neck;

@@ -734,8 +734,7 @@ Ws spe_plan(const spe_model* m, int B) {
   w.dqc = take((size_t)B * Q * d * E);
   w.dffn = take((size_t)B * Q * ff * E);
   // split-F partials (ffn.hip's split count, or one per 256-wide hidden chunk for decsa.hip's decffn)
-  const int fsplit = std::max({spe_ffn_splits((int)(B * Q), (int)ff), m->esz == 2 && d == 256 && ff % 256 == 0 ? (int)ff / 256 : 1,
-                               m->h3 ? DEC_L2_SPLIT : 1});
+  const int fsplit = std::max(spe_ffn_splits((int)(B * Q), (int)ff), m->esz == 2 && d == 256 && ff % 256 == 0 ? (int)ff / 256 : 1);
   w.dffnpart = take((size_t)std::max(1, fsplit) * B * Q * d * 4);
   w.hs = take((size_t)B * Q * d * 4);
   w.amax = take(m->h3 ? SPE_AMAX_SLOTS * 4 : 0);

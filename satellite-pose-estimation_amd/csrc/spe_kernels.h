@@ -46,10 +46,6 @@ struct GemmArgs {
   // head-transposed S planes as fp16 instead of bf16 (the fp32h3 encoder attention's value operand):
   // hi / lo of x * vplane_scale(amax_a, s_l1, s_bmax), s_l1 = max_n sum_k |W[n][k]|, s_bmax = max |bias|
   int s_f16; float s_l1, s_bmax;
-  // fp32h3 few-row linear problems (gemm.hip, M <= H3_FEW_ROWS): ksplit > 1 splits K into that many
-  // equal ranges, each writing its fp32 partial C + k * M * ldc (no bias / residual / activation /
-  // amax_c: the caller's reduce adds them)
-  int ksplit;
 };
 bool spe_gemm_ln_fusable(const GemmArgs& g);   // the large-tile kernel can fuse ln_g/ln_b for g
 int spe_launch_gemm(const GemmArgs& g, int dtype, int mode, hipStream_t s);
@@ -222,9 +218,6 @@ int spe_launch_ffn_w2_chunk_pack(const void* w2, int ld2, int F, void* dst, hipS
 int spe_launch_ffn_ln(const FfnArgs& a, hipStream_t s);
 // y = LN(x + sum_s partial[s] + b2) over a.splits fp32 partials [splits][M][256] (ffn.hip)
 int spe_launch_ffn_reduce_ln(const FfnArgs& a, hipStream_t s);
-// fp32 rows of 256: y[m] = LayerNorm(x[m] + b + sum_s partial[s][m]) (gamma, beta; eps 1e-5), y may alias x
-int spe_launch_reduce_ln_f32(const float* x, const float* partial, int splits, const float* b, const float* gamma,
-                             const float* beta, float* y, int M, hipStream_t s);
 // fp32h3 encoder FFN + residual + LayerNorm in one pass (ffn_h3.hip): fp32 x / y [M][256], W1 as its
 // h3 finalize planes fp16 [2][F][ld1] (rows scaled by 2^e1), meta1 [F/32][64] = (2^-e1, b1) of each
 // 32-unit hidden chunk, W2 as fp16 planes [2][256][ld2] (rows scaled by 2^e2) with the columns of
