@@ -1244,7 +1244,7 @@ __global__ __launch_bounds__(H3_NT, 2) void gemm_h3d_conv_pl_n64(GemmArgs g) { g
 // M go to an out-of-range offset, which the buffer unit drops), the per-column bias and scale come
 // by LDS-DMA with the tile's first step (two regions, by tile parity), a residual tile is loaded
 // into registers before the DMA of the step that ends the tile, and max |C| is published once per
-// workgroup.  Needs nk >= 2 (the bias region of tile i + 2 is written after tile i's epilogue).
+// workgroup.  Needs nk >= NS (the bias region of tile i + 2 is written after tile i's epilogue).
 // (The non-persistent kernel with its stores removed ran the encoder's linear1 in 0.63 instead of
 // 1.14 ms: the store phase, not the MFMAs, was half of that launch.)
 constexpr int H3P_EPI = 2 * 128 * 4;                 // bias[BN] + sinv[BN] floats (BN <= 128) per region
@@ -1270,7 +1270,7 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
   constexpr int BM = G::BM, BNH = G::BN, PB = G::PB, STG = G::STG, NBQ = G::NBQ, NQ = G::NQ, D = G::D;
   constexpr bool TR = EPI != 2;                        // transposed accumulators (row stores)
   static_assert(!(EPI == 2 && RES), "no residual on head-transposed stores");
-  static_assert(NBQ >= 1 && (NS == 2 || NS == 3), "geometry");
+  static_assert(NBQ >= 1 && NS >= 2 && (NS - 1) * D <= 63 && (NS - 2) * D + FJ * 8 <= 63, "geometry / vmcnt");
   constexpr int S_ST = FJ * 4 * (EPI == 0 ? 1 : 2);    // stores per lane per tile
   __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1553,9 +1553,8 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
   };
 
   setup(w0);
-  issue_next(0);
-  issue_next(1);
-  if constexpr (NS == 3) issue_next(2);
+#pragma unroll
+  for (int i = 0; i < NS; ++i) issue_next(i);
   __builtin_amdgcn_s_waitcnt(d6_waitcnt_vm((NS - 1) * D));   // step 0's DMA (the bias pieces are older)
   __syncthreads();
   Frag X, Y;
@@ -1635,6 +1634,21 @@ __global__ __launch_bounds__(256, 2) void gemm_h3p_linear_vt(GemmArgs g) { gemm_
 __global__ __launch_bounds__(256, 2) void gemm_h3p_linear_fr(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 2, false, false, 4, 3>(g); }
 __global__ __launch_bounds__(256, 2) void gemm_h3p_linear_r_fr(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 2, false, true, 4, 3>(g); }
 __global__ __launch_bounds__(256, 2) void gemm_h3p_linear_vt_fr(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 2, false, false, 4, 3, 2>(g); }
+// long-K few-row problems (the decoder's linear2, K = 2048, on 24 work-groups: a chain of 64 K-steps
+// per work-group, each waiting on its DMA): six stages, five K-steps in flight, one work-group per CU
+// (148 KB of LDS).  The MFMA sequence per output is the one of every h3 kernel (K-steps in order; per
+// 16-wide chunk lo.hi, hi.lo, hi.hi), so the results are the same bits as the non-persistent kernel's.
+#ifndef SPE_FRD_NS
+#define SPE_FRD_NS 6
+#endif
+#ifndef SPE_FRD_FJ
+#define SPE_FRD_FJ 2
+#endif
+__global__ __launch_bounds__(256, 1) void gemm_h3p_linear_frd(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, SPE_FRD_FJ, false, false, 4, SPE_FRD_NS>(g); }
+__global__ __launch_bounds__(256, 1) void gemm_h3p_linear_r_frd(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, SPE_FRD_FJ, false, true, 4, SPE_FRD_NS>(g); }
+#ifndef SPE_FRD_MIN_K
+#define SPE_FRD_MIN_K 1281
+#endif
 constexpr int H3_FEW_ROWS = 4096;
 
 // 1 = not a problem for the h3 kernel (the caller runs the x6 path)
@@ -1674,7 +1688,7 @@ int launch_h3d(const GemmArgs& g, int mode, hipStream_t s) {
         (!g.vt_swz || (g.S && g.vt_T % 16 == 0)) && (!g.s_f16 || g.S) &&
         g.vt_T % 4 == 0 && g.M == g.vt_B * g.vt_T && !(g.N & 255) && (!g.S || g.s_col0 == 0) &&
         (long long)g.vt_B * g.N * g.vt_T * 4 < LIM && !(reinterpret_cast<uintptr_t>(g.C) & 15)) {
-      if (g.M <= H3_FEW_ROWS) {
+      if (g.M <= H3_FEW_ROWS && g.K >= 96) {
         const int t2 = ((g.M + H3_BM - 1) / H3_BM) * ((g.N + 63) / 64);
         hipLaunchKernelGGL(gemm_h3p_linear_vt_fr, dim3(t2 < 2 * ncu || ncu <= 0 ? t2 : 2 * ncu), pb, 0, s, g);
       } else {
@@ -1683,6 +1697,17 @@ int launch_h3d(const GemmArgs& g, int mode, hipStream_t s) {
       spe_gemm_last_path = 8;
       return (int)hipGetLastError();
     }
+  }
+  if (mode == GEMM_LINEAR && !narrow && g.M <= H3_FEW_ROWS && g.K >= SPE_FRD_MIN_K && g.vt_T <= 0 && !g.S &&
+      (g.K >> 5) >= SPE_FRD_NS && !(g.N & 3) && !(g.ldc & 3) && !(reinterpret_cast<uintptr_t>(g.C) & 15) &&
+      (long long)g.M * g.ldc * 4 < LIM && (!res || (!(g.ldr & 3) && !(reinterpret_cast<uintptr_t>(g.R) & 15)))) {
+    const int ncu = spe_cu_count();
+    const int t2 = ((g.M + H3_BM - 1) / H3_BM) * ((g.N + 32 * SPE_FRD_FJ - 1) / (32 * SPE_FRD_FJ));
+    const dim3 pg(t2 < ncu || ncu <= 0 ? t2 : ncu), pb(256);
+    if (res) hipLaunchKernelGGL(gemm_h3p_linear_r_frd, pg, pb, 0, s, g);
+    else hipLaunchKernelGGL(gemm_h3p_linear_frd, pg, pb, 0, s, g);
+    spe_gemm_last_path = 8;
+    return (int)hipGetLastError();
   }
   // (long-K problems keep the non-persistent kernel: the layer-3 3x3, K = 2304, measured 0.213 vs
   // 0.245 ms and the neck, K = 4608, 1.35 vs 1.39 ms; up to K = 1152 the persistent form is as fast
@@ -1695,7 +1720,7 @@ int launch_h3d(const GemmArgs& g, int mode, hipStream_t s) {
     const dim3 pg(tiles < 2 * ncu || ncu <= 0 ? tiles : 2 * ncu), pb(256);
 #define H3P_GO(K) hipLaunchKernelGGL(K, pg, pb, 0, s, g)
 #define H3P_SEL(NAME) H3P_GO(NAME)
-    if (mode == GEMM_LINEAR && !narrow && g.M <= H3_FEW_ROWS) {
+    if (mode == GEMM_LINEAR && !narrow && g.M <= H3_FEW_ROWS && g.K >= 96) {
       const int t2 = ((g.M + H3_BM - 1) / H3_BM) * ((g.N + 63) / 64);
       const dim3 pg2(t2 < 2 * ncu || ncu <= 0 ? t2 : 2 * ncu);
       if (res) hipLaunchKernelGGL(gemm_h3p_linear_r_fr, pg2, pb, 0, s, g);

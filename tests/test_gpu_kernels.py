@@ -1107,14 +1107,15 @@ def _split_gemm_err(gpu_device, case, dtype, planes=False, want_path=None, amp=1
     else:
         M, N, K = {"vt": (2 * 2704, 256, 256), "linear_n64": (3000, 64, 256), "linear_n40": (3000, 40, 256),
                    "linear_many_res": (150001, 256, 64), "linear_many_n64": (150001, 64, 128),
-                   "linear_big_res": (150001, 256, 256)}.get(case, (3000, 200, 512))
+                   "linear_big_res": (150001, 256, 256), "linear_longk_res": (704, 256, 2048),
+                   "linear_longk": (77, 520, 2048)}.get(case, (3000, 200, 512))
         A = torch.randn(M, K, generator=g, dtype=torch.float64) * amp
         Wt = torch.randn(N, K, generator=g, dtype=torch.float64) / K ** 0.5
         bias = torch.randn(N, generator=g, dtype=torch.float64)
         ref = A @ Wt.t() + bias
         kw = {}
         ldc = N + 8
-        if case in ("linear_add_relu_res", "linear_many_res", "linear_big_res"):
+        if case in ("linear_add_relu_res", "linear_many_res", "linear_big_res", "linear_longk_res"):
             R = torch.randn(M, ldc, generator=g, dtype=torch.float64)
             ref = torch.relu(ref + R[:, :N])
             kw = dict(R=R.to(dev, f), ldr=ldc, relu=1)
@@ -1174,7 +1175,7 @@ def test_gemm_x6_dma_close_to_fp64(gpu_device, case):
                                       ("linear_n64", 1.0), ("linear_n40", 1.0), ("conv3x3_n64", 1.0),
                                       ("conv7x7s2_c8", 1.0), ("linear", 1e-7), ("linear", 1e6), ("conv3x3", 3e-5),
                                       ("linear_many_res", 1.0), ("linear_many_n64", 1.0), ("linear_big_res", 1.0),
-                                      ("conv3x3_big", 1.0)])
+                                      ("conv3x3_big", 1.0), ("linear_longk_res", 1.0), ("linear_longk", 1.0)])
 def test_gemm_h3_close_to_fp64(gpu_device, case, amp):
     """fp32h3 (the scaled two-way fp16 split, three fp16 MFMAs) at the exact-f32 MFMA kernel's own
     error on the same problem -- ragged M and N tiles, residual + ReLU epilogue, padded 3x3 / strided
@@ -1183,7 +1184,9 @@ def test_gemm_h3_close_to_fp64(gpu_device, case, amp):
     the power-of-two scale from max |A| keeps them at fp32 accuracy.  These row-store problems run
     the persistent form (gemm path 8); the *_many / *_big cases give each workgroup several tiles
     with a ragged last tile (linear_many_res at K = 64: a tile boundary every second step, 2344
-    tiles on 512 slots; linear_many_n64, linear_big_res, conv3x3_big: K = 128, 256, 576).  The published max |C| equals the stored output's exactly."""
+    tiles on 512 slots; linear_many_n64, linear_big_res, conv3x3_big: K = 128, 256, 576); the
+    linear_longk* cases (few rows, K = 2048: the decoder's linear2 shape, ragged M / N) the six-stage
+    few-row form.  The published max |C| equals the stored output's exactly."""
     # (K = 2304, the layer-3 3x3: the non-persistent kernel, path 7; every other case persistent)
     err = _split_gemm_err(gpu_device, case, "fp32h3", amp=amp, want_path=7 if case == "conv3x3" else 8)
     e32 = _split_gemm_err(gpu_device, case, "fp32", amp=amp)
