@@ -1268,10 +1268,10 @@ template <int MODE, int FJ, bool PL, bool RES, int WM = 4, int NS = 2, int EPI =
 __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
   using G = H3PGeo<FJ, WM, NS>;
   constexpr int BM = G::BM, BNH = G::BN, PB = G::PB, STG = G::STG, NBQ = G::NBQ, NQ = G::NQ, D = G::D;
-  constexpr bool TR = EPI != 2;                        // transposed accumulators (row stores)
-  static_assert(!(EPI == 2 && RES), "no residual on head-transposed stores");
-  static_assert(NBQ >= 1 && NS >= 2 && (NS - 1) * D <= 63 && (NS - 2) * D + FJ * 8 <= 63, "geometry / vmcnt");
-  constexpr int S_ST = FJ * 4 * (EPI == 0 ? 1 : 2);    // stores per lane per tile
+  constexpr bool TR = EPI < 2;                         // transposed accumulators (row stores)
+  static_assert(!(EPI >= 2 && RES), "no residual on head-transposed stores");
+  constexpr int S_ST = FJ * 4 * (EPI == 0 ? 1 : EPI == 3 ? 4 : 2);   // stores per lane per tile
+  static_assert(NBQ >= 1 && NS >= 2 && (NS - 1) * D <= 63 && (NS - 2) * D + S_ST <= 63, "geometry / vmcnt");
   __shared__ __attribute__((aligned(1024))) char smem[G::SMEM];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wid = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1288,7 +1288,7 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
   const __amdgpu_buffer_rsrc_t rse = __builtin_amdgcn_make_buffer_rsrc((void*)g.h3_sinv, (short)0, g.N * 4, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsbias =
       __builtin_amdgcn_make_buffer_rsrc((void*)(g.bias ? g.bias : g.h3_sinv), (short)0, g.N * 4, 0x00020000);
-  const long long cbytes = EPI == 2 ? (long long)g.vt_B * g.N * g.vt_T * 4 : (long long)g.M * g.ldc * 4;
+  const long long cbytes = EPI >= 2 ? (long long)g.vt_B * g.N * g.vt_T * 4 : (long long)g.M * g.ldc * 4;
   const __amdgpu_buffer_rsrc_t rsc = __builtin_amdgcn_make_buffer_rsrc(g.C, (short)0, (int)cbytes, 0x00020000);
   const int ns = g.N - g.s_col0;                       // EPI 1: columns in the planes
   const long long sbytes = EPI == 2 ? (long long)g.vt_B * g.N * g.vt_T * 4 : (long long)g.M * ns * 4;
@@ -1302,6 +1302,10 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
   // ---- issue side: the tile / K-step of the next DMA and that tile's per-lane source offsets
   int it = w0, iks = 0, iord = 0;
   int avo[4], ih0[4], iw0[4], bvo[NBQ], evo = 0;
+  // the tile's sinv / bias piece of this wave (64 columns each): four waves one piece each, two
+  // waves (64-column tiles at most) the first half of sinv and of bias
+  static_assert(WM >= 4 || (WM == 2 && BNH <= 64), "sinv / bias pieces");
+  const int ep = WM >= 4 ? wid : 2 * wid;
   auto setup = [&](int t) {
     const int m0 = (t / tilesN) * BM, n0 = (t % tilesN) * BNH;
 #pragma unroll
@@ -1324,7 +1328,7 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
       const int c = (lane & 3) ^ ((row >> 2) & 3), n = n0 + row;
       bvo[q] = n < g.N ? (int)((plane * pstride + (size_t)n * g.ldb) * 2) + c * 16 : D6_BAD;
     }
-    const int en = n0 + lane + (wid & 1) * 64;         // waves 0/1: sinv, waves 2/3: bias
+    const int en = n0 + lane + (ep & 1) * 64;          // pieces 0/1: sinv, 2/3: bias
     evo = en < g.N && en < n0 + BNH ? en * 4 : D6_BAD;
   };
   const int ck = (lane & 7) ^ ((wid * 4 + (lane >> 4)) & 7);
@@ -1368,9 +1372,9 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
     for (int q = 0; q < NBQ; ++q)
       __builtin_amdgcn_raw_ptr_buffer_load_lds(rsb, (lds_ptr6_t)(base + G::AB + (wid + WM * q) * 1024), 16, bvo[q],
                                                iks * 64, 0, 0);
-    if (iks == 0 && wid < 4) {                       // the tile's sinv / bias columns, 4 bytes a lane
-      char* eb = smem + NS * STG + (iord & 1) * H3P_EPI + (wid >> 1) * (128 * 4) + (wid & 1) * 256;
-      if (wid < 2) __builtin_amdgcn_raw_ptr_buffer_load_lds(rse, (lds_ptr6_t)eb, 4, evo, 0, 0, 0);
+    if (iks == 0 && ep < 4) {                        // the tile's sinv / bias columns, 4 bytes a lane
+      char* eb = smem + NS * STG + (iord & 1) * H3P_EPI + (ep >> 1) * (128 * 4) + (ep & 1) * 256;
+      if (ep < 2) __builtin_amdgcn_raw_ptr_buffer_load_lds(rse, (lds_ptr6_t)eb, 4, evo, 0, 0, 0);
       else __builtin_amdgcn_raw_ptr_buffer_load_lds(rsbias, (lds_ptr6_t)eb, 4, g.bias ? evo : D6_BAD, 0, 0, 0);
     }
     if (++iks == nk) {                               // past the last tile: keep issuing the last tile's
@@ -1458,6 +1462,36 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
       const float r2 = v[2] - __uint_as_float(h.y << 16), r3 = v[3] - __uint_as_float(h.y & 0xffff0000u);
       l = u32x2{pack_bf16x2(r0, r1), pack_bf16x2(r2, r3)};
     };
+    if constexpr (EPI == 3) {
+      // head-transposed fp32 at any token count: the lane's four rows may straddle images, one
+      // 4-byte store each
+      const int mb = m0 + wid * 32 + 4 * hi;
+#pragma unroll
+      for (int j = 0; j < FJ; ++j) {
+        const int c = 32 * j + l31, n = n0 + c;
+        const float sv = eb[c] * inv_sa, bv = eb[128 + c];
+        const int grp = n >> 8, hd = n & 255;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int mr = mb + 8 * q + e;
+            const bool ok = mr < g.M && n < g.N;
+            const int b = mr / g.vt_T, tok = mr - b * g.vt_T;
+            const int idx = ok ? ((grp * g.vt_B + b) * 256 + hd) * g.vt_T + tok : 0;
+            float v = acc[j][4 * q + e] * sv + bv;
+            if (g.act) v = apply_act(v, g.act);
+            if (ok) runmax = fmaxf(runmax, fabsf(v));
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rsc, ok ? idx * 4 : D6_BAD, 0, 0);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < FJ; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[j][r] = 0.f;
+      return;
+    }
     if constexpr (EPI == 2) {
       const int mb = m0 + wid * 32 + 4 * hi;         // + 8 q: four consecutive tokens of one image
       const long long lo = (long long)g.vt_B * g.N * g.vt_T;
@@ -1634,6 +1668,7 @@ __global__ __launch_bounds__(256, 2) void gemm_h3p_linear_vt(GemmArgs g) { gemm_
 __global__ __launch_bounds__(256, 2) void gemm_h3p_linear_fr(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 2, false, false, 4, 3>(g); }
 __global__ __launch_bounds__(256, 2) void gemm_h3p_linear_r_fr(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 2, false, true, 4, 3>(g); }
 __global__ __launch_bounds__(256, 2) void gemm_h3p_linear_vt_fr(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 2, false, false, 4, 3, 2>(g); }
+__global__ __launch_bounds__(256, 2) void gemm_h3p_linear_vte_fr(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, 2, false, false, 4, 3, 3>(g); }
 // long-K few-row problems (the decoder's linear2, K = 2048, on 24 work-groups: a chain of 64 K-steps
 // per work-group, each waiting on its DMA): six stages, five K-steps in flight, one work-group per CU
 // (148 KB of LDS).  The MFMA sequence per output is the one of every h3 kernel (K-steps in order; per
@@ -1642,10 +1677,17 @@ __global__ __launch_bounds__(256, 2) void gemm_h3p_linear_vt_fr(GemmArgs g) { ge
 #define SPE_FRD_NS 6
 #endif
 #ifndef SPE_FRD_FJ
-#define SPE_FRD_FJ 2
+#define SPE_FRD_FJ 1
 #endif
-__global__ __launch_bounds__(256, 1) void gemm_h3p_linear_frd(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, SPE_FRD_FJ, false, false, 4, SPE_FRD_NS>(g); }
-__global__ __launch_bounds__(256, 1) void gemm_h3p_linear_r_frd(GemmArgs g) { gemm_h3p_body<GEMM_LINEAR, SPE_FRD_FJ, false, true, 4, SPE_FRD_NS>(g); }
+#ifndef SPE_FRD_WM
+#define SPE_FRD_WM 2
+#endif
+__global__ __launch_bounds__(64 * SPE_FRD_WM, 1) void gemm_h3p_linear_frd(GemmArgs g) {
+  gemm_h3p_body<GEMM_LINEAR, SPE_FRD_FJ, false, false, SPE_FRD_WM, SPE_FRD_NS>(g);
+}
+__global__ __launch_bounds__(64 * SPE_FRD_WM, 1) void gemm_h3p_linear_r_frd(GemmArgs g) {
+  gemm_h3p_body<GEMM_LINEAR, SPE_FRD_FJ, false, true, SPE_FRD_WM, SPE_FRD_NS>(g);
+}
 #ifndef SPE_FRD_MIN_K
 #define SPE_FRD_MIN_K 1281
 #endif
@@ -1697,13 +1739,24 @@ int launch_h3d(const GemmArgs& g, int mode, hipStream_t s) {
       spe_gemm_last_path = 8;
       return (int)hipGetLastError();
     }
+    // few-row head-transposed fp32 at a token count the 16-byte form cannot take (the decoder's
+    // self-attention V^T, T = Q = 11)
+    if (mode == GEMM_LINEAR && !narrow && g.M <= H3_FEW_ROWS && g.K >= 96 && g.vt_T > 0 && !res && !g.S &&
+        !g.out_f16 && !g.vt_swz && g.M == g.vt_B * g.vt_T && !(g.N & 255) &&
+        (long long)g.vt_B * g.N * g.vt_T * 4 < LIM) {
+      const int t2 = ((g.M + H3_BM - 1) / H3_BM) * ((g.N + 63) / 64);
+      hipLaunchKernelGGL(gemm_h3p_linear_vte_fr, dim3(t2 < 2 * ncu || ncu <= 0 ? t2 : 2 * ncu), pb, 0, s, g);
+      spe_gemm_last_path = 8;
+      return (int)hipGetLastError();
+    }
   }
   if (mode == GEMM_LINEAR && !narrow && g.M <= H3_FEW_ROWS && g.K >= SPE_FRD_MIN_K && g.vt_T <= 0 && !g.S &&
       (g.K >> 5) >= SPE_FRD_NS && !(g.N & 3) && !(g.ldc & 3) && !(reinterpret_cast<uintptr_t>(g.C) & 15) &&
       (long long)g.M * g.ldc * 4 < LIM && (!res || (!(g.ldr & 3) && !(reinterpret_cast<uintptr_t>(g.R) & 15)))) {
     const int ncu = spe_cu_count();
-    const int t2 = ((g.M + H3_BM - 1) / H3_BM) * ((g.N + 32 * SPE_FRD_FJ - 1) / (32 * SPE_FRD_FJ));
-    const dim3 pg(t2 < ncu || ncu <= 0 ? t2 : ncu), pb(256);
+    constexpr int FBM = 32 * SPE_FRD_WM, FBN = 32 * SPE_FRD_FJ;
+    const int t2 = ((g.M + FBM - 1) / FBM) * ((g.N + FBN - 1) / FBN);
+    const dim3 pg(t2 < ncu || ncu <= 0 ? t2 : ncu), pb(64 * SPE_FRD_WM);
     if (res) hipLaunchKernelGGL(gemm_h3p_linear_r_frd, pg, pb, 0, s, g);
     else hipLaunchKernelGGL(gemm_h3p_linear_frd, pg, pb, 0, s, g);
     spe_gemm_last_path = 8;

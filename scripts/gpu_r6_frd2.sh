@@ -8,8 +8,8 @@ mkdir -p gpurun_out
 SPE_LIB_PATH=ab_old/libspe.so timeout -k 10 600 python -u scripts/lab/bitwise_forward.py dump gpurun_out/${TAG}_old.npz > gpurun_out/${TAG}_dump_old.log 2>&1 \
   || { tail -5 gpurun_out/${TAG}_dump_old.log; exit 2; }
 for v in ${VARIANTS:-fj1 fj1n7}; do
-  export SPE_LIB_PATH=ab_$v/libspe.so
-  timeout -k 10 300 python -u -m pytest tests/test_gpu_kernels.py -m gpu -x -q -k "gemm_h3_close" --timeout 200 --timeout-method thread > gpurun_out/${TAG}_${v}_tests.log 2>&1 \
+  if [ "$v" = main ]; then unset SPE_LIB_PATH; else export SPE_LIB_PATH=ab_$v/libspe.so; fi
+  timeout -k 10 500 python -u -m pytest tests/test_gpu_kernels.py tests/test_gpu_parity.py -m gpu -x -q -k "${TESTK:-gemm_h3_close}" --timeout 200 --timeout-method thread > gpurun_out/${TAG}_${v}_tests.log 2>&1 \
     || { grep -E "^E |FAILED" gpurun_out/${TAG}_${v}_tests.log | head; exit 1; }
   echo "$v $(tail -1 gpurun_out/${TAG}_${v}_tests.log)"
   timeout -k 10 600 python -u scripts/lab/bitwise_forward.py dump gpurun_out/${TAG}_$v.npz > gpurun_out/${TAG}_dump_$v.log 2>&1 \
