@@ -1221,7 +1221,7 @@ __device__ __forceinline__ void gemm_h3d_body(const GemmArgs& g) {
     for (int e = 0; e < 8; ++e) bv[e] = (g.bias && n + e < g.N) ? g.bias[n + e] : 0.f;
   }
   const float am = store_tile<float, H3_BM, H3_NT, BNH>(g, ct, m0, n0, tid, bv);
-  if (g.amax_c) amax_publish(am, g.amax_c, g.amax_c_mul);
+  if (g.amax_c) amax_publish_block(am, g.amax_c, g.amax_c_mul, ct);
 }
 
 __global__ __launch_bounds__(H3_NT, 2) void gemm_h3d_linear(GemmArgs g) { gemm_h3d_body<GEMM_LINEAR, 4>(g); }
@@ -1643,22 +1643,7 @@ __device__ __forceinline__ void gemm_h3p_body(const GemmArgs& g) {
   }
 #undef H3P_MMA
   __builtin_amdgcn_s_waitcnt(d6_waitcnt_vm0());
-  if (g.amax_c) {
-    // one atomic per work-group, not per wave: the few-row launches' work-groups all end together,
-    // and their atomics on the one slot serialize (max is exact, so the order does not matter)
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) runmax = fmaxf(runmax, __shfl_xor(runmax, o, 64));
-    __syncthreads();
-    float* red = reinterpret_cast<float*>(smem);
-    if (lane == 0) red[wid] = runmax;
-    __syncthreads();
-    if (tid == 0) {
-      float am = red[0];
-#pragma unroll
-      for (int w = 1; w < WM; ++w) am = fmaxf(am, red[w]);
-      if (am > 0.f) amax_update(g.amax_c, am * (g.amax_c_mul > 0.f ? g.amax_c_mul : 1.f));
-    }
-  }
+  if (g.amax_c) amax_publish_block(runmax, g.amax_c, g.amax_c_mul, reinterpret_cast<float*>(smem));
 }
 
 #define H3P_KERNELS(SUF, WM, NS, OCC)                                                                                  \

@@ -116,6 +116,22 @@ SPE_DEV void amax_update(float* slot, float v) {
   if (__float_as_uint(v) > cur) atomicMax((unsigned*)slot, __float_as_uint(v));
 }
 
+// max over the work-group of the threads' am (>= 0) raised into slot (times mul when mul > 0) with
+// ONE atomic: every thread of the block calls it (blockDim.x a multiple of 64); red = LDS scratch of
+// blockDim.x / 64 floats that no thread reads or writes any more (barriers on both sides).  The
+// work-groups of a small launch end together, and per-wave atomics on the one slot serialize.
+SPE_DEV void amax_publish_block(float am, float* slot, float mul, float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) am = fmaxf(am, __shfl_xor(am, o, 64));
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = am;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < (int)(blockDim.x >> 6); ++w) am = fmaxf(am, red[w]);
+    if (am > 0.f) amax_update(slot, am * (mul > 0.f ? mul : 1.f));
+  }
+}
+
 // Bijective XCD-aware remap of a 1-D grid: blocks that land on one XCD (b % 8 equal under
 // round-robin dispatch) get a contiguous range of tile ids, so neighbouring tiles that share
 // operand panels hit the same L2.  Speed only, never correctness.

@@ -407,8 +407,7 @@ __global__ __launch_bounds__(256) void xattn_h3_merge_wv_kernel(XattnArgs a) {
     st8((float*)a.o + (size_t)bq * a.ldo + h * 32 + j, u32x2{__float_as_uint(o0), __float_as_uint(o1)});
     mx = __builtin_fmaxf(__builtin_fabsf(o0), __builtin_fabsf(o1));
   }
-  mx = wave_max(mx);
-  if ((tid & 63) == 0 && a.o_amax) amax_update(a.o_amax, mx);
+  if (a.o_amax) amax_publish_block(mx, a.o_amax, 1.f, us);
 }
 
 }  // namespace
