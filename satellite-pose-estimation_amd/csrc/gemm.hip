@@ -1688,9 +1688,7 @@ __global__ __launch_bounds__(64 * SPE_FRD_WM, 1) void gemm_h3p_linear_frd(GemmAr
 __global__ __launch_bounds__(64 * SPE_FRD_WM, 1) void gemm_h3p_linear_r_frd(GemmArgs g) {
   gemm_h3p_body<GEMM_LINEAR, SPE_FRD_FJ, false, true, SPE_FRD_WM, SPE_FRD_NS>(g);
 }
-#ifndef SPE_FRD_MIN_K
-#define SPE_FRD_MIN_K 1281
-#endif
+constexpr int H3_FRD_MIN_K = 1281;
 constexpr int H3_FEW_ROWS = 4096;
 
 // 1 = not a problem for the h3 kernel (the caller runs the x6 path)
@@ -1750,13 +1748,16 @@ int launch_h3d(const GemmArgs& g, int mode, hipStream_t s) {
       return (int)hipGetLastError();
     }
   }
-  if (mode == GEMM_LINEAR && !narrow && g.M <= H3_FEW_ROWS && g.K >= SPE_FRD_MIN_K && g.vt_T <= 0 && !g.S &&
+  // (also the N <= 512 ones: 13 -> 11 us a launch for the decoder's 256-column projections; the
+  // 2048-column ones are slower on it, 704 tiles)
+  if (mode == GEMM_LINEAR && !narrow && g.M <= H3_FEW_ROWS && (g.K >= H3_FRD_MIN_K || g.N <= 512) && g.vt_T <= 0 && !g.S &&
       (g.K >> 5) >= SPE_FRD_NS && !(g.N & 3) && !(g.ldc & 3) && !(reinterpret_cast<uintptr_t>(g.C) & 15) &&
       (long long)g.M * g.ldc * 4 < LIM && (!res || (!(g.ldr & 3) && !(reinterpret_cast<uintptr_t>(g.R) & 15)))) {
     const int ncu = spe_cu_count();
     constexpr int FBM = 32 * SPE_FRD_WM, FBN = 32 * SPE_FRD_FJ;
     const int t2 = ((g.M + FBM - 1) / FBM) * ((g.N + FBN - 1) / FBN);
-    const dim3 pg(t2 < ncu || ncu <= 0 ? t2 : ncu), pb(64 * SPE_FRD_WM);
+    const int slots = SPE_FRD_WM == 2 ? 2 * ncu : ncu;   // 76 KB (two waves) / 148 KB (four) of LDS
+    const dim3 pg(t2 < slots || ncu <= 0 ? t2 : slots), pb(64 * SPE_FRD_WM);
     if (res) hipLaunchKernelGGL(gemm_h3p_linear_r_frd, pg, pb, 0, s, g);
     else hipLaunchKernelGGL(gemm_h3p_linear_frd, pg, pb, 0, s, g);
     spe_gemm_last_path = 8;
