@@ -24,7 +24,7 @@ SHAPES = {
     "l1.conv1": (64 * 104 * 104, 64, 256), "l3.conv3": (64 * 26 * 26, 1024, 256),
     "l1.3x3": (64, 104, 64, 64, 3, 1, 1), "l2.3x3": (64, 52, 128, 128, 3, 1, 1), "l3.3x3": (64, 26, 256, 256, 3, 1, 1),
     "neck.3x3": (64, 52, 512, 256, 3, 1, 1), "l4.3x3": (64, 13, 512, 512, 3, 1, 1),
-    "l4.conv1": (64 * 169, 512, 2048), "l4.conv3": (64 * 169, 2048, 512),
+    "l4.conv1": (64 * 169, 512, 2048), "l4.conv3": (64 * 169, 2048, 512), "stem": (64, 416, 4, 64, 7, 2, 3),
 }
 
 
