@@ -2,6 +2,8 @@
 # Round 6: the six-stage few-row h3 GEMM for the decoder's long-K linear2 -- h3 GEMM tests, fp32h3
 # goldens, a bit-for-bit comparison of the fp32h3 model outputs (configs 2 / 4 / 5) against the
 # previous tree's library (ab_old/libspe.so), the serialized launch table, and old / new bench lines.
+# (ab_old/libspe.so: the previous commit built in a git worktree,
+#  make -C <worktree>/satellite-pose-estimation_amd/csrc OBJDIR=/tmp/obj OUT=$PWD/ab_old/libspe.so)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 TAG=${PROF_TAG:-r6frd}

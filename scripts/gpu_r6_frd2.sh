@@ -1,6 +1,8 @@
 #!/bin/bash
 # Round 6: column width / depth of the few-row long-K h3 GEMM form (variant libraries ab_<v>/libspe.so):
 # h3 GEMM tests, bit-for-bit fp32h3 outputs against ab_old, the serialized decoder launches.
+# (ab_old/libspe.so: the previous commit built in a git worktree,
+#  make -C <worktree>/satellite-pose-estimation_amd/csrc OBJDIR=/tmp/obj OUT=$PWD/ab_old/libspe.so)
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 TAG=${PROF_TAG:-r6frd2}
